@@ -1,0 +1,359 @@
+"""ddpca-admm_amd: MI355X-native hot path of DDPCA-ADMM (per-subdomain solve loop of the ADMM).
+
+Python mirror of the reference's class surface for this path -- ``MULTIGRID`` (MULTIGRID.h:10-95),
+``MGPIS`` (MGPIS.h:8-38) and ``MCONTACT`` (MCONTACT.h:9-95) -- over the C ABI of
+``libddpca_amd.so`` (include/ddpca_amd.h).  All compute runs in the HIP library; this module only
+marshals arrays.  There is no CPU fallback: if the library is missing or no gfx950 GPU is visible,
+the device entry points raise.
+
+The package directory name contains a hyphen, so import it with
+``importlib.import_module("ddpca-admm_amd")`` (see ``__graft_entry__.py``).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+from typing import Optional, Sequence
+
+import numpy as np
+
+_HERE = Path(__file__).resolve().parent
+LIBPATH = _HERE / "libddpca_amd.so"
+
+_lib: Optional[C.CDLL] = None
+
+
+class DdpcaError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"[ddpca error {code}] {msg}")
+        self.code = code
+
+
+def lib() -> C.CDLL:
+    """Load libddpca_amd.so (built in-tree by build.py); raise loudly if it is missing."""
+    global _lib
+    if _lib is None:
+        if not LIBPATH.exists():
+            raise ImportError(f"{LIBPATH} is missing: run `python ddpca-admm_amd/build.py` (hipcc, gfx950)")
+        _lib = C.CDLL(str(LIBPATH), mode=C.RTLD_GLOBAL)
+        _declare(_lib)
+    return _lib
+
+
+class MgpisOptions(C.Structure):
+    _fields_ = [("smoother", C.c_int), ("nu", C.c_int), ("omega", C.c_double), ("iters_per_graph", C.c_int)]
+
+
+_P = C.c_void_p
+_I64P = C.POINTER(C.c_int64)
+_DP = C.POINTER(C.c_double)
+
+
+def _declare(L: C.CDLL) -> None:
+    L.ddpca_last_error.restype = C.c_char_p
+    L.ddpca_gpu_available.restype = C.c_int
+    L.mgpis_default_options.argtypes = [C.POINTER(MgpisOptions)]
+    L.mgpis_default_options.restype = None
+    L.ddpca_problem_create.argtypes = [C.c_char_p, _DP, C.c_int, C.POINTER(_P)]
+    L.ddpca_problem_set_ips.argtypes = [_P, C.c_int64, C.c_int64, _P, _P, _P, _P, _P, C.c_double, C.c_double,
+                                        C.c_double]
+    L.ddpca_problem_establish.argtypes = [_P]
+    L.ddpca_problem_view.argtypes = [_P, C.c_char_p, C.c_int64, C.c_int64, C.POINTER(_P), _I64P,
+                                     C.POINTER(C.c_int)]
+    L.ddpca_problem_destroy.argtypes = [_P]
+    L.ddpca_problem_mgpis.argtypes = [_P, C.c_int64, C.c_int, C.POINTER(MgpisOptions), C.POINTER(_P)]
+    L.mgpis_gpu_create.argtypes = [C.c_int, C.c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P,
+                                   C.POINTER(MgpisOptions), C.POINTER(_P)]
+    L.mgpis_gpu_create_bsr3.argtypes = [C.c_int, C.c_int, _P, _P, _P, _P, _P, _P, _P, _P,
+                                        C.POINTER(MgpisOptions), C.POINTER(_P)]
+    L.mgpis_gpu_solve.argtypes = [_P, _P, _P, C.c_int, C.c_double, C.c_int64, _I64P, _DP]
+    L.mgpis_gpu_spmv.argtypes = [_P, C.c_int, _P, _P]
+    L.mgpis_gpu_vcycle.argtypes = [_P, _P, _P]
+    L.mgpis_gpu_info.argtypes = [_P, _I64P]
+    L.mgpis_gpu_destroy.argtypes = [_P]
+    if hasattr(L, "mcontact_gpu_create"):
+        L.mcontact_gpu_create.argtypes = [_P, C.c_int, C.c_int, C.c_int, _P, C.POINTER(MgpisOptions),
+                                          C.POINTER(_P)]
+        L.mcontact_gpu_comm_init.argtypes = [_P, _P]
+        L.mcontact_gpu_unique_id.argtypes = [_P]
+        L.mcontact_gpu_iterate.argtypes = [_P, C.c_int64, C.c_int]
+        L.mcontact_gpu_iterate.restype = C.c_int64
+        L.mcontact_gpu_monitor.argtypes = [_P, _DP, C.c_int64]
+        L.mcontact_gpu_monitor.restype = C.c_int64
+        L.mcontact_gpu_get.argtypes = [_P, C.c_char_p, C.c_int64, _P, C.c_int64]
+        L.mcontact_gpu_get.restype = C.c_int64
+        L.mcontact_gpu_timing.argtypes = [_P, _DP]
+        L.mcontact_gpu_destroy.argtypes = [_P]
+
+
+def _check(rc: int) -> int:
+    if rc < 0:
+        raise DdpcaError(rc, lib().ddpca_last_error().decode())
+    return rc
+
+
+def gpu_available() -> bool:
+    return bool(lib().ddpca_gpu_available())
+
+
+def default_options(**kw) -> MgpisOptions:
+    o = MgpisOptions()
+    lib().mgpis_default_options(C.byref(o))
+    for k, v in kw.items():
+        setattr(o, k, v)
+    return o
+
+
+def _ptr(a: np.ndarray) -> C.c_void_p:
+    return C.c_void_p(a.ctypes.data)
+
+
+_DTYPES = {0: np.float64, 1: np.int64, 2: np.int32, 3: np.uint8}
+
+
+# ============================================================================ host problem
+class Problem:
+    """Host problem (MULTIGRID meshes + MCONTACT interfaces); setup only.
+
+    kind/params: ``beam`` (d0, d1, d2, globLeve, D0, D1, D2), ``twoblock`` (fric, globLeve),
+    ``dehw`` (ngroups, nx, ny, nz, globLeve, fric).
+    """
+
+    def __init__(self, kind: str, *params: float):
+        p = np.asarray(params, dtype=np.float64)
+        h = C.c_void_p()
+        _check(lib().ddpca_problem_create(kind.encode(), p.ctypes.data_as(_DP), len(p), C.byref(h)))
+        self._h = h
+        self.kind = kind
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h and _lib is not None:
+            _lib.ddpca_problem_destroy(h)
+            self._h = None
+
+    @property
+    def handle(self) -> C.c_void_p:
+        return self._h
+
+    def array(self, name: str, index: int = 0, level: int = 0) -> np.ndarray:
+        data = C.c_void_p()
+        count = C.c_int64()
+        dt = C.c_int()
+        _check(lib().ddpca_problem_view(self._h, name.encode(), index, level, C.byref(data), C.byref(count),
+                                        C.byref(dt)))
+        dtype = np.dtype(_DTYPES[dt.value])
+        if count.value == 0:
+            return np.zeros(0, dtype)
+        buf = (C.c_char * (count.value * dtype.itemsize)).from_address(data.value)
+        return np.frombuffer(buf, dtype=dtype).copy()
+
+    def csr(self, base: str, index: int = 0, level: int = 0):
+        import scipy.sparse as sp
+        shape = tuple(self.array(f"{base}:shape", index, level))
+        return sp.csr_matrix((self.array(f"{base}:val", index, level), self.array(f"{base}:col", index, level),
+                              self.array(f"{base}:ptr", index, level)), shape=shape)
+
+    @property
+    def nsub(self) -> int:
+        return int(self.array("sizes")[0])
+
+    @property
+    def nint(self) -> int:
+        return int(self.array("sizes")[1])
+
+    def set_ips(self, ts: int, node, shap, basis, gap, w, fric: float, penN: float, penF: float) -> None:
+        """Replace interface ts's integration points (CSEARCH::intePoin data contract)."""
+        node = np.ascontiguousarray(node, dtype=np.int64)
+        shap = np.ascontiguousarray(shap, dtype=np.float64)
+        basis = np.ascontiguousarray(basis, dtype=np.float64)
+        gap = np.ascontiguousarray(gap, dtype=np.float64)
+        w = np.ascontiguousarray(w, dtype=np.float64)
+        _check(lib().ddpca_problem_set_ips(self._h, ts, len(gap), _ptr(node), _ptr(shap), _ptr(basis), _ptr(gap),
+                                           _ptr(w), fric, penN, penF))
+
+    def ESTABLISH(self) -> "Problem":
+        _check(lib().ddpca_problem_establish(self._h))
+        return self
+
+    def grid(self, tv: int = 0) -> "MULTIGRID":
+        return MULTIGRID(self, tv)
+
+
+class MULTIGRID:
+    """Read-only view of one subdomain's operators (MULTIGRID.h public members)."""
+
+    def __init__(self, problem: Problem, tv: int):
+        self.problem = problem
+        self.tv = tv
+
+    @property
+    def maxiLeve(self) -> int:
+        return int(self.problem.array("maxiLeve", self.tv)[0])
+
+    @property
+    def nodeCoor(self) -> np.ndarray:
+        return self.problem.array("coords", self.tv).reshape(-1, 3)
+
+    @property
+    def consFlag(self) -> np.ndarray:
+        return self.problem.array("consFlag", self.tv)
+
+    @property
+    def consForc(self) -> np.ndarray:
+        return self.problem.array("consForc", self.tv)
+
+    def consStif(self, level: int):
+        return self.problem.csr("K", self.tv, level)
+
+    def realProl(self, level: int):
+        return self.problem.csr("P", self.tv, level)
+
+    def OUTP_SUB1(self, x: np.ndarray) -> np.ndarray:
+        """Condensed solution -> nodal displacement (MULTIGRID.h:1263-1281; no rotations)."""
+        flag = self.consFlag
+        fi = self.problem.array("freeIndex", self.tv)
+        u = np.zeros(len(flag))
+        u[flag == 1] = x[fi[flag == 1]]
+        return u
+
+
+# ============================================================================ device MGPIS
+class MGPIS:
+    """Device multigrid-preconditioned CG for one subdomain (MGPIS.h:8-225)."""
+
+    def __init__(self, handle: C.c_void_p):
+        self._h = handle
+
+    @classmethod
+    def from_problem(cls, problem: Problem, tv: int = 0, device: int = 0, **opts) -> "MGPIS":
+        h = C.c_void_p()
+        o = default_options(**opts)
+        _check(lib().ddpca_problem_mgpis(problem.handle, tv, device, C.byref(o), C.byref(h)))
+        return cls(h)
+
+    @classmethod
+    def from_csr(cls, nnodes: Sequence[int], free_dof: Sequence[np.ndarray], K: Sequence, S: Sequence,
+                 device: int = 0, **opts) -> "MGPIS":
+        """Reference layout: consStif[l] (scipy CSR, condensed), free_dof[l], scalar stencils S[l]."""
+        nlev = len(nnodes)
+        keep = []
+
+        def arr(a, dt):
+            a = np.ascontiguousarray(a, dtype=dt)
+            keep.append(a)
+            return a.ctypes.data
+
+        nn = arr(nnodes, np.int64)
+        nf = arr([k.shape[0] for k in K], np.int64)
+        fd = (C.c_void_p * nlev)(*[arr(f, np.int32) for f in free_dof])
+        kp = (C.c_void_p * nlev)(*[arr(k.indptr, np.int64) for k in K])
+        kc = (C.c_void_p * nlev)(*[arr(k.indices, np.int32) for k in K])
+        kv = (C.c_void_p * nlev)(*[arr(k.data, np.float64) for k in K])
+        ns = max(nlev - 1, 1)
+        sp_ = (C.c_void_p * ns)(*[arr(s.indptr, np.int64) for s in S])
+        sc_ = (C.c_void_p * ns)(*[arr(s.indices, np.int32) for s in S])
+        sw_ = (C.c_void_p * ns)(*[arr(s.data, np.float64) for s in S])
+        h = C.c_void_p()
+        o = default_options(**opts)
+        _check(lib().mgpis_gpu_create(device, nlev, C.c_void_p(nn), C.c_void_p(nf), fd, kp, kc, kv, sp_, sc_, sw_,
+                                      C.byref(o), C.byref(h)))
+        return cls(h)
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h and _lib is not None:
+            _lib.mgpis_gpu_destroy(h)
+            self._h = None
+
+    def info(self) -> dict:
+        out = (C.c_int64 * 7)()
+        _check(lib().mgpis_gpu_info(self._h, out))
+        return dict(nlev=out[0], nfree=out[1], nnzb=out[2], chunks=out[3], omega=out[4] / 1e6, lmax=out[5] / 1e6,
+                    device=out[6])
+
+    def CG_SOLV(self, precSwit: int, totaForc: np.ndarray, rtol: float = 1e-14, maxit: Optional[int] = None):
+        """Returns (x, iterations, recursive relative residual); reference defaults rtol=1e-14, maxit=n."""
+        b = np.ascontiguousarray(totaForc, dtype=np.float64)
+        x = np.zeros_like(b)
+        it = C.c_int64()
+        rr = C.c_double()
+        _check(lib().mgpis_gpu_solve(self._h, _ptr(b), _ptr(x), precSwit, rtol, len(b) if maxit is None else maxit,
+                                     C.byref(it), C.byref(rr)))
+        return x, it.value, rr.value
+
+    def MULT_VCYC(self, r: np.ndarray) -> np.ndarray:
+        r = np.ascontiguousarray(r, dtype=np.float64)
+        z = np.zeros_like(r)
+        _check(lib().mgpis_gpu_vcycle(self._h, _ptr(r), _ptr(z)))
+        return z
+
+    def spmv(self, x: np.ndarray) -> np.ndarray:
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        y = np.zeros_like(x)
+        info = self.info()
+        _check(lib().mgpis_gpu_spmv(self._h, info["nlev"] - 1, _ptr(x), _ptr(y)))
+        return y
+
+
+# ============================================================================ device MCONTACT
+class MCONTACT:
+    """Device ADMM loop of MCONTACT::CONTACT_ANALYSIS (MCONTACT.h:2493-2845) for one rank."""
+
+    def __init__(self, problem: Problem, device: int = 0, rank: int = 0, nranks: int = 1,
+                 owner: Optional[Sequence[int]] = None, **opts):
+        nsub = problem.nsub
+        own = np.zeros(nsub, np.int32) if owner is None else np.ascontiguousarray(owner, dtype=np.int32)
+        self._owner = own
+        h = C.c_void_p()
+        o = default_options(**opts)
+        _check(lib().mcontact_gpu_create(problem.handle, device, rank, nranks, _ptr(own), C.byref(o), C.byref(h)))
+        self._h = h
+        self.problem = problem
+        self.nsub, self.nint = nsub, problem.nint
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h and _lib is not None:
+            _lib.mcontact_gpu_destroy(h)
+            self._h = None
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = (C.c_char * 128)()
+        _check(lib().mcontact_gpu_unique_id(buf))
+        return bytes(buf)
+
+    def comm_init(self, uid: bytes) -> None:
+        buf = (C.c_char * 128).from_buffer_copy(uid)
+        _check(lib().mcontact_gpu_comm_init(self._h, buf))
+
+    def CONTACT_ANALYSIS(self, maxit: int = 3000, check: bool = True) -> int:
+        return _check(lib().mcontact_gpu_iterate(self._h, maxit, 1 if check else 0))
+
+    def monitor(self) -> np.ndarray:
+        ncol = 2 * self.nsub + 8 * self.nint + 2
+        rows = _check(lib().mcontact_gpu_monitor(self._h, None, 0))
+        out = np.zeros((rows, ncol))
+        if rows:
+            _check(lib().mcontact_gpu_monitor(self._h, out.ctypes.data_as(_DP), rows))
+        return out
+
+    def get(self, what: str, index: int = 0) -> np.ndarray:
+        n = _check(lib().mcontact_gpu_get(self._h, what.encode(), index, None, 0))
+        dtype = np.int64 if what == "pcg_iters" else np.float64
+        out = np.zeros(n, dtype)
+        if n:
+            _check(lib().mcontact_gpu_get(self._h, what.encode(), index, _ptr(out), n))
+        return out
+
+    def timing(self) -> dict:
+        out = (C.c_double * 7)()
+        _check(lib().mcontact_gpu_timing(self._h, out))
+        keys = ["total_ms", "solve_ms", "iface_ms", "comm_ms", "spmv_kernel_ms", "spmv_launches", "pcg_iterations"]
+        return dict(zip(keys, list(out)))
+
+
+__all__ = ["Problem", "MULTIGRID", "MGPIS", "MCONTACT", "DdpcaError", "lib", "gpu_available", "default_options",
+           "LIBPATH"]

@@ -1,0 +1,79 @@
+"""In-tree build of libddpca_amd.so (hipcc, gfx950) -- no JIT cache, no pip install.
+
+Every translation unit under csrc/ is compiled by hipcc (``--offload-arch=gfx950`` for the
+.hip device sources) into build/obj and linked into ``libddpca_amd.so`` next to this file, so
+the built library travels with the repository snapshot to the GPU box.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import hashlib
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+HERE = Path(__file__).resolve().parent
+CSRC = HERE / "csrc"
+OBJ = HERE / "build" / "obj"
+LIB = HERE / "libddpca_amd.so"
+ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
+HIPCC = str(ROCM / "bin" / "hipcc")
+ARCH = "gfx950"
+
+COMMON = ["-O3", "-std=c++17", "-fPIC", "-fopenmp", "-Wall", "-Wno-unused-function",
+          "-Wno-unknown-pragmas", f"-I{HERE.parent / 'include'}", f"-I{CSRC}"]
+DEVICE = [f"--offload-arch={ARCH}", "-munsafe-fp-atomics"]
+LINK = ["-shared", "-fopenmp", f"--offload-arch={ARCH}", f"-L{ROCM / 'lib'}", "-lamdhip64", "-lrccl",
+        f"-Wl,-rpath,{ROCM / 'lib'}", f"-Wl,-rpath,{ROCM / 'llvm' / 'lib'}"]
+
+
+def _sources() -> list[Path]:
+    return sorted(list(CSRC.glob("*.cpp")) + list(CSRC.glob("*.hip")))
+
+
+def _digest(src: Path, flags: list[str]) -> str:
+    h = hashlib.sha1(" ".join(flags).encode())
+    h.update(src.read_bytes())
+    for hdr in sorted(CSRC.glob("*.hpp")) + sorted((HERE.parent / "include").glob("*.h")):
+        h.update(hdr.read_bytes())
+    return h.hexdigest()[:16]
+
+
+def _compile(src: Path) -> Path:
+    flags = COMMON + (DEVICE if src.suffix == ".hip" else [])
+    if src.suffix == ".hip":
+        flags = flags + ["-x", "hip"]
+    obj = OBJ / f"{src.stem}.{_digest(src, flags)}.o"
+    if not obj.exists():
+        cmd = [HIPCC, *flags, "-c", str(src), "-o", str(obj)]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"compile failed: {src.name}\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    return obj
+
+
+def build(verbose: bool = False) -> Path:
+    OBJ.mkdir(parents=True, exist_ok=True)
+    srcs = _sources()
+    jobs = min(len(srcs), int(os.environ.get("MAX_JOBS", os.cpu_count() or 4)), 16)
+    with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+        objs = list(ex.map(_compile, srcs))
+    stamp = hashlib.sha1("".join(o.name for o in objs).encode()).hexdigest()[:16]
+    stamp_file = OBJ / "link.stamp"
+    if LIB.exists() and stamp_file.exists() and stamp_file.read_text() == stamp:
+        return LIB
+    tmp = LIB.with_suffix(".so.tmp")
+    cmd = [HIPCC, *[str(o) for o in objs], *LINK, "-o", str(tmp)]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    os.replace(tmp, LIB)
+    stamp_file.write_text(stamp)
+    if verbose:
+        print(f"built {LIB}", file=sys.stderr)
+    return LIB
+
+
+if __name__ == "__main__":
+    build(verbose=True)

@@ -1,0 +1,232 @@
+// C ABI: MGPIS device solver entry points (mgpis_gpu_*), see include/ddpca_amd.h.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <memory>
+
+#include "../../include/ddpca_amd.h"
+#include "device_mgpis.hpp"
+#include "problem.hpp"
+
+using namespace ddpca;
+
+struct ddpca_mgpis {
+    std::unique_ptr<MgpisDevice> dev;
+};
+
+namespace {
+
+// Condensed CSR (reference consStif[l]) + free_dof map -> unconstrained-layout BSR3 whose
+// constrained rows/cols are zero (the device masks them to identity anyway).
+Bsr3 csr_to_bsr3(int64_t nn, int64_t nfree, const int32_t* free_dof, const int64_t* ptr, const int32_t* col,
+                 const double* val) {
+    std::vector<std::vector<std::pair<int32_t, int>>> rows(nn);
+    std::vector<std::vector<int32_t>> bcols(nn);
+    for (int64_t r = 0; r < nfree; ++r) {
+        const int32_t dr = free_dof[r];
+        for (int64_t k = ptr[r]; k < ptr[r + 1]; ++k) bcols[dr / 3].push_back(free_dof[col[k]] / 3);
+    }
+    Bsr3 B;
+    B.nb = B.mb = nn;
+    B.ptr.assign(nn + 1, 0);
+    for (int64_t i = 0; i < nn; ++i) {
+        bcols[i].push_back((int32_t)i);  // keep the diagonal block even for fully constrained nodes
+        std::sort(bcols[i].begin(), bcols[i].end());
+        bcols[i].erase(std::unique(bcols[i].begin(), bcols[i].end()), bcols[i].end());
+        B.ptr[i + 1] = B.ptr[i] + (int64_t)bcols[i].size();
+    }
+    B.col.resize(B.ptr[nn]);
+    B.val.assign(9 * B.ptr[nn], 0.0);
+    for (int64_t i = 0; i < nn; ++i) std::copy(bcols[i].begin(), bcols[i].end(), B.col.begin() + B.ptr[i]);
+    for (int64_t r = 0; r < nfree; ++r) {
+        const int32_t dr = free_dof[r];
+        const int64_t i = dr / 3;
+        const int32_t* cb = &B.col[B.ptr[i]];
+        const int64_t len = B.ptr[i + 1] - B.ptr[i];
+        for (int64_t k = ptr[r]; k < ptr[r + 1]; ++k) {
+            const int32_t dc = free_dof[col[k]];
+            const int64_t pos = B.ptr[i] + (std::lower_bound(cb, cb + len, dc / 3) - cb);
+            B.val[9 * pos + 3 * (dr % 3) + dc % 3] += val[k];
+        }
+    }
+    return B;
+}
+
+Stencil make_stencil(int64_t nf, int64_t nc, const int64_t* ptr, const int32_t* col, const double* w) {
+    Stencil S;
+    S.nf = nf;
+    S.nc = nc;
+    S.ptr.assign(ptr, ptr + nf + 1);
+    S.col.assign(col, col + ptr[nf]);
+    S.w.assign(w, w + ptr[nf]);
+    return S;
+}
+
+mgpis_options_t resolve(const mgpis_options_t* opt) {
+    mgpis_options_t o;
+    mgpis_default_options(&o);
+    if (opt) o = *opt;
+    return o;
+}
+
+}  // namespace
+
+extern "C" {
+
+void mgpis_default_options(mgpis_options_t* opt) {
+    opt->smoother = 1;
+    opt->nu = 1;
+    opt->omega = 0.0;
+    opt->iters_per_graph = 4;
+}
+
+int ddpca_gpu_available(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return 0;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, 0) != hipSuccess) return 0;
+    return std::strncmp(prop.gcnArchName, "gfx950", 6) == 0 ? 1 : 0;
+}
+
+int mgpis_gpu_create(int device, int nlev, const int64_t* nnodes, const int64_t* nfree,
+                     const int32_t* const* free_dof, const int64_t* const* K_ptr, const int32_t* const* K_col,
+                     const double* const* K_val, const int64_t* const* S_ptr, const int32_t* const* S_col,
+                     const double* const* S_w, const mgpis_options_t* opt, mgpis_t* out) {
+    return guarded([&] {
+        if (nlev < 1 || !nnodes || !nfree || !free_dof || !K_ptr || !K_col || !K_val || !out)
+            throw ApiError(DDPCA_EINVAL, "null argument");
+        std::vector<Bsr3> B(nlev);
+        std::vector<Stencil> S(nlev - 1);
+        for (int l = 0; l < nlev; ++l) B[l] = csr_to_bsr3(nnodes[l], nfree[l], free_dof[l], K_ptr[l], K_col[l], K_val[l]);
+        for (int l = 0; l + 1 < nlev; ++l) S[l] = make_stencil(nnodes[l + 1], nnodes[l], S_ptr[l], S_col[l], S_w[l]);
+        const int64_t nn = nnodes[nlev - 1];
+        std::vector<uint8_t> fr(3 * nn, 0);
+        for (int64_t r = 0; r < nfree[nlev - 1]; ++r) fr[free_dof[nlev - 1][r]] = 1;
+        std::vector<int64_t> nn_v(nnodes, nnodes + nlev);
+        std::vector<const Bsr3*> Bp;
+        std::vector<const Stencil*> Sp;
+        for (auto& b : B) Bp.push_back(&b);
+        for (auto& s : S) Sp.push_back(&s);
+        auto h = std::make_unique<ddpca_mgpis>();
+        h->dev = std::make_unique<MgpisDevice>(device, nn_v, Bp, fr, Sp, resolve(opt));
+        *out = h.release();
+    });
+}
+
+int mgpis_gpu_create_bsr3(int device, int nlev, const int64_t* nnodes, const int64_t* const* B_ptr,
+                          const int32_t* const* B_col, const double* const* B_val, const uint8_t* dof_free,
+                          const int64_t* const* S_ptr, const int32_t* const* S_col, const double* const* S_w,
+                          const mgpis_options_t* opt, mgpis_t* out) {
+    return guarded([&] {
+        if (nlev < 1 || !nnodes || !B_ptr || !B_col || !B_val || !dof_free || !out) throw ApiError(DDPCA_EINVAL, "null argument");
+        std::vector<Bsr3> B(nlev);
+        std::vector<Stencil> S(nlev - 1);
+        for (int l = 0; l < nlev; ++l) {
+            B[l].nb = B[l].mb = nnodes[l];
+            B[l].ptr.assign(B_ptr[l], B_ptr[l] + nnodes[l] + 1);
+            B[l].col.assign(B_col[l], B_col[l] + B_ptr[l][nnodes[l]]);
+            B[l].val.assign(B_val[l], B_val[l] + 9 * B_ptr[l][nnodes[l]]);
+        }
+        for (int l = 0; l + 1 < nlev; ++l) S[l] = make_stencil(nnodes[l + 1], nnodes[l], S_ptr[l], S_col[l], S_w[l]);
+        std::vector<uint8_t> fr(dof_free, dof_free + 3 * nnodes[nlev - 1]);
+        std::vector<int64_t> nn_v(nnodes, nnodes + nlev);
+        std::vector<const Bsr3*> Bp;
+        std::vector<const Stencil*> Sp;
+        for (auto& b : B) Bp.push_back(&b);
+        for (auto& s : S) Sp.push_back(&s);
+        auto h = std::make_unique<ddpca_mgpis>();
+        h->dev = std::make_unique<MgpisDevice>(device, nn_v, Bp, fr, Sp, resolve(opt));
+        *out = h.release();
+    });
+}
+
+int ddpca_problem_mgpis(ddpca_problem_t p, int64_t tv, int device, const mgpis_options_t* opt, mgpis_t* out) {
+    return guarded([&] {
+        Problem& P = *reinterpret_cast<Problem*>(p);
+        if (!P.established) throw ApiError(DDPCA_ESTATE, "problem not established");
+        if (tv < 0 || tv >= (int64_t)P.mc.multGrid.size()) throw ApiError(DDPCA_EINVAL, "subdomain index");
+        const MULTIGRID& g = P.mc.multGrid[tv];
+        std::vector<int64_t> nn(g.leveCount.begin(), g.leveCount.end());
+        std::vector<const Bsr3*> Bp;
+        std::vector<const Stencil*> Sp;
+        for (const auto& b : g.levelStif) Bp.push_back(&b);
+        for (const auto& s : g.scalProl) Sp.push_back(&s);
+        auto h = std::make_unique<ddpca_mgpis>();
+        h->dev = std::make_unique<MgpisDevice>(device, nn, Bp, g.consFlag, Sp, resolve(opt));
+        *out = h.release();
+    });
+}
+
+int mgpis_gpu_solve(mgpis_t h, const double* b, double* x, int prec, double rtol, int64_t maxit, int64_t* iters,
+                    double* relres) {
+    int64_t it = 0;
+    int rc = guarded([&] {
+        if (!h || !b || !x) throw ApiError(DDPCA_EINVAL, "null argument");
+        if (prec != 0 && prec != 1) throw ApiError(DDPCA_EINVAL, "prec must be 0 or 1");
+        MgpisDevice& D = *h->dev;
+        select_device(D.device);
+        DevBuf<double> tmp;
+        tmp.upload(b, D.nfree);
+        D.scatter_free(tmp.p, D.bs.p);
+        D.pcg_solve(prec, rtol, maxit, &it, relres);
+        D.gather_free(D.xs.p, tmp.p);
+        DDPCA_HIP(hipMemcpyAsync(x, tmp.p, D.nfree * sizeof(double), hipMemcpyDeviceToHost, D.stream));
+        DDPCA_HIP(hipStreamSynchronize(D.stream));
+        if (iters) *iters = it;
+    });
+    if (rc != 0) return rc;
+    return (maxit > 0 && it >= maxit) ? (int)std::min<int64_t>(it, 1 << 30) : 0;
+}
+
+int mgpis_gpu_spmv(mgpis_t h, int level, const double* x, double* y) {
+    return guarded([&] {
+        MgpisDevice& D = *h->dev;
+        select_device(D.device);
+        if (level < 0 || level >= (int)D.lev.size()) throw ApiError(DDPCA_EINVAL, "level");
+        if (level != (int)D.lev.size() - 1) throw ApiError(DDPCA_EINVAL, "condensed spmv is defined on the fine level");
+        DevBuf<double> tmp, full_x, full_y;
+        tmp.upload(x, D.nfree);
+        full_x.alloc(3 * D.lev.back().nn);
+        full_y.alloc(3 * D.lev.back().nn);
+        D.scatter_free(tmp.p, full_x.p);
+        D.spmv(level, full_x.p, full_y.p);
+        D.gather_free(full_y.p, tmp.p);
+        DDPCA_HIP(hipMemcpyAsync(y, tmp.p, D.nfree * sizeof(double), hipMemcpyDeviceToHost, D.stream));
+        DDPCA_HIP(hipStreamSynchronize(D.stream));
+    });
+}
+
+int mgpis_gpu_vcycle(mgpis_t h, const double* r, double* z) {
+    return guarded([&] {
+        MgpisDevice& D = *h->dev;
+        select_device(D.device);
+        DevBuf<double> tmp;
+        tmp.upload(r, D.nfree);
+        D.scatter_free(tmp.p, D.rs.p);
+        DDPCA_HIP(hipMemsetAsync(D.sc.p, 0, sizeof(PcgScal), D.stream));  // done = 0
+        D.vcycle(D.rs.p, D.zs.p, false);
+        D.gather_free(D.zs.p, tmp.p);
+        DDPCA_HIP(hipMemcpyAsync(z, tmp.p, D.nfree * sizeof(double), hipMemcpyDeviceToHost, D.stream));
+        DDPCA_HIP(hipStreamSynchronize(D.stream));
+    });
+}
+
+int mgpis_gpu_info(mgpis_t h, int64_t* out7) {
+    return guarded([&] {
+        MgpisDevice& D = *h->dev;
+        out7[0] = (int64_t)D.lev.size();
+        out7[1] = D.nfree;
+        out7[2] = D.lev.back().nnzb;
+        out7[3] = D.lev.back().nch;
+        out7[4] = (int64_t)(D.lev.back().omega * 1e6);
+        out7[5] = (int64_t)(D.lev.back().lmax * 1e6);
+        out7[6] = D.device;
+    });
+}
+
+int mgpis_gpu_destroy(mgpis_t h) {
+    return guarded([&] { delete h; });
+}
+
+}  // extern "C"

@@ -1,0 +1,59 @@
+// MCONTACT: host restatement of the reference's interface operator assembly
+// (MCONTACT::ESTABLISH, MCONTACT.h:181-896) and the per-iteration data contract of
+// CONTACT_ANALYSIS (MCONTACT.h:2493-2723).  The ADMM loop itself runs on the GPU
+// (device_mcontact.hip); this file only builds operands.
+#pragma once
+#include <array>
+#include <cstdint>
+#include <vector>
+
+#include "multigrid.hpp"
+
+namespace ddpca {
+
+// CSEARCH::INTEGRAL_POINT (CSEARCH.h:19-32): the setup-time data contract of one interface.
+struct IntegralPoint {
+    int64_t node[2][4];
+    double shap[2][4];
+    double basis[3][3];  // 0 normal (master side), 1/2 tangents
+    double gap;          // initNgap
+    double w;            // quadWeig
+};
+
+struct Interface {
+    int64_t body[2] = {0, 0};      // contBody[ts]
+    double fric = -1.0;            // fricCoef: <0 glued, 0 frictionless, >0 Coulomb
+    double penN = 0.0, penF = 0.0;  // penaFact_n / penaFact_f
+    std::vector<IntegralPoint> ip;
+    // ---- operators (MCONTACT.h:213-810); side s in {0, 1}
+    std::vector<int64_t> nodeCont[2];  // contact index -> body node id (insertion order)
+    Csr systMass[2], systTran[2], systTran_pena[2];
+    Csr inteMass[2], inteMass_pena[2];
+    Csr inpoLagr[2], inpoDisp[2], inteInpo[2], pemaInpo_r[2];
+    std::vector<double> inpoNgap;  // m_ip
+    std::vector<double> pemaDiag;  // pemaInpo diagonal, m_ip
+    int comp() const { return fric == 0.0 ? 1 : 3; }
+    int64_t mip() const { return comp() * (int64_t)ip.size(); }
+    int64_t mside(int s) const { return comp() * (int64_t)nodeCont[s].size(); }
+    void BUILD(const MULTIGRID& g0, const MULTIGRID& g1);
+};
+
+class MCONTACT {
+public:
+    std::vector<MULTIGRID> multGrid;
+    std::vector<Interface> searCont;
+    int64_t muscSett = 0;
+    // ESTABLISH: interface operators, systMass added to each body's stiffness, then
+    // TRANSFER / STIF_MATR / CONSTRAINT(1) per body (MCONTACT.h:812-825).
+    void ESTABLISH();
+    double GET_CHAR_LENG() const;  // MCONTACT.h:2478-2491
+};
+
+// Conforming-face integration points (restatement of CSEARCH::SEGMENT_INTERSECT for two
+// coincident quadrilateral faces: polygon = master face, 4 centroid triangles x 4-point
+// triangle rule, CSEARCH.h:614-775).  mast/slav: 4 node ids of matching faces, oriented as
+// EFACE_SURFACE returns them.
+void conforming_face_ips(const MULTIGRID& gm, const int64_t mast[4], const MULTIGRID& gs,
+                         const int64_t slav[4], std::vector<IntegralPoint>& out);
+
+}  // namespace ddpca

@@ -1,0 +1,518 @@
+// Host restatement of the reference's MULTIGRID operator pipeline (see multigrid.hpp).
+#include "multigrid.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <stdexcept>
+#include <omp.h>
+
+namespace ddpca {
+
+namespace {
+
+uint64_t latt_key(const std::array<int64_t, 3>& p) {
+    for (int a = 0; a < 3; ++a)
+        if (p[a] < 0 || p[a] >= (int64_t(1) << 21)) throw std::runtime_error("lattice coordinate out of range");
+    return (uint64_t(p[0]) << 42) | (uint64_t(p[1]) << 21) | uint64_t(p[2]);
+}
+
+// Corner positions of a hex on the 3x3x3 subdivision grid (reference refiTemp_2, corners).
+const int kCornerPos[8][3] = {{0, 0, 0}, {2, 0, 0}, {2, 2, 0}, {0, 2, 0},
+                              {0, 0, 2}, {2, 0, 2}, {2, 2, 2}, {0, 2, 2}};
+// Creation order of the 19 new nodes of a pattern-0 refinement (12 edge midpoints, 6 face
+// centres, 1 body centre) as positions on the subdivision grid (MULTIGRID.h:382-443).
+const int kNewPos[19][3] = {{1, 0, 0}, {2, 1, 0}, {1, 2, 0}, {0, 1, 0}, {0, 0, 1}, {2, 0, 1}, {2, 2, 1},
+                            {0, 2, 1}, {1, 0, 2}, {2, 1, 2}, {1, 2, 2}, {0, 1, 2}, {0, 1, 1}, {2, 1, 1},
+                            {1, 0, 1}, {1, 2, 1}, {1, 1, 0}, {1, 1, 2}, {1, 1, 1}};
+// Local corner offsets of a child element on the subdivision grid (MULTIGRID.h:445-453).
+const int kHexOff[8][3] = {{0, 0, 0}, {1, 0, 0}, {1, 1, 0}, {0, 1, 0},
+                           {0, 0, 1}, {1, 0, 1}, {1, 1, 1}, {0, 1, 1}};
+
+// 3-point Gauss rule (PREP.h:235-281): index g = i*9 + j*3 + k over (xi, eta, zeta).
+struct HexQuad {
+    double w[27];
+    double dN[27][3][8];
+    HexQuad() {
+        const double pt[3] = {-std::sqrt(3.0 / 5.0), 0.0, std::sqrt(3.0 / 5.0)};
+        const double wt[3] = {5.0 / 9.0, 8.0 / 9.0, 5.0 / 9.0};
+        const double nc[8][3] = {{-1, -1, -1}, {1, -1, -1}, {1, 1, -1}, {-1, 1, -1},
+                                 {-1, -1, 1},  {1, -1, 1},  {1, 1, 1},  {-1, 1, 1}};
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j)
+                for (int k = 0; k < 3; ++k) {
+                    const int g = i * 9 + j * 3 + k;
+                    const double x = pt[i], y = pt[j], z = pt[k];
+                    w[g] = wt[i] * wt[j] * wt[k];
+                    for (int n = 0; n < 8; ++n) {
+                        dN[g][0][n] = nc[n][0] * (1.0 + nc[n][1] * y) * (1.0 + nc[n][2] * z) / 8.0;
+                        dN[g][1][n] = (1.0 + nc[n][0] * x) * nc[n][1] * (1.0 + nc[n][2] * z) / 8.0;
+                        dN[g][2][n] = (1.0 + nc[n][0] * x) * (1.0 + nc[n][1] * y) * nc[n][2] / 8.0;
+                    }
+                }
+    }
+};
+const HexQuad& hexquad() {
+    static HexQuad q;
+    return q;
+}
+
+double jacobian(const double dN[3][8], const double X[8][3], double J[3][3]) {
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) {
+            double s = 0;
+            for (int n = 0; n < 8; ++n) s += dN[r][n] * X[n][c];
+            J[r][c] = s;
+        }
+    return J[0][0] * (J[1][1] * J[2][2] - J[1][2] * J[2][1]) - J[0][1] * (J[1][0] * J[2][2] - J[1][2] * J[2][0]) +
+           J[0][2] * (J[1][0] * J[2][1] - J[1][1] * J[2][0]);
+}
+
+// 24x24 element stiffness, K_E = sum_g w_g det(J) B^T D B  (MULTIGRID.h:988-1014)
+void element_stiffness(const double X[8][3], const double D[6][6], double KE[24][24]) {
+    const HexQuad& q = hexquad();
+    for (int a = 0; a < 24; ++a)
+        for (int b = 0; b < 24; ++b) KE[a][b] = 0.0;
+    for (int g = 0; g < 27; ++g) {
+        double J[3][3];
+        const double det = jacobian(q.dN[g], X, J);
+        double Ji[3][3];
+        Ji[0][0] = (J[1][1] * J[2][2] - J[1][2] * J[2][1]) / det;
+        Ji[0][1] = (J[0][2] * J[2][1] - J[0][1] * J[2][2]) / det;
+        Ji[0][2] = (J[0][1] * J[1][2] - J[0][2] * J[1][1]) / det;
+        Ji[1][0] = (J[1][2] * J[2][0] - J[1][0] * J[2][2]) / det;
+        Ji[1][1] = (J[0][0] * J[2][2] - J[0][2] * J[2][0]) / det;
+        Ji[1][2] = (J[0][2] * J[1][0] - J[0][0] * J[1][2]) / det;
+        Ji[2][0] = (J[1][0] * J[2][1] - J[1][1] * J[2][0]) / det;
+        Ji[2][1] = (J[0][1] * J[2][0] - J[0][0] * J[2][1]) / det;
+        Ji[2][2] = (J[0][0] * J[1][1] - J[0][1] * J[1][0]) / det;
+        double B[6][24] = {};
+        for (int n = 0; n < 8; ++n) {
+            double d[3];
+            for (int c = 0; c < 3; ++c) d[c] = Ji[c][0] * q.dN[g][0][n] + Ji[c][1] * q.dN[g][1][n] + Ji[c][2] * q.dN[g][2][n];
+            B[0][3 * n + 0] = d[0];
+            B[1][3 * n + 1] = d[1];
+            B[2][3 * n + 2] = d[2];
+            B[3][3 * n + 0] = d[1];
+            B[3][3 * n + 1] = d[0];
+            B[4][3 * n + 1] = d[2];
+            B[4][3 * n + 2] = d[1];
+            B[5][3 * n + 0] = d[2];
+            B[5][3 * n + 2] = d[0];
+        }
+        double DB[6][24];
+        for (int r = 0; r < 6; ++r)
+            for (int c = 0; c < 24; ++c) {
+                double s = 0;
+                for (int k = 0; k < 6; ++k) s += D[r][k] * B[k][c];
+                DB[r][c] = s;
+            }
+        const double f = q.w[g] * det;
+        for (int a = 0; a < 24; ++a)
+            for (int b = 0; b < 24; ++b) {
+                double s = 0;
+                for (int k = 0; k < 6; ++k) s += B[k][a] * DB[k][b];
+                KE[a][b] += f * s;
+            }
+    }
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------------- mesh
+int64_t MULTIGRID::TRY_ADD_NODE(const std::array<int64_t, 3>& latt, const std::array<double, 3>& xyz) {
+    const uint64_t key = latt_key(latt);
+    auto it = lattNode.find(key);
+    if (it != lattNode.end()) return it->second;
+    const int64_t id = (int64_t)nodeCoor.size();
+    lattNode.emplace(key, id);
+    nodeCoor.push_back(xyz);
+    nodeLatt.push_back(latt);
+    nodeLevel.push_back(0);
+    nodeParents.emplace_back();
+    return id;
+}
+
+int64_t MULTIGRID::ADD_ELEMENT(const TreeElem& e) {
+    elemVect.push_back(e);
+    maxiLeve = std::max<int64_t>(maxiLeve, e.level);
+    return (int64_t)elemVect.size() - 1;
+}
+
+void MULTIGRID::REFINE_ALL() {
+    const int64_t ne = (int64_t)elemVect.size();
+    for (int64_t e = 0; e < ne; ++e) {
+        if (elemVect[e].firstChild >= 0) continue;
+        const std::array<int64_t, 8> corn = elemVect[e].cornNode;
+        const int lev = elemVect[e].level;
+        int64_t grid[3][3][3];
+        for (int k = 0; k < 8; ++k) grid[kCornerPos[k][0]][kCornerPos[k][1]][kCornerPos[k][2]] = corn[k];
+        for (int t = 0; t < 19; ++t) {
+            const int* q = kNewPos[t];
+            std::vector<int64_t> par;
+            for (int k = 0; k < 8; ++k) {
+                bool on = true;
+                for (int a = 0; a < 3; ++a) on &= (q[a] == 1 || q[a] == kCornerPos[k][a]);
+                if (on) par.push_back(corn[k]);
+            }
+            std::sort(par.begin(), par.end());
+            std::array<int64_t, 3> latt{0, 0, 0};
+            std::array<double, 3> xyz{0.0, 0.0, 0.0};
+            for (int64_t p : par)
+                for (int a = 0; a < 3; ++a) {
+                    latt[a] += nodeLatt[p][a];
+                    xyz[a] = xyz[a] + nodeCoor[p][a];
+                }
+            for (int a = 0; a < 3; ++a) {
+                if (latt[a] % (int64_t)par.size()) throw std::runtime_error("lattice too coarse for refinement");
+                latt[a] /= (int64_t)par.size();
+                xyz[a] = xyz[a] / (double)par.size();
+            }
+            const int64_t before = numNodes();
+            const int64_t id = TRY_ADD_NODE(latt, xyz);
+            if (id == before) {
+                nodeLevel[id] = lev + 1;
+                nodeParents[id] = par;
+            }
+            grid[q[0]][q[1]][q[2]] = id;
+        }
+        elemVect[e].firstChild = (int64_t)elemVect.size();
+        for (int c = 0; c < 8; ++c) {
+            TreeElem ch;
+            ch.parent = e;
+            ch.level = lev + 1;
+            for (int m = 0; m < 8; ++m)
+                ch.cornNode[m] = grid[(c & 1) + kHexOff[m][0]][((c >> 1) & 1) + kHexOff[m][1]][((c >> 2) & 1) + kHexOff[m][2]];
+            ADD_ELEMENT(ch);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------- transfer
+void MULTIGRID::TRANSFER() {
+    const int64_t N = numNodes();
+    leveCount.assign(maxiLeve + 1, 0);
+    for (int64_t i = 0; i < N; ++i) {
+        if (i > 0 && nodeLevel[i] < nodeLevel[i - 1])
+            throw std::runtime_error("node ids are not level ordered (non-uniform refinement)");
+        leveCount[nodeLevel[i]]++;
+    }
+    for (int64_t l = 1; l <= maxiLeve; ++l) leveCount[l] += leveCount[l - 1];
+    scalProl.assign(maxiLeve, Stencil());
+    for (int64_t l = 0; l < maxiLeve; ++l) {
+        Stencil& S = scalProl[l];
+        S.nc = leveCount[l];
+        S.nf = leveCount[l + 1];
+        S.ptr.assign(S.nf + 1, 0);
+        for (int64_t i = 0; i < S.nf; ++i) {
+            if (i < S.nc) {
+                S.col.push_back((int32_t)i);
+                S.w.push_back(1.0);
+            } else {
+                const auto& par = nodeParents[i];
+                for (int64_t p : par) {
+                    S.col.push_back((int32_t)p);
+                    S.w.push_back(1.0 / (double)par.size());
+                }
+            }
+            S.ptr[i + 1] = (int64_t)S.col.size();
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------- stiffness
+void MULTIGRID::STIF_MATR() {
+    const int64_t N = numNodes();
+    const double lam = mateElas * matePois / (1.0 + matePois) / (1.0 - 2.0 * matePois);
+    const double mu = mateElas / 2.0 / (1.0 + matePois);
+    double D[6][6] = {};
+    for (int a = 0; a < 3; ++a)
+        for (int b = 0; b < 3; ++b) D[a][b] = lam + (a == b ? 2.0 * mu : 0.0);
+    D[3][3] = D[4][4] = D[5][5] = mu;
+    std::vector<int64_t> leaves;
+    for (int64_t e = 0; e < (int64_t)elemVect.size(); ++e)
+        if (elemVect[e].firstChild < 0) leaves.push_back(e);
+    // node adjacency (nodes sharing a leaf element)
+    std::vector<std::vector<int32_t>> adj(N);
+    for (int64_t e : leaves)
+        for (int a = 0; a < 8; ++a)
+            for (int b = 0; b < 8; ++b) adj[elemVect[e].cornNode[a]].push_back((int32_t)elemVect[e].cornNode[b]);
+#pragma omp parallel for schedule(dynamic, 1024)
+    for (int64_t i = 0; i < N; ++i) {
+        std::sort(adj[i].begin(), adj[i].end());
+        adj[i].erase(std::unique(adj[i].begin(), adj[i].end()), adj[i].end());
+    }
+    origStif = Bsr3();
+    origStif.nb = origStif.mb = N;
+    origStif.ptr.assign(N + 1, 0);
+    for (int64_t i = 0; i < N; ++i) origStif.ptr[i + 1] = origStif.ptr[i] + (int64_t)adj[i].size();
+    origStif.col.resize(origStif.ptr[N]);
+    for (int64_t i = 0; i < N; ++i) std::copy(adj[i].begin(), adj[i].end(), origStif.col.begin() + origStif.ptr[i]);
+    adj.clear();
+    adj.shrink_to_fit();
+    origStif.val.assign(9 * origStif.ptr[N], 0.0);
+    // colour leaf elements so that one colour shares no node (uniform octree: lattice parity)
+    int64_t h = -1;
+    bool uniform = true;
+    for (int64_t e : leaves) {
+        const auto& c0 = nodeLatt[elemVect[e].cornNode[0]];
+        int64_t ext = 0;
+        for (int k = 1; k < 8; ++k)
+            for (int a = 0; a < 3; ++a) ext = std::max<int64_t>(ext, std::llabs(nodeLatt[elemVect[e].cornNode[k]][a] - c0[a]));
+        if (h < 0) h = ext;
+        if (ext != h) uniform = false;
+    }
+    std::vector<std::vector<int64_t>> colour(uniform ? 8 : 1);
+    for (int64_t e : leaves) {
+        if (!uniform) { colour[0].push_back(e); continue; }
+        int64_t lo[3] = {INT64_MAX, INT64_MAX, INT64_MAX};
+        for (int k = 0; k < 8; ++k)
+            for (int a = 0; a < 3; ++a) lo[a] = std::min(lo[a], nodeLatt[elemVect[e].cornNode[k]][a]);
+        colour[((lo[0] / h) & 1) | (((lo[1] / h) & 1) << 1) | (((lo[2] / h) & 1) << 2)].push_back(e);
+    }
+    for (const auto& list : colour) {
+#pragma omp parallel if (uniform)
+        {
+            double KE[24][24];
+            double Xlast[8][3];
+            bool have = false;
+#pragma omp for schedule(static)
+            for (int64_t t = 0; t < (int64_t)list.size(); ++t) {
+                const TreeElem& el = elemVect[list[t]];
+                double X[8][3], R[8][3];
+                for (int k = 0; k < 8; ++k)
+                    for (int a = 0; a < 3; ++a) {
+                        X[k][a] = nodeCoor[el.cornNode[k]][a];
+                        R[k][a] = X[k][a] - X[0][a];
+                    }
+                bool same = have;
+                for (int k = 0; k < 8 && same; ++k)
+                    for (int a = 0; a < 3; ++a) same &= (R[k][a] == Xlast[k][a]);
+                if (!same) {
+                    element_stiffness(X, D, KE);
+                    for (int k = 0; k < 8; ++k)
+                        for (int a = 0; a < 3; ++a) Xlast[k][a] = R[k][a];
+                    have = true;
+                }
+                for (int a = 0; a < 8; ++a) {
+                    const int64_t r = el.cornNode[a];
+                    const int32_t* cb = &origStif.col[origStif.ptr[r]];
+                    const int64_t len = origStif.ptr[r + 1] - origStif.ptr[r];
+                    for (int b = 0; b < 8; ++b) {
+                        const int64_t pos = origStif.ptr[r] + (std::lower_bound(cb, cb + len, (int32_t)el.cornNode[b]) - cb);
+                        double* blk = origStif.block(pos);
+                        for (int i = 0; i < 3; ++i)
+                            for (int j = 0; j < 3; ++j) blk[3 * i + j] += KE[3 * a + i][3 * b + j];
+                    }
+                }
+            }
+        }
+    }
+}
+
+double MULTIGRID::GET_VOLUME() const {
+    const HexQuad& q = hexquad();
+    const int64_t ne = (int64_t)elemVect.size();
+    const int64_t part = 50000;
+    const int64_t np = (ne + part - 1) / part;
+    std::vector<double> pv(np, 0.0);
+#pragma omp parallel for schedule(static)
+    for (int64_t p = 0; p < np; ++p)
+        for (int64_t e = p * part; e < std::min(ne, (p + 1) * part); ++e) {
+            if (elemVect[e].firstChild >= 0) continue;
+            double X[8][3], J[3][3];
+            for (int k = 0; k < 8; ++k)
+                for (int a = 0; a < 3; ++a) X[k][a] = nodeCoor[elemVect[e].cornNode[k]][a];
+            for (int g = 0; g < 27; ++g) pv[p] += q.w[g] * jacobian(q.dN[g], X, J);
+        }
+    double v = 0.0;
+    for (double x : pv) v += x;
+    return v;
+}
+
+void MULTIGRID::ADD_NODAL(const Csr& A) {
+    for (int64_t r = 0; r < A.nrow; ++r)
+        for (int64_t k = A.ptr[r]; k < A.ptr[r + 1]; ++k) {
+            const int64_t i = r / 3, j = A.col[k] / 3;
+            const int32_t* cb = &origStif.col[origStif.ptr[i]];
+            const int64_t len = origStif.ptr[i + 1] - origStif.ptr[i];
+            const int32_t* hit = std::lower_bound(cb, cb + len, (int32_t)j);
+            if (hit == cb + len || *hit != j) throw std::runtime_error("ADD_NODAL: entry outside stiffness pattern");
+            origStif.block(origStif.ptr[i] + (hit - cb))[3 * (r % 3) + (A.col[k] % 3)] += A.val[k];
+        }
+}
+
+// ---------------------------------------------------------------------------------- constraints
+void MULTIGRID::LOAD_ACCU(int64_t dof, double v) {
+    if (consDofv.count(dof)) return;  // MULTIGRID.h:1084-1100: loads on constrained dofs dropped
+    auto it = exteForc.find(dof);
+    if (it == exteForc.end()) exteForc.emplace(dof, v);
+    else it->second = it->second + v;
+}
+
+void MULTIGRID::CONSTRAINT() {
+    const int64_t N = numNodes();
+    const int64_t L = maxiLeve;
+    levelStif.assign(L + 1, Bsr3());
+    levelStif[L] = origStif;
+    for (int64_t l = L - 1; l >= 0; --l) levelStif[l] = galerkin_rap(levelStif[l + 1], scalProl[l]);
+    consFlag.assign(3 * N, 1);
+    std::vector<double> dfull(3 * N, 0.0);
+    for (const auto& kv : consDofv) {
+        consFlag[kv.first] = 0;
+        dfull[kv.first] = kv.second;
+    }
+    freeIndex.assign(3 * N, -1);
+    freeCount.assign(L + 1, 0);
+    int64_t nf = 0;
+    dispForc.clear();
+    for (int64_t d = 0; d < 3 * N; ++d) {
+        if (consFlag[d]) freeIndex[d] = (int32_t)nf++;
+        else dispForc.push_back(dfull[d]);
+    }
+    for (int64_t l = 0; l <= L; ++l) {
+        int64_t c = 0;
+        for (int64_t d = 0; d < 3 * leveCount[l]; ++d) c += consFlag[d];
+        freeCount[l] = c;
+    }
+    std::vector<double> f(3 * N, 0.0);
+    for (const auto& kv : exteForc) f[kv.first] += kv.second;
+    std::vector<double> Kd(3 * N, 0.0);
+    if (!consDofv.empty()) levelStif[L].apply(dfull.data(), Kd.data());
+    consForc.assign(nf, 0.0);
+    for (int64_t d = 0; d < 3 * N; ++d)
+        if (consFlag[d]) consForc[freeIndex[d]] = f[d] - Kd[d];
+}
+
+void MULTIGRID::ADDITIONAL_FORCE(const double* f_nodal, double* f_free) const {
+    const int64_t n = 3 * numNodes();
+    for (int64_t d = 0; d < n; ++d)
+        if (consFlag[d]) f_free[freeIndex[d]] = f_nodal[d];
+}
+
+void MULTIGRID::OUTP_SUB1(const double* x_free, double* u_nodal) const {
+    const int64_t n = 3 * numNodes();
+    for (int64_t d = 0; d < n; ++d) u_nodal[d] = consFlag[d] ? x_free[freeIndex[d]] : 0.0;
+    for (const auto& kv : consDofv) u_nodal[kv.first] = kv.second;
+}
+
+Csr MULTIGRID::consStif(int64_t level) const {
+    return condense(levelStif[level], freeIndex, freeCount[level]);
+}
+
+Csr MULTIGRID::realProl(int64_t level) const {
+    const Stencil& S = scalProl[level];
+    Csr P;
+    P.nrow = freeCount[level + 1];
+    P.ncol = freeCount[level];
+    P.ptr.assign(P.nrow + 1, 0);
+    for (int64_t i = 0; i < S.nf; ++i)
+        for (int a = 0; a < 3; ++a) {
+            const int32_t r = freeIndex[3 * i + a];
+            if (r < 0) continue;
+            for (int64_t k = S.ptr[i]; k < S.ptr[i + 1]; ++k) {
+                const int32_t c = freeIndex[3 * (int64_t)S.col[k] + a];
+                if (c < 0) continue;
+                P.col.push_back(c);
+                P.val.push_back(S.w[k]);
+            }
+            P.ptr[r + 1] = (int64_t)P.col.size();
+        }
+    return P;
+}
+
+// ---------------------------------------------------------------------------------- builders
+void build_beam(MULTIGRID& g, const int64_t divi[3], int64_t globLeve, const int64_t doma[3], int64_t tg) {
+    const double PI = std::acos(-1.0);
+    const double leng[3] = {1.0, 0.12, 0.06};
+    const double lengFact = 1.0 / 3.0;
+    const double angl = 45.0 * PI / 180.0;
+    const double loadInte = -8000.0;
+    const int64_t real[3] = {divi[0] / doma[0], divi[1] / doma[1], divi[2] / doma[2]};
+    const int64_t t0 = tg / (doma[1] * doma[2]);
+    const int64_t t1 = (tg % (doma[1] * doma[2])) / doma[2];
+    const int64_t t2 = (tg % (doma[1] * doma[2])) % doma[2];
+    const int64_t scale = int64_t(1) << globLeve;
+    std::vector<int64_t> id((real[0] + 1) * (real[1] + 1) * (real[2] + 1));
+    auto I = [&](int64_t i, int64_t j, int64_t k) { return (i * (real[1] + 1) + j) * (real[2] + 1) + k; };
+    for (int64_t i = 0; i <= real[0]; ++i) {
+        const int64_t ir = t0 * real[0] + i;
+        const double x = leng[0] / divi[0] * ir;
+        const double heig = leng[1] * (1.0 - (double)ir / divi[0] * lengFact);
+        const double widt = leng[2] * (1.0 - (double)ir / divi[0] * lengFact);
+        for (int64_t j = 0; j <= real[1]; ++j) {
+            const int64_t jr = t1 * real[1] + j;
+            const double y = -heig / 2.0 + heig / divi[1] * (double)jr;
+            for (int64_t k = 0; k <= real[2]; ++k) {
+                const int64_t kr = t2 * real[2] + k;
+                const double z = -widt / 2.0 + widt / divi[2] * (double)kr;
+                id[I(i, j, k)] = g.TRY_ADD_NODE({ir * scale, jr * scale, kr * scale}, {x, y, z});
+            }
+        }
+    }
+    for (int64_t i = 0; i < real[0]; ++i)
+        for (int64_t j = 0; j < real[1]; ++j)
+            for (int64_t k = 0; k < real[2]; ++k) {
+                TreeElem e;
+                e.cornNode = {id[I(i, j, k)],         id[I(i, j + 1, k)],         id[I(i, j + 1, k + 1)],
+                              id[I(i, j, k + 1)],     id[I(i + 1, j, k)],         id[I(i + 1, j + 1, k)],
+                              id[I(i + 1, j + 1, k + 1)], id[I(i + 1, j, k + 1)]};
+                g.ADD_ELEMENT(e);
+            }
+    for (int64_t r = 0; r < globLeve; ++r) g.REFINE_ALL();
+    if (g.maxiLeve < 0) g.maxiLeve = 0;
+    // COOR_ADJU (BEAM.h:79-99): twist about the x axis, angle proportional to x
+    for (auto& c : g.nodeCoor) {
+        const double a = 1.0 * (angl * c[0] / leng[0]);
+        const double y = std::cos(a) * c[1] - std::sin(a) * c[2];
+        const double z = std::sin(a) * c[1] + std::cos(a) * c[2];
+        c[1] = y;
+        c[2] = z;
+    }
+    // SUBR_COLO, loadType 0 (BEAM.h:101-141)
+    for (int64_t n = 0; n < g.numNodes(); ++n)
+        if (g.nodeCoor[n][0] <= 1.0e-10)
+            for (int a = 0; a < 3; ++a) g.consDofv.emplace(3 * n + a, 0.0);
+    static const int kLine[12][2] = {{0, 1}, {1, 2}, {2, 3}, {3, 0}, {0, 4}, {1, 5},
+                                     {2, 6}, {3, 7}, {4, 5}, {5, 6}, {6, 7}, {7, 4}};
+    for (const auto& el : g.elemVect) {
+        if (el.firstChild >= 0) continue;
+        for (const auto& ln : kLine) {
+            const int64_t n0 = el.cornNode[ln[0]], n1 = el.cornNode[ln[1]];
+            bool on = true;
+            for (int64_t n : {n0, n1})
+                if (std::abs(g.nodeCoor[n][1]) > 1.0e-10 || std::abs(g.nodeCoor[n][2]) > 1.0e-10) on = false;
+            if (!on) continue;
+            const double f = loadInte * std::abs(g.nodeCoor[n0][0] - g.nodeCoor[n1][0]) / 2.0 / 4.0;
+            for (int64_t n : {n0, n1})
+                if (g.nodeCoor[n][0] > 1.0e-10) g.LOAD_ACCU(3 * n + 2, f);
+        }
+    }
+}
+
+void build_box(MULTIGRID& g, const double lo[3], const double hi[3], const int64_t n[3], int64_t globLeve,
+               const int64_t latt_off[3]) {
+    const int64_t scale = int64_t(1) << globLeve;
+    const int64_t o[3] = {latt_off ? latt_off[0] : 0, latt_off ? latt_off[1] : 0, latt_off ? latt_off[2] : 0};
+    std::vector<int64_t> id((n[0] + 1) * (n[1] + 1) * (n[2] + 1));
+    auto I = [&](int64_t i, int64_t j, int64_t k) { return (i * (n[1] + 1) + j) * (n[2] + 1) + k; };
+    for (int64_t i = 0; i <= n[0]; ++i)
+        for (int64_t j = 0; j <= n[1]; ++j)
+            for (int64_t k = 0; k <= n[2]; ++k)
+                id[I(i, j, k)] = g.TRY_ADD_NODE({(o[0] + i) * scale, (o[1] + j) * scale, (o[2] + k) * scale},
+                                                {lo[0] + (hi[0] - lo[0]) / n[0] * i, lo[1] + (hi[1] - lo[1]) / n[1] * j,
+                                                 lo[2] + (hi[2] - lo[2]) / n[2] * k});
+    for (int64_t i = 0; i < n[0]; ++i)
+        for (int64_t j = 0; j < n[1]; ++j)
+            for (int64_t k = 0; k < n[2]; ++k) {
+                TreeElem e;
+                e.cornNode = {id[I(i, j, k)],     id[I(i + 1, j, k)],     id[I(i + 1, j + 1, k)],     id[I(i, j + 1, k)],
+                              id[I(i, j, k + 1)], id[I(i + 1, j, k + 1)], id[I(i + 1, j + 1, k + 1)], id[I(i, j + 1, k + 1)]};
+                g.ADD_ELEMENT(e);
+            }
+    for (int64_t r = 0; r < globLeve; ++r) g.REFINE_ALL();
+    if (g.maxiLeve < 0) g.maxiLeve = 0;
+}
+
+}  // namespace ddpca

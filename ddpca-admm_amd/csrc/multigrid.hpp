@@ -1,0 +1,95 @@
+// MULTIGRID: host restatement of the reference's operator-producing subset
+// (MULTIGRID.h:10-95) for uniformly refined hexahedral octrees:
+//   REFINE (pattern 0)   MULTIGRID.h:375-545   node creation order reproduced exactly, so the
+//                                              level-ordered numbering equals the reference's
+//   TRANSFER             MULTIGRID.h:756-948   level sets + scalar prolongation stencils
+//   STIF_MATR            MULTIGRID.h:950-1039  8-node hex, 3x3x3 Gauss, isotropic
+//   GET_VOLUME           MULTIGRID.h:1041-1082
+//   CONSTRAINT(1)        MULTIGRID.h:1102-1255 Galerkin hierarchy, Dirichlet condensation
+//   ADDITIONAL_FORCE     MULTIGRID.h:1257-1261
+//   OUTP_SUB1            MULTIGRID.h:1263-1281
+// Out of scope here: local/anisotropic refinement, hanging nodes, nodal
+// rotations (nodeRota), coupling nodes, stress recovery, text output.
+#pragma once
+#include <array>
+#include <cstdint>
+#include <map>
+#include <unordered_map>
+#include <vector>
+
+#include "sparse.hpp"
+
+namespace ddpca {
+
+struct TreeElem {
+    int64_t parent = -1;
+    std::array<int64_t, 8> cornNode{};
+    int level = 0;
+    int64_t firstChild = -1;  // 8 children are consecutive (ADD_ELEMENT order)
+};
+
+class MULTIGRID {
+public:
+    // ---------------------------------------------------------------- mesh
+    std::vector<std::array<double, 3>> nodeCoor;   // node id == reference node id
+    std::vector<std::array<int64_t, 3>> nodeLatt;  // integer lattice position (topology key)
+    std::vector<int> nodeLevel;
+    std::vector<std::vector<int64_t>> nodeParents;  // parents of a refined node (sorted ids)
+    std::vector<TreeElem> elemVect;
+    std::unordered_map<uint64_t, int64_t> lattNode;  // lattice key -> node (TRY_ADD_NODE lookup)
+    int64_t maxiLeve = -1;
+    int64_t TRY_ADD_NODE(const std::array<int64_t, 3>& latt, const std::array<double, 3>& xyz);
+    int64_t ADD_ELEMENT(const TreeElem& e);
+    // One uniform refinement round: MULTIGRID::REFINE with refiPatt = 0 on every leaf element.
+    void REFINE_ALL();
+    int64_t numNodes() const { return (int64_t)nodeCoor.size(); }
+
+    // ---------------------------------------------------------------- transfer
+    std::vector<int64_t> leveCount;   // nodes of levels <= l  (levels 0..maxiLeve)
+    std::vector<Stencil> scalProl;    // level l+1 nodes x level l nodes
+    void TRANSFER();
+
+    // ---------------------------------------------------------------- stiffness
+    double mateElas = 210.0e9;
+    double matePois = 0.3;
+    Bsr3 origStif;  // full nodal stiffness (reference origStif[maxiLeve + 1])
+    void STIF_MATR();
+    double GET_VOLUME() const;
+    // origStif += A (A given as scalar CSR on the 3N nodal dofs, pattern inside node adjacency)
+    void ADD_NODAL(const Csr& A);
+
+    // ---------------------------------------------------------------- constraints
+    std::map<int64_t, double> consDofv;  // prescribed dof values
+    std::map<int64_t, double> exteForc;  // external nodal forces
+    void LOAD_ACCU(int64_t dof, double v);
+    std::vector<Bsr3> levelStif;          // unconstrained Galerkin operators origStif[l]
+    std::vector<uint8_t> consFlag;        // 3N: 1 free, 0 constrained
+    std::vector<int32_t> freeIndex;       // 3N: condensed index or -1
+    std::vector<int64_t> freeCount;       // free dofs on level l
+    std::vector<double> consForc;         // condensed load (MULTIGRID::consForc)
+    std::vector<double> dispForc;         // prescribed values of constrained dofs, dof order
+    void CONSTRAINT();
+
+    // ---------------------------------------------------------------- per-iteration adapters
+    // f_free = consOper * prolOper^T * earlTran^T * f_nodal (identities except consOper here)
+    void ADDITIONAL_FORCE(const double* f_nodal, double* f_free) const;
+    // u_nodal = earlTran * prolOper * [x_free scattered; prescribed values]
+    void OUTP_SUB1(const double* x_free, double* u_nodal) const;
+
+    // reference-layout operators (MGPIS::consStif / realProl, condensed scalar CSR)
+    Csr consStif(int64_t level) const;
+    Csr realProl(int64_t level) const;  // level+1 <- level
+};
+
+// Coarse-mesh builders used by the examples (node creation order as in the reference).
+// BEAM (BEAM.h:61-186, 251-388): subdomain tg of a domaNumb decomposition of the tapered,
+// twisted cantilever (domaNumb = {1,1,1}, tg = 0 is MESH_NODD), incl. COOR_ADJU and
+// SUBR_COLO with loadType 0 (clamped root, centreline line load).
+void build_beam(MULTIGRID& g, const int64_t divi[3], int64_t globLeve, const int64_t doma[3],
+                int64_t tg);
+// Axis-aligned box with BLOCK.h's corner convention, refined globLeve times.
+// latt_off: this block's origin on a lattice shared with its neighbours (coarse units).
+void build_box(MULTIGRID& g, const double lo[3], const double hi[3], const int64_t n[3],
+               int64_t globLeve, const int64_t latt_off[3] = nullptr);
+
+}  // namespace ddpca

@@ -1,0 +1,138 @@
+// Host sparse kernels for operator setup (not on the per-iteration path).
+#include "sparse.hpp"
+
+#include <algorithm>
+#include <numeric>
+#include <omp.h>
+
+namespace ddpca {
+
+void Bsr3::apply(const double* x, double* y) const {
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < nb; ++i) {
+        double a0 = 0, a1 = 0, a2 = 0;
+        for (int64_t k = ptr[i]; k < ptr[i + 1]; ++k) {
+            const double* b = &val[9 * k];
+            const double* xj = x + 3 * (int64_t)col[k];
+            a0 += b[0] * xj[0] + b[1] * xj[1] + b[2] * xj[2];
+            a1 += b[3] * xj[0] + b[4] * xj[1] + b[5] * xj[2];
+            a2 += b[6] * xj[0] + b[7] * xj[1] + b[8] * xj[2];
+        }
+        y[3 * i] = a0;
+        y[3 * i + 1] = a1;
+        y[3 * i + 2] = a2;
+    }
+}
+
+Bsr3 galerkin_rap(const Bsr3& A, const Stencil& S) {
+    const int64_t nc = S.nc;
+    // S^T: coarse node -> list of (fine node, weight)
+    std::vector<int64_t> tptr(nc + 1, 0);
+    for (int64_t f = 0; f < S.nf; ++f)
+        for (int64_t k = S.ptr[f]; k < S.ptr[f + 1]; ++k) tptr[S.col[k] + 1]++;
+    for (int64_t c = 0; c < nc; ++c) tptr[c + 1] += tptr[c];
+    std::vector<int32_t> tcol(tptr[nc]);
+    std::vector<double> tw(tptr[nc]);
+    {
+        std::vector<int64_t> fill(tptr.begin(), tptr.end() - 1);
+        for (int64_t f = 0; f < S.nf; ++f)
+            for (int64_t k = S.ptr[f]; k < S.ptr[f + 1]; ++k) {
+                int64_t p = fill[S.col[k]]++;
+                tcol[p] = (int32_t)f;
+                tw[p] = S.w[k];
+            }
+    }
+    std::vector<std::vector<int32_t>> rcol(nc);
+    std::vector<std::vector<double>> rval(nc);
+#pragma omp parallel
+    {
+        std::vector<int32_t> mark(nc, -1);
+        std::vector<int32_t> cols;
+        std::vector<double> acc;
+#pragma omp for schedule(dynamic, 64)
+        for (int64_t c1 = 0; c1 < nc; ++c1) {
+            cols.clear();
+            acc.clear();
+            for (int64_t t = tptr[c1]; t < tptr[c1 + 1]; ++t) {
+                const int64_t f1 = tcol[t];
+                const double w1 = tw[t];
+                for (int64_t k = A.ptr[f1]; k < A.ptr[f1 + 1]; ++k) {
+                    const int64_t f2 = A.col[k];
+                    const double* blk = A.block(k);
+                    for (int64_t s = S.ptr[f2]; s < S.ptr[f2 + 1]; ++s) {
+                        const int32_t c2 = S.col[s];
+                        const double ww = w1 * S.w[s];
+                        int32_t pos = mark[c2];
+                        if (pos < 0) {
+                            pos = (int32_t)cols.size();
+                            mark[c2] = pos;
+                            cols.push_back(c2);
+                            acc.resize(acc.size() + 9, 0.0);
+                        }
+                        double* a = &acc[9 * (size_t)pos];
+                        for (int q = 0; q < 9; ++q) a[q] += ww * blk[q];
+                    }
+                }
+            }
+            std::vector<int32_t> order(cols.size());
+            std::iota(order.begin(), order.end(), 0);
+            std::sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return cols[a] < cols[b]; });
+            rcol[c1].resize(cols.size());
+            rval[c1].resize(9 * cols.size());
+            for (size_t q = 0; q < order.size(); ++q) {
+                rcol[c1][q] = cols[order[q]];
+                std::copy(&acc[9 * (size_t)order[q]], &acc[9 * (size_t)order[q]] + 9, &rval[c1][9 * q]);
+            }
+            for (int32_t c2 : cols) mark[c2] = -1;
+        }
+    }
+    Bsr3 C;
+    C.nb = C.mb = nc;
+    C.ptr.assign(nc + 1, 0);
+    for (int64_t c = 0; c < nc; ++c) C.ptr[c + 1] = C.ptr[c] + (int64_t)rcol[c].size();
+    C.col.resize(C.ptr[nc]);
+    C.val.resize(9 * C.ptr[nc]);
+#pragma omp parallel for schedule(static)
+    for (int64_t c = 0; c < nc; ++c) {
+        std::copy(rcol[c].begin(), rcol[c].end(), C.col.begin() + C.ptr[c]);
+        std::copy(rval[c].begin(), rval[c].end(), C.val.begin() + 9 * C.ptr[c]);
+    }
+    return C;
+}
+
+Csr condense(const Bsr3& A, const std::vector<int32_t>& free_index, int64_t nfree) {
+    Csr C;
+    C.nrow = C.ncol = nfree;
+    C.ptr.assign(nfree + 1, 0);
+    // row counts
+    for (int64_t i = 0; i < A.nb; ++i)
+        for (int a = 0; a < 3; ++a) {
+            const int32_t r = free_index[3 * i + a];
+            if (r < 0) continue;
+            int64_t cnt = 0;
+            for (int64_t k = A.ptr[i]; k < A.ptr[i + 1]; ++k)
+                for (int b = 0; b < 3; ++b) cnt += free_index[3 * (int64_t)A.col[k] + b] >= 0;
+            C.ptr[r + 1] = cnt;
+        }
+    for (int64_t r = 0; r < nfree; ++r) C.ptr[r + 1] += C.ptr[r];
+    C.col.resize(C.ptr[nfree]);
+    C.val.resize(C.ptr[nfree]);
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < A.nb; ++i)
+        for (int a = 0; a < 3; ++a) {
+            const int32_t r = free_index[3 * i + a];
+            if (r < 0) continue;
+            int64_t p = C.ptr[r];
+            for (int64_t k = A.ptr[i]; k < A.ptr[i + 1]; ++k)
+                for (int b = 0; b < 3; ++b) {
+                    const int32_t c = free_index[3 * (int64_t)A.col[k] + b];
+                    if (c < 0) continue;
+                    C.col[p] = c;
+                    C.val[p] = A.val[9 * k + 3 * a + b];
+                    ++p;
+                }
+        }
+    return C;
+}
+
+}  // namespace ddpca

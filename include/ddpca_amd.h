@@ -1,0 +1,161 @@
+/*
+ * ddpca_amd.h -- C ABI of libddpca_amd.so, the MI355X-native hot path of DDPCA-ADMM.
+ *
+ * Drop-in boundary for the per-subdomain solve loop of the reference
+ * (QuanchengP/DDPCA-ADMM).  The reference is header-only C++ with no FFI; its interface for
+ * this path is the class surface of MGPIS (MGPIS.h:8-38), MULTIGRID (MULTIGRID.h:10-95) and
+ * MCONTACT (MCONTACT.h:9-95).  Each entry point below cites the reference member it replaces.
+ * Plain pointers and sizes only.  Host pointers are borrowed (copied at create); device memory
+ * is owned by the handle.  Return 0 on success, a negative DDPCA_E* code on error; a positive
+ * return from a solve is the iteration count when the iteration cap was reached.
+ * Handles are independent: calls on different handles may run concurrently from different
+ * host threads (the reference calls CG_SOLV concurrently per subdomain, MCONTACT.h:2511).
+ */
+#ifndef DDPCA_AMD_H
+#define DDPCA_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DDPCA_OK 0
+#define DDPCA_EINVAL (-1)   /* bad argument / shape */
+#define DDPCA_EHIP (-2)     /* HIP runtime error */
+#define DDPCA_ENOGPU (-3)   /* no gfx950 device visible */
+#define DDPCA_ESTATE (-4)   /* call sequence error */
+#define DDPCA_ECOMM (-5)    /* RCCL error */
+#define DDPCA_ENUMERIC (-6) /* NaN/Inf or breakdown in a Krylov scalar */
+
+/* last error message of the calling thread (never NULL) */
+const char* ddpca_last_error(void);
+/* 1 if a gfx950 device is visible, 0 otherwise (no HIP context is created otherwise) */
+int ddpca_gpu_available(void);
+
+/* ========================================================================================
+ * MGPIS -- multigrid-preconditioned CG on one subdomain (MGPIS.h:8-225)
+ * ======================================================================================== */
+typedef struct ddpca_mgpis* mgpis_t;
+
+typedef struct {
+    int smoother;      /* 0 = damped point Jacobi, 1 = 3x3 node-block Jacobi, 2 = Chebyshev(deg) on block Jacobi */
+    int nu;            /* sweeps (Jacobi) or polynomial degree (Chebyshev) pre and post */
+    double omega;      /* Jacobi damping; <= 0: 4 / (3 * lambda_max(D^-1 K)) estimated at create */
+    int iters_per_graph; /* PCG iterations captured per hipGraph replay (>= 1) */
+} mgpis_options_t;
+
+/* Fill default options. */
+void mgpis_default_options(mgpis_options_t* opt);
+
+/* Replaces MULTIGRID::CONSTRAINT(1) -> MGPIS::ESTABLISH() (MULTIGRID.h:1245-1252,
+ * MGPIS.h:40-53): uploads the level hierarchy in the reference's own layout.
+ *   nlev                       = maxiLeve + 1
+ *   nnodes[l]                  nodes of level <= l (level-ordered numbering, MULTIGRID.h:884-910)
+ *   nfree[l]                   rows of consStif[l]
+ *   free_dof[l][i]             nodal dof (3*node + comp) of condensed row i (consOper[l])
+ *   K_ptr/K_col/K_val[l]       consStif[l] as CSR (int64 row pointer, int32 columns)
+ *   S_ptr/S_col/S_w[l]         scalar stencil scalProl[l], nnodes[l+1] x nnodes[l], l < nlev-1
+ *                              (realProl[l] = consOper[l+1] (S (x) I3) consOper[l]^T)
+ * The coarse level is inverted once here (the reference re-factorises it on every CG_SOLV
+ * call, MGPIS.h:185). */
+int mgpis_gpu_create(int device, int nlev, const int64_t* nnodes, const int64_t* nfree,
+                     const int32_t* const* free_dof, const int64_t* const* K_ptr,
+                     const int32_t* const* K_col, const double* const* K_val,
+                     const int64_t* const* S_ptr, const int32_t* const* S_col,
+                     const double* const* S_w, const mgpis_options_t* opt, mgpis_t* out);
+
+/* Same hierarchy in node-block form: B_*[l] is the UNCONSTRAINED Galerkin operator
+ * origStif[l] (MULTIGRID.h:1182-1184) as 3x3-block CSR (9 doubles per block, row-major);
+ * dof_free[3*nnodes[nlev-1]] marks free dofs (consFlag, MULTIGRID.h:1186-1194). */
+int mgpis_gpu_create_bsr3(int device, int nlev, const int64_t* nnodes,
+                          const int64_t* const* B_ptr, const int32_t* const* B_col,
+                          const double* const* B_val, const uint8_t* dof_free,
+                          const int64_t* const* S_ptr, const int32_t* const* S_col,
+                          const double* const* S_w, const mgpis_options_t* opt, mgpis_t* out);
+
+/* Replaces MGPIS::CG_SOLV(precSwit, totaForc, resuSolu) (MGPIS.h:163-225):
+ * x0 = 0, stop when ||r|| <= rtol * ||b|| on the recursive residual (reference rtol = 1e-14)
+ * or after maxit iterations (reference maxit = rows).  prec: 0 diagonal (DIAG_PREC,
+ * PREP.h:393-401), 1 multigrid V-cycle.  b, x are condensed host vectors of length nfree[L].
+ * iters/relres may be NULL.  Returns 0, or maxit (> 0) when the cap was hit. */
+int mgpis_gpu_solve(mgpis_t h, const double* b, double* x, int prec, double rtol,
+                    int64_t maxit, int64_t* iters, double* relres);
+
+/* y = consStif[level] * x (condensed host vectors), for parity tests of the SpMV kernel. */
+int mgpis_gpu_spmv(mgpis_t h, int level, const double* x, double* y);
+/* z = M^-1 r: one V-cycle from zero (MGPIS::MULT_VCYC, MGPIS.h:55-128) on condensed vectors. */
+int mgpis_gpu_vcycle(mgpis_t h, const double* r, double* z);
+/* Informational: [nlev, n_fine_free, nnzb_fine, chunks_fine, omega*1e6, lambda_max*1e6, device] */
+int mgpis_gpu_info(mgpis_t h, int64_t* out7);
+int mgpis_gpu_destroy(mgpis_t h);
+
+/* ========================================================================================
+ * Host problem construction (setup only, not on the hot path): the reference's MULTIGRID
+ * mesh/operator pipeline and MCONTACT::ESTABLISH restated in C++ (mcontact.cpp,
+ * multigrid.cpp).  Produces the operands of the device path.
+ * ======================================================================================== */
+typedef struct ddpca_problem* ddpca_problem_t;
+
+/* kind / params:
+ *   "beam"     d0 d1 d2 globLeve D0 D1 D2       BEAM.h (D = 1,1,1: MESH_NODD; else MESH_DD,
+ *                                              glued interfaces fricCoef = -1, BEAM.h:424-470)
+ *   "twoblock" fric globLeve                    two stacked blocks, one contact interface
+ *   "dehw"     ngroups nx ny nz globLeve fric   synthetic DEHW-shaped chain: per group one
+ *                                              worm and one wheel block in frictional contact,
+ *                                              groups glued along x (worm-worm, wheel-wheel) */
+int ddpca_problem_create(const char* kind, const double* params, int nparams, ddpca_problem_t* out);
+/* Replace the integration points of interface ts (CSEARCH::intePoin, CSEARCH.h:19-32):
+ * node[n][2][4], shap[n][2][4], basis[n][3][3], gap[n], w[n]. */
+int ddpca_problem_set_ips(ddpca_problem_t p, int64_t ts, int64_t n, const int64_t* node,
+                          const double* shap, const double* basis, const double* gap,
+                          const double* w, double fric, double penN, double penF);
+/* MCONTACT::ESTABLISH (MCONTACT.h:181-896) minus the coarse space; single grids just run
+ * TRANSFER / STIF_MATR / CONSTRAINT(1). */
+int ddpca_problem_establish(ddpca_problem_t p);
+/* Read-only view of an internal array.  dtype: 0 float64, 1 int64, 2 int32, 3 uint8.
+ * Names: see ddpca_amd.py (_ARRAYS). index = subdomain, level or 2*interface+side. */
+int ddpca_problem_view(ddpca_problem_t p, const char* name, int64_t index, int64_t level,
+                       const void** data, int64_t* count, int* dtype);
+int ddpca_problem_destroy(ddpca_problem_t p);
+/* Build the device solver of subdomain tv from the problem (mgpis_gpu_create_bsr3). */
+int ddpca_problem_mgpis(ddpca_problem_t p, int64_t tv, int device, const mgpis_options_t* opt,
+                        mgpis_t* out);
+
+/* ========================================================================================
+ * MCONTACT -- the ADMM loop of CONTACT_ANALYSIS on the GPU (MCONTACT.h:2493-2845)
+ * One handle per process (= per GPU); it owns the subdomains assigned to its rank and the
+ * interface sides that belong to them.  Interfaces whose sides live on different ranks are
+ * coupled by one RCCL all-reduce per iteration (gamma contributions) plus one of monitor
+ * norms.
+ * ======================================================================================== */
+typedef struct ddpca_mcontact* mcontact_t;
+
+/* owner[tv] = rank owning subdomain tv (all ranks pass the same array). */
+int mcontact_gpu_create(ddpca_problem_t p, int device, int rank, int nranks,
+                        const int32_t* owner, const mgpis_options_t* opt, mcontact_t* out);
+/* RCCL communicator from an ncclUniqueId (128 bytes) produced by rank 0 and broadcast by the
+ * caller (e.g. through torch.distributed); not needed when nranks == 1. */
+int mcontact_gpu_comm_init(mcontact_t h, const void* nccl_unique_id);
+/* 128-byte ncclUniqueId for rank 0 to broadcast. */
+int mcontact_gpu_unique_id(void* out128);
+/* Run up to maxit ADMM iterations (reference maxiIter = 3000) from the current state;
+ * stop on MONITOR convergence (MCONTACT.h:2725-2845) when check != 0.
+ * Returns the number of iterations run (>= 0) or a negative error. */
+int64_t mcontact_gpu_iterate(mcontact_t h, int64_t maxit, int check);
+/* Number of resuMoni columns (2*nsub + 8*nint + 2) and the monitor rows recorded so far
+ * (row-major, rows x cols) -- same columns as resuMoni.txt. */
+int64_t mcontact_gpu_monitor(mcontact_t h, double* out, int64_t cap_rows);
+/* Copy state to host: what = "resuDisp" (index = subdomain, nodal 3N), "inteAuxi"/"inteLagr"
+ * (index = 2*ts+side), "inpoGamm" (index = ts, projected gamma of the last iteration),
+ * "pcg_iters" (int64 per owned subdomain, last iteration). */
+int64_t mcontact_gpu_get(mcontact_t h, const char* what, int64_t index, void* out, int64_t cap);
+/* Device timing of the last iterate() call: [total_ms, solve_ms, iface_ms, comm_ms,
+ * spmv_kernel_ms, spmv_launches, pcg_iterations] */
+int mcontact_gpu_timing(mcontact_t h, double* out7);
+int mcontact_gpu_destroy(mcontact_t h);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DDPCA_AMD_H */
