@@ -630,6 +630,8 @@ MgpisDevice::~MgpisDevice() {
     if (stream) (void)hipStreamSynchronize(stream);
     for (auto& g : graph_)
         if (g) (void)hipGraphExecDestroy(g);
+    for (auto& g : graph_timed_)
+        if (g) (void)hipGraphExecDestroy(g);
     if (sc_host) (void)hipHostFree(sc_host);
     if (ev_k0) (void)hipEventDestroy(ev_k0);
     if (ev_k1) (void)hipEventDestroy(ev_k1);
@@ -814,16 +816,20 @@ void MgpisDevice::enqueue_iteration(int prec, bool timed) {
     hipLaunchKernelGGL(k_fin, dim3(1), dim3(kBlock), 0, stream, (int)kFinBeta, partial.p, nblk_fine, sc.p);
 }
 
+// graph_[prec]: iters_per_graph PCG iterations; graph_timed_[prec]: the same with two event
+// records bracketing the first fine-level SpMV (launched once per solve when timing is on, so
+// no later replay overwrites its events before pcg_poll() reads them).
 void MgpisDevice::build_graph(int prec) {
-    if (graph_[prec] && graph_timed_[prec] == time_kernel) return;
-    if (graph_[prec]) DDPCA_HIP(hipGraphExecDestroy(graph_[prec]));
-    graph_timed_[prec] = time_kernel;
-    hipGraph_t g;
-    DDPCA_HIP(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
-    for (int k = 0; k < opt.iters_per_graph; ++k) enqueue_iteration(prec, time_kernel && k == 0);
-    DDPCA_HIP(hipStreamEndCapture(stream, &g));
-    DDPCA_HIP(hipGraphInstantiate(&graph_[prec], g, nullptr, nullptr, 0));
-    DDPCA_HIP(hipGraphDestroy(g));
+    for (int timed = 0; timed < 2; ++timed) {
+        hipGraphExec_t& ge = timed ? graph_timed_[prec] : graph_[prec];
+        if (ge || (timed && !time_kernel)) continue;
+        hipGraph_t g;
+        DDPCA_HIP(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
+        for (int k = 0; k < opt.iters_per_graph; ++k) enqueue_iteration(prec, timed && k == 0);
+        DDPCA_HIP(hipStreamEndCapture(stream, &g));
+        DDPCA_HIP(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+        DDPCA_HIP(hipGraphDestroy(g));
+    }
 }
 
 void MgpisDevice::pcg_begin(int prec, double rtol, int64_t maxit) {
@@ -843,27 +849,33 @@ void MgpisDevice::pcg_begin(int prec, double rtol, int64_t maxit) {
 }
 
 void MgpisDevice::pcg_step(int prec, bool sample) {
-    DDPCA_HIP(hipGraphLaunch(graph_[prec], stream));
-    if (sample && time_kernel) {
-        // the events of the first captured iteration bracket one fine-level SpMV
-        DDPCA_HIP(hipStreamSynchronize(stream));
-        float ms = 0.f;
-        if (hipEventElapsedTime(&ms, ev_k0, ev_k1) == hipSuccess && ms > 0.f) {
-            timed_kernel_ms += ms;
-            timed_kernel_samples += 1;
-        }
-    }
+    const bool timed = sample && time_kernel && graph_timed_[prec] && !sample_pending_;
+    DDPCA_HIP(hipGraphLaunch(timed ? graph_timed_[prec] : graph_[prec], stream));
+    sample_pending_ |= timed;
 }
 
 bool MgpisDevice::pcg_poll() {
     DDPCA_HIP(hipMemcpyAsync(sc_host, sc.p, sizeof(PcgScal), hipMemcpyDeviceToHost, stream));
     DDPCA_HIP(hipStreamSynchronize(stream));
+    if (sample_pending_) {
+        // events of the timed replay bracket one fine-level SpMV that ran with done == 0
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, ev_k0, ev_k1) == hipSuccess && ms > 0.f) {
+            timed_kernel_ms += ms;
+            timed_kernel_samples += 1;
+        }
+        sample_pending_ = false;
+    }
     return sc_host->done != 0;
 }
 
 int64_t MgpisDevice::pcg_solve(int prec, double rtol, int64_t maxit, int64_t* iters, double* relres) {
     pcg_begin(prec, rtol, maxit);
-    while (!pcg_poll()) pcg_step(prec, true);
+    bool first = true;
+    while (!pcg_poll()) {
+        pcg_step(prec, first);
+        first = false;
+    }
     if (sc_host->fail) throw ApiError(DDPCA_ENUMERIC, "PCG breakdown (non-finite or non-positive curvature)");
     if (iters) *iters = sc_host->iter;
     if (relres) *relres = sc_host->bb > 0 ? std::sqrt(sc_host->rr / sc_host->bb) : 0.0;

@@ -102,7 +102,8 @@ public:
 
 private:
     hipGraphExec_t graph_[2] = {nullptr, nullptr};
-    bool graph_timed_[2] = {false, false};
+    hipGraphExec_t graph_timed_[2] = {nullptr, nullptr};
+    bool sample_pending_ = false;
     void build_graph(int prec);
     void enqueue_iteration(int prec, bool timed);
     void estimate_lmax(int level);

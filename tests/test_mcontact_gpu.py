@@ -1,0 +1,111 @@
+"""GPU parity of the ADMM loop (MCONTACT::CONTACT_ANALYSIS) against the reference itself.
+
+Golden cases were produced by running the reference (tests/golden/make_golden.py): a 2-subdomain
+glued beam (fricCoef -1, 3000 non-converged iterations), and two stacked blocks in frictionless
+(patch test) and Coulomb (mu = 0.3) contact.  The GPU path solves subdomains with MG-PCG to a
+1e-14 recursive residual where the reference uses LDLT (n < 50000), so trajectories agree to the
+PCG accuracy.  Tolerances: ADMM iteration count equal +-1; resuMoni rows k <= 50
+within 1e-7 relative (entries below 1e-12 of their column's peak are compared absolutely at
+that level); final displacements <= 1e-6 relative L2 per subdomain; contact pressures <= 1e-5
+relative on active integration points.
+"""
+import numpy as np
+import pytest
+
+from conftest import CASE_PARAMS, golden
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(ddpca, case, maxit=3000, **opts):
+    g = golden(case)
+    P = ddpca.Problem(*CASE_PARAMS[case])
+    # integration points from the reference (CSEARCH output), to pin the data contract exactly
+    for ts in range(P.nint):
+        fric, pn, pf = g[f"if{ts}_param"]
+        P.set_ips(ts, g[f"if{ts}_ip_node"], g[f"if{ts}_ip_shap"], g[f"if{ts}_ip_basis"], g[f"if{ts}_ip_gap"],
+                  g[f"if{ts}_ip_w"], float(fric), float(pn), float(pf))
+    P.ESTABLISH()
+    mc = ddpca.MCONTACT(P, **opts)
+    n = mc.CONTACT_ANALYSIS(maxit)
+    return g, P, mc, n
+
+
+def _rows_close(rows, ref, k=50, rtol=1e-7, floor=1e-12):
+    k = min(k, len(ref), len(rows))
+    a, b = rows[:k], ref[:k]
+    scale = np.abs(ref).max(axis=0, keepdims=True)
+    err = np.abs(a - b)
+    ok = err <= rtol * np.abs(b) + floor * scale
+    return ok.all(), (err / np.maximum(np.abs(b), floor * scale)).max()
+
+
+@pytest.mark.parametrize("case", ["twoblock_f0", "twoblock_f3", "beam_dd"])
+def test_admm_matches_reference(ddpca, gpu, case):
+    g, P, mc, n = _run(ddpca, case)
+    ref_iters = len(g["resuMoni"])
+    assert abs(n - ref_iters) <= 1, (n, ref_iters)
+    ok, worst = _rows_close(mc.monitor(), g["resuMoni"])
+    assert ok, worst
+    for tv in range(P.nsub):
+        u, ur = mc.get("resuDisp", tv), g[f"sd{tv}_resuDisp"]
+        assert np.linalg.norm(u - ur) <= 1e-6 * np.linalg.norm(ur)
+
+
+@pytest.mark.parametrize("case", ["twoblock_f0", "twoblock_f3"])
+def test_contact_pressure_matches_reference(ddpca, gpu, case):
+    g, P, mc, n = _run(ddpca, case)
+    gam = mc.get("inpoGamm", 0)
+    fric = float(g["if0_param"][0])
+    ref = g["if0_resuCont"].reshape(-1, 1 if fric == 0.0 else 5)
+    gn = gam if fric == 0.0 else gam.reshape(-1, 3)[:, 0]
+    active = ref[:, 0] > 1e-3 * ref[:, 0].max()
+    assert active.any()
+    assert np.all(np.abs(gn[active] - ref[active, 0]) <= 1e-5 * np.abs(ref[active, 0]))
+    if fric > 0.0:
+        basis = g["if0_ip_basis"]
+        gt = gam.reshape(-1, 3)
+        trac = gt[:, 1:2] * basis[:, 1, :] + gt[:, 2:3] * basis[:, 2, :]
+        scale = np.abs(ref[:, 1:4]).max()
+        assert np.abs(trac - ref[:, 1:4]).max() <= 1e-5 * scale
+
+
+def test_patch_test_pressure(ddpca, gpu):
+    """BLOCK-style patch test: uniform 1e7 Pa load gives a uniform contact pressure."""
+    g, P, mc, n = _run(ddpca, "twoblock_f0")
+    gam = mc.get("inpoGamm", 0)
+    assert abs(gam.mean() / 1.0e7 - 1.0) < 1e-4
+    assert gam.min() > 0.999e7 and gam.max() < 1.001e7
+
+
+@pytest.mark.parametrize("smoother,nu", [(1, 1), (2, 2)])
+def test_admm_matches_oracle_on_generated_problem(ddpca, oracle, gpu, smoother, nu):
+    """Fixed-k trajectory of a synthetic DEHW-shaped problem (frictional contact + glued chain)
+    against the CPU oracle (exact subdomain solves) built from the same host operators."""
+    import scipy.sparse as sp
+    P = ddpca.Problem("dehw", 2, 2, 2, 1, 2, 0.3).ESTABLISH()
+    mc = ddpca.MCONTACT(P, smoother=smoother, nu=nu)
+    k = 40
+    assert mc.CONTACT_ANALYSIS(k, check=False) == k
+    subs, ifaces = _oracle_problem(P)
+    res = oracle.admm(subs, ifaces, maxit=k, check=False)
+    ok, worst = _rows_close(mc.monitor(), res["rows"], k=k, rtol=1e-6)
+    assert ok, worst
+
+
+def _oracle_problem(P):
+    from oracle.oracle import DenseSolver
+    subs = []
+    for tv in range(P.nsub):
+        G = P.grid(tv)
+        subs.append(dict(consForc=G.consForc, solve=DenseSolver(G.consStif(G.maxiLeve)), consFlag=G.consFlag,
+                         presc=np.zeros(len(G.consFlag))))
+    names = ["systTran", "systTran_pena", "inteMass", "inteMass_pena", "inpoLagr", "pemaInpo_r", "inteInpo"]
+    ifaces = []
+    for ts in range(P.nint):
+        fric, pn, pf = P.array("iface_param", ts)
+        ifaces.append(dict(body=tuple(int(b) for b in P.array("iface_body", ts)), fric=float(fric),
+                           comp=1 if fric == 0.0 else 3, pemaDiag=P.array("pemaDiag", ts),
+                           inpoNgap=P.array("inpoNgap", ts),
+                           ops=[{n: P.csr(n, 2 * ts + s) for n in names} for s in range(2)]))
+    return subs, ifaces
