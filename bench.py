@@ -1,0 +1,200 @@
+"""Benchmark: ADMM iterations/s of the DDPCA-ADMM solve loop on a synthetic DEHW-shaped mesh.
+
+Workload (BASELINE.json configs[4]): 8 subdomains of 1.23M DOF each
+(9.8M DOF), 4 worm/wheel groups -- each a frictional contact (mu = 0.2) between a worm block and
+a wheel block -- glued into two chains along x, 6 multigrid levels per subdomain.  One ADMM
+iteration = every subdomain's MGPIS PCG solve (1e-14 recursive residual, x0 = 0, as
+MGPIS::CG_SOLV) + the interface step + MONITOR.  The global problem is fixed and its subdomains
+are spread over the ranks (strong scaling); N = 1 runs all 8 on one MI355X.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+
+Rank 0 prints one JSON line.  `roofline` is the fine-level SELL-BSR3 SpMV kernel (the dominant
+kernel family), timed by HIP events recorded inside the replayed hipGraph on the solve stream;
+`cpu_baseline` is the CPU oracle (oracle/, SGS-faithful restatement of MGPIS) on one subdomain
+solve of the same workload, scaled to one ADMM iteration.
+"""
+from __future__ import annotations
+
+import argparse
+import importlib
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--groups", type=int, default=4, help="worm/wheel groups (2 subdomains each)")
+    ap.add_argument("--nx", type=int, default=3)
+    ap.add_argument("--ny", type=int, default=2)
+    ap.add_argument("--nz", type=int, default=2)
+    ap.add_argument("--gl", type=int, default=5, help="uniform refinements (levels = gl + 1)")
+    ap.add_argument("--fric", type=float, default=0.2)
+    ap.add_argument("--smoother", type=int, default=2)
+    ap.add_argument("--nu", type=int, default=2)
+    ap.add_argument("--iters-per-graph", type=int, default=4)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default=os.environ.get("DDPCA_TRAFFIC_JSON", ""),
+                    help="PMC-derived HBM bytes per launch of the roofline kernel (profiles/)")
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        if world == 1 and a.gpus > 1:
+            raise SystemExit("--gpus > 1 must be launched with torch.distributed.run (one process per GPU)")
+    import torch
+    import torch.distributed as dist
+
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    D = importlib.import_module("ddpca-admm_amd")
+    from importlib import import_module
+    part = import_module("ddpca-admm_amd.partition")
+
+    t_setup = time.perf_counter()
+    P = D.Problem("dehw", a.groups, a.nx, a.ny, a.nz, a.gl, a.fric)
+    nsub = P.nsub
+    owner = part.block_owner(nsub, world)
+    P.ESTABLISH(owner, rank)
+    mc = D.MCONTACT(P, device=local, rank=rank, nranks=world, owner=owner, smoother=a.smoother, nu=a.nu,
+                    iters_per_graph=a.iters_per_graph)
+    if world > 1:
+        obj = [mc.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        mc.comm_init(obj[0])
+    t_setup = time.perf_counter() - t_setup
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    if a.warmup > 0:
+        mc.CONTACT_ANALYSIS(a.warmup, check=False)
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    n = mc.CONTACT_ANALYSIS(a.steps, check=False)
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    tm = mc.timing()
+    if world > 1:
+        t = torch.tensor([elapsed, tm["dof_iterations"], tm["pcg_iterations"]], dtype=torch.float64)
+        tmax = t.clone()
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        tsum = t.clone()
+        dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
+        elapsed = float(tmax[0])
+        dof_its, pcg_its = float(tsum[1]), float(tsum[2])
+    else:
+        dof_its, pcg_its = tm["dof_iterations"], tm["pcg_iterations"]
+    dofs = [int(P.array("freeCount", tv)[-1]) if owner[tv] == rank else 0 for tv in range(nsub)]
+    total_dofs = sum(dofs)
+    if world > 1:
+        t = torch.tensor([float(total_dofs)], dtype=torch.float64)
+        dist.all_reduce(t)
+        total_dofs = int(t[0])
+
+    result = None
+    if rank == 0:
+        kern_ms = tm["spmv_kernel_ms"] / max(tm["spmv_samples"], 1.0)
+        kbytes = tm["spmv_bytes_per_launch"]
+        achieved = kbytes / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else None
+        traffic = None
+        if a.traffic_json and Path(a.traffic_json).exists():
+            traffic = json.loads(Path(a.traffic_json).read_text()).get("hbm_bytes_per_launch")
+        result = {
+            "metric": "ADMM iters/sec",
+            "value": n / elapsed,
+            "unit": "ADMM it/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": elapsed / n * 1e3,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic",
+            "config": {
+                "workload": f"dehw-synthetic: {nsub} subdomains x {total_dofs // nsub} DOF = {total_dofs} DOF, "
+                            f"{a.groups} frictional contacts (mu={a.fric}) + {2 * (a.groups - 1)} glued interfaces, "
+                            f"{a.gl + 1} MG levels, MGPIS-PCG rtol 1e-14",
+                "subdomains": nsub,
+                "dof": total_dofs,
+                "interfaces": P.nint,
+                "mg_levels": a.gl + 1,
+                "smoother": {0: "jacobi", 1: "block-jacobi", 2: "chebyshev"}[a.smoother] + f"({a.nu})",
+                "parallelism": f"dd{world}",
+            },
+            "mgpis_dof_iter_per_s": dof_its / elapsed,
+            "pcg_iters_per_solve": pcg_its / max(n * nsub, 1),
+            "setup_s": t_setup,
+            "roofline": {
+                "bound": "hbm",
+                "kernel": "k_sell<kPcg> fine level (SELL-BSR3 SpMV q=Kz+beta q, p=z+beta p, p.q)",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS if achieved else None,
+                "traffic": traffic,
+                "algorithmic_bytes_per_launch": kbytes,
+                "avg_launch_ms": kern_ms,
+                "samples": int(tm["spmv_samples"]),
+            },
+        }
+        if world == 1 and not a.no_cpu_baseline:
+            result["cpu_baseline"] = cpu_baseline(P, nsub, owner)
+    # release device state before the process group
+    del mc
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    if result is not None:
+        print(json.dumps(result), flush=True)
+
+
+def cpu_baseline(P, nsub, owner):
+    """SGS-faithful CPU restatement (oracle/) of one subdomain's CG_SOLV(1) on this workload."""
+    from oracle import oracle as O
+    tv = 1  # a wheel block: its RHS at ADMM iteration 0 is consForc (aux = lambda = 0)
+    G = P.grid(tv)
+    L = G.maxiLeve
+    K = [G.consStif(l) for l in range(L + 1)]
+    Pr = [G.realProl(l) for l in range(L)]
+    M = O.MgpisOracle(K, Pr)
+    del K, Pr
+    b = G.consForc
+    t0 = time.perf_counter()
+    x, it, rr = M.CG_SOLV(1, b)
+    t = time.perf_counter() - t0
+    return {
+        "value": 1.0 / (nsub * t),
+        "unit": "ADMM it/s",
+        "cores": O.threads(),
+        "kind": "port",
+        "sample": f"one SGS-V-cycle CG_SOLV(1) of subdomain {tv} ({len(b)} DOF, {it} iterations, {t:.2f} s) "
+                  f"at ADMM iteration 0; one ADMM iteration = {nsub} such solves (interface step ignored)",
+        "dof_iter_per_s": len(b) * it / t,
+    }
+
+
+if __name__ == "__main__":
+    main()

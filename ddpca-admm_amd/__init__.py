@@ -59,6 +59,7 @@ def _declare(L: C.CDLL) -> None:
     L.ddpca_problem_set_ips.argtypes = [_P, C.c_int64, C.c_int64, _P, _P, _P, _P, _P, C.c_double, C.c_double,
                                         C.c_double]
     L.ddpca_problem_establish.argtypes = [_P]
+    L.ddpca_problem_establish_owned.argtypes = [_P, _P, C.c_int]
     L.ddpca_problem_view.argtypes = [_P, C.c_char_p, C.c_int64, C.c_int64, C.POINTER(_P), _I64P,
                                      C.POINTER(C.c_int)]
     L.ddpca_problem_destroy.argtypes = [_P]
@@ -173,8 +174,13 @@ class Problem:
         _check(lib().ddpca_problem_set_ips(self._h, ts, len(gap), _ptr(node), _ptr(shap), _ptr(basis), _ptr(gap),
                                            _ptr(w), fric, penN, penF))
 
-    def ESTABLISH(self) -> "Problem":
-        _check(lib().ddpca_problem_establish(self._h))
+    def ESTABLISH(self, owner: Optional[Sequence[int]] = None, rank: int = 0) -> "Problem":
+        """MCONTACT::ESTABLISH; with owner/rank only this rank's subdomains are built."""
+        if owner is None:
+            _check(lib().ddpca_problem_establish(self._h))
+        else:
+            own = np.ascontiguousarray(owner, dtype=np.int32)
+            _check(lib().ddpca_problem_establish_owned(self._h, _ptr(own), rank))
         return self
 
     def grid(self, tv: int = 0) -> "MULTIGRID":
@@ -349,9 +355,10 @@ class MCONTACT:
         return out
 
     def timing(self) -> dict:
-        out = (C.c_double * 7)()
+        out = (C.c_double * 10)()
         _check(lib().mcontact_gpu_timing(self._h, out))
-        keys = ["total_ms", "solve_ms", "iface_ms", "comm_ms", "spmv_kernel_ms", "spmv_launches", "pcg_iterations"]
+        keys = ["total_ms", "solve_ms", "iface_ms", "comm_ms", "spmv_kernel_ms", "spmv_samples", "pcg_iterations",
+                "spmv_bytes_per_launch", "dof_iterations", "owned_dofs"]
         return dict(zip(keys, list(out)))
 
 

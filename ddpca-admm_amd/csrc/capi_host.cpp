@@ -175,7 +175,8 @@ void make_dehw(Problem& P, const double* q) {
     const int64_t gl = (int64_t)q[4];
     const double fric = q[5];
     if (G < 1) throw std::invalid_argument("dehw: ngroups >= 1");
-    const double Lx = 0.02, Ly = 0.02, H = 0.01, p = 1.0e7;
+    const double h = 0.01;  // cubic coarse elements
+    const double Lx = n[0] * h, Ly = n[1] * h, H = n[2] * h, p = 1.0e7;
     P.mc.multGrid.resize(2 * G);
 #pragma omp parallel for schedule(dynamic, 1)
     for (int64_t s = 0; s < 2 * G; ++s) {
@@ -293,6 +294,19 @@ int ddpca_problem_establish(ddpca_problem_t h) {
         Problem& P = *reinterpret_cast<Problem*>(h);
         if (P.established) return;
         P.mc.ESTABLISH();
+        P.owned.assign(P.mc.multGrid.size(), 1);
+        P.established = true;
+    });
+}
+
+int ddpca_problem_establish_owned(ddpca_problem_t h, const int32_t* owner, int rank) {
+    return guarded([&] {
+        Problem& P = *reinterpret_cast<Problem*>(h);
+        if (P.established) throw ApiError(DDPCA_ESTATE, "problem already established");
+        if (!owner) throw ApiError(DDPCA_EINVAL, "null owner");
+        P.owned.assign(P.mc.multGrid.size(), 0);
+        for (size_t tv = 0; tv < P.owned.size(); ++tv) P.owned[tv] = owner[tv] == rank ? 1 : 0;
+        P.mc.ESTABLISH(&P.owned);
         P.established = true;
     });
 }

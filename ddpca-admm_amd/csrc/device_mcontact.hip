@@ -339,7 +339,7 @@ struct ddpca_mcontact {
     int64_t mult_maxi = 1000;  // PREP.h:75 (global in the reference)
     std::vector<std::vector<double>> moniReco;
     std::vector<std::vector<double>> rows;
-    double timing[7] = {0, 0, 0, 0, 0, 0, 0};
+    double timing[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     std::vector<int64_t> last_pcg;
     mgpis_options_t opt{};
 };
@@ -423,6 +423,8 @@ void build(ddpca_mcontact& H, Problem& P) {
     // ---- owned subdomains
     for (int64_t tv = 0; tv < H.nsub; ++tv) {
         if (H.owner[tv] != H.rank) continue;
+        if (P.owned.size() != (size_t)H.nsub || !P.owned[tv])
+            throw ApiError(DDPCA_ESTATE, "subdomain " + std::to_string(tv) + " is owned by this rank but was not established");
         const MULTIGRID& g = mc.multGrid[tv];
         ddpca_mcontact::Sub S;
         S.tv = tv;
@@ -693,7 +695,9 @@ bool iterate_once(ddpca_mcontact& H, bool check) {
     (void)tc0;
     for (auto& S : H.subs) {
         H.timing[6] += (double)S.last_iters;
+        H.timing[8] += (double)S.last_iters * (double)S.mg->nfree;
         if (S.mg->timed_kernel_samples) {
+            H.timing[7] += S.mg->fine_kernel_bytes() * (double)S.mg->timed_kernel_samples;
             H.timing[4] += S.mg->timed_kernel_ms;
             H.timing[5] += (double)S.mg->timed_kernel_samples;
             S.mg->timed_kernel_ms = 0.0;
@@ -824,8 +828,12 @@ int64_t mcontact_gpu_get(mcontact_t h, const char* what, int64_t index, void* ou
     return rc < 0 ? rc : n;
 }
 
-int mcontact_gpu_timing(mcontact_t h, double* out7) {
-    std::memcpy(out7, h->timing, sizeof(h->timing));
+int mcontact_gpu_timing(mcontact_t h, double* out10) {
+    std::memcpy(out10, h->timing, sizeof(h->timing));
+    if (h->timing[5] > 0) out10[7] = h->timing[7] / h->timing[5];  // bytes per timed launch
+    double dofs = 0.0;
+    for (auto& S : h->subs) dofs += (double)S.mg->nfree;
+    out10[9] = dofs;
     return DDPCA_OK;
 }
 

@@ -2,47 +2,24 @@
 #include "mcontact.hpp"
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <map>
+#include <numeric>
 #include <stdexcept>
 #include <unordered_map>
 
 namespace ddpca {
 
-namespace {
-
-struct Trip {
-    int64_t r, c;
-    double v;
-};
-
-// Triplets -> CSR, duplicates summed (Eigen setFromTriplets semantics).
-Csr from_triplets(int64_t nrow, int64_t ncol, std::vector<Trip>& t) {
-    std::stable_sort(t.begin(), t.end(), [](const Trip& a, const Trip& b) { return a.r != b.r ? a.r < b.r : a.c < b.c; });
-    Csr m;
-    m.nrow = nrow;
-    m.ncol = ncol;
-    m.ptr.assign(nrow + 1, 0);
-    for (size_t i = 0; i < t.size();) {
-        size_t j = i;
-        double s = 0.0;
-        while (j < t.size() && t[j].r == t[i].r && t[j].c == t[i].c) s += t[j++].v;
-        m.col.push_back((int32_t)t[i].c);
-        m.val.push_back(s);
-        m.ptr[t[i].r + 1]++;
-        i = j;
-    }
-    for (int64_t r = 0; r < nrow; ++r) m.ptr[r + 1] += m.ptr[r];
-    return m;
-}
-
-}  // namespace
 
 void Interface::BUILD(const MULTIGRID& g0, const MULTIGRID& g1) {
     const int C = comp();
     const int64_t nip = (int64_t)ip.size();
     const MULTIGRID* g[2] = {&g0, &g1};
     const double pen[3] = {penN, penF, penF};
+#pragma omp parallel for schedule(static, 1) num_threads(2)
     for (int s = 0; s < 2; ++s) {
         std::unordered_map<int64_t, int64_t> nc;
         nodeCont[s].clear();
@@ -50,77 +27,198 @@ void Interface::BUILD(const MULTIGRID& g0, const MULTIGRID& g1) {
             for (int k = 0; k < 4; ++k)
                 if (nc.emplace(p.node[s][k], (int64_t)nc.size()).second) nodeCont[s].push_back(p.node[s][k]);
         const int64_t nn = g[s]->numNodes();
-        const int64_t mc = C * (int64_t)nodeCont[s].size();
-        std::vector<Trip> tM, tT, tTp, tI, tIp, tL, tD, tII;
+        const int64_t ncn = (int64_t)nodeCont[s].size();
+        const int64_t mc = C * ncn;
+        // ---- contact-node pairs coupled by an integration point (node-block sparsity)
+        std::vector<int32_t> ipc(4 * nip);
+        std::vector<std::vector<int32_t>> part(ncn);
+        for (int64_t q = 0; q < nip; ++q)
+            for (int a = 0; a < 4; ++a) ipc[4 * q + a] = (int32_t)nc.at(ip[q].node[s][a]);
+        for (int64_t q = 0; q < nip; ++q)
+            for (int a = 0; a < 4; ++a)
+                for (int b = 0; b < 4; ++b) part[ipc[4 * q + a]].push_back(ipc[4 * q + b]);
+        std::vector<int64_t> pptr(ncn + 1, 0);
+        for (int64_t a = 0; a < ncn; ++a) {
+            std::sort(part[a].begin(), part[a].end());
+            part[a].erase(std::unique(part[a].begin(), part[a].end()), part[a].end());
+            pptr[a + 1] = pptr[a] + (int64_t)part[a].size();
+        }
+        // per pair: sum_q w M_a M_b (T^T P T), sum_q w M_a M_b (T^T T) [C = 3] or
+        // sum_q w M_a M_b n (3) and sum_q w M_a M_b [C = 1]   (MCONTACT.h:241-568)
+        std::vector<double> aGP(9 * pptr[ncn], 0.0), aG(9 * pptr[ncn], 0.0), aN(3 * pptr[ncn], 0.0),
+            aM(pptr[ncn], 0.0);
         for (int64_t q = 0; q < nip; ++q) {
             const IntegralPoint& p = ip[q];
             const double* M = p.shap[s];
-            // T: rows n, t1, t2 (C == 3); n only (C == 1)
-            double T[3][3];
-            for (int a = 0; a < 3; ++a)
-                for (int b = 0; b < 3; ++b) T[a][b] = p.basis[a][b];
-            // G = T^T T, GP = T^T P T, GPi = T^T P^-1 T (3x3 nodal-space couplings)
-            double G[3][3], GP[3][3];
+            double GP[3][3], G[3][3];
             for (int i = 0; i < 3; ++i)
                 for (int j = 0; j < 3; ++j) {
-                    double a = 0, b = 0;
+                    double x = 0, y = 0;
                     for (int m = 0; m < C; ++m) {
-                        a += T[m][i] * T[m][j];
-                        b += T[m][i] * pen[m] * T[m][j];
+                        x += p.basis[m][i] * p.basis[m][j];
+                        y += p.basis[m][i] * pen[m] * p.basis[m][j];
                     }
-                    G[i][j] = a;
-                    GP[i][j] = b;
+                    G[i][j] = x;
+                    GP[i][j] = y;
                 }
             for (int a = 0; a < 4; ++a) {
-                const int64_t na = p.node[s][a], ca = nc.at(na);
+                const int32_t ca = ipc[4 * q + a];
                 for (int b = 0; b < 4; ++b) {
-                    const int64_t nb = p.node[s][b], cb = nc.at(nb);
+                    const int32_t cb = ipc[4 * q + b];
+                    const int64_t k = pptr[ca] + (std::lower_bound(part[ca].begin(), part[ca].end(), cb) - part[ca].begin());
                     const double mm = p.w * M[a] * M[b];
-                    for (int i = 0; i < 3; ++i)
-                        for (int j = 0; j < 3; ++j) tM.push_back({3 * na + i, 3 * nb + j, mm * GP[i][j]});
-                    if (C == 1) {
-                        for (int i = 0; i < 3; ++i) {
-                            tT.push_back({3 * na + i, cb, p.w * M[a] * T[0][i] * M[b]});
-                            tTp.push_back({3 * na + i, cb, penN * (p.w * M[a] * T[0][i] * M[b])});
-                        }
-                        tI.push_back({ca, cb, mm});
-                        tIp.push_back({ca, cb, mm * penN});
-                    } else {
-                        for (int i = 0; i < 3; ++i)
-                            for (int j = 0; j < 3; ++j) {
-                                tT.push_back({3 * na + i, 3 * cb + j, mm * G[i][j]});
-                                tTp.push_back({3 * na + i, 3 * cb + j, mm * GP[i][j]});
-                                tI.push_back({3 * ca + i, 3 * cb + j, mm * G[i][j]});
-                                tIp.push_back({3 * ca + i, 3 * cb + j, mm * GP[i][j]});
-                            }
+                    for (int t = 0; t < 9; ++t) {
+                        aGP[9 * k + t] += mm * GP[t / 3][t % 3];
+                        aG[9 * k + t] += mm * G[t / 3][t % 3];
                     }
-                }
-                // inpoLagr, inpoDisp (rows: ip components), inteInpo (rows: contact dofs)
-                const double sgn = (s == 0) ? -1.0 : 1.0;
-                for (int m = 0; m < C; ++m)
-                    for (int k = 0; k < 3; ++k) {
-                        if (C == 1) {
-                            tD.push_back({q, 3 * na + k, T[0][k] * M[a]});
-                        } else {
-                            tL.push_back({3 * q + m, 3 * ca + k, T[m][k] * M[a]});
-                            tD.push_back({3 * q + m, 3 * na + k, T[m][k] * M[a]});
-                            tII.push_back({3 * ca + k, 3 * q + m, sgn * (p.w * M[a] * T[m][k])});
-                        }
-                    }
-                if (C == 1) {
-                    tL.push_back({q, ca, M[a]});
-                    tII.push_back({ca, q, sgn * (p.w * M[a])});
+                    for (int i = 0; i < 3; ++i) aN[3 * k + i] += mm * p.basis[0][i];
+                    aM[k] += mm;
                 }
             }
         }
-        systMass[s] = from_triplets(3 * nn, 3 * nn, tM);
-        systTran[s] = from_triplets(3 * nn, mc, tT);
-        systTran_pena[s] = from_triplets(3 * nn, mc, tTp);
-        inteMass[s] = from_triplets(mc, mc, tI);
-        inteMass_pena[s] = from_triplets(mc, mc, tIp);
-        inpoLagr[s] = from_triplets(C * nip, mc, tL);
-        inpoDisp[s] = from_triplets(C * nip, 3 * nn, tD);
-        inteInpo[s] = from_triplets(mc, C * nip, tII);
+        // partners ordered by body node id (rows/cols of nodal-space operators)
+        std::vector<std::vector<int32_t>> bypos(ncn);
+        for (int64_t a = 0; a < ncn; ++a) {
+            bypos[a].resize(part[a].size());
+            std::iota(bypos[a].begin(), bypos[a].end(), 0);
+            std::sort(bypos[a].begin(), bypos[a].end(),
+                      [&](int32_t x, int32_t y) { return nodeCont[s][part[a][x]] < nodeCont[s][part[a][y]]; });
+        }
+        std::vector<int64_t> rowc(nn, -1);  // body node -> contact index
+        for (int64_t a = 0; a < ncn; ++a) rowc[nodeCont[s][a]] = a;
+        // nodal-space rows (3 nn): systMass (cols 3 nn), systTran(_pena) (cols mc)
+        auto emit_nodal = [&](bool mass, bool pena) {
+            Csr m;
+            m.nrow = 3 * nn;
+            m.ncol = mass ? 3 * nn : mc;
+            m.ptr.assign(3 * nn + 1, 0);
+            for (int64_t n = 0; n < nn; ++n) {
+                const int64_t a = rowc[n];
+                const int64_t per = a < 0 ? 0 : (int64_t)part[a].size() * ((mass || C == 3) ? 3 : 1);
+                for (int i = 0; i < 3; ++i) m.ptr[3 * n + i + 1] = per;
+            }
+            for (int64_t r = 0; r < 3 * nn; ++r) m.ptr[r + 1] += m.ptr[r];
+            m.col.resize(m.ptr[3 * nn]);
+            m.val.resize(m.ptr[3 * nn]);
+            for (int64_t a = 0; a < ncn; ++a) {
+                const int64_t n = nodeCont[s][a];
+                for (int i = 0; i < 3; ++i) {
+                    int64_t w = m.ptr[3 * n + i];
+                    for (size_t t = 0; t < part[a].size(); ++t) {
+                        const int64_t kk = mass ? bypos[a][t] : (int64_t)t;
+                        const int64_t k = pptr[a] + kk;
+                        const int64_t cb = part[a][kk];
+                        if (mass) {
+                            const int64_t nb = nodeCont[s][cb];
+                            for (int j = 0; j < 3; ++j) { m.col[w] = (int32_t)(3 * nb + j); m.val[w++] = aGP[9 * k + 3 * i + j]; }
+                        } else if (C == 3) {
+                            for (int j = 0; j < 3; ++j) {
+                                m.col[w] = (int32_t)(3 * cb + j);
+                                m.val[w++] = pena ? aGP[9 * k + 3 * i + j] : aG[9 * k + 3 * i + j];
+                            }
+                        } else {
+                            m.col[w] = (int32_t)cb;
+                            m.val[w++] = pena ? penN * aN[3 * k + i] : aN[3 * k + i];
+                        }
+                    }
+                }
+            }
+            return m;
+        };
+        // contact-space rows (mc): inteMass(_pena)
+        auto emit_contact = [&](bool pena) {
+            Csr m;
+            m.nrow = m.ncol = mc;
+            m.ptr.assign(mc + 1, 0);
+            for (int64_t a = 0; a < ncn; ++a)
+                for (int i = 0; i < C; ++i) m.ptr[C * a + i + 1] = (int64_t)part[a].size() * C;
+            for (int64_t r = 0; r < mc; ++r) m.ptr[r + 1] += m.ptr[r];
+            m.col.resize(m.ptr[mc]);
+            m.val.resize(m.ptr[mc]);
+            for (int64_t a = 0; a < ncn; ++a)
+                for (int i = 0; i < C; ++i) {
+                    int64_t w = m.ptr[C * a + i];
+                    for (size_t t = 0; t < part[a].size(); ++t) {
+                        const int64_t k = pptr[a] + (int64_t)t, cb = part[a][t];
+                        for (int j = 0; j < C; ++j) {
+                            m.col[w] = (int32_t)(C * cb + j);
+                            m.val[w++] = C == 3 ? (pena ? aGP[9 * k + 3 * i + j] : aG[9 * k + 3 * i + j])
+                                                : (pena ? aM[k] * penN : aM[k]);
+                        }
+                    }
+                }
+            return m;
+        };
+        systMass[s] = emit_nodal(true, false);
+        systTran[s] = emit_nodal(false, false);
+        systTran_pena[s] = emit_nodal(false, true);
+        inteMass[s] = emit_contact(false);
+        inteMass_pena[s] = emit_contact(true);
+        // per-ip operators: inpoLagr (C nip x mc), inpoDisp (C nip x 3 nn), inteInpo (mc x C nip)
+        const double sgn = (s == 0) ? -1.0 : 1.0;
+        Csr& L = inpoLagr[s];
+        Csr& Dd = inpoDisp[s];
+        L.nrow = Dd.nrow = C * nip;
+        L.ncol = mc;
+        Dd.ncol = 3 * nn;
+        L.ptr.assign(C * nip + 1, 0);
+        Dd.ptr.assign(C * nip + 1, 0);
+        for (int64_t r = 0; r < C * nip; ++r) {
+            L.ptr[r + 1] = L.ptr[r] + 4 * C;
+            Dd.ptr[r + 1] = Dd.ptr[r] + 12;
+        }
+        L.col.resize(L.ptr.back());
+        L.val.resize(L.ptr.back());
+        Dd.col.resize(Dd.ptr.back());
+        Dd.val.resize(Dd.ptr.back());
+        Csr& Ii = inteInpo[s];
+        Ii.nrow = mc;
+        Ii.ncol = C * nip;
+        Ii.ptr.assign(mc + 1, 0);
+        for (int64_t q = 0; q < nip; ++q)
+            for (int a = 0; a < 4; ++a)
+                for (int k = 0; k < C; ++k) Ii.ptr[C * ipc[4 * q + a] + k + 1] += C;
+        for (int64_t r = 0; r < mc; ++r) Ii.ptr[r + 1] += Ii.ptr[r];
+        Ii.col.resize(Ii.ptr[mc]);
+        Ii.val.resize(Ii.ptr[mc]);
+        std::vector<int64_t> ifill(Ii.ptr.begin(), Ii.ptr.end() - 1);
+        for (int64_t q = 0; q < nip; ++q) {
+            const IntegralPoint& p = ip[q];
+            const double* M = p.shap[s];
+            int ord_c[4] = {0, 1, 2, 3}, ord_n[4] = {0, 1, 2, 3};
+            std::sort(ord_c, ord_c + 4, [&](int x, int y) { return ipc[4 * q + x] < ipc[4 * q + y]; });
+            std::sort(ord_n, ord_n + 4, [&](int x, int y) { return p.node[s][x] < p.node[s][y]; });
+            for (int m = 0; m < C; ++m) {
+                const int64_t r = C * q + m;
+                int64_t wl = L.ptr[r], wd = Dd.ptr[r];
+                for (int t = 0; t < 4; ++t) {
+                    const int a = ord_c[t];
+                    if (C == 1) {
+                        L.col[wl] = ipc[4 * q + a];
+                        L.val[wl++] = M[a];
+                    } else {
+                        for (int k = 0; k < 3; ++k) {
+                            L.col[wl] = 3 * ipc[4 * q + a] + k;
+                            L.val[wl++] = p.basis[m][k] * M[a];
+                        }
+                    }
+                    const int an = ord_n[t];
+                    for (int k = 0; k < 3; ++k) {
+                        Dd.col[wd] = (int32_t)(3 * p.node[s][an] + k);
+                        Dd.val[wd++] = p.basis[C == 1 ? 0 : m][k] * M[an];
+                    }
+                }
+            }
+            for (int a = 0; a < 4; ++a)
+                for (int k = 0; k < C; ++k) {
+                    const int64_t row = C * ipc[4 * q + a] + k;
+                    for (int m = 0; m < C; ++m) {
+                        const int64_t w = ifill[row]++;
+                        Ii.col[w] = (int32_t)(C * q + m);
+                        Ii.val[w] = sgn * (p.w * M[a] * (C == 1 ? 1.0 : p.basis[m][k]));
+                    }
+                }
+        }
     }
     inpoNgap.assign(C * nip, 0.0);
     pemaDiag.assign(C * nip, 0.0);
@@ -135,17 +233,35 @@ void Interface::BUILD(const MULTIGRID& g0, const MULTIGRID& g1) {
     }
 }
 
-void MCONTACT::ESTABLISH() {
-    for (auto& itf : searCont) itf.BUILD(multGrid[itf.body[0]], multGrid[itf.body[1]]);
+void MCONTACT::ESTABLISH(const std::vector<uint8_t>* owned) {
+    auto mine = [&](int64_t tv) { return !owned || (*owned)[tv] != 0; };
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int64_t ts = 0; ts < (int64_t)searCont.size(); ++ts) {
+        Interface& itf = searCont[ts];
+        if (mine(itf.body[0]) || mine(itf.body[1])) itf.BUILD(multGrid[itf.body[0]], multGrid[itf.body[1]]);
+    }
 #pragma omp parallel for schedule(dynamic, 1)
     for (int64_t tv = 0; tv < (int64_t)multGrid.size(); ++tv) {
+        if (!mine(tv)) continue;
         MULTIGRID& g = multGrid[tv];
+        const bool verbose = std::getenv("DDPCA_VERBOSE") != nullptr;
+        auto now = [] { return std::chrono::steady_clock::now(); };
+        auto t0 = now();
         g.TRANSFER();
+        auto t1 = now();
         g.STIF_MATR();
+        auto t2 = now();
         for (const auto& itf : searCont)
             for (int s = 0; s < 2; ++s)
                 if (itf.body[s] == tv) g.ADD_NODAL(itf.systMass[s]);
+        auto t3 = now();
         g.CONSTRAINT();
+        auto t4 = now();
+        if (verbose) {
+            auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+            std::fprintf(stderr, "[ddpca] establish sd %ld: transfer %.0f ms, stif %.0f ms, systMass %.0f ms, constraint %.0f ms\n",
+                         (long)tv, ms(t0, t1), ms(t1, t2), ms(t2, t3), ms(t3, t4));
+        }
     }
 }
 

@@ -44,8 +44,10 @@ public:
     std::vector<Interface> searCont;
     int64_t muscSett = 0;
     // ESTABLISH: interface operators, systMass added to each body's stiffness, then
-    // TRANSFER / STIF_MATR / CONSTRAINT(1) per body (MCONTACT.h:812-825).
-    void ESTABLISH();
+    // TRANSFER / STIF_MATR / CONSTRAINT(1) per body (MCONTACT.h:812-825).  owned (optional):
+    // per-subdomain mask; only owned bodies and interfaces touching them are built (one rank's
+    // share of a multi-GPU run).
+    void ESTABLISH(const std::vector<uint8_t>* owned = nullptr);
     double GET_CHAR_LENG() const;  // MCONTACT.h:2478-2491
 };
 

@@ -233,25 +233,6 @@ void MULTIGRID::STIF_MATR() {
     std::vector<int64_t> leaves;
     for (int64_t e = 0; e < (int64_t)elemVect.size(); ++e)
         if (elemVect[e].firstChild < 0) leaves.push_back(e);
-    // node adjacency (nodes sharing a leaf element)
-    std::vector<std::vector<int32_t>> adj(N);
-    for (int64_t e : leaves)
-        for (int a = 0; a < 8; ++a)
-            for (int b = 0; b < 8; ++b) adj[elemVect[e].cornNode[a]].push_back((int32_t)elemVect[e].cornNode[b]);
-#pragma omp parallel for schedule(dynamic, 1024)
-    for (int64_t i = 0; i < N; ++i) {
-        std::sort(adj[i].begin(), adj[i].end());
-        adj[i].erase(std::unique(adj[i].begin(), adj[i].end()), adj[i].end());
-    }
-    origStif = Bsr3();
-    origStif.nb = origStif.mb = N;
-    origStif.ptr.assign(N + 1, 0);
-    for (int64_t i = 0; i < N; ++i) origStif.ptr[i + 1] = origStif.ptr[i] + (int64_t)adj[i].size();
-    origStif.col.resize(origStif.ptr[N]);
-    for (int64_t i = 0; i < N; ++i) std::copy(adj[i].begin(), adj[i].end(), origStif.col.begin() + origStif.ptr[i]);
-    adj.clear();
-    adj.shrink_to_fit();
-    origStif.val.assign(9 * origStif.ptr[N], 0.0);
     // colour leaf elements so that one colour shares no node (uniform octree: lattice parity)
     int64_t h = -1;
     bool uniform = true;
@@ -271,6 +252,37 @@ void MULTIGRID::STIF_MATR() {
             for (int a = 0; a < 3; ++a) lo[a] = std::min(lo[a], nodeLatt[elemVect[e].cornNode[k]][a]);
         colour[((lo[0] / h) & 1) | (((lo[1] / h) & 1) << 1) | (((lo[2] / h) & 1) << 2)].push_back(e);
     }
+    // node adjacency (nodes sharing a leaf element): flat buffer of 64 candidates per node,
+    // filled colour by colour (no two elements of a colour share a node), then sort + unique
+    {
+        std::vector<int32_t> cnt(N, 0), flat(N * 64);
+        for (const auto& list : colour) {
+#pragma omp parallel for schedule(static) if (uniform)
+            for (int64_t t = 0; t < (int64_t)list.size(); ++t) {
+                const TreeElem& el = elemVect[list[t]];
+                for (int a = 0; a < 8; ++a) {
+                    const int64_t r = el.cornNode[a];
+                    if (cnt[r] + 8 > 64) throw std::runtime_error("STIF_MATR: node in more than 8 elements");
+                    for (int b = 0; b < 8; ++b) flat[r * 64 + cnt[r] + b] = (int32_t)el.cornNode[b];
+                    cnt[r] += 8;
+                }
+            }
+        }
+#pragma omp parallel for schedule(static)
+        for (int64_t i = 0; i < N; ++i) {
+            int32_t* b = &flat[i * 64];
+            std::sort(b, b + cnt[i]);
+            cnt[i] = (int32_t)(std::unique(b, b + cnt[i]) - b);
+        }
+        origStif = Bsr3();
+        origStif.nb = origStif.mb = N;
+        origStif.ptr.assign(N + 1, 0);
+        for (int64_t i = 0; i < N; ++i) origStif.ptr[i + 1] = origStif.ptr[i] + cnt[i];
+        origStif.col.resize(origStif.ptr[N]);
+#pragma omp parallel for schedule(static)
+        for (int64_t i = 0; i < N; ++i) std::copy(&flat[i * 64], &flat[i * 64] + cnt[i], origStif.col.begin() + origStif.ptr[i]);
+        origStif.val.assign(9 * origStif.ptr[N], 0.0);
+    }
     for (const auto& list : colour) {
 #pragma omp parallel if (uniform)
         {
@@ -281,14 +293,18 @@ void MULTIGRID::STIF_MATR() {
             for (int64_t t = 0; t < (int64_t)list.size(); ++t) {
                 const TreeElem& el = elemVect[list[t]];
                 double X[8][3], R[8][3];
+                double ext = 0.0;
                 for (int k = 0; k < 8; ++k)
                     for (int a = 0; a < 3; ++a) {
                         X[k][a] = nodeCoor[el.cornNode[k]][a];
                         R[k][a] = X[k][a] - X[0][a];
+                        ext = std::max(ext, std::abs(R[k][a]));
                     }
+                // congruent element (same corner offsets up to last-bit noise of the refined
+                // coordinates): reuse the previous element stiffness
                 bool same = have;
                 for (int k = 0; k < 8 && same; ++k)
-                    for (int a = 0; a < 3; ++a) same &= (R[k][a] == Xlast[k][a]);
+                    for (int a = 0; a < 3; ++a) same &= std::abs(R[k][a] - Xlast[k][a]) <= 1e-13 * ext;
                 if (!same) {
                     element_stiffness(X, D, KE);
                     for (int k = 0; k < 8; ++k)

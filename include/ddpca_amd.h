@@ -113,6 +113,9 @@ int ddpca_problem_set_ips(ddpca_problem_t p, int64_t ts, int64_t n, const int64_
 /* MCONTACT::ESTABLISH (MCONTACT.h:181-896) minus the coarse space; single grids just run
  * TRANSFER / STIF_MATR / CONSTRAINT(1). */
 int ddpca_problem_establish(ddpca_problem_t p);
+/* Rank-local ESTABLISH: operators only for subdomains with owner[tv] == rank and for the
+ * interfaces touching them (each process of a multi-GPU run builds its own share). */
+int ddpca_problem_establish_owned(ddpca_problem_t p, const int32_t* owner, int rank);
 /* Read-only view of an internal array.  dtype: 0 float64, 1 int64, 2 int32, 3 uint8.
  * Names: see ddpca_amd.py (_ARRAYS). index = subdomain, level or 2*interface+side. */
 int ddpca_problem_view(ddpca_problem_t p, const char* name, int64_t index, int64_t level,
@@ -150,9 +153,12 @@ int64_t mcontact_gpu_monitor(mcontact_t h, double* out, int64_t cap_rows);
  * (index = 2*ts+side), "inpoGamm" (index = ts, projected gamma of the last iteration),
  * "pcg_iters" (int64 per owned subdomain, last iteration). */
 int64_t mcontact_gpu_get(mcontact_t h, const char* what, int64_t index, void* out, int64_t cap);
-/* Device timing of the last iterate() call: [total_ms, solve_ms, iface_ms, comm_ms,
- * spmv_kernel_ms, spmv_launches, pcg_iterations] */
-int mcontact_gpu_timing(mcontact_t h, double* out7);
+/* Timing of the last iterate() call, summed over its iterations: [total_ms (host wall),
+ * solve_ms (host wall of the body balance), iface_ms (device, interface step + monitor),
+ * comm_ms (device, gamma exchange), spmv_kernel_ms (device events around sampled fine-level
+ * SpMV launches), spmv_samples, pcg_iterations (summed over owned subdomain solves),
+ * spmv_bytes_per_launch (algorithmic), dof_iterations (sum n_free * PCG its), owned_dofs] */
+int mcontact_gpu_timing(mcontact_t h, double* out10);
 int mcontact_gpu_destroy(mcontact_t h);
 
 #ifdef __cplusplus

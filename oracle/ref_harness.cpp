@@ -89,10 +89,12 @@ void save_csr(const std::string& name, Eigen::SparseMatrix<double, Eigen::RowMaj
     save_ivec(name + "_shape", {(int64_t)m.rows(), (int64_t)m.cols()});
 }
 
-// Deterministic probe vector used by every fingerprint (no RNG dependence).
+// Deterministic probe vector used by every fingerprint: integer arithmetic and one correctly
+// rounded division, so every compiler/libm (and numpy) produces the same bits -- a libm sin()
+// with FMA-contracted arguments (-march=native) does not.
 Eigen::VectorXd probe(long n) {
     Eigen::VectorXd v(n);
-    for (long i = 0; i < n; ++i) v(i) = std::sin(0.37 * (double)i + 0.11);
+    for (long i = 0; i < n; ++i) v(i) = (double)((i * 7919 + 13) % 2003) / 2003.0 - 0.5;
     return v;
 }
 
