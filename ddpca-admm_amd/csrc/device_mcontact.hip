@@ -595,7 +595,7 @@ bool iterate_once(ddpca_mcontact& H, bool check) {
         // pre-enqueue the predicted number of graph replays
         const int64_t k = std::max(1, D.opt.iters_per_graph);
         const int64_t pre = S.pred_iters > 0 ? std::max<int64_t>(1, S.pred_iters / k) : 1;
-        for (int64_t r = 0; r < pre; ++r) D.pcg_step(1, r == 0);
+        for (int64_t r = 0; r < pre; ++r) D.pcg_step(1);
     }
     std::vector<bool> done(H.subs.size(), false);
     size_t left = H.subs.size();
@@ -610,7 +610,7 @@ bool iterate_once(ddpca_mcontact& H, bool check) {
                 H.subs[i].last_iters = D.sc_host->iter;
                 H.subs[i].pred_iters = D.sc_host->iter;
             } else {
-                D.pcg_step(1, false);
+                D.pcg_step(1);
             }
         }
     }

@@ -630,8 +630,6 @@ MgpisDevice::~MgpisDevice() {
     if (stream) (void)hipStreamSynchronize(stream);
     for (auto& g : graph_)
         if (g) (void)hipGraphExecDestroy(g);
-    for (auto& g : graph_timed_)
-        if (g) (void)hipGraphExecDestroy(g);
     if (sc_host) (void)hipHostFree(sc_host);
     if (ev_k0) (void)hipEventDestroy(ev_k0);
     if (ev_k1) (void)hipEventDestroy(ev_k1);
@@ -816,20 +814,15 @@ void MgpisDevice::enqueue_iteration(int prec, bool timed) {
     hipLaunchKernelGGL(k_fin, dim3(1), dim3(kBlock), 0, stream, (int)kFinBeta, partial.p, nblk_fine, sc.p);
 }
 
-// graph_[prec]: iters_per_graph PCG iterations; graph_timed_[prec]: the same with two event
-// records bracketing the first fine-level SpMV (launched once per solve when timing is on, so
-// no later replay overwrites its events before pcg_poll() reads them).
+// graph_[prec]: iters_per_graph PCG iterations captured once and replayed.
 void MgpisDevice::build_graph(int prec) {
-    for (int timed = 0; timed < 2; ++timed) {
-        hipGraphExec_t& ge = timed ? graph_timed_[prec] : graph_[prec];
-        if (ge || (timed && !time_kernel)) continue;
-        hipGraph_t g;
-        DDPCA_HIP(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
-        for (int k = 0; k < opt.iters_per_graph; ++k) enqueue_iteration(prec, timed && k == 0);
-        DDPCA_HIP(hipStreamEndCapture(stream, &g));
-        DDPCA_HIP(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
-        DDPCA_HIP(hipGraphDestroy(g));
-    }
+    if (graph_[prec]) return;
+    hipGraph_t g;
+    DDPCA_HIP(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
+    for (int k = 0; k < opt.iters_per_graph; ++k) enqueue_iteration(prec, false);
+    DDPCA_HIP(hipStreamEndCapture(stream, &g));
+    DDPCA_HIP(hipGraphInstantiate(&graph_[prec], g, nullptr, nullptr, 0));
+    DDPCA_HIP(hipGraphDestroy(g));
 }
 
 void MgpisDevice::pcg_begin(int prec, double rtol, int64_t maxit) {
@@ -846,21 +839,22 @@ void MgpisDevice::pcg_begin(int prec, double rtol, int64_t maxit) {
     if (prec == 1) vcycle(rs.p, zs.p, true);
     else hipLaunchKernelGGL(k_diag, dim3(nblk_fine), dim3(kBlock), 0, stream, rs.p, L.dinv.p, zs.p, partial.p, L.nn, done);
     hipLaunchKernelGGL(k_fin, dim3(1), dim3(kBlock), 0, stream, (int)kFinBeta0, partial.p, nblk_fine, sc.p);
+    if (time_kernel) {
+        // first iteration eagerly, with HIP events around its fine-level SpMV on this stream
+        enqueue_iteration(prec, true);
+        sample_pending_ = true;
+    }
 }
 
-void MgpisDevice::pcg_step(int prec, bool sample) {
-    const bool timed = sample && time_kernel && graph_timed_[prec] && !sample_pending_;
-    DDPCA_HIP(hipGraphLaunch(timed ? graph_timed_[prec] : graph_[prec], stream));
-    sample_pending_ |= timed;
-}
+void MgpisDevice::pcg_step(int prec) { DDPCA_HIP(hipGraphLaunch(graph_[prec], stream)); }
 
 bool MgpisDevice::pcg_poll() {
     DDPCA_HIP(hipMemcpyAsync(sc_host, sc.p, sizeof(PcgScal), hipMemcpyDeviceToHost, stream));
     DDPCA_HIP(hipStreamSynchronize(stream));
     if (sample_pending_) {
-        // events of the timed replay bracket one fine-level SpMV that ran with done == 0
+        // keep the sample only if the timed SpMV ran a real iteration (done was 0)
         float ms = 0.f;
-        if (hipEventElapsedTime(&ms, ev_k0, ev_k1) == hipSuccess && ms > 0.f) {
+        if (sc_host->iter >= 1 && hipEventElapsedTime(&ms, ev_k0, ev_k1) == hipSuccess && ms > 0.f) {
             timed_kernel_ms += ms;
             timed_kernel_samples += 1;
         }
@@ -871,11 +865,7 @@ bool MgpisDevice::pcg_poll() {
 
 int64_t MgpisDevice::pcg_solve(int prec, double rtol, int64_t maxit, int64_t* iters, double* relres) {
     pcg_begin(prec, rtol, maxit);
-    bool first = true;
-    while (!pcg_poll()) {
-        pcg_step(prec, first);
-        first = false;
-    }
+    while (!pcg_poll()) pcg_step(prec);
     if (sc_host->fail) throw ApiError(DDPCA_ENUMERIC, "PCG breakdown (non-finite or non-positive curvature)");
     if (iters) *iters = sc_host->iter;
     if (relres) *relres = sc_host->bb > 0 ? std::sqrt(sc_host->rr / sc_host->bb) : 0.0;

@@ -88,12 +88,12 @@ public:
     // PCG on full-layout device vectors; b in bs, result in xs.  begin() enqueues the setup,
     // step() enqueues one graph replay (iters_per_graph iterations), poll() reads done.
     void pcg_begin(int prec, double rtol, int64_t maxit);
-    void pcg_step(int prec, bool sample);  // sample: read the in-graph kernel timer (syncs)
+    void pcg_step(int prec);    // one graph replay (iters_per_graph iterations)
     bool pcg_poll();           // synchronises the stream
     int64_t pcg_solve(int prec, double rtol, int64_t maxit, int64_t* iters, double* relres);
     void scatter_free(const double* cond, double* full);   // device pointers
     void gather_free(const double* full, double* cond);
-    // timing of the fine-level smoother kernel (HIP events inside the captured graph)
+    // timing of the fine-level SpMV (HIP events around it in the eager first iteration)
     hipEvent_t ev_k0 = nullptr, ev_k1 = nullptr;
     double timed_kernel_ms = 0.0;
     int64_t timed_kernel_samples = 0;
@@ -102,7 +102,6 @@ public:
 
 private:
     hipGraphExec_t graph_[2] = {nullptr, nullptr};
-    hipGraphExec_t graph_timed_[2] = {nullptr, nullptr};
     bool sample_pending_ = false;
     void build_graph(int prec);
     void enqueue_iteration(int prec, bool timed);
