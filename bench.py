@@ -11,7 +11,8 @@ are spread over the ranks (strong scaling); N = 1 runs all 8 on one MI355X.
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
 Rank 0 prints one JSON line.  `roofline` is the fine-level SELL-BSR3 SpMV kernel (the dominant
-kernel family), timed by HIP events recorded inside the replayed hipGraph on the solve stream;
+kernel family, one launch covers every owned subdomain), timed by HIP events around its launch in
+the eager first PCG iteration of every batched solve, on the solve stream;
 `cpu_baseline` is the CPU oracle (oracle/, SGS-faithful restatement of MGPIS) on one subdomain
 solve of the same workload, scaled to one ADMM iteration.
 """
@@ -45,6 +46,10 @@ def parse():
     ap.add_argument("--smoother", type=int, default=2)
     ap.add_argument("--nu", type=int, default=2)
     ap.add_argument("--iters-per-graph", type=int, default=4)
+    ap.add_argument("--warm-start", type=int, default=0,
+                    help="1: each subdomain PCG starts from its previous solution (same 1e-14 stop rule)")
+    ap.add_argument("--precond-fp32", type=int, default=0,
+                    help="1: V-cycle level operators stored in fp32 (arithmetic, Krylov operator and stop rule fp64)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=os.environ.get("DDPCA_TRAFFIC_JSON", ""),
                     help="PMC-derived HBM bytes per launch of the roofline kernel (profiles/)")
@@ -74,7 +79,7 @@ def main():
     owner = part.block_owner(nsub, world)
     P.ESTABLISH(owner, rank)
     mc = D.MCONTACT(P, device=local, rank=rank, nranks=world, owner=owner, smoother=a.smoother, nu=a.nu,
-                    iters_per_graph=a.iters_per_graph)
+                    iters_per_graph=a.iters_per_graph, warm_start=a.warm_start, precond_fp32=a.precond_fp32)
     if world > 1:
         obj = [mc.unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
@@ -142,11 +147,14 @@ def main():
                 "interfaces": P.nint,
                 "mg_levels": a.gl + 1,
                 "smoother": {0: "jacobi", 1: "block-jacobi", 2: "chebyshev"}[a.smoother] + f"({a.nu})",
+                "pcg_x0": "previous solution" if a.warm_start else "zero",
+                "vcycle_operator_storage": "fp32" if a.precond_fp32 else "fp64",
                 "parallelism": f"dd{world}",
             },
             "mgpis_dof_iter_per_s": dof_its / elapsed,
             "pcg_iters_per_solve": pcg_its / max(n * nsub, 1),
             "setup_s": t_setup,
+            "mass_cg_iters_per_admm_iter": int(mc.get("mass_iters")[0]) / max(n, 1),
             "roofline": {
                 "bound": "hbm",
                 "kernel": "k_sell<kPcg> fine level (SELL-BSR3 SpMV q=Kz+beta q, p=z+beta p, p.q)",

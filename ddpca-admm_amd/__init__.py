@@ -42,7 +42,8 @@ def lib() -> C.CDLL:
 
 
 class MgpisOptions(C.Structure):
-    _fields_ = [("smoother", C.c_int), ("nu", C.c_int), ("omega", C.c_double), ("iters_per_graph", C.c_int)]
+    _fields_ = [("smoother", C.c_int), ("nu", C.c_int), ("omega", C.c_double), ("iters_per_graph", C.c_int),
+                ("warm_start", C.c_int), ("precond_fp32", C.c_int)]
 
 
 _P = C.c_void_p
@@ -72,6 +73,7 @@ def _declare(L: C.CDLL) -> None:
     L.mgpis_gpu_spmv.argtypes = [_P, C.c_int, _P, _P]
     L.mgpis_gpu_vcycle.argtypes = [_P, _P, _P]
     L.mgpis_gpu_info.argtypes = [_P, _I64P]
+    L.mgpis_gpu_bench_spmv.argtypes = [_P, C.c_int, C.c_int, _DP, _DP]
     L.mgpis_gpu_destroy.argtypes = [_P]
     if hasattr(L, "mcontact_gpu_create"):
         L.mcontact_gpu_create.argtypes = [_P, C.c_int, C.c_int, C.c_int, _P, C.POINTER(MgpisOptions),
@@ -279,6 +281,12 @@ class MGPIS:
         return dict(nlev=out[0], nfree=out[1], nnzb=out[2], chunks=out[3], omega=out[4] / 1e6, lmax=out[5] / 1e6,
                     device=out[6])
 
+    def bench_spmv(self, variant: int = 0, reps: int = 20) -> tuple:
+        """Diagnostic: (ms per launch, algorithmic bytes per launch) of a fine-level kernel variant."""
+        ms, nbytes = C.c_double(), C.c_double()
+        _check(lib().mgpis_gpu_bench_spmv(self._h, variant, reps, C.byref(ms), C.byref(nbytes)))
+        return ms.value, nbytes.value
+
     def CG_SOLV(self, precSwit: int, totaForc: np.ndarray, rtol: float = 1e-14, maxit: Optional[int] = None):
         """Returns (x, iterations, recursive relative residual); reference defaults rtol=1e-14, maxit=n."""
         b = np.ascontiguousarray(totaForc, dtype=np.float64)
@@ -348,7 +356,7 @@ class MCONTACT:
 
     def get(self, what: str, index: int = 0) -> np.ndarray:
         n = _check(lib().mcontact_gpu_get(self._h, what.encode(), index, None, 0))
-        dtype = np.int64 if what == "pcg_iters" else np.float64
+        dtype = np.int64 if what in ("pcg_iters", "owned", "mass_iters") else np.float64
         out = np.zeros(n, dtype)
         if n:
             _check(lib().mcontact_gpu_get(self._h, what.encode(), index, _ptr(out), n))

@@ -2,6 +2,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstring>
 #include <memory>
 
@@ -70,6 +71,18 @@ mgpis_options_t resolve(const mgpis_options_t* opt) {
     return o;
 }
 
+std::unique_ptr<MgpisDevice> single(int device, const std::vector<int64_t>& nn, const std::vector<const Bsr3*>& B,
+                                    const std::vector<uint8_t>& fr, const std::vector<const Stencil*>& S,
+                                    const mgpis_options_t* opt, const double* coords = nullptr) {
+    SubdomainOps ops;
+    ops.nnodes = nn;
+    ops.K = B;
+    ops.dof_free = fr.data();
+    ops.S = S;
+    ops.coords = coords;
+    return std::make_unique<MgpisDevice>(device, std::vector<SubdomainOps>{ops}, resolve(opt));
+}
+
 }  // namespace
 
 extern "C" {
@@ -79,6 +92,8 @@ void mgpis_default_options(mgpis_options_t* opt) {
     opt->nu = 1;
     opt->omega = 0.0;
     opt->iters_per_graph = 4;
+    opt->warm_start = 0;
+    opt->precond_fp32 = 0;
 }
 
 int ddpca_gpu_available(void) {
@@ -109,7 +124,7 @@ int mgpis_gpu_create(int device, int nlev, const int64_t* nnodes, const int64_t*
         for (auto& b : B) Bp.push_back(&b);
         for (auto& s : S) Sp.push_back(&s);
         auto h = std::make_unique<ddpca_mgpis>();
-        h->dev = std::make_unique<MgpisDevice>(device, nn_v, Bp, fr, Sp, resolve(opt));
+        h->dev = single(device, nn_v, Bp, fr, Sp, opt);
         *out = h.release();
     });
 }
@@ -136,7 +151,7 @@ int mgpis_gpu_create_bsr3(int device, int nlev, const int64_t* nnodes, const int
         for (auto& b : B) Bp.push_back(&b);
         for (auto& s : S) Sp.push_back(&s);
         auto h = std::make_unique<ddpca_mgpis>();
-        h->dev = std::make_unique<MgpisDevice>(device, nn_v, Bp, fr, Sp, resolve(opt));
+        h->dev = single(device, nn_v, Bp, fr, Sp, opt);
         *out = h.release();
     });
 }
@@ -153,7 +168,7 @@ int ddpca_problem_mgpis(ddpca_problem_t p, int64_t tv, int device, const mgpis_o
         for (const auto& b : g.levelStif) Bp.push_back(&b);
         for (const auto& s : g.scalProl) Sp.push_back(&s);
         auto h = std::make_unique<ddpca_mgpis>();
-        h->dev = std::make_unique<MgpisDevice>(device, nn, Bp, g.consFlag, Sp, resolve(opt));
+        h->dev = single(device, nn, Bp, g.consFlag, Sp, opt, g.nodeCoor.empty() ? nullptr : g.nodeCoor[0].data());
         *out = h.release();
     });
 }
@@ -167,13 +182,15 @@ int mgpis_gpu_solve(mgpis_t h, const double* b, double* x, int prec, double rtol
         MgpisDevice& D = *h->dev;
         select_device(D.device);
         DevBuf<double> tmp;
-        tmp.upload(b, D.nfree);
-        D.scatter_free(tmp.p, D.bs.p);
-        D.pcg_solve(prec, rtol, maxit, &it, relres);
-        D.gather_free(D.xs.p, tmp.p);
-        DDPCA_HIP(hipMemcpyAsync(x, tmp.p, D.nfree * sizeof(double), hipMemcpyDeviceToHost, D.stream));
+        tmp.upload(b, D.nfree[0]);
+        D.scatter_free(0, tmp.p, D.bs.p);
+        D.pcg_solve(prec, rtol, {maxit});
+        it = D.sc_host[0].iter;
+        D.gather_free(0, D.xs.p, tmp.p);
+        DDPCA_HIP(hipMemcpyAsync(x, tmp.p, D.nfree[0] * sizeof(double), hipMemcpyDeviceToHost, D.stream));
         DDPCA_HIP(hipStreamSynchronize(D.stream));
         if (iters) *iters = it;
+        if (relres) *relres = D.sc_host[0].bb > 0 ? std::sqrt(D.sc_host[0].rr / D.sc_host[0].bb) : 0.0;
     });
     if (rc != 0) return rc;
     return (maxit > 0 && it >= maxit) ? (int)std::min<int64_t>(it, 1 << 30) : 0;
@@ -186,13 +203,13 @@ int mgpis_gpu_spmv(mgpis_t h, int level, const double* x, double* y) {
         if (level < 0 || level >= (int)D.lev.size()) throw ApiError(DDPCA_EINVAL, "level");
         if (level != (int)D.lev.size() - 1) throw ApiError(DDPCA_EINVAL, "condensed spmv is defined on the fine level");
         DevBuf<double> tmp, full_x, full_y;
-        tmp.upload(x, D.nfree);
+        tmp.upload(x, D.nfree[0]);
         full_x.alloc(3 * D.lev.back().nn);
         full_y.alloc(3 * D.lev.back().nn);
-        D.scatter_free(tmp.p, full_x.p);
+        D.scatter_free(0, tmp.p, full_x.p);
         D.spmv(level, full_x.p, full_y.p);
-        D.gather_free(full_y.p, tmp.p);
-        DDPCA_HIP(hipMemcpyAsync(y, tmp.p, D.nfree * sizeof(double), hipMemcpyDeviceToHost, D.stream));
+        D.gather_free(0, full_y.p, tmp.p);
+        DDPCA_HIP(hipMemcpyAsync(y, tmp.p, D.nfree[0] * sizeof(double), hipMemcpyDeviceToHost, D.stream));
         DDPCA_HIP(hipStreamSynchronize(D.stream));
     });
 }
@@ -202,12 +219,12 @@ int mgpis_gpu_vcycle(mgpis_t h, const double* r, double* z) {
         MgpisDevice& D = *h->dev;
         select_device(D.device);
         DevBuf<double> tmp;
-        tmp.upload(r, D.nfree);
-        D.scatter_free(tmp.p, D.rs.p);
+        tmp.upload(r, D.nfree[0]);
+        D.scatter_free(0, tmp.p, D.rs.p);
         DDPCA_HIP(hipMemsetAsync(D.sc.p, 0, sizeof(PcgScal), D.stream));  // done = 0
         D.vcycle(D.rs.p, D.zs.p, false);
-        D.gather_free(D.zs.p, tmp.p);
-        DDPCA_HIP(hipMemcpyAsync(z, tmp.p, D.nfree * sizeof(double), hipMemcpyDeviceToHost, D.stream));
+        D.gather_free(0, D.zs.p, tmp.p);
+        DDPCA_HIP(hipMemcpyAsync(z, tmp.p, D.nfree[0] * sizeof(double), hipMemcpyDeviceToHost, D.stream));
         DDPCA_HIP(hipStreamSynchronize(D.stream));
     });
 }
@@ -216,12 +233,29 @@ int mgpis_gpu_info(mgpis_t h, int64_t* out7) {
     return guarded([&] {
         MgpisDevice& D = *h->dev;
         out7[0] = (int64_t)D.lev.size();
-        out7[1] = D.nfree;
+        const double lmax = D.lev.size() > 1 ? D.lev.back().lmax[0] : 0.0;
+        out7[1] = D.nfree[0];
         out7[2] = D.lev.back().nnzb;
         out7[3] = D.lev.back().nch;
-        out7[4] = (int64_t)(D.lev.back().omega * 1e6);
-        out7[5] = (int64_t)(D.lev.back().lmax * 1e6);
+        out7[4] = (int64_t)((D.opt.omega > 0.0 ? D.opt.omega : lmax > 0.0 ? 4.0 / (3.0 * lmax) : 1.0) * 1e6);
+        out7[5] = (int64_t)(lmax * 1e6);
         out7[6] = D.device;
+    });
+}
+
+int mgpis_gpu_bench_spmv(mgpis_t h, int variant, int reps, double* ms, double* bytes) {
+    return guarded([&] {
+        if (!h || !ms) throw ApiError(DDPCA_EINVAL, "null argument");
+        MgpisDevice& D = *h->dev;
+        select_device(D.device);
+        *ms = D.bench_spmv(variant, reps);
+        // 76 B per block + x gathered once (24 B/node) + per-node vector traffic of the mode:
+        // y = Kx writes y; PCG reads/writes p, q; residual reads b, writes r; Chebyshev reads b,
+        // x, d, the 9-entry block inverse and writes d, x_new
+        const double per_node[4] = {24.0, 96.0, 48.0, 24.0 * 5.0 + 72.0};
+        const int mode = (variant >> 2) & 3;
+        const LevelDev& L = D.lev.back();
+        if (bytes) *bytes = 76.0 * (double)L.nnzb_sub[0] + (24.0 + per_node[mode]) * (double)L.nloc[0];
     });
 }
 

@@ -63,8 +63,39 @@ struct DevBuf {
 };
 
 inline int ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
+inline int64_t pad64(int64_t n) { return (n + 63) / 64 * 64; }
 
 // Make `device` current and check it is a gfx950 part (no silent fallback anywhere).
 void select_device(int device);
+
+// Host-visible stop state of one iterative solve, written by the device with system-scope
+// stores into pinned, device-mapped host memory: the host paces graph replays by reading it,
+// with no copy and no stream synchronisation per poll.
+struct PcgMirror {
+    int64_t iter;
+    int32_t done;
+    int32_t fail;
+};
+
+__device__ __forceinline__ void mirror_store(PcgMirror* m, int64_t iter, int done, int fail) {
+    __hip_atomic_store(&m->iter, iter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&m->fail, fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&m->done, done, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Pinned host array of n mirrors plus its device alias.
+struct MirrorBuf {
+    PcgMirror* host = nullptr;
+    PcgMirror* dev = nullptr;
+    int n = 0;
+    void alloc(int count);
+    void reset();  // host-side zeroing; only while no kernel can write it
+    ~MirrorBuf();
+};
+
+// Replay `graph` (k iterations each) on `stream` until every mirror reports done, keeping
+// about one replay queued ahead of the slowest unfinished solve.  `launched` = iterations
+// already enqueued (eager + pre-enqueued replays).  Returns the number of replays launched.
+int64_t pace_until_done(hipStream_t stream, hipGraphExec_t graph, const MirrorBuf& m, int64_t k, int64_t launched);
 
 }  // namespace ddpca

@@ -4,7 +4,7 @@
 // Per iteration (same data flow as the reference):
 //   body balance   b_tv = consForc + consOper (systTran_pena aux - systTran lambda)   (2514-2524)
 //                  u_tv = OUTP_SUB1(MGPIS PCG(b_tv))                                 (2531-2533)
-//                  -- all owned subdomains solve concurrently, one HIP stream each
+//                  -- every owned subdomain in ONE batched PCG (device_mgpis.hpp)
 //   interface      gamma = 1/2 (L0 l0 - L1 l1 + R0 u0 - R1 u1 - pema g)              (2632-2636)
 //                  -- each side contributes its half; sides on different ranks swap their
 //                     halves with one RCCL send/recv pair over xGMI (no global collective)
@@ -13,8 +13,9 @@
 //   Lagrange       l += M^-1 (T^T u - M^rho aux)                                      (2689-2704)
 //   MONITOR        squared norms reduced on device, one small RCCL all-reduce,
 //                  reference stopping logic on the host                               (2725-2845)
-// The surface mass solves (LDLT in the reference, < 120000 rows) run as a batched Jacobi-PCG,
-// one workgroup per system, to a 1e-14 relative residual.
+// The surface mass solves (LDLT in the reference, < 120000 rows) run as ONE batched
+// Jacobi-PCG over every owned side (ELL-64 rows, per-side scalars, all CUs busy) to a 1e-14
+// relative residual.  Everything runs on the batch's single stream.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -24,6 +25,7 @@
 #include <cstring>
 #include <map>
 #include <memory>
+#include <numeric>
 
 #include "../../include/ddpca_amd.h"
 #include "device_mgpis.hpp"
@@ -86,6 +88,12 @@ __device__ __forceinline__ double csr_row(const int64_t* ptr, const int32_t* col
     return s;
 }
 
+// y = x, 16 B per lane (n even: batch vectors are 3 * multiple-of-64 long)
+__global__ void k_copy2(double2* y, const double2* x, int64_t n2) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n2) y[i] = x[i];
+}
+
 // b[rows[i]] += sum_k val[k] state[col[k]]  (coupling of the body-balance RHS)
 __global__ void k_cpl(const int32_t* rows, const int64_t* ptr, const int32_t* col, const double* val,
                       const double* state, double* b, int64_t n) {
@@ -94,12 +102,15 @@ __global__ void k_cpl(const int32_t* rows, const int64_t* ptr, const int32_t* co
     b[rows[i]] += csr_row(ptr, col, val, state, i);
 }
 
-// u = mask ? x : prescribed  (OUTP_SUB1 without rotations)
-__global__ void k_outp(const double* x, const uint8_t* mask, const double* presc, double* u, int64_t nn) {
+// u = mask ? x : prescribed  (OUTP_SUB1 without rotations); x and mask in the solver's device
+// node order, u and presc in the reference order (onode: device node -> reference node)
+__global__ void k_outp(const double* x, const uint8_t* mask, const int32_t* onode, const double* presc, double* u,
+                       int64_t nn) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nn) return;
     const uint8_t m = mask[i];
-    for (int a = 0; a < 3; ++a) u[3 * i + a] = ((m >> a) & 1) ? x[3 * i + a] : presc[3 * i + a];
+    const int64_t o = onode[i];
+    for (int a = 0; a < 3; ++a) u[3 * o + a] = ((m >> a) & 1) ? x[3 * i + a] : presc[3 * o + a];
 }
 
 // gamma_seg += sgn/2 (L lambda + R u) + cst
@@ -165,82 +176,131 @@ __global__ void k_rhs3(const int64_t* ap, const int32_t* ac, const double* av, c
     rhs[i] = s;
 }
 
-struct MassSys {
-    const int64_t* ptr;
+// ---- batched Jacobi-PCG over the owned sides' surface mass systems.  Rows of all systems
+// are concatenated, each padded to a multiple of 64 (ELL-64: chunk = 64 rows = one wave,
+// lane = row, slot k at (off[c]+k)*64 + lane); per-system scalars live in PcgScal.
+struct EllArgs {
+    const int32_t* slots;
+    const int64_t* off;
     const int32_t* col;
     const double* val;
+    const int32_t* csys;
     const double* dinv;
-    const double* b;
-    double* x;     // solution (overwritten) or increment target when accumulate
-    double* r;
-    double* p;
-    double* q;
-    int64_t n;
-    int accumulate;  // 1: x += solution
+    int64_t nch;
 };
 
-__device__ double block_sum1024(double v, double* red) {
-    v = wsum(v);
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    __syncthreads();
-    if (lane == 0) red[w] = v;
-    __syncthreads();
-    double s = 0.0;
-    const int nw = blockDim.x >> 6;
-    for (int k = 0; k < nw; ++k) s += red[k];
-    return s;
+// r = b, x = 0, z = D^-1 b, p = q = 0; partials (b.z, b.b) per chunk
+__global__ __launch_bounds__(256) void k_mcg_init(const double* b, const double* dinv, double* x, double* r, double* z,
+                                                  double* p, double* q, double* partial, int64_t nrow) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= nrow) return;
+    const double bi = b[i], zi = dinv[i] * bi;
+    x[i] = 0.0;
+    r[i] = bi;
+    z[i] = zi;
+    p[i] = 0.0;
+    q[i] = 0.0;
+    const double a = wsum(bi * zi), c = wsum(bi * bi);
+    if ((threadIdx.x & 63) == 0) {
+        partial[2 * (i >> 6)] = a;
+        partial[2 * (i >> 6) + 1] = c;
+    }
 }
 
-// Batched Jacobi-preconditioned CG, one workgroup per SPD surface-mass system.
-__global__ __launch_bounds__(1024) void k_mass_cg(const MassSys* sys, double rtol, int maxit) {
-    __shared__ double red[16];
-    const MassSys S = sys[blockIdx.x];
-    const int64_t n = S.n;
-    double* xs = S.accumulate ? S.q + n : S.x;  // accumulate: solve into scratch, then add
-    double rz = 0.0, bb = 0.0;
-    {
-        double a = 0.0, c = 0.0;
-        for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
-            const double bi = S.b[i];
-            xs[i] = 0.0;
-            S.r[i] = bi;
-            const double zi = S.dinv[i] * bi;
-            S.p[i] = zi;
-            a += bi * zi;
-            c += bi * bi;
-        }
-        rz = block_sum1024(a, red);
-        bb = block_sum1024(c, red);
+// q = A z + beta q, p = z + beta p; partial p.q per chunk
+__global__ __launch_bounds__(256) void k_mcg_spmv(EllArgs e, const PcgScal* sc, const double* z, double* q, double* p,
+                                                  double* partial) {
+    const int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (c >= e.nch) return;
+    const int sys = e.csys[c];
+    if (sc[sys].done) return;
+    const int lane = threadIdx.x & 63;
+    const int64_t row = c * 64 + lane;
+    const int ns = e.slots[c];
+    const int32_t* cp = e.col + e.off[c] * 64 + lane;
+    const double* vp = e.val + e.off[c] * 64 + lane;
+    double s = 0.0;
+#pragma unroll 4
+    for (int k = 0; k < ns; ++k) s += vp[(int64_t)k * 64] * z[cp[(int64_t)k * 64]];
+    const double be = sc[sys].beta;
+    const double qi = s + be * q[row], pi = z[row] + be * p[row];
+    q[row] = qi;
+    p[row] = pi;
+    const double d = wsum(pi * qi);
+    if (lane == 0) partial[2 * c] = d;
+}
+
+// x += alpha p, r -= alpha q, z = D^-1 r; partials (r.r, r.z) per chunk
+__global__ __launch_bounds__(256) void k_mcg_axpy(EllArgs e, const PcgScal* sc, double* x, double* r, double* z,
+                                                  const double* p, const double* q, double* partial) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t c = i >> 6;
+    if (c >= e.nch) return;
+    const int sys = e.csys[c];
+    if (sc[sys].done) return;
+    const double al = sc[sys].alpha;
+    x[i] += al * p[i];
+    const double ri = r[i] - al * q[i], zi = e.dinv[i] * ri;
+    r[i] = ri;
+    z[i] = zi;
+    const double a = wsum(ri * ri), b = wsum(ri * zi);
+    if ((threadIdx.x & 63) == 0) {
+        partial[2 * c] = a;
+        partial[2 * c + 1] = b;
     }
-    const double tol2 = rtol * rtol * bb;
-    for (int it = 0; it < maxit && bb > 0.0; ++it) {
-        __syncthreads();
-        double pq = 0.0;
-        for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
-            const double qi = csr_row(S.ptr, S.col, S.val, S.p, i);
-            S.q[i] = qi;
-            pq += S.p[i] * qi;
-        }
-        pq = block_sum1024(pq, red);
-        const double al = rz / pq;
-        double rr = 0.0, rzn = 0.0;
-        for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
-            xs[i] += al * S.p[i];
-            const double ri = S.r[i] - al * S.q[i];
-            S.r[i] = ri;
-            rr += ri * ri;
-            rzn += ri * S.dinv[i] * ri;
-        }
-        rr = block_sum1024(rr, red);
-        rzn = block_sum1024(rzn, red);
-        if (rr <= tol2) break;
-        const double be = rzn / rz;
-        rz = rzn;
-        for (int64_t i = threadIdx.x; i < n; i += blockDim.x) S.p[i] = S.dinv[i] * S.r[i] + be * S.p[i];
+}
+
+enum McgWhat { kMcgInit = 0, kMcgAlpha = 1, kMcgBeta = 2 };
+
+// per-system scalars: one workgroup per system, fixed order over its chunks
+__global__ __launch_bounds__(256) void k_mcg_fin(int what, const double* partial, const int64_t* cb, PcgScal* scv,
+                                                 PcgMirror* mirror) {
+    const int sys = blockIdx.x;
+    PcgScal* sc = scv + sys;
+    if (what != kMcgInit && sc->done) return;
+    __shared__ double r0[4], r1[4];
+    double a = 0.0, b = 0.0;
+    for (int64_t k = cb[sys] + threadIdx.x; k < cb[sys + 1]; k += 256) {
+        a += partial[2 * k];
+        b += partial[2 * k + 1];
+    }
+    a = wsum(a);
+    b = wsum(b);
+    if ((threadIdx.x & 63) == 0) {
+        r0[threadIdx.x >> 6] = a;
+        r1[threadIdx.x >> 6] = b;
     }
     __syncthreads();
-    if (S.accumulate)
-        for (int64_t i = threadIdx.x; i < n; i += blockDim.x) S.x[i] += xs[i];
+    if (threadIdx.x != 0) return;
+    a = (r0[0] + r0[1]) + (r0[2] + r0[3]);
+    b = (r1[0] + r1[1]) + (r1[2] + r1[3]);
+    if (what == kMcgInit) {
+        sc->delta = a;
+        sc->bb = b;
+        sc->rr = b;
+        sc->tol2 = sc->tol2 * b;
+        sc->beta = 0.0;
+        sc->iter = 0;
+        sc->fail = 0;
+        sc->done = (b <= sc->tol2 || sc->maxit <= 0) ? 1 : 0;
+        mirror_store(mirror + sys, 0, sc->done, 0);
+    } else if (what == kMcgAlpha) {
+        sc->pq = a;
+        if (!(a > 0.0) || !isfinite(a)) {
+            sc->fail = 1;
+            sc->done = 1;
+            mirror_store(mirror + sys, sc->iter, 1, 1);
+        }
+        sc->alpha = sc->delta / a;
+    } else {
+        sc->rr = a;
+        sc->iter += 1;
+        if (!isfinite(a) || !isfinite(b)) sc->fail = 1;
+        if (sc->fail || a <= sc->tol2 || sc->iter >= sc->maxit) sc->done = 1;
+        sc->beta = b / sc->delta;
+        sc->delta = b;
+        mirror_store(mirror + sys, sc->iter, sc->done, sc->fail);
+    }
 }
 
 // partial[2b], partial[2b+1] = sum (a-o)^2, sum a^2 over block b of one vector pair
@@ -288,29 +348,143 @@ __global__ void k_reduce_pairs(const double* partial, int64_t nb, double* out2) 
 
 inline int nb256(int64_t n) { return (int)std::max<int64_t>(1, (n + 255) / 256); }
 
+// Batched surface-mass solver: one graph of `k` CG iterations over every system, replayed
+// until every system reports done through the host-mapped mirror.
+class MassBatch {
+public:
+    int nsys = 0;
+    int64_t nrow = 0, nch = 0;
+    DevBuf<int32_t> slots, col, csys;
+    DevBuf<int64_t> off, cb;
+    DevBuf<double> val, dinv, b, x, r, z, p, q, partial;
+    DevBuf<PcgScal> sc;
+    PcgScal* sc_host = nullptr;
+    MirrorBuf mirror;
+    int64_t k = 8;
+    int64_t last_iters = 0;
+
+    // A[i] = system i (rows m_i), placed at rows roff[i] (multiples of 64) of nrow_total.
+    void build(const std::vector<const Csr*>& A, const std::vector<int64_t>& roff, int64_t nrow_total) {
+        nsys = (int)A.size();
+        nrow = nrow_total;
+        nch = nrow / 64;
+        std::vector<int32_t> sl(std::max<int64_t>(nch, 1), 0), cs(std::max<int64_t>(nch, 1), 0);
+        std::vector<int64_t> of(nch + 1, 0), c0(nsys + 1, nch);
+        std::vector<double> di(std::max<int64_t>(nrow, 1), 0.0);
+        for (int s = 0; s < nsys; ++s) {
+            const Csr& M = *A[s];
+            c0[s] = roff[s] / 64;
+            for (int64_t c = roff[s] / 64; c < (roff[s] + pad64(M.nrow)) / 64; ++c) {
+                cs[c] = s;
+                int64_t mx = 0;
+                for (int64_t r = (c * 64 - roff[s]); r < std::min(M.nrow, c * 64 - roff[s] + 64); ++r)
+                    mx = std::max(mx, M.ptr[r + 1] - M.ptr[r]);
+                sl[c] = (int32_t)mx;
+            }
+        }
+        for (int64_t c = 0; c < nch; ++c) of[c + 1] = of[c] + sl[c];
+        std::vector<int32_t> co(std::max<int64_t>(of[nch] * 64, 1), 0);
+        std::vector<double> va(std::max<int64_t>(of[nch] * 64, 1), 0.0);
+        for (int64_t c = 0; c < nch; ++c)
+            for (int64_t q = of[c]; q < of[c + 1]; ++q)
+                for (int lane = 0; lane < 64; ++lane) co[q * 64 + lane] = (int32_t)(c * 64 + lane);  // pad: self, 0
+        for (int s = 0; s < nsys; ++s) {
+            const Csr& M = *A[s];
+            for (int64_t r = 0; r < M.nrow; ++r) {
+                const int64_t g = roff[s] + r, c = g / 64, lane = g % 64;
+                for (int64_t k2 = M.ptr[r]; k2 < M.ptr[r + 1]; ++k2) {
+                    const int64_t q = of[c] + (k2 - M.ptr[r]);
+                    co[q * 64 + lane] = (int32_t)(roff[s] + M.col[k2]);
+                    va[q * 64 + lane] = M.val[k2];
+                    if (M.col[k2] == r) di[g] = 1.0 / M.val[k2];
+                }
+            }
+        }
+        slots.upload(sl);
+        csys.upload(cs);
+        off.upload(of);
+        col.upload(co);
+        val.upload(va);
+        dinv.upload(di);
+        cb.upload(c0);
+        for (auto* v : {&b, &x, &r, &z, &p, &q}) {
+            v->alloc(std::max<int64_t>(nrow, 2));
+            v->zero();
+        }
+        partial.alloc(2 * std::max<int64_t>(nch, 1));
+        sc.alloc(std::max(nsys, 1));
+        DDPCA_HIP(hipHostMalloc(reinterpret_cast<void**>(&sc_host), std::max(nsys, 1) * sizeof(PcgScal)));
+        mirror.alloc(nsys);
+    }
+    ~MassBatch() {
+        if (graph_) (void)hipGraphExecDestroy(graph_);
+        if (sc_host) (void)hipHostFree(sc_host);
+    }
+
+    // x_out (nrow) = A^-1 b.  Asynchronous on `s` except for the host pacing of replays.
+    void solve(hipStream_t s, double* x_out, double rtol, int64_t maxit) {
+        if (nsys == 0) return;
+        if (x_out != x_target_) {
+            if (graph_) (void)hipGraphExecDestroy(graph_);
+            graph_ = nullptr;
+            x_target_ = x_out;
+        }
+        if (!graph_) capture(s);
+        mirror.reset();  // the previous solve on `s` was paced to completion before this point
+        for (int i = 0; i < nsys; ++i) {
+            sc_host[i] = PcgScal{};
+            sc_host[i].tol2 = rtol * rtol;
+            sc_host[i].maxit = maxit;
+        }
+        DDPCA_HIP(hipMemcpyAsync(sc.p, sc_host, nsys * sizeof(PcgScal), hipMemcpyHostToDevice, s));
+        hipLaunchKernelGGL(k_mcg_init, dim3(nb256(nrow)), dim3(256), 0, s, b.p, dinv.p, x_out, r.p, z.p, p.p, q.p,
+                           partial.p, nrow);
+        hipLaunchKernelGGL(k_mcg_fin, dim3(nsys), dim3(256), 0, s, (int)kMcgInit, partial.p, cb.p, sc.p, mirror.dev);
+        pace_until_done(s, graph_, mirror, k, 0);
+    }
+
+    // after the stream synchronised: iterations of the last solve, breakdown check
+    void check() {
+        last_iters = 0;
+        for (int i = 0; i < nsys; ++i) {
+            if (mirror.host[i].fail) throw ApiError(DDPCA_ENUMERIC, "surface mass CG breakdown");
+            last_iters = std::max<int64_t>(last_iters, mirror.host[i].iter);
+        }
+    }
+
+private:
+    hipGraphExec_t graph_ = nullptr;
+    double* x_target_ = nullptr;
+    void capture(hipStream_t s) {
+        EllArgs e{slots.p, off.p, col.p, val.p, csys.p, dinv.p, nch};
+        hipGraph_t g;
+        DDPCA_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+        for (int64_t it = 0; it < k; ++it) {
+            hipLaunchKernelGGL(k_mcg_spmv, dim3(ceil_div(nch, 4)), dim3(256), 0, s, e, sc.p, z.p, q.p, p.p, partial.p);
+            hipLaunchKernelGGL(k_mcg_fin, dim3(nsys), dim3(256), 0, s, (int)kMcgAlpha, partial.p, cb.p, sc.p, mirror.dev);
+            hipLaunchKernelGGL(k_mcg_axpy, dim3(nb256(nrow)), dim3(256), 0, s, e, sc.p, x_target_, r.p, z.p, p.p, q.p,
+                               partial.p);
+            hipLaunchKernelGGL(k_mcg_fin, dim3(nsys), dim3(256), 0, s, (int)kMcgBeta, partial.p, cb.p, sc.p, mirror.dev);
+        }
+        DDPCA_HIP(hipStreamEndCapture(s, &g));
+        DDPCA_HIP(hipGraphInstantiate(&graph_, g, nullptr, nullptr, 0));
+        DDPCA_HIP(hipGraphDestroy(g));
+    }
+};
+
 }  // namespace
 
 // ================================================================================ handle
 struct ddpca_mcontact {
     struct Sub {
-        int64_t tv = 0;
-        std::unique_ptr<MgpisDevice> mg;
-        DevBuf<double> cf;      // consForc scattered to the nodal layout
-        DevBuf<double> presc;   // prescribed dof values (nodal)
-        DevBuf<double> u, uo;   // resuDisp (nodal) and previous iterate
-        DevBuf<int32_t> crow;   // coupling rows (nodal dofs, free only)
-        DevBuf<int64_t> cptr;
-        DevBuf<int32_t> ccol;
-        DevBuf<double> cval;
-        int64_t ncrow = 0, nn = 0;
-        int64_t last_iters = 0;
-        int64_t pred_iters = 0;
+        int64_t tv = 0, nn = 0;
+        int64_t dof0 = 0;  // first dof in the batch's fine layout
     };
     struct Side {
         int64_t ts = 0, s = 0, tv = 0, m = 0, mip = 0;
-        int64_t soff = 0;  // offset of [aux ; lambda] in the rank state vector
+        int64_t roff = 0;  // rows of aux at state[roff], lambda at state[R + roff]
+        int sub = 0;       // index into subs
         DevCsr lagr, pemr, tTp, mass, massp, iinpo;
-        DevBuf<double> dmass, dmassp, rhs, scratch;  // scratch: r, p, q, x2 (4m)
     };
     struct Itf {
         int64_t ts = 0, mip = 0, goff = 0;
@@ -328,10 +502,21 @@ struct ddpca_mcontact {
     std::vector<Sub> subs;
     std::vector<Side> sides;
     std::vector<Itf> itfs;
+    std::unique_ptr<MgpisDevice> mg;
+    std::vector<int64_t> maxit;          // per owned subdomain: n_free (reference maxit = rows)
+    DevBuf<double> cf;                   // consForc, solver (device) node order
+    DevBuf<double> presc, u, uo;         // batch fine layout, reference node order (3 nn_L)
+    DevBuf<int32_t> onode;               // device node -> reference-order node of the batch
+    DevBuf<int32_t> crow;                // coupling rows (solver dofs, free only)
+    DevBuf<int64_t> cptr;
+    DevBuf<int32_t> ccol;
+    DevBuf<double> cval;
+    int64_t ncrow = 0;
+    int64_t R = 0;                       // padded rows of all owned sides
     DevBuf<double> state, state_old, gamma, partial, moni;
-    DevBuf<MassSys> sys_aux, sys_lam;
+    MassBatch mb_aux, mb_lam;
     std::vector<double> moni_host;
-    hipStream_t main = nullptr;
+    hipStream_t main = nullptr;          // == mg->stream
     ncclComm_t comm = nullptr;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     // reference MONITOR state (MCONTACT.h:2494-2498, 2725-2845)
@@ -340,7 +525,7 @@ struct ddpca_mcontact {
     std::vector<std::vector<double>> moniReco;
     std::vector<std::vector<double>> rows;
     double timing[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    std::vector<int64_t> last_pcg;
+    double mass_iters = 0.0;
     mgpis_options_t opt{};
 };
 
@@ -350,8 +535,61 @@ void build(ddpca_mcontact& H, Problem& P) {
     MCONTACT& mc = P.mc;
     H.nsub = (int64_t)mc.multGrid.size();
     H.nint = (int64_t)mc.searCont.size();
-    // ---- owned interface sides: state layout [aux ; lambda] per side
-    int64_t soff = 0;
+    // ---- owned subdomains: one batched MGPIS
+    std::vector<SubdomainOps> ops;
+    for (int64_t tv = 0; tv < H.nsub; ++tv) {
+        if (H.owner[tv] != H.rank) continue;
+        if (P.owned.size() != (size_t)H.nsub || !P.owned[tv])
+            throw ApiError(DDPCA_ESTATE, "subdomain " + std::to_string(tv) + " is owned by this rank but was not established");
+        const MULTIGRID& g = mc.multGrid[tv];
+        SubdomainOps o;
+        o.nnodes.assign(g.leveCount.begin(), g.leveCount.end());
+        for (const auto& b : g.levelStif) o.K.push_back(&b);
+        for (const auto& s : g.scalProl) o.S.push_back(&s);
+        o.dof_free = g.consFlag.data();
+        o.coords = g.nodeCoor.empty() ? nullptr : g.nodeCoor[0].data();
+        ops.push_back(o);
+        ddpca_mcontact::Sub S;
+        S.tv = tv;
+        S.nn = g.numNodes();
+        H.subs.push_back(S);
+    }
+    if (!ops.empty()) {
+        H.mg = std::make_unique<MgpisDevice>(H.device, ops, H.opt);
+        H.main = H.mg->stream;
+    } else {
+        DDPCA_HIP(hipStreamCreateWithFlags(&H.main, hipStreamNonBlocking));
+    }
+    auto sub_index = [&](int64_t tv) {
+        for (size_t i = 0; i < H.subs.size(); ++i)
+            if (H.subs[i].tv == tv) return (int)i;
+        return -1;
+    };
+    const int64_t NN = H.mg ? H.mg->lev.back().nn : 0;
+    {
+        std::vector<double> cf(std::max<int64_t>(3 * NN, 2), 0.0), pr(std::max<int64_t>(3 * NN, 2), 0.0);
+        std::vector<int32_t> on(std::max<int64_t>(NN, 1));
+        std::iota(on.begin(), on.end(), 0);  // padding nodes map to themselves
+        for (size_t i = 0; i < H.subs.size(); ++i) {
+            auto& S = H.subs[i];
+            S.dof0 = H.mg->fine_dof_offset((int)i);
+            H.maxit.push_back(H.mg->nfree[i]);
+            const MULTIGRID& g = mc.multGrid[S.tv];
+            for (int64_t d = 0; d < 3 * S.nn; ++d)
+                if (g.consFlag[d]) cf[H.mg->fine_dof((int)i, d)] = g.consForc[g.freeIndex[d]];
+            for (const auto& kv : g.consDofv) pr[S.dof0 + kv.first] = kv.second;
+            for (int64_t r = 0; r < S.nn; ++r) on[S.dof0 / 3 + H.mg->fine_perm[i][r]] = (int32_t)(S.dof0 / 3 + r);
+        }
+        H.cf.upload(cf);
+        H.presc.upload(pr);
+        H.onode.upload(on);
+        H.u.alloc(cf.size());
+        H.uo.alloc(cf.size());
+        H.u.zero(H.main);
+        H.uo.zero(H.main);
+    }
+    // ---- owned interface sides: aux rows [roff, roff + m), lambda rows R + the same
+    int64_t roff = 0;
     std::map<std::pair<int64_t, int64_t>, size_t> side_of;
     for (int64_t ts = 0; ts < H.nint; ++ts) {
         const Interface& itf = mc.searCont[ts];
@@ -361,35 +599,38 @@ void build(ddpca_mcontact& H, Problem& P) {
             sd.ts = ts;
             sd.s = s;
             sd.tv = itf.body[s];
+            sd.sub = sub_index(sd.tv);
             sd.m = itf.mside(s);
             sd.mip = itf.mip();
-            sd.soff = soff;
-            soff += 2 * sd.m;
+            sd.roff = roff;
+            roff += pad64(sd.m);
             sd.lagr.upload(itf.inpoLagr[s]);
             sd.pemr.upload(itf.pemaInpo_r[s]);
             sd.tTp.upload(transpose(itf.systTran_pena[s]));
             sd.mass.upload(itf.inteMass[s]);
             sd.massp.upload(itf.inteMass_pena[s]);
             sd.iinpo.upload(itf.inteInpo[s]);
-            auto diag_inv = [](const Csr& A) {
-                std::vector<double> d(A.nrow, 0.0);
-                for (int64_t r = 0; r < A.nrow; ++r)
-                    for (int64_t k = A.ptr[r]; k < A.ptr[r + 1]; ++k)
-                        if (A.col[k] == r) d[r] = 1.0 / A.val[k];
-                return d;
-            };
-            sd.dmass.upload(diag_inv(itf.inteMass[s]));
-            sd.dmassp.upload(diag_inv(itf.inteMass_pena[s]));
-            sd.rhs.alloc(std::max<int64_t>(sd.m, 1));
-            sd.scratch.alloc(std::max<int64_t>(5 * sd.m, 1));
             side_of[{ts, s}] = H.sides.size();
             H.sides.push_back(std::move(sd));
         }
     }
-    H.state.alloc(std::max<int64_t>(soff, 1));
-    H.state_old.alloc(std::max<int64_t>(soff, 1));
+    H.R = roff;
+    H.state.alloc(std::max<int64_t>(2 * H.R, 2));
+    H.state_old.alloc(std::max<int64_t>(2 * H.R, 2));
     H.state.zero(H.main);
     H.state_old.zero(H.main);
+    {
+        std::vector<const Csr*> Ma, Ml;
+        std::vector<int64_t> ro;
+        for (auto& sd : H.sides) {
+            const Interface& itf = mc.searCont[sd.ts];
+            Ma.push_back(&itf.inteMass_pena[sd.s]);
+            Ml.push_back(&itf.inteMass[sd.s]);
+            ro.push_back(sd.roff);
+        }
+        H.mb_aux.build(Ma, ro, H.R);
+        H.mb_lam.build(Ml, ro, H.R);
+    }
     // ---- interfaces: gamma layout (cross-rank interfaces first, then rank-local)
     int64_t goff = 0;
     for (int pass = 0; pass < 2; ++pass)
@@ -420,46 +661,28 @@ void build(ddpca_mcontact& H, Problem& P) {
         }
     std::sort(H.itfs.begin(), H.itfs.end(), [](const auto& a, const auto& b) { return a.ts < b.ts; });
     H.gamma.alloc(std::max<int64_t>(goff, 1));
-    // ---- owned subdomains
-    for (int64_t tv = 0; tv < H.nsub; ++tv) {
-        if (H.owner[tv] != H.rank) continue;
-        if (P.owned.size() != (size_t)H.nsub || !P.owned[tv])
-            throw ApiError(DDPCA_ESTATE, "subdomain " + std::to_string(tv) + " is owned by this rank but was not established");
-        const MULTIGRID& g = mc.multGrid[tv];
-        ddpca_mcontact::Sub S;
-        S.tv = tv;
-        S.nn = g.numNodes();
-        std::vector<int64_t> nn(g.leveCount.begin(), g.leveCount.end());
-        std::vector<const Bsr3*> Bp;
-        std::vector<const Stencil*> Sp;
-        for (const auto& b : g.levelStif) Bp.push_back(&b);
-        for (const auto& s : g.scalProl) Sp.push_back(&s);
-        S.mg = std::make_unique<MgpisDevice>(H.device, nn, Bp, g.consFlag, Sp, H.opt);
-        std::vector<double> cf(3 * S.nn, 0.0), pr(3 * S.nn, 0.0);
-        for (int64_t d = 0; d < 3 * S.nn; ++d)
-            if (g.consFlag[d]) cf[d] = g.consForc[g.freeIndex[d]];
-        for (const auto& kv : g.consDofv) pr[kv.first] = kv.second;
-        S.cf.upload(cf);
-        S.presc.upload(pr);
-        S.u.alloc(3 * S.nn);
-        S.uo.alloc(3 * S.nn);
-        S.u.zero(H.main);
-        S.uo.zero(H.main);
-        // coupling rows: sum over incident sides of [systTran_pena | -systTran] on free dofs
+    // ---- coupling rows of the body-balance RHS: sum over incident sides of
+    //      [systTran_pena | -systTran] on free dofs, in batch dof / state coordinates
+    {
         std::map<int64_t, std::vector<std::pair<int32_t, double>>> rowmap;
-        for (int64_t ts = 0; ts < H.nint; ++ts) {
-            const Interface& itf = mc.searCont[ts];
-            for (int s = 0; s < 2; ++s) {
-                if (itf.body[s] != tv) continue;
-                const auto& sd = H.sides[side_of.at({ts, s})];
-                const Csr& Tp = itf.systTran_pena[s];
-                const Csr& T = itf.systTran[s];
-                for (int64_t r = 0; r < Tp.nrow; ++r) {
-                    if (!g.consFlag[r]) continue;
-                    for (int64_t k = Tp.ptr[r]; k < Tp.ptr[r + 1]; ++k)
-                        rowmap[r].push_back({(int32_t)(sd.soff + Tp.col[k]), Tp.val[k]});
-                    for (int64_t k = T.ptr[r]; k < T.ptr[r + 1]; ++k)
-                        rowmap[r].push_back({(int32_t)(sd.soff + sd.m + T.col[k]), -T.val[k]});
+        for (size_t si = 0; si < H.subs.size(); ++si) {
+            const auto& S = H.subs[si];
+            const MULTIGRID& g = mc.multGrid[S.tv];
+            for (int64_t ts = 0; ts < H.nint; ++ts) {
+                const Interface& itf = mc.searCont[ts];
+                for (int s = 0; s < 2; ++s) {
+                    if (itf.body[s] != S.tv) continue;
+                    const auto& sd = H.sides[side_of.at({ts, s})];
+                    const Csr& Tp = itf.systTran_pena[s];
+                    const Csr& T = itf.systTran[s];
+                    for (int64_t r = 0; r < Tp.nrow; ++r) {
+                        if (!g.consFlag[r]) continue;
+                        auto& row = rowmap[H.mg->fine_dof((int)si, r)];  // added into the solver RHS
+                        for (int64_t k = Tp.ptr[r]; k < Tp.ptr[r + 1]; ++k)
+                            row.push_back({(int32_t)(sd.roff + Tp.col[k]), Tp.val[k]});
+                        for (int64_t k = T.ptr[r]; k < T.ptr[r + 1]; ++k)
+                            row.push_back({(int32_t)(H.R + sd.roff + T.col[k]), -T.val[k]});
+                    }
                 }
             }
         }
@@ -475,39 +698,15 @@ void build(ddpca_mcontact& H, Problem& P) {
             }
             cptr.push_back((int64_t)ccol.size());
         }
-        S.ncrow = (int64_t)crow.size();
-        S.crow.upload(crow);
-        S.cptr.upload(cptr);
-        S.ccol.upload(ccol);
-        S.cval.upload(cval);
-        H.subs.push_back(std::move(S));
+        H.ncrow = (int64_t)crow.size();
+        H.crow.upload(crow);
+        H.cptr.upload(cptr);
+        H.ccol.upload(ccol);
+        H.cval.upload(cval);
     }
-    // ---- batched mass systems
-    auto make_sys = [&](bool aux) {
-        std::vector<MassSys> v;
-        for (auto& sd : H.sides) {
-            MassSys m{};
-            const DevCsr& A = aux ? sd.massp : sd.mass;
-            m.ptr = A.ptr.p;
-            m.col = A.col.p;
-            m.val = A.val.p;
-            m.dinv = aux ? sd.dmassp.p : sd.dmass.p;
-            m.b = sd.rhs.p;
-            m.x = H.state.p + sd.soff + (aux ? 0 : sd.m);
-            m.r = sd.scratch.p;
-            m.p = sd.scratch.p + sd.m;
-            m.q = sd.scratch.p + 2 * sd.m;  // accumulate mode uses q + n as the solution scratch
-            m.n = sd.m;
-            m.accumulate = aux ? 0 : 1;
-            v.push_back(m);
-        }
-        return v;
-    };
-    H.sys_aux.upload(make_sys(true));
-    H.sys_lam.upload(make_sys(false));
     int64_t maxn = 1;
     for (auto& S : H.subs) maxn = std::max(maxn, 3 * S.nn);
-    for (auto& sd : H.sides) maxn = std::max(maxn, 2 * sd.m);
+    for (auto& sd : H.sides) maxn = std::max(maxn, sd.m);
     H.partial.alloc(2 * nb256(maxn));
     const int64_t nmon = 2 * H.nsub + 8 * H.nint;
     H.moni.alloc(nmon);
@@ -576,132 +775,122 @@ double ms_since(std::chrono::steady_clock::time_point t0) {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
 
+void copy_dev(hipStream_t s, double* y, const double* x, int64_t n) {
+    // every batch vector has an even length (3 x multiple of 64, or 2R)
+    hipLaunchKernelGGL(k_copy2, dim3(nb256(n / 2)), dim3(256), 0, s, reinterpret_cast<double2*>(y),
+                       reinterpret_cast<const double2*>(x), n / 2);
+}
+
 // One ADMM iteration; returns true when MONITOR reports convergence.
 bool iterate_once(ddpca_mcontact& H, bool check) {
     const auto t0 = std::chrono::steady_clock::now();
+    hipStream_t st = H.main;
     // snapshot for MONITOR (resuDisp_0 / inteAuxi_0 / inteLagr_0, MCONTACT.h:2507-2509)
-    if (H.state.n) DDPCA_HIP(hipMemcpyAsync(H.state_old.p, H.state.p, H.state.n * sizeof(double), hipMemcpyDeviceToDevice, H.main));
-    DDPCA_HIP(hipEventRecord(H.ev[0], H.main));
-    // ---- body balance: all owned subdomains concurrently
-    for (auto& S : H.subs) {
-        MgpisDevice& D = *S.mg;
-        DDPCA_HIP(hipStreamWaitEvent(D.stream, H.ev[0], 0));
-        std::swap(S.u.p, S.uo.p);
-        DDPCA_HIP(hipMemcpyAsync(D.bs.p, S.cf.p, 3 * S.nn * sizeof(double), hipMemcpyDeviceToDevice, D.stream));
-        if (S.ncrow)
-            hipLaunchKernelGGL(k_cpl, dim3(nb256(S.ncrow)), dim3(256), 0, D.stream, S.crow.p, S.cptr.p, S.ccol.p, S.cval.p,
-                               H.state.p, D.bs.p, S.ncrow);
-        D.pcg_begin(1, 1.0e-14, D.nfree);
-        // pre-enqueue the predicted number of graph replays
-        const int64_t k = std::max(1, D.opt.iters_per_graph);
-        const int64_t pre = S.pred_iters > 0 ? std::max<int64_t>(1, S.pred_iters / k) : 1;
-        for (int64_t r = 0; r < pre; ++r) D.pcg_step(1);
+    if (H.R) copy_dev(st, H.state_old.p, H.state.p, 2 * H.R);
+    std::swap(H.u.p, H.uo.p);
+    // ---- body balance: every owned subdomain in one batched PCG
+    if (H.mg) {
+        MgpisDevice& D = *H.mg;
+        copy_dev(st, D.bs.p, H.cf.p, 3 * D.lev.back().nn);
+        if (H.ncrow)
+            hipLaunchKernelGGL(k_cpl, dim3(nb256(H.ncrow)), dim3(256), 0, st, H.crow.p, H.cptr.p, H.ccol.p, H.cval.p,
+                               H.state.p, D.bs.p, H.ncrow);
+        D.pcg_begin(1, 1.0e-14, H.maxit, H.opt.warm_start != 0 && H.tc > 0);
+        D.pcg_wait(1, 0);
+        hipLaunchKernelGGL(k_outp, dim3(nb256(D.lev.back().nn)), dim3(256), 0, st, D.xs.p, D.lev.back().mask.p,
+                           H.onode.p, H.presc.p, H.u.p, D.lev.back().nn);
     }
-    std::vector<bool> done(H.subs.size(), false);
-    size_t left = H.subs.size();
-    while (left) {
-        for (size_t i = 0; i < H.subs.size(); ++i) {
-            if (done[i]) continue;
-            MgpisDevice& D = *H.subs[i].mg;
-            if (D.pcg_poll()) {
-                done[i] = true;
-                --left;
-                if (D.sc_host->fail) throw ApiError(DDPCA_ENUMERIC, "subdomain PCG breakdown");
-                H.subs[i].last_iters = D.sc_host->iter;
-                H.subs[i].pred_iters = D.sc_host->iter;
-            } else {
-                D.pcg_step(1);
-            }
-        }
-    }
-    for (auto& S : H.subs) {
-        MgpisDevice& D = *S.mg;
-        hipLaunchKernelGGL(k_outp, dim3(nb256(S.nn)), dim3(256), 0, D.stream, D.xs.p, D.lev.back().mask.p, S.presc.p,
-                           S.u.p, S.nn);
-        DDPCA_HIP(hipEventRecord(H.ev[1], D.stream));
-        DDPCA_HIP(hipStreamWaitEvent(H.main, H.ev[1], 0));
-    }
-    DDPCA_HIP(hipEventRecord(H.ev[1], H.main));
+    DDPCA_HIP(hipEventRecord(H.ev[1], st));
     const double t_solve = ms_since(t0);
     // ---- interface balance: gamma contributions of owned sides
-    if (H.gamma.n) DDPCA_HIP(hipMemsetAsync(H.gamma.p, 0, H.gamma.n * sizeof(double), H.main));
-    auto sub_u = [&](int64_t tv) -> const double* {
-        for (auto& S : H.subs)
-            if (S.tv == tv) return S.u.p;
-        return nullptr;
+    if (H.gamma.n) DDPCA_HIP(hipMemsetAsync(H.gamma.p, 0, H.gamma.n * sizeof(double), st));
+    auto sub_u = [&](const ddpca_mcontact::Side& sd) -> const double* { return H.u.p + H.subs[sd.sub].dof0; };
+    auto itf_of = [&](int64_t ts) -> ddpca_mcontact::Itf& {
+        return *std::find_if(H.itfs.begin(), H.itfs.end(), [&](const auto& x) { return x.ts == ts; });
     };
     for (auto& sd : H.sides) {
-        const auto& I = *std::find_if(H.itfs.begin(), H.itfs.end(), [&](const auto& x) { return x.ts == sd.ts; });
-        hipLaunchKernelGGL(k_gamma, dim3(nb256(sd.mip)), dim3(256), 0, H.main, sd.lagr.ptr.p, sd.lagr.col.p,
-                           sd.lagr.val.p, H.state.p + sd.soff + sd.m, sd.pemr.ptr.p, sd.pemr.col.p, sd.pemr.val.p,
-                           sub_u(sd.tv), sd.s == 0 ? I.cgap.p : nullptr, sd.s == 0 ? 1.0 : -1.0, H.gamma.p + I.goff,
-                           sd.mip);
+        const auto& I = itf_of(sd.ts);
+        hipLaunchKernelGGL(k_gamma, dim3(nb256(sd.mip)), dim3(256), 0, st, sd.lagr.ptr.p, sd.lagr.col.p, sd.lagr.val.p,
+                           H.state.p + H.R + sd.roff, sd.pemr.ptr.p, sd.pemr.col.p, sd.pemr.val.p, sub_u(sd),
+                           sd.s == 0 ? I.cgap.p : nullptr, sd.s == 0 ? 1.0 : -1.0, H.gamma.p + I.goff, sd.mip);
     }
-    const auto tc0 = std::chrono::steady_clock::now();
     bool any_cross = false;
     for (auto& I : H.itfs) any_cross |= (I.cross && I.mine);
+    DDPCA_HIP(hipEventRecord(H.ev[0], st));
     if (any_cross) {
         if (!H.comm) throw ApiError(DDPCA_ESTATE, "cross-rank interfaces need mcontact_gpu_comm_init");
         DDPCA_NCCL(ncclGroupStart());
         for (auto& I : H.itfs) {
             if (!(I.cross && I.mine)) continue;
             const int peer = I.owner[0] == H.rank ? I.owner[1] : I.owner[0];
-            DDPCA_NCCL(ncclSend(H.gamma.p + I.goff, I.mip, ncclDouble, peer, H.comm, H.main));
-            DDPCA_NCCL(ncclRecv(I.recv.p, I.mip, ncclDouble, peer, H.comm, H.main));
+            DDPCA_NCCL(ncclSend(H.gamma.p + I.goff, I.mip, ncclDouble, peer, H.comm, st));
+            DDPCA_NCCL(ncclRecv(I.recv.p, I.mip, ncclDouble, peer, H.comm, st));
         }
         DDPCA_NCCL(ncclGroupEnd());
         for (auto& I : H.itfs)
             if (I.cross && I.mine)
-                hipLaunchKernelGGL(k_add, dim3(nb256(I.mip)), dim3(256), 0, H.main, H.gamma.p + I.goff, I.recv.p, I.mip);
+                hipLaunchKernelGGL(k_add, dim3(nb256(I.mip)), dim3(256), 0, st, H.gamma.p + I.goff, I.recv.p, I.mip);
     }
-    DDPCA_HIP(hipEventRecord(H.ev[2], H.main));
+    DDPCA_HIP(hipEventRecord(H.ev[2], st));
     for (auto& I : H.itfs)
         if (I.mine)
-            hipLaunchKernelGGL(k_project, dim3(nb256(I.mip / I.comp)), dim3(256), 0, H.main, H.gamma.p + I.goff, I.stat.p,
+            hipLaunchKernelGGL(k_project, dim3(nb256(I.mip / I.comp)), dim3(256), 0, st, H.gamma.p + I.goff, I.stat.p,
                                I.mip / I.comp, I.comp, I.fric);
     // ---- aux = (M^rho)^-1 (T^T u + M lambda + I gamma)
     for (auto& sd : H.sides) {
-        const auto& I = *std::find_if(H.itfs.begin(), H.itfs.end(), [&](const auto& x) { return x.ts == sd.ts; });
-        hipLaunchKernelGGL(k_rhs3, dim3(nb256(sd.m)), dim3(256), 0, H.main, sd.tTp.ptr.p, sd.tTp.col.p, sd.tTp.val.p,
-                           sub_u(sd.tv), sd.mass.ptr.p, sd.mass.col.p, sd.mass.val.p, H.state.p + sd.soff + sd.m, 1.0,
-                           sd.iinpo.ptr.p, sd.iinpo.col.p, sd.iinpo.val.p, H.gamma.p + I.goff, sd.rhs.p, sd.m);
+        const auto& I = itf_of(sd.ts);
+        hipLaunchKernelGGL(k_rhs3, dim3(nb256(sd.m)), dim3(256), 0, st, sd.tTp.ptr.p, sd.tTp.col.p, sd.tTp.val.p,
+                           sub_u(sd), sd.mass.ptr.p, sd.mass.col.p, sd.mass.val.p, H.state.p + H.R + sd.roff, 1.0,
+                           sd.iinpo.ptr.p, sd.iinpo.col.p, sd.iinpo.val.p, H.gamma.p + I.goff, H.mb_aux.b.p + sd.roff,
+                           sd.m);
     }
-    if (!H.sides.empty()) hipLaunchKernelGGL(k_mass_cg, dim3(H.sides.size()), dim3(1024), 0, H.main, H.sys_aux.p, 1.0e-14, 2000);
+    H.mb_aux.solve(st, H.state.p, 1.0e-14, 2000);
     // ---- lambda += M^-1 (T^T u - M^rho aux)
     for (auto& sd : H.sides)
-        hipLaunchKernelGGL(k_rhs3, dim3(nb256(sd.m)), dim3(256), 0, H.main, sd.tTp.ptr.p, sd.tTp.col.p, sd.tTp.val.p,
-                           sub_u(sd.tv), sd.massp.ptr.p, sd.massp.col.p, sd.massp.val.p, H.state.p + sd.soff, -1.0,
-                           nullptr, nullptr, nullptr, nullptr, sd.rhs.p, sd.m);
-    if (!H.sides.empty()) hipLaunchKernelGGL(k_mass_cg, dim3(H.sides.size()), dim3(1024), 0, H.main, H.sys_lam.p, 1.0e-14, 2000);
+        hipLaunchKernelGGL(k_rhs3, dim3(nb256(sd.m)), dim3(256), 0, st, sd.tTp.ptr.p, sd.tTp.col.p, sd.tTp.val.p,
+                           sub_u(sd), sd.massp.ptr.p, sd.massp.col.p, sd.massp.val.p, H.state.p + sd.roff, -1.0,
+                           nullptr, nullptr, nullptr, nullptr, H.mb_lam.b.p + sd.roff, sd.m);
+    if (!H.sides.empty()) {
+        H.mb_lam.solve(st, H.mb_lam.x.p, 1.0e-14, 2000);
+        hipLaunchKernelGGL(k_add, dim3(nb256(H.R)), dim3(256), 0, st, H.state.p + H.R, H.mb_lam.x.p, H.R);
+    }
     // ---- MONITOR norms (owned entries; others zero) and their reduction across ranks
-    DDPCA_HIP(hipMemsetAsync(H.moni.p, 0, H.moni.n * sizeof(double), H.main));
-    for (auto& S : H.subs) pair_norm(H, S.u.p, S.uo.p, 3 * S.nn, 2 * S.tv);
+    DDPCA_HIP(hipMemsetAsync(H.moni.p, 0, H.moni.n * sizeof(double), st));
+    for (auto& S : H.subs) pair_norm(H, H.u.p + S.dof0, H.uo.p + S.dof0, 3 * S.nn, 2 * S.tv);
     for (auto& sd : H.sides) {
         const int64_t base = 2 * H.nsub + 8 * sd.ts + 4 * sd.s;
-        pair_norm(H, H.state.p + sd.soff, H.state_old.p + sd.soff, sd.m, base);
-        pair_norm(H, H.state.p + sd.soff + sd.m, H.state_old.p + sd.soff + sd.m, sd.m, base + 2);
+        pair_norm(H, H.state.p + sd.roff, H.state_old.p + sd.roff, sd.m, base);
+        pair_norm(H, H.state.p + H.R + sd.roff, H.state_old.p + H.R + sd.roff, sd.m, base + 2);
     }
-    if (H.nranks > 1) DDPCA_NCCL(ncclAllReduce(H.moni.p, H.moni.p, H.moni.n, ncclDouble, ncclSum, H.comm, H.main));
-    DDPCA_HIP(hipEventRecord(H.ev[3], H.main));
-    DDPCA_HIP(hipMemcpyAsync(H.moni_host.data(), H.moni.p, H.moni.n * sizeof(double), hipMemcpyDeviceToHost, H.main));
-    DDPCA_HIP(hipStreamSynchronize(H.main));
+    if (H.nranks > 1) DDPCA_NCCL(ncclAllReduce(H.moni.p, H.moni.p, H.moni.n, ncclDouble, ncclSum, H.comm, st));
+    DDPCA_HIP(hipEventRecord(H.ev[3], st));
+    DDPCA_HIP(hipMemcpyAsync(H.moni_host.data(), H.moni.p, H.moni.n * sizeof(double), hipMemcpyDeviceToHost, st));
+    if (H.mg) H.mg->pcg_fetch();
+    DDPCA_HIP(hipStreamSynchronize(st));
+    if (H.mg) H.mg->pcg_check();
+    H.mb_aux.check();
+    H.mb_lam.check();
     float a = 0, b = 0;
     (void)hipEventElapsedTime(&a, H.ev[1], H.ev[3]);
-    (void)hipEventElapsedTime(&b, H.ev[1], H.ev[2]);
+    (void)hipEventElapsedTime(&b, H.ev[0], H.ev[2]);
     H.timing[0] += ms_since(t0);
     H.timing[1] += t_solve;
     H.timing[2] += a;
     H.timing[3] += any_cross ? b : 0.0;
-    (void)tc0;
-    for (auto& S : H.subs) {
-        H.timing[6] += (double)S.last_iters;
-        H.timing[8] += (double)S.last_iters * (double)S.mg->nfree;
-        if (S.mg->timed_kernel_samples) {
-            H.timing[7] += S.mg->fine_kernel_bytes() * (double)S.mg->timed_kernel_samples;
-            H.timing[4] += S.mg->timed_kernel_ms;
-            H.timing[5] += (double)S.mg->timed_kernel_samples;
-            S.mg->timed_kernel_ms = 0.0;
-            S.mg->timed_kernel_samples = 0;
+    H.mass_iters += (double)(H.mb_aux.last_iters + H.mb_lam.last_iters);
+    if (H.mg) {
+        MgpisDevice& D = *H.mg;
+        for (int s = 0; s < D.nsub; ++s) {
+            H.timing[6] += (double)D.sc_host[s].iter;
+            H.timing[8] += (double)D.sc_host[s].iter * (double)D.nfree[s];
+        }
+        if (D.timed_kernel_samples) {
+            H.timing[7] += D.timed_kernel_bytes;
+            H.timing[4] += D.timed_kernel_ms;
+            H.timing[5] += (double)D.timed_kernel_samples;
+            D.timed_kernel_ms = 0.0;
+            D.timed_kernel_bytes = 0.0;
+            D.timed_kernel_samples = 0;
         }
     }
     const bool conv = monitor(H);
@@ -729,7 +918,6 @@ int mcontact_gpu_create(ddpca_problem_t p, int device, int rank, int nranks, con
             if (o < 0 || o >= nranks) throw ApiError(DDPCA_EINVAL, "owner out of range");
         if (opt) H->opt = *opt;
         else mgpis_default_options(&H->opt);
-        DDPCA_HIP(hipStreamCreateWithFlags(&H->main, hipStreamNonBlocking));
         for (auto& e : H->ev) DDPCA_HIP(hipEventCreate(&e));
         build(*H, P);
         *out = H.release();
@@ -759,7 +947,8 @@ int64_t mcontact_gpu_iterate(mcontact_t h, int64_t maxit, int check) {
     const int rc = guarded([&] {
         select_device(h->device);
         for (double& t : h->timing) t = 0.0;
-        for (auto& S : h->subs) S.mg->time_kernel = true;
+        h->mass_iters = 0.0;
+        if (h->mg) h->mg->time_kernel = true;
         for (; n < maxit;) {
             const bool conv = iterate_once(*h, check != 0);
             ++n;
@@ -787,7 +976,7 @@ int64_t mcontact_gpu_get(mcontact_t h, const char* what, int64_t index, void* ou
             for (auto& S : h->subs)
                 if (S.tv == index) {
                     n = 3 * S.nn;
-                    if (out) DDPCA_HIP(hipMemcpy(out, S.u.p, std::min(n, cap) * sizeof(double), hipMemcpyDeviceToHost));
+                    if (out) DDPCA_HIP(hipMemcpy(out, h->u.p + S.dof0, std::min(n, cap) * sizeof(double), hipMemcpyDeviceToHost));
                     return;
                 }
             throw ApiError(DDPCA_EINVAL, "subdomain not owned by this rank");
@@ -796,7 +985,7 @@ int64_t mcontact_gpu_get(mcontact_t h, const char* what, int64_t index, void* ou
             for (auto& sd : h->sides)
                 if (2 * sd.ts + sd.s == index) {
                     n = sd.m;
-                    const double* src = h->state.p + sd.soff + (w == "inteAuxi" ? 0 : sd.m);
+                    const double* src = h->state.p + sd.roff + (w == "inteAuxi" ? 0 : h->R);
                     if (out) DDPCA_HIP(hipMemcpy(out, src, std::min(n, cap) * sizeof(double), hipMemcpyDeviceToHost));
                     return;
                 }
@@ -814,13 +1003,18 @@ int64_t mcontact_gpu_get(mcontact_t h, const char* what, int64_t index, void* ou
         if (w == "pcg_iters") {
             n = (int64_t)h->subs.size();
             if (out)
-                for (int64_t i = 0; i < std::min(n, cap); ++i) static_cast<int64_t*>(out)[i] = h->subs[i].last_iters;
+                for (int64_t i = 0; i < std::min(n, cap); ++i) static_cast<int64_t*>(out)[i] = h->mg->sc_host[i].iter;
             return;
         }
         if (w == "owned") {
             n = (int64_t)h->subs.size();
             if (out)
                 for (int64_t i = 0; i < std::min(n, cap); ++i) static_cast<int64_t*>(out)[i] = h->subs[i].tv;
+            return;
+        }
+        if (w == "mass_iters") {
+            n = 1;
+            if (out && cap >= 1) static_cast<int64_t*>(out)[0] = (int64_t)h->mass_iters;
             return;
         }
         throw ApiError(DDPCA_EINVAL, "unknown quantity " + w);
@@ -832,7 +1026,8 @@ int mcontact_gpu_timing(mcontact_t h, double* out10) {
     std::memcpy(out10, h->timing, sizeof(h->timing));
     if (h->timing[5] > 0) out10[7] = h->timing[7] / h->timing[5];  // bytes per timed launch
     double dofs = 0.0;
-    for (auto& S : h->subs) dofs += (double)S.mg->nfree;
+    if (h->mg)
+        for (int64_t nf : h->mg->nfree) dofs += (double)nf;
     out10[9] = dofs;
     return DDPCA_OK;
 }
@@ -845,9 +1040,10 @@ int mcontact_gpu_destroy(mcontact_t h) {
         if (h->comm) (void)ncclCommDestroy(h->comm);
         for (auto& e : h->ev)
             if (e) (void)hipEventDestroy(e);
-        h->subs.clear();
-        if (h->main) (void)hipStreamDestroy(h->main);
+        const bool own_stream = !h->mg && h->main;
+        hipStream_t st = h->main;
         delete h;
+        if (own_stream) (void)hipStreamDestroy(st);
     });
 }
 

@@ -1,12 +1,16 @@
-// MGPIS device path: SELL-BSR3 kernels, V-cycle and PCG for gfx950 (see device_mgpis.hpp).
+// MGPIS device path: SELL-BSR3 kernels, V-cycle and PCG for gfx950 over a batch of
+// subdomains (see device_mgpis.hpp for the layout).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
+#include <climits>
 #include <cmath>
 #include <cstring>
 #include <numeric>
 #include <omp.h>
 #include <random>
+#include <thread>
 
 #include "device_mgpis.hpp"
 
@@ -16,25 +20,24 @@ namespace ddpca {
 namespace {
 
 enum SellMode { kSpmv = 0, kResid = 1, kJac = 2, kPcg = 3, kCheb = 4 };
-enum FinWhat { kFinInit = 0, kFinBeta0 = 1, kFinAlpha = 2, kFinRR = 3, kFinBeta = 4 };
+enum FinWhat { kFinInit = 0, kFinBeta0 = 1, kFinAlpha = 2, kFinRR = 3, kFinBeta = 4, kFinInitWarm = 5 };
 
 struct SellArgs {
     const int32_t* slots;
     const int64_t* off;
     const int32_t* col;
-    const double* val;
-    int64_t nn, nch;
-    const double* x;   // gathered operand
-    double* y;         // SPMV / RESID output, PCG: q (in place)
-    const double* b;   // RESID / JAC / CHEB right-hand side
+    const void* val;       // double (Krylov operator) or float (fp32-stored V-cycle operator)
+    const int32_t* csub;   // chunk -> subdomain
+    int64_t nch;
+    const double* x;       // gathered operand
+    double* y;             // SPMV / RESID output, PCG: q (in place)
+    const double* b;       // RESID / JAC / CHEB right-hand side
     const double* minv;
-    double omega;
-    double* xo;        // JAC / CHEB new iterate
-    double* p;         // PCG: p (in place), CHEB: direction d (in place)
-    double c1, c2;     // CHEB coefficients
-    const PcgScal* sc;
-    double* partial;
-    const int* done;
+    const double* coef;    // per subdomain (c1, c2) of this sweep; JAC uses c2 = omega
+    double* xo;            // JAC / CHEB new iterate
+    double* p;             // PCG: p (in place), CHEB: direction d (in place)
+    const PcgScal* sc;     // per-subdomain stop flags / beta; nullptr = never stopped
+    double* partial;       // per chunk
 };
 
 __device__ __forceinline__ double wave_sum(double v) {
@@ -43,15 +46,13 @@ __device__ __forceinline__ double wave_sum(double v) {
     return v;
 }
 
-// Deterministic per-workgroup partial sum (4 waves of 64 lanes).
-__device__ __forceinline__ void block_partial(double v, double* partial) {
-    __shared__ double red[kBlock / kWave];
+// Chunk partial of a dot product: one wavefront = one 64-node chunk, fixed shuffle order.
+__device__ __forceinline__ void chunk_partial(double v, double* partial, int64_t chunk) {
     v = wave_sum(v);
-    const int w = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) red[w] = v;
-    __syncthreads();
-    if (threadIdx.x == 0) partial[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+    if ((threadIdx.x & 63) == 0) partial[chunk] = v;
 }
+
+__device__ __forceinline__ bool stopped(const PcgScal* sc, int sub) { return sc && sc[sub].done; }
 
 template <bool BJ>
 __device__ __forceinline__ void apply_m(const double* minv, int64_t row, double r0, double r1, double r2,
@@ -69,116 +70,191 @@ __device__ __forceinline__ void apply_m(const double* minv, int64_t row, double 
     }
 }
 
-// One wavefront per 64-node chunk, one lane per node row, three accumulators per lane.
-template <int MODE, bool BJ, bool DOT>
-__global__ __launch_bounds__(kBlock) void k_sell(SellArgs a) {
-    if (*a.done) return;
-    const int lane = threadIdx.x & 63;
-    const int64_t c = (int64_t)blockIdx.x * (kBlock / kWave) + (threadIdx.x >> 6);
-    double dotv = 0.0;
-    if (c < a.nch) {
-        const int64_t row = c * kChunk + lane;
-        const int ns = a.slots[c];
-        const int64_t base = a.off[c];
-        const int32_t* colp = a.col + base * kChunk + lane;
-        const double* valp = a.val + base * 9 * kChunk + lane;
-        double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+// 3x3 block (9 entries, one 512-B (fp64) / 256-B (fp32) wave load each) times x_j, accumulated
+// in fp64; the matrix is streamed once per launch, so its loads are non-temporal and leave the
+// caches to the x gathers.
+template <typename T>
+__device__ __forceinline__ void block_fma(const T* v, const double* xj, double& s0, double& s1, double& s2) {
+    const double x0 = xj[0], x1 = xj[1], x2 = xj[2];
+    auto ld = [&](int i) { return (double)__builtin_nontemporal_load(v + i * kChunk); };
+    s0 += ld(0) * x0 + ld(1) * x1 + ld(2) * x2;
+    s1 += ld(3) * x0 + ld(4) * x1 + ld(5) * x2;
+    s2 += ld(6) * x0 + ld(7) * x1 + ld(8) * x2;
+}
+
+// plain 3x3 block times x_j
+template <typename T>
+__device__ __forceinline__ void block_fma_plain(const T* v, const double* xj, double& s0, double& s1, double& s2) {
+    const double x0 = xj[0], x1 = xj[1], x2 = xj[2];
+    s0 += (double)v[0 * kChunk] * x0 + (double)v[1 * kChunk] * x1 + (double)v[2 * kChunk] * x2;
+    s1 += (double)v[3 * kChunk] * x0 + (double)v[4 * kChunk] * x1 + (double)v[5 * kChunk] * x2;
+    s2 += (double)v[6 * kChunk] * x0 + (double)v[7 * kChunk] * x1 + (double)v[8 * kChunk] * x2;
+}
+
+// Row sums of one chunk, loop variant V (the production kernels use default_variant; the others
+// are kept for mgpis_gpu_bench_spmv, which times them on a live operator):
+//   0  slot loop unrolled x3, cached loads
+//   1  as 0 with non-temporal matrix loads
+//   2  groups of 3 slots with the next group's columns prefetched, non-temporal matrix loads
+template <int V, typename T>
+__device__ __forceinline__ void sell_rows(const int32_t* colp, const T* valp, const double* x, int ns, int64_t row,
+                                          double& s0, double& s1, double& s2) {
+    if constexpr (V == 0) {
+#pragma unroll 3
+        for (int k = 0; k < ns; ++k)
+            block_fma_plain(valp + (int64_t)k * 9 * kChunk, x + 3 * (int64_t)colp[(int64_t)k * kChunk], s0, s1, s2);
+    } else if constexpr (V == 1) {
+#pragma unroll 3
+        for (int k = 0; k < ns; ++k)
+            block_fma(valp + (int64_t)k * 9 * kChunk, x + 3 * (int64_t)__builtin_nontemporal_load(colp + (int64_t)k * kChunk),
+                      s0, s1, s2);
+    } else if constexpr (V == 3) {
+        // diagnostic bound only (wrong product): as 1 but x gathered at the row's own node, i.e.
+        // perfectly coalesced gathers -- what a locality-optimal node numbering could approach
 #pragma unroll 3
         for (int k = 0; k < ns; ++k) {
-            const int64_t j = colp[(int64_t)k * kChunk];
-            const double* xj = a.x + 3 * j;
-            const double x0 = xj[0], x1 = xj[1], x2 = xj[2];
-            const double* v = valp + (int64_t)k * 9 * kChunk;
-            s0 += v[0 * kChunk] * x0 + v[1 * kChunk] * x1 + v[2 * kChunk] * x2;
-            s1 += v[3 * kChunk] * x0 + v[4 * kChunk] * x1 + v[5 * kChunk] * x2;
-            s2 += v[6 * kChunk] * x0 + v[7 * kChunk] * x1 + v[8 * kChunk] * x2;
+            const int32_t j = __builtin_nontemporal_load(colp + (int64_t)k * kChunk);
+            block_fma(valp + (int64_t)k * 9 * kChunk, x + 3 * (row + (j & 0)), s0, s1, s2);
         }
-        if (row < a.nn) {
-            const int64_t o = 3 * row;
-            if (MODE == kSpmv) {
-                a.y[o] = s0;
-                a.y[o + 1] = s1;
-                a.y[o + 2] = s2;
-            } else if (MODE == kResid) {
-                a.y[o] = a.b[o] - s0;
-                a.y[o + 1] = a.b[o + 1] - s1;
-                a.y[o + 2] = a.b[o + 2] - s2;
-            } else if (MODE == kJac) {
-                const double b0 = a.b[o], b1 = a.b[o + 1], b2 = a.b[o + 2];
-                double m0, m1, m2;
-                apply_m<BJ>(a.minv, row, b0 - s0, b1 - s1, b2 - s2, m0, m1, m2);
-                const double n0 = a.x[o] + a.omega * m0, n1 = a.x[o + 1] + a.omega * m1, n2 = a.x[o + 2] + a.omega * m2;
-                a.xo[o] = n0;
-                a.xo[o + 1] = n1;
-                a.xo[o + 2] = n2;
-                if (DOT) dotv = b0 * n0 + b1 * n1 + b2 * n2;
-            } else if (MODE == kPcg) {
-                // q = K z + beta q_old, p = z + beta p_old  (K p = K z + beta K p_old)
-                const double be = a.sc->beta;
-                const double q0 = s0 + be * a.y[o], q1 = s1 + be * a.y[o + 1], q2 = s2 + be * a.y[o + 2];
-                const double p0 = a.x[o] + be * a.p[o], p1 = a.x[o + 1] + be * a.p[o + 1], p2 = a.x[o + 2] + be * a.p[o + 2];
-                a.y[o] = q0;
-                a.y[o + 1] = q1;
-                a.y[o + 2] = q2;
-                a.p[o] = p0;
-                a.p[o + 1] = p1;
-                a.p[o + 2] = p2;
-                if (DOT) dotv = p0 * q0 + p1 * q1 + p2 * q2;
-            } else if (MODE == kCheb) {
-                const double b0 = a.b[o], b1 = a.b[o + 1], b2 = a.b[o + 2];
-                double m0, m1, m2;
-                apply_m<BJ>(a.minv, row, b0 - s0, b1 - s1, b2 - s2, m0, m1, m2);
-                const double d0 = a.c1 * a.p[o] + a.c2 * m0, d1 = a.c1 * a.p[o + 1] + a.c2 * m1,
-                             d2 = a.c1 * a.p[o + 2] + a.c2 * m2;
-                a.p[o] = d0;
-                a.p[o + 1] = d1;
-                a.p[o + 2] = d2;
-                const double n0 = a.x[o] + d0, n1 = a.x[o + 1] + d1, n2 = a.x[o + 2] + d2;
-                a.xo[o] = n0;
-                a.xo[o + 1] = n1;
-                a.xo[o + 2] = n2;
-                if (DOT) dotv = b0 * n0 + b1 * n1 + b2 * n2;
+    } else {
+        int k = 0;
+        int32_t c0 = 0, c1 = 0, c2 = 0;
+        if (ns >= 3) {
+            c0 = __builtin_nontemporal_load(colp);
+            c1 = __builtin_nontemporal_load(colp + kChunk);
+            c2 = __builtin_nontemporal_load(colp + 2 * kChunk);
+        }
+        for (; k + 3 <= ns; k += 3) {
+            const int64_t j0 = c0, j1 = c1, j2 = c2;
+            if (k + 6 <= ns) {
+                c0 = __builtin_nontemporal_load(colp + (int64_t)(k + 3) * kChunk);
+                c1 = __builtin_nontemporal_load(colp + (int64_t)(k + 4) * kChunk);
+                c2 = __builtin_nontemporal_load(colp + (int64_t)(k + 5) * kChunk);
             }
+            const T* v = valp + (int64_t)k * 9 * kChunk;
+            block_fma(v, x + 3 * j0, s0, s1, s2);
+            block_fma(v + 9 * kChunk, x + 3 * j1, s0, s1, s2);
+            block_fma(v + 18 * kChunk, x + 3 * j2, s0, s1, s2);
         }
+        for (; k < ns; ++k) block_fma(valp + (int64_t)k * 9 * kChunk, x + 3 * (int64_t)colp[(int64_t)k * kChunk], s0, s1, s2);
     }
-    if (DOT) block_partial(dotv, a.partial);
 }
+
+// Production loop variant per mode.  Measured on a 1.22M-dof fine level (mgpis_gpu_bench_spmv):
+// the column prefetch pays for the light-epilogue modes (y = Kx, residual), plain non-temporal
+// streaming for the PCG and Chebyshev epilogues; an XCD-contiguous chunk mapping (each XCD one
+// range of chunks) was 17 % slower than the dispatcher's round-robin and is gone.
+constexpr int default_variant(int mode) { return (mode == 0 || mode == 1) ? 2 : 1; }
+
+// One wavefront per 64-node chunk, one lane per node row, three accumulators per lane; T is the
+// storage type of the operator values (all arithmetic fp64).
+template <int MODE, bool BJ, bool DOT, typename T = double, int V = default_variant(MODE)>
+__global__ __launch_bounds__(kBlock) void k_sell(SellArgs a) {
+    const int lane = threadIdx.x & 63;
+    const int64_t c = (int64_t)blockIdx.x * (kBlock / kWave) + (threadIdx.x >> 6);
+    if (c >= a.nch) return;
+    const int sub = a.csub[c];
+    if (stopped(a.sc, sub)) return;
+    const int64_t row = c * kChunk + lane;
+    const int ns = a.slots[c];
+    const int64_t base = a.off[c];
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+    sell_rows<V>(a.col + base * kChunk + lane, static_cast<const T*>(a.val) + base * 9 * kChunk + lane, a.x, ns, row,
+                 s0, s1, s2);
+    double dotv = 0.0;
+    const int64_t o = 3 * row;
+    if (MODE == kSpmv) {
+        a.y[o] = s0;
+        a.y[o + 1] = s1;
+        a.y[o + 2] = s2;
+    } else if (MODE == kResid) {
+        const double r0 = a.b[o] - s0, r1 = a.b[o + 1] - s1, r2 = a.b[o + 2] - s2;
+        a.y[o] = r0;
+        a.y[o + 1] = r1;
+        a.y[o + 2] = r2;
+        if (DOT) dotv = r0 * r0 + r1 * r1 + r2 * r2;
+    } else if (MODE == kJac) {
+        const double om = a.coef[2 * sub + 1];
+        const double b0 = a.b[o], b1 = a.b[o + 1], b2 = a.b[o + 2];
+        double m0, m1, m2;
+        apply_m<BJ>(a.minv, row, b0 - s0, b1 - s1, b2 - s2, m0, m1, m2);
+        const double n0 = a.x[o] + om * m0, n1 = a.x[o + 1] + om * m1, n2 = a.x[o + 2] + om * m2;
+        a.xo[o] = n0;
+        a.xo[o + 1] = n1;
+        a.xo[o + 2] = n2;
+        if (DOT) dotv = b0 * n0 + b1 * n1 + b2 * n2;
+    } else if (MODE == kPcg) {
+        // q = K z + beta q_old, p = z + beta p_old  (K p = K z + beta K p_old)
+        const double be = a.sc[sub].beta;
+        const double q0 = s0 + be * a.y[o], q1 = s1 + be * a.y[o + 1], q2 = s2 + be * a.y[o + 2];
+        const double p0 = a.x[o] + be * a.p[o], p1 = a.x[o + 1] + be * a.p[o + 1], p2 = a.x[o + 2] + be * a.p[o + 2];
+        a.y[o] = q0;
+        a.y[o + 1] = q1;
+        a.y[o + 2] = q2;
+        a.p[o] = p0;
+        a.p[o + 1] = p1;
+        a.p[o + 2] = p2;
+        if (DOT) dotv = p0 * q0 + p1 * q1 + p2 * q2;
+    } else if (MODE == kCheb) {
+        const double c1 = a.coef[2 * sub], c2 = a.coef[2 * sub + 1];
+        const double b0 = a.b[o], b1 = a.b[o + 1], b2 = a.b[o + 2];
+        double m0, m1, m2;
+        apply_m<BJ>(a.minv, row, b0 - s0, b1 - s1, b2 - s2, m0, m1, m2);
+        const double d0 = c1 * a.p[o] + c2 * m0, d1 = c1 * a.p[o + 1] + c2 * m1, d2 = c1 * a.p[o + 2] + c2 * m2;
+        a.p[o] = d0;
+        a.p[o + 1] = d1;
+        a.p[o + 2] = d2;
+        const double n0 = a.x[o] + d0, n1 = a.x[o + 1] + d1, n2 = a.x[o + 2] + d2;
+        a.xo[o] = n0;
+        a.xo[o + 1] = n1;
+        a.xo[o + 2] = n2;
+        if (DOT) dotv = b0 * n0 + b1 * n1 + b2 * n2;
+    }
+    if (DOT) chunk_partial(dotv, a.partial, c);
+}
+
+// Node-parallel kernels: thread = node, 256 nodes per workgroup; a wavefront is one chunk, so
+// the subdomain (and its stop flag) is uniform per wavefront.  nn is a multiple of 64.
+#define NODE_PROLOGUE(nn, csub, sc)                         \
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; \
+    if (i >= (nn)) return;                                  \
+    const int sub = (csub)[i >> 6];                         \
+    if (stopped((sc), sub)) return;
 
 // x = omega M b  (first smoothing sweep from a zero guess); CHEB: also d = x
 template <bool BJ, bool SETD>
-__global__ __launch_bounds__(kBlock) void k_jac0(const double* b, const double* minv, double omega, double* x,
-                                                 double* d, int64_t nn, const int* done) {
-    if (*done) return;
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= nn) return;
+__global__ __launch_bounds__(kBlock) void k_jac0(const double* b, const double* minv, const double* coef, double* x,
+                                                 double* d, int64_t nn, const int32_t* csub, const PcgScal* sc) {
+    NODE_PROLOGUE(nn, csub, sc)
+    const double om = coef[2 * sub + 1];
     double m0, m1, m2;
     apply_m<BJ>(minv, i, b[3 * i], b[3 * i + 1], b[3 * i + 2], m0, m1, m2);
-    x[3 * i] = omega * m0;
-    x[3 * i + 1] = omega * m1;
-    x[3 * i + 2] = omega * m2;
+    x[3 * i] = om * m0;
+    x[3 * i + 1] = om * m1;
+    x[3 * i + 2] = om * m2;
     if (SETD) {
-        d[3 * i] = omega * m0;
-        d[3 * i + 1] = omega * m1;
-        d[3 * i + 2] = omega * m2;
+        d[3 * i] = om * m0;
+        d[3 * i + 1] = om * m1;
+        d[3 * i + 2] = om * m2;
     }
 }
 
-// b_c = mask_c (r_f[j] + sum_children w r_f[child]); optionally x_c = omega M b_c (CHEB: d_c too)
+// b_c = mask_c (sum_children w r_f[child]), the coarse node's own fine copy first with w = 1;
+// optionally x_c = omega M b_c (CHEB: d_c too)
 template <bool INIT, bool BJ, bool SETD>
 __global__ __launch_bounds__(kBlock) void k_restrict(const double* rf, const int64_t* rptr, const int32_t* rch,
                                                      const double* rw, const uint8_t* cmask, double* bc, double* xc,
-                                                     double* dc, const double* minv, double omega, int64_t nc,
-                                                     const int* done) {
-    if (*done) return;
-    const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (j >= nc) return;
-    double s0 = rf[3 * j], s1 = rf[3 * j + 1], s2 = rf[3 * j + 2];
+                                                     double* dc, const double* minv, const double* coef, int64_t nc,
+                                                     const int32_t* csub, const PcgScal* sc) {
+    NODE_PROLOGUE(nc, csub, sc)
+    const int64_t j = i;
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0;
     for (int64_t k = rptr[j]; k < rptr[j + 1]; ++k) {
-        const int64_t i = rch[k];
+        const int64_t f = rch[k];
         const double w = rw[k];
-        s0 += w * rf[3 * i];
-        s1 += w * rf[3 * i + 1];
-        s2 += w * rf[3 * i + 2];
+        s0 += w * rf[3 * f];
+        s1 += w * rf[3 * f + 1];
+        s2 += w * rf[3 * f + 2];
     }
     const uint8_t m = cmask[j];
     s0 = (m & 1) ? s0 : 0.0;
@@ -188,43 +264,34 @@ __global__ __launch_bounds__(kBlock) void k_restrict(const double* rf, const int
     bc[3 * j + 1] = s1;
     bc[3 * j + 2] = s2;
     if (INIT) {
+        const double om = coef[2 * sub + 1];
         double m0, m1, m2;
         apply_m<BJ>(minv, j, s0, s1, s2, m0, m1, m2);
-        xc[3 * j] = omega * m0;
-        xc[3 * j + 1] = omega * m1;
-        xc[3 * j + 2] = omega * m2;
+        xc[3 * j] = om * m0;
+        xc[3 * j + 1] = om * m1;
+        xc[3 * j + 2] = om * m2;
         if (SETD) {
-            dc[3 * j] = omega * m0;
-            dc[3 * j + 1] = omega * m1;
-            dc[3 * j + 2] = omega * m2;
+            dc[3 * j] = om * m0;
+            dc[3 * j + 1] = om * m1;
+            dc[3 * j + 2] = om * m2;
         }
     }
 }
 
 // x_f += mask_f (P e_c)
 __global__ __launch_bounds__(kBlock) void k_prolong(const double* ec, const int32_t* ppar, const double* pw,
-                                                    const uint8_t* fmask, double* xf, int64_t nf, int64_t nc,
-                                                    const int* done) {
-    if (*done) return;
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= nf) return;
-    double e0, e1, e2;
-    if (i < nc) {
-        e0 = ec[3 * i];
-        e1 = ec[3 * i + 1];
-        e2 = ec[3 * i + 2];
-    } else {
-        e0 = e1 = e2 = 0.0;
-        const int64_t k = i - nc, stride = nf - nc;
+                                                    const uint8_t* fmask, double* xf, int64_t nf, const int32_t* csub,
+                                                    const PcgScal* sc) {
+    NODE_PROLOGUE(nf, csub, sc)
+    double e0 = 0.0, e1 = 0.0, e2 = 0.0;
 #pragma unroll
-        for (int p = 0; p < 8; ++p) {
-            const int32_t c = ppar[p * stride + k];
-            if (c < 0) break;
-            const double w = pw[p * stride + k];
-            e0 += w * ec[3 * (int64_t)c];
-            e1 += w * ec[3 * (int64_t)c + 1];
-            e2 += w * ec[3 * (int64_t)c + 2];
-        }
+    for (int p = 0; p < 8; ++p) {
+        const int32_t c = ppar[p * nf + i];
+        if (c < 0) break;
+        const double w = pw[p * nf + i];
+        e0 += w * ec[3 * (int64_t)c];
+        e1 += w * ec[3 * (int64_t)c + 1];
+        e2 += w * ec[3 * (int64_t)c + 2];
     }
     const uint8_t m = fmask[i];
     if (m & 1) xf[3 * i] += e0;
@@ -232,98 +299,132 @@ __global__ __launch_bounds__(kBlock) void k_prolong(const double* ec, const int3
     if (m & 4) xf[3 * i + 2] += e2;
 }
 
-// x0 = A0^-1 b0, one wavefront per row
-__global__ __launch_bounds__(kBlock) void k_coarse(const double* ainv, const double* b, double* x, int64_t n,
-                                                   const int* done) {
-    if (*done) return;
-    const int64_t row = (int64_t)blockIdx.x * (kBlock / kWave) + (threadIdx.x >> 6);
-    if (row >= n) return;
+// x0 = A0^-1 b0 per subdomain, one wavefront per coarse dof row
+__global__ __launch_bounds__(kBlock) void k_coarse(const double* ainv, const int64_t* aoff, const int64_t* noff,
+                                                   const int64_t* n0, const double* b, double* x, int64_t nrow,
+                                                   const int32_t* csub, const PcgScal* sc) {
+    const int64_t r = (int64_t)blockIdx.x * (kBlock / kWave) + (threadIdx.x >> 6);
+    if (r >= nrow) return;
+    const int sub = csub[(r / 3) >> 6];
+    if (stopped(sc, sub)) return;
     const int lane = threadIdx.x & 63;
+    const int64_t lr = r - 3 * noff[sub], n = n0[sub];
+    if (lr >= n) {
+        if (lane == 0) x[r] = 0.0;
+        return;
+    }
+    const double* arow = ainv + aoff[sub] + lr * n;
+    const double* bs = b + 3 * noff[sub];
     double s = 0.0;
-    for (int64_t k = lane; k < n; k += kWave) s += ainv[row * n + k] * b[k];
+    for (int64_t k = lane; k < n; k += kWave) s += arow[k] * bs[k];
     s = wave_sum(s);
-    if (lane == 0) x[row] = s;
+    if (lane == 0) x[r] = s;
 }
 
-// r = b, x = p = q = 0, partial ||b||^2  (per node, 256 nodes per workgroup)
+// r = b, x = p = q = 0, partial ||b||^2 per chunk
 __global__ __launch_bounds__(kBlock) void k_pcg_init(const double* b, double* x, double* r, double* p, double* q,
                                                      double* partial, int64_t nn) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= nn) return;
     double s = 0.0;
-    if (i < nn)
-        for (int a = 0; a < 3; ++a) {
-            const double v = b[3 * i + a];
-            r[3 * i + a] = v;
-            x[3 * i + a] = 0.0;
-            p[3 * i + a] = 0.0;
-            q[3 * i + a] = 0.0;
-            s += v * v;
-        }
-    block_partial(s, partial);
+    for (int a = 0; a < 3; ++a) {
+        const double v = b[3 * i + a];
+        r[3 * i + a] = v;
+        x[3 * i + a] = 0.0;
+        p[3 * i + a] = 0.0;
+        q[3 * i + a] = 0.0;
+        s += v * v;
+    }
+    chunk_partial(s, partial, i >> 6);
+}
+
+// warm start: p = q = 0, partial ||b||^2 per chunk (r = b - K x0 by k_sell<kResid>)
+__global__ __launch_bounds__(kBlock) void k_pcg_init_warm(const double* b, double* p, double* q, double* partial,
+                                                          int64_t nn) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= nn) return;
+    double s = 0.0;
+    for (int a = 0; a < 3; ++a) {
+        const double v = b[3 * i + a];
+        p[3 * i + a] = 0.0;
+        q[3 * i + a] = 0.0;
+        s += v * v;
+    }
+    chunk_partial(s, partial, i >> 6);
 }
 
 // x += alpha p, r -= alpha q, partial ||r||^2
 __global__ __launch_bounds__(kBlock) void k_axpy(double* x, double* r, const double* p, const double* q,
-                                                 const PcgScal* sc, double* partial, int64_t nn, const int* done) {
-    if (*done) return;
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    const double al = sc->alpha;
+                                                 const PcgScal* sc, double* partial, int64_t nn, const int32_t* csub) {
+    NODE_PROLOGUE(nn, csub, sc)
+    const double al = sc[sub].alpha;
     double s = 0.0;
-    if (i < nn)
-        for (int a = 0; a < 3; ++a) {
-            x[3 * i + a] += al * p[3 * i + a];
-            const double v = r[3 * i + a] - al * q[3 * i + a];
-            r[3 * i + a] = v;
-            s += v * v;
-        }
-    block_partial(s, partial);
+    for (int a = 0; a < 3; ++a) {
+        x[3 * i + a] += al * p[3 * i + a];
+        const double v = r[3 * i + a] - al * q[3 * i + a];
+        r[3 * i + a] = v;
+        s += v * v;
+    }
+    chunk_partial(s, partial, i >> 6);
 }
 
 // z = D^-1 r (diagonal preconditioner, DIAG_PREC), partial r^T z
 __global__ __launch_bounds__(kBlock) void k_diag(const double* r, const double* dinv, double* z, double* partial,
-                                                 int64_t nn, const int* done) {
-    if (*done) return;
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+                                                 int64_t nn, const int32_t* csub, const PcgScal* sc) {
+    NODE_PROLOGUE(nn, csub, sc)
     double s = 0.0;
-    if (i < nn)
-        for (int a = 0; a < 3; ++a) {
-            const double v = dinv[3 * i + a] * r[3 * i + a];
-            z[3 * i + a] = v;
-            s += r[3 * i + a] * v;
-        }
-    block_partial(s, partial);
+    for (int a = 0; a < 3; ++a) {
+        const double v = dinv[3 * i + a] * r[3 * i + a];
+        z[3 * i + a] = v;
+        s += r[3 * i + a] * v;
+    }
+    chunk_partial(s, partial, i >> 6);
 }
 
-// partial x^T y per node block (used after a coarse-only "V-cycle")
+// partial x^T y per chunk (used after a coarse-only "V-cycle")
 __global__ __launch_bounds__(kBlock) void k_dot(const double* x, const double* y, double* partial, int64_t nn,
-                                                const int* done) {
-    if (*done) return;
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+                                                const int32_t* csub, const PcgScal* sc) {
+    NODE_PROLOGUE(nn, csub, sc)
     double s = 0.0;
-    if (i < nn)
-        for (int a = 0; a < 3; ++a) s += x[3 * i + a] * y[3 * i + a];
-    block_partial(s, partial);
+    for (int a = 0; a < 3; ++a) s += x[3 * i + a] * y[3 * i + a];
+    chunk_partial(s, partial, i >> 6);
 }
 
-// Scalar updates of the PCG recurrence (one workgroup, fixed summation order).
-__global__ __launch_bounds__(kBlock) void k_fin(int what, const double* partial, int64_t nblk, PcgScal* sc) {
-    if (what != kFinInit && sc->done) return;
-    double s = 0.0;
-    for (int64_t k = threadIdx.x; k < nblk; k += kBlock) s += partial[k];
-    __shared__ double red[kBlock / kWave];
+// Scalar updates of the PCG recurrence: one workgroup per subdomain, fixed summation order
+// over that subdomain's chunk partials.  Stop-state changes are mirrored to host memory.
+__global__ __launch_bounds__(kBlock) void k_fin(int what, const double* partial, const double* partial2,
+                                                const int64_t* cb, PcgScal* scv, PcgMirror* mirror) {
+    const int sub = blockIdx.x;
+    PcgScal* sc = scv + sub;
+    if (what != kFinInit && what != kFinInitWarm && sc->done) return;
+    __shared__ double red[kBlock / kWave], red2[kBlock / kWave];
+    double s = 0.0, s2 = 0.0;
+    for (int64_t k = cb[sub] + threadIdx.x; k < cb[sub + 1]; k += kBlock) {
+        s += partial[k];
+        if (what == kFinInitWarm) s2 += partial2[k];
+    }
     s = wave_sum(s);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    s2 = wave_sum(s2);
+    if ((threadIdx.x & 63) == 0) {
+        red[threadIdx.x >> 6] = s;
+        red2[threadIdx.x >> 6] = s2;
+    }
     __syncthreads();
     if (threadIdx.x != 0) return;
     s = (red[0] + red[1]) + (red[2] + red[3]);
-    if (what == kFinInit) {
+    s2 = (red2[0] + red2[1]) + (red2[2] + red2[3]);
+    const int was_done = sc->done;
+    if (what == kFinInit || what == kFinInitWarm) {
+        const double bb = what == kFinInit ? s : s2;
         sc->rr = s;
-        sc->bb = s;
-        sc->tol2 = sc->tol2 * s;  // tol2 holds rtol^2 on entry
+        sc->bb = bb;
+        sc->tol2 = sc->tol2 * bb;  // tol2 holds rtol^2 on entry
         sc->iter = 0;
         sc->fail = 0;
         sc->beta = 0.0;
         sc->done = (s <= sc->tol2 || sc->maxit <= 0) ? 1 : 0;
+        mirror_store(mirror + sub, 0, sc->done, 0);
+        return;
     } else if (what == kFinBeta0) {
         sc->delta = s;
         sc->beta = 0.0;
@@ -342,6 +443,8 @@ __global__ __launch_bounds__(kBlock) void k_fin(int what, const double* partial,
             sc->done = 1;
         }
         if (s <= sc->tol2 || sc->iter >= sc->maxit) sc->done = 1;
+        mirror_store(mirror + sub, sc->iter, sc->done, sc->fail);
+        return;
     } else {
         if (!isfinite(s)) {
             sc->fail = 1;
@@ -350,6 +453,7 @@ __global__ __launch_bounds__(kBlock) void k_fin(int what, const double* partial,
         sc->beta = s / sc->delta;
         sc->delta = s;
     }
+    if (sc->done != was_done) mirror_store(mirror + sub, sc->iter, sc->done, sc->fail);
 }
 
 // full[free_dof[i]] = cond[i] (full zero-filled first) / cond[i] = full[free_dof[i]]
@@ -362,29 +466,25 @@ __global__ void k_gather(const double* full, const int32_t* free_dof, double* co
     if (i < n) cond[i] = full[free_dof[i]];
 }
 
-// y = M x, partial ||y||^2 (power iteration for lambda_max(M K) at setup)
+// y = M x, partial ||y||^2 per chunk (power iteration for lambda_max(M K) at setup)
 template <bool BJ>
 __global__ void k_apply_m(const double* x, const double* minv, double* y, double* partial, int64_t nn) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    double s = 0.0;
-    if (i < nn) {
-        double m0, m1, m2;
-        apply_m<BJ>(minv, i, x[3 * i], x[3 * i + 1], x[3 * i + 2], m0, m1, m2);
-        y[3 * i] = m0;
-        y[3 * i + 1] = m1;
-        y[3 * i + 2] = m2;
-        s = m0 * m0 + m1 * m1 + m2 * m2;
-    }
-    block_partial(s, partial);
+    if (i >= nn) return;
+    double m0, m1, m2;
+    apply_m<BJ>(minv, i, x[3 * i], x[3 * i + 1], x[3 * i + 2], m0, m1, m2);
+    y[3 * i] = m0;
+    y[3 * i + 1] = m1;
+    y[3 * i + 2] = m2;
+    chunk_partial(m0 * m0 + m1 * m1 + m2 * m2, partial, i >> 6);
 }
 
-const int* zero_flag() {
-    static int* z = nullptr;
-    if (!z) {
-        DDPCA_HIP(hipMalloc(&z, sizeof(int)));
-        DDPCA_HIP(hipMemset(z, 0, sizeof(int)));
-    }
-    return z;
+// v = w * scale[subdomain]
+__global__ void k_scale_sub(const double* w, const double* scale, double* v, int64_t nn, const int32_t* csub) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= nn) return;
+    const double s = scale[csub[i >> 6]];
+    for (int a = 0; a < 3; ++a) v[3 * i + a] = w[3 * i + a] * s;
 }
 
 // ---- host helpers
@@ -443,10 +543,64 @@ bool invert3(const double m[9], double r[9]) {
     return true;
 }
 
+// Device node order of one level: lexicographic in (z, y, x), coordinates quantised to 1e-9 of
+// the bounding box so nodes of one mesh plane share a key despite rounding in their coordinates.
+// Returns p[reference node] = device node.
+std::vector<int32_t> lex_order(const double* xyz, int64_t n) {
+    double lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0};
+    for (int64_t i = 0; i < n; ++i)
+        for (int a = 0; a < 3; ++a) {
+            lo[a] = i ? std::min(lo[a], xyz[3 * i + a]) : xyz[3 * i + a];
+            hi[a] = i ? std::max(hi[a], xyz[3 * i + a]) : xyz[3 * i + a];
+        }
+    const double ext = std::max({hi[0] - lo[0], hi[1] - lo[1], hi[2] - lo[2]});
+    const double q = ext > 0.0 ? 1e-9 * ext : 1.0;
+    std::vector<std::array<int64_t, 3>> key(n);
+    for (int64_t i = 0; i < n; ++i)
+        key[i] = {std::llround((xyz[3 * i + 2] - lo[2]) / q), std::llround((xyz[3 * i + 1] - lo[1]) / q),
+                  std::llround((xyz[3 * i] - lo[0]) / q)};
+    std::vector<int32_t> idx(n), p(n);
+    std::iota(idx.begin(), idx.end(), 0);
+    std::stable_sort(idx.begin(), idx.end(), [&](int32_t a, int32_t b) { return key[a] < key[b]; });
+    for (int64_t k = 0; k < n; ++k) p[idx[k]] = (int32_t)k;
+    return p;
+}
+
+constexpr int64_t kMaxRowBlocks = 128;  // node-block row length bound of the setup sort
+
+std::vector<int32_t> identity_order(int64_t n) {
+    std::vector<int32_t> p(n);
+    std::iota(p.begin(), p.end(), 0);
+    return p;
+}
+
+// Chebyshev coefficients of sweep k on [lmax/30, lmax] of M K (k = 0: the 1/theta start)
+void cheb_coef(double lmax, int k, double& c1, double& c2) {
+    const double lmin = lmax / 30.0;
+    const double theta = 0.5 * (lmax + lmin), delta = 0.5 * (lmax - lmin), sigma = theta / delta;
+    if (k == 0) {
+        c1 = 0.0;
+        c2 = 1.0 / theta;
+        return;
+    }
+    double rho_old = 1.0 / sigma, rho = rho_old;
+    for (int i = 1; i <= k; ++i) {
+        rho = 1.0 / (2.0 * sigma - rho_old);
+        if (i < k) rho_old = rho;
+    }
+    c1 = rho * rho_old;
+    c2 = 2.0 * rho / delta;
+}
+
 }  // namespace
 
-// ============================================================================== setup
+// ============================================================================== host plumbing
 void select_device(int device) {
+    static thread_local int checked = -1;  // last device verified to be a gfx950 part
+    if (device == checked) {
+        DDPCA_HIP(hipSetDevice(device));
+        return;
+    }
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n == 0) throw ApiError(DDPCA_ENOGPU, "no HIP device visible");
     if (device < 0 || device >= n) throw ApiError(DDPCA_EINVAL, "device index out of range");
@@ -455,119 +609,225 @@ void select_device(int device) {
     DDPCA_HIP(hipGetDeviceProperties(&prop, device));
     if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
         throw ApiError(DDPCA_ENOGPU, std::string("device is ") + prop.gcnArchName + ", kernels are built for gfx950");
+    checked = device;
 }
 
-MgpisDevice::MgpisDevice(int dev, const std::vector<int64_t>& nnodes, const std::vector<const Bsr3*>& K,
-                         const std::vector<uint8_t>& dof_free, const std::vector<const Stencil*>& S,
-                         const mgpis_options_t& o)
+void MirrorBuf::alloc(int count) {
+    n = count;
+    DDPCA_HIP(hipHostMalloc(reinterpret_cast<void**>(&host), std::max(1, count) * sizeof(PcgMirror),
+                            hipHostMallocMapped | hipHostMallocCoherent));
+    DDPCA_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&dev), host, 0));
+    reset();
+}
+
+void MirrorBuf::reset() { std::memset(host, 0, std::max(1, n) * sizeof(PcgMirror)); }
+
+MirrorBuf::~MirrorBuf() {
+    if (host) (void)hipHostFree(host);
+}
+
+int64_t pace_until_done(hipStream_t stream, hipGraphExec_t graph, const MirrorBuf& m, int64_t k, int64_t launched) {
+    int64_t replays = 0;
+    for (int64_t spin = 0;; ++spin) {
+        bool all = true;
+        int64_t slowest = INT64_MAX;
+        for (int s = 0; s < m.n; ++s) {
+            if (__atomic_load_n(&m.host[s].done, __ATOMIC_ACQUIRE)) continue;
+            all = false;
+            slowest = std::min<int64_t>(slowest, __atomic_load_n(&m.host[s].iter, __ATOMIC_RELAXED));
+        }
+        if (all) return replays;
+        // keep one replay of runway: launch when the slowest solve has entered the last one
+        if (launched - slowest <= k) {
+            DDPCA_HIP(hipGraphLaunch(graph, stream));
+            launched += k;
+            ++replays;
+            continue;
+        }
+        if ((spin & 255) == 255) {
+            const hipError_t q = hipStreamQuery(stream);
+            if (q == hipSuccess) {
+                // stream drained: the mirror is final for everything enqueued so far
+                bool done_now = true;
+                for (int s = 0; s < m.n; ++s) done_now &= __atomic_load_n(&m.host[s].done, __ATOMIC_ACQUIRE) != 0;
+                if (done_now) return replays;
+                DDPCA_HIP(hipGraphLaunch(graph, stream));
+                launched += k;
+                ++replays;
+            } else if (q != hipErrorNotReady) {
+                DDPCA_HIP(q);
+            }
+        }
+        std::this_thread::yield();
+    }
+}
+
+// ============================================================================== setup
+MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const mgpis_options_t& o)
     : device(dev), opt(o) {
     select_device(device);
+    nsub = (int)subs.size();
+    if (nsub < 1) throw ApiError(DDPCA_EINVAL, "empty subdomain batch");
+    const int nlev = (int)subs[0].nnodes.size();
+    for (const auto& S : subs) {
+        if ((int)S.nnodes.size() != nlev || nlev < 1 || (int)S.K.size() != nlev || (int)S.S.size() != nlev - 1)
+            throw ApiError(DDPCA_EINVAL, "level counts differ within the batch");
+        if (!S.dof_free) throw ApiError(DDPCA_EINVAL, "dof_free missing");
+        for (int l = 0; l < nlev; ++l)
+            if (S.K[l]->nb != S.nnodes[l] || S.K[l]->mb != S.nnodes[l]) throw ApiError(DDPCA_EINVAL, "operator size does not match nnodes");
+    }
     DDPCA_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
-    const int nlev = (int)nnodes.size();
-    if (nlev < 1 || (int)K.size() != nlev || (int)S.size() != nlev - 1) throw ApiError(DDPCA_EINVAL, "level counts");
-    if ((int64_t)dof_free.size() != 3 * nnodes.back()) throw ApiError(DDPCA_EINVAL, "dof_free length");
     if (opt.nu < 1) opt.nu = 1;
     if (opt.iters_per_graph < 1) opt.iters_per_graph = 1;
     const bool bj = opt.smoother >= 1;
+    // device numbering: perm[l][s][reference local node] = device local node
+    std::vector<std::vector<std::vector<int32_t>>> perm(nlev, std::vector<std::vector<int32_t>>(nsub));
+    for (int l = 0; l < nlev; ++l)
+        for (int s = 0; s < nsub; ++s) perm[l][s] = (l > 0 && subs[s].coords) ? lex_order(subs[s].coords, subs[s].nnodes[l])
+                                                                              : identity_order(subs[s].nnodes[l]);
     lev.resize(nlev);
     for (int l = 0; l < nlev; ++l) {
         LevelDev& L = lev[l];
-        const Bsr3& A = *K[l];
-        const int64_t nn = nnodes[l];
-        if (A.nb != nn || A.mb != nn) throw ApiError(DDPCA_EINVAL, "operator size does not match nnodes");
-        L.nn = nn;
-        L.nch = (nn + kChunk - 1) / kChunk;
-        L.nnzb = A.nnzb();
-        auto fr = [&](int64_t dof) { return dof_free[dof] != 0; };
-        std::vector<int32_t> slots(L.nch);
-        std::vector<int64_t> off(L.nch + 1, 0);
-        for (int64_t c = 0; c < L.nch; ++c) {
-            int64_t mx = 0;
-            for (int64_t r = c * kChunk; r < std::min(nn, (c + 1) * kChunk); ++r) mx = std::max(mx, A.ptr[r + 1] - A.ptr[r]);
-            slots[c] = (int32_t)mx;
-            off[c + 1] = off[c] + mx;
+        L.noff.resize(nsub);
+        L.nloc.resize(nsub);
+        int64_t tot = 0;
+        for (int s = 0; s < nsub; ++s) {
+            L.noff[s] = tot;
+            L.nloc[s] = subs[s].nnodes[l];
+            tot += pad64(L.nloc[s]);
         }
+        L.nn = tot;
+        L.nch = tot / kChunk;
+        std::vector<int32_t> slots(L.nch, 0), csub(L.nch, 0);
+        std::vector<int64_t> off(L.nch + 1, 0);
+        for (int s = 0; s < nsub; ++s) {
+            const Bsr3& A = *subs[s].K[l];
+            const auto& p = perm[l][s];
+            const int64_t c0 = L.noff[s] / kChunk;
+            for (int64_t c = c0; c < c0 + pad64(L.nloc[s]) / kChunk; ++c) csub[c] = s;
+            for (int64_t r = 0; r < L.nloc[s]; ++r) {
+                int32_t& sl = slots[c0 + p[r] / kChunk];
+                sl = std::max<int32_t>(sl, (int32_t)(A.ptr[r + 1] - A.ptr[r]));
+                if (A.ptr[r + 1] - A.ptr[r] > kMaxRowBlocks) throw ApiError(DDPCA_EINVAL, "too many blocks in an operator row");
+            }
+            L.nnzb += A.nnzb();
+            L.nnzb_sub.push_back(A.nnzb());
+        }
+        for (int64_t c = 0; c < L.nch; ++c) off[c + 1] = off[c] + slots[c];
         L.nslots = off[L.nch];
         std::vector<int32_t> col(L.nslots * kChunk, 0);
         std::vector<double> val(L.nslots * kChunk * 9, 0.0);
-        std::vector<double> dinv(3 * nn, 0.0), minv(bj ? 9 * nn : 3 * nn, 0.0);
-        std::vector<uint8_t> mask(nn, 0);
-#pragma omp parallel for schedule(static)
-        for (int64_t r = 0; r < nn; ++r) {
-            const int64_t c = r / kChunk, lane = r % kChunk;
-            uint8_t m = 0;
-            for (int a = 0; a < 3; ++a) m |= fr(3 * r + a) ? (1 << a) : 0;
-            mask[r] = m;
-            double diag[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-            for (int64_t k = A.ptr[r]; k < A.ptr[r + 1]; ++k) {
-                const int64_t s = off[c] + (k - A.ptr[r]);
-                const int64_t j = A.col[k];
-                col[s * kChunk + lane] = (int32_t)j;
-                for (int a = 0; a < 3; ++a)
-                    for (int b = 0; b < 3; ++b) {
-                        double v = A.val[9 * k + 3 * a + b];
-                        if (!fr(3 * r + a) || !fr(3 * j + b)) v = (j == r && a == b) ? 1.0 : 0.0;
-                        val[(s * 9 + 3 * a + b) * kChunk + lane] = v;
-                        if (j == r) diag[3 * a + b] = v;
-                    }
+        std::vector<double> dinv(3 * L.nn, 0.0), minv(bj ? 9 * L.nn : 3 * L.nn, 0.0);
+        std::vector<uint8_t> mask(L.nn, 0);
+        for (int s = 0; s < nsub; ++s) {
+            const Bsr3& A = *subs[s].K[l];
+            const uint8_t* fr = subs[s].dof_free;  // reference order: level-l nodes are a prefix
+            const auto& p = perm[l][s];
+            const int64_t base = L.noff[s];
+            // padded rows of the subdomain: self column, zero values
+            for (int64_t r = L.nloc[s]; r < pad64(L.nloc[s]); ++r) {
+                const int64_t g = base + r, c = g / kChunk, lane = g % kChunk;
+                for (int64_t q = off[c]; q < off[c + 1]; ++q) col[q * kChunk + lane] = (int32_t)g;
             }
-            for (int64_t s = off[c] + (A.ptr[r + 1] - A.ptr[r]); s < off[c + 1]; ++s) col[s * kChunk + lane] = (int32_t)r;
-            for (int a = 0; a < 3; ++a) dinv[3 * r + a] = fr(3 * r + a) ? 1.0 / diag[4 * a] : 0.0;
-            if (bj) {
-                double inv[9];
-                if (!invert3(diag, inv)) for (int q = 0; q < 9; ++q) inv[q] = 0.0;
-                for (int a = 0; a < 3; ++a)
-                    for (int b = 0; b < 3; ++b) minv[9 * r + 3 * a + b] = (fr(3 * r + a) && fr(3 * r + b)) ? inv[3 * a + b] : 0.0;
-            } else {
-                for (int a = 0; a < 3; ++a) minv[3 * r + a] = dinv[3 * r + a];
+#pragma omp parallel for schedule(static)
+            for (int64_t r = 0; r < L.nloc[s]; ++r) {
+                const int64_t g = base + p[r], c = g / kChunk, lane = g % kChunk;
+                uint8_t m = 0;
+                for (int a = 0; a < 3; ++a) m |= fr[3 * r + a] ? (1 << a) : 0;
+                mask[g] = m;
+                // this row's blocks in increasing device column
+                int64_t ord[kMaxRowBlocks];
+                const int64_t len = A.ptr[r + 1] - A.ptr[r];
+                for (int64_t t = 0; t < len; ++t) ord[t] = A.ptr[r] + t;
+                std::sort(ord, ord + len, [&](int64_t u, int64_t v) { return p[A.col[u]] < p[A.col[v]]; });
+                double diag[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+                for (int64_t t = 0; t < len; ++t) {
+                    const int64_t k = ord[t], q = off[c] + t;
+                    const int64_t j = A.col[k];
+                    col[q * kChunk + lane] = (int32_t)(base + p[j]);
+                    for (int a = 0; a < 3; ++a)
+                        for (int b = 0; b < 3; ++b) {
+                            double v = A.val[9 * k + 3 * a + b];
+                            if (!fr[3 * r + a] || !fr[3 * j + b]) v = (j == r && a == b) ? 1.0 : 0.0;
+                            val[(q * 9 + 3 * a + b) * kChunk + lane] = v;
+                            if (j == r) diag[3 * a + b] = v;
+                        }
+                }
+                for (int64_t q = off[c] + len; q < off[c + 1]; ++q) col[q * kChunk + lane] = (int32_t)g;
+                for (int a = 0; a < 3; ++a) dinv[3 * g + a] = fr[3 * r + a] ? 1.0 / diag[4 * a] : 0.0;
+                if (bj) {
+                    double inv[9];
+                    if (!invert3(diag, inv)) for (int q = 0; q < 9; ++q) inv[q] = 0.0;
+                    for (int a = 0; a < 3; ++a)
+                        for (int b = 0; b < 3; ++b)
+                            minv[9 * g + 3 * a + b] = (fr[3 * r + a] && fr[3 * r + b]) ? inv[3 * a + b] : 0.0;
+                } else {
+                    for (int a = 0; a < 3; ++a) minv[3 * g + a] = dinv[3 * g + a];
+                }
             }
         }
-        // padding lanes of the last chunk point at node 0 with zero values
         L.slots.upload(slots);
+        L.csub.upload(csub);
         L.off.upload(off);
         L.col.upload(col);
-        L.val.upload(val);
+        // fp64 values: the fine level (Krylov operator) and, without the fp32 preconditioner
+        // copy, every level; the fp32 copy serves the V-cycle on levels >= 1 (level 0 is the
+        // dense inverse)
+        const bool vc32 = opt.precond_fp32 != 0 && nlev > 1;
+        if (l == nlev - 1 || !vc32) L.val.upload(val);
+        if (vc32 && l >= 1) {
+            std::vector<float> v32(val.size());
+#pragma omp parallel for schedule(static)
+            for (int64_t i = 0; i < (int64_t)val.size(); ++i) v32[i] = (float)val[i];
+            L.val32.upload(v32);
+        }
         L.dinv.upload(dinv);
         L.minv.upload(minv);
         L.mask.upload(mask);
-        L.x.alloc(3 * nn);
-        L.t.alloc(3 * nn);
-        L.b.alloc(3 * nn);
-        L.r.alloc(3 * nn);
-        L.d.alloc(3 * nn);
-        L.x.zero(stream);
-        L.t.zero(stream);
+        for (auto* v : {&L.x, &L.t, &L.b, &L.r, &L.d}) {
+            v->alloc(3 * L.nn);
+            v->zero(stream);
+        }
         if (l > 0) {
-            const Stencil& st = *S[l - 1];
-            if (st.nf != nn || st.nc != nnodes[l - 1]) throw ApiError(DDPCA_EINVAL, "stencil shape");
-            const int64_t nc = st.nc, nfn = nn - nc;
-            L.nc = nc;
-            std::vector<int32_t> ppar(8 * std::max<int64_t>(nfn, 1), -1);
-            std::vector<double> pw(8 * std::max<int64_t>(nfn, 1), 0.0);
-            std::vector<int64_t> cnt(nc + 1, 0);
-            for (int64_t i = 0; i < nn; ++i) {
-                const int64_t np = st.ptr[i + 1] - st.ptr[i];
-                if (i < nc) {
-                    if (np != 1 || st.col[st.ptr[i]] != i || st.w[st.ptr[i]] != 1.0)
-                        throw ApiError(DDPCA_EINVAL, "stencil is not identity on coarse nodes");
-                    continue;
-                }
-                if (np > 8) throw ApiError(DDPCA_EINVAL, "more than 8 parents");
-                for (int64_t k = 0; k < np; ++k) {
-                    ppar[k * nfn + (i - nc)] = st.col[st.ptr[i] + k];
-                    pw[k * nfn + (i - nc)] = st.w[st.ptr[i] + k];
-                    cnt[st.col[st.ptr[i] + k] + 1]++;
+            const LevelDev& C = lev[l - 1];
+            std::vector<int32_t> ppar(8 * L.nn, -1);
+            std::vector<double> pw(8 * L.nn, 0.0);
+            std::vector<int64_t> cnt(C.nn + 1, 0);
+            std::vector<std::vector<std::pair<int32_t, double>>> kids(C.nn);
+            for (int s = 0; s < nsub; ++s) {
+                const Stencil& st = *subs[s].S[l - 1];
+                const auto& pf = perm[l][s];
+                const auto& pc = perm[l - 1][s];
+                const int64_t nc = C.nloc[s];
+                if (st.nf != L.nloc[s] || st.nc != nc) throw ApiError(DDPCA_EINVAL, "stencil shape");
+                for (int64_t i = 0; i < L.nloc[s]; ++i) {
+                    const int64_t np = st.ptr[i + 1] - st.ptr[i];
+                    const int64_t gf = L.noff[s] + pf[i];
+                    if (i < nc) {
+                        if (np != 1 || st.col[st.ptr[i]] != i || st.w[st.ptr[i]] != 1.0)
+                            throw ApiError(DDPCA_EINVAL, "stencil is not identity on coarse nodes");
+                        const int64_t gc = C.noff[s] + pc[i];
+                        ppar[gf] = (int32_t)gc;
+                        pw[gf] = 1.0;
+                        kids[gc].insert(kids[gc].begin(), {(int32_t)gf, 1.0});
+                        continue;
+                    }
+                    if (np > 8) throw ApiError(DDPCA_EINVAL, "more than 8 parents");
+                    for (int64_t k = 0; k < np; ++k) {
+                        const int64_t gc = C.noff[s] + pc[st.col[st.ptr[i] + k]];
+                        ppar[k * L.nn + gf] = (int32_t)gc;
+                        pw[k * L.nn + gf] = st.w[st.ptr[i] + k];
+                        kids[gc].push_back({(int32_t)gf, st.w[st.ptr[i] + k]});
+                    }
                 }
             }
-            for (int64_t c = 0; c < nc; ++c) cnt[c + 1] += cnt[c];
-            std::vector<int32_t> rch(cnt[nc]);
-            std::vector<double> rw(cnt[nc]);
-            std::vector<int64_t> fill(cnt.begin(), cnt.end() - 1);
-            for (int64_t i = nc; i < nn; ++i)
-                for (int64_t k = st.ptr[i]; k < st.ptr[i + 1]; ++k) {
-                    const int64_t p = fill[st.col[k]]++;
-                    rch[p] = (int32_t)i;
-                    rw[p] = st.w[k];
+            for (int64_t c = 0; c < C.nn; ++c) cnt[c + 1] = cnt[c] + (int64_t)kids[c].size();
+            std::vector<int32_t> rch(std::max<int64_t>(cnt[C.nn], 1));
+            std::vector<double> rw(std::max<int64_t>(cnt[C.nn], 1));
+            for (int64_t c = 0; c < C.nn; ++c)
+                for (size_t k = 0; k < kids[c].size(); ++k) {
+                    rch[cnt[c] + k] = kids[c][k].first;
+                    rw[cnt[c] + k] = kids[c][k].second;
                 }
             L.ppar.upload(ppar);
             L.pw.upload(pw);
@@ -576,52 +836,82 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<int64_t>& nnodes, const std:
             L.rw.upload(rw);
         }
     }
-    // exact coarse solve: dense inverse of the masked level-0 operator
+    fine_perm = perm[nlev - 1];
+    // exact coarse solve: dense inverse of each subdomain's masked level-0 operator
     {
-        const Bsr3& A = *K[0];
-        n0 = 3 * nnodes[0];
-        std::vector<double> D(n0 * n0, 0.0);
-        for (int64_t r = 0; r < nnodes[0]; ++r)
-            for (int64_t k = A.ptr[r]; k < A.ptr[r + 1]; ++k) {
-                const int64_t j = A.col[k];
-                for (int a = 0; a < 3; ++a)
-                    for (int b = 0; b < 3; ++b) {
-                        double v = A.val[9 * k + 3 * a + b];
-                        if (!dof_free[3 * r + a] || !dof_free[3 * j + b]) v = (j == r && a == b) ? 1.0 : 0.0;
-                        D[(3 * r + a) * n0 + 3 * j + b] = v;
-                    }
-            }
-        invert_spd_dense(D, n0);
-        for (int64_t d = 0; d < n0; ++d)
-            if (!dof_free[d])
-                for (int64_t e = 0; e < n0; ++e) D[d * n0 + e] = D[e * n0 + d] = 0.0;
-        ainv.upload(D);
+        std::vector<double> packed;
+        std::vector<int64_t> ao(nsub), no(nsub), nz(nsub);
+        for (int s = 0; s < nsub; ++s) {
+            const Bsr3& A = *subs[s].K[0];
+            const uint8_t* fr = subs[s].dof_free;
+            const int64_t n0 = 3 * subs[s].nnodes[0];
+            std::vector<double> D(n0 * n0, 0.0);
+            for (int64_t r = 0; r < subs[s].nnodes[0]; ++r)
+                for (int64_t k = A.ptr[r]; k < A.ptr[r + 1]; ++k) {
+                    const int64_t j = A.col[k];
+                    for (int a = 0; a < 3; ++a)
+                        for (int b = 0; b < 3; ++b) {
+                            double v = A.val[9 * k + 3 * a + b];
+                            if (!fr[3 * r + a] || !fr[3 * j + b]) v = (j == r && a == b) ? 1.0 : 0.0;
+                            D[(3 * r + a) * n0 + 3 * j + b] = v;
+                        }
+                }
+            invert_spd_dense(D, n0);
+            for (int64_t d = 0; d < n0; ++d)
+                if (!fr[d])
+                    for (int64_t e = 0; e < n0; ++e) D[d * n0 + e] = D[e * n0 + d] = 0.0;
+            ao[s] = (int64_t)packed.size();
+            no[s] = lev[0].noff[s];
+            nz[s] = n0;
+            packed.insert(packed.end(), D.begin(), D.end());
+        }
+        ainv.upload(packed);
+        aoff.upload(ao);
+        c_noff.upload(no);
+        c_n.upload(nz);
     }
     // condensed <-> nodal map of the fine level
-    for (int64_t d = 0; d < 3 * nnodes.back(); ++d)
-        if (dof_free[d]) free_dof_host.push_back((int32_t)d);
-    nfree = (int64_t)free_dof_host.size();
-    free_dof.upload(free_dof_host);
-    const int64_t nnL = nnodes.back();
+    const LevelDev& F = lev.back();
+    nfree.resize(nsub);
+    free_dof_host.resize(nsub);
+    free_dof.resize(nsub);
+    std::vector<int64_t> cb(nsub + 1, 0);
+    for (int s = 0; s < nsub; ++s) {
+        for (int64_t d = 0; d < 3 * F.nloc[s]; ++d)
+            if (subs[s].dof_free[d]) free_dof_host[s].push_back((int32_t)fine_dof(s, d));
+        nfree[s] = (int64_t)free_dof_host[s].size();
+        free_dof[s].upload(free_dof_host[s]);
+        cb[s] = F.noff[s] / kChunk;
+    }
+    cb[nsub] = F.nch;
+    fin_cb.upload(cb);
     for (auto* v : {&xs, &rs, &zs, &ps, &qs, &bs}) {
-        v->alloc(3 * nnL);
+        v->alloc(3 * F.nn);
         v->zero(stream);
     }
-    nblk_fine = ceil_div(nnL, kBlock);
-    int64_t maxblk = nblk_fine;
-    for (auto& L : lev) maxblk = std::max<int64_t>(maxblk, ceil_div(L.nn, kBlock));
-    partial.alloc(maxblk);
-    sc.alloc(1);
-    DDPCA_HIP(hipHostMalloc(&sc_host, sizeof(PcgScal)));
-    std::memset(sc_host, 0, sizeof(PcgScal));
+    int64_t maxch = 0;
+    for (auto& L : lev) maxch = std::max<int64_t>(maxch, L.nch);
+    partial.alloc(2 * maxch);
+    sc.alloc(nsub);
+    DDPCA_HIP(hipHostMalloc(reinterpret_cast<void**>(&sc_host), nsub * sizeof(PcgScal)));
+    std::memset(sc_host, 0, nsub * sizeof(PcgScal));
+    mirror.alloc(nsub);
     DDPCA_HIP(hipEventCreate(&ev_k0));
     DDPCA_HIP(hipEventCreate(&ev_k1));
-    // smoother damping from the spectrum of M K on each smoothed level
+    // smoother coefficients from the spectrum of M K on each smoothed level and subdomain
     for (int l = 1; l < nlev; ++l) {
         estimate_lmax(l);
-        lev[l].omega = opt.omega > 0.0 ? opt.omega : 4.0 / (3.0 * lev[l].lmax);
+        std::vector<double> coef(2 * (opt.nu + 1) * nsub, 0.0);
+        for (int k = 0; k <= opt.nu; ++k)
+            for (int s = 0; s < nsub; ++s) {
+                double c1 = 0.0, c2;
+                if (opt.smoother == 2) cheb_coef(lev[l].lmax[s], k, c1, c2);
+                else c2 = opt.omega > 0.0 ? opt.omega : 4.0 / (3.0 * lev[l].lmax[s]);
+                coef[2 * (k * nsub + s)] = c1;
+                coef[2 * (k * nsub + s) + 1] = c2;
+            }
+        lev[l].coef.upload(coef);
     }
-    if (nlev == 1) lev[0].omega = 1.0;
     DDPCA_HIP(hipStreamSynchronize(stream));
 }
 
@@ -636,53 +926,147 @@ MgpisDevice::~MgpisDevice() {
     if (stream) (void)hipStreamDestroy(stream);
 }
 
+// lambda_max(M K) per subdomain by 24 power iterations (all subdomains of the batch at once).
 void MgpisDevice::estimate_lmax(int l) {
     LevelDev& L = lev[l];
     const bool bj = opt.smoother >= 1;
     const int64_t n = 3 * L.nn;
-    std::vector<double> h(n);
-    std::mt19937_64 rng(20251017 + l);
-    std::uniform_real_distribution<double> U(-1.0, 1.0);
+    std::vector<double> h(n, 0.0);
     std::vector<uint8_t> mask = L.mask.download();
-    for (int64_t i = 0; i < n; ++i) h[i] = (mask[i / 3] >> (i % 3)) & 1 ? U(rng) : 0.0;
-    DevBuf<double> v, w;
+    for (int s = 0; s < nsub; ++s) {
+        std::mt19937_64 rng(20251017 + l);
+        std::uniform_real_distribution<double> U(-1.0, 1.0);
+        for (int64_t i = 3 * L.noff[s]; i < 3 * (L.noff[s] + L.nloc[s]); ++i) h[i] = (mask[i / 3] >> (i % 3)) & 1 ? U(rng) : 0.0;
+    }
+    DevBuf<double> v, w, scale(nsub);
     v.upload(h);
     w.alloc(n);
     const int nb = ceil_div(L.nn, kBlock);
-    double lam = 0.0;
-    auto norm2 = [&]() {
-        std::vector<double> p(nb);
-        DDPCA_HIP(hipMemcpyAsync(p.data(), partial.p, nb * sizeof(double), hipMemcpyDeviceToHost, stream));
+    std::vector<double> part(L.nch), nrm(nsub), inv(nsub);
+    auto norms = [&]() {
+        DDPCA_HIP(hipMemcpyAsync(part.data(), partial.p, L.nch * sizeof(double), hipMemcpyDeviceToHost, stream));
         DDPCA_HIP(hipStreamSynchronize(stream));
-        return std::accumulate(p.begin(), p.end(), 0.0);
+        for (int s = 0; s < nsub; ++s) {
+            double t = 0.0;
+            for (int64_t c = L.noff[s] / kChunk; c < (L.noff[s] + pad64(L.nloc[s])) / kChunk; ++c) t += part[c];
+            nrm[s] = std::sqrt(t);
+            inv[s] = nrm[s] > 0.0 ? 1.0 / nrm[s] : 0.0;
+        }
     };
-    // normalise
-    if (bj) hipLaunchKernelGGL((k_apply_m<true>), dim3(nb), dim3(kBlock), 0, stream, v.p, L.minv.p, w.p, partial.p, L.nn);
-    else hipLaunchKernelGGL((k_apply_m<false>), dim3(nb), dim3(kBlock), 0, stream, v.p, L.minv.p, w.p, partial.p, L.nn);
-    double nrm = std::sqrt(norm2());
+    auto apply_m = [&](const double* x) {
+        if (bj) hipLaunchKernelGGL((k_apply_m<true>), dim3(nb), dim3(kBlock), 0, stream, x, L.minv.p, w.p, partial.p, L.nn);
+        else hipLaunchKernelGGL((k_apply_m<false>), dim3(nb), dim3(kBlock), 0, stream, x, L.minv.p, w.p, partial.p, L.nn);
+    };
+    apply_m(v.p);
+    norms();
     for (int it = 0; it < 24; ++it) {
         // v <- w / |w| ; w <- M K v
-        std::vector<double> tmp(n);
-        DDPCA_HIP(hipMemcpyAsync(tmp.data(), w.p, n * sizeof(double), hipMemcpyDeviceToHost, stream));
-        DDPCA_HIP(hipStreamSynchronize(stream));
-        for (auto& t : tmp) t /= nrm;
-        DDPCA_HIP(hipMemcpyAsync(v.p, tmp.data(), n * sizeof(double), hipMemcpyHostToDevice, stream));
-        spmv(l, v.p, L.r.p);
-        if (bj) hipLaunchKernelGGL((k_apply_m<true>), dim3(nb), dim3(kBlock), 0, stream, L.r.p, L.minv.p, w.p, partial.p, L.nn);
-        else hipLaunchKernelGGL((k_apply_m<false>), dim3(nb), dim3(kBlock), 0, stream, L.r.p, L.minv.p, w.p, partial.p, L.nn);
-        nrm = std::sqrt(norm2());
-        lam = nrm;
+        DDPCA_HIP(hipMemcpyAsync(scale.p, inv.data(), nsub * sizeof(double), hipMemcpyHostToDevice, stream));
+        hipLaunchKernelGGL(k_scale_sub, dim3(nb), dim3(kBlock), 0, stream, w.p, scale.p, v.p, L.nn, L.csub.p);
+        spmv(l, v.p, L.r.p, true);  // the smoother's operator
+        apply_m(L.r.p);
+        norms();
     }
-    L.lmax = lam * 1.05;  // safety margin on the power-iteration estimate
+    L.lmax.resize(nsub);
+    for (int s = 0; s < nsub; ++s) L.lmax[s] = nrm[s] * 1.05;  // safety margin on the estimate
 }
 
 // ============================================================================== operations
-void MgpisDevice::spmv(int level, const double* x, double* y) {
-    LevelDev& L = lev[level];
+namespace {
+// Krylov-operator arguments (fp64 values) of a level
+SellArgs level_args(const LevelDev& L) {
     SellArgs a{};
-    a.slots = L.slots.p; a.off = L.off.p; a.col = L.col.p; a.val = L.val.p;
-    a.nn = L.nn; a.nch = L.nch; a.x = x; a.y = y; a.done = zero_flag();
-    hipLaunchKernelGGL((k_sell<kSpmv, false, false>), dim3(ceil_div(L.nch, 4)), dim3(kBlock), 0, stream, a);
+    a.slots = L.slots.p;
+    a.off = L.off.p;
+    a.col = L.col.p;
+    a.val = L.val.p;
+    a.csub = L.csub.p;
+    a.nch = L.nch;
+    a.minv = L.minv.p;
+    return a;
+}
+
+// one SELL launch over a level, values stored as fp32 (f32) or fp64
+template <int MODE, bool BJ, bool DOT>
+void launch_sell(bool f32, const SellArgs& a, hipStream_t s) {
+    const int grid = ceil_div(a.nch, 4);
+    if (f32) hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, float>), dim3(grid), dim3(kBlock), 0, s, a);
+    else hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, double>), dim3(grid), dim3(kBlock), 0, s, a);
+}
+
+template <int MODE, bool BJ, bool DOT>
+void launch_loop(int loop, bool f32, const SellArgs& a, int grid, hipStream_t s) {
+    if (f32) {
+        switch (loop) {
+            case 0: hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, float, 0>), dim3(grid), dim3(kBlock), 0, s, a); break;
+            case 1: hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, float, 1>), dim3(grid), dim3(kBlock), 0, s, a); break;
+            case 2: hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, float, 2>), dim3(grid), dim3(kBlock), 0, s, a); break;
+            default: hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, float, 3>), dim3(grid), dim3(kBlock), 0, s, a); break;
+        }
+        return;
+    }
+    switch (loop) {
+        case 0: hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, double, 0>), dim3(grid), dim3(kBlock), 0, s, a); break;
+        case 1: hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, double, 1>), dim3(grid), dim3(kBlock), 0, s, a); break;
+        case 2: hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, double, 2>), dim3(grid), dim3(kBlock), 0, s, a); break;
+        default: hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, double, 3>), dim3(grid), dim3(kBlock), 0, s, a); break;
+    }
+}
+}  // namespace
+
+namespace {
+// V-cycle-operator arguments of a level: the fp32 copy when the preconditioner stores it
+SellArgs vc_level_args(const MgpisDevice& D, int level) {
+    SellArgs a = level_args(D.lev[level]);
+    if (D.vc32()) a.val = D.lev[level].val32.p;
+    return a;
+}
+}  // namespace
+
+void MgpisDevice::spmv(int level, const double* x, double* y, bool vc_op) {
+    SellArgs a = vc_op ? vc_level_args(*this, level) : level_args(lev[level]);
+    if (!a.val) throw ApiError(DDPCA_ESTATE, "operator of this level is not stored in the requested precision");
+    a.x = x;
+    a.y = y;
+    launch_sell<kSpmv, false, false>(vc_op && vc32(), a, stream);
+}
+
+double MgpisDevice::bench_spmv(int variant, int reps) {
+    // variant = loop (0..3) + 4 * mode (0 y = Kx, 1 PCG, 2 residual, 3 Chebyshev sweep) + 16 *
+    // fp32 values (the V-cycle copy); fine level, whole batch, operands in the PCG work vectors
+    // (values are irrelevant to the timing)
+    const LevelDev& L = lev.back();
+    const int loop = variant & 3, mode = (variant >> 2) & 3;
+    const bool f32 = (variant & 16) != 0;
+    if (variant >= 32) throw ApiError(DDPCA_EINVAL, "unknown SpMV variant");
+    if (mode == 3 && (lev.size() < 2 || opt.smoother < 1)) throw ApiError(DDPCA_EINVAL, "Chebyshev mode needs block smoothing");
+    if (f32 && !L.val32.p) throw ApiError(DDPCA_EINVAL, "no fp32 operator (precond_fp32 = 0)");
+    DDPCA_HIP(hipMemsetAsync(sc.p, 0, nsub * sizeof(PcgScal), stream));  // done = 0, beta = 0
+    SellArgs a = level_args(L);
+    if (f32) a.val = L.val32.p;
+    a.x = xs.p;
+    a.y = qs.p;
+    a.p = ps.p;
+    a.b = bs.p;
+    a.xo = rs.p;
+    a.partial = partial.p;
+    a.sc = sc.p;
+    if (lev.size() > 1) a.coef = L.coef.p;
+    const int grid = ceil_div(L.nch, 4);
+    auto launch = [&]() {
+        if (mode == 0) launch_loop<kSpmv, false, false>(loop, f32, a, grid, stream);
+        else if (mode == 1) launch_loop<kPcg, false, true>(loop, f32, a, grid, stream);
+        else if (mode == 2) launch_loop<kResid, false, false>(loop, f32, a, grid, stream);
+        else launch_loop<kCheb, true, false>(loop, f32, a, grid, stream);
+    };
+    launch();
+    DDPCA_HIP(hipEventRecord(ev_k0, stream));
+    for (int r = 0; r < reps; ++r) launch();
+    DDPCA_HIP(hipEventRecord(ev_k1, stream));
+    DDPCA_HIP(hipEventSynchronize(ev_k1));
+    float ms = 0.f;
+    DDPCA_HIP(hipEventElapsedTime(&ms, ev_k0, ev_k1));
+    return (double)ms / std::max(reps, 1);
 }
 
 void MgpisDevice::vcycle(const double* rin, double* zout, bool dot) {
@@ -691,10 +1075,13 @@ void MgpisDevice::vcycle(const double* rin, double* zout, bool dot) {
     const bool bj = opt.smoother >= 1;
     const bool cheb = opt.smoother == 2;
     const int nu = opt.nu;
-    const int* done = reinterpret_cast<const int*>(&sc.p->done);
+    const PcgScal* scp = sc.p;
     if (Lf == 0) {
-        hipLaunchKernelGGL(k_coarse, dim3(ceil_div(n0, 4)), dim3(kBlock), 0, stream, ainv.p, rin, zout, n0, done);
-        if (dot) hipLaunchKernelGGL(k_dot, dim3(nblk_fine), dim3(kBlock), 0, stream, rin, zout, partial.p, lev[0].nn, done);
+        hipLaunchKernelGGL(k_coarse, dim3(ceil_div(3 * lev[0].nn, 4)), dim3(kBlock), 0, stream, ainv.p, aoff.p, c_noff.p,
+                           c_n.p, rin, zout, 3 * lev[0].nn, lev[0].csub.p, scp);
+        if (dot)
+            hipLaunchKernelGGL(k_dot, dim3(ceil_div(lev[0].nn, kBlock)), dim3(kBlock), 0, stream, rin, zout, partial.p,
+                               lev[0].nn, lev[0].csub.p, scp);
         return;
     }
     std::vector<double*> cur(nlev), oth(nlev);
@@ -702,116 +1089,103 @@ void MgpisDevice::vcycle(const double* rin, double* zout, bool dot) {
     cur[Lf] = lev[Lf].t.p;
     oth[Lf] = zout;
     auto bvec = [&](int l) -> const double* { return l == Lf ? rin : lev[l].b.p; };
-    auto sell_args = [&](int l) {
-        LevelDev& L = lev[l];
-        SellArgs a{};
-        a.slots = L.slots.p; a.off = L.off.p; a.col = L.col.p; a.val = L.val.p;
-        a.nn = L.nn; a.nch = L.nch; a.minv = L.minv.p; a.omega = L.omega; a.done = done; a.partial = partial.p;
-        a.sc = sc.p;
-        return a;
-    };
-    // Chebyshev coefficients on [lmax/30, lmax] of M K (sweep k uses coefficient pair k)
-    auto cheb_coef = [&](int l, int k, double& c1, double& c2) {
-        const double lmax = lev[l].lmax, lmin = lmax / 30.0;
-        const double theta = 0.5 * (lmax + lmin), delta = 0.5 * (lmax - lmin), sigma = theta / delta;
-        double rho_old = 1.0 / sigma, rho = rho_old;
-        for (int i = 1; i <= k; ++i) {
-            rho = 1.0 / (2.0 * sigma - rho_old);
-            if (i < k) rho_old = rho;
-        }
-        c1 = rho * rho_old;
-        c2 = 2.0 * rho / delta;
-    };
+    auto coef = [&](int l, int sweep) { return lev[l].coef.p + 2 * (int64_t)sweep * nsub; };
     // smoothing sweeps on level l from the current iterate (first: jac0/restrict already did sweep 0)
+    const bool f32 = vc32();
     auto smooth = [&](int l, int first, int count, bool last_dot) {
         for (int s = first; s < first + count; ++s) {
-            SellArgs a = sell_args(l);
+            SellArgs a = vc_level_args(*this, l);
+            a.sc = scp;
+            a.partial = partial.p;
             a.x = cur[l];
             a.b = bvec(l);
             a.xo = oth[l];
+            a.coef = coef(l, s);
             const bool d = last_dot && s == first + count - 1;
-            const int grid = ceil_div(lev[l].nch, 4);
             if (cheb) {
                 a.p = lev[l].d.p;
-                cheb_coef(l, s, a.c1, a.c2);
-                if (s == 0) { a.c1 = 0.0; a.c2 = 1.0 / (0.5 * (lev[l].lmax + lev[l].lmax / 30.0)); }
-                if (d) hipLaunchKernelGGL((k_sell<kCheb, true, true>), dim3(grid), dim3(kBlock), 0, stream, a);
-                else hipLaunchKernelGGL((k_sell<kCheb, true, false>), dim3(grid), dim3(kBlock), 0, stream, a);
+                if (d) launch_sell<kCheb, true, true>(f32, a, stream);
+                else launch_sell<kCheb, true, false>(f32, a, stream);
             } else if (bj) {
-                if (d) hipLaunchKernelGGL((k_sell<kJac, true, true>), dim3(grid), dim3(kBlock), 0, stream, a);
-                else hipLaunchKernelGGL((k_sell<kJac, true, false>), dim3(grid), dim3(kBlock), 0, stream, a);
+                if (d) launch_sell<kJac, true, true>(f32, a, stream);
+                else launch_sell<kJac, true, false>(f32, a, stream);
             } else {
-                if (d) hipLaunchKernelGGL((k_sell<kJac, false, true>), dim3(grid), dim3(kBlock), 0, stream, a);
-                else hipLaunchKernelGGL((k_sell<kJac, false, false>), dim3(grid), dim3(kBlock), 0, stream, a);
+                if (d) launch_sell<kJac, false, true>(f32, a, stream);
+                else launch_sell<kJac, false, false>(f32, a, stream);
             }
             std::swap(cur[l], oth[l]);
         }
     };
-    // omega of the zero-guess first sweep (Chebyshev: 1/theta)
-    auto first_omega = [&](int l) { return cheb ? 1.0 / (0.5 * (lev[l].lmax + lev[l].lmax / 30.0)) : lev[l].omega; };
     // ---- descend
     {
-        const int grid = ceil_div(lev[Lf].nn, kBlock);
-        const double om = first_omega(Lf);
-        if (cheb) hipLaunchKernelGGL((k_jac0<true, true>), dim3(grid), dim3(kBlock), 0, stream, rin, lev[Lf].minv.p, om, cur[Lf], lev[Lf].d.p, lev[Lf].nn, done);
-        else if (bj) hipLaunchKernelGGL((k_jac0<true, false>), dim3(grid), dim3(kBlock), 0, stream, rin, lev[Lf].minv.p, om, cur[Lf], nullptr, lev[Lf].nn, done);
-        else hipLaunchKernelGGL((k_jac0<false, false>), dim3(grid), dim3(kBlock), 0, stream, rin, lev[Lf].minv.p, om, cur[Lf], nullptr, lev[Lf].nn, done);
+        const LevelDev& F = lev[Lf];
+        const int grid = ceil_div(F.nn, kBlock);
+        if (cheb) hipLaunchKernelGGL((k_jac0<true, true>), dim3(grid), dim3(kBlock), 0, stream, rin, F.minv.p, coef(Lf, 0), cur[Lf], F.d.p, F.nn, F.csub.p, scp);
+        else if (bj) hipLaunchKernelGGL((k_jac0<true, false>), dim3(grid), dim3(kBlock), 0, stream, rin, F.minv.p, coef(Lf, 0), cur[Lf], nullptr, F.nn, F.csub.p, scp);
+        else hipLaunchKernelGGL((k_jac0<false, false>), dim3(grid), dim3(kBlock), 0, stream, rin, F.minv.p, coef(Lf, 0), cur[Lf], nullptr, F.nn, F.csub.p, scp);
     }
     for (int l = Lf; l >= 1; --l) {
         smooth(l, 1, nu - 1, false);
         {
-            SellArgs a = sell_args(l);
+            SellArgs a = vc_level_args(*this, l);
+            a.sc = scp;
             a.x = cur[l];
             a.b = bvec(l);
             a.y = lev[l].r.p;
-            hipLaunchKernelGGL((k_sell<kResid, false, false>), dim3(ceil_div(lev[l].nch, 4)), dim3(kBlock), 0, stream, a);
+            launch_sell<kResid, false, false>(f32, a, stream);
         }
         const int c = l - 1;
-        const int grid = ceil_div(lev[c].nn, kBlock);
         const LevelDev& F = lev[l];
-        const double om = c > 0 ? first_omega(c) : 0.0;
+        const LevelDev& C = lev[c];
+        const int grid = ceil_div(C.nn, kBlock);
+        const double* cf = c > 0 ? coef(c, 0) : nullptr;
         if (c == 0)
-            hipLaunchKernelGGL((k_restrict<false, false, false>), dim3(grid), dim3(kBlock), 0, stream, F.r.p, F.rptr.p, F.rch.p, F.rw.p, lev[c].mask.p, lev[c].b.p, nullptr, nullptr, nullptr, 0.0, lev[c].nn, done);
+            hipLaunchKernelGGL((k_restrict<false, false, false>), dim3(grid), dim3(kBlock), 0, stream, F.r.p, F.rptr.p, F.rch.p, F.rw.p, C.mask.p, C.b.p, nullptr, nullptr, nullptr, nullptr, C.nn, C.csub.p, scp);
         else if (cheb)
-            hipLaunchKernelGGL((k_restrict<true, true, true>), dim3(grid), dim3(kBlock), 0, stream, F.r.p, F.rptr.p, F.rch.p, F.rw.p, lev[c].mask.p, lev[c].b.p, cur[c], lev[c].d.p, lev[c].minv.p, om, lev[c].nn, done);
+            hipLaunchKernelGGL((k_restrict<true, true, true>), dim3(grid), dim3(kBlock), 0, stream, F.r.p, F.rptr.p, F.rch.p, F.rw.p, C.mask.p, C.b.p, cur[c], C.d.p, C.minv.p, cf, C.nn, C.csub.p, scp);
         else if (bj)
-            hipLaunchKernelGGL((k_restrict<true, true, false>), dim3(grid), dim3(kBlock), 0, stream, F.r.p, F.rptr.p, F.rch.p, F.rw.p, lev[c].mask.p, lev[c].b.p, cur[c], nullptr, lev[c].minv.p, om, lev[c].nn, done);
+            hipLaunchKernelGGL((k_restrict<true, true, false>), dim3(grid), dim3(kBlock), 0, stream, F.r.p, F.rptr.p, F.rch.p, F.rw.p, C.mask.p, C.b.p, cur[c], nullptr, C.minv.p, cf, C.nn, C.csub.p, scp);
         else
-            hipLaunchKernelGGL((k_restrict<true, false, false>), dim3(grid), dim3(kBlock), 0, stream, F.r.p, F.rptr.p, F.rch.p, F.rw.p, lev[c].mask.p, lev[c].b.p, cur[c], nullptr, lev[c].minv.p, om, lev[c].nn, done);
+            hipLaunchKernelGGL((k_restrict<true, false, false>), dim3(grid), dim3(kBlock), 0, stream, F.r.p, F.rptr.p, F.rch.p, F.rw.p, C.mask.p, C.b.p, cur[c], nullptr, C.minv.p, cf, C.nn, C.csub.p, scp);
     }
-    hipLaunchKernelGGL(k_coarse, dim3(ceil_div(n0, 4)), dim3(kBlock), 0, stream, ainv.p, lev[0].b.p, cur[0], n0, done);
+    hipLaunchKernelGGL(k_coarse, dim3(ceil_div(3 * lev[0].nn, 4)), dim3(kBlock), 0, stream, ainv.p, aoff.p, c_noff.p, c_n.p,
+                       lev[0].b.p, cur[0], 3 * lev[0].nn, lev[0].csub.p, scp);
     // ---- ascend
     for (int l = 1; l <= Lf; ++l) {
         const LevelDev& F = lev[l];
-        hipLaunchKernelGGL(k_prolong, dim3(ceil_div(F.nn, kBlock)), dim3(kBlock), 0, stream, cur[l - 1], F.ppar.p, F.pw.p, F.mask.p, cur[l], F.nn, F.nc, done);
+        hipLaunchKernelGGL(k_prolong, dim3(ceil_div(F.nn, kBlock)), dim3(kBlock), 0, stream, cur[l - 1], F.ppar.p, F.pw.p,
+                           F.mask.p, cur[l], F.nn, F.csub.p, scp);
         // post-smoothing restarts the smoother (Chebyshev recurrence) from the prolongated iterate
         smooth(l, 0, nu, dot && l == Lf);
     }
     if (cur[Lf] != zout) throw ApiError(DDPCA_ESTATE, "V-cycle buffer parity");
 }
 
-double MgpisDevice::fine_kernel_bytes() const {
-    // algorithmic bytes of one fine-level k_sell<kPcg>: 76 B per stored block (72 value + 4 index)
-    // + z gathered once (24 B/node) + p, q read and written (4 x 24 B/node)
+double MgpisDevice::fine_kernel_bytes(int s) const {
+    // algorithmic bytes of one fine-level k_sell<kPcg> for member s: 76 B per stored block
+    // (72 value + 4 index) + z gathered once (24 B/node) + p, q read and written (4 x 24 B/node)
     const LevelDev& L = lev.back();
-    return 76.0 * (double)L.nnzb + 24.0 * 5.0 * (double)L.nn;
+    return 76.0 * (double)L.nnzb_sub[s] + 24.0 * 5.0 * (double)L.nloc[s];
 }
 
 void MgpisDevice::enqueue_iteration(int prec, bool timed) {
     LevelDev& L = lev.back();
-    const int* done = reinterpret_cast<const int*>(&sc.p->done);
-    SellArgs a{};
-    a.slots = L.slots.p; a.off = L.off.p; a.col = L.col.p; a.val = L.val.p;
-    a.nn = L.nn; a.nch = L.nch; a.x = zs.p; a.y = qs.p; a.p = ps.p; a.sc = sc.p; a.partial = partial.p; a.done = done;
+    SellArgs a = level_args(L);
+    a.x = zs.p;
+    a.y = qs.p;
+    a.p = ps.p;
+    a.sc = sc.p;
+    a.partial = partial.p;
+    const int nblk = ceil_div(L.nn, kBlock);
     if (timed) DDPCA_HIP(hipEventRecord(ev_k0, stream));
     hipLaunchKernelGGL((k_sell<kPcg, false, true>), dim3(ceil_div(L.nch, 4)), dim3(kBlock), 0, stream, a);
     if (timed) DDPCA_HIP(hipEventRecord(ev_k1, stream));
-    hipLaunchKernelGGL(k_fin, dim3(1), dim3(kBlock), 0, stream, (int)kFinAlpha, partial.p, nblk_fine, sc.p);
-    hipLaunchKernelGGL(k_axpy, dim3(nblk_fine), dim3(kBlock), 0, stream, xs.p, rs.p, ps.p, qs.p, sc.p, partial.p, L.nn, done);
-    hipLaunchKernelGGL(k_fin, dim3(1), dim3(kBlock), 0, stream, (int)kFinRR, partial.p, nblk_fine, sc.p);
+    hipLaunchKernelGGL(k_fin, dim3(nsub), dim3(kBlock), 0, stream, (int)kFinAlpha, partial.p, nullptr, fin_cb.p, sc.p, mirror.dev);
+    hipLaunchKernelGGL(k_axpy, dim3(nblk), dim3(kBlock), 0, stream, xs.p, rs.p, ps.p, qs.p, sc.p, partial.p, L.nn, L.csub.p);
+    hipLaunchKernelGGL(k_fin, dim3(nsub), dim3(kBlock), 0, stream, (int)kFinRR, partial.p, nullptr, fin_cb.p, sc.p, mirror.dev);
     if (prec == 1) vcycle(rs.p, zs.p, true);
-    else hipLaunchKernelGGL(k_diag, dim3(nblk_fine), dim3(kBlock), 0, stream, rs.p, L.dinv.p, zs.p, partial.p, L.nn, done);
-    hipLaunchKernelGGL(k_fin, dim3(1), dim3(kBlock), 0, stream, (int)kFinBeta, partial.p, nblk_fine, sc.p);
+    else hipLaunchKernelGGL(k_diag, dim3(nblk), dim3(kBlock), 0, stream, rs.p, L.dinv.p, zs.p, partial.p, L.nn, L.csub.p, sc.p);
+    hipLaunchKernelGGL(k_fin, dim3(nsub), dim3(kBlock), 0, stream, (int)kFinBeta, partial.p, nullptr, fin_cb.p, sc.p, mirror.dev);
 }
 
 // graph_[prec]: iters_per_graph PCG iterations captured once and replayed.
@@ -825,20 +1199,39 @@ void MgpisDevice::build_graph(int prec) {
     DDPCA_HIP(hipGraphDestroy(g));
 }
 
-void MgpisDevice::pcg_begin(int prec, double rtol, int64_t maxit) {
+void MgpisDevice::pcg_begin(int prec, double rtol, const std::vector<int64_t>& maxit, bool warm) {
     select_device(device);
+    if ((int)maxit.size() != nsub) throw ApiError(DDPCA_EINVAL, "maxit per subdomain");
     build_graph(prec);
     LevelDev& L = lev.back();
-    PcgScal init{};
-    init.tol2 = rtol * rtol;
-    init.maxit = maxit;
-    DDPCA_HIP(hipMemcpyAsync(sc.p, &init, sizeof(PcgScal), hipMemcpyHostToDevice, stream));
-    hipLaunchKernelGGL(k_pcg_init, dim3(nblk_fine), dim3(kBlock), 0, stream, bs.p, xs.p, rs.p, ps.p, qs.p, partial.p, L.nn);
-    hipLaunchKernelGGL(k_fin, dim3(1), dim3(kBlock), 0, stream, (int)kFinInit, partial.p, nblk_fine, sc.p);
-    const int* done = reinterpret_cast<const int*>(&sc.p->done);
+    // the previous solve on this stream has finished (pcg_finish synchronised), so the
+    // host-side reset of the mirror and the staging buffer cannot race a kernel
+    mirror.reset();
+    for (int s = 0; s < nsub; ++s) {
+        sc_host[s] = PcgScal{};
+        sc_host[s].tol2 = rtol * rtol;
+        sc_host[s].maxit = maxit[s];
+    }
+    DDPCA_HIP(hipMemcpyAsync(sc.p, sc_host, nsub * sizeof(PcgScal), hipMemcpyHostToDevice, stream));
+    const int nblk = ceil_div(L.nn, kBlock);
+    if (!warm) {
+        hipLaunchKernelGGL(k_pcg_init, dim3(nblk), dim3(kBlock), 0, stream, bs.p, xs.p, rs.p, ps.p, qs.p, partial.p, L.nn);
+        hipLaunchKernelGGL(k_fin, dim3(nsub), dim3(kBlock), 0, stream, (int)kFinInit, partial.p, nullptr, fin_cb.p, sc.p, mirror.dev);
+    } else {
+        double* partial2 = partial.p + L.nch;
+        hipLaunchKernelGGL(k_pcg_init_warm, dim3(nblk), dim3(kBlock), 0, stream, bs.p, ps.p, qs.p, partial2, L.nn);
+        SellArgs a = level_args(L);
+        a.x = xs.p;
+        a.b = bs.p;
+        a.y = rs.p;
+        a.partial = partial.p;
+        hipLaunchKernelGGL((k_sell<kResid, false, true>), dim3(ceil_div(L.nch, 4)), dim3(kBlock), 0, stream, a);
+        hipLaunchKernelGGL(k_fin, dim3(nsub), dim3(kBlock), 0, stream, (int)kFinInitWarm, partial.p, partial2, fin_cb.p, sc.p, mirror.dev);
+    }
     if (prec == 1) vcycle(rs.p, zs.p, true);
-    else hipLaunchKernelGGL(k_diag, dim3(nblk_fine), dim3(kBlock), 0, stream, rs.p, L.dinv.p, zs.p, partial.p, L.nn, done);
-    hipLaunchKernelGGL(k_fin, dim3(1), dim3(kBlock), 0, stream, (int)kFinBeta0, partial.p, nblk_fine, sc.p);
+    else hipLaunchKernelGGL(k_diag, dim3(nblk), dim3(kBlock), 0, stream, rs.p, L.dinv.p, zs.p, partial.p, L.nn, L.csub.p, sc.p);
+    hipLaunchKernelGGL(k_fin, dim3(nsub), dim3(kBlock), 0, stream, (int)kFinBeta0, partial.p, nullptr, fin_cb.p, sc.p, mirror.dev);
+    sample_pending_ = false;
     if (time_kernel) {
         // first iteration eagerly, with HIP events around its fine-level SpMV on this stream
         enqueue_iteration(prec, true);
@@ -846,39 +1239,59 @@ void MgpisDevice::pcg_begin(int prec, double rtol, int64_t maxit) {
     }
 }
 
-void MgpisDevice::pcg_step(int prec) { DDPCA_HIP(hipGraphLaunch(graph_[prec], stream)); }
+void MgpisDevice::pcg_step(int prec) {
+    DDPCA_HIP(hipGraphLaunch(graph_[prec], stream));
+    ++graphs_launched;
+}
 
-bool MgpisDevice::pcg_poll() {
-    DDPCA_HIP(hipMemcpyAsync(sc_host, sc.p, sizeof(PcgScal), hipMemcpyDeviceToHost, stream));
+void MgpisDevice::pcg_wait(int prec, int64_t pre_enqueued) {
+    const int64_t k = opt.iters_per_graph;
+    const int64_t launched = (sample_pending_ ? 1 : 0) + pre_enqueued * k;
+    graphs_launched += pace_until_done(stream, graph_[prec], mirror, k, launched);
+}
+
+void MgpisDevice::pcg_fetch() {
+    DDPCA_HIP(hipMemcpyAsync(sc_host, sc.p, nsub * sizeof(PcgScal), hipMemcpyDeviceToHost, stream));
+}
+
+void MgpisDevice::pcg_finish() {
+    pcg_fetch();
     DDPCA_HIP(hipStreamSynchronize(stream));
+    pcg_check();
+}
+
+void MgpisDevice::pcg_check() {
     if (sample_pending_) {
-        // keep the sample only if the timed SpMV ran a real iteration (done was 0)
+        // the sampled launch did work only for members that ran an iteration (the others were
+        // done at init, e.g. zero right-hand side, and their chunks exited at once)
+        double bytes = 0.0;
+        for (int s = 0; s < nsub; ++s)
+            if (sc_host[s].iter >= 1) bytes += fine_kernel_bytes(s);
         float ms = 0.f;
-        if (sc_host->iter >= 1 && hipEventElapsedTime(&ms, ev_k0, ev_k1) == hipSuccess && ms > 0.f) {
+        if (bytes > 0.0 && hipEventElapsedTime(&ms, ev_k0, ev_k1) == hipSuccess && ms > 0.f) {
             timed_kernel_ms += ms;
+            timed_kernel_bytes += bytes;
             timed_kernel_samples += 1;
         }
         sample_pending_ = false;
     }
-    return sc_host->done != 0;
+    for (int s = 0; s < nsub; ++s)
+        if (sc_host[s].fail) throw ApiError(DDPCA_ENUMERIC, "PCG breakdown (non-finite or non-positive curvature) in batch member " + std::to_string(s));
 }
 
-int64_t MgpisDevice::pcg_solve(int prec, double rtol, int64_t maxit, int64_t* iters, double* relres) {
-    pcg_begin(prec, rtol, maxit);
-    while (!pcg_poll()) pcg_step(prec);
-    if (sc_host->fail) throw ApiError(DDPCA_ENUMERIC, "PCG breakdown (non-finite or non-positive curvature)");
-    if (iters) *iters = sc_host->iter;
-    if (relres) *relres = sc_host->bb > 0 ? std::sqrt(sc_host->rr / sc_host->bb) : 0.0;
-    return sc_host->iter;
+void MgpisDevice::pcg_solve(int prec, double rtol, const std::vector<int64_t>& maxit, bool warm) {
+    pcg_begin(prec, rtol, maxit, warm);
+    pcg_wait(prec, 0);
+    pcg_finish();
 }
 
-void MgpisDevice::scatter_free(const double* cond, double* full) {
-    DDPCA_HIP(hipMemsetAsync(full, 0, 3 * lev.back().nn * sizeof(double), stream));
-    hipLaunchKernelGGL(k_scatter, dim3(ceil_div(nfree, kBlock)), dim3(kBlock), 0, stream, cond, free_dof.p, full, nfree);
+void MgpisDevice::scatter_free(int s, const double* cond, double* full) {
+    DDPCA_HIP(hipMemsetAsync(full + 3 * lev.back().noff[s], 0, 3 * pad64(lev.back().nloc[s]) * sizeof(double), stream));
+    hipLaunchKernelGGL(k_scatter, dim3(ceil_div(nfree[s], kBlock)), dim3(kBlock), 0, stream, cond, free_dof[s].p, full, nfree[s]);
 }
 
-void MgpisDevice::gather_free(const double* full, double* cond) {
-    hipLaunchKernelGGL(k_gather, dim3(ceil_div(nfree, kBlock)), dim3(kBlock), 0, stream, full, free_dof.p, cond, nfree);
+void MgpisDevice::gather_free(int s, const double* full, double* cond) {
+    hipLaunchKernelGGL(k_gather, dim3(ceil_div(nfree[s], kBlock)), dim3(kBlock), 0, stream, full, free_dof[s].p, cond, nfree[s]);
 }
 
 }  // namespace ddpca

@@ -1,18 +1,35 @@
 // MGPIS on the GPU: multigrid-preconditioned CG (MGPIS.h:163-225) with a V-cycle
 // (MGPIS.h:55-128) whose smoother is (block-)Jacobi or Chebyshev, built for gfx950.
 //
-// Layout in HBM (per level l, nodes in the reference's level order):
+// One MgpisDevice solves a BATCH of independent subdomains (every subdomain a rank owns) with
+// one stream and one hipGraph: level l of all subdomains is concatenated, each subdomain padded
+// to a multiple of 64 nodes so a 64-node chunk (= one wavefront) never straddles two of them.
+// Every launch therefore covers all subdomains -- the coarse levels (a few thousand nodes per
+// subdomain) get batch-wide grids instead of 8 latency-bound launches on 4 hardware queues --
+// while the PCG scalars, stop flags, smoother coefficients and coarse inverses stay per
+// subdomain (a converged subdomain's chunks exit at their first instruction).
+//
+// Node numbering: the reference numbers nodes level by level (a coarse level is a prefix of the
+// next, MULTIGRID.h:884-910), which scatters a fine node's neighbours over the whole vector.  On
+// the device every level >= 1 of every subdomain is renumbered lexicographically by (z, y, x)
+// when coordinates are supplied, and each row's blocks are sorted by the new column: the 64
+// lanes of a chunk then gather x from a few contiguous runs (measured bound: coalesced gathers
+// take the fine SpMV from 5.4 to 6.7 TB/s).  The transfer operators are explicit index lists,
+// so nothing depends on the prefix property; level 0 keeps the reference order.
+//
+// Layout in HBM (per level l, nodes in the device order inside each subdomain):
 //   K  : SELL-64 over 3x3 blocks ("SELL-BSR3"): chunk = 64 consecutive node rows = one
 //        wavefront, lane = node row; slot k of chunk c holds one block per lane:
-//          col[(off[c]+k)*64 + lane]            int32 block column
+//          col[(off[c]+k)*64 + lane]            int32 block column (batch-global node index)
 //          val[((off[c]+k)*9 + ij)*64 + lane]   fp64, ij = 3*a + b of the 3x3 block
 //        so every load of a slot is a contiguous 256 B (col) / 512 B (val) wave access.
 //        Constrained dofs are kept in place with identity rows/cols (mask), which is the
 //        reference's condensed operator consOper*K*consOper^T (MULTIGRID.h:1227) embedded
 //        in the nodal space -- the 3x3 block structure survives Dirichlet condensation.
-//   P  : scalar stencil (x) I3, fine-major (<= 8 parents, slot-major) for prolongation and
-//        coarse-major children lists for restriction (gather, deterministic, no atomics).
-//   A0^-1 : dense inverse of the coarsest level (exact coarse solve, one GEMV per cycle).
+//   P  : scalar stencil (x) I3, fine-major (<= 8 parents, slot-major; a node also present on
+//        the coarse level has itself as the only parent, weight 1) for prolongation and
+//        coarse-major child lists (self first, weight 1) for restriction: gathers, no atomics.
+//   A0^-1 : dense inverse of each subdomain's coarsest level (exact coarse solve, one GEMV).
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -25,7 +42,7 @@
 
 namespace ddpca {
 
-// Device scalar block of one PCG solve (lives in device memory, read by every kernel).
+// Per-subdomain scalar block of the PCG recurrence (device memory, read by every kernel).
 struct PcgScal {
     double delta;     // r^T z
     double alpha, beta;
@@ -39,66 +56,101 @@ struct PcgScal {
     int fail;         // 1: NaN/Inf or non-positive curvature
 };
 
+// Operators of one subdomain, in the host (MULTIGRID restatement) layout.
+struct SubdomainOps {
+    std::vector<int64_t> nnodes;           // nodes of level <= l
+    std::vector<const Bsr3*> K;            // unconstrained Galerkin operator per level
+    const uint8_t* dof_free = nullptr;     // 3 * nnodes.back() flags (consFlag)
+    std::vector<const Stencil*> S;         // scalar prolongation stencils, nlev - 1
+    const double* coords = nullptr;        // optional 3 * nnodes.back() node coordinates: when
+                                           // given, levels >= 1 are renumbered on the device
+};
+
 struct LevelDev {
-    int64_t nn = 0, nch = 0, nslots = 0, nnzb = 0;
-    DevBuf<int32_t> slots, col;
+    int64_t nn = 0, nch = 0, nslots = 0, nnzb = 0;  // batch totals (nn, nch padded)
+    std::vector<int64_t> noff, nloc, nnzb_sub;      // per subdomain: first node, real nodes, blocks
+    DevBuf<int32_t> slots, col, csub;               // csub: chunk -> subdomain
     DevBuf<int64_t> off;
-    DevBuf<double> val;
+    DevBuf<double> val;    // fp64 operator: fine level (Krylov operator), or every level when the
+                           // V-cycle runs on fp64 operators
+    DevBuf<float> val32;   // V-cycle operator rounded once to fp32 (opt.precond_fp32), levels >= 1
     DevBuf<double> minv;   // point: 3 per node; block: 9 per node
     DevBuf<double> dinv;   // point Jacobi inverse (diagonal preconditioner at the fine level)
     DevBuf<uint8_t> mask;  // bit a set = dof 3i+a free
-    // transfer from level l-1
-    int64_t nc = 0;
-    DevBuf<int32_t> ppar;  // 8 x (nn - nc), slot-major, -1 = unused
+    DevBuf<double> coef;   // [(sweep * nsub + sub) * 2 + {0,1}]: Chebyshev (c1, c2) / Jacobi (-, omega)
+    std::vector<double> lmax;  // per subdomain, lambda_max(M K)
+    // transfer from level l-1 (batch-global indices)
+    DevBuf<int32_t> ppar;  // 8 x nn, slot-major, -1 = unused
     DevBuf<double> pw;
-    DevBuf<int64_t> rptr;  // nc + 1
+    DevBuf<int64_t> rptr;  // nn_{l-1} + 1
     DevBuf<int32_t> rch;
     DevBuf<double> rw;
     // vectors (3 nn)
     DevBuf<double> x, t, b, r, d;
-    double omega = 0.0, lmax = 0.0;
 };
 
 class MgpisDevice {
 public:
-    MgpisDevice(int device, const std::vector<int64_t>& nnodes, const std::vector<const Bsr3*>& K,
-                const std::vector<uint8_t>& dof_free, const std::vector<const Stencil*>& S,
-                const mgpis_options_t& opt);
+    MgpisDevice(int device, const std::vector<SubdomainOps>& subs, const mgpis_options_t& opt);
     ~MgpisDevice();
 
     int device = 0;
+    int nsub = 0;
     hipStream_t stream = nullptr;
     mgpis_options_t opt{};
     std::vector<LevelDev> lev;
-    int64_t n0 = 0;            // coarse dofs (3 nn_0)
-    DevBuf<double> ainv;       // n0 x n0
-    int64_t nfree = 0;         // condensed fine dofs
-    DevBuf<int32_t> free_dof;  // condensed -> nodal dof (fine)
-    std::vector<int32_t> free_dof_host;
+    // exact coarse solve: per-subdomain dense inverses, packed
+    DevBuf<double> ainv;
+    DevBuf<int64_t> aoff;      // per subdomain offset into ainv
+    DevBuf<int64_t> c_noff;    // per subdomain first node of level 0
+    DevBuf<int64_t> c_n;       // per subdomain coarse dofs (3 nloc_0)
+    // device node numbering: fine_perm[s][i] = device position (inside member s's segment of
+    // the fine level) of the member's node i in the reference (level-ordered) numbering
+    std::vector<std::vector<int32_t>> fine_perm;
+    int64_t fine_dof(int s, int64_t dof) const {  // batch fine-level dof of member s's nodal dof
+        return 3 * (lev.back().noff[s] + fine_perm[s][dof / 3]) + dof % 3;
+    }
+    // condensed <-> nodal map of the fine level, per subdomain (batch-global nodal dofs)
+    std::vector<int64_t> nfree;              // per subdomain
+    std::vector<std::vector<int32_t>> free_dof_host;
+    std::vector<DevBuf<int32_t>> free_dof;
 
-    // PCG work vectors (fine level, 3 nn_L) + scalars
+    // PCG work vectors (fine level, 3 nn_L) + per-subdomain scalars
     DevBuf<double> xs, rs, zs, ps, qs, bs, partial;
     DevBuf<PcgScal> sc;
-    PcgScal* sc_host = nullptr;  // pinned mirror
-    int64_t nblk_fine = 0;
+    PcgScal* sc_host = nullptr;      // pinned, filled by pcg_finish()
+    MirrorBuf mirror;                // per-subdomain stop state, host-mapped
+    DevBuf<int64_t> fin_cb;          // per-subdomain first chunk of the fine level (nsub + 1)
+
+    int64_t fine_dof_offset(int s) const { return 3 * lev.back().noff[s]; }
+    int64_t fine_nodes(int s) const { return lev.back().nloc[s]; }
 
     // ---- operations (all asynchronous on `stream` unless stated)
-    void spmv(int level, const double* x, double* y);      // full-layout device vectors
-    void vcycle(const double* r, double* z, bool dot);     // z = M^-1 r (fine level, full layout)
-    // PCG on full-layout device vectors; b in bs, result in xs.  begin() enqueues the setup,
-    // step() enqueues one graph replay (iters_per_graph iterations), poll() reads done.
-    void pcg_begin(int prec, double rtol, int64_t maxit);
-    void pcg_step(int prec);    // one graph replay (iters_per_graph iterations)
-    bool pcg_poll();           // synchronises the stream
-    int64_t pcg_solve(int prec, double rtol, int64_t maxit, int64_t* iters, double* relres);
-    void scatter_free(const double* cond, double* full);   // device pointers
-    void gather_free(const double* full, double* cond);
+    // y = K_level x (batch nodal layout); vc_op: the V-cycle's copy of the operator
+    void spmv(int level, const double* x, double* y, bool vc_op = false);
+    bool vc32() const { return opt.precond_fp32 != 0 && lev.size() > 1; }
+    void vcycle(const double* r, double* z, bool dot);     // z = M^-1 r (fine level)
+    // PCG over every subdomain of the batch; b in bs, result in xs (x0 = xs when warm).
+    // begin() enqueues the setup, step() one graph replay (iters_per_graph iterations),
+    // wait() paces replays on the host-mapped stop flags until every subdomain is done.
+    void pcg_begin(int prec, double rtol, const std::vector<int64_t>& maxit, bool warm = false);
+    void pcg_step(int prec);
+    void pcg_wait(int prec, int64_t pre_enqueued);
+    void pcg_fetch();                  // enqueue the copy of the scalars into sc_host
+    void pcg_check();                  // after the stream synchronised: timing sample, breakdown
+    void pcg_finish();                 // fetch + synchronise + check
+    void pcg_solve(int prec, double rtol, const std::vector<int64_t>& maxit, bool warm = false);
+    void scatter_free(int s, const double* cond, double* full);   // device pointers
+    void gather_free(int s, const double* full, double* cond);
     // timing of the fine-level SpMV (HIP events around it in the eager first iteration)
     hipEvent_t ev_k0 = nullptr, ev_k1 = nullptr;
     double timed_kernel_ms = 0.0;
+    double timed_kernel_bytes = 0.0;  // algorithmic bytes of the sampled launches (active members)
     int64_t timed_kernel_samples = 0;
     bool time_kernel = false;
-    double fine_kernel_bytes() const;  // algorithmic bytes of the timed kernel
+    double fine_kernel_bytes(int s) const;  // algorithmic bytes of the timed kernel, member s
+    double bench_spmv(int variant, int reps);  // ms per launch of a fine-level SpMV loop variant
+    int64_t graphs_launched = 0;
 
 private:
     hipGraphExec_t graph_[2] = {nullptr, nullptr};

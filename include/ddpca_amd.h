@@ -43,6 +43,12 @@ typedef struct {
     int nu;            /* sweeps (Jacobi) or polynomial degree (Chebyshev) pre and post */
     double omega;      /* Jacobi damping; <= 0: 4 / (3 * lambda_max(D^-1 K)) estimated at create */
     int iters_per_graph; /* PCG iterations captured per hipGraph replay (>= 1) */
+    int warm_start;    /* MCONTACT loop only: start each subdomain PCG from its previous solution
+                          instead of x0 = 0 (MGPIS.h:168); same ||r|| <= rtol ||b|| stop rule */
+    int precond_fp32;  /* 1: the V-cycle's level operators are stored rounded to fp32 (once, at
+                          create; still exactly symmetric, all arithmetic fp64).  The Krylov
+                          operator, vectors and the stop rule stay fp64, so the solution meets the
+                          same ||r|| <= rtol ||b||; only the preconditioner differs slightly. */
 } mgpis_options_t;
 
 /* Fill default options. */
@@ -88,6 +94,13 @@ int mgpis_gpu_spmv(mgpis_t h, int level, const double* x, double* y);
 int mgpis_gpu_vcycle(mgpis_t h, const double* r, double* z);
 /* Informational: [nlev, n_fine_free, nnzb_fine, chunks_fine, omega*1e6, lambda_max*1e6, device] */
 int mgpis_gpu_info(mgpis_t h, int64_t* out7);
+/* Diagnostic (no reference counterpart): average ms per launch of a fine-level SELL-BSR3
+ * kernel over `reps` back-to-back launches on this operator.  variant = loop (0 cached x3
+ * unroll, 1 non-temporal matrix loads, 2 column prefetch + non-temporal, 3 a bound only: x
+ * gathered at the row's own node, wrong values) + 4 * mode (0 y = Kx, 1 PCG q = Kz + beta q,
+ * p = z + beta p with p.q, 2 residual b - Kx, 3 Chebyshev sweep on block Jacobi).
+ * bytes (may be NULL) = algorithmic bytes per launch. */
+int mgpis_gpu_bench_spmv(mgpis_t h, int variant, int reps, double* ms, double* bytes);
 int mgpis_gpu_destroy(mgpis_t h);
 
 /* ========================================================================================

@@ -40,9 +40,13 @@ def _rows_close(rows, ref, k=50, rtol=1e-7, floor=1e-12):
     return ok.all(), (err / np.maximum(np.abs(b), floor * scale)).max()
 
 
+@pytest.mark.parametrize("warm,f32", [(0, 0), (1, 0), (0, 1)])
 @pytest.mark.parametrize("case", ["twoblock_f0", "twoblock_f3", "beam_dd"])
-def test_admm_matches_reference(ddpca, gpu, case):
-    g, P, mc, n = _run(ddpca, case)
+def test_admm_matches_reference(ddpca, gpu, case, warm, f32):
+    """warm = 1 starts every subdomain PCG from its previous solution; f32 = 1 stores the V-cycle
+    operators in fp32 (precond_fp32).  Both keep the ||r|| <= 1e-14 ||b|| stop rule of MGPIS.h:198
+    on the fp64 operator, so neither may move the trajectory beyond the PCG accuracy."""
+    g, P, mc, n = _run(ddpca, case, warm_start=warm, precond_fp32=f32, smoother=2, nu=2)
     ref_iters = len(g["resuMoni"])
     assert abs(n - ref_iters) <= 1, (n, ref_iters)
     ok, worst = _rows_close(mc.monitor(), g["resuMoni"])

@@ -48,6 +48,22 @@ def test_cg_solution_matches_reference(ddpca, gpu, case, smoother, nu):
     assert np.linalg.norm(x - xr) <= 1e-8 * np.linalg.norm(xr), (it, np.linalg.norm(x - xr) / np.linalg.norm(xr))
 
 
+@pytest.mark.parametrize("case", ["beam_s1", "beam_s2", "beam_gl1"])
+def test_fp32_stored_preconditioner_keeps_the_solution(ddpca, gpu, case):
+    """precond_fp32: the V-cycle's level operators rounded once to fp32.  The Krylov operator and
+    the stop rule stay fp64, so the solution still meets ||r|| <= 1e-14 ||b|| and matches the
+    reference's CG_SOLV result like the fp64 path; the preconditioner changes only slightly, so
+    the iteration count stays within 2 of the fp64-preconditioned run."""
+    g = golden(case)
+    P = _problem(ddpca, case)
+    b = P.grid(0).consForc
+    x64, it64, _ = ddpca.MGPIS.from_problem(P, 0, smoother=2, nu=2).CG_SOLV(1, b)
+    x32, it32, rr = ddpca.MGPIS.from_problem(P, 0, smoother=2, nu=2, precond_fp32=1).CG_SOLV(1, b)
+    assert rr <= 1e-14
+    assert abs(it32 - it64) <= 2, (it32, it64)
+    assert np.linalg.norm(x32 - g["x_mg"]) <= 1e-8 * np.linalg.norm(g["x_mg"])
+
+
 @pytest.mark.parametrize("case", ["beam_s1", "beam_gl1"])
 def test_diag_pcg_matches_reference(ddpca, gpu, case):
     g = golden(case)
@@ -70,8 +86,8 @@ def test_vcycle_is_symmetric_positive(ddpca, gpu):
     P = _problem(ddpca, "beam_s2")
     n = len(P.grid(0).consForc)
     rng = np.random.default_rng(20251017)
-    for smoother, nu in [(0, 1), (1, 1), (2, 2)]:
-        M = ddpca.MGPIS.from_problem(P, 0, smoother=smoother, nu=nu)
+    for smoother, nu, f32 in [(0, 1, 0), (1, 1, 0), (2, 2, 0), (2, 2, 1)]:
+        M = ddpca.MGPIS.from_problem(P, 0, smoother=smoother, nu=nu, precond_fp32=f32)
         u, v = rng.standard_normal(n), rng.standard_normal(n)
         Mu, Mv = M.MULT_VCYC(u), M.MULT_VCYC(v)
         assert abs(u @ Mv - v @ Mu) <= 1e-10 * abs(u @ Mv)
@@ -79,7 +95,10 @@ def test_vcycle_is_symmetric_positive(ddpca, gpu):
 
 
 def test_csr_dropin_matches_native(ddpca, gpu):
-    """mgpis_gpu_create from the reference layout (condensed CSR) == the native BSR3 create."""
+    """mgpis_gpu_create from the reference layout (condensed CSR) == the native create.  The CSR
+    entry point has no coordinates, so it keeps the reference node order while the native create
+    renumbers levels >= 1 for gather locality: the sums run in another order, so the two agree
+    to the solver accuracy (iterations +-2, solutions 1e-10), not bit for bit."""
     g = golden("beam_s1")
     P = _problem(ddpca, "beam_s1")
     G = P.grid(0)
@@ -96,6 +115,6 @@ def test_csr_dropin_matches_native(ddpca, gpu):
     b = G.consForc
     x1, i1, _ = M1.CG_SOLV(1, b)
     x2, i2, _ = M2.CG_SOLV(1, b)
-    assert i1 == i2
-    assert np.linalg.norm(x1 - x2) <= 1e-12 * np.linalg.norm(x2)
+    assert abs(i1 - i2) <= 2
+    assert np.linalg.norm(x1 - x2) <= 1e-10 * np.linalg.norm(x2)
     assert np.linalg.norm(x1 - g["x_mg"]) <= 1e-8 * np.linalg.norm(g["x_mg"])
