@@ -51,6 +51,11 @@ _I64P = C.POINTER(C.c_int64)
 _DP = C.POINTER(C.c_double)
 
 
+class _CsrArg(C.Structure):  # ddpca_csr_t
+    _fields_ = [("nrow", C.c_int64), ("ncol", C.c_int64), ("ptr", C.c_void_p), ("col", C.c_void_p),
+                ("val", C.c_void_p)]
+
+
 def _declare(L: C.CDLL) -> None:
     L.ddpca_last_error.restype = C.c_char_p
     L.ddpca_gpu_available.restype = C.c_int
@@ -65,6 +70,11 @@ def _declare(L: C.CDLL) -> None:
                                      C.POINTER(C.c_int)]
     L.ddpca_problem_destroy.argtypes = [_P]
     L.ddpca_problem_mgpis.argtypes = [_P, C.c_int64, C.c_int, C.POINTER(MgpisOptions), C.POINTER(_P)]
+    L.ddpca_problem_empty.argtypes = [C.c_int64, C.c_int64, C.POINTER(_P)]
+    L.ddpca_problem_set_subdomain.argtypes = [_P, C.c_int64, C.c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]
+    L.ddpca_problem_set_interface.argtypes = [_P, C.c_int64, C.c_int64, C.c_int64, C.c_double, C.c_int64, C.c_int64,
+                                              C.c_int64, _P, _P, C.POINTER(_CsrArg)]
+    L.ddpca_problem_finalize.argtypes = [_P]
     L.mgpis_gpu_create.argtypes = [C.c_int, C.c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P,
                                    C.POINTER(MgpisOptions), C.POINTER(_P)]
     L.mgpis_gpu_create_bsr3.argtypes = [C.c_int, C.c_int, _P, _P, _P, _P, _P, _P, _P, _P,
@@ -187,6 +197,90 @@ class Problem:
 
     def grid(self, tv: int = 0) -> "MULTIGRID":
         return MULTIGRID(self, tv)
+
+    # ---- operator-level builder (ddpca_problem_empty / set_subdomain / set_interface / finalize)
+    IFACE_OPS = ("inpoLagr", "pemaInpo_r", "systTran", "systTran_pena", "inteMass", "inteMass_pena", "inteInpo")
+
+    @classmethod
+    def from_operators(cls, subdomains: Sequence[dict], interfaces: Sequence[dict]) -> "Problem":
+        """Established problem from operators in the reference's layouts (no host restatement).
+
+        subdomains[tv]: nnodes (per level), free_dof (per level, increasing nodal dofs), K (per
+        level, condensed consStif CSR), S (per level < L, scalar stencil CSR), consForc, and
+        optionally presc (3N nodal Dirichlet values) and coords (N x 3).
+        interfaces[ts]: body (2), fric, nip, nnc (2), pemaDiag, inpoNgap, ops[s][name] CSR for
+        the names in Problem.IFACE_OPS."""
+        self = cls.__new__(cls)
+        h = C.c_void_p()
+        _check(lib().ddpca_problem_empty(len(subdomains), len(interfaces), C.byref(h)))
+        self._h = h
+        self.kind = "operators"
+        keep = []
+
+        def arr(a, dt):
+            a = np.ascontiguousarray(a, dtype=dt)
+            keep.append(a)
+            return a
+
+        def ptrs(lst, ctype):
+            p = (C.c_void_p * max(1, len(lst)))(*[a.ctypes.data for a in lst])
+            keep.append(p)
+            return p
+
+        for tv, s in enumerate(subdomains):
+            nlev = len(s["nnodes"])
+            K = [m.tocsr() for m in s["K"]]
+            S = [m.tocsr() for m in s.get("S", [])]
+            presc = s.get("presc")
+            coords = s.get("coords")
+            _check(lib().ddpca_problem_set_subdomain(
+                self._h, tv, nlev, _ptr(arr(s["nnodes"], np.int64)), _ptr(arr([m.shape[0] for m in K], np.int64)),
+                ptrs([arr(f, np.int32) for f in s["free_dof"]], None),
+                ptrs([arr(m.indptr, np.int64) for m in K], None), ptrs([arr(m.indices, np.int32) for m in K], None),
+                ptrs([arr(m.data, np.float64) for m in K], None),
+                ptrs([arr(m.indptr, np.int64) for m in S], None), ptrs([arr(m.indices, np.int32) for m in S], None),
+                ptrs([arr(m.data, np.float64) for m in S], None), _ptr(arr(s["consForc"], np.float64)),
+                None if presc is None else _ptr(arr(presc, np.float64)),
+                None if coords is None else _ptr(arr(np.asarray(coords).reshape(-1), np.float64))))
+        for ts, f in enumerate(interfaces):
+            ops = (_CsrArg * 14)()
+            for side in range(2):
+                for k, name in enumerate(cls.IFACE_OPS):
+                    m = f["ops"][side][name].tocsr()
+                    ops[7 * side + k] = _CsrArg(m.shape[0], m.shape[1], _ptr(arr(m.indptr, np.int64)),
+                                                _ptr(arr(m.indices, np.int32)), _ptr(arr(m.data, np.float64)))
+            _check(lib().ddpca_problem_set_interface(
+                self._h, ts, int(f["body"][0]), int(f["body"][1]), float(f["fric"]), int(f["nip"]), int(f["nnc"][0]),
+                int(f["nnc"][1]), _ptr(arr(f["pemaDiag"], np.float64)), _ptr(arr(f["inpoNgap"], np.float64)), ops))
+        _check(lib().ddpca_problem_finalize(self._h))
+        return self
+
+    def export_operators(self) -> tuple:
+        """(subdomains, interfaces) of an established problem in from_operators' format -- what a
+        reference-side caller would hand over from its own MCONTACT after ESTABLISH."""
+        import scipy.sparse as sp
+        subs = []
+        for tv in range(self.nsub):
+            G = self.grid(tv)
+            L = G.maxiLeve
+            nn = [int(x) for x in self.array("leveCount", tv)]
+            flag = G.consFlag
+            S = [sp.csr_matrix((self.array("S:w", tv, l), self.array("S:col", tv, l), self.array("S:ptr", tv, l)),
+                               shape=(nn[l + 1], nn[l])) for l in range(L)]
+            presc = np.zeros(3 * nn[-1])
+            presc[self.array("consDofv", tv)] = self.array("dispForc", tv)  # both in constrained-dof order
+            subs.append(dict(nnodes=nn, free_dof=[np.flatnonzero(flag[: 3 * nn[l]]) for l in range(L + 1)],
+                             K=[G.consStif(l) for l in range(L + 1)], S=S, consForc=G.consForc, presc=presc,
+                             coords=G.nodeCoor))
+        ifaces = []
+        for ts in range(self.nint):
+            fric = float(self.array("iface_param", ts)[0])
+            ifaces.append(dict(body=[int(b) for b in self.array("iface_body", ts)], fric=fric,
+                               nip=len(self.array("ip_w", ts)),
+                               nnc=[len(self.array("nodeCont", 2 * ts + s)) for s in range(2)],
+                               pemaDiag=self.array("pemaDiag", ts), inpoNgap=self.array("inpoNgap", ts),
+                               ops=[{n: self.csr(n, 2 * ts + s) for n in self.IFACE_OPS} for s in range(2)]))
+        return subs, ifaces
 
 
 class MULTIGRID:

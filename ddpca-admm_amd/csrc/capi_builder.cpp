@@ -1,0 +1,177 @@
+// C ABI: operator-level problem builder.  A caller that already owns the reference's operators
+// (its MULTIGRID/MGPIS hierarchy per subdomain and the interface operators MCONTACT::ESTABLISH
+// produced, MCONTACT.h:181-896) hands them over in the reference's own layouts, and the result
+// is an established ddpca_problem_t that mcontact_gpu_create / ddpca_problem_mgpis accept --
+// the host restatement (multigrid.cpp, mcontact.cpp) is bypassed entirely.
+#include <cstring>
+#include <memory>
+#include <string>
+
+#include "../../include/ddpca_amd.h"
+#include "common.hpp"
+#include "problem.hpp"
+
+using namespace ddpca;
+
+namespace {
+
+Csr to_csr(const ddpca_csr_t& m, const char* what) {
+    if (m.nrow < 0 || m.ncol < 0 || (!m.ptr && m.nrow > 0)) throw ApiError(DDPCA_EINVAL, std::string(what) + ": bad CSR");
+    Csr c;
+    c.nrow = m.nrow;
+    c.ncol = m.ncol;
+    c.ptr.assign(m.ptr, m.ptr + m.nrow + 1);
+    if (m.nrow == 0) c.ptr.assign(1, 0);
+    const int64_t nnz = c.ptr.back();
+    if (nnz < 0 || (nnz > 0 && (!m.col || !m.val))) throw ApiError(DDPCA_EINVAL, std::string(what) + ": bad CSR");
+    c.col.assign(m.col, m.col + nnz);
+    c.val.assign(m.val, m.val + nnz);
+    for (int64_t r = 0; r < c.nrow; ++r)
+        if (c.ptr[r + 1] < c.ptr[r]) throw ApiError(DDPCA_EINVAL, std::string(what) + ": row pointer not monotone");
+    for (int32_t j : c.col)
+        if (j < 0 || j >= c.ncol) throw ApiError(DDPCA_EINVAL, std::string(what) + ": column out of range");
+    return c;
+}
+
+void expect_shape(const Csr& c, int64_t r, int64_t k, const char* what) {
+    if (c.nrow != r || c.ncol != k)
+        throw ApiError(DDPCA_EINVAL, std::string(what) + ": shape " + std::to_string(c.nrow) + "x" + std::to_string(c.ncol) +
+                                         ", expected " + std::to_string(r) + "x" + std::to_string(k));
+}
+
+Problem& builder(ddpca_problem_t h) {
+    Problem& P = *reinterpret_cast<Problem*>(h);
+    if (P.established) throw ApiError(DDPCA_ESTATE, "problem already established");
+    return P;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ddpca_problem_empty(int64_t nsub, int64_t nint, ddpca_problem_t* out) {
+    return guarded([&] {
+        if (nsub < 1 || nint < 0 || !out) throw ApiError(DDPCA_EINVAL, "nsub >= 1, nint >= 0");
+        auto P = std::make_unique<Problem>();
+        P->mc.multGrid.resize(nsub);
+        P->mc.searCont.resize(nint);
+        P->owned.assign(nsub, 0);
+        *out = reinterpret_cast<ddpca_problem_t>(P.release());
+    });
+}
+
+int ddpca_problem_set_subdomain(ddpca_problem_t h, int64_t tv, int nlev, const int64_t* nnodes, const int64_t* nfree,
+                                const int32_t* const* free_dof, const int64_t* const* K_ptr,
+                                const int32_t* const* K_col, const double* const* K_val,
+                                const int64_t* const* S_ptr, const int32_t* const* S_col,
+                                const double* const* S_w, const double* consForc, const double* presc,
+                                const double* coords) {
+    return guarded([&] {
+        Problem& P = builder(h);
+        if (tv < 0 || tv >= (int64_t)P.mc.multGrid.size()) throw ApiError(DDPCA_EINVAL, "subdomain index");
+        if (nlev < 1 || !nnodes || !nfree || !free_dof || !K_ptr || !K_col || !K_val || !consForc)
+            throw ApiError(DDPCA_EINVAL, "null argument");
+        if (nlev > 1 && (!S_ptr || !S_col || !S_w)) throw ApiError(DDPCA_EINVAL, "stencils missing");
+        for (int l = 0; l < nlev; ++l) {
+            if (nnodes[l] < 1 || (l > 0 && nnodes[l] < nnodes[l - 1])) throw ApiError(DDPCA_EINVAL, "nnodes must grow by level");
+            if (nfree[l] < 0 || nfree[l] > 3 * nnodes[l]) throw ApiError(DDPCA_EINVAL, "nfree out of range");
+        }
+        MULTIGRID g;
+        const int64_t N = nnodes[nlev - 1];
+        g.maxiLeve = nlev - 1;
+        g.leveCount.assign(nnodes, nnodes + nlev);
+        g.freeCount.assign(nfree, nfree + nlev);
+        g.levelStif.resize(nlev);
+        for (int l = 0; l < nlev; ++l) {
+            // the level-l free dofs must be the level-(l+1) free dofs of the first nnodes[l] nodes
+            // (level-ordered numbering, MULTIGRID.h:884-910)
+            for (int64_t r = 0; r < nfree[l]; ++r)
+                if (free_dof[l][r] < 0 || free_dof[l][r] >= 3 * nnodes[l] || (r && free_dof[l][r] <= free_dof[l][r - 1]))
+                    throw ApiError(DDPCA_EINVAL, "free_dof[" + std::to_string(l) + "] must be increasing nodal dofs of the level");
+            g.levelStif[l] = condensed_to_bsr3(nnodes[l], nfree[l], free_dof[l], K_ptr[l], K_col[l], K_val[l]);
+        }
+        for (int l = 0; l + 1 < nlev; ++l) g.scalProl.push_back(make_stencil(nnodes[l + 1], nnodes[l], S_ptr[l], S_col[l], S_w[l]));
+        g.consFlag.assign(3 * N, 0);
+        g.freeIndex.assign(3 * N, -1);
+        for (int64_t r = 0; r < nfree[nlev - 1]; ++r) {
+            g.consFlag[free_dof[nlev - 1][r]] = 1;
+            g.freeIndex[free_dof[nlev - 1][r]] = (int32_t)r;
+        }
+        for (int l = 0; l + 1 < nlev; ++l)
+            for (int64_t r = 0; r < nfree[l]; ++r)
+                if (!g.consFlag[free_dof[l][r]]) throw ApiError(DDPCA_EINVAL, "coarse free dof constrained on the fine level");
+        g.consForc.assign(consForc, consForc + nfree[nlev - 1]);
+        g.dispForc.clear();  // constrained dofs' values in dof order (MULTIGRID::CONSTRAINT layout)
+        for (int64_t d = 0; d < 3 * N; ++d)
+            if (!g.consFlag[d]) {
+                const double v = presc ? presc[d] : 0.0;
+                g.consDofv[d] = v;
+                g.dispForc.push_back(v);
+            }
+        if (coords) {
+            g.nodeCoor.resize(N);
+            for (int64_t i = 0; i < N; ++i)
+                for (int a = 0; a < 3; ++a) g.nodeCoor[i][a] = coords[3 * i + a];
+        }
+        P.mc.multGrid[tv] = std::move(g);
+        P.owned[tv] = 1;
+    });
+}
+
+int ddpca_problem_set_interface(ddpca_problem_t h, int64_t ts, int64_t body0, int64_t body1, double fric,
+                                int64_t nip, int64_t nnc0, int64_t nnc1, const double* pemaDiag,
+                                const double* inpoNgap, const ddpca_csr_t* ops) {
+    return guarded([&] {
+        Problem& P = builder(h);
+        const int64_t nsub = (int64_t)P.mc.multGrid.size();
+        if (ts < 0 || ts >= (int64_t)P.mc.searCont.size()) throw ApiError(DDPCA_EINVAL, "interface index");
+        if (body0 < 0 || body0 >= nsub || body1 < 0 || body1 >= nsub || body0 == body1)
+            throw ApiError(DDPCA_EINVAL, "interface bodies");
+        if (nip < 0 || nnc0 < 0 || nnc1 < 0 || !ops || (nip > 0 && (!pemaDiag || !inpoNgap)))
+            throw ApiError(DDPCA_EINVAL, "null argument");
+        Interface I;
+        I.body[0] = body0;
+        I.body[1] = body1;
+        I.fric = fric;
+        I.ip.resize(nip);  // the device path needs the count only; the geometry stays with the caller
+        I.nodeCont[0].resize(nnc0);
+        I.nodeCont[1].resize(nnc1);
+        const int64_t mip = I.mip();
+        I.pemaDiag.assign(pemaDiag, pemaDiag + mip);
+        I.inpoNgap.assign(inpoNgap, inpoNgap + mip);
+        static const char* kName[7] = {"inpoLagr", "pemaInpo_r", "systTran", "systTran_pena", "inteMass",
+                                       "inteMass_pena", "inteInpo"};
+        for (int s = 0; s < 2; ++s) {
+            const ddpca_csr_t* o = ops + 7 * s;
+            Csr* dst[7] = {&I.inpoLagr[s], &I.pemaInpo_r[s], &I.systTran[s], &I.systTran_pena[s], &I.inteMass[s],
+                           &I.inteMass_pena[s], &I.inteInpo[s]};
+            for (int k = 0; k < 7; ++k) *dst[k] = to_csr(o[k], kName[k]);
+            const int64_t m = I.mside(s);
+            if (P.mc.multGrid[I.body[s]].leveCount.empty())
+                throw ApiError(DDPCA_ESTATE, "set the interface's subdomains before the interface");
+            const int64_t n3 = 3 * P.mc.multGrid[I.body[s]].leveCount.back();
+            expect_shape(I.inpoLagr[s], mip, m, "inpoLagr");
+            expect_shape(I.pemaInpo_r[s], mip, n3, "pemaInpo_r");
+            expect_shape(I.systTran[s], n3, m, "systTran");
+            expect_shape(I.systTran_pena[s], n3, m, "systTran_pena");
+            expect_shape(I.inteMass[s], m, m, "inteMass");
+            expect_shape(I.inteMass_pena[s], m, m, "inteMass_pena");
+            expect_shape(I.inteInpo[s], m, mip, "inteInpo");
+        }
+        P.mc.searCont[ts] = std::move(I);
+    });
+}
+
+int ddpca_problem_finalize(ddpca_problem_t h) {
+    return guarded([&] {
+        Problem& P = builder(h);
+        for (size_t tv = 0; tv < P.mc.multGrid.size(); ++tv)
+            if (!P.owned[tv]) throw ApiError(DDPCA_ESTATE, "subdomain " + std::to_string(tv) + " was not set");
+        for (size_t ts = 0; ts < P.mc.searCont.size(); ++ts)
+            if (P.mc.searCont[ts].inteMass[0].ptr.empty())
+                throw ApiError(DDPCA_ESTATE, "interface " + std::to_string(ts) + " was not set");
+        P.established = true;
+    });
+}
+
+}  // extern "C"

@@ -18,52 +18,6 @@ struct ddpca_mgpis {
 
 namespace {
 
-// Condensed CSR (reference consStif[l]) + free_dof map -> unconstrained-layout BSR3 whose
-// constrained rows/cols are zero (the device masks them to identity anyway).
-Bsr3 csr_to_bsr3(int64_t nn, int64_t nfree, const int32_t* free_dof, const int64_t* ptr, const int32_t* col,
-                 const double* val) {
-    std::vector<std::vector<std::pair<int32_t, int>>> rows(nn);
-    std::vector<std::vector<int32_t>> bcols(nn);
-    for (int64_t r = 0; r < nfree; ++r) {
-        const int32_t dr = free_dof[r];
-        for (int64_t k = ptr[r]; k < ptr[r + 1]; ++k) bcols[dr / 3].push_back(free_dof[col[k]] / 3);
-    }
-    Bsr3 B;
-    B.nb = B.mb = nn;
-    B.ptr.assign(nn + 1, 0);
-    for (int64_t i = 0; i < nn; ++i) {
-        bcols[i].push_back((int32_t)i);  // keep the diagonal block even for fully constrained nodes
-        std::sort(bcols[i].begin(), bcols[i].end());
-        bcols[i].erase(std::unique(bcols[i].begin(), bcols[i].end()), bcols[i].end());
-        B.ptr[i + 1] = B.ptr[i] + (int64_t)bcols[i].size();
-    }
-    B.col.resize(B.ptr[nn]);
-    B.val.assign(9 * B.ptr[nn], 0.0);
-    for (int64_t i = 0; i < nn; ++i) std::copy(bcols[i].begin(), bcols[i].end(), B.col.begin() + B.ptr[i]);
-    for (int64_t r = 0; r < nfree; ++r) {
-        const int32_t dr = free_dof[r];
-        const int64_t i = dr / 3;
-        const int32_t* cb = &B.col[B.ptr[i]];
-        const int64_t len = B.ptr[i + 1] - B.ptr[i];
-        for (int64_t k = ptr[r]; k < ptr[r + 1]; ++k) {
-            const int32_t dc = free_dof[col[k]];
-            const int64_t pos = B.ptr[i] + (std::lower_bound(cb, cb + len, dc / 3) - cb);
-            B.val[9 * pos + 3 * (dr % 3) + dc % 3] += val[k];
-        }
-    }
-    return B;
-}
-
-Stencil make_stencil(int64_t nf, int64_t nc, const int64_t* ptr, const int32_t* col, const double* w) {
-    Stencil S;
-    S.nf = nf;
-    S.nc = nc;
-    S.ptr.assign(ptr, ptr + nf + 1);
-    S.col.assign(col, col + ptr[nf]);
-    S.w.assign(w, w + ptr[nf]);
-    return S;
-}
-
 mgpis_options_t resolve(const mgpis_options_t* opt) {
     mgpis_options_t o;
     mgpis_default_options(&o);
@@ -113,7 +67,7 @@ int mgpis_gpu_create(int device, int nlev, const int64_t* nnodes, const int64_t*
             throw ApiError(DDPCA_EINVAL, "null argument");
         std::vector<Bsr3> B(nlev);
         std::vector<Stencil> S(nlev - 1);
-        for (int l = 0; l < nlev; ++l) B[l] = csr_to_bsr3(nnodes[l], nfree[l], free_dof[l], K_ptr[l], K_col[l], K_val[l]);
+        for (int l = 0; l < nlev; ++l) B[l] = condensed_to_bsr3(nnodes[l], nfree[l], free_dof[l], K_ptr[l], K_col[l], K_val[l]);
         for (int l = 0; l + 1 < nlev; ++l) S[l] = make_stencil(nnodes[l + 1], nnodes[l], S_ptr[l], S_col[l], S_w[l]);
         const int64_t nn = nnodes[nlev - 1];
         std::vector<uint8_t> fr(3 * nn, 0);

@@ -551,7 +551,7 @@ void build(ddpca_mcontact& H, Problem& P) {
         ops.push_back(o);
         ddpca_mcontact::Sub S;
         S.tv = tv;
-        S.nn = g.numNodes();
+        S.nn = g.leveCount.back();
         H.subs.push_back(S);
     }
     if (!ops.empty()) {

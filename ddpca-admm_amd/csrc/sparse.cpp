@@ -4,6 +4,7 @@
 #include <algorithm>
 #include <numeric>
 #include <omp.h>
+#include <stdexcept>
 
 namespace ddpca {
 
@@ -133,6 +134,59 @@ Csr condense(const Bsr3& A, const std::vector<int32_t>& free_index, int64_t nfre
                 }
         }
     return C;
+}
+
+}  // namespace ddpca
+
+namespace ddpca {
+
+Bsr3 condensed_to_bsr3(int64_t nn, int64_t nfree, const int32_t* free_dof, const int64_t* ptr, const int32_t* col,
+                       const double* val) {
+    std::vector<std::vector<int32_t>> bcols(nn);
+    for (int64_t r = 0; r < nfree; ++r) {
+        const int32_t dr = free_dof[r];
+        if (dr < 0 || dr >= 3 * nn) throw std::invalid_argument("free dof out of range");
+        for (int64_t k = ptr[r]; k < ptr[r + 1]; ++k) {
+            if (col[k] < 0 || col[k] >= nfree) throw std::invalid_argument("column out of range");
+            bcols[dr / 3].push_back(free_dof[col[k]] / 3);
+        }
+    }
+    Bsr3 B;
+    B.nb = B.mb = nn;
+    B.ptr.assign(nn + 1, 0);
+    for (int64_t i = 0; i < nn; ++i) {
+        bcols[i].push_back((int32_t)i);
+        std::sort(bcols[i].begin(), bcols[i].end());
+        bcols[i].erase(std::unique(bcols[i].begin(), bcols[i].end()), bcols[i].end());
+        B.ptr[i + 1] = B.ptr[i] + (int64_t)bcols[i].size();
+    }
+    B.col.resize(B.ptr[nn]);
+    B.val.assign(9 * B.ptr[nn], 0.0);
+    for (int64_t i = 0; i < nn; ++i) std::copy(bcols[i].begin(), bcols[i].end(), B.col.begin() + B.ptr[i]);
+    for (int64_t r = 0; r < nfree; ++r) {
+        const int32_t dr = free_dof[r];
+        const int64_t i = dr / 3;
+        const int32_t* cb = &B.col[B.ptr[i]];
+        const int64_t len = B.ptr[i + 1] - B.ptr[i];
+        for (int64_t k = ptr[r]; k < ptr[r + 1]; ++k) {
+            const int32_t dc = free_dof[col[k]];
+            const int64_t pos = B.ptr[i] + (std::lower_bound(cb, cb + len, dc / 3) - cb);
+            B.val[9 * pos + 3 * (dr % 3) + dc % 3] += val[k];
+        }
+    }
+    return B;
+}
+
+Stencil make_stencil(int64_t nf, int64_t nc, const int64_t* ptr, const int32_t* col, const double* w) {
+    Stencil S;
+    S.nf = nf;
+    S.nc = nc;
+    S.ptr.assign(ptr, ptr + nf + 1);
+    S.col.assign(col, col + ptr[nf]);
+    S.w.assign(w, w + ptr[nf]);
+    for (int32_t c : S.col)
+        if (c < 0 || c >= nc) throw std::invalid_argument("stencil column out of range");
+    return S;
 }
 
 }  // namespace ddpca

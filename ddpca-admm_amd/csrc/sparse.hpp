@@ -52,4 +52,13 @@ Bsr3 galerkin_rap(const Bsr3& A, const Stencil& S);
 // MULTIGRID.h:1213-1227).  free_index[dof] = condensed index or -1.
 Csr condense(const Bsr3& A, const std::vector<int32_t>& free_index, int64_t nfree);
 
+// Inverse direction, from the reference's layout: condensed CSR (consStif[l], nfree rows) and
+// its free-dof map (condensed row -> nodal dof 3*node + comp) -> node-block BSR3 on nn nodes
+// whose constrained rows/cols are zero (the device masks them to identity); every node keeps
+// its diagonal block.
+Bsr3 condensed_to_bsr3(int64_t nn, int64_t nfree, const int32_t* free_dof, const int64_t* ptr, const int32_t* col,
+                       const double* val);
+
+Stencil make_stencil(int64_t nf, int64_t nc, const int64_t* ptr, const int32_t* col, const double* w);
+
 }  // namespace ddpca

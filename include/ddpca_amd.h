@@ -138,12 +138,51 @@ int ddpca_problem_destroy(ddpca_problem_t p);
 int ddpca_problem_mgpis(ddpca_problem_t p, int64_t tv, int device, const mgpis_options_t* opt,
                         mgpis_t* out);
 
+/* ---- Operator-level builder: a caller that already holds the reference's operators (its
+ * MULTIGRID/MGPIS hierarchy per subdomain and the interface operators of MCONTACT::ESTABLISH,
+ * MCONTACT.h:181-896) hands them over in the reference's layouts; after finalize the problem
+ * is established and mcontact_gpu_create / ddpca_problem_mgpis accept it.  The host
+ * restatement is bypassed. */
+typedef struct {
+    int64_t nrow, ncol;
+    const int64_t* ptr;  /* nrow + 1 */
+    const int32_t* col;
+    const double* val;
+} ddpca_csr_t;
+
+int ddpca_problem_empty(int64_t nsub, int64_t nint, ddpca_problem_t* out);
+/* Subdomain tv: the MGPIS hierarchy exactly as mgpis_gpu_create takes it (nnodes, nfree,
+ * free_dof, consStif[l] CSR, scalar stencils scalProl[l]), consForc (nfree[nlev-1] condensed
+ * load, MULTIGRID::consForc), presc (3*nnodes[nlev-1] nodal values, read at constrained dofs:
+ * the Dirichlet values OUTP_SUB1 writes, MULTIGRID.h:1263-1281; NULL = 0) and coords
+ * (3*nnodes[nlev-1] node coordinates, level-ordered; NULL = keep the reference node order on
+ * the device). */
+int ddpca_problem_set_subdomain(ddpca_problem_t p, int64_t tv, int nlev, const int64_t* nnodes,
+                                const int64_t* nfree, const int32_t* const* free_dof,
+                                const int64_t* const* K_ptr, const int32_t* const* K_col,
+                                const double* const* K_val, const int64_t* const* S_ptr,
+                                const int32_t* const* S_col, const double* const* S_w,
+                                const double* consForc, const double* presc, const double* coords);
+/* Interface ts between contBody {body0, body1} with fricCoef fric (< 0 glued, 0 frictionless,
+ * > 0 Coulomb; comp = 1 if fric == 0 else 3), nip integration points, nnc_s contact nodes per
+ * side; pemaDiag / inpoNgap have comp*nip entries.  ops[7*s + k] is side s's
+ *   k = 0 inpoLagr (comp*nip x comp*nnc_s)     1 pemaInpo_r (comp*nip x 3N_s)
+ *       2 systTran (3N_s x comp*nnc_s)         3 systTran_pena (3N_s x comp*nnc_s)
+ *       4 inteMass (comp*nnc_s square)          5 inteMass_pena (comp*nnc_s square)
+ *       6 inteInpo (comp*nnc_s x comp*nip)
+ * (MCONTACT.h:213-810).  Set both subdomains first. */
+int ddpca_problem_set_interface(ddpca_problem_t p, int64_t ts, int64_t body0, int64_t body1, double fric,
+                                int64_t nip, int64_t nnc0, int64_t nnc1, const double* pemaDiag,
+                                const double* inpoNgap, const ddpca_csr_t* ops);
+/* Check that every subdomain and interface was set; mark the problem established. */
+int ddpca_problem_finalize(ddpca_problem_t p);
+
 /* ========================================================================================
  * MCONTACT -- the ADMM loop of CONTACT_ANALYSIS on the GPU (MCONTACT.h:2493-2845)
- * One handle per process (= per GPU); it owns the subdomains assigned to its rank and the
- * interface sides that belong to them.  Interfaces whose sides live on different ranks are
- * coupled by one RCCL all-reduce per iteration (gamma contributions) plus one of monitor
- * norms.
+ * One handle per process (= per GPU); it owns the subdomains assigned to its rank (solved as
+ * one batch) and the interface sides that belong to them.  Interfaces whose sides live on
+ * different ranks swap their gamma halves with one grouped RCCL send/recv pair per iteration;
+ * the MONITOR norms take one small RCCL all-reduce.
  * ======================================================================================== */
 typedef struct ddpca_mcontact* mcontact_t;
 

@@ -1,0 +1,137 @@
+// Reference-side binding of the MI355X path -- the code a DDPCA-ADMM maintainer adds to call
+// libddpca_amd.so from the reference's own classes (INTEGRATION.md quotes it).  Compiled here
+// only as a check against the reference headers (oracle/ref_bind.cpp, TEST INFRASTRUCTURE);
+// nothing in the product includes it.
+//
+//   ddpca_bind::from_reference(mc)     MCONTACT after ESTABLISH() -> established ddpca_problem_t
+//   ddpca_bind::mgpis_create(g, ...)   one MULTIGRID's MGPIS hierarchy -> mgpis_t (CG_SOLV drop-in)
+//
+// Numbering: MULTIGRID keeps operators in the level-ordered position numbering (nodeLepo /
+// posiNode, MULTIGRID.h:884-910) and maps to node ids with earlTran (OUTP_SUB1,
+// MULTIGRID.h:1263-1281).  The device problem uses ONE nodal numbering per subdomain -- the
+// position numbering -- so the interface operators that act on node-id vectors are moved to it:
+// systTran(_pena) rows by earlTran^T, pemaInpo_r columns by earlTran.  Hanging-node prolOper and
+// nodal rotations are identities on uniformly refined meshes (the scope of this path).
+#pragma once
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "ddpca_amd.h"
+
+namespace ddpca_bind {
+
+using SpMat = Eigen::SparseMatrix<double, Eigen::RowMajor>;
+
+inline void check(int rc) {
+    if (rc < 0) throw std::runtime_error(std::string("libddpca_amd: ") + ddpca_last_error());
+}
+
+// A CSR view with the int64 row pointer the C ABI takes; owns that pointer copy.
+struct Csr {
+    SpMat m;
+    std::vector<int64_t> ptr;
+    explicit Csr(SpMat a) : m(std::move(a)) {
+        m.makeCompressed();
+        ptr.assign(m.outerIndexPtr(), m.outerIndexPtr() + m.rows() + 1);
+    }
+    ddpca_csr_t view() const { return {m.rows(), m.cols(), ptr.data(), m.innerIndexPtr(), m.valuePtr()}; }
+};
+
+// The MGPIS hierarchy of one MULTIGRID in mgpis_gpu_create's layout (+ what set_subdomain needs).
+struct Hierarchy {
+    int nlev = 0;
+    std::vector<int64_t> nnodes, nfree;
+    std::vector<std::vector<int32_t>> free_dof;
+    std::vector<Csr> K, S;
+    std::vector<const int32_t*> fd_p;
+    std::vector<const int64_t*> Kp, Sp;
+    std::vector<const int32_t*> Kc, Sc;
+    std::vector<const double*> Kv, Sv;
+    std::vector<double> presc, coords;
+
+    explicit Hierarchy(MULTIGRID& g) {
+        MGPIS& mg = g.mgpi;
+        nlev = (int)mg.maxiLeve + 1;
+        int64_t acc = 0;
+        for (int l = 0; l < nlev; ++l) {
+            acc += (int64_t)g.leveNode[l].size();
+            nnodes.push_back(acc);
+        }
+        for (int l = 0; l < nlev; ++l) {
+            SpMat C = g.consOper[l];  // one 1 per row: condensed row -> position dof
+            C.makeCompressed();
+            free_dof.emplace_back(C.innerIndexPtr(), C.innerIndexPtr() + C.rows());
+            nfree.push_back(C.rows());
+            K.emplace_back(mg.consStif[l]);
+        }
+        for (int l = 0; l + 1 < nlev; ++l) S.emplace_back(g.scalProl[l]);
+        for (int l = 0; l < nlev; ++l) {
+            fd_p.push_back(free_dof[l].data());
+            Kp.push_back(K[l].ptr.data());
+            Kc.push_back(K[l].m.innerIndexPtr());
+            Kv.push_back(K[l].m.valuePtr());
+        }
+        for (auto& s : S) {
+            Sp.push_back(s.ptr.data());
+            Sc.push_back(s.m.innerIndexPtr());
+            Sv.push_back(s.m.valuePtr());
+        }
+        // Dirichlet values (dispForc: constrained dofs in position order) and coordinates
+        const int64_t N = nnodes.back();
+        presc.assign(3 * N, 0.0);
+        for (int64_t d = 0, k = 0; d < 3 * N; ++d)
+            if (g.consFlag(d) == 0) presc[d] = g.dispForc(k++);
+        coords.resize(3 * N);
+        for (int64_t p = 0; p < N; ++p)
+            for (int a = 0; a < 3; ++a) coords[3 * p + a] = g.nodeCoor.at(g.posiNode[p])[a];
+    }
+};
+
+// MGPIS::CG_SOLV drop-in: a device solver for this MULTIGRID (solve with mgpis_gpu_solve on the
+// condensed consForc-shaped vectors, exactly CG_SOLV's arguments).
+inline mgpis_t mgpis_create(MULTIGRID& g, int device, const mgpis_options_t* opt) {
+    Hierarchy h(g);
+    mgpis_t out = nullptr;
+    check(mgpis_gpu_create(device, h.nlev, h.nnodes.data(), h.nfree.data(), h.fd_p.data(), h.Kp.data(), h.Kc.data(),
+                           h.Kv.data(), h.Sp.data(), h.Sc.data(), h.Sv.data(), opt, &out));
+    return out;
+}
+
+// MCONTACT after ESTABLISH() (muscSett = 0) -> an established device problem.
+inline ddpca_problem_t from_reference(MCONTACT& mc) {
+    const int64_t nsub = (int64_t)mc.multGrid.size(), nint = (int64_t)mc.searCont.size();
+    ddpca_problem_t p = nullptr;
+    check(ddpca_problem_empty(nsub, nint, &p));
+    for (int64_t tv = 0; tv < nsub; ++tv) {
+        MULTIGRID& g = mc.multGrid[tv];
+        Hierarchy h(g);
+        check(ddpca_problem_set_subdomain(p, tv, h.nlev, h.nnodes.data(), h.nfree.data(), h.fd_p.data(), h.Kp.data(),
+                                          h.Kc.data(), h.Kv.data(), h.Sp.data(), h.Sc.data(), h.Sv.data(),
+                                          g.consForc.data(), h.presc.data(), h.coords.data()));
+    }
+    for (int64_t ts = 0; ts < nint; ++ts) {
+        std::vector<Csr> ops;
+        for (int s = 0; s < 2; ++s) {
+            const SpMat& E = mc.multGrid[mc.contBody[ts][s]].earlTran;  // position -> node id
+            ops.emplace_back(mc.inpoLagr[ts][s]);
+            ops.emplace_back(SpMat(mc.pemaInpo_r[ts][s] * E));
+            ops.emplace_back(SpMat(E.transpose() * mc.systTran[ts][s]));
+            ops.emplace_back(SpMat(E.transpose() * mc.systTran_pena[ts][s]));
+            ops.emplace_back(mc.inteMass[ts][s]);
+            ops.emplace_back(mc.inteMass_pena[ts][s]);
+            ops.emplace_back(mc.inteInpo[ts][s]);
+        }
+        std::vector<ddpca_csr_t> v;
+        for (const auto& o : ops) v.push_back(o.view());
+        Eigen::VectorXd pema = mc.pemaInpo[ts].diagonal();
+        check(ddpca_problem_set_interface(p, ts, mc.contBody[ts][0], mc.contBody[ts][1], mc.fricCoef[ts],
+                                          (int64_t)mc.searCont[ts].intePoin.size(), (int64_t)mc.nodeCont[ts][0].size(),
+                                          (int64_t)mc.nodeCont[ts][1].size(), pema.data(), mc.inpoNgap[ts].data(),
+                                          v.data()));
+    }
+    check(ddpca_problem_finalize(p));
+    return p;
+}
+
+}  // namespace ddpca_bind

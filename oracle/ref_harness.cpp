@@ -364,8 +364,9 @@ void face_traction(MULTIGRID& g, double zc, const Eigen::Vector3d& t) {
     }
 }
 
-int twoblock(double fric, long gl) {
-    MCONTACT mc;
+// Two stacked blocks up to and including CONTACT_SEARCH (ESTABLISH / CONTACT_ANALYSIS left to
+// the caller).  mc must stay in place: the search keeps pointers to its grids.
+void twoblock_build(MCONTACT& mc, double fric, long gl) {
     mc.multGrid.resize(2);
     const double L = 0.02, H = 0.01, p = 1.0e7;
     box_mesh(mc.multGrid[0], 0, L, 0, L, 0, H, 2, 2, 1, gl);       // lower block (master)
@@ -416,16 +417,24 @@ int twoblock(double fric, long gl) {
         }
         return c;
     };
-    double t0 = now_s();
     capture_iters([&] {
         cs.BUCKET_SORT(centroids(mc.multGrid[0], cs.mastSegm), {nf, nf});
         cs.CONTACT_SEARCH(centroids(mc.multGrid[1], cs.slavSegm));
+    }, &log);
+}
+
+int twoblock(double fric, long gl) {
+    MCONTACT mc;
+    twoblock_build(mc, fric, gl);
+    std::string log;
+    double t0 = now_s();
+    capture_iters([&] {
         mc.ESTABLISH();
         mc.CONTACT_ANALYSIS();
     }, &log);
     double t = now_s() - t0;
     dump_mcontact(mc, DIRECTORY("resuMoni.txt"));
-    std::printf("twoblock fric=%g ips=%zu iters=%ld wall=%.3fs\n", fric, cs.intePoin.size(),
+    std::printf("twoblock fric=%g ips=%zu iters=%ld wall=%.3fs\n", fric, mc.searCont[0].intePoin.size(),
                 mc.iterNumbReco, t);
     return 0;
 }
@@ -460,6 +469,7 @@ int time_cg(long d0, long d1, long d2, long gl, long reps) {
 
 }  // namespace harness
 
+#ifndef HARNESS_NO_MAIN
 int main(int argc, char** argv) {
     using namespace harness;
     if (argc < 2) { std::fprintf(stderr, "usage: see header\n"); return 2; }
@@ -481,3 +491,4 @@ int main(int argc, char** argv) {
     std::fprintf(stderr, "bad arguments\n");
     return 2;
 }
+#endif  // HARNESS_NO_MAIN

@@ -1,0 +1,56 @@
+"""Operator-level builder (ddpca_problem_empty / set_subdomain / set_interface / finalize): the
+drop-in entry for a caller that already holds the reference's operators.  CPU-only checks:
+exact round trip of every operator the device path reads, and argument validation."""
+import numpy as np
+import pytest
+
+
+@pytest.fixture(scope="module")
+def pair(ddpca):
+    P = ddpca.Problem("dehw", 2, 2, 2, 1, 1, 0.3).ESTABLISH()
+    subs, ifaces = P.export_operators()
+    return P, subs, ifaces
+
+
+def test_round_trip_is_exact(ddpca, pair):
+    P, subs, ifaces = pair
+    Q = ddpca.Problem.from_operators(subs, ifaces)
+    assert (Q.nsub, Q.nint) == (P.nsub, P.nint)
+    for tv in range(P.nsub):
+        G, H = P.grid(tv), Q.grid(tv)
+        assert G.maxiLeve == H.maxiLeve
+        for l in range(G.maxiLeve + 1):
+            assert abs(G.consStif(l) - H.consStif(l)).max() == 0.0
+        for l in range(G.maxiLeve):
+            assert abs(G.realProl(l) - H.realProl(l)).max() == 0.0
+        assert np.array_equal(G.consForc, H.consForc)
+        assert np.array_equal(G.consFlag, H.consFlag)
+        assert np.array_equal(G.nodeCoor, H.nodeCoor)
+    for ts in range(P.nint):
+        assert np.array_equal(P.array("pemaDiag", ts), Q.array("pemaDiag", ts))
+        assert np.array_equal(P.array("inpoNgap", ts), Q.array("inpoNgap", ts))
+        for s in range(2):
+            for n in ddpca.Problem.IFACE_OPS:
+                assert abs(P.csr(n, 2 * ts + s) - Q.csr(n, 2 * ts + s)).max() == 0.0, n
+
+
+def test_shape_errors_are_reported(ddpca, pair):
+    P, subs, ifaces = pair
+    bad = [dict(f, ops=[dict(o) for o in f["ops"]]) for f in ifaces]
+    bad[0]["ops"][0]["inteMass"] = bad[0]["ops"][0]["inteMass"][:-1, :-1]
+    with pytest.raises(ddpca.DdpcaError, match="inteMass"):
+        ddpca.Problem.from_operators(subs, bad)
+
+
+def test_unset_members_are_reported(ddpca):
+    import ctypes as C
+    L = ddpca.lib()
+    h = C.c_void_p()
+    assert L.ddpca_problem_empty(1, 1, C.byref(h)) == 0
+    try:
+        assert L.ddpca_problem_finalize(h) < 0
+        assert b"subdomain 0" in L.ddpca_last_error()
+    finally:
+        L.ddpca_problem_destroy(h)
+    with pytest.raises(ddpca.DdpcaError):
+        ddpca.Problem.from_operators([], [])

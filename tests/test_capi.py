@@ -58,3 +58,19 @@ def test_partition_helpers():
     own = part.lpt_owner([5, 4, 3, 3, 2, 1], 3)
     loads = [sum(d for d, o in zip([5, 4, 3, 3, 2, 1], own) if o == r) for r in range(3)]
     assert max(loads) - min(loads) <= 1
+
+
+REF_BIND = Path(__file__).resolve().parents[1] / "oracle" / "_ref" / "ref_bind"
+
+
+@pytest.mark.skipif(not REF_BIND.exists(), reason="oracle/_ref/ref_bind is built only where the reference is")
+@pytest.mark.parametrize("fric", ["0", "0.3"])
+def test_reference_binding_hands_over_operators_exactly(fric):
+    """oracle/ref_bind.hpp (the binding INTEGRATION.md shows) compiled against the reference's own
+    classes: the reference's ESTABLISH output, read back through the C ABI, is bit-identical."""
+    import json
+    import subprocess
+    out = subprocess.run([str(REF_BIND), fric, "1"], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stdout + out.stderr
+    res = json.loads(out.stdout.splitlines()[0])
+    assert res["ok"] and res["K_rel"] == 0 and res["iface_ops"] == 0

@@ -97,6 +97,48 @@ def test_admm_matches_oracle_on_generated_problem(ddpca, oracle, gpu, smoother, 
     assert ok, worst
 
 
+@pytest.mark.parametrize("case", ["twoblock_f0", "twoblock_f3"])
+def test_admm_on_reference_operators_via_builder(ddpca, gpu, case):
+    """Drop-in path: the reference's OWN ESTABLISH output from the fixture -- fine stiffness
+    consStif[L], consForc, inpoNgap and all seven interface operators per side -- handed over
+    through the operator-level builder (coarse levels as Galerkin products with the stencils,
+    which equal the reference's realProl entrywise).  Same bar as the native path."""
+    from conftest import ref_csr
+    g = golden(case)
+    P = ddpca.Problem(*CASE_PARAMS[case])
+    for ts in range(P.nint):
+        fric, pn, pf = g[f"if{ts}_param"]
+        P.set_ips(ts, g[f"if{ts}_ip_node"], g[f"if{ts}_ip_shap"], g[f"if{ts}_ip_basis"], g[f"if{ts}_ip_gap"],
+                  g[f"if{ts}_ip_w"], float(fric), float(pn), float(pf))
+    P.ESTABLISH()
+    subs, ifaces = P.export_operators()
+    for tv, s in enumerate(subs):
+        G = P.grid(tv)
+        L = G.maxiLeve
+        assert np.array_equal(G.consFlag, g[f"sd{tv}_consFlag"])
+        K = [None] * (L + 1)
+        K[L] = ref_csr(g, f"sd{tv}_KL")
+        for l in range(L - 1, -1, -1):
+            Pr = G.realProl(l)
+            K[l] = (Pr.T @ K[l + 1] @ Pr).tocsr()
+        s["K"] = K
+        s["consForc"] = g[f"sd{tv}_consForc"]
+    for ts, f in enumerate(ifaces):
+        f["inpoNgap"] = g[f"if{ts}_inpoNgap"]
+        for side in range(2):
+            for n in ddpca.Problem.IFACE_OPS:
+                f["ops"][side][n] = ref_csr(g, f"if{ts}_s{side}_{n}")
+    Q = ddpca.Problem.from_operators(subs, ifaces)
+    mc = ddpca.MCONTACT(Q)
+    n = mc.CONTACT_ANALYSIS(3000)
+    assert abs(n - len(g["resuMoni"])) <= 1, (n, len(g["resuMoni"]))
+    ok, worst = _rows_close(mc.monitor(), g["resuMoni"])
+    assert ok, worst
+    for tv in range(Q.nsub):
+        u, ur = mc.get("resuDisp", tv), g[f"sd{tv}_resuDisp"]
+        assert np.linalg.norm(u - ur) <= 1e-6 * np.linalg.norm(ur)
+
+
 def _oracle_problem(P):
     from oracle.oracle import DenseSolver
     subs = []
@@ -113,3 +155,20 @@ def _oracle_problem(P):
                            inpoNgap=P.array("inpoNgap", ts),
                            ops=[{n: P.csr(n, 2 * ts + s) for n in names} for s in range(2)]))
     return subs, ifaces
+
+
+@pytest.mark.parametrize("fric", ["0", "0.3"])
+def test_reference_binding_end_to_end(gpu, fric):
+    """The reference's own classes build and ESTABLISH the two-block problem, oracle/ref_bind.hpp
+    hands it to the C ABI, the device loop runs, and the result is compared in the same process
+    with the reference's own CONTACT_ANALYSIS (iterations +-1, resuDisp 1e-6)."""
+    import json
+    import subprocess
+    from pathlib import Path
+    exe = Path(__file__).resolve().parents[1] / "oracle" / "_ref" / "ref_bind"
+    if not exe.exists():
+        pytest.skip("oracle/_ref/ref_bind is built only where the reference is (travels with the snapshot)")
+    out = subprocess.run([str(exe), fric, "1", "gpu"], capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stdout + out.stderr
+    res = json.loads(out.stdout.splitlines()[-1])
+    assert res["gpu_ok"], res
