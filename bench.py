@@ -68,7 +68,10 @@ def main():
     import torch
     import torch.distributed as dist
 
+    torch.cuda.set_device(local)  # the timing syncs below must hit this rank's GPU, not device 0
     if world > 1:
+        # host-side coordination only (barriers, the RCCL unique id, max-over-ranks timing); the
+        # data path's exchanges are RCCL calls inside libddpca_amd on the solve stream
         dist.init_process_group("gloo", rank=rank, world_size=world)
     D = importlib.import_module("ddpca-admm_amd")
     from importlib import import_module

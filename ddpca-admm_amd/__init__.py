@@ -19,7 +19,8 @@ from typing import Optional, Sequence
 import numpy as np
 
 _HERE = Path(__file__).resolve().parent
-LIBPATH = _HERE / "libddpca_amd.so"
+# DDPCA_AMD_LIB: an in-tree experiment build (build.py with DDPCA_BUILD_OUT) for kernel A/B runs
+LIBPATH = Path(os.environ.get("DDPCA_AMD_LIB", _HERE / "libddpca_amd.so"))
 
 _lib: Optional[C.CDLL] = None
 

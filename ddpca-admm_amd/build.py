@@ -16,13 +16,16 @@ from pathlib import Path
 HERE = Path(__file__).resolve().parent
 CSRC = HERE / "csrc"
 OBJ = HERE / "build" / "obj"
-LIB = HERE / "libddpca_amd.so"
+# experiment builds (A/B of a kernel change): DDPCA_BUILD_DEFINES="-DFOO=1" DDPCA_BUILD_OUT=libx.so
+# produce a second library next to this file; load it with DDPCA_AMD_LIB=<path>
+LIB = HERE / os.environ.get("DDPCA_BUILD_OUT", "libddpca_amd.so")
 ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
 HIPCC = str(ROCM / "bin" / "hipcc")
 ARCH = "gfx950"
 
 COMMON = ["-O3", "-std=c++17", "-fPIC", "-fopenmp", "-Wall", "-Wno-unused-function",
-          "-Wno-unknown-pragmas", f"-I{HERE.parent / 'include'}", f"-I{CSRC}"]
+          "-Wno-unknown-pragmas", f"-I{HERE.parent / 'include'}", f"-I{CSRC}",
+          *os.environ.get("DDPCA_BUILD_DEFINES", "").split()]
 DEVICE = [f"--offload-arch={ARCH}", "-munsafe-fp-atomics"]
 LINK = ["-shared", "-fopenmp", f"--offload-arch={ARCH}", f"-L{ROCM / 'lib'}", "-lamdhip64", "-lrccl",
         f"-Wl,-rpath,{ROCM / 'lib'}", f"-Wl,-rpath,{ROCM / 'llvm' / 'lib'}"]
@@ -60,7 +63,7 @@ def build(verbose: bool = False) -> Path:
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
         objs = list(ex.map(_compile, srcs))
     stamp = hashlib.sha1("".join(o.name for o in objs).encode()).hexdigest()[:16]
-    stamp_file = OBJ / "link.stamp"
+    stamp_file = OBJ / f"link.{LIB.name}.stamp"
     if LIB.exists() and stamp_file.exists() and stamp_file.read_text() == stamp:
         return LIB
     tmp = LIB.with_suffix(".so.tmp")

@@ -62,6 +62,16 @@ struct DevBuf {
     }
 };
 
+// Non-owning device range carved out of a DevBuf.
+template <typename T>
+struct DevSpan {
+    T* p = nullptr;
+    size_t n = 0;
+    void zero(hipStream_t s = 0) {
+        if (n) DDPCA_HIP(hipMemsetAsync(p, 0, n * sizeof(T), s));
+    }
+};
+
 inline int ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 inline int64_t pad64(int64_t n) { return (n + 63) / 64 * 64; }
 

@@ -13,14 +13,21 @@
 //   Lagrange       l += M^-1 (T^T u - M^rho aux)                                      (2689-2704)
 //   MONITOR        squared norms reduced on device, one small RCCL all-reduce,
 //                  reference stopping logic on the host                               (2725-2845)
-// The surface mass solves (LDLT in the reference, < 120000 rows) run as ONE batched
-// Jacobi-PCG over every owned side (ELL-64 rows, per-side scalars, all CUs busy) to a 1e-14
-// relative residual.  Everything runs on the batch's single stream.
+//
+// Layout: one device workspace W = [u | aux, lambda | gamma] per rank.  u: displacements of all
+// owned subdomains in the batch's fine layout (reference node order inside each subdomain);
+// aux / lambda: all owned sides, each padded to 64 rows; gamma: every interface.  The three
+// interface products (gamma, the aux right-hand side, the lambda right-hand side) of ALL owned
+// sides are each ONE SELL-64 operator whose columns index W, so each is one coalesced launch.
+// The surface mass solves (LDLT in the reference, < 120000 rows) run as ONE batched Jacobi-PCG
+// over every owned side (ELL-64 rows, per-side scalars) to a 1e-14 relative residual.
+// Everything runs on the batch's single stream.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
 #include <algorithm>
 #include <chrono>
+#include <climits>
 #include <cmath>
 #include <cstring>
 #include <map>
@@ -40,20 +47,6 @@ namespace {
         ncclResult_t r_ = (call);                                                                         \
         if (r_ != ncclSuccess) throw ApiError(DDPCA_ECOMM, std::string(#call) + ": " + ncclGetErrorString(r_)); \
     } while (0)
-
-struct DevCsr {
-    int64_t nrow = 0, ncol = 0;
-    DevBuf<int64_t> ptr;
-    DevBuf<int32_t> col;
-    DevBuf<double> val;
-    void upload(const Csr& m) {
-        nrow = m.nrow;
-        ncol = m.ncol;
-        ptr.upload(m.ptr);
-        col.upload(m.col);
-        val.upload(m.val);
-    }
-};
 
 Csr transpose(const Csr& A) {
     Csr T;
@@ -88,18 +81,18 @@ __device__ __forceinline__ double csr_row(const int64_t* ptr, const int32_t* col
     return s;
 }
 
-// y = x, 16 B per lane (n even: batch vectors are 3 * multiple-of-64 long)
+// y = x, 16 B per lane (n even: batch vectors are 3 * multiple-of-64 long, or 2R)
 __global__ void k_copy2(double2* y, const double2* x, int64_t n2) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n2) y[i] = x[i];
 }
 
-// b[rows[i]] += sum_k val[k] state[col[k]]  (coupling of the body-balance RHS)
-__global__ void k_cpl(const int32_t* rows, const int64_t* ptr, const int32_t* col, const double* val,
-                      const double* state, double* b, int64_t n) {
+// b[rows[i]] += sum_k val[k] W[col[k]]  (coupling of the body-balance RHS, surface rows only)
+__global__ void k_cpl(const int32_t* rows, const int64_t* ptr, const int32_t* col, const double* val, const double* W,
+                      double* b, int64_t n) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    b[rows[i]] += csr_row(ptr, col, val, state, i);
+    b[rows[i]] += csr_row(ptr, col, val, W, i);
 }
 
 // u = mask ? x : prescribed  (OUTP_SUB1 without rotations); x and mask in the solver's device
@@ -113,19 +106,27 @@ __global__ void k_outp(const double* x, const uint8_t* mask, const int32_t* onod
     for (int a = 0; a < 3; ++a) u[3 * o + a] = ((m >> a) & 1) ? x[3 * i + a] : presc[3 * o + a];
 }
 
-// gamma_seg += sgn/2 (L lambda + R u) + cst
-__global__ void k_gamma(const int64_t* lp, const int32_t* lc, const double* lv, const double* lam, const int64_t* rp,
-                        const int32_t* rc, const double* rv, const double* u, const double* cst, double sgn,
-                        double* gam, int64_t mip) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= mip) return;
-    const double c = 0.5 * sgn * (csr_row(lp, lc, lv, lam, i) + csr_row(rp, rc, rv, u, i));
-    gam[i] += cst ? c + cst[i] : c;
-}
-
 __global__ void k_add(double* y, const double* x, int64_t n) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) y[i] += x[i];
+}
+
+// y[row] = sum_k val * W[col] (+ add[row]): one wavefront per 64 rows, slot-major (SELL-64)
+__global__ __launch_bounds__(256) void k_sell_w(const int32_t* slots, const int64_t* off, const int32_t* col,
+                                                const double* val, int64_t nch, const double* W, double* y,
+                                                const double* add) {
+    const int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (c >= nch) return;
+    const int lane = threadIdx.x & 63;
+    const int ns = slots[c];
+    const int32_t* cp = col + off[c] * 64 + lane;
+    const double* vp = val + off[c] * 64 + lane;
+    double s = 0.0;
+#pragma unroll 4
+    for (int k = 0; k < ns; ++k)
+        s += __builtin_nontemporal_load(vp + (int64_t)k * 64) * W[__builtin_nontemporal_load(cp + (int64_t)k * 64)];
+    const int64_t row = c * 64 + lane;
+    y[row] = add ? s + add[row] : s;
 }
 
 // normal / Coulomb projection at integration points (MCONTACT.h:2637-2668)
@@ -162,18 +163,6 @@ __global__ void k_project(double* g, int32_t* stat, int64_t nip, int comp, doubl
         v[2] = 0.0;
         stat[q] = 0;
     }
-}
-
-// rhs = A u + B l + C g   (B, C optional; sign sb on B)
-__global__ void k_rhs3(const int64_t* ap, const int32_t* ac, const double* av, const double* u, const int64_t* bp,
-                       const int32_t* bc, const double* bv, const double* l, double sb, const int64_t* cp,
-                       const int32_t* cc, const double* cv, const double* g, double* rhs, int64_t m) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= m) return;
-    double s = csr_row(ap, ac, av, u, i);
-    if (bp) s += sb * csr_row(bp, bc, bv, l, i);
-    if (cp) s += csr_row(cp, cc, cv, g, i);
-    rhs[i] = s;
 }
 
 // ---- batched Jacobi-PCG over the owned sides' surface mass systems.  Rows of all systems
@@ -348,6 +337,45 @@ __global__ void k_reduce_pairs(const double* partial, int64_t nb, double* out2) 
 
 inline int nb256(int64_t n) { return (int)std::max<int64_t>(1, (n + 255) / 256); }
 
+// Row lists -> SELL-64 (rows padded to a multiple of 64; padding slots: column 0, value 0).
+using Rows = std::vector<std::vector<std::pair<int64_t, double>>>;
+
+struct SellOp {
+    int64_t nrow = 0, nch = 0;
+    DevBuf<int32_t> slots, col;
+    DevBuf<int64_t> off;
+    DevBuf<double> val;
+    void build(const Rows& rows) {
+        nrow = pad64((int64_t)rows.size());
+        nch = nrow / 64;
+        std::vector<int32_t> sl(std::max<int64_t>(nch, 1), 0);
+        std::vector<int64_t> of(nch + 1, 0);
+        for (int64_t c = 0; c < nch; ++c) {
+            size_t mx = 0;
+            for (int64_t r = c * 64; r < std::min<int64_t>((int64_t)rows.size(), (c + 1) * 64); ++r) mx = std::max(mx, rows[r].size());
+            sl[c] = (int32_t)mx;
+            of[c + 1] = of[c] + (int64_t)mx;
+        }
+        std::vector<int32_t> co(std::max<int64_t>(of[nch] * 64, 1), 0);
+        std::vector<double> va(std::max<int64_t>(of[nch] * 64, 1), 0.0);
+        for (int64_t r = 0; r < (int64_t)rows.size(); ++r) {
+            const int64_t c = r / 64, lane = r % 64;
+            for (size_t k = 0; k < rows[r].size(); ++k) {
+                if (rows[r][k].first > INT32_MAX) throw ApiError(DDPCA_EINVAL, "workspace index exceeds int32");
+                co[(of[c] + (int64_t)k) * 64 + lane] = (int32_t)rows[r][k].first;
+                va[(of[c] + (int64_t)k) * 64 + lane] = rows[r][k].second;
+            }
+        }
+        slots.upload(sl);
+        off.upload(of);
+        col.upload(co);
+        val.upload(va);
+    }
+    void apply(hipStream_t s, const double* W, double* y, const double* add) const {
+        if (nch) hipLaunchKernelGGL(k_sell_w, dim3(ceil_div(nch, 4)), dim3(256), 0, s, slots.p, off.p, col.p, val.p, nch, W, y, add);
+    }
+};
+
 // Batched surface-mass solver: one graph of `k` CG iterations over every system, replayed
 // until every system reports done through the host-mapped mirror.
 class MassBatch {
@@ -386,17 +414,17 @@ public:
         std::vector<int32_t> co(std::max<int64_t>(of[nch] * 64, 1), 0);
         std::vector<double> va(std::max<int64_t>(of[nch] * 64, 1), 0.0);
         for (int64_t c = 0; c < nch; ++c)
-            for (int64_t q = of[c]; q < of[c + 1]; ++q)
-                for (int lane = 0; lane < 64; ++lane) co[q * 64 + lane] = (int32_t)(c * 64 + lane);  // pad: self, 0
+            for (int64_t q2 = of[c]; q2 < of[c + 1]; ++q2)
+                for (int lane = 0; lane < 64; ++lane) co[q2 * 64 + lane] = (int32_t)(c * 64 + lane);  // pad: self, 0
         for (int s = 0; s < nsys; ++s) {
             const Csr& M = *A[s];
-            for (int64_t r = 0; r < M.nrow; ++r) {
-                const int64_t g = roff[s] + r, c = g / 64, lane = g % 64;
-                for (int64_t k2 = M.ptr[r]; k2 < M.ptr[r + 1]; ++k2) {
-                    const int64_t q = of[c] + (k2 - M.ptr[r]);
-                    co[q * 64 + lane] = (int32_t)(roff[s] + M.col[k2]);
-                    va[q * 64 + lane] = M.val[k2];
-                    if (M.col[k2] == r) di[g] = 1.0 / M.val[k2];
+            for (int64_t r0 = 0; r0 < M.nrow; ++r0) {
+                const int64_t g = roff[s] + r0, c = g / 64, lane = g % 64;
+                for (int64_t k2 = M.ptr[r0]; k2 < M.ptr[r0 + 1]; ++k2) {
+                    const int64_t q2 = of[c] + (k2 - M.ptr[r0]);
+                    co[q2 * 64 + lane] = (int32_t)(roff[s] + M.col[k2]);
+                    va[q2 * 64 + lane] = M.val[k2];
+                    if (M.col[k2] == r0) di[g] = 1.0 / M.val[k2];
                 }
             }
         }
@@ -482,9 +510,8 @@ struct ddpca_mcontact {
     };
     struct Side {
         int64_t ts = 0, s = 0, tv = 0, m = 0, mip = 0;
-        int64_t roff = 0;  // rows of aux at state[roff], lambda at state[R + roff]
+        int64_t roff = 0;  // rows of aux at W[oS + roff], lambda at W[oS + R + roff]
         int sub = 0;       // index into subs
-        DevCsr lagr, pemr, tTp, mass, massp, iinpo;
     };
     struct Itf {
         int64_t ts = 0, mip = 0, goff = 0;
@@ -492,7 +519,6 @@ struct ddpca_mcontact {
         double fric = -1.0;
         int owner[2] = {0, 0};
         bool mine = false, cross = false;
-        DevBuf<double> cgap;  // -1/2 pema g (added by the side-0 owner)
         DevBuf<int32_t> stat;
         DevBuf<double> recv;
     };
@@ -505,15 +531,22 @@ struct ddpca_mcontact {
     std::unique_ptr<MgpisDevice> mg;
     std::vector<int64_t> maxit;          // per owned subdomain: n_free (reference maxit = rows)
     DevBuf<double> cf;                   // consForc, solver (device) node order
-    DevBuf<double> presc, u, uo;         // batch fine layout, reference node order (3 nn_L)
+    DevBuf<double> presc;                // Dirichlet values, reference node order (3 nn_L)
     DevBuf<int32_t> onode;               // device node -> reference-order node of the batch
-    DevBuf<int32_t> crow;                // coupling rows (solver dofs, free only)
+    DevBuf<int32_t> crow;                // coupling rows (solver dofs, surface rows only)
     DevBuf<int64_t> cptr;
-    DevBuf<int32_t> ccol;
+    DevBuf<int32_t> ccol;                // columns index W
     DevBuf<double> cval;
     int64_t ncrow = 0;
     int64_t R = 0;                       // padded rows of all owned sides
-    DevBuf<double> state, state_old, gamma, partial, moni;
+    // workspace W = [u (NU) | aux, lambda (2R) | gamma (G)] and its regions
+    DevBuf<double> W;
+    int64_t NU = 0, G = 0, oS = 0, oG = 0;
+    double* u = nullptr;
+    double* state = nullptr;
+    double* gamma = nullptr;
+    DevBuf<double> uo, state_old, gcst, partial, moni;
+    SellOp op_gamma, op_aux, op_lam;     // gamma (my halves), aux RHS, lambda RHS
     MassBatch mb_aux, mb_lam;
     std::vector<double> moni_host;
     hipStream_t main = nullptr;          // == mg->stream
@@ -566,8 +599,9 @@ void build(ddpca_mcontact& H, Problem& P) {
         return -1;
     };
     const int64_t NN = H.mg ? H.mg->lev.back().nn : 0;
+    H.NU = std::max<int64_t>(3 * NN, 64);
     {
-        std::vector<double> cf(std::max<int64_t>(3 * NN, 2), 0.0), pr(std::max<int64_t>(3 * NN, 2), 0.0);
+        std::vector<double> cf(H.NU, 0.0), pr(H.NU, 0.0);
         std::vector<int32_t> on(std::max<int64_t>(NN, 1));
         std::iota(on.begin(), on.end(), 0);  // padding nodes map to themselves
         for (size_t i = 0; i < H.subs.size(); ++i) {
@@ -583,10 +617,6 @@ void build(ddpca_mcontact& H, Problem& P) {
         H.cf.upload(cf);
         H.presc.upload(pr);
         H.onode.upload(on);
-        H.u.alloc(cf.size());
-        H.uo.alloc(cf.size());
-        H.u.zero(H.main);
-        H.uo.zero(H.main);
     }
     // ---- owned interface sides: aux rows [roff, roff + m), lambda rows R + the same
     int64_t roff = 0;
@@ -604,33 +634,11 @@ void build(ddpca_mcontact& H, Problem& P) {
             sd.mip = itf.mip();
             sd.roff = roff;
             roff += pad64(sd.m);
-            sd.lagr.upload(itf.inpoLagr[s]);
-            sd.pemr.upload(itf.pemaInpo_r[s]);
-            sd.tTp.upload(transpose(itf.systTran_pena[s]));
-            sd.mass.upload(itf.inteMass[s]);
-            sd.massp.upload(itf.inteMass_pena[s]);
-            sd.iinpo.upload(itf.inteInpo[s]);
             side_of[{ts, s}] = H.sides.size();
-            H.sides.push_back(std::move(sd));
+            H.sides.push_back(sd);
         }
     }
     H.R = roff;
-    H.state.alloc(std::max<int64_t>(2 * H.R, 2));
-    H.state_old.alloc(std::max<int64_t>(2 * H.R, 2));
-    H.state.zero(H.main);
-    H.state_old.zero(H.main);
-    {
-        std::vector<const Csr*> Ma, Ml;
-        std::vector<int64_t> ro;
-        for (auto& sd : H.sides) {
-            const Interface& itf = mc.searCont[sd.ts];
-            Ma.push_back(&itf.inteMass_pena[sd.s]);
-            Ml.push_back(&itf.inteMass[sd.s]);
-            ro.push_back(sd.roff);
-        }
-        H.mb_aux.build(Ma, ro, H.R);
-        H.mb_lam.build(Ml, ro, H.R);
-    }
     // ---- interfaces: gamma layout (cross-rank interfaces first, then rank-local)
     int64_t goff = 0;
     for (int pass = 0; pass < 2; ++pass)
@@ -651,18 +659,83 @@ void build(ddpca_mcontact& H, Problem& P) {
             I.goff = goff;
             goff += I.mip;
             if (I.mine) {
-                std::vector<double> cg(I.mip);
-                for (int64_t i = 0; i < I.mip; ++i) cg[i] = -0.5 * (itf.pemaDiag[i] * itf.inpoNgap[i]);
-                I.cgap.upload(cg);
                 I.stat.alloc(std::max<int64_t>(I.mip / I.comp, 1));
                 if (cross) I.recv.alloc(I.mip);
             }
             H.itfs.push_back(std::move(I));
         }
     std::sort(H.itfs.begin(), H.itfs.end(), [](const auto& a, const auto& b) { return a.ts < b.ts; });
-    H.gamma.alloc(std::max<int64_t>(goff, 1));
+    H.G = pad64(std::max<int64_t>(goff, 1));
+    // ---- workspace
+    H.oS = H.NU;
+    H.oG = H.NU + 2 * H.R;
+    H.W.alloc(H.oG + H.G);
+    H.W.zero(H.main);
+    H.u = H.W.p;
+    H.state = H.W.p + H.oS;
+    H.gamma = H.W.p + H.oG;
+    H.uo.alloc(H.NU);
+    H.uo.zero(H.main);
+    H.state_old.alloc(std::max<int64_t>(2 * H.R, 2));
+    H.state_old.zero(H.main);
+    auto itf_of = [&](int64_t ts) -> const ddpca_mcontact::Itf& {
+        return *std::find_if(H.itfs.begin(), H.itfs.end(), [&](const auto& x) { return x.ts == ts; });
+    };
+    // ---- interface operators over W (MCONTACT.h:2632-2636, 2671-2704)
+    {
+        Rows rg(H.G), ra(H.R), rl(H.R);
+        std::vector<double> gc(H.G, 0.0);
+        for (const auto& sd : H.sides) {
+            const Interface& itf = mc.searCont[sd.ts];
+            const auto& I = itf_of(sd.ts);
+            const int s = (int)sd.s;
+            const double half = s == 0 ? 0.5 : -0.5;
+            const int64_t u0 = H.subs[sd.sub].dof0;
+            const int64_t lam0 = H.oS + H.R + sd.roff, aux0 = H.oS + sd.roff;
+            // gamma half: +-1/2 (inpoLagr lambda + pemaInpo_r u); side 0 adds -1/2 pema g
+            const Csr& Lg = itf.inpoLagr[s];
+            const Csr& Rg = itf.pemaInpo_r[s];
+            for (int64_t i = 0; i < sd.mip; ++i) {
+                auto& row = rg[I.goff + i];
+                for (int64_t k = Lg.ptr[i]; k < Lg.ptr[i + 1]; ++k) row.push_back({lam0 + Lg.col[k], half * Lg.val[k]});
+                for (int64_t k = Rg.ptr[i]; k < Rg.ptr[i + 1]; ++k) row.push_back({u0 + Rg.col[k], half * Rg.val[k]});
+                if (s == 0) gc[I.goff + i] = -0.5 * (itf.pemaDiag[i] * itf.inpoNgap[i]);
+            }
+            // aux RHS: systTran_pena^T u + inteMass lambda + inteInpo gamma
+            const Csr tTp = transpose(itf.systTran_pena[s]);
+            const Csr& M = itf.inteMass[s];
+            const Csr& Mp = itf.inteMass_pena[s];
+            const Csr& Ii = itf.inteInpo[s];
+            for (int64_t r = 0; r < sd.m; ++r) {
+                auto& a = ra[sd.roff + r];
+                auto& l = rl[sd.roff + r];
+                for (int64_t k = tTp.ptr[r]; k < tTp.ptr[r + 1]; ++k) {
+                    a.push_back({u0 + tTp.col[k], tTp.val[k]});
+                    l.push_back({u0 + tTp.col[k], tTp.val[k]});
+                }
+                for (int64_t k = M.ptr[r]; k < M.ptr[r + 1]; ++k) a.push_back({lam0 + M.col[k], M.val[k]});
+                for (int64_t k = Ii.ptr[r]; k < Ii.ptr[r + 1]; ++k) a.push_back({H.oG + I.goff + Ii.col[k], Ii.val[k]});
+                // lambda RHS: systTran_pena^T u - inteMass_pena aux
+                for (int64_t k = Mp.ptr[r]; k < Mp.ptr[r + 1]; ++k) l.push_back({aux0 + Mp.col[k], -Mp.val[k]});
+            }
+        }
+        H.op_gamma.build(rg);
+        H.op_aux.build(ra);
+        H.op_lam.build(rl);
+        H.gcst.upload(gc);
+        std::vector<const Csr*> Ma, Ml;
+        std::vector<int64_t> ro;
+        for (auto& sd : H.sides) {
+            const Interface& itf = mc.searCont[sd.ts];
+            Ma.push_back(&itf.inteMass_pena[sd.s]);
+            Ml.push_back(&itf.inteMass[sd.s]);
+            ro.push_back(sd.roff);
+        }
+        H.mb_aux.build(Ma, ro, H.R);
+        H.mb_lam.build(Ml, ro, H.R);
+    }
     // ---- coupling rows of the body-balance RHS: sum over incident sides of
-    //      [systTran_pena | -systTran] on free dofs, in batch dof / state coordinates
+    //      [systTran_pena | -systTran] on free dofs, solver dofs x W columns
     {
         std::map<int64_t, std::vector<std::pair<int32_t, double>>> rowmap;
         for (size_t si = 0; si < H.subs.size(); ++si) {
@@ -676,12 +749,13 @@ void build(ddpca_mcontact& H, Problem& P) {
                     const Csr& Tp = itf.systTran_pena[s];
                     const Csr& T = itf.systTran[s];
                     for (int64_t r = 0; r < Tp.nrow; ++r) {
-                        if (!g.consFlag[r]) continue;
+                        // only free dofs the interface actually couples (surface rows)
+                        if (!g.consFlag[r] || (Tp.ptr[r] == Tp.ptr[r + 1] && T.ptr[r] == T.ptr[r + 1])) continue;
                         auto& row = rowmap[H.mg->fine_dof((int)si, r)];  // added into the solver RHS
                         for (int64_t k = Tp.ptr[r]; k < Tp.ptr[r + 1]; ++k)
-                            row.push_back({(int32_t)(sd.roff + Tp.col[k]), Tp.val[k]});
+                            row.push_back({(int32_t)(H.oS + sd.roff + Tp.col[k]), Tp.val[k]});
                         for (int64_t k = T.ptr[r]; k < T.ptr[r + 1]; ++k)
-                            row.push_back({(int32_t)(H.R + sd.roff + T.col[k]), -T.val[k]});
+                            row.push_back({(int32_t)(H.oS + H.R + sd.roff + T.col[k]), -T.val[k]});
                     }
                 }
             }
@@ -776,7 +850,7 @@ double ms_since(std::chrono::steady_clock::time_point t0) {
 }
 
 void copy_dev(hipStream_t s, double* y, const double* x, int64_t n) {
-    // every batch vector has an even length (3 x multiple of 64, or 2R)
+    // every copied vector has an even length (3 x multiple of 64, or 2R)
     hipLaunchKernelGGL(k_copy2, dim3(nb256(n / 2)), dim3(256), 0, s, reinterpret_cast<double2*>(y),
                        reinterpret_cast<const double2*>(x), n / 2);
 }
@@ -786,34 +860,24 @@ bool iterate_once(ddpca_mcontact& H, bool check) {
     const auto t0 = std::chrono::steady_clock::now();
     hipStream_t st = H.main;
     // snapshot for MONITOR (resuDisp_0 / inteAuxi_0 / inteLagr_0, MCONTACT.h:2507-2509)
-    if (H.R) copy_dev(st, H.state_old.p, H.state.p, 2 * H.R);
-    std::swap(H.u.p, H.uo.p);
+    if (H.R) copy_dev(st, H.state_old.p, H.state, 2 * H.R);
+    copy_dev(st, H.uo.p, H.u, H.NU);
     // ---- body balance: every owned subdomain in one batched PCG
     if (H.mg) {
         MgpisDevice& D = *H.mg;
         copy_dev(st, D.bs.p, H.cf.p, 3 * D.lev.back().nn);
         if (H.ncrow)
             hipLaunchKernelGGL(k_cpl, dim3(nb256(H.ncrow)), dim3(256), 0, st, H.crow.p, H.cptr.p, H.ccol.p, H.cval.p,
-                               H.state.p, D.bs.p, H.ncrow);
+                               H.W.p, D.bs.p, H.ncrow);
         D.pcg_begin(1, 1.0e-14, H.maxit, H.opt.warm_start != 0 && H.tc > 0);
         D.pcg_wait(1, 0);
         hipLaunchKernelGGL(k_outp, dim3(nb256(D.lev.back().nn)), dim3(256), 0, st, D.xs.p, D.lev.back().mask.p,
-                           H.onode.p, H.presc.p, H.u.p, D.lev.back().nn);
+                           H.onode.p, H.presc.p, H.u, D.lev.back().nn);
     }
     DDPCA_HIP(hipEventRecord(H.ev[1], st));
     const double t_solve = ms_since(t0);
-    // ---- interface balance: gamma contributions of owned sides
-    if (H.gamma.n) DDPCA_HIP(hipMemsetAsync(H.gamma.p, 0, H.gamma.n * sizeof(double), st));
-    auto sub_u = [&](const ddpca_mcontact::Side& sd) -> const double* { return H.u.p + H.subs[sd.sub].dof0; };
-    auto itf_of = [&](int64_t ts) -> ddpca_mcontact::Itf& {
-        return *std::find_if(H.itfs.begin(), H.itfs.end(), [&](const auto& x) { return x.ts == ts; });
-    };
-    for (auto& sd : H.sides) {
-        const auto& I = itf_of(sd.ts);
-        hipLaunchKernelGGL(k_gamma, dim3(nb256(sd.mip)), dim3(256), 0, st, sd.lagr.ptr.p, sd.lagr.col.p, sd.lagr.val.p,
-                           H.state.p + H.R + sd.roff, sd.pemr.ptr.p, sd.pemr.col.p, sd.pemr.val.p, sub_u(sd),
-                           sd.s == 0 ? I.cgap.p : nullptr, sd.s == 0 ? 1.0 : -1.0, H.gamma.p + I.goff, sd.mip);
-    }
+    // ---- interface balance: this rank's gamma halves, one launch for every owned side
+    H.op_gamma.apply(st, H.W.p, H.gamma, H.gcst.p);
     bool any_cross = false;
     for (auto& I : H.itfs) any_cross |= (I.cross && I.mine);
     DDPCA_HIP(hipEventRecord(H.ev[0], st));
@@ -823,44 +887,35 @@ bool iterate_once(ddpca_mcontact& H, bool check) {
         for (auto& I : H.itfs) {
             if (!(I.cross && I.mine)) continue;
             const int peer = I.owner[0] == H.rank ? I.owner[1] : I.owner[0];
-            DDPCA_NCCL(ncclSend(H.gamma.p + I.goff, I.mip, ncclDouble, peer, H.comm, st));
+            DDPCA_NCCL(ncclSend(H.gamma + I.goff, I.mip, ncclDouble, peer, H.comm, st));
             DDPCA_NCCL(ncclRecv(I.recv.p, I.mip, ncclDouble, peer, H.comm, st));
         }
         DDPCA_NCCL(ncclGroupEnd());
         for (auto& I : H.itfs)
             if (I.cross && I.mine)
-                hipLaunchKernelGGL(k_add, dim3(nb256(I.mip)), dim3(256), 0, st, H.gamma.p + I.goff, I.recv.p, I.mip);
+                hipLaunchKernelGGL(k_add, dim3(nb256(I.mip)), dim3(256), 0, st, H.gamma + I.goff, I.recv.p, I.mip);
     }
     DDPCA_HIP(hipEventRecord(H.ev[2], st));
     for (auto& I : H.itfs)
         if (I.mine)
-            hipLaunchKernelGGL(k_project, dim3(nb256(I.mip / I.comp)), dim3(256), 0, st, H.gamma.p + I.goff, I.stat.p,
+            hipLaunchKernelGGL(k_project, dim3(nb256(I.mip / I.comp)), dim3(256), 0, st, H.gamma + I.goff, I.stat.p,
                                I.mip / I.comp, I.comp, I.fric);
     // ---- aux = (M^rho)^-1 (T^T u + M lambda + I gamma)
-    for (auto& sd : H.sides) {
-        const auto& I = itf_of(sd.ts);
-        hipLaunchKernelGGL(k_rhs3, dim3(nb256(sd.m)), dim3(256), 0, st, sd.tTp.ptr.p, sd.tTp.col.p, sd.tTp.val.p,
-                           sub_u(sd), sd.mass.ptr.p, sd.mass.col.p, sd.mass.val.p, H.state.p + H.R + sd.roff, 1.0,
-                           sd.iinpo.ptr.p, sd.iinpo.col.p, sd.iinpo.val.p, H.gamma.p + I.goff, H.mb_aux.b.p + sd.roff,
-                           sd.m);
-    }
-    H.mb_aux.solve(st, H.state.p, 1.0e-14, 2000);
-    // ---- lambda += M^-1 (T^T u - M^rho aux)
-    for (auto& sd : H.sides)
-        hipLaunchKernelGGL(k_rhs3, dim3(nb256(sd.m)), dim3(256), 0, st, sd.tTp.ptr.p, sd.tTp.col.p, sd.tTp.val.p,
-                           sub_u(sd), sd.massp.ptr.p, sd.massp.col.p, sd.massp.val.p, H.state.p + sd.roff, -1.0,
-                           nullptr, nullptr, nullptr, nullptr, H.mb_lam.b.p + sd.roff, sd.m);
     if (!H.sides.empty()) {
+        H.op_aux.apply(st, H.W.p, H.mb_aux.b.p, nullptr);
+        H.mb_aux.solve(st, H.state, 1.0e-14, 2000);
+        // ---- lambda += M^-1 (T^T u - M^rho aux)
+        H.op_lam.apply(st, H.W.p, H.mb_lam.b.p, nullptr);
         H.mb_lam.solve(st, H.mb_lam.x.p, 1.0e-14, 2000);
-        hipLaunchKernelGGL(k_add, dim3(nb256(H.R)), dim3(256), 0, st, H.state.p + H.R, H.mb_lam.x.p, H.R);
+        hipLaunchKernelGGL(k_add, dim3(nb256(H.R)), dim3(256), 0, st, H.state + H.R, H.mb_lam.x.p, H.R);
     }
     // ---- MONITOR norms (owned entries; others zero) and their reduction across ranks
     DDPCA_HIP(hipMemsetAsync(H.moni.p, 0, H.moni.n * sizeof(double), st));
-    for (auto& S : H.subs) pair_norm(H, H.u.p + S.dof0, H.uo.p + S.dof0, 3 * S.nn, 2 * S.tv);
+    for (auto& S : H.subs) pair_norm(H, H.u + S.dof0, H.uo.p + S.dof0, 3 * S.nn, 2 * S.tv);
     for (auto& sd : H.sides) {
         const int64_t base = 2 * H.nsub + 8 * sd.ts + 4 * sd.s;
-        pair_norm(H, H.state.p + sd.roff, H.state_old.p + sd.roff, sd.m, base);
-        pair_norm(H, H.state.p + H.R + sd.roff, H.state_old.p + H.R + sd.roff, sd.m, base + 2);
+        pair_norm(H, H.state + sd.roff, H.state_old.p + sd.roff, sd.m, base);
+        pair_norm(H, H.state + H.R + sd.roff, H.state_old.p + H.R + sd.roff, sd.m, base + 2);
     }
     if (H.nranks > 1) DDPCA_NCCL(ncclAllReduce(H.moni.p, H.moni.p, H.moni.n, ncclDouble, ncclSum, H.comm, st));
     DDPCA_HIP(hipEventRecord(H.ev[3], st));
@@ -976,7 +1031,7 @@ int64_t mcontact_gpu_get(mcontact_t h, const char* what, int64_t index, void* ou
             for (auto& S : h->subs)
                 if (S.tv == index) {
                     n = 3 * S.nn;
-                    if (out) DDPCA_HIP(hipMemcpy(out, h->u.p + S.dof0, std::min(n, cap) * sizeof(double), hipMemcpyDeviceToHost));
+                    if (out) DDPCA_HIP(hipMemcpy(out, h->u + S.dof0, std::min(n, cap) * sizeof(double), hipMemcpyDeviceToHost));
                     return;
                 }
             throw ApiError(DDPCA_EINVAL, "subdomain not owned by this rank");
@@ -985,7 +1040,7 @@ int64_t mcontact_gpu_get(mcontact_t h, const char* what, int64_t index, void* ou
             for (auto& sd : h->sides)
                 if (2 * sd.ts + sd.s == index) {
                     n = sd.m;
-                    const double* src = h->state.p + sd.roff + (w == "inteAuxi" ? 0 : h->R);
+                    const double* src = h->state + sd.roff + (w == "inteAuxi" ? 0 : h->R);
                     if (out) DDPCA_HIP(hipMemcpy(out, src, std::min(n, cap) * sizeof(double), hipMemcpyDeviceToHost));
                     return;
                 }
@@ -995,7 +1050,7 @@ int64_t mcontact_gpu_get(mcontact_t h, const char* what, int64_t index, void* ou
             for (auto& I : h->itfs)
                 if (I.ts == index && I.mine) {
                     n = I.mip;
-                    if (out) DDPCA_HIP(hipMemcpy(out, h->gamma.p + I.goff, std::min(n, cap) * sizeof(double), hipMemcpyDeviceToHost));
+                    if (out) DDPCA_HIP(hipMemcpy(out, h->gamma + I.goff, std::min(n, cap) * sizeof(double), hipMemcpyDeviceToHost));
                     return;
                 }
             throw ApiError(DDPCA_EINVAL, "interface not handled by this rank");

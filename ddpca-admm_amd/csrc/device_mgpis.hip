@@ -240,18 +240,24 @@ __global__ __launch_bounds__(kBlock) void k_jac0(const double* b, const double* 
 }
 
 // b_c = mask_c (sum_children w r_f[child]), the coarse node's own fine copy first with w = 1;
-// optionally x_c = omega M b_c (CHEB: d_c too)
+// optionally x_c = omega M b_c (CHEB: d_c too).  Children in SELL-64 layout: slot k of chunk c
+// at (roff[c] + k) * 64 + lane, so index and weight loads are contiguous wave accesses.
 template <bool INIT, bool BJ, bool SETD>
-__global__ __launch_bounds__(kBlock) void k_restrict(const double* rf, const int64_t* rptr, const int32_t* rch,
-                                                     const double* rw, const uint8_t* cmask, double* bc, double* xc,
-                                                     double* dc, const double* minv, const double* coef, int64_t nc,
-                                                     const int32_t* csub, const PcgScal* sc) {
+__global__ __launch_bounds__(kBlock) void k_restrict(const double* rf, const int32_t* rslots, const int64_t* roff,
+                                                     const int32_t* rcol, const double* rwt, const uint8_t* cmask,
+                                                     double* bc, double* xc, double* dc, const double* minv,
+                                                     const double* coef, int64_t nc, const int32_t* csub,
+                                                     const PcgScal* sc) {
     NODE_PROLOGUE(nc, csub, sc)
-    const int64_t j = i;
+    const int64_t j = i, c = j >> 6;
+    const int ns = rslots[c];
+    const int32_t* cp = rcol + roff[c] * kChunk + (j & 63);
+    const double* wp = rwt + roff[c] * kChunk + (j & 63);
     double s0 = 0.0, s1 = 0.0, s2 = 0.0;
-    for (int64_t k = rptr[j]; k < rptr[j + 1]; ++k) {
-        const int64_t f = rch[k];
-        const double w = rw[k];
+#pragma unroll 4
+    for (int k = 0; k < ns; ++k) {
+        const int64_t f = __builtin_nontemporal_load(cp + (int64_t)k * kChunk);
+        const double w = __builtin_nontemporal_load(wp + (int64_t)k * kChunk);
         s0 += w * rf[3 * f];
         s1 += w * rf[3 * f + 1];
         s2 += w * rf[3 * f + 2];
@@ -792,7 +798,6 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
             const LevelDev& C = lev[l - 1];
             std::vector<int32_t> ppar(8 * L.nn, -1);
             std::vector<double> pw(8 * L.nn, 0.0);
-            std::vector<int64_t> cnt(C.nn + 1, 0);
             std::vector<std::vector<std::pair<int32_t, double>>> kids(C.nn);
             for (int s = 0; s < nsub; ++s) {
                 const Stencil& st = *subs[s].S[l - 1];
@@ -821,19 +826,33 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
                     }
                 }
             }
-            for (int64_t c = 0; c < C.nn; ++c) cnt[c + 1] = cnt[c] + (int64_t)kids[c].size();
-            std::vector<int32_t> rch(std::max<int64_t>(cnt[C.nn], 1));
-            std::vector<double> rw(std::max<int64_t>(cnt[C.nn], 1));
-            for (int64_t c = 0; c < C.nn; ++c)
-                for (size_t k = 0; k < kids[c].size(); ++k) {
-                    rch[cnt[c] + k] = kids[c][k].first;
-                    rw[cnt[c] + k] = kids[c][k].second;
+            // restriction children in SELL-64 over the coarse chunks; padding slots carry weight 0
+            // on the node's own first child (or fine node 0 for padding nodes)
+            std::vector<int32_t> rsl(C.nch, 0);
+            std::vector<int64_t> rof(C.nch + 1, 0);
+            for (int64_t c = 0; c < C.nch; ++c) {
+                size_t mx = 0;
+                for (int64_t j = c * kChunk; j < (c + 1) * kChunk; ++j) mx = std::max(mx, kids[j].size());
+                rsl[c] = (int32_t)mx;
+                rof[c + 1] = rof[c] + (int64_t)mx;
+            }
+            std::vector<int32_t> rcol(std::max<int64_t>(rof[C.nch] * kChunk, 1), 0);
+            std::vector<double> rwt(std::max<int64_t>(rof[C.nch] * kChunk, 1), 0.0);
+            for (int64_t j = 0; j < C.nn; ++j) {
+                const int64_t c = j / kChunk, lane = j % kChunk;
+                for (int64_t k = 0; k < rsl[c]; ++k) {
+                    const int64_t q = (rof[c] + k) * kChunk + lane;
+                    const bool real = k < (int64_t)kids[j].size();
+                    rcol[q] = real ? kids[j][k].first : (kids[j].empty() ? 0 : kids[j][0].first);
+                    rwt[q] = real ? kids[j][k].second : 0.0;
                 }
+            }
             L.ppar.upload(ppar);
             L.pw.upload(pw);
-            L.rptr.upload(cnt);
-            L.rch.upload(rch);
-            L.rw.upload(rw);
+            L.rslots.upload(rsl);
+            L.roff.upload(rof);
+            L.rcol.upload(rcol);
+            L.rwt.upload(rwt);
         }
     }
     fine_perm = perm[nlev - 1];
@@ -885,9 +904,22 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
     }
     cb[nsub] = F.nch;
     fin_cb.upload(cb);
-    for (auto* v : {&xs, &rs, &zs, &ps, &qs, &bs}) {
-        v->alloc(3 * F.nn);
-        v->zero(stream);
+    {
+        // the six PCG vectors in one allocation; DDPCA_STAGGER (doubles) shifts each vector's
+        // start so equal indices of z, p, q do not share address bits
+#ifdef DDPCA_STAGGER
+        const int64_t stag = DDPCA_STAGGER;
+#else
+        const int64_t stag = 0;
+#endif
+        const int64_t seg = (3 * F.nn + 511) / 512 * 512 + stag;
+        pcg_mem.alloc(6 * seg);
+        pcg_mem.zero(stream);
+        int i = 0;
+        for (auto* v : {&xs, &rs, &zs, &ps, &qs, &bs}) {
+            v->p = pcg_mem.p + (i++) * seg;
+            v->n = 3 * F.nn;
+        }
     }
     int64_t maxch = 0;
     for (auto& L : lev) maxch = std::max<int64_t>(maxch, L.nch);
@@ -1140,13 +1172,13 @@ void MgpisDevice::vcycle(const double* rin, double* zout, bool dot) {
         const int grid = ceil_div(C.nn, kBlock);
         const double* cf = c > 0 ? coef(c, 0) : nullptr;
         if (c == 0)
-            hipLaunchKernelGGL((k_restrict<false, false, false>), dim3(grid), dim3(kBlock), 0, stream, F.r.p, F.rptr.p, F.rch.p, F.rw.p, C.mask.p, C.b.p, nullptr, nullptr, nullptr, nullptr, C.nn, C.csub.p, scp);
+            hipLaunchKernelGGL((k_restrict<false, false, false>), dim3(grid), dim3(kBlock), 0, stream, F.r.p, F.rslots.p, F.roff.p, F.rcol.p, F.rwt.p, C.mask.p, C.b.p, nullptr, nullptr, nullptr, nullptr, C.nn, C.csub.p, scp);
         else if (cheb)
-            hipLaunchKernelGGL((k_restrict<true, true, true>), dim3(grid), dim3(kBlock), 0, stream, F.r.p, F.rptr.p, F.rch.p, F.rw.p, C.mask.p, C.b.p, cur[c], C.d.p, C.minv.p, cf, C.nn, C.csub.p, scp);
+            hipLaunchKernelGGL((k_restrict<true, true, true>), dim3(grid), dim3(kBlock), 0, stream, F.r.p, F.rslots.p, F.roff.p, F.rcol.p, F.rwt.p, C.mask.p, C.b.p, cur[c], C.d.p, C.minv.p, cf, C.nn, C.csub.p, scp);
         else if (bj)
-            hipLaunchKernelGGL((k_restrict<true, true, false>), dim3(grid), dim3(kBlock), 0, stream, F.r.p, F.rptr.p, F.rch.p, F.rw.p, C.mask.p, C.b.p, cur[c], nullptr, C.minv.p, cf, C.nn, C.csub.p, scp);
+            hipLaunchKernelGGL((k_restrict<true, true, false>), dim3(grid), dim3(kBlock), 0, stream, F.r.p, F.rslots.p, F.roff.p, F.rcol.p, F.rwt.p, C.mask.p, C.b.p, cur[c], nullptr, C.minv.p, cf, C.nn, C.csub.p, scp);
         else
-            hipLaunchKernelGGL((k_restrict<true, false, false>), dim3(grid), dim3(kBlock), 0, stream, F.r.p, F.rptr.p, F.rch.p, F.rw.p, C.mask.p, C.b.p, cur[c], nullptr, C.minv.p, cf, C.nn, C.csub.p, scp);
+            hipLaunchKernelGGL((k_restrict<true, false, false>), dim3(grid), dim3(kBlock), 0, stream, F.r.p, F.rslots.p, F.roff.p, F.rcol.p, F.rwt.p, C.mask.p, C.b.p, cur[c], nullptr, C.minv.p, cf, C.nn, C.csub.p, scp);
     }
     hipLaunchKernelGGL(k_coarse, dim3(ceil_div(3 * lev[0].nn, 4)), dim3(kBlock), 0, stream, ainv.p, aoff.p, c_noff.p, c_n.p,
                        lev[0].b.p, cur[0], 3 * lev[0].nn, lev[0].csub.p, scp);

@@ -82,9 +82,12 @@ struct LevelDev {
     // transfer from level l-1 (batch-global indices)
     DevBuf<int32_t> ppar;  // 8 x nn, slot-major, -1 = unused
     DevBuf<double> pw;
-    DevBuf<int64_t> rptr;  // nn_{l-1} + 1
-    DevBuf<int32_t> rch;
-    DevBuf<double> rw;
+    // restriction: SELL-64 over the coarse nodes of level l-1 (chunk = 64 coarse nodes, lane =
+    // node, slot k = k-th child: own fine copy first, padding = weight 0)
+    DevBuf<int32_t> rslots;  // per coarse chunk
+    DevBuf<int64_t> roff;    // per coarse chunk + 1
+    DevBuf<int32_t> rcol;    // fine node
+    DevBuf<double> rwt;
     // vectors (3 nn)
     DevBuf<double> x, t, b, r, d;
 };
@@ -116,7 +119,8 @@ public:
     std::vector<DevBuf<int32_t>> free_dof;
 
     // PCG work vectors (fine level, 3 nn_L) + per-subdomain scalars
-    DevBuf<double> xs, rs, zs, ps, qs, bs, partial;
+    DevBuf<double> pcg_mem, partial;         // pcg_mem holds the six vectors below
+    DevSpan<double> xs, rs, zs, ps, qs, bs;
     DevBuf<PcgScal> sc;
     PcgScal* sc_host = nullptr;      // pinned, filled by pcg_finish()
     MirrorBuf mirror;                // per-subdomain stop state, host-mapped

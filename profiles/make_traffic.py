@@ -8,7 +8,8 @@ over `bench.py --steps 1 --warmup 1`.  Only the fine-level launches (largest gri
 subdomain iterates are used (the first ADMM iteration's worm subdomains have a zero right-hand
 side and skip the kernel; those launches show about half the bytes and are dropped).
 
-Corrections (MI355X_MICROARCH.md, HBM/rocprofv3 section, checked here with scratch/calib.hip:
+Corrections (MI355X_MICROARCH.md, HBM/rocprofv3 section, checked here with profiles/calib_stream.hip
+(`hipcc --offload-arch=gfx950 -O3`, run under `rocprofv3 --pmc FETCH_SIZE`; r01_pmc_calibration.txt):
 1 GiB streamed with 8-B and 16-B lanes reads back FETCH_SIZE = 524,29x KB): FETCH_SIZE counts
 half of the bytes of coalesced streaming reads on gfx950 -> x2; WRITE_SIZE is taken as bytes.
 FETCH_SIZE counts L2 misses served by the Infinity Cache too, so it bounds HBM reads from above.
