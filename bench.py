@@ -51,6 +51,9 @@ def parse():
                     help="1: each subdomain PCG starts from its previous solution (same 1e-14 stop rule)")
     ap.add_argument("--precond-fp32", type=int, default=1,
                     help="1: V-cycle level operators stored in fp32 (arithmetic, Krylov operator and stop rule fp64)")
+    ap.add_argument("--table-mode", type=int, default=0,
+                    help="1: keep one copy of bit-identical operator rows (pays on regular meshes only; the "
+                         "synthetic box mesh is far more regular than DEHW's curved one, so the headline keeps 0)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=os.environ.get("DDPCA_TRAFFIC_JSON", str(ROOT / "profiles" / "traffic.json")),
                     help="PMC-derived HBM bytes per launch of the roofline kernel (profiles/make_traffic.py)")
@@ -83,7 +86,8 @@ def main():
     owner = part.block_owner(nsub, world)
     P.ESTABLISH(owner, rank)
     mc = D.MCONTACT(P, device=local, rank=rank, nranks=world, owner=owner, smoother=a.smoother, nu=a.nu,
-                    iters_per_graph=a.iters_per_graph, warm_start=a.warm_start, precond_fp32=a.precond_fp32)
+                    iters_per_graph=a.iters_per_graph, warm_start=a.warm_start, precond_fp32=a.precond_fp32,
+                    table_mode=a.table_mode)
     if world > 1:
         obj = [mc.unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
@@ -157,6 +161,7 @@ def main():
                 "smoother": {0: "jacobi", 1: "block-jacobi", 2: "chebyshev"}[a.smoother] + f"({a.nu})",
                 "pcg_x0": "previous solution" if a.warm_start else "zero",
                 "vcycle_operator_storage": "fp32" if a.precond_fp32 else "fp64",
+                "operator_rows": "deduplicated table" if a.table_mode else "streamed",
                 "parallelism": f"dd{world}",
             },
             "mgpis_dof_iter_per_s": dof_its / elapsed,
@@ -189,7 +194,7 @@ def main():
 
 def traffic_key(a) -> dict:
     return dict(groups=a.groups, nx=a.nx, ny=a.ny, nz=a.nz, gl=a.gl, smoother=a.smoother, nu=a.nu,
-                precond_fp32=a.precond_fp32)
+                precond_fp32=a.precond_fp32, table_mode=a.table_mode)
 
 
 def cpu_baseline(P, nsub, owner, budget_s=10.0):

@@ -48,6 +48,7 @@ void mgpis_default_options(mgpis_options_t* opt) {
     opt->iters_per_graph = 4;
     opt->warm_start = 0;
     opt->precond_fp32 = 0;
+    opt->table_mode = 1;
 }
 
 int ddpca_gpu_available(void) {
@@ -208,8 +209,8 @@ int mgpis_gpu_bench_spmv(mgpis_t h, int variant, int reps, double* ms, double* b
         // x, d, the 9-entry block inverse and writes d, x_new
         const double per_node[4] = {24.0, 96.0, 48.0, 24.0 * 5.0 + 72.0};
         const int mode = (variant >> 2) & 3;
-        const LevelDev& L = D.lev.back();
-        if (bytes) *bytes = 76.0 * (double)L.nnzb_sub[0] + (24.0 + per_node[mode]) * (double)L.nloc[0];
+        const bool f32 = (variant & 16) != 0;
+        if (bytes) *bytes = D.fine_matrix_bytes(0, f32) + (24.0 + per_node[mode]) * (double)D.lev.back().nloc[0];
     });
 }
 

@@ -6,11 +6,14 @@
 #include <array>
 #include <climits>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <numeric>
 #include <omp.h>
 #include <random>
 #include <thread>
+#include <unordered_map>
 
 #include "device_mgpis.hpp"
 
@@ -38,6 +41,10 @@ struct SellArgs {
     double* p;             // PCG: p (in place), CHEB: direction d (in place)
     const PcgScal* sc;     // per-subdomain stop flags / beta; nullptr = never stopped
     double* partial;       // per chunk
+    const int32_t* rtype;  // table mode: row -> table row
+    const double* tab;     // table mode: tstride doubles per table row, slot-major 3x3 blocks
+    int64_t tstride;
+    const int32_t* ctype;  // table mode: chunk -> its rows' common table row, -1 = mixed
 };
 
 __device__ __forceinline__ double wave_sum(double v) {
@@ -140,6 +147,76 @@ __device__ __forceinline__ void sell_rows(const int32_t* colp, const T* valp, co
     }
 }
 
+// Table mode: the row's blocks are the 9-double records tv[9k .. 9k+8] of its table row (shared
+// with every row of the same type, so they come from L1/L2), columns prefetched one group ahead.
+__device__ __forceinline__ void sell_rows_tbl(const int32_t* colp, const double* tv, const double* x, int ns,
+                                              double& s0, double& s1, double& s2) {
+    int k = 0;
+    int32_t c0 = 0, c1 = 0, c2 = 0;
+    if (ns >= 3) {
+        c0 = __builtin_nontemporal_load(colp);
+        c1 = __builtin_nontemporal_load(colp + kChunk);
+        c2 = __builtin_nontemporal_load(colp + 2 * kChunk);
+    }
+    auto blk = [&](const double* v, const double* xj) {
+        const double x0 = xj[0], x1 = xj[1], x2 = xj[2];
+        s0 += v[0] * x0 + v[1] * x1 + v[2] * x2;
+        s1 += v[3] * x0 + v[4] * x1 + v[5] * x2;
+        s2 += v[6] * x0 + v[7] * x1 + v[8] * x2;
+    };
+    for (; k + 3 <= ns; k += 3) {
+        const int64_t j0 = c0, j1 = c1, j2 = c2;
+        if (k + 6 <= ns) {
+            c0 = __builtin_nontemporal_load(colp + (int64_t)(k + 3) * kChunk);
+            c1 = __builtin_nontemporal_load(colp + (int64_t)(k + 4) * kChunk);
+            c2 = __builtin_nontemporal_load(colp + (int64_t)(k + 5) * kChunk);
+        }
+        blk(tv + 9 * k, x + 3 * j0);
+        blk(tv + 9 * (k + 1), x + 3 * j1);
+        blk(tv + 9 * (k + 2), x + 3 * j2);
+    }
+    for (; k < ns; ++k) blk(tv + 9 * k, x + 3 * (int64_t)colp[(int64_t)k * kChunk]);
+}
+
+// Table mode, type-homogeneous chunk: the table row is wave-uniform, so its values are read with
+// scalar loads into SGPRs (the FMAs take them as scalar operands): no per-lane value traffic.
+// XV selects how x_j is read: 0 production (x stride 3, three 8-B loads); diagnostics for
+// mgpis_gpu_bench_spmv: 3 x at the row's own node (coalesced bound, wrong product), 4 x stride 4
+// as one 16-B + one 8-B load, 5 x stride 4 as two 16-B loads.
+template <int XV = 0>
+__device__ __forceinline__ void sell_rows_uniform(const int32_t* colp, const double* __restrict__ tv, const double* x,
+                                                  int ns, int64_t row, double& s0, double& s1, double& s2) {
+#pragma unroll 3
+    for (int k = 0; k < ns; ++k) {
+        const int64_t j = __builtin_nontemporal_load(colp + (int64_t)k * kChunk);
+        double x0, x1, x2;
+        if constexpr (XV == 3) {
+            x0 = x[3 * row + (j & 0)];
+            x1 = x[3 * row + 1];
+            x2 = x[3 * row + 2];
+        } else if constexpr (XV == 4) {
+            const double2 a = reinterpret_cast<const double2*>(x)[2 * j];
+            x0 = a.x;
+            x1 = a.y;
+            x2 = x[4 * j + 2];
+        } else if constexpr (XV == 5) {
+            const double2 a = reinterpret_cast<const double2*>(x)[2 * j];
+            const double2 b = reinterpret_cast<const double2*>(x)[2 * j + 1];
+            x0 = a.x;
+            x1 = a.y;
+            x2 = b.x;
+        } else {
+            x0 = x[3 * j];
+            x1 = x[3 * j + 1];
+            x2 = x[3 * j + 2];
+        }
+        const double* v = tv + 9 * k;
+        s0 += v[0] * x0 + v[1] * x1 + v[2] * x2;
+        s1 += v[3] * x0 + v[4] * x1 + v[5] * x2;
+        s2 += v[6] * x0 + v[7] * x1 + v[8] * x2;
+    }
+}
+
 // Production loop variant per mode.  Measured on a 1.22M-dof fine level (mgpis_gpu_bench_spmv):
 // the column prefetch pays for the light-epilogue modes (y = Kx, residual), plain non-temporal
 // streaming for the PCG and Chebyshev epilogues; an XCD-contiguous chunk mapping (each XCD one
@@ -147,9 +224,9 @@ __device__ __forceinline__ void sell_rows(const int32_t* colp, const T* valp, co
 constexpr int default_variant(int mode) { return (mode == 0 || mode == 1) ? 2 : 1; }
 
 // One wavefront per 64-node chunk, one lane per node row, three accumulators per lane; T is the
-// storage type of the operator values (all arithmetic fp64).
-template <int MODE, bool BJ, bool DOT, typename T = double, int V = default_variant(MODE)>
-__global__ __launch_bounds__(kBlock) void k_sell(SellArgs a) {
+// storage type of streamed operator values (all arithmetic fp64); TBL: values from the table.
+template <int MODE, bool BJ, bool DOT, typename T = double, int V = default_variant(MODE), bool TBL = false>
+__global__ __launch_bounds__(kBlock) void k_sell(SellArgs a, const double* __restrict__ tab) {
     const int lane = threadIdx.x & 63;
     const int64_t c = (int64_t)blockIdx.x * (kBlock / kWave) + (threadIdx.x >> 6);
     if (c >= a.nch) return;
@@ -159,8 +236,18 @@ __global__ __launch_bounds__(kBlock) void k_sell(SellArgs a) {
     const int ns = a.slots[c];
     const int64_t base = a.off[c];
     double s0 = 0.0, s1 = 0.0, s2 = 0.0;
-    sell_rows<V>(a.col + base * kChunk + lane, static_cast<const T*>(a.val) + base * 9 * kChunk + lane, a.x, ns, row,
-                 s0, s1, s2);
+    if (TBL) {
+        // table loop variants (mgpis_gpu_bench_spmv): 0 per-lane table rows only, 3/4/5 the
+        // sell_rows_uniform diagnostics, others production
+        const int ct = V == 0 ? -1 : __builtin_amdgcn_readfirstlane(a.ctype[c]);
+        if (ct >= 0)
+            sell_rows_uniform<(V >= 3 ? V : 0)>(a.col + base * kChunk + lane, tab + (int64_t)ct * a.tstride, a.x, ns, row,
+                                                s0, s1, s2);
+        else
+            sell_rows_tbl(a.col + base * kChunk + lane, tab + (int64_t)a.rtype[row] * a.tstride, a.x, ns, s0, s1, s2);
+    } else
+        sell_rows<V>(a.col + base * kChunk + lane, static_cast<const T*>(a.val) + base * 9 * kChunk + lane, a.x, ns,
+                     row, s0, s1, s2);
     double dotv = 0.0;
     const int64_t o = 3 * row;
     if (MODE == kSpmv) {
@@ -549,10 +636,12 @@ bool invert3(const double m[9], double r[9]) {
     return true;
 }
 
-// Device node order of one level: lexicographic in (z, y, x), coordinates quantised to 1e-9 of
-// the bounding box so nodes of one mesh plane share a key despite rounding in their coordinates.
-// Returns p[reference node] = device node.
-std::vector<int32_t> lex_order(const double* xyz, int64_t n) {
+constexpr int64_t kMaxRowBlocks = 128;  // node-block row length bound of the setup sort
+
+// Quantised (z, y, x) keys of a level's nodes: coordinates quantised to 1e-9 of the bounding
+// box, so nodes of one mesh plane share a key despite rounding in their coordinates.
+using Key3 = std::array<int64_t, 3>;
+std::vector<Key3> quantised_keys(const double* xyz, int64_t n) {
     double lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0};
     for (int64_t i = 0; i < n; ++i)
         for (int a = 0; a < 3; ++a) {
@@ -561,18 +650,164 @@ std::vector<int32_t> lex_order(const double* xyz, int64_t n) {
         }
     const double ext = std::max({hi[0] - lo[0], hi[1] - lo[1], hi[2] - lo[2]});
     const double q = ext > 0.0 ? 1e-9 * ext : 1.0;
-    std::vector<std::array<int64_t, 3>> key(n);
+    std::vector<Key3> key(n);
     for (int64_t i = 0; i < n; ++i)
         key[i] = {std::llround((xyz[3 * i + 2] - lo[2]) / q), std::llround((xyz[3 * i + 1] - lo[1]) / q),
                   std::llround((xyz[3 * i] - lo[0]) / q)};
+    return key;
+}
+
+// Device node order of one level, p[reference node] = device node: lexicographic in (z, y, x);
+// with row types, grouped by type first (lexicographic inside a type), so 64-row chunks are
+// type-homogeneous wherever a type has enough rows.
+std::vector<int32_t> device_order(const std::vector<Key3>& key, const std::vector<int32_t>* type) {
+    const int64_t n = (int64_t)key.size();
     std::vector<int32_t> idx(n), p(n);
     std::iota(idx.begin(), idx.end(), 0);
-    std::stable_sort(idx.begin(), idx.end(), [&](int32_t a, int32_t b) { return key[a] < key[b]; });
+    std::stable_sort(idx.begin(), idx.end(), [&](int32_t a, int32_t b) {
+        if (type && (*type)[a] != (*type)[b]) return (*type)[a] < (*type)[b];
+        return key[a] < key[b];
+    });
     for (int64_t k = 0; k < n; ++k) p[idx[k]] = (int32_t)k;
     return p;
 }
 
-constexpr int64_t kMaxRowBlocks = 128;  // node-block row length bound of the setup sort
+// Canonical slot order of row r: its blocks sorted by the neighbour's quantised offset from the
+// row node -- independent of any numbering, so equal rows stay equal after renumbering.
+void canonical_slots(const Bsr3& A, int64_t r, const std::vector<Key3>& key, int64_t* ord) {
+    const int64_t len = A.ptr[r + 1] - A.ptr[r];
+    for (int64_t t = 0; t < len; ++t) ord[t] = A.ptr[r] + t;
+    const Key3& kr = key[r];
+    std::sort(ord, ord + len, [&](int64_t u, int64_t v) {
+        const Key3& a = key[A.col[u]];
+        const Key3& b = key[A.col[v]];
+        for (int d = 0; d < 3; ++d)
+            if (a[d] - kr[d] != b[d] - kr[d]) return a[d] - kr[d] < b[d] - kr[d];
+        return false;
+    });
+}
+
+// Bit-exact row types of one level of one subdomain: masked block values in canonical slot order.
+std::vector<int32_t> row_types(const Bsr3& A, const uint8_t* fr, const std::vector<Key3>& key, int64_t& ntypes) {
+    const int64_t n = A.nb;
+    std::vector<int32_t> t(n);
+    std::unordered_map<uint64_t, std::vector<int32_t>> bucket;
+    std::vector<std::vector<double>> reps;
+    std::vector<double> v;
+    int64_t ord[128];
+    for (int64_t r = 0; r < n; ++r) {
+        const int64_t len = A.ptr[r + 1] - A.ptr[r];
+        canonical_slots(A, r, key, ord);
+        v.assign(9 * len, 0.0);
+        for (int64_t s = 0; s < len; ++s) {
+            const int64_t k = ord[s], j = A.col[k];
+            for (int a = 0; a < 3; ++a)
+                for (int b = 0; b < 3; ++b) {
+                    double x = A.val[9 * k + 3 * a + b];
+                    if (!fr[3 * r + a] || !fr[3 * j + b]) x = (j == r && a == b) ? 1.0 : 0.0;
+                    v[9 * s + 3 * a + b] = x;
+                }
+        }
+        uint64_t h = 1469598103934665603ull ^ (uint64_t)len;
+        for (double x : v) {
+            uint64_t b;
+            std::memcpy(&b, &x, 8);
+            h = (h ^ b) * 1099511628211ull;
+            h ^= h >> 29;
+        }
+        auto& cand = bucket[h];
+        int32_t id = -1;
+        for (int32_t c : cand)
+            if (reps[c].size() == v.size() && std::memcmp(reps[c].data(), v.data(), v.size() * sizeof(double)) == 0) {
+                id = c;
+                break;
+            }
+        if (id < 0) {
+            id = (int32_t)reps.size();
+            cand.push_back(id);
+            reps.push_back(v);
+        }
+        t[r] = id;
+    }
+    ntypes = (int64_t)reps.size();
+    return t;
+}
+
+// Table mode of one level: every row's values (device slot order, masks applied, zero beyond the
+// row) are deduplicated bit-exactly, per subdomain in parallel, then merged into one table.  Used
+// when the table is at most a fifth of the streamed values (or when forced, for tests).
+void build_table(LevelDev& L, const std::vector<int32_t>& slots, const std::vector<int64_t>& off,
+                 const std::vector<double>& val, bool force) {
+    int64_t tmax = 0;
+    for (int32_t s : slots) tmax = std::max<int64_t>(tmax, s);
+    const int64_t ts9 = std::max<int64_t>(tmax * 9, 1);
+    const int nsub = (int)L.noff.size();
+    std::vector<std::vector<double>> subtab(nsub);
+    std::vector<int32_t> rt(L.nn, 0);
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int s = 0; s < nsub; ++s) {
+        std::unordered_map<uint64_t, std::vector<int32_t>> bucket;
+        std::vector<double>& T = subtab[s];
+        std::vector<double> rowv(ts9);
+        int32_t nt = 0;
+        for (int64_t g = L.noff[s]; g < L.noff[s] + pad64(L.nloc[s]); ++g) {
+            const int64_t c = g / kChunk, lane = g % kChunk;
+            std::fill(rowv.begin(), rowv.end(), 0.0);
+            for (int64_t t = 0; t < slots[c]; ++t)
+                for (int ij = 0; ij < 9; ++ij) rowv[t * 9 + ij] = val[((off[c] + t) * 9 + ij) * kChunk + lane];
+            uint64_t h = 1469598103934665603ull;
+            for (double v : rowv) {
+                uint64_t b;
+                std::memcpy(&b, &v, 8);
+                h = (h ^ b) * 1099511628211ull;
+                h ^= h >> 29;
+            }
+            int32_t id = -1;
+            auto& cand = bucket[h];
+            for (int32_t t : cand)
+                if (std::memcmp(&T[(size_t)t * ts9], rowv.data(), ts9 * sizeof(double)) == 0) {
+                    id = t;
+                    break;
+                }
+            if (id < 0) {
+                id = nt++;
+                cand.push_back(id);
+                T.insert(T.end(), rowv.begin(), rowv.end());
+            }
+            rt[g] = id;
+        }
+    }
+    int64_t ntypes = 0;
+    std::vector<int64_t> base(nsub);
+    for (int s = 0; s < nsub; ++s) {
+        base[s] = ntypes;
+        ntypes += (int64_t)subtab[s].size() / ts9;
+    }
+    const double tab_bytes = (double)ntypes * ts9 * 8.0, val_bytes = (double)val.size() * 8.0;
+    if (!force && tab_bytes > 0.2 * val_bytes) return;
+    std::vector<double> tab;
+    tab.reserve((size_t)ntypes * ts9);
+    for (int s = 0; s < nsub; ++s) {
+        tab.insert(tab.end(), subtab[s].begin(), subtab[s].end());
+        for (int64_t g = L.noff[s]; g < L.noff[s] + pad64(L.nloc[s]); ++g) rt[g] += (int32_t)base[s];
+    }
+    // chunks whose 64 rows share one type read their table row through scalar loads
+    std::vector<int32_t> ct(L.nch);
+    int64_t uniform = 0;
+    for (int64_t c = 0; c < L.nch; ++c) {
+        ct[c] = rt[c * kChunk];
+        for (int64_t lane = 1; lane < kChunk && ct[c] >= 0; ++lane)
+            if (rt[c * kChunk + lane] != ct[c]) ct[c] = -1;
+        uniform += ct[c] >= 0;
+    }
+    L.tbl = true;
+    L.tstride = ts9;
+    L.ntypes = ntypes;
+    L.nuniform = uniform;
+    L.rtype.upload(rt);
+    L.ctype.upload(ct);
+    L.tab.upload(tab);
+}
 
 std::vector<int32_t> identity_order(int64_t n) {
     std::vector<int32_t> p(n);
@@ -686,11 +921,37 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
     if (opt.nu < 1) opt.nu = 1;
     if (opt.iters_per_graph < 1) opt.iters_per_graph = 1;
     const bool bj = opt.smoother >= 1;
-    // device numbering: perm[l][s][reference local node] = device local node
+    // device numbering: perm[l][s][reference local node] = device local node.  Levels >= 1 with
+    // coordinates: lexicographic, or -- table mode, when the level's distinct rows compress --
+    // grouped by row type so chunks are type-homogeneous; their slots go in canonical order.
     std::vector<std::vector<std::vector<int32_t>>> perm(nlev, std::vector<std::vector<int32_t>>(nsub));
-    for (int l = 0; l < nlev; ++l)
-        for (int s = 0; s < nsub; ++s) perm[l][s] = (l > 0 && subs[s].coords) ? lex_order(subs[s].coords, subs[s].nnodes[l])
-                                                                              : identity_order(subs[s].nnodes[l]);
+    std::vector<std::vector<std::vector<Key3>>> keys(nlev, std::vector<std::vector<Key3>>(nsub));
+    std::vector<char> grouped(nlev, 0);
+    for (int l = 0; l < nlev; ++l) {
+        bool geo = l > 0;
+        for (int s = 0; s < nsub; ++s) geo = geo && subs[s].coords != nullptr;
+        if (!geo) {
+            for (int s = 0; s < nsub; ++s) perm[l][s] = identity_order(subs[s].nnodes[l]);
+            continue;
+        }
+        std::vector<std::vector<int32_t>> types(nsub);
+        double tab_blocks = 0.0, blocks = 0.0;
+#pragma omp parallel for schedule(dynamic, 1) reduction(+ : tab_blocks, blocks)
+        for (int s = 0; s < nsub; ++s) {
+            const Bsr3& A = *subs[s].K[l];
+            keys[l][s] = quantised_keys(subs[s].coords, subs[s].nnodes[l]);
+            if (opt.table_mode == 0) continue;
+            int64_t nt = 0, tmax = 0;
+            for (int64_t r = 0; r < A.nb; ++r) tmax = std::max<int64_t>(tmax, A.ptr[r + 1] - A.ptr[r]);
+            if (tmax > kMaxRowBlocks) continue;  // reported by the SELL build below
+            types[s] = row_types(A, subs[s].dof_free, keys[l][s], nt);
+            tab_blocks += (double)nt * (double)tmax;
+            blocks += (double)A.nnzb();
+        }
+        grouped[l] = opt.table_mode == 2 || (opt.table_mode == 1 && tab_blocks <= 0.2 * blocks);
+        for (int s = 0; s < nsub; ++s)
+            perm[l][s] = device_order(keys[l][s], grouped[l] && !types[s].empty() ? &types[s] : nullptr);
+    }
     lev.resize(nlev);
     for (int l = 0; l < nlev; ++l) {
         LevelDev& L = lev[l];
@@ -741,11 +1002,16 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
                 uint8_t m = 0;
                 for (int a = 0; a < 3; ++a) m |= fr[3 * r + a] ? (1 << a) : 0;
                 mask[g] = m;
-                // this row's blocks in increasing device column
+                // this row's blocks in canonical order (= increasing device column under the
+                // lexicographic numbering), else in increasing device column
                 int64_t ord[kMaxRowBlocks];
                 const int64_t len = A.ptr[r + 1] - A.ptr[r];
-                for (int64_t t = 0; t < len; ++t) ord[t] = A.ptr[r] + t;
-                std::sort(ord, ord + len, [&](int64_t u, int64_t v) { return p[A.col[u]] < p[A.col[v]]; });
+                if (!keys[l][s].empty()) {
+                    canonical_slots(A, r, keys[l][s], ord);
+                } else {
+                    for (int64_t t = 0; t < len; ++t) ord[t] = A.ptr[r] + t;
+                    std::sort(ord, ord + len, [&](int64_t u, int64_t v) { return p[A.col[u]] < p[A.col[v]]; });
+                }
                 double diag[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
                 for (int64_t t = 0; t < len; ++t) {
                     const int64_t k = ord[t], q = off[c] + t;
@@ -776,12 +1042,17 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
         L.csub.upload(csub);
         L.off.upload(off);
         L.col.upload(col);
+        if (opt.table_mode != 0 && l >= 1) build_table(L, slots, off, val, opt.table_mode == 2 || grouped[l]);
+        if (std::getenv("DDPCA_VERBOSE"))
+            std::fprintf(stderr, "[ddpca] level %d: %lld nodes, %lld chunks, %lld slots, table %d (%lld types, %lld uniform chunks)\n",
+                         l, (long long)L.nn, (long long)L.nch, (long long)L.nslots, (int)L.tbl, (long long)L.ntypes,
+                         (long long)L.nuniform);
         // fp64 values: the fine level (Krylov operator) and, without the fp32 preconditioner
         // copy, every level; the fp32 copy serves the V-cycle on levels >= 1 (level 0 is the
-        // dense inverse)
+        // dense inverse).  Table-mode levels need neither.
         const bool vc32 = opt.precond_fp32 != 0 && nlev > 1;
-        if (l == nlev - 1 || !vc32) L.val.upload(val);
-        if (vc32 && l >= 1) {
+        if (!L.tbl && (l == nlev - 1 || !vc32)) L.val.upload(val);
+        if (!L.tbl && vc32 && l >= 1) {
             std::vector<float> v32(val.size());
 #pragma omp parallel for schedule(static)
             for (int64_t i = 0; i < (int64_t)val.size(); ++i) v32[i] = (float)val[i];
@@ -1015,33 +1286,42 @@ SellArgs level_args(const LevelDev& L) {
     a.csub = L.csub.p;
     a.nch = L.nch;
     a.minv = L.minv.p;
+    if (L.tbl) {
+        a.val = nullptr;
+        a.rtype = L.rtype.p;
+        a.ctype = L.ctype.p;
+        a.tab = L.tab.p;
+        a.tstride = L.tstride;
+    }
     return a;
 }
 
-// one SELL launch over a level, values stored as fp32 (f32) or fp64
+// one SELL launch over a level: table mode when the arguments carry a table, else values
+// streamed as fp32 (f32) or fp64
 template <int MODE, bool BJ, bool DOT>
 void launch_sell(bool f32, const SellArgs& a, hipStream_t s) {
     const int grid = ceil_div(a.nch, 4);
-    if (f32) hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, float>), dim3(grid), dim3(kBlock), 0, s, a);
-    else hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, double>), dim3(grid), dim3(kBlock), 0, s, a);
+    if (a.tab) hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, double, default_variant(MODE), true>), dim3(grid), dim3(kBlock), 0, s, a, a.tab);
+    else if (f32) hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, float>), dim3(grid), dim3(kBlock), 0, s, a, a.tab);
+    else hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, double>), dim3(grid), dim3(kBlock), 0, s, a, a.tab);
 }
 
 template <int MODE, bool BJ, bool DOT>
 void launch_loop(int loop, bool f32, const SellArgs& a, int grid, hipStream_t s) {
     if (f32) {
         switch (loop) {
-            case 0: hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, float, 0>), dim3(grid), dim3(kBlock), 0, s, a); break;
-            case 1: hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, float, 1>), dim3(grid), dim3(kBlock), 0, s, a); break;
-            case 2: hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, float, 2>), dim3(grid), dim3(kBlock), 0, s, a); break;
-            default: hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, float, 3>), dim3(grid), dim3(kBlock), 0, s, a); break;
+            case 0: hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, float, 0>), dim3(grid), dim3(kBlock), 0, s, a, a.tab); break;
+            case 1: hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, float, 1>), dim3(grid), dim3(kBlock), 0, s, a, a.tab); break;
+            case 2: hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, float, 2>), dim3(grid), dim3(kBlock), 0, s, a, a.tab); break;
+            default: hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, float, 3>), dim3(grid), dim3(kBlock), 0, s, a, a.tab); break;
         }
         return;
     }
     switch (loop) {
-        case 0: hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, double, 0>), dim3(grid), dim3(kBlock), 0, s, a); break;
-        case 1: hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, double, 1>), dim3(grid), dim3(kBlock), 0, s, a); break;
-        case 2: hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, double, 2>), dim3(grid), dim3(kBlock), 0, s, a); break;
-        default: hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, double, 3>), dim3(grid), dim3(kBlock), 0, s, a); break;
+        case 0: hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, double, 0>), dim3(grid), dim3(kBlock), 0, s, a, a.tab); break;
+        case 1: hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, double, 1>), dim3(grid), dim3(kBlock), 0, s, a, a.tab); break;
+        case 2: hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, double, 2>), dim3(grid), dim3(kBlock), 0, s, a, a.tab); break;
+        default: hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, double, 3>), dim3(grid), dim3(kBlock), 0, s, a, a.tab); break;
     }
 }
 }  // namespace
@@ -1050,14 +1330,14 @@ namespace {
 // V-cycle-operator arguments of a level: the fp32 copy when the preconditioner stores it
 SellArgs vc_level_args(const MgpisDevice& D, int level) {
     SellArgs a = level_args(D.lev[level]);
-    if (D.vc32()) a.val = D.lev[level].val32.p;
+    if (D.vc32() && !D.lev[level].tbl) a.val = D.lev[level].val32.p;
     return a;
 }
 }  // namespace
 
 void MgpisDevice::spmv(int level, const double* x, double* y, bool vc_op) {
     SellArgs a = vc_op ? vc_level_args(*this, level) : level_args(lev[level]);
-    if (!a.val) throw ApiError(DDPCA_ESTATE, "operator of this level is not stored in the requested precision");
+    if (!a.val && !a.tab) throw ApiError(DDPCA_ESTATE, "operator of this level is not stored in the requested precision");
     a.x = x;
     a.y = y;
     launch_sell<kSpmv, false, false>(vc_op && vc32(), a, stream);
@@ -1067,15 +1347,21 @@ double MgpisDevice::bench_spmv(int variant, int reps) {
     // variant = loop (0..3) + 4 * mode (0 y = Kx, 1 PCG, 2 residual, 3 Chebyshev sweep) + 16 *
     // fp32 values (the V-cycle copy); fine level, whole batch, operands in the PCG work vectors
     // (values are irrelevant to the timing)
+    // table-mode levels (y = Kx only): + 32 selects the table diagnostics, loop 0 per-lane
+    // table rows, 1 production, 3 coalesced-x bound, 32 + 0/1 x stride 4 (16+8 B / 2x16 B loads)
     const LevelDev& L = lev.back();
     const int loop = variant & 3, mode = (variant >> 2) & 3;
     const bool f32 = (variant & 16) != 0;
-    if (variant >= 32) throw ApiError(DDPCA_EINVAL, "unknown SpMV variant");
+    const int tloop = (variant & 32) ? 4 + (loop & 1) : loop;
+    if (variant >= 64 || ((variant & 32) && (!L.tbl || mode != 0 || f32))) throw ApiError(DDPCA_EINVAL, "unknown SpMV variant");
     if (mode == 3 && (lev.size() < 2 || opt.smoother < 1)) throw ApiError(DDPCA_EINVAL, "Chebyshev mode needs block smoothing");
     if (f32 && !L.val32.p) throw ApiError(DDPCA_EINVAL, "no fp32 operator (precond_fp32 = 0)");
     DDPCA_HIP(hipMemsetAsync(sc.p, 0, nsub * sizeof(PcgScal), stream));  // done = 0, beta = 0
     SellArgs a = level_args(L);
-    if (f32) a.val = L.val32.p;
+    if (f32) {
+        a.val = L.val32.p;
+        a.tab = nullptr;
+    }
     a.x = xs.p;
     a.y = qs.p;
     a.p = ps.p;
@@ -1085,7 +1371,32 @@ double MgpisDevice::bench_spmv(int variant, int reps) {
     a.sc = sc.p;
     if (lev.size() > 1) a.coef = L.coef.p;
     const int grid = ceil_div(L.nch, 4);
+    DevBuf<double> x4;
+    if (tloop >= 4) {  // x in a 4-double-per-node copy
+        x4.alloc(4 * L.nn);
+        DDPCA_HIP(hipMemcpy2DAsync(x4.p, 32, xs.p, 24, 24, L.nn, hipMemcpyDeviceToDevice, stream));
+        a.x = x4.p;
+    }
     auto launch = [&]() {
+        if (a.tab && mode == 0 && tloop != 1) {
+#define TBL_V(v) hipLaunchKernelGGL((k_sell<kSpmv, false, false, double, v, true>), dim3(grid), dim3(kBlock), 0, stream, a, a.tab)
+            switch (tloop) {
+                case 0: TBL_V(0); break;
+                case 3: TBL_V(3); break;
+                case 4: TBL_V(4); break;
+                case 5: TBL_V(5); break;
+                default: TBL_V(2); break;
+            }
+#undef TBL_V
+            return;
+        }
+        if (a.tab) {  // table mode: one loop variant
+            if (mode == 0) launch_sell<kSpmv, false, false>(false, a, stream);
+            else if (mode == 1) launch_sell<kPcg, false, true>(false, a, stream);
+            else if (mode == 2) launch_sell<kResid, false, false>(false, a, stream);
+            else launch_sell<kCheb, true, false>(false, a, stream);
+            return;
+        }
         if (mode == 0) launch_loop<kSpmv, false, false>(loop, f32, a, grid, stream);
         else if (mode == 1) launch_loop<kPcg, false, true>(loop, f32, a, grid, stream);
         else if (mode == 2) launch_loop<kResid, false, false>(loop, f32, a, grid, stream);
@@ -1193,11 +1504,22 @@ void MgpisDevice::vcycle(const double* rin, double* zout, bool dot) {
     if (cur[Lf] != zout) throw ApiError(DDPCA_ESTATE, "V-cycle buffer parity");
 }
 
-double MgpisDevice::fine_kernel_bytes(int s) const {
-    // algorithmic bytes of one fine-level k_sell<kPcg> for member s: 76 B per stored block
-    // (72 value + 4 index) + z gathered once (24 B/node) + p, q read and written (4 x 24 B/node)
+double MgpisDevice::fine_matrix_bytes(int s, bool f32) const {
+    // operator bytes one fine-level pass reads for member s: streamed values = 4 B index + 72 B
+    // (fp64) or 36 B (fp32) per stored block; table mode = 4 B index per block + 4 B row type
+    // per node + the member's share of the table (read once per launch)
     const LevelDev& L = lev.back();
-    return 76.0 * (double)L.nnzb_sub[s] + 24.0 * 5.0 * (double)L.nloc[s];
+    if (!L.tbl) return (f32 ? 40.0 : 76.0) * (double)L.nnzb_sub[s];
+    double nodes = 0.0;
+    for (int64_t n : L.nloc) nodes += (double)n;
+    return 4.0 * (double)L.nnzb_sub[s] + 4.0 * (double)L.nloc[s] +
+           (double)L.ntypes * (double)L.tstride * 8.0 * (double)L.nloc[s] / nodes;
+}
+
+double MgpisDevice::fine_kernel_bytes(int s) const {
+    // algorithmic bytes of one fine-level k_sell<kPcg> for member s: the operator + z gathered
+    // once (24 B/node) + p, q read and written (4 x 24 B/node)
+    return fine_matrix_bytes(s, false) + 24.0 * 5.0 * (double)lev.back().nloc[s];
 }
 
 void MgpisDevice::enqueue_iteration(int prec, bool timed) {
@@ -1210,7 +1532,7 @@ void MgpisDevice::enqueue_iteration(int prec, bool timed) {
     a.partial = partial.p;
     const int nblk = ceil_div(L.nn, kBlock);
     if (timed) DDPCA_HIP(hipEventRecord(ev_k0, stream));
-    hipLaunchKernelGGL((k_sell<kPcg, false, true>), dim3(ceil_div(L.nch, 4)), dim3(kBlock), 0, stream, a);
+    launch_sell<kPcg, false, true>(false, a, stream);
     if (timed) DDPCA_HIP(hipEventRecord(ev_k1, stream));
     hipLaunchKernelGGL(k_fin, dim3(nsub), dim3(kBlock), 0, stream, (int)kFinAlpha, partial.p, nullptr, fin_cb.p, sc.p, mirror.dev);
     hipLaunchKernelGGL(k_axpy, dim3(nblk), dim3(kBlock), 0, stream, xs.p, rs.p, ps.p, qs.p, sc.p, partial.p, L.nn, L.csub.p);
@@ -1257,7 +1579,7 @@ void MgpisDevice::pcg_begin(int prec, double rtol, const std::vector<int64_t>& m
         a.b = bs.p;
         a.y = rs.p;
         a.partial = partial.p;
-        hipLaunchKernelGGL((k_sell<kResid, false, true>), dim3(ceil_div(L.nch, 4)), dim3(kBlock), 0, stream, a);
+        launch_sell<kResid, false, true>(false, a, stream);
         hipLaunchKernelGGL(k_fin, dim3(nsub), dim3(kBlock), 0, stream, (int)kFinInitWarm, partial.p, partial2, fin_cb.p, sc.p, mirror.dev);
     }
     if (prec == 1) vcycle(rs.p, zs.p, true);

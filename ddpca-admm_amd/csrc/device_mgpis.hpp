@@ -74,6 +74,16 @@ struct LevelDev {
     DevBuf<double> val;    // fp64 operator: fine level (Krylov operator), or every level when the
                            // V-cycle runs on fp64 operators
     DevBuf<float> val32;   // V-cycle operator rounded once to fp32 (opt.precond_fp32), levels >= 1
+    // table mode: rows whose block values (in device slot order, masks applied) are bit-identical
+    // share one table row; the kernel streams only column indices and a row type, the values
+    // come from the cache-resident table (structured meshes: ~30x fewer distinct rows than rows)
+    bool tbl = false;
+    int64_t tstride = 0;     // doubles per table row (max row length * 9)
+    int64_t ntypes = 0;
+    int64_t nuniform = 0;    // chunks whose rows all share one type
+    DevBuf<int32_t> rtype;   // per node row
+    DevBuf<int32_t> ctype;   // per chunk: the common type, -1 = mixed
+    DevBuf<double> tab;
     DevBuf<double> minv;   // point: 3 per node; block: 9 per node
     DevBuf<double> dinv;   // point Jacobi inverse (diagonal preconditioner at the fine level)
     DevBuf<uint8_t> mask;  // bit a set = dof 3i+a free
@@ -153,6 +163,7 @@ public:
     int64_t timed_kernel_samples = 0;
     bool time_kernel = false;
     double fine_kernel_bytes(int s) const;  // algorithmic bytes of the timed kernel, member s
+    double fine_matrix_bytes(int s, bool f32) const;  // operator bytes of one fine pass, member s
     double bench_spmv(int variant, int reps);  // ms per launch of a fine-level SpMV loop variant
     int64_t graphs_launched = 0;
 

@@ -49,6 +49,10 @@ typedef struct {
                           create; still exactly symmetric, all arithmetic fp64).  The Krylov
                           operator, vectors and the stop rule stay fp64, so the solution meets the
                           same ||r|| <= rtol ||b||; only the preconditioner differs slightly. */
+    int table_mode;    /* levels >= 1: 0 stream every block value; 1 (default) when the rows'
+                          block values deduplicate well (structured meshes), keep one copy per
+                          distinct row in a cache-resident table and stream only column indices
+                          and a row type -- the operator is bit-identical; 2 force (tests) */
 } mgpis_options_t;
 
 /* Fill default options. */
