@@ -66,6 +66,7 @@ def _declare(L: C.CDLL) -> None:
     L.ddpca_problem_set_ips.argtypes = [_P, C.c_int64, C.c_int64, _P, _P, _P, _P, _P, C.c_double, C.c_double,
                                         C.c_double]
     L.ddpca_problem_establish.argtypes = [_P]
+    L.ddpca_problem_set_coarse.argtypes = [_P, C.c_int64, _P]
     L.ddpca_problem_establish_owned.argtypes = [_P, _P, C.c_int]
     L.ddpca_problem_view.argtypes = [_P, C.c_char_p, C.c_int64, C.c_int64, C.POINTER(_P), _I64P,
                                      C.POINTER(C.c_int)]
@@ -186,6 +187,14 @@ class Problem:
         w = np.ascontiguousarray(w, dtype=np.float64)
         _check(lib().ddpca_problem_set_ips(self._h, ts, len(gap), _ptr(node), _ptr(shap), _ptr(basis), _ptr(gap),
                                            _ptr(w), fric, penN, penF))
+
+    def set_coarse(self, muscSett: int, doleMcsc: Optional[Sequence[int]] = None) -> "Problem":
+        """MCONTACT::muscSett / doleMcsc (MCONTACT.h:22-23) before ESTABLISH; 2 = the
+        interface-eliminated coarse space (MULTISCALE_1)."""
+        d = None if doleMcsc is None else np.ascontiguousarray(doleMcsc, dtype=np.int64)
+        _check(lib().ddpca_problem_set_coarse(self._h, int(muscSett), None if d is None else _ptr(d)))
+        self._keep_dole = d
+        return self
 
     def ESTABLISH(self, owner: Optional[Sequence[int]] = None, rank: int = 0) -> "Problem":
         """MCONTACT::ESTABLISH; with owner/rank only this rank's subdomains are built."""

@@ -289,6 +289,23 @@ int ddpca_problem_set_ips(ddpca_problem_t h, int64_t ts, int64_t n, const int64_
     });
 }
 
+int ddpca_problem_set_coarse(ddpca_problem_t h, int64_t muscSett, const int64_t* doleMcsc) {
+    return guarded([&] {
+        Problem& P = *reinterpret_cast<Problem*>(h);
+        if (P.established) throw ApiError(DDPCA_ESTATE, "set_coarse after establish");
+        if (muscSett & 1) throw ApiError(DDPCA_EINVAL, "muscSett bit 0 (MULTISCALE) is not supported; use 2");
+        if (muscSett < 0 || muscSett > 3) throw ApiError(DDPCA_EINVAL, "muscSett");
+        P.mc.muscSett = muscSett;
+        const int64_t nsub = (int64_t)P.mc.multGrid.size();
+        P.mc.doleMcsc.assign(nsub, 0);
+        for (int64_t tv = 0; tv < nsub; ++tv) {
+            const int64_t d = doleMcsc ? doleMcsc[tv] : 0;
+            if (d < 0 || d > P.mc.multGrid[tv].maxiLeve) throw ApiError(DDPCA_EINVAL, "doleMcsc out of range");
+            P.mc.doleMcsc[tv] = d;
+        }
+    });
+}
+
 int ddpca_problem_establish(ddpca_problem_t h) {
     return guarded([&] {
         Problem& P = *reinterpret_cast<Problem*>(h);
@@ -329,6 +346,40 @@ int ddpca_problem_view(ddpca_problem_t h, const char* cname, int64_t index, int6
             return;
         }
         const std::string key = name + "#" + std::to_string(index) + "#" + std::to_string(level);
+        // ---- coarse space (MCONTACT::MULTISCALE_1 output)
+        {
+            const CoarseSpace& cs = P.mc.coarse;
+            auto put_csr = [&](const Csr& m, const std::string& part) {
+                if (part == "ptr") put(m.ptr, data, count, dtype);
+                else if (part == "col") put(m.col, data, count, dtype);
+                else if (part == "val") put(m.val, data, count, dtype);
+                else if (part == "shape") { auto& v = P.cache_i64[key]; v = {m.nrow, m.ncol}; put(v, data, count, dtype); }
+                else throw ApiError(DDPCA_EINVAL, "csr part");
+            };
+            auto need = [&] { if (!cs.ready) throw ApiError(DDPCA_ESTATE, "no coarse space (set_coarse before establish)"); };
+            if (name == "baseReco") { need(); put(cs.baseReco, data, count, dtype); return; }
+            if (name == "globForc_1") { need(); put(cs.globForc_1, data, count, dtype); return; }
+            if (name == "doleMcsc") { put(P.mc.doleMcsc, data, count, dtype); return; }
+            if (name.rfind("globCoup_1:", 0) == 0) { need(); put_csr(cs.globCoup_1, name.substr(11)); return; }
+            if (name.rfind("globTran_1:", 0) == 0) {
+                need();
+                if (index < 0 || index >= 2 * nint) throw ApiError(DDPCA_EINVAL, "side index");
+                put_csr(cs.globTran_1[index / 2][index % 2], name.substr(11));
+                return;
+            }
+            for (const char* base : {"globTran_D_1:", "accuProl:"}) {
+                const std::string b(base);
+                if (name.rfind(b, 0) != 0) continue;
+                need();
+                if (index < 0 || index >= nsub || !cs.built[index]) throw ApiError(DDPCA_EINVAL, "subdomain index");
+                const std::string ck = b + std::to_string(index);
+                auto it = P.cache_csr.find(ck);
+                if (it == P.cache_csr.end())
+                    it = P.cache_csr.emplace(ck, b[0] == 'g' ? P.mc.globTran_D_1(index) : P.mc.accuProl(index)).first;
+                put_csr(it->second, name.substr(b.size()));
+                return;
+            }
+        }
         // ---- interface-side arrays: index = 2*ts + side
         static const char* kSideCsr[] = {"systMass", "systTran", "systTran_pena", "inteMass", "inteMass_pena",
                                           "inpoLagr", "inpoDisp", "inteInpo", "pemaInpo_r"};

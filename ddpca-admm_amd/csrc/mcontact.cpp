@@ -263,6 +263,20 @@ void MCONTACT::ESTABLISH(const std::vector<uint8_t>* owned) {
                          (long)tv, ms(t0, t1), ms(t1, t2), ms(t2, t3), ms(t3, t4));
         }
     }
+    // ---- coarse space (MCONTACT.h:858-863)
+    if (muscSett & 1)
+        throw std::invalid_argument("muscSett bit 0 (MULTISCALE, MCONTACT.h:898-1536) is not supported; use bit 1");
+    if (muscSett & 2) {
+        // the dof bookkeeping of every subdomain (baseReco) and the transfer stencils of the
+        // mates of owned interface sides (their restriction chains)
+        for (int64_t tv = 0; tv < (int64_t)multGrid.size(); ++tv) {
+            if (mine(tv)) continue;
+            MULTIGRID& g = multGrid[tv];
+            if (g.scalProl.empty()) g.TRANSFER();
+            g.FLAGS();
+        }
+        MULTISCALE_1(owned);
+    }
 }
 
 double MCONTACT::GET_CHAR_LENG() const {

@@ -38,11 +38,35 @@ struct Interface {
     void BUILD(const MULTIGRID& g0, const MULTIGRID& g1);
 };
 
+// Interface-eliminated coarse space (MCONTACT::MULTISCALE_1, MCONTACT.h:1672-2301).  Built
+// rank-locally: rows/columns that belong to owned subdomains and owned interface sides.
+struct CoarseSpace {
+    bool ready = false;
+    std::vector<uint8_t> built;               // per subdomain: its rows were assembled here
+    std::vector<int64_t> baseReco;            // nsub + 1 (MCONTACT.h:849-857)
+    int64_t n = 0;                            // globCoup_1 dimension
+    Csr globCoup_1;                           // n x n, rows of built subdomains
+    std::vector<double> globForc_1;           // n, rows of built subdomains
+    std::vector<std::array<Csr, 2>> globTran_1;  // [ts][s] n x comp*nnc_s (owned sides)
+    std::vector<Csr> globTran_S;              // [tv] n x 3N_tv: interface part of globTran_D_1
+                                              // (the stiffness part Rc consStif[L] C_L is applied
+                                              // in factored form)
+    std::vector<Stencil> accuQ;               // [tv] fine node -> level-d node prolongation chain
+};
+
+// prolOper[L-1] ... prolOper[d] of one grid as a single scalar stencil (no masks)
+Stencil accumulated_stencil(const MULTIGRID& g, int64_t d);
+
 class MCONTACT {
 public:
     std::vector<MULTIGRID> multGrid;
     std::vector<Interface> searCont;
-    int64_t muscSett = 0;
+    int64_t muscSett = 0;                  // bit 1: interface-eliminated coarse space
+    std::vector<int64_t> doleMcsc;         // coarse level per subdomain (MCONTACT.h:23)
+    CoarseSpace coarse;
+    void MULTISCALE_1(const std::vector<uint8_t>* owned = nullptr);
+    Csr globTran_D_1(int64_t tv) const;    // assembled (tests)
+    Csr accuProl(int64_t tv) const;        // assembled (tests)
     // ESTABLISH: interface operators, systMass added to each body's stiffness, then
     // TRANSFER / STIF_MATR / CONSTRAINT(1) per body (MCONTACT.h:812-825).  owned (optional):
     // per-subdomain mask; only owned bodies and interfaces touching them are built (one rank's

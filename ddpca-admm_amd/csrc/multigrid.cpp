@@ -367,12 +367,9 @@ void MULTIGRID::LOAD_ACCU(int64_t dof, double v) {
     else it->second = it->second + v;
 }
 
-void MULTIGRID::CONSTRAINT() {
+void MULTIGRID::FLAGS() {
     const int64_t N = numNodes();
     const int64_t L = maxiLeve;
-    levelStif.assign(L + 1, Bsr3());
-    levelStif[L] = origStif;
-    for (int64_t l = L - 1; l >= 0; --l) levelStif[l] = galerkin_rap(levelStif[l + 1], scalProl[l]);
     consFlag.assign(3 * N, 1);
     std::vector<double> dfull(3 * N, 0.0);
     for (const auto& kv : consDofv) {
@@ -392,11 +389,22 @@ void MULTIGRID::CONSTRAINT() {
         for (int64_t d = 0; d < 3 * leveCount[l]; ++d) c += consFlag[d];
         freeCount[l] = c;
     }
+}
+
+void MULTIGRID::CONSTRAINT() {
+    const int64_t N = numNodes();
+    const int64_t L = maxiLeve;
+    levelStif.assign(L + 1, Bsr3());
+    levelStif[L] = origStif;
+    for (int64_t l = L - 1; l >= 0; --l) levelStif[l] = galerkin_rap(levelStif[l + 1], scalProl[l]);
+    FLAGS();
+    std::vector<double> dfull(3 * N, 0.0);
+    for (const auto& kv : consDofv) dfull[kv.first] = kv.second;
     std::vector<double> f(3 * N, 0.0);
     for (const auto& kv : exteForc) f[kv.first] += kv.second;
     std::vector<double> Kd(3 * N, 0.0);
     if (!consDofv.empty()) levelStif[L].apply(dfull.data(), Kd.data());
-    consForc.assign(nf, 0.0);
+    consForc.assign(freeCount[L], 0.0);
     for (int64_t d = 0; d < 3 * N; ++d)
         if (consFlag[d]) consForc[freeIndex[d]] = f[d] - Kd[d];
 }

@@ -68,7 +68,8 @@ public:
     std::vector<int64_t> freeCount;       // free dofs on level l
     std::vector<double> consForc;         // condensed load (MULTIGRID::consForc)
     std::vector<double> dispForc;         // prescribed values of constrained dofs, dof order
-    void CONSTRAINT();
+    void FLAGS();       // the dof bookkeeping of CONSTRAINT only (consFlag/freeIndex/freeCount)
+    void CONSTRAINT();  // FLAGS + Galerkin hierarchy + condensed load
 
     // ---------------------------------------------------------------- per-iteration adapters
     // f_free = consOper * prolOper^T * earlTran^T * f_nodal (identities except consOper here)

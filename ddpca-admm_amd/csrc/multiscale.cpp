@@ -1,0 +1,372 @@
+// Host restatement of the interface-eliminated coarse space, MCONTACT::MULTISCALE_1
+// (MCONTACT.h:1672-2301), and of accuProl (MCONTACT.h:864-872), for the uniformly refined
+// hexahedral hierarchies of multigrid.cpp (earlTran, prolOper[maxiLeve] and CONT_ROTA are
+// identities there).  Setup only: the per-iteration correction runs on the GPU
+// (device_mcontact.hip, MCONTACT.h:2578-2612).
+//
+// Notation for body b: L = maxiLeve, d = doleMcsc[b], C_l = consOper[l] (free-dof selection),
+// Q = the nodal prolongation prolOper[L-1] ... prolOper[d] as one scalar stencil (fine node ->
+// level-d nodes, <= 8 parents for nested trilinear refinement), Rc = realProl[d]^T ...
+// realProl[L-1]^T (the condensed chain, masked at every level).  The reference uses Q inside
+// globCoup_1 and accuProl, and Rc for every right-hand-side operator; both are kept.
+#include <algorithm>
+#include <cstdio>
+#include <numeric>
+#include <stdexcept>
+#include <string>
+
+#include "mcontact.hpp"
+
+namespace ddpca {
+
+namespace {
+
+struct Trip {
+    int64_t r, c;
+    double v;
+};
+
+// CSR from triplets, duplicates summed, columns sorted (Eigen setFromTriplets)
+Csr from_triplets(int64_t nrow, int64_t ncol, std::vector<Trip>& t) {
+    std::sort(t.begin(), t.end(), [](const Trip& a, const Trip& b) { return a.r != b.r ? a.r < b.r : a.c < b.c; });
+    Csr m;
+    m.nrow = nrow;
+    m.ncol = ncol;
+    m.ptr.assign(nrow + 1, 0);
+    for (size_t k = 0; k < t.size();) {
+        size_t e = k;
+        double v = 0.0;
+        while (e < t.size() && t[e].r == t[k].r && t[e].c == t[k].c) v += t[e++].v;
+        if (t[k].r < 0 || t[k].r >= nrow || t[k].c < 0 || t[k].c >= ncol)
+            throw std::logic_error("MULTISCALE_1: triplet out of range");
+        m.col.push_back((int32_t)t[k].c);
+        m.val.push_back(v);
+        m.ptr[t[k].r + 1]++;
+        k = e;
+    }
+    for (int64_t r = 0; r < nrow; ++r) m.ptr[r + 1] += m.ptr[r];
+    return m;
+}
+
+void append(std::vector<Trip>& t, const Csr& A, int64_t roff, int64_t coff, double scale = 1.0) {
+    for (int64_t r = 0; r < A.nrow; ++r)
+        for (int64_t k = A.ptr[r]; k < A.ptr[r + 1]; ++k) t.push_back({roff + r, coff + A.col[k], scale * A.val[k]});
+}
+
+Csr transpose_csr(const Csr& A) {
+    std::vector<Trip> t;
+    t.reserve(A.nnz());
+    for (int64_t r = 0; r < A.nrow; ++r)
+        for (int64_t k = A.ptr[r]; k < A.ptr[r + 1]; ++k) t.push_back({A.col[k], r, A.val[k]});
+    return from_triplets(A.ncol, A.nrow, t);
+}
+
+// A * B, both CSR
+Csr spgemm(const Csr& A, const Csr& B) {
+    if (A.ncol != B.nrow) throw std::logic_error("MULTISCALE_1: spgemm shape");
+    std::vector<Trip> t;
+    for (int64_t r = 0; r < A.nrow; ++r)
+        for (int64_t k = A.ptr[r]; k < A.ptr[r + 1]; ++k) {
+            const int64_t i = A.col[k];
+            for (int64_t q = B.ptr[i]; q < B.ptr[i + 1]; ++q) t.push_back({r, B.col[q], A.val[k] * B.val[q]});
+        }
+    return from_triplets(A.nrow, B.ncol, t);
+}
+
+// free index -> nodal dof (all levels: the level-ordered numbering makes level l's free dofs a
+// prefix of the fine level's)
+std::vector<int64_t> free_to_dof(const MULTIGRID& g) {
+    std::vector<int64_t> f(g.freeCount.back());
+    for (int64_t d = 0; d < (int64_t)g.consFlag.size(); ++d)
+        if (g.freeIndex[d] >= 0) f[g.freeIndex[d]] = d;
+    return f;
+}
+
+// C_L A: nodal rows -> free rows of the fine level
+Csr rows_to_free(const MULTIGRID& g, const Csr& A) {
+    std::vector<Trip> t;
+    for (int64_t r = 0; r < A.nrow; ++r) {
+        const int32_t fr = g.freeIndex[r];
+        if (fr < 0) continue;
+        for (int64_t k = A.ptr[r]; k < A.ptr[r + 1]; ++k) t.push_back({fr, A.col[k], A.val[k]});
+    }
+    return from_triplets(g.freeCount.back(), A.ncol, t);
+}
+
+// A C_L^T C_L: zero the columns of constrained nodal dofs
+Csr drop_constrained_cols(const MULTIGRID& g, const Csr& A) {
+    Csr m = A;
+    for (int64_t k = 0; k < m.nnz(); ++k)
+        if (!g.consFlag[m.col[k]]) m.val[k] = 0.0;
+    return m;
+}
+
+// Rc A = realProl[d]^T ... realProl[L-1]^T A for A with rows = free dofs of level L
+// (MCONTACT.h:1885-1887, 2113-2115, 2142-2144, 2286-2288): scatter form, touching only A's
+// nonempty rows (surface operators).
+Csr restrict_chain(const MULTIGRID& g, int64_t d, const std::vector<int64_t>& f2d, Csr A) {
+    for (int64_t l = g.maxiLeve - 1; l >= d; --l) {
+        const Stencil& S = g.scalProl[l];
+        std::vector<Trip> t;
+        for (int64_t r = 0; r < A.nrow; ++r) {
+            if (A.ptr[r] == A.ptr[r + 1]) continue;
+            const int64_t dof = f2d[r];  // free row r of level l+1 -> nodal dof
+            const int64_t n = dof / 3, a = dof % 3;
+            for (int64_t s = S.ptr[n]; s < S.ptr[n + 1]; ++s) {
+                const int32_t c = g.freeIndex[3 * (int64_t)S.col[s] + a];
+                if (c < 0) continue;  // realProl keeps free coarse columns only
+                for (int64_t k = A.ptr[r]; k < A.ptr[r + 1]; ++k) t.push_back({c, A.col[k], S.w[s] * A.val[k]});
+            }
+        }
+        A = from_triplets(g.freeCount[l], A.ncol, t);
+    }
+    return A;
+}
+
+// Q (x) I3 C_d^T as rows 3*node + a for the selected fine nodes (others empty): nodal rows,
+// columns = free dofs of level d (MCONTACT.h:1794-1800, 1825-1827, 866-871)
+Csr nodal_prolong(const MULTIGRID& g, const Stencil& Q, int64_t d, const std::vector<uint8_t>* sel) {
+    std::vector<Trip> t;
+    for (int64_t n = 0; n < Q.nf; ++n) {
+        if (sel && !(*sel)[n]) continue;
+        for (int a = 0; a < 3; ++a)
+            for (int64_t k = Q.ptr[n]; k < Q.ptr[n + 1]; ++k) {
+                const int32_t c = g.freeIndex[3 * (int64_t)Q.col[k] + a];
+                if (c >= 0) t.push_back({3 * n + a, c, Q.w[k]});
+            }
+    }
+    return from_triplets(3 * Q.nf, g.freeCount[d], t);
+}
+
+Csr dense_vector_csr(const std::vector<double>& v) {
+    Csr m;
+    m.nrow = (int64_t)v.size();
+    m.ncol = 1;
+    m.ptr.assign(m.nrow + 1, 0);
+    for (int64_t i = 0; i < m.nrow; ++i) {
+        if (v[i] != 0.0) {
+            m.col.push_back(0);
+            m.val.push_back(v[i]);
+        }
+        m.ptr[i + 1] = (int64_t)m.col.size();
+    }
+    return m;
+}
+
+}  // namespace
+
+// Composite nodal prolongation from level d to the fine level (prolOper chain, no masks).
+Stencil accumulated_stencil(const MULTIGRID& g, int64_t d) {
+    const int64_t N = g.numNodes(), nd = g.leveCount.at(d);
+    Stencil Q;
+    Q.nf = N;
+    Q.nc = nd;
+    std::vector<std::vector<std::pair<int32_t, double>>> row(N);
+    for (int64_t n = 0; n < N; ++n) {
+        if (n < nd) {
+            row[n] = {{(int32_t)n, 1.0}};
+            continue;
+        }
+        const int lv = g.nodeLevel[n];  // created on level lv: parents on level lv - 1
+        const Stencil& S = g.scalProl[lv - 1];
+        std::vector<std::pair<int32_t, double>> acc;
+        for (int64_t k = S.ptr[n]; k < S.ptr[n + 1]; ++k)
+            for (const auto& e : row[S.col[k]]) acc.push_back({e.first, S.w[k] * e.second});
+        std::sort(acc.begin(), acc.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
+        auto& out = row[n];
+        for (const auto& e : acc) {
+            if (!out.empty() && out.back().first == e.first) out.back().second += e.second;
+            else out.push_back(e);
+        }
+    }
+    Q.ptr.assign(N + 1, 0);
+    for (int64_t n = 0; n < N; ++n) {
+        for (const auto& e : row[n]) {
+            Q.col.push_back(e.first);
+            Q.w.push_back(e.second);
+        }
+        Q.ptr[n + 1] = (int64_t)Q.col.size();
+    }
+    return Q;
+}
+
+void MCONTACT::MULTISCALE_1(const std::vector<uint8_t>* owned) {
+    const int64_t nsub = (int64_t)multGrid.size(), nint = (int64_t)searCont.size();
+    auto mine = [&](int64_t tv) { return !owned || (*owned)[tv] != 0; };
+    if ((int64_t)doleMcsc.size() != nsub) doleMcsc.assign(nsub, 0);  // MCONTACT.h:185-187
+    CoarseSpace& C = coarse;
+    C = CoarseSpace();
+    C.built.assign(nsub, 0);
+    // bodies whose restriction chain / nodal prolongation is needed here: owned ones and the
+    // mates of their interface sides
+    std::vector<uint8_t> need(nsub, 0);
+    for (int64_t tv = 0; tv < nsub; ++tv) need[tv] = mine(tv);
+    for (const auto& itf : searCont)
+        if (mine(itf.body[0]) || mine(itf.body[1])) need[itf.body[0]] = need[itf.body[1]] = 1;
+    for (int64_t tv = 0; tv < nsub; ++tv) {
+        const MULTIGRID& g = multGrid[tv];
+        if (need[tv] && g.freeCount.empty()) throw std::logic_error("MULTISCALE_1: grid flags missing");
+        if (doleMcsc[tv] < 0 || doleMcsc[tv] > g.maxiLeve) throw std::invalid_argument("doleMcsc out of range");
+    }
+    // baseReco (MCONTACT.h:849-857): every rank knows every subdomain's level-d size
+    C.baseReco.assign(nsub + 1, 0);
+    for (int64_t tv = 0; tv < nsub; ++tv) {
+        const MULTIGRID& g = multGrid[tv];
+        int64_t nd = 0;
+        if (!g.freeCount.empty()) nd = g.freeCount[doleMcsc[tv]];
+        else throw std::logic_error("MULTISCALE_1: every subdomain needs its dof flags (FLAGS)");
+        C.baseReco[tv + 1] = C.baseReco[tv] + nd;
+    }
+    C.n = C.baseReco[nsub];
+    std::vector<std::vector<int64_t>> f2d(nsub);
+    C.accuQ.assign(nsub, Stencil());
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int64_t tv = 0; tv < nsub; ++tv) {
+        if (!need[tv]) continue;
+        f2d[tv] = free_to_dof(multGrid[tv]);
+        C.accuQ[tv] = accumulated_stencil(multGrid[tv], doleMcsc[tv]);
+    }
+    for (int64_t tv = 0; tv < nsub; ++tv) C.built[tv] = mine(tv);
+    auto Rc = [&](int64_t tv, const Csr& A_free) { return restrict_chain(multGrid[tv], doleMcsc[tv], f2d[tv], A_free); };
+    auto QI = [&](int64_t tv, const std::vector<uint8_t>& sel) {
+        return nodal_prolong(multGrid[tv], C.accuQ[tv], doleMcsc[tv], &sel);
+    };
+    // ---- per interface side: nodal surface operators from the integration points
+    //      (MCONTACT.h:1699-1786, 1906-1990, 2007-2040, 2150-2246)
+    std::vector<Trip> coup;                       // globCoup_1 (owned rows)
+    std::vector<std::vector<Trip>> tranS(nsub);   // globTran_S[tv]
+    std::vector<double> forc(C.n, 0.0);
+    C.globTran_1.assign(nint, {});
+    for (int64_t ts = 0; ts < nint; ++ts) {
+        const Interface& itf = searCont[ts];
+        const int Cc = itf.comp();
+        const double pen[3] = {itf.penN, itf.penF, itf.penF};
+        for (int s = 0; s < 2; ++s) {
+            const int64_t e = itf.body[s], m = itf.body[1 - s];
+            if (!mine(e)) continue;
+            const MULTIGRID& ge = multGrid[e];
+            const MULTIGRID& gm = multGrid[m];
+            const int64_t Ne = ge.numNodes(), Nm = gm.numNodes();
+            std::vector<int64_t> cidx(Ne, -1);
+            for (size_t k = 0; k < itf.nodeCont[s].size(); ++k) cidx[itf.nodeCont[s][k]] = (int64_t)k;
+            std::vector<Trip> tS, tM, tMT, tTs, tTm;
+            std::vector<double> gap(3 * Ne, 0.0);
+            std::vector<uint8_t> sel_e(Ne, 0), sel_m(Nm, 0);
+            for (const auto& p : itf.ip) {
+                double G[3][3], GP[3][3];
+                for (int i = 0; i < 3; ++i)
+                    for (int j = 0; j < 3; ++j) {
+                        double x = 0, y = 0;
+                        for (int c = 0; c < Cc; ++c) {
+                            x += p.basis[c][i] * p.basis[c][j];
+                            y += p.basis[c][i] * pen[c] * p.basis[c][j];
+                        }
+                        G[i][j] = x;
+                        GP[i][j] = y;
+                    }
+                const double* Me = p.shap[s];
+                const double* Mm = p.shap[1 - s];
+                for (int a = 0; a < 4; ++a) {
+                    const int64_t na = p.node[s][a], ma = p.node[1 - s][a];
+                    sel_e[na] = 1;
+                    sel_m[ma] = 1;
+                    for (int b = 0; b < 4; ++b) {
+                        const int64_t nb = p.node[s][b], mb = p.node[1 - s][b];
+                        const double cee = -0.5 * p.w * Me[a] * Me[b];
+                        const double cem = -0.5 * p.w * Me[a] * Mm[b];
+                        const double cme = -0.5 * p.w * Mm[a] * Me[b];
+                        for (int i = 0; i < 3; ++i)
+                            for (int j = 0; j < 3; ++j) {
+                                tS.push_back({3 * na + i, 3 * nb + j, cee * GP[i][j]});
+                                tM.push_back({3 * na + i, 3 * mb + j, cem * GP[i][j]});
+                                tMT.push_back({3 * ma + i, 3 * nb + j, cme * GP[i][j]});
+                            }
+                        // globTran_1 (MCONTACT.h:2188-2245): self -1/2 w N_e^T T^T [T] N_e,
+                        // mate +1/2 w N_m^T T^T [T] N_e, columns = side s contact dofs
+                        const int64_t cb = cidx[nb];
+                        for (int i = 0; i < 3; ++i) {
+                            if (Cc == 1) {
+                                tTs.push_back({3 * na + i, cb, -0.5 * p.w * Me[a] * p.basis[0][i] * Me[b]});
+                                tTm.push_back({3 * ma + i, cb, 0.5 * p.w * Mm[a] * p.basis[0][i] * Me[b]});
+                            } else {
+                                for (int j = 0; j < 3; ++j) {
+                                    tTs.push_back({3 * na + i, 3 * cb + j, -0.5 * p.w * Me[a] * Me[b] * G[i][j]});
+                                    tTm.push_back({3 * ma + i, 3 * cb + j, 0.5 * p.w * Mm[a] * Me[b] * G[i][j]});
+                                }
+                            }
+                        }
+                    }
+                    // initial-gap force, normal only (MCONTACT.h:2061-2098), side 1 negated
+                    const double gsc = (s == 1 ? -0.5 : 0.5) * p.w * itf.penN * p.gap * Me[a];
+                    for (int i = 0; i < 3; ++i) gap[3 * na + i] += gsc * p.basis[0][i];
+                }
+            }
+            const Csr S = from_triplets(3 * Ne, 3 * Ne, tS);
+            const Csr Mx = from_triplets(3 * Ne, 3 * Nm, tM);
+            const Csr MT = from_triplets(3 * Nm, 3 * Ne, tMT);
+            const Csr Ts = from_triplets(3 * Ne, itf.mside(s), tTs);
+            const Csr Tm = from_triplets(3 * Nm, itf.mside(s), tTm);
+            // globCoup_1 += inteCoup[ts][s] (MCONTACT.h:1787-1841): Q-based Galerkin blocks
+            {
+                const Csr Qe = QI(e, sel_e), Qm = QI(m, sel_m);
+                const Csr QeT = transpose_csr(Qe);
+                append(coup, spgemm(QeT, spgemm(S, Qe)), C.baseReco[e], C.baseReco[e]);
+                append(coup, spgemm(QeT, spgemm(Mx, Qm)), C.baseReco[e], C.baseReco[m]);
+            }
+            // globTran_D_1 interface part (MCONTACT.h:1993-2048): rows e and rows m, columns = u_e
+            append(tranS[e], Rc(e, rows_to_free(ge, drop_constrained_cols(ge, S))), C.baseReco[e], 0);
+            append(tranS[e], Rc(m, rows_to_free(gm, drop_constrained_cols(ge, MT))), C.baseReco[m], 0);
+            // globForc_1 gap part (MCONTACT.h:2099-2109)
+            {
+                const Csr gc = Rc(e, rows_to_free(ge, dense_vector_csr(gap)));
+                for (int64_t r = 0; r < gc.nrow; ++r)
+                    for (int64_t k = gc.ptr[r]; k < gc.ptr[r + 1]; ++k) forc[C.baseReco[e] + r] += gc.val[k];
+            }
+            // globTran_1[ts][s] (MCONTACT.h:2248-2297)
+            {
+                std::vector<Trip> t;
+                append(t, Rc(e, rows_to_free(ge, Ts)), C.baseReco[e], 0);
+                append(t, Rc(m, rows_to_free(gm, Tm)), C.baseReco[m], 0);
+                C.globTran_1[ts][s] = from_triplets(C.n, itf.mside(s), t);
+            }
+        }
+    }
+    // ---- subdomain blocks: consStif[d] (MCONTACT.h:1675-1693) and Rc consForc (2052-2059)
+    for (int64_t tv = 0; tv < nsub; ++tv) {
+        if (!mine(tv)) continue;
+        const MULTIGRID& g = multGrid[tv];
+        append(coup, g.consStif(doleMcsc[tv]), C.baseReco[tv], C.baseReco[tv]);
+        const Csr fc = Rc(tv, dense_vector_csr(g.consForc));
+        for (int64_t r = 0; r < fc.nrow; ++r)
+            for (int64_t k = fc.ptr[r]; k < fc.ptr[r + 1]; ++k) forc[C.baseReco[tv] + r] += fc.val[k];
+    }
+    C.globCoup_1 = from_triplets(C.n, C.n, coup);
+    C.globForc_1 = std::move(forc);
+    C.globTran_S.assign(nsub, Csr());
+    for (int64_t tv = 0; tv < nsub; ++tv)
+        if (mine(tv)) C.globTran_S[tv] = from_triplets(C.n, 3 * multGrid[tv].numNodes(), tranS[tv]);
+    C.ready = true;
+}
+
+// Full globTran_D_1[tv] = Rc consStif[L] C_L + interface part (tests; the device applies the
+// stiffness part as an SpMV followed by the restriction chain instead)
+Csr MCONTACT::globTran_D_1(int64_t tv) const {
+    const MULTIGRID& g = multGrid.at(tv);
+    const std::vector<int64_t> f2d = free_to_dof(g);
+    Csr K = g.consStif(g.maxiLeve);
+    for (auto& c : K.col) c = (int32_t)f2d[c];
+    K.ncol = 3 * g.numNodes();
+    Csr R = restrict_chain(g, doleMcsc.at(tv), f2d, K);
+    std::vector<Trip> t;
+    append(t, R, coarse.baseReco[tv], 0);
+    append(t, coarse.globTran_S.at(tv), 0, 0);
+    return from_triplets(coarse.n, 3 * g.numNodes(), t);
+}
+
+// accuProl[tv] = C_L (Q (x) I3) C_d^T (MCONTACT.h:864-872), free_L x free_d
+Csr MCONTACT::accuProl(int64_t tv) const {
+    const MULTIGRID& g = multGrid.at(tv);
+    return rows_to_free(g, nodal_prolong(g, coarse.accuQ.at(tv), doleMcsc.at(tv), nullptr));
+}
+
+}  // namespace ddpca

@@ -127,8 +127,15 @@ int ddpca_problem_create(const char* kind, const double* params, int nparams, dd
 int ddpca_problem_set_ips(ddpca_problem_t p, int64_t ts, int64_t n, const int64_t* node,
                           const double* shap, const double* basis, const double* gap,
                           const double* w, double fric, double penN, double penF);
-/* MCONTACT::ESTABLISH (MCONTACT.h:181-896) minus the coarse space; single grids just run
- * TRANSFER / STIF_MATR / CONSTRAINT(1). */
+/* Coarse-space setting of MCONTACT (muscSett / doleMcsc, MCONTACT.h:22-23), before establish.
+ * muscSett = 2 selects the interface-eliminated coarse space (MULTISCALE_1, MCONTACT.h:
+ * 1672-2301; the examples' choice, e.g. BLOCK.h:38, TORSION.h:39, DEHW.h:2222), built by
+ * establish and applied by every ADMM iteration while tc <= MULT_MAXI (MCONTACT.h:2578-2612);
+ * doleMcsc[tv] = coarse level of subdomain tv (NULL = 0).  muscSett = 0 (default): none.
+ * Bit 0 (MULTISCALE, the LATIN-type space of CYLINDER.h:42) is not supported: DDPCA_EINVAL. */
+int ddpca_problem_set_coarse(ddpca_problem_t p, int64_t muscSett, const int64_t* doleMcsc);
+/* MCONTACT::ESTABLISH (MCONTACT.h:181-896); single grids just run TRANSFER / STIF_MATR /
+ * CONSTRAINT(1). */
 int ddpca_problem_establish(ddpca_problem_t p);
 /* Rank-local ESTABLISH: operators only for subdomains with owner[tv] == rank and for the
  * interfaces touching them (each process of a multi-GPU run builds its own share). */

@@ -12,11 +12,14 @@
 //   beam_nodd d0 d1 d2 globLeve outdir full(0/1) [cg(0/1)]
 //       single-domain BEAM (BEAM.h:251-311, 403-422) -> level fingerprints, consForc,
 //       one V-cycle application, CG_SOLV(1) and CG_SOLV(0) solutions + iteration counts.
-//   beam_dd d0 d1 d2 globLeve D0 D1 D2 outdir
-//       DD BEAM with glued interfaces (fricCoef=-1, BEAM.h:424-610), muscSett = 0.
-//   twoblock fric globLeve outdir
+//   beam_dd d0 d1 d2 globLeve D0 D1 D2 outdir [muscSett]
+//       DD BEAM with glued interfaces (fricCoef=-1, BEAM.h:424-610), muscSett = 0 unless given.
+//   twoblock fric globLeve outdir [muscSett]
 //       two stacked blocks, one contact interface (fric = 0: frictionless, > 0: Coulomb),
 //       built from the reference's MULTIGRID/CSEARCH/CURVEDS/MCONTACT API.
+//   With muscSett = 2 (interface-eliminated coarse space, MCONTACT.h:1672-2301) doleMcsc = 1
+//   for every subdomain (the examples' setting, e.g. BLOCK.h:38-41, DEHW.h:2222, 2239) and the
+//   coarse operators globCoup_1 / globForc_1 / globTran_1 / globTran_D_1 / accuProl are dumped.
 //   time_cg d0 d1 d2 globLeve reps
 //       wall time of MGPIS::CG_SOLV(1) on the BEAM mesh (CPU baseline calibration).
 #include "examples/BEAM.h"
@@ -276,6 +279,22 @@ void dump_mcontact(MCONTACT& mc, const std::string& moni_path) {
         while (f >> v) cont_out.push_back(v);
         save_dvec(pre + "resuCont", cont_out);
     }
+    if ((mc.muscSett >> 1) % 2 == 1) {
+        save_csr("globCoup_1", mc.globCoup_1);
+        save_vec("globForc_1", mc.globForc_1);
+        std::vector<int64_t> base(mc.baseReco.begin(), mc.baseReco.end());
+        save_ivec("baseReco", base);
+        std::vector<int64_t> dole(mc.doleMcsc.begin(), mc.doleMcsc.end());
+        save_ivec("doleMcsc", dole);
+        for (long tv = 0; tv < nsub; ++tv) {
+            save_csr("sd" + std::to_string(tv) + "_globTran_D_1", mc.globTran_D_1[tv]);
+            save_csr("sd" + std::to_string(tv) + "_accuProl", mc.accuProl[tv]);
+        }
+        for (long ts = 0; ts < nint; ++ts)
+            for (int s = 0; s < 2; ++s)
+                save_csr("if" + std::to_string(ts) + "_s" + std::to_string(s) + "_globTran_1", mc.globTran_1[ts][s]);
+    }
+    save_ivec("muscSett", {mc.muscSett});
     // resuMoni.txt (MCONTACT.h:2742-2836): one row per ADMM iteration
     std::ifstream f(moni_path);
     std::vector<double> rows;
@@ -291,13 +310,14 @@ void dump_mcontact(MCONTACT& mc, const std::string& moni_path) {
     save_npy(P("resuMoni"), rows.data(), {nrow, ncol});
 }
 
-int beam_dd(long d0, long d1, long d2, long gl, long D0, long D1, long D2) {
+int beam_dd(long d0, long d1, long d2, long gl, long D0, long D1, long D2, long musc) {
     BEAM beam(1);
     beam.diviNumb = {d0, d1, d2};
     beam.globLeve = gl;
     beam.domaNumb = {D0, D1, D2};
-    beam.muscSett = 0;
+    beam.muscSett = musc;
     beam.doleMcsc.clear();
+    if (musc) beam.doleMcsc.assign(D0 * D1 * D2, 1);
     double t0 = now_s();
     std::string log;
     capture_iters([&] { beam.SOLVE(1, 1, 0); }, &log);
@@ -423,9 +443,11 @@ void twoblock_build(MCONTACT& mc, double fric, long gl) {
     }, &log);
 }
 
-int twoblock(double fric, long gl) {
+int twoblock(double fric, long gl, long musc) {
     MCONTACT mc;
     twoblock_build(mc, fric, gl);
+    mc.muscSett = musc;
+    if (musc) mc.doleMcsc.assign(2, 1);
     std::string log;
     double t0 = now_s();
     capture_iters([&] {
@@ -481,11 +503,11 @@ int main(int argc, char** argv) {
     }
     if (mode == "beam_dd" && argc >= 10) {
         g_out = argv[9];
-        return beam_dd(L(2), L(3), L(4), L(5), L(6), L(7), L(8));
+        return beam_dd(L(2), L(3), L(4), L(5), L(6), L(7), L(8), argc >= 11 ? L(10) : 0);
     }
     if (mode == "twoblock" && argc >= 5) {
         g_out = argv[4];
-        return twoblock(std::stod(argv[2]), L(3));
+        return twoblock(std::stod(argv[2]), L(3), argc >= 6 ? L(5) : 0);
     }
     if (mode == "time_cg" && argc >= 7) return time_cg(L(2), L(3), L(4), L(5), L(6));
     std::fprintf(stderr, "bad arguments\n");

@@ -33,6 +33,11 @@ CASES = {
     # two stacked blocks: frictionless patch test and Coulomb friction (mu = 0.3)
     "twoblock_f0": ["twoblock", "0", "2", "{out}"],
     "twoblock_f3": ["twoblock", "0.3", "2", "{out}"],
+    # the same with the interface-eliminated coarse space (muscSett = 2, doleMcsc = 1,
+    # MCONTACT.h:1672-2301 / 2578-2612): converged runs, coarse operators dumped
+    "beam_dd_m2": ["beam_dd", "4", "2", "2", "2", "2", "1", "1", "{out}", "2"],
+    "twoblock_f0_m2": ["twoblock", "0", "2", "{out}", "2"],
+    "twoblock_f3_m2": ["twoblock", "0.3", "2", "{out}", "2"],
 }
 
 
