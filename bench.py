@@ -4,7 +4,8 @@ Workload (BASELINE.json configs[4]): 8 subdomains of 1.23M DOF
 (9.8M DOF), 4 worm/wheel groups -- each a frictional contact (mu = 0.2) between a worm block and
 a wheel block -- glued into two chains along x, 6 multigrid levels per subdomain.  One ADMM
 iteration = every subdomain's MGPIS PCG solve (1e-14 recursive residual, x0 = 0, as
-MGPIS::CG_SOLV) + the interface step + MONITOR.  The global problem is fixed and its subdomains
+MGPIS::CG_SOLV) + the interface-eliminated coarse-space correction (muscSett = 2, doleMcsc = 1:
+DEHW's own setting, DEHW.h:2222, 2239) + the interface step + MONITOR.  The global problem is fixed and its subdomains
 are spread over the ranks (strong scaling); N = 1 runs all 8 on one MI355X.
 
     python bench.py [--gpus N --steps K --warmup W]
@@ -54,6 +55,9 @@ def parse():
     ap.add_argument("--table-mode", type=int, default=0,
                     help="1: keep one copy of bit-identical operator rows (pays on regular meshes only; the "
                          "synthetic box mesh is far more regular than DEHW's curved one, so the headline keeps 0)")
+    ap.add_argument("--musc", type=int, default=2,
+                    help="muscSett: 2 = interface-eliminated coarse space every ADMM iteration (DEHW.h:2222), 0 = none")
+    ap.add_argument("--dole", type=int, default=1, help="doleMcsc: coarse-space level of every subdomain (DEHW.h:2239)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=os.environ.get("DDPCA_TRAFFIC_JSON", str(ROOT / "profiles" / "traffic.json")),
                     help="PMC-derived HBM bytes per launch of the roofline kernel (profiles/make_traffic.py)")
@@ -84,6 +88,8 @@ def main():
     P = D.Problem("dehw", a.groups, a.nx, a.ny, a.nz, a.gl, a.fric)
     nsub = P.nsub
     owner = part.block_owner(nsub, world)
+    if a.musc:
+        P.set_coarse(a.musc, [a.dole] * nsub)
     P.ESTABLISH(owner, rank)
     mc = D.MCONTACT(P, device=local, rank=rank, nranks=world, owner=owner, smoother=a.smoother, nu=a.nu,
                     iters_per_graph=a.iters_per_graph, warm_start=a.warm_start, precond_fp32=a.precond_fp32,
@@ -162,6 +168,7 @@ def main():
                 "pcg_x0": "previous solution" if a.warm_start else "zero",
                 "vcycle_operator_storage": "fp32" if a.precond_fp32 else "fp64",
                 "operator_rows": "deduplicated table" if a.table_mode else "streamed",
+                "coarse_space": f"interface-eliminated (muscSett={a.musc}, doleMcsc={a.dole})" if a.musc else "none",
                 "parallelism": f"dd{world}",
             },
             "mgpis_dof_iter_per_s": dof_its / elapsed,
@@ -194,7 +201,7 @@ def main():
 
 def traffic_key(a) -> dict:
     return dict(groups=a.groups, nx=a.nx, ny=a.ny, nz=a.nz, gl=a.gl, smoother=a.smoother, nu=a.nu,
-                precond_fp32=a.precond_fp32, table_mode=a.table_mode)
+                precond_fp32=a.precond_fp32, table_mode=a.table_mode)  # the SpMV launch is unchanged by musc
 
 
 def cpu_baseline(P, nsub, owner, budget_s=10.0):

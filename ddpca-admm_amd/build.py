@@ -27,7 +27,7 @@ COMMON = ["-O3", "-std=c++17", "-fPIC", "-fopenmp", "-Wall", "-Wno-unused-functi
           "-Wno-unknown-pragmas", f"-I{HERE.parent / 'include'}", f"-I{CSRC}",
           *os.environ.get("DDPCA_BUILD_DEFINES", "").split()]
 DEVICE = [f"--offload-arch={ARCH}", "-munsafe-fp-atomics"]
-LINK = ["-shared", "-fopenmp", f"--offload-arch={ARCH}", f"-L{ROCM / 'lib'}", "-lamdhip64", "-lrccl",
+LINK = ["-shared", "-fopenmp", f"--offload-arch={ARCH}", f"-L{ROCM / 'lib'}", "-lamdhip64", "-lrccl", "-lrocsolver", "-lrocblas",
         f"-Wl,-rpath,{ROCM / 'lib'}", f"-Wl,-rpath,{ROCM / 'llvm' / 'lib'}"]
 
 

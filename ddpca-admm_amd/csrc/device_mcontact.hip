@@ -24,6 +24,8 @@
 // Everything runs on the batch's single stream.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
+#include <rocblas/rocblas.h>
+#include <rocsolver/rocsolver.h>
 
 #include <algorithm>
 #include <chrono>
@@ -335,6 +337,77 @@ __global__ void k_reduce_pairs(const double* partial, int64_t nb, double* out2) 
     }
 }
 
+// ---- interface-eliminated coarse-space correction (MCONTACT.h:2578-2612)
+// y[r] = sum_k val[k] W[col[k]] + add[r]: one wavefront per row (coarse rows are long:
+// thousands of surface entries each)
+__global__ __launch_bounds__(256) void k_csr_wave(const int64_t* ptr, const int32_t* col, const double* val,
+                                                  int64_t nrow, const double* W, double* y, const double* add) {
+    const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= nrow) return;
+    const int lane = threadIdx.x & 63;
+    double s = 0.0;
+    for (int64_t k = ptr[r] + lane; k < ptr[r + 1]; k += 64) s += val[k] * W[col[k]];
+    s = wsum(s);
+    if (lane == 0) y[r] = add[r] + s;
+}
+
+// g[rows[i]] -= yd[src[i]]: the stiffness part of globTran_D_1 u, restricted on the device
+__global__ void k_cs_kpart(const int32_t* rows, const int64_t* src, const double* yd, double* g, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) g[rows[i]] -= yd[src[i]];
+}
+
+// x[i] = sum_j A[i n + j] g[j]: one wavefront per row of the owned block of globCoup_1^-1
+__global__ __launch_bounds__(256) void k_gemv_wave(const double* A, const double* g, double* x, int64_t m, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (i >= m) return;
+    const int lane = threadIdx.x & 63;
+    const double* a = A + i * n;
+    double s = 0.0;
+    for (int64_t j = lane; j < n; j += 64) s += a[j] * g[j];
+    s = wsum(s);
+    if (lane == 0) x[i] = s;
+}
+
+// xn = C_d^T xc: nodal level-d values of the owned subdomains (constrained dofs 0)
+__global__ void k_cs_scatter(const int32_t* src, const double* xc, double* xn, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) xn[i] = src[i] >= 0 ? xc[src[i]] : 0.0;
+}
+
+// u += OUTP_SUB1(accuProl xc): free dofs get (Q (x) I3) xn, constrained dofs their prescribed
+// value again (MCONTACT.h:2606-2608 adds OUTP_SUB1's output, Dirichlet values included).
+// One thread per batch fine node in the reference order; Q slot-major, <= 8 parents.
+__global__ void k_cs_prolong(const int32_t* qcol, const double* qw, int64_t nn, const double* xn, const uint8_t* flag,
+                             const double* presc, double* u) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nn) return;
+    double e0 = 0.0, e1 = 0.0, e2 = 0.0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const int32_t c = qcol[(int64_t)k * nn + i];
+        if (c < 0) break;
+        const double w = qw[(int64_t)k * nn + i];
+        e0 += w * xn[c];
+        e1 += w * xn[c + 1];
+        e2 += w * xn[c + 2];
+    }
+    const double e[3] = {e0, e1, e2};
+    for (int a = 0; a < 3; ++a) {
+        const int64_t d = 3 * i + a;
+        u[d] += flag[d] ? e[a] : presc[d];
+    }
+}
+
+// potri(lower) on the column-major view leaves the inverse in the row-major upper triangle;
+// mirror it into the lower one
+__global__ void k_fill_lower(double* A, int64_t n) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= n * n) return;
+    const int64_t i = idx / n, j = idx % n;
+    if (j < i) A[i * n + j] = A[j * n + i];
+}
+
 inline int nb256(int64_t n) { return (int)std::max<int64_t>(1, (n + 255) / 256); }
 
 // Row lists -> SELL-64 (rows padded to a multiple of 64; padding slots: column 0, value 0).
@@ -502,6 +575,38 @@ private:
 
 }  // namespace
 
+// Interface-eliminated coarse space on the device (MCONTACT.h:2578-2612, operators from
+// MULTISCALE_1).  Per ADMM iteration, after the subdomain solves:
+//   g  = globForc_1 + sum globTran_1 lambda - sum globTran_D_1 u          (2580-2587)
+//        globTran_D_1 u = Rc (consStif[L] x) + interface part; the stiffness part is one fp64
+//        SpMV of the batch's fine operator followed by the restriction chain to level doleMcsc
+//        (factored: Rc consStif[L] would have ~30 entries per fine dof), the rest is one CSR
+//        product over the workspace W (columns: owned u and lambda)
+//   g summed over ranks (each rank holds the columns it owns), one RCCL all-reduce
+//   xc = globCoup_1^-1 g, rows of the owned subdomains (dense inverse from rocSOLVER potrf/potri
+//        at setup; the reference factorises with SimplicialLDLT, 2589-2591)
+//   u += OUTP_SUB1(accuProl xc)                                             (2600-2610)
+struct CoarseDev {
+    bool on = false, inverted = false;
+    int64_t n = 0, nown = 0, nxn = 0, qnn = 0;
+    DevBuf<double> g, f0, xc, xn, ainv;
+    DevBuf<int64_t> rptr;
+    DevBuf<int32_t> rcol;
+    DevBuf<double> rval;
+    struct KGroup {
+        int level = 0;
+        DevBuf<int32_t> rows;
+        DevBuf<int64_t> src;
+    };
+    std::vector<KGroup> kg;
+    int dmin = 0;
+    DevBuf<int32_t> xsrc, qcol;
+    DevBuf<double> qw;
+    DevBuf<uint8_t> flag;
+    std::vector<int64_t> own_rows;  // global coarse rows of this rank, in xc order
+    std::vector<double> dense;      // host, until inverted: this rank's rows of globCoup_1 (n x n, zeros elsewhere)
+};
+
 // ================================================================================ handle
 struct ddpca_mcontact {
     struct Sub {
@@ -548,6 +653,7 @@ struct ddpca_mcontact {
     DevBuf<double> uo, state_old, gcst, partial, moni;
     SellOp op_gamma, op_aux, op_lam;     // gamma (my halves), aux RHS, lambda RHS
     MassBatch mb_aux, mb_lam;
+    CoarseDev cs;
     std::vector<double> moni_host;
     hipStream_t main = nullptr;          // == mg->stream
     ncclComm_t comm = nullptr;
@@ -789,6 +895,207 @@ void build(ddpca_mcontact& H, Problem& P) {
     DDPCA_HIP(hipStreamSynchronize(H.main));
 }
 
+// ---- coarse space: device operands from the host MULTISCALE_1 output
+void build_coarse(ddpca_mcontact& H, Problem& P) {
+    MCONTACT& mc = P.mc;
+    const CoarseSpace& cs = mc.coarse;
+    CoarseDev& C = H.cs;
+    if (!(mc.muscSett & 2)) return;
+    if (!cs.ready) throw ApiError(DDPCA_ESTATE, "muscSett = 2 but the coarse space was not built");
+    C.on = true;
+    C.n = cs.n;
+    const int64_t n = C.n;
+    std::vector<int64_t> xoff(H.subs.size());
+    for (size_t i = 0; i < H.subs.size(); ++i) {
+        const int64_t tv = H.subs[i].tv;
+        if (!cs.built[tv]) throw ApiError(DDPCA_ESTATE, "coarse rows of an owned subdomain were not built");
+        xoff[i] = (int64_t)C.own_rows.size();
+        for (int64_t r = cs.baseReco[tv]; r < cs.baseReco[tv + 1]; ++r) C.own_rows.push_back(r);
+    }
+    C.nown = (int64_t)C.own_rows.size();
+    // RHS rows over W: + globTran_1 (owned sides, lambda columns), - interface part of
+    // globTran_D_1 (owned subdomains, u columns)
+    std::vector<std::vector<std::pair<int32_t, double>>> rows(n);
+    for (const auto& sd : H.sides) {
+        const Csr& T = cs.globTran_1[sd.ts][sd.s];
+        const int64_t lam0 = H.oS + H.R + sd.roff;
+        for (int64_t r = 0; r < T.nrow; ++r)
+            for (int64_t k = T.ptr[r]; k < T.ptr[r + 1]; ++k) rows[r].push_back({(int32_t)(lam0 + T.col[k]), T.val[k]});
+    }
+    for (size_t i = 0; i < H.subs.size(); ++i) {
+        const Csr& T = cs.globTran_S[H.subs[i].tv];
+        const int64_t u0 = H.subs[i].dof0;
+        for (int64_t r = 0; r < T.nrow; ++r)
+            for (int64_t k = T.ptr[r]; k < T.ptr[r + 1]; ++k) rows[r].push_back({(int32_t)(u0 + T.col[k]), -T.val[k]});
+    }
+    {
+        std::vector<int64_t> ptr(n + 1, 0);
+        std::vector<int32_t> col;
+        std::vector<double> val;
+        for (int64_t r = 0; r < n; ++r) {
+            auto& row = rows[r];
+            std::sort(row.begin(), row.end());
+            for (const auto& e : row) {
+                col.push_back(e.first);
+                val.push_back(e.second);
+            }
+            ptr[r + 1] = (int64_t)col.size();
+            std::vector<std::pair<int32_t, double>>().swap(row);
+        }
+        C.rptr.upload(ptr);
+        C.rcol.upload(col.empty() ? std::vector<int32_t>{0} : col);
+        C.rval.upload(val.empty() ? std::vector<double>{0.0} : val);
+    }
+    std::vector<double> f0(n, 0.0);
+    for (int64_t r : C.own_rows) f0[r] = cs.globForc_1[r];
+    C.f0.upload(f0);
+    C.g.alloc(std::max<int64_t>(n, 1));
+    C.xc.alloc(std::max<int64_t>(C.nown, 1));
+    // dense rows of globCoup_1 (inverted once every rank holds all rows)
+    C.dense.assign((size_t)n * n, 0.0);
+    for (int64_t r : C.own_rows)
+        for (int64_t k = cs.globCoup_1.ptr[r]; k < cs.globCoup_1.ptr[r + 1]; ++k)
+            C.dense[(size_t)r * n + cs.globCoup_1.col[k]] = cs.globCoup_1.val[k];
+    if (!H.mg) return;
+    MgpisDevice& D = *H.mg;
+    const int L = (int)D.lev.size() - 1;
+    // stiffness part: gather level-d device values into the owned coarse rows
+    C.dmin = L;
+    std::map<int, std::pair<std::vector<int32_t>, std::vector<int64_t>>> groups;
+    std::vector<int64_t> xnoff(H.subs.size(), 0);
+    int64_t nxn = 0;
+    for (size_t i = 0; i < H.subs.size(); ++i) {
+        const int64_t tv = H.subs[i].tv;
+        const MULTIGRID& g = mc.multGrid[tv];
+        const int d = (int)mc.doleMcsc[tv];
+        if (g.maxiLeve != L) throw ApiError(DDPCA_EINVAL, "batched subdomains need equal level counts");
+        C.dmin = std::min(C.dmin, d);
+        auto& grp = groups[d];
+        const auto& perm = D.level_perm[d][i];
+        for (int64_t dof = 0; dof < 3 * g.leveCount[d]; ++dof) {
+            const int32_t fi = g.freeIndex[dof];
+            if (fi < 0) continue;
+            grp.first.push_back((int32_t)(cs.baseReco[tv] + fi));
+            grp.second.push_back(3 * (D.lev[d].noff[i] + perm[dof / 3]) + dof % 3);
+        }
+        xnoff[i] = nxn;
+        nxn += 3 * g.leveCount[d];
+    }
+    for (auto& kv : groups) {
+        CoarseDev::KGroup G;
+        G.level = kv.first;
+        G.rows.upload(kv.second.first);
+        G.src.upload(kv.second.second);
+        C.kg.push_back(std::move(G));
+    }
+    // xn <- xc, and the accumulated prolongation (fine node -> level-d node) per batch node
+    C.nxn = nxn;
+    std::vector<int32_t> xsrc(std::max<int64_t>(nxn, 1), -1);
+    C.qnn = D.lev.back().nn;
+    std::vector<int32_t> qcol(8 * C.qnn, -1);
+    std::vector<double> qw(8 * C.qnn, 0.0);
+    std::vector<uint8_t> flag(H.NU, 0);
+    for (size_t i = 0; i < H.subs.size(); ++i) {
+        const int64_t tv = H.subs[i].tv;
+        const MULTIGRID& g = mc.multGrid[tv];
+        const int d = (int)mc.doleMcsc[tv];
+        for (int64_t dof = 0; dof < 3 * g.leveCount[d]; ++dof) {
+            const int32_t fi = g.freeIndex[dof];
+            xsrc[xnoff[i] + dof] = fi < 0 ? -1 : (int32_t)(xoff[i] + fi);
+        }
+        const Stencil& Q = cs.accuQ[tv];
+        const int64_t b0 = H.subs[i].dof0 / 3;
+        for (int64_t nd = 0; nd < Q.nf; ++nd) {
+            const int64_t len = Q.ptr[nd + 1] - Q.ptr[nd];
+            if (len > 8) throw ApiError(DDPCA_EINVAL, "accumulated prolongation with more than 8 parents");
+            for (int64_t k = 0; k < len; ++k) {
+                qcol[k * C.qnn + b0 + nd] = (int32_t)(xnoff[i] + 3 * Q.col[Q.ptr[nd] + k]);
+                qw[k * C.qnn + b0 + nd] = Q.w[Q.ptr[nd] + k];
+            }
+        }
+        for (int64_t dof = 0; dof < 3 * g.numNodes(); ++dof) flag[H.subs[i].dof0 + dof] = g.consFlag[dof];
+    }
+    C.xsrc.upload(xsrc);
+    C.xn.alloc(std::max<int64_t>(nxn, 1));
+    C.qcol.upload(qcol);
+    C.qw.upload(qw);
+    C.flag.upload(flag);
+}
+
+// globCoup_1^-1 rows of the owned subdomains: every rank's rows are summed into a full dense
+// copy (one RCCL all-reduce at setup), factorised by rocSOLVER (potrf + potri) on the device
+void coarse_invert(ddpca_mcontact& H) {
+    CoarseDev& C = H.cs;
+    if (!C.on || C.inverted) return;
+    const int64_t n = C.n;
+    if (n > 46000) throw ApiError(DDPCA_EINVAL, "coarse space too large for the dense inverse (n > 46000)");
+    DevBuf<double> A;
+    A.upload(C.dense);
+    std::vector<double>().swap(C.dense);
+    hipStream_t st = H.main;
+    if (H.nranks > 1) {
+        if (!H.comm) throw ApiError(DDPCA_ESTATE, "the coarse space of a multi-rank run needs mcontact_gpu_comm_init");
+        DDPCA_NCCL(ncclAllReduce(A.p, A.p, (size_t)n * n, ncclDouble, ncclSum, H.comm, st));
+    }
+    rocblas_handle rh = nullptr;
+    if (rocblas_create_handle(&rh) != rocblas_status_success) throw ApiError(DDPCA_EHIP, "rocblas_create_handle");
+    DevBuf<rocblas_int> info(2);
+    info.zero(st);
+    rocblas_set_stream(rh, st);
+    const rocblas_status s1 = rocsolver_dpotrf(rh, rocblas_fill_lower, (rocblas_int)n, A.p, (rocblas_int)n, info.p);
+    const rocblas_status s2 = rocsolver_dpotri(rh, rocblas_fill_lower, (rocblas_int)n, A.p, (rocblas_int)n, info.p + 1);
+    hipLaunchKernelGGL(k_fill_lower, dim3(std::max<int64_t>(1, ((int64_t)n * n + 255) / 256)), dim3(256), 0, st, A.p, n);
+    C.ainv.alloc(std::max<int64_t>(C.nown, 1) * n);
+    // owned rows are contiguous per subdomain (baseReco blocks)
+    for (size_t k = 0; k < C.own_rows.size();) {
+        size_t e = k;
+        while (e + 1 < C.own_rows.size() && C.own_rows[e + 1] == C.own_rows[e] + 1) ++e;
+        DDPCA_HIP(hipMemcpyAsync(C.ainv.p + k * n, A.p + C.own_rows[k] * n, (e - k + 1) * n * sizeof(double),
+                                 hipMemcpyDeviceToDevice, st));
+        k = e + 1;
+    }
+    DDPCA_HIP(hipStreamSynchronize(st));
+    rocblas_destroy_handle(rh);
+    const auto inf = info.download();
+    if (s1 != rocblas_status_success || s2 != rocblas_status_success)
+        throw ApiError(DDPCA_EHIP, "rocsolver potrf/potri failed on globCoup_1");
+    if (inf[0] != 0 || inf[1] != 0)
+        throw ApiError(DDPCA_ENUMERIC, "globCoup_1 is not positive definite (potrf info " + std::to_string(inf[0]) + ")");
+    C.inverted = true;
+}
+
+// One coarse-space correction (MCONTACT.h:2578-2612) on the stream, after k_outp wrote u.
+void coarse_correct(ddpca_mcontact& H) {
+    CoarseDev& C = H.cs;
+    if (!C.inverted) throw ApiError(DDPCA_ESTATE, "coarse space not factorised (multi-rank runs: comm_init first)");
+    hipStream_t st = H.main;
+    const int64_t n = C.n;
+    if (H.mg) {
+        MgpisDevice& D = *H.mg;
+        const int L = (int)D.lev.size() - 1;
+        // consStif[L] x on every owned subdomain, then realProl^T down to level doleMcsc
+        D.spmv(L, D.xs.p, D.lev[L].r.p);
+        for (int l = L; l > C.dmin; --l) D.restrict_level(l, l == L ? D.lev[L].r.p : D.lev[l].b.p, D.lev[l - 1].b.p);
+    }
+    hipLaunchKernelGGL(k_csr_wave, dim3(ceil_div(n, 4)), dim3(256), 0, st, C.rptr.p, C.rcol.p, C.rval.p, n, H.W.p,
+                       C.g.p, C.f0.p);
+    if (H.mg) {
+        MgpisDevice& D = *H.mg;
+        const int L = (int)D.lev.size() - 1;
+        for (auto& G : C.kg) {
+            const double* yd = G.level == L ? D.lev[L].r.p : D.lev[G.level].b.p;
+            hipLaunchKernelGGL(k_cs_kpart, dim3(nb256(G.rows.n)), dim3(256), 0, st, G.rows.p, G.src.p, yd, C.g.p,
+                               (int64_t)G.rows.n);
+        }
+    }
+    if (H.nranks > 1) DDPCA_NCCL(ncclAllReduce(C.g.p, C.g.p, n, ncclDouble, ncclSum, H.comm, st));
+    if (!C.nown) return;
+    hipLaunchKernelGGL(k_gemv_wave, dim3(ceil_div(C.nown, 4)), dim3(256), 0, st, C.ainv.p, C.g.p, C.xc.p, C.nown, n);
+    hipLaunchKernelGGL(k_cs_scatter, dim3(nb256(C.nxn)), dim3(256), 0, st, C.xsrc.p, C.xc.p, C.xn.p, C.nxn);
+    hipLaunchKernelGGL(k_cs_prolong, dim3(nb256(C.qnn)), dim3(256), 0, st, C.qcol.p, C.qw.p, C.qnn, C.xn.p, C.flag.p,
+                       H.presc.p, H.u);
+}
+
 void pair_norm(ddpca_mcontact& H, const double* a, const double* o, int64_t n, int64_t slot) {
     const int nb = nb256(n);
     hipLaunchKernelGGL(k_pair_norms, dim3(nb), dim3(256), 0, H.main, a, o, n, H.partial.p);
@@ -874,6 +1181,8 @@ bool iterate_once(ddpca_mcontact& H, bool check) {
         hipLaunchKernelGGL(k_outp, dim3(nb256(D.lev.back().nn)), dim3(256), 0, st, D.xs.p, D.lev.back().mask.p,
                            H.onode.p, H.presc.p, H.u, D.lev.back().nn);
     }
+    // ---- interface-eliminated coarse-space correction (MCONTACT.h:2578-2612)
+    if (H.cs.on && H.tc <= H.mult_maxi) coarse_correct(H);
     DDPCA_HIP(hipEventRecord(H.ev[1], st));
     const double t_solve = ms_since(t0);
     // ---- interface balance: this rank's gamma halves, one launch for every owned side
@@ -975,6 +1284,8 @@ int mcontact_gpu_create(ddpca_problem_t p, int device, int rank, int nranks, con
         else mgpis_default_options(&H->opt);
         for (auto& e : H->ev) DDPCA_HIP(hipEventCreate(&e));
         build(*H, P);
+        build_coarse(*H, P);
+        if (nranks == 1) coarse_invert(*H);
         *out = H.release();
     });
 }
@@ -994,6 +1305,7 @@ int mcontact_gpu_comm_init(mcontact_t h, const void* uid) {
         ncclUniqueId id;
         std::memcpy(&id, uid, sizeof(id));
         DDPCA_NCCL(ncclCommInitRank(&h->comm, h->nranks, id, h->rank));
+        coarse_invert(*h);
     });
 }
 

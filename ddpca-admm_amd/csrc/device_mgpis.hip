@@ -1127,6 +1127,7 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
         }
     }
     fine_perm = perm[nlev - 1];
+    level_perm = perm;
     // exact coarse solve: dense inverse of each subdomain's masked level-0 operator
     {
         std::vector<double> packed;
@@ -1334,6 +1335,15 @@ SellArgs vc_level_args(const MgpisDevice& D, int level) {
     return a;
 }
 }  // namespace
+
+void MgpisDevice::restrict_level(int l, const double* rf, double* bc) {
+    if (l < 1 || l >= (int)lev.size()) throw ApiError(DDPCA_EINVAL, "restrict_level: level");
+    const LevelDev& F = lev[l];
+    const LevelDev& C = lev[l - 1];
+    hipLaunchKernelGGL((k_restrict<false, false, false>), dim3(ceil_div(C.nn, kBlock)), dim3(kBlock), 0, stream, rf,
+                       F.rslots.p, F.roff.p, F.rcol.p, F.rwt.p, C.mask.p, bc, nullptr, nullptr, nullptr, nullptr, C.nn,
+                       C.csub.p, nullptr);
+}
 
 void MgpisDevice::spmv(int level, const double* x, double* y, bool vc_op) {
     SellArgs a = vc_op ? vc_level_args(*this, level) : level_args(lev[level]);

@@ -120,6 +120,8 @@ public:
     // device node numbering: fine_perm[s][i] = device position (inside member s's segment of
     // the fine level) of the member's node i in the reference (level-ordered) numbering
     std::vector<std::vector<int32_t>> fine_perm;
+    // the same for every level: level_perm[l][s][reference local node] = device local node
+    std::vector<std::vector<std::vector<int32_t>>> level_perm;
     int64_t fine_dof(int s, int64_t dof) const {  // batch fine-level dof of member s's nodal dof
         return 3 * (lev.back().noff[s] + fine_perm[s][dof / 3]) + dof % 3;
     }
@@ -144,6 +146,8 @@ public:
     void spmv(int level, const double* x, double* y, bool vc_op = false);
     bool vc32() const { return opt.precond_fp32 != 0 && lev.size() > 1; }
     void vcycle(const double* r, double* z, bool dot);     // z = M^-1 r (fine level)
+    // b_{l-1} = realProl[l-1]^T r_l on every member (masked), batch nodal layouts of levels l, l-1
+    void restrict_level(int l, const double* rf, double* bc);
     // PCG over every subdomain of the batch; b in bs, result in xs (x0 = xs when warm).
     // begin() enqueues the setup, step() one graph replay (iters_per_graph iterations),
     // wait() paces replays on the host-mapped stop flags until every subdomain is done.

@@ -10,7 +10,9 @@
 // realProl[L-1]^T (the condensed chain, masked at every level).  The reference uses Q inside
 // globCoup_1 and accuProl, and Rc for every right-hand-side operator; both are kept.
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <numeric>
 #include <stdexcept>
 #include <string>
@@ -196,6 +198,15 @@ void MCONTACT::MULTISCALE_1(const std::vector<uint8_t>* owned) {
     if ((int64_t)doleMcsc.size() != nsub) doleMcsc.assign(nsub, 0);  // MCONTACT.h:185-187
     CoarseSpace& C = coarse;
     C = CoarseSpace();
+    const bool verbose = std::getenv("DDPCA_VERBOSE") != nullptr;
+    auto t_start = std::chrono::steady_clock::now();
+    auto lap = [&](const char* what) {
+        if (!verbose) return;
+        auto now = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[ddpca] MULTISCALE_1 %s: %.0f ms\n", what,
+                     std::chrono::duration<double, std::milli>(now - t_start).count());
+        t_start = now;
+    };
     C.built.assign(nsub, 0);
     // bodies whose restriction chain / nodal prolongation is needed here: owned ones and the
     // mates of their interface sides
@@ -227,6 +238,7 @@ void MCONTACT::MULTISCALE_1(const std::vector<uint8_t>* owned) {
         C.accuQ[tv] = accumulated_stencil(multGrid[tv], doleMcsc[tv]);
     }
     for (int64_t tv = 0; tv < nsub; ++tv) C.built[tv] = mine(tv);
+    lap("accumulated stencils");
     auto Rc = [&](int64_t tv, const Csr& A_free) { return restrict_chain(multGrid[tv], doleMcsc[tv], f2d[tv], A_free); };
     auto QI = [&](int64_t tv, const std::vector<uint8_t>& sel) {
         return nodal_prolong(multGrid[tv], C.accuQ[tv], doleMcsc[tv], &sel);
@@ -237,23 +249,49 @@ void MCONTACT::MULTISCALE_1(const std::vector<uint8_t>* owned) {
     std::vector<std::vector<Trip>> tranS(nsub);   // globTran_S[tv]
     std::vector<double> forc(C.n, 0.0);
     C.globTran_1.assign(nint, {});
-    for (int64_t ts = 0; ts < nint; ++ts) {
+    // one task per owned interface side, run in parallel; results merged in task order
+    struct SideOut {
+        std::vector<Trip> coup, tran;     // globCoup_1 rows e, globTran_D_1[e] interface part
+        std::vector<std::pair<int64_t, double>> forc;
+    };
+    std::vector<std::pair<int64_t, int>> tasks;
+    for (int64_t ts = 0; ts < nint; ++ts)
+        for (int s = 0; s < 2; ++s)
+            if (mine(searCont[ts].body[s])) tasks.push_back({ts, s});
+    std::vector<SideOut> outs(tasks.size());
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int64_t task = 0; task < (int64_t)tasks.size(); ++task) {
+        const int64_t ts = tasks[task].first;
+        const int s = tasks[task].second;
+        std::vector<Trip>& coup_t = outs[task].coup;
+        std::vector<Trip>& tran_t = outs[task].tran;
+        auto& forc_t = outs[task].forc;
+        {
         const Interface& itf = searCont[ts];
         const int Cc = itf.comp();
         const double pen[3] = {itf.penN, itf.penF, itf.penF};
-        for (int s = 0; s < 2; ++s) {
+        {
             const int64_t e = itf.body[s], m = itf.body[1 - s];
-            if (!mine(e)) continue;
             const MULTIGRID& ge = multGrid[e];
             const MULTIGRID& gm = multGrid[m];
             const int64_t Ne = ge.numNodes(), Nm = gm.numNodes();
-            std::vector<int64_t> cidx(Ne, -1);
+            // self operators are the interface mass / transfer of ESTABLISH up to -1/2:
+            //   sum_ip -1/2 w N_e^T T^T P T N_e = -1/2 systMass[s]           (MCONTACT.h:1734-1762)
+            //   sum_ip -1/2 w N_e^T T^T [T] M_e  = -1/2 systTran[s]           (MCONTACT.h:2188-2245)
+            Csr S = itf.systMass[s], Ts = itf.systTran[s];
+            for (auto& v : S.val) v *= -0.5;
+            for (auto& v : Ts.val) v *= -0.5;
+            // cross (self node a, mate node b) blocks: sum_ip w Me_a Mm_b {T^T P T, T^T T, n}
+            std::vector<int64_t> cidx(Ne, -1), midx(Nm, -1);
             for (size_t k = 0; k < itf.nodeCont[s].size(); ++k) cidx[itf.nodeCont[s][k]] = (int64_t)k;
-            std::vector<Trip> tS, tM, tMT, tTs, tTm;
+            for (size_t k = 0; k < itf.nodeCont[1 - s].size(); ++k) midx[itf.nodeCont[1 - s][k]] = (int64_t)k;
+            const int64_t nce = (int64_t)itf.nodeCont[s].size();
+            std::vector<std::vector<int64_t>> part(nce);     // mate contact nodes per self contact node
+            std::vector<std::vector<double>> blk(nce);       // 9 GP + 9 G + 3 n per partner
             std::vector<double> gap(3 * Ne, 0.0);
             std::vector<uint8_t> sel_e(Ne, 0), sel_m(Nm, 0);
             for (const auto& p : itf.ip) {
-                double G[3][3], GP[3][3];
+                double G[9], GP[9];
                 for (int i = 0; i < 3; ++i)
                     for (int j = 0; j < 3; ++j) {
                         double x = 0, y = 0;
@@ -261,66 +299,69 @@ void MCONTACT::MULTISCALE_1(const std::vector<uint8_t>* owned) {
                             x += p.basis[c][i] * p.basis[c][j];
                             y += p.basis[c][i] * pen[c] * p.basis[c][j];
                         }
-                        G[i][j] = x;
-                        GP[i][j] = y;
+                        G[3 * i + j] = x;
+                        GP[3 * i + j] = y;
                     }
                 const double* Me = p.shap[s];
                 const double* Mm = p.shap[1 - s];
                 for (int a = 0; a < 4; ++a) {
-                    const int64_t na = p.node[s][a], ma = p.node[1 - s][a];
+                    const int64_t na = p.node[s][a], ca = cidx[na];
                     sel_e[na] = 1;
-                    sel_m[ma] = 1;
+                    sel_m[p.node[1 - s][a]] = 1;
                     for (int b = 0; b < 4; ++b) {
-                        const int64_t nb = p.node[s][b], mb = p.node[1 - s][b];
-                        const double cee = -0.5 * p.w * Me[a] * Me[b];
-                        const double cem = -0.5 * p.w * Me[a] * Mm[b];
-                        const double cme = -0.5 * p.w * Mm[a] * Me[b];
-                        for (int i = 0; i < 3; ++i)
-                            for (int j = 0; j < 3; ++j) {
-                                tS.push_back({3 * na + i, 3 * nb + j, cee * GP[i][j]});
-                                tM.push_back({3 * na + i, 3 * mb + j, cem * GP[i][j]});
-                                tMT.push_back({3 * ma + i, 3 * nb + j, cme * GP[i][j]});
-                            }
-                        // globTran_1 (MCONTACT.h:2188-2245): self -1/2 w N_e^T T^T [T] N_e,
-                        // mate +1/2 w N_m^T T^T [T] N_e, columns = side s contact dofs
-                        const int64_t cb = cidx[nb];
-                        for (int i = 0; i < 3; ++i) {
-                            if (Cc == 1) {
-                                tTs.push_back({3 * na + i, cb, -0.5 * p.w * Me[a] * p.basis[0][i] * Me[b]});
-                                tTm.push_back({3 * ma + i, cb, 0.5 * p.w * Mm[a] * p.basis[0][i] * Me[b]});
-                            } else {
-                                for (int j = 0; j < 3; ++j) {
-                                    tTs.push_back({3 * na + i, 3 * cb + j, -0.5 * p.w * Me[a] * Me[b] * G[i][j]});
-                                    tTm.push_back({3 * ma + i, 3 * cb + j, 0.5 * p.w * Mm[a] * Me[b] * G[i][j]});
-                                }
-                            }
+                        const int64_t cb = midx[p.node[1 - s][b]];
+                        auto& pl = part[ca];
+                        size_t k = std::find(pl.begin(), pl.end(), cb) - pl.begin();
+                        if (k == pl.size()) {
+                            pl.push_back(cb);
+                            blk[ca].resize(21 * pl.size(), 0.0);
                         }
+                        double* q = &blk[ca][21 * k];
+                        const double ww = p.w * Me[a] * Mm[b];
+                        for (int t = 0; t < 9; ++t) {
+                            q[t] += ww * GP[t];
+                            q[9 + t] += ww * G[t];
+                        }
+                        for (int t = 0; t < 3; ++t) q[18 + t] += ww * p.basis[0][t];
                     }
                     // initial-gap force, normal only (MCONTACT.h:2061-2098), side 1 negated
                     const double gsc = (s == 1 ? -0.5 : 0.5) * p.w * itf.penN * p.gap * Me[a];
                     for (int i = 0; i < 3; ++i) gap[3 * na + i] += gsc * p.basis[0][i];
                 }
             }
-            const Csr S = from_triplets(3 * Ne, 3 * Ne, tS);
-            const Csr Mx = from_triplets(3 * Ne, 3 * Nm, tM);
-            const Csr MT = from_triplets(3 * Nm, 3 * Ne, tMT);
-            const Csr Ts = from_triplets(3 * Ne, itf.mside(s), tTs);
+            std::vector<Trip> tM, tTm;
+            for (int64_t ca = 0; ca < nce; ++ca) {
+                const int64_t na = itf.nodeCont[s][ca];
+                for (size_t k = 0; k < part[ca].size(); ++k) {
+                    const int64_t mb = itf.nodeCont[1 - s][part[ca][k]];
+                    const double* q = &blk[ca][21 * k];
+                    for (int i = 0; i < 3; ++i) {
+                        for (int j = 0; j < 3; ++j) tM.push_back({3 * na + i, 3 * mb + j, -0.5 * q[3 * i + j]});
+                        // globTran_1 mate: +1/2 w N_m^T T^T [T] N_e, row = mate dof, col = self contact dof
+                        if (Cc == 1) tTm.push_back({3 * mb + i, ca, 0.5 * q[18 + i]});
+                        else
+                            for (int j = 0; j < 3; ++j) tTm.push_back({3 * mb + i, 3 * ca + j, 0.5 * q[9 + 3 * j + i]});
+                    }
+                }
+            }
+            const Csr Mx = from_triplets(3 * Ne, 3 * Nm, tM);   // -1/2 w N_e^T T^T P T N_m
+            const Csr MT = transpose_csr(Mx);                     // -1/2 w N_m^T T^T P T N_e
             const Csr Tm = from_triplets(3 * Nm, itf.mside(s), tTm);
             // globCoup_1 += inteCoup[ts][s] (MCONTACT.h:1787-1841): Q-based Galerkin blocks
             {
                 const Csr Qe = QI(e, sel_e), Qm = QI(m, sel_m);
                 const Csr QeT = transpose_csr(Qe);
-                append(coup, spgemm(QeT, spgemm(S, Qe)), C.baseReco[e], C.baseReco[e]);
-                append(coup, spgemm(QeT, spgemm(Mx, Qm)), C.baseReco[e], C.baseReco[m]);
+                append(coup_t, spgemm(QeT, spgemm(S, Qe)), C.baseReco[e], C.baseReco[e]);
+                append(coup_t, spgemm(QeT, spgemm(Mx, Qm)), C.baseReco[e], C.baseReco[m]);
             }
             // globTran_D_1 interface part (MCONTACT.h:1993-2048): rows e and rows m, columns = u_e
-            append(tranS[e], Rc(e, rows_to_free(ge, drop_constrained_cols(ge, S))), C.baseReco[e], 0);
-            append(tranS[e], Rc(m, rows_to_free(gm, drop_constrained_cols(ge, MT))), C.baseReco[m], 0);
+            append(tran_t, Rc(e, rows_to_free(ge, drop_constrained_cols(ge, S))), C.baseReco[e], 0);
+            append(tran_t, Rc(m, rows_to_free(gm, drop_constrained_cols(ge, MT))), C.baseReco[m], 0);
             // globForc_1 gap part (MCONTACT.h:2099-2109)
             {
                 const Csr gc = Rc(e, rows_to_free(ge, dense_vector_csr(gap)));
                 for (int64_t r = 0; r < gc.nrow; ++r)
-                    for (int64_t k = gc.ptr[r]; k < gc.ptr[r + 1]; ++k) forc[C.baseReco[e] + r] += gc.val[k];
+                    for (int64_t k = gc.ptr[r]; k < gc.ptr[r + 1]; ++k) forc_t.push_back({C.baseReco[e] + r, gc.val[k]});
             }
             // globTran_1[ts][s] (MCONTACT.h:2248-2297)
             {
@@ -330,7 +371,16 @@ void MCONTACT::MULTISCALE_1(const std::vector<uint8_t>* owned) {
                 C.globTran_1[ts][s] = from_triplets(C.n, itf.mside(s), t);
             }
         }
+        }
     }
+    for (size_t task = 0; task < tasks.size(); ++task) {
+        const int64_t e = searCont[tasks[task].first].body[tasks[task].second];
+        coup.insert(coup.end(), outs[task].coup.begin(), outs[task].coup.end());
+        tranS[e].insert(tranS[e].end(), outs[task].tran.begin(), outs[task].tran.end());
+        for (const auto& rv : outs[task].forc) forc[rv.first] += rv.second;
+        outs[task] = SideOut();
+    }
+    lap("interface operators");
     // ---- subdomain blocks: consStif[d] (MCONTACT.h:1675-1693) and Rc consForc (2052-2059)
     for (int64_t tv = 0; tv < nsub; ++tv) {
         if (!mine(tv)) continue;
@@ -345,6 +395,7 @@ void MCONTACT::MULTISCALE_1(const std::vector<uint8_t>* owned) {
     C.globTran_S.assign(nsub, Csr());
     for (int64_t tv = 0; tv < nsub; ++tv)
         if (mine(tv)) C.globTran_S[tv] = from_triplets(C.n, 3 * multGrid[tv].numNodes(), tranS[tv]);
+    lap("subdomain blocks");
     C.ready = true;
 }
 

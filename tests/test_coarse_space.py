@@ -73,3 +73,39 @@ def test_set_coarse_rejects_multiscale(ddpca):
     P = ddpca.Problem(*CASE_PARAMS["twoblock_f0_m2"])
     with pytest.raises(ddpca.DdpcaError):
         P.set_coarse(1)
+
+
+def test_rank_local_build_matches_global(ddpca):
+    """Each rank of a multi-GPU run builds the coarse rows/columns it owns (ESTABLISH(owner,
+    rank)); together they equal the single-process MULTISCALE_1 -- the device sums the RHS
+    contributions and the dense rows with RCCL all-reduces."""
+    args = ("dehw", 2, 2, 2, 1, 2, 0.3)
+    full = ddpca.Problem(*args)
+    full.set_coarse(2, [1] * full.nsub)
+    full.ESTABLISH()
+    base = full.array("baseReco")
+    A = full.csr("globCoup_1").toarray()
+    f = full.array("globForc_1")
+    owner = [0, 1, 0, 1]  # worms on rank 0, wheels on rank 1: every interface crosses ranks
+    for rank in range(2):
+        P = ddpca.Problem(*args)
+        P.set_coarse(2, [1] * P.nsub)
+        P.ESTABLISH(owner, rank)
+        assert np.array_equal(P.array("baseReco"), base)
+        Ar = P.csr("globCoup_1").toarray()
+        fr = P.array("globForc_1")
+        for tv in range(P.nsub):
+            rows = slice(base[tv], base[tv + 1])
+            if owner[tv] == rank:
+                assert np.abs(Ar[rows] - A[rows]).max() <= 1e-12 * np.abs(A).max()
+                assert np.abs(fr[rows] - f[rows]).max() <= 1e-12 * max(np.abs(f).max(), 1e-300)
+                assert abs(P.csr("globTran_D_1", tv) - full.csr("globTran_D_1", tv)).max() <= \
+                    1e-12 * abs(full.csr("globTran_D_1", tv)).max()
+            else:
+                assert not Ar[rows].any() and not fr[rows].any()
+        for ts in range(P.nint):
+            body = P.array("iface_body", ts)
+            for s in range(2):
+                if owner[body[s]] == rank:
+                    B = full.csr("globTran_1", 2 * ts + s)
+                    assert abs(P.csr("globTran_1", 2 * ts + s) - B).max() <= 1e-12 * abs(B).max()

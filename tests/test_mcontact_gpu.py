@@ -25,6 +25,8 @@ def _run(ddpca, case, maxit=3000, **opts):
         fric, pn, pf = g[f"if{ts}_param"]
         P.set_ips(ts, g[f"if{ts}_ip_node"], g[f"if{ts}_ip_shap"], g[f"if{ts}_ip_basis"], g[f"if{ts}_ip_gap"],
                   g[f"if{ts}_ip_w"], float(fric), float(pn), float(pf))
+    if "doleMcsc" in g.files:  # muscSett = 2 cases
+        P.set_coarse(int(g["muscSett"][0]), g["doleMcsc"])
     P.ESTABLISH()
     mc = ddpca.MCONTACT(P, **opts)
     n = mc.CONTACT_ANALYSIS(maxit)
@@ -54,6 +56,31 @@ def test_admm_matches_reference(ddpca, gpu, case, warm, f32):
     for tv in range(P.nsub):
         u, ur = mc.get("resuDisp", tv), g[f"sd{tv}_resuDisp"]
         assert np.linalg.norm(u - ur) <= 1e-6 * np.linalg.norm(ur)
+
+
+@pytest.mark.parametrize("f32", [0, 1])
+@pytest.mark.parametrize("case", ["twoblock_f0_m2", "twoblock_f3_m2", "beam_dd_m2"])
+def test_admm_coarse_space_matches_reference(ddpca, gpu, case, f32):
+    """Interface-eliminated coarse space (muscSett = 2, doleMcsc = 1; MCONTACT.h:2578-2612) on
+    the device: converged runs of 2 / 24 / 36 ADMM iterations, same bar as without it."""
+    g, P, mc, n = _run(ddpca, case, precond_fp32=f32)
+    ref_iters = len(g["resuMoni"])
+    assert abs(n - ref_iters) <= 1, (n, ref_iters)
+    ok, worst = _rows_close(mc.monitor(), g["resuMoni"])
+    assert ok, worst
+    for tv in range(P.nsub):
+        u, ur = mc.get("resuDisp", tv), g[f"sd{tv}_resuDisp"]
+        assert np.linalg.norm(u - ur) <= 1e-6 * np.linalg.norm(ur)
+
+
+def test_coarse_space_contact_pressure(ddpca, gpu):
+    """Patch test with the coarse space: converged in 2 iterations to the uniform 1e7 Pa."""
+    g, P, mc, n = _run(ddpca, "twoblock_f0_m2")
+    gam = mc.get("inpoGamm", 0)
+    ref = g["if0_resuCont"]
+    active = ref > 1e-3 * ref.max()
+    assert np.all(np.abs(gam[active] - ref[active]) <= 1e-5 * np.abs(ref[active]))
+    assert abs(gam.mean() / 1.0e7 - 1.0) < 1e-4
 
 
 @pytest.mark.parametrize("case", ["twoblock_f0", "twoblock_f3"])
@@ -137,6 +164,31 @@ def test_admm_on_reference_operators_via_builder(ddpca, gpu, case):
     for tv in range(Q.nsub):
         u, ur = mc.get("resuDisp", tv), g[f"sd{tv}_resuDisp"]
         assert np.linalg.norm(u - ur) <= 1e-6 * np.linalg.norm(ur)
+
+
+def test_admm_coarse_space_matches_oracle_on_generated_problem(ddpca, oracle, gpu):
+    """Synthetic DEHW-shaped chain (3 levels, doleMcsc = 1) with the coarse space: fixed-k
+    trajectory against the CPU oracle on the same host-built operators (coarse ones included)."""
+    P = ddpca.Problem("dehw", 2, 2, 2, 1, 2, 0.3)
+    P.set_coarse(2, [1] * P.nsub)
+    P.ESTABLISH()
+    mc = ddpca.MCONTACT(P)
+    k = 30
+    assert mc.CONTACT_ANALYSIS(k, check=False) == k
+    subs, ifaces = _oracle_problem(P)
+    res = oracle.admm(subs, ifaces, maxit=k, check=False, coarse=_oracle_coarse(P))
+    ok, worst = _rows_close(mc.monitor(), res["rows"], k=k, rtol=1e-6)
+    assert ok, worst
+    for tv in range(P.nsub):
+        u, ur = mc.get("resuDisp", tv), res["u"][tv]
+        assert np.linalg.norm(u - ur) <= 1e-7 * np.linalg.norm(ur)
+
+
+def _oracle_coarse(P):
+    return dict(globCoup_1=P.csr("globCoup_1"), globForc_1=P.array("globForc_1"), baseReco=P.array("baseReco"),
+                globTran_1=[[P.csr("globTran_1", 2 * ts + s) for s in range(2)] for ts in range(P.nint)],
+                globTran_D_1=[P.csr("globTran_D_1", tv) for tv in range(P.nsub)],
+                accuProl=[P.csr("accuProl", tv) for tv in range(P.nsub)])
 
 
 def _oracle_problem(P):
