@@ -47,6 +47,8 @@ def parse():
     # defaults: the fastest configuration of the round-1 sweep (profiles/r01_sweep.txt)
     ap.add_argument("--smoother", type=int, default=1, help="0 point Jacobi, 1 block Jacobi, 2 Chebyshev")
     ap.add_argument("--nu", type=int, default=1)
+    ap.add_argument("--omega-scale", type=float, default=1.7,
+                    help="Jacobi damping = scale / lambda_max(M^-1 K) per level (profiles/r01_sweep_omega.txt)")
     ap.add_argument("--iters-per-graph", type=int, default=4)
     ap.add_argument("--warm-start", type=int, default=0,
                     help="1: each subdomain PCG starts from its previous solution (same 1e-14 stop rule)")
@@ -92,6 +94,7 @@ def main():
         P.set_coarse(a.musc, [a.dole] * nsub)
     P.ESTABLISH(owner, rank)
     mc = D.MCONTACT(P, device=local, rank=rank, nranks=world, owner=owner, smoother=a.smoother, nu=a.nu,
+                    omega=-a.omega_scale,
                     iters_per_graph=a.iters_per_graph, warm_start=a.warm_start, precond_fp32=a.precond_fp32,
                     table_mode=a.table_mode)
     if world > 1:

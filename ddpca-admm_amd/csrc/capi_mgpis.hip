@@ -44,7 +44,7 @@ extern "C" {
 void mgpis_default_options(mgpis_options_t* opt) {
     opt->smoother = 1;
     opt->nu = 1;
-    opt->omega = 0.0;
+    opt->omega = -1.7;  // 1.7 / lambda_max: damping sweep, profiles/r01_sweep_omega.txt
     opt->iters_per_graph = 4;
     opt->warm_start = 0;
     opt->precond_fp32 = 0;
@@ -192,7 +192,8 @@ int mgpis_gpu_info(mgpis_t h, int64_t* out7) {
         out7[1] = D.nfree[0];
         out7[2] = D.lev.back().nnzb;
         out7[3] = D.lev.back().nch;
-        out7[4] = (int64_t)((D.opt.omega > 0.0 ? D.opt.omega : lmax > 0.0 ? 4.0 / (3.0 * lmax) : 1.0) * 1e6);
+        const double scale = D.opt.omega < 0.0 ? -D.opt.omega : 4.0 / 3.0;
+        out7[4] = (int64_t)((D.opt.omega > 0.0 ? D.opt.omega : lmax > 0.0 ? scale / lmax : 1.0) * 1e6);
         out7[5] = (int64_t)(lmax * 1e6);
         out7[6] = D.device;
     });

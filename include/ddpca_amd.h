@@ -41,7 +41,9 @@ typedef struct ddpca_mgpis* mgpis_t;
 typedef struct {
     int smoother;      /* 0 = damped point Jacobi, 1 = 3x3 node-block Jacobi, 2 = Chebyshev(deg) on block Jacobi */
     int nu;            /* sweeps (Jacobi) or polynomial degree (Chebyshev) pre and post */
-    double omega;      /* Jacobi damping; <= 0: 4 / (3 * lambda_max(D^-1 K)) estimated at create */
+    double omega;      /* Jacobi damping; > 0: this value; 0: 4 / (3 lambda_max(M^-1 K)) estimated at
+                          create per level and subdomain; < 0: -omega / lambda_max(M^-1 K)
+                          (mgpis_default_options: -1.7, the measured optimum for block Jacobi) */
     int iters_per_graph; /* PCG iterations captured per hipGraph replay (>= 1) */
     int warm_start;    /* MCONTACT loop only: start each subdomain PCG from its previous solution
                           instead of x0 = 0 (MGPIS.h:168); same ||r|| <= rtol ||b|| stop rule */
