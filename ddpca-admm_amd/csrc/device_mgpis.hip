@@ -45,15 +45,6 @@ struct SellArgs {
     const double* tab;     // table mode: tstride doubles per table row, slot-major 3x3 blocks
     int64_t tstride;
     const int32_t* ctype;  // table mode: chunk -> its rows' common table row, -1 = mixed
-    // symmetric storage (SYM-SELL): slots/off/col/val hold each row's upper blocks (column >=
-    // row); the lower blocks K_ij = K_ji^T are read from row j's upper storage: lcol[] = j,
-    // lidx[] = element offset of K_ji's first value in val (slot-major, as col)
-    const int32_t* lslots;
-    const int64_t* loff;
-    const int32_t* lcol;
-    const int32_t* lidx;
-    const int32_t* cmap;   // wave slot -> chunk (XCD-aware order), -1 = idle; nullptr = identity
-    int64_t nwave;         // wave slots of the launch (nch without cmap)
 };
 
 __device__ __forceinline__ double wave_sum(double v) {
@@ -86,25 +77,57 @@ __device__ __forceinline__ void apply_m(const double* minv, int64_t row, double 
     }
 }
 
-// 3x3 block (9 entries, one 512-B (fp64) / 256-B (fp32) wave load each) times x_j, accumulated
-// in fp64; the matrix is streamed once per launch, so its loads are non-temporal and leave the
-// caches to the x gathers.
+// Value layout of one slot (64 lanes x one 3x3 block) of a streamed SELL-BSR3 operator.
+// fp64, paired (DDPCA_PAIRED_VALUES = 1, default): 16-B lane loads -- four 1-KiB wave runs of
+// (v[2p], v[2p+1]), then a 512-B run of v[8]: 5 load instructions per block instead of 9, the
+// fine PCG SpMV 5-8 % faster (profiles/r01_spmv_ab.json).  fp32 keeps nine 256-B runs, one per
+// entry: its paired form (two 16-B quads + v[8]) measured 7-10 % SLOWER in the smoothing and
+// residual kernels.  Element (ij, lane) of slot base sb:
+//   paired fp64: sb[(ij < 8 ? 128 * (ij / 2) + 2 * lane + ij % 2 : 512 + lane)]
+//   otherwise:   sb[ij * 64 + lane]
+#ifndef DDPCA_PAIRED_VALUES
+#define DDPCA_PAIRED_VALUES 1
+#endif
 template <typename T>
-__device__ __forceinline__ void block_fma(const T* v, const double* xj, double& s0, double& s1, double& s2) {
-    const double x0 = xj[0], x1 = xj[1], x2 = xj[2];
-    auto ld = [&](int i) { return (double)__builtin_nontemporal_load(v + i * kChunk); };
-    s0 += ld(0) * x0 + ld(1) * x1 + ld(2) * x2;
-    s1 += ld(3) * x0 + ld(4) * x1 + ld(5) * x2;
-    s2 += ld(6) * x0 + ld(7) * x1 + ld(8) * x2;
+constexpr bool paired_values() { return DDPCA_PAIRED_VALUES != 0 && sizeof(T) == 8; }
+typedef double dbl2_t __attribute__((ext_vector_type(2)));
+
+template <typename T>
+__host__ __device__ inline int64_t slot_elem(int ij, int64_t lane) {
+    if (!paired_values<T>()) return (int64_t)ij * kChunk + lane;
+    return ij == 8 ? 512 + lane : 128 * (ij / 2) + 2 * lane + ij % 2;
 }
 
-// plain 3x3 block times x_j
+// 3x3 block times x_j, accumulated in fp64; v = slot base + lane.  The matrix is streamed once
+// per launch (NT: non-temporal loads, leaving the caches to the x gathers).
+template <bool NT, typename T>
+__device__ __forceinline__ void block_fma_any(const T* v, const double* xj, double& s0, double& s1, double& s2) {
+    const double x0 = xj[0], x1 = xj[1], x2 = xj[2];
+    auto ldv = [](const auto* p) { if constexpr (NT) return __builtin_nontemporal_load(p); else return *p; };
+    if constexpr (paired_values<T>()) {
+        const int lane = threadIdx.x & 63;
+        const dbl2_t* p = reinterpret_cast<const dbl2_t*>(v - lane) + lane;
+        const dbl2_t a = ldv(p), b = ldv(p + 64), c = ldv(p + 128), d = ldv(p + 192);
+        const double v8 = ldv(v + 512);
+        s0 += a.x * x0 + a.y * x1 + b.x * x2;
+        s1 += b.y * x0 + c.x * x1 + c.y * x2;
+        s2 += d.x * x0 + d.y * x1 + v8 * x2;
+    } else {
+        auto ld = [&](int i) { return (double)ldv(v + i * kChunk); };
+        s0 += ld(0) * x0 + ld(1) * x1 + ld(2) * x2;
+        s1 += ld(3) * x0 + ld(4) * x1 + ld(5) * x2;
+        s2 += ld(6) * x0 + ld(7) * x1 + ld(8) * x2;
+    }
+}
+
+template <typename T>
+__device__ __forceinline__ void block_fma(const T* v, const double* xj, double& s0, double& s1, double& s2) {
+    block_fma_any<true>(v, xj, s0, s1, s2);
+}
+
 template <typename T>
 __device__ __forceinline__ void block_fma_plain(const T* v, const double* xj, double& s0, double& s1, double& s2) {
-    const double x0 = xj[0], x1 = xj[1], x2 = xj[2];
-    s0 += (double)v[0 * kChunk] * x0 + (double)v[1 * kChunk] * x1 + (double)v[2 * kChunk] * x2;
-    s1 += (double)v[3 * kChunk] * x0 + (double)v[4 * kChunk] * x1 + (double)v[5 * kChunk] * x2;
-    s2 += (double)v[6 * kChunk] * x0 + (double)v[7 * kChunk] * x1 + (double)v[8 * kChunk] * x2;
+    block_fma_any<false>(v, xj, s0, s1, s2);
 }
 
 // Row sums of one chunk, loop variant V (the production kernels use default_variant; the others
@@ -231,36 +254,14 @@ __device__ __forceinline__ void sell_rows_uniform(const int32_t* colp, const dou
 // streaming for the PCG and Chebyshev epilogues; an XCD-contiguous chunk mapping (each XCD one
 // range of chunks) was 17 % slower than the dispatcher's round-robin and is gone.
 constexpr int default_variant(int mode) { return (mode == 0 || mode == 1) ? 2 : 1; }
-// SYM-SELL upper loop: cached loads, so the lower blocks re-read the rows' upper blocks from L2
-constexpr int kSymVariant = 0;
 
 // One wavefront per 64-node chunk, one lane per node row, three accumulators per lane; T is the
 // storage type of streamed operator values (all arithmetic fp64); TBL: values from the table.
-// Lower blocks of a SYM-SELL row: K_ij = K_ji^T, K_ji read in place from row j's upper storage
-// (element (a,b) of K_ij is K_ji(b,a) at lidx + (3b+a)*64).  These loads are cached: row j's
-// upper blocks were streamed shortly before by a nearby wave (same XCD under the cmap order).
-template <typename T>
-__device__ __forceinline__ void sym_lower_rows(const int32_t* lc, const int32_t* li, const T* val, const double* x,
-                                               int ns, double& s0, double& s1, double& s2) {
-#pragma unroll 2
-    for (int m = 0; m < ns; ++m) {
-        const int64_t j = __builtin_nontemporal_load(lc + (int64_t)m * kChunk);
-        const T* v = val + __builtin_nontemporal_load(li + (int64_t)m * kChunk);
-        const double x0 = x[3 * j], x1 = x[3 * j + 1], x2 = x[3 * j + 2];
-        s0 += (double)v[0 * kChunk] * x0 + (double)v[3 * kChunk] * x1 + (double)v[6 * kChunk] * x2;
-        s1 += (double)v[1 * kChunk] * x0 + (double)v[4 * kChunk] * x1 + (double)v[7 * kChunk] * x2;
-        s2 += (double)v[2 * kChunk] * x0 + (double)v[5 * kChunk] * x1 + (double)v[8 * kChunk] * x2;
-    }
-}
-
-template <int MODE, bool BJ, bool DOT, typename T = double, int V = default_variant(MODE), bool TBL = false,
-          bool SYM = false>
+template <int MODE, bool BJ, bool DOT, typename T = double, int V = default_variant(MODE), bool TBL = false>
 __global__ __launch_bounds__(kBlock) void k_sell(SellArgs a, const double* __restrict__ tab) {
     const int lane = threadIdx.x & 63;
-    const int64_t w = (int64_t)blockIdx.x * (kBlock / kWave) + (threadIdx.x >> 6);
-    if (w >= a.nwave) return;
-    const int64_t c = a.cmap ? (int64_t)a.cmap[w] : w;
-    if (c < 0) return;
+    const int64_t c = (int64_t)blockIdx.x * (kBlock / kWave) + (threadIdx.x >> 6);
+    if (c >= a.nch) return;
     const int sub = a.csub[c];
     if (stopped(a.sc, sub)) return;
     const int64_t row = c * kChunk + lane;
@@ -279,11 +280,6 @@ __global__ __launch_bounds__(kBlock) void k_sell(SellArgs a, const double* __res
     } else
         sell_rows<V>(a.col + base * kChunk + lane, static_cast<const T*>(a.val) + base * 9 * kChunk + lane, a.x, ns,
                      row, s0, s1, s2);
-    if (SYM) {
-        const int64_t lb = a.loff[c];
-        sym_lower_rows<T>(a.lcol + lb * kChunk + lane, a.lidx + lb * kChunk + lane, static_cast<const T*>(a.val),
-                          a.x, a.lslots[c], s0, s1, s2);
-    }
     double dotv = 0.0;
     const int64_t o = 3 * row;
     if (MODE == kSpmv) {
@@ -940,143 +936,6 @@ int64_t pace_until_done(hipStream_t stream, hipGraphExec_t graph, const MirrorBu
 }
 
 // ============================================================================== setup
-namespace {
-long opt_sym_levels(const mgpis_options_t&) { return 0; }
-}  // namespace
-
-// Convert a level's full SELL arrays (every row's blocks in increasing column order) to SYM-SELL
-// in place: slots/off/col/val keep the upper blocks (column >= row); the lower blocks become
-// (column, element offset of the transposed block) references; plus the XCD-aware wave order.
-void build_sym(LevelDev& L, const std::vector<SubdomainOps>& subs, const std::vector<int32_t>& rowlen,
-               std::vector<int32_t>& slots, std::vector<int64_t>& off, std::vector<int32_t>& col,
-               std::vector<double>& val) {
-    const int64_t nch = L.nch, nn = L.nn;
-    std::vector<int32_t> cu(nn, 0), cl(nn, 0);
-#pragma omp parallel for schedule(static)
-    for (int64_t g = 0; g < nn; ++g) {
-        const int64_t c = g / kChunk, lane = g % kChunk;
-        for (int t = 0; t < rowlen[g]; ++t) (col[(off[c] + t) * kChunk + lane] >= g ? cu[g] : cl[g])++;
-    }
-    std::vector<int32_t> us(nch, 0), ls(nch, 0);
-    std::vector<int64_t> uo(nch + 1, 0), lo(nch + 1, 0);
-    for (int64_t c = 0; c < nch; ++c) {
-        for (int64_t lane = 0; lane < kChunk; ++lane) {
-            us[c] = std::max(us[c], cu[c * kChunk + lane]);
-            ls[c] = std::max(ls[c], cl[c * kChunk + lane]);
-        }
-        uo[c + 1] = uo[c] + us[c];
-        lo[c + 1] = lo[c] + ls[c];
-    }
-    const int64_t nsu = uo[nch], nsl = lo[nch];
-    if ((nsu + 1) * 9 * kChunk > (int64_t)INT32_MAX) {
-        std::fprintf(stderr, "[ddpca] level too large for 32-bit SYM-SELL offsets; kept full storage\n");
-        return;
-    }
-    std::vector<int32_t> ucol(std::max<int64_t>(nsu, 1) * kChunk, 0), lcol(std::max<int64_t>(nsl, 1) * kChunk, 0),
-        lidx(std::max<int64_t>(nsl, 1) * kChunk, 0);
-    std::vector<double> uval((nsu + 1) * 9 * kChunk, 0.0);  // + one zero slot for lower padding
-    const int32_t zero_idx = (int32_t)(nsu * 9 * kChunk);
-#pragma omp parallel for schedule(static)
-    for (int64_t g = 0; g < nn; ++g) {
-        const int64_t c = g / kChunk, lane = g % kChunk;
-        int64_t k = 0;
-        for (int t = 0; t < rowlen[g]; ++t) {
-            const int64_t q = off[c] + t;
-            const int32_t j = col[q * kChunk + lane];
-            if (j < g) continue;
-            const int64_t qu = uo[c] + k++;
-            ucol[qu * kChunk + lane] = j;
-            for (int ij = 0; ij < 9; ++ij) uval[(qu * 9 + ij) * kChunk + lane] = val[(q * 9 + ij) * kChunk + lane];
-        }
-        for (; k < us[c]; ++k) ucol[(uo[c] + k) * kChunk + lane] = (int32_t)g;
-    }
-    bool ok = true;
-    double asym = 0.0;
-#pragma omp parallel for schedule(static) reduction(&& : ok) reduction(max : asym)
-    for (int64_t g = 0; g < nn; ++g) {
-        const int64_t c = g / kChunk, lane = g % kChunk;
-        int64_t m = 0;
-        for (int t = 0; t < rowlen[g]; ++t) {
-            const int64_t q = off[c] + t;
-            const int32_t j = col[q * kChunk + lane];
-            if (j >= g) continue;
-            const int64_t cj = j / kChunk, lj = j % kChunk;
-            int64_t pos = -1;
-            for (int64_t k = 0; k < cu[j]; ++k)
-                if (ucol[(uo[cj] + k) * kChunk + lj] == g) { pos = (uo[cj] + k) * 9 * kChunk + lj; break; }
-            if (pos < 0) { ok = false; continue; }
-            for (int a = 0; a < 3; ++a)
-                for (int b = 0; b < 3; ++b) {
-                    const double v = val[(q * 9 + 3 * a + b) * kChunk + lane], vt = uval[pos + (3 * b + a) * kChunk];
-                    asym = std::max(asym, std::abs(v - vt) / std::max(std::abs(v), 1e-300));
-                }
-            const int64_t ql = lo[c] + m++;
-            lcol[ql * kChunk + lane] = j;
-            lidx[ql * kChunk + lane] = (int32_t)pos;
-        }
-        for (; m < ls[c]; ++m) {
-            lcol[(lo[c] + m) * kChunk + lane] = (int32_t)g;
-            lidx[(lo[c] + m) * kChunk + lane] = zero_idx;
-        }
-    }
-    if (!ok) throw ApiError(DDPCA_EINVAL, "SYM-SELL: operator is not structurally symmetric");
-    // XCD-aware wave order: chunks at the same position of consecutive node planes (the rows a
-    // lower block refers back to) go to the same XCD, in increasing order, so the transposed
-    // blocks and the x gathers are served by that XCD's L2.  Blocks are dealt round-robin over
-    // the 8 XCDs (speed only, never correctness).
-    std::vector<std::vector<int32_t>> lists(8);
-    for (size_t s = 0; s < L.noff.size(); ++s) {
-        const int64_t c0 = L.noff[s] / kChunk, nc = pad64(L.nloc[s]) / kChunk;
-        std::vector<int64_t> back;
-        for (int64_t g = L.noff[s]; g < L.noff[s] + L.nloc[s]; g += 7) {
-            const int64_t c = g / kChunk, lane = g % kChunk;
-            int64_t mn = g;
-            for (int t = 0; t < rowlen[g]; ++t) mn = std::min<int64_t>(mn, col[(off[c] + t) * kChunk + lane]);
-            if (mn < g) back.push_back(g - mn);
-        }
-        int64_t D = 1;
-        if (!back.empty()) {
-            std::nth_element(back.begin(), back.begin() + back.size() / 2, back.end());
-            D = std::max<int64_t>(1, (back[back.size() / 2] + kChunk / 2) / kChunk);
-        }
-        for (int64_t c = c0; c < c0 + nc; ++c) lists[(size_t)(((c - c0) % D) * 8 / D)].push_back((int32_t)c);
-        (void)subs;
-    }
-    size_t mx = 0;
-    for (const auto& v : lists) mx = std::max(mx, v.size());
-    const size_t per = (mx + 3) / 4;  // blocks per XCD
-    std::vector<int32_t> cmap(per * 8 * 4, -1);
-    for (int x = 0; x < 8; ++x)
-        for (size_t i = 0; i < lists[x].size(); ++i) {
-            const size_t t = i / 4, w = i % 4;
-            cmap[(t * 8 + x) * 4 + w] = lists[x][i];
-        }
-    const char* xm = std::getenv("DDPCA_XCDMAP");
-    if (!xm || std::atoi(xm) != 0) L.cmap.upload(cmap);
-    // per-subdomain block counts (byte accounting)
-    L.nnzb_u_sub.assign(L.noff.size(), 0);
-    L.nnzb_l_sub.assign(L.noff.size(), 0);
-    for (size_t s = 0; s < L.noff.size(); ++s)
-        for (int64_t g = L.noff[s]; g < L.noff[s] + L.nloc[s]; ++g) {
-            L.nnzb_u_sub[s] += cu[g];
-            L.nnzb_l_sub[s] += cl[g];
-        }
-    if (std::getenv("DDPCA_VERBOSE"))
-        std::fprintf(stderr, "[ddpca] SYM-SELL level: %lld upper + %lld lower slots (full %lld), max rel asymmetry %.3g, cmap %zu\n",
-                     (long long)nsu, (long long)nsl, (long long)off[nch], asym, L.cmap.n);
-    slots.swap(us);
-    off.swap(uo);
-    col.swap(ucol);
-    val.swap(uval);
-    L.nslots = nsu;
-    L.nslots_l = nsl;
-    L.sym = true;
-    L.lslots.upload(ls);
-    L.loff.upload(lo);
-    L.lcol.upload(lcol);
-    L.lidx.upload(lidx);
-}
-
 MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const mgpis_options_t& o)
     : device(dev), opt(o) {
     select_device(device);
@@ -1159,7 +1018,6 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
         std::vector<double> val(L.nslots * kChunk * 9, 0.0);
         std::vector<double> dinv(3 * L.nn, 0.0), minv(bj ? 9 * L.nn : 3 * L.nn, 0.0);
         std::vector<uint8_t> mask(L.nn, 0);
-        std::vector<int32_t> rowlen(L.nn, 0);
         for (int s = 0; s < nsub; ++s) {
             const Bsr3& A = *subs[s].K[l];
             const uint8_t* fr = subs[s].dof_free;  // reference order: level-l nodes are a prefix
@@ -1180,7 +1038,6 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
                 // lexicographic numbering), else in increasing device column
                 int64_t ord[kMaxRowBlocks];
                 const int64_t len = A.ptr[r + 1] - A.ptr[r];
-                rowlen[g] = (int32_t)len;
                 if (!keys[l][s].empty()) {
                     canonical_slots(A, r, keys[l][s], ord);
                 } else {
@@ -1213,15 +1070,6 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
                 }
             }
         }
-        // symmetric storage of this level (SYM-SELL): DDPCA_SYM_LEVELS = bit mask counted from the
-        // fine level (bit 0 = fine); not combined with table mode
-        {
-            const char* env = std::getenv("DDPCA_SYM_LEVELS");
-            const long bits = env ? std::strtol(env, nullptr, 0) : (long)opt_sym_levels(opt);
-            const int from_top = nlev - 1 - l;
-            if (l >= 1 && opt.table_mode == 0 && from_top < 31 && ((bits >> from_top) & 1))
-                build_sym(L, subs, rowlen, slots, off, col, val);
-        }
         L.slots.upload(slots);
         L.csub.upload(csub);
         L.off.upload(off);
@@ -1235,11 +1083,23 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
         // copy, every level; the fp32 copy serves the V-cycle on levels >= 1 (level 0 is the
         // dense inverse).  Table-mode levels need neither.
         const bool vc32 = opt.precond_fp32 != 0 && nlev > 1;
-        if (!L.tbl && (l == nlev - 1 || !vc32)) L.val.upload(val);
+        const int64_t nslot = L.nslots;
+        if (!L.tbl && (l == nlev - 1 || !vc32)) {
+            std::vector<double> v64(val.size());
+#pragma omp parallel for schedule(static)
+            for (int64_t q = 0; q < nslot; ++q)
+                for (int ij = 0; ij < 9; ++ij)
+                    for (int64_t lane = 0; lane < kChunk; ++lane)
+                        v64[q * 9 * kChunk + slot_elem<double>(ij, lane)] = val[(q * 9 + ij) * kChunk + lane];
+            L.val.upload(v64);
+        }
         if (!L.tbl && vc32 && l >= 1) {
             std::vector<float> v32(val.size());
 #pragma omp parallel for schedule(static)
-            for (int64_t i = 0; i < (int64_t)val.size(); ++i) v32[i] = (float)val[i];
+            for (int64_t q = 0; q < nslot; ++q)
+                for (int ij = 0; ij < 9; ++ij)
+                    for (int64_t lane = 0; lane < kChunk; ++lane)
+                        v32[q * 9 * kChunk + slot_elem<float>(ij, lane)] = (float)val[(q * 9 + ij) * kChunk + lane];
             L.val32.upload(v32);
         }
         L.dinv.upload(dinv);
@@ -1471,18 +1331,8 @@ SellArgs level_args(const LevelDev& L) {
     a.val = L.val.p;
     a.csub = L.csub.p;
     a.nch = L.nch;
-    a.nwave = L.nch;
     a.minv = L.minv.p;
-    if (L.sym) {
-        a.lslots = L.lslots.p;
-        a.loff = L.loff.p;
-        a.lcol = L.lcol.p;
-        a.lidx = L.lidx.p;
-    }
-    if (L.cmap.p) {
-        a.cmap = L.cmap.p;
-        a.nwave = (int64_t)L.cmap.n;
-    }
+
     if (L.tbl) {
         a.val = nullptr;
         a.rtype = L.rtype.p;
@@ -1497,27 +1347,15 @@ SellArgs level_args(const LevelDev& L) {
 // streamed as fp32 (f32) or fp64
 template <int MODE, bool BJ, bool DOT>
 void launch_sell(bool f32, const SellArgs& a, hipStream_t s) {
-    const int grid = ceil_div(a.nwave, 4);
+    const int grid = ceil_div(a.nch, 4);
     constexpr int V = default_variant(MODE);
     if (a.tab) hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, double, V, true>), dim3(grid), dim3(kBlock), 0, s, a, a.tab);
-    else if (a.lidx && f32) hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, float, kSymVariant, false, true>), dim3(grid), dim3(kBlock), 0, s, a, a.tab);
-    else if (a.lidx) hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, double, kSymVariant, false, true>), dim3(grid), dim3(kBlock), 0, s, a, a.tab);
     else if (f32) hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, float>), dim3(grid), dim3(kBlock), 0, s, a, a.tab);
     else hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, double>), dim3(grid), dim3(kBlock), 0, s, a, a.tab);
 }
 
 template <int MODE, bool BJ, bool DOT>
 void launch_loop(int loop, bool f32, const SellArgs& a, int grid, hipStream_t s) {
-    if (a.lidx) {  // SYM-SELL: upper loop variant 0 (cached) or 1 (non-temporal)
-        if (f32) {
-            if (loop == 0) hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, float, 0, false, true>), dim3(grid), dim3(kBlock), 0, s, a, a.tab);
-            else hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, float, 1, false, true>), dim3(grid), dim3(kBlock), 0, s, a, a.tab);
-        } else {
-            if (loop == 0) hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, double, 0, false, true>), dim3(grid), dim3(kBlock), 0, s, a, a.tab);
-            else hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, double, 1, false, true>), dim3(grid), dim3(kBlock), 0, s, a, a.tab);
-        }
-        return;
-    }
     if (f32) {
         switch (loop) {
             case 0: hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, float, 0>), dim3(grid), dim3(kBlock), 0, s, a, a.tab); break;
@@ -1589,7 +1427,7 @@ double MgpisDevice::bench_spmv(int variant, int reps) {
     a.partial = partial.p;
     a.sc = sc.p;
     if (lev.size() > 1) a.coef = L.coef.p;
-    const int grid = ceil_div(a.nwave, 4);
+    const int grid = ceil_div(a.nch, 4);
     DevBuf<double> x4;
     if (tloop >= 4) {  // x in a 4-double-per-node copy
         x4.alloc(4 * L.nn);
@@ -1728,8 +1566,6 @@ double MgpisDevice::fine_matrix_bytes(int s, bool f32) const {
     // (fp64) or 36 B (fp32) per stored block; table mode = 4 B index per block + 4 B row type
     // per node + the member's share of the table (read once per launch)
     const LevelDev& L = lev.back();
-    if (L.sym)  // upper blocks streamed once; a lower block is a 4-B column + a 4-B offset
-        return (f32 ? 40.0 : 76.0) * (double)L.nnzb_u_sub[s] + 8.0 * (double)L.nnzb_l_sub[s];
     if (!L.tbl) return (f32 ? 40.0 : 76.0) * (double)L.nnzb_sub[s];
     double nodes = 0.0;
     for (int64_t n : L.nloc) nodes += (double)n;

@@ -84,15 +84,7 @@ struct LevelDev {
     DevBuf<int32_t> rtype;   // per node row
     DevBuf<int32_t> ctype;   // per chunk: the common type, -1 = mixed
     DevBuf<double> tab;
-    // symmetric storage (SYM-SELL): slots/off/col/val keep only each row's upper blocks
-    // (column >= row); the lower ones are references into them (lcol: column, lidx: element
-    // offset of the transposed block in val), one 4-B column + one 4-B offset per block
-    bool sym = false;
-    int64_t nslots_l = 0;
-    std::vector<int64_t> nnzb_u_sub, nnzb_l_sub;
-    DevBuf<int32_t> lslots, lcol, lidx;
-    DevBuf<int64_t> loff;
-    DevBuf<int32_t> cmap;    // XCD-aware wave -> chunk order (-1 = idle), empty = identity
+
     DevBuf<double> minv;   // point: 3 per node; block: 9 per node
     DevBuf<double> dinv;   // point Jacobi inverse (diagonal preconditioner at the fine level)
     DevBuf<uint8_t> mask;  // bit a set = dof 3i+a free

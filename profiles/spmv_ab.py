@@ -1,20 +1,18 @@
-"""SpMV storage experiment on one fine level (a 1.22M-dof wheel block of the bench workload):
-full SELL-BSR3 vs SYM-SELL (upper blocks streamed, lower blocks re-read in place), with and
-without the XCD-aware wave order.  Each configuration runs in its own process (the storage is
-chosen at create from DDPCA_SYM_LEVELS / DDPCA_XCDMAP); y = Kx on a fixed vector is checked
-against the full-storage result.
+"""A/B of fine-level SpMV kernels on one 1.22M-dof wheel block of the bench workload
+(mgpis_gpu_bench_spmv): each configuration runs in its own process with its own environment,
+e.g. a second library built with other -D switches (DDPCA_AMD_LIB) -- y = Kx on a fixed vector
+is printed for the cross-check.  r01_spmv_sym.json was made by this script when it compared the
+full SELL-BSR3 storage with a symmetric (upper-block) storage, since removed (commit 99c5bfc).
 
-    python profiles/spmv_sym.py OUT
+    python profiles/spmv_ab.py OUT tag1:NAME=VAL,NAME=VAL tag2:...
 """
 import json
 import os
 import subprocess
 import sys
 
-CONFIGS = [("full", {"DDPCA_SYM_LEVELS": "0"}), ("sym", {"DDPCA_SYM_LEVELS": "1", "DDPCA_XCDMAP": "0"}),
-           ("sym+xcd", {"DDPCA_SYM_LEVELS": "1", "DDPCA_XCDMAP": "1"})]
-VARIANTS = [("f64 spmv L0", 0), ("f64 spmv L1", 1), ("f64 pcg L0", 4), ("f64 pcg L1", 5),
-            ("f32 resid L0", 16 + 8), ("f32 resid L1", 16 + 9), ("f32 cheb L1", 16 + 13)]
+VARIANTS = [("f64 spmv L1", 1), ("f64 spmv L2", 2), ("f64 spmv L3", 3), ("f64 pcg L1", 5), ("f64 pcg L2", 6),
+            ("f32 resid L1", 16 + 9), ("f32 resid L2", 16 + 10), ("f32 resid L3", 16 + 11), ("f32 cheb L1", 16 + 13)]
 
 
 def child():
@@ -28,12 +26,10 @@ def child():
     x = np.sin(np.arange(n) * 0.37)
     y = M.spmv(x)
     out = {"y": [float(np.linalg.norm(y)), float(y[::997].sum())], "ms": {}}
-    np.save("/tmp/spmv_y.npy", y)
     for name, v in VARIANTS:
-        if "L0" in name and os.environ.get("DDPCA_SYM_LEVELS", "0") != "0" and "f32" in name:
-            continue
         ms, nb = M.bench_spmv(v, 50)
-        out["ms"][name] = ms
+        out["ms"][name] = round(ms * 1e3, 2)  # us
+        out.setdefault("GBs", {})[name] = round(nb / ms / 1e6)
     print(json.dumps(out), flush=True)
 
 
@@ -42,7 +38,9 @@ def main():
         return child()
     out = sys.argv[1]
     res = {}
-    for tag, env in CONFIGS:
+    for spec in sys.argv[2:]:
+        tag, _, kv = spec.partition(":")
+        env = dict(p.split("=", 1) for p in kv.split(",") if p)
         e = dict(os.environ, **env)
         r = subprocess.run([sys.executable, __file__, "--child"], env=e, capture_output=True, text=True, timeout=300)
         line = [l for l in r.stdout.splitlines() if l.startswith("{")]
