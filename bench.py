@@ -60,6 +60,8 @@ def parse():
     ap.add_argument("--musc", type=int, default=2,
                     help="muscSett: 2 = interface-eliminated coarse space every ADMM iteration (DEHW.h:2222), 0 = none")
     ap.add_argument("--dole", type=int, default=1, help="doleMcsc: coarse-space level of every subdomain (DEHW.h:2239)")
+    ap.add_argument("--coarse-level", type=int, default=-1,
+                    help="V-cycle level of the exact dense coarse solve (-1: auto, 0: the reference's)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=os.environ.get("DDPCA_TRAFFIC_JSON", str(ROOT / "profiles" / "traffic.json")),
                     help="PMC-derived HBM bytes per launch of the roofline kernel (profiles/make_traffic.py)")
@@ -94,7 +96,7 @@ def main():
         P.set_coarse(a.musc, [a.dole] * nsub)
     P.ESTABLISH(owner, rank)
     mc = D.MCONTACT(P, device=local, rank=rank, nranks=world, owner=owner, smoother=a.smoother, nu=a.nu,
-                    omega=-a.omega_scale,
+                    omega=-a.omega_scale, coarse_level=a.coarse_level,
                     iters_per_graph=a.iters_per_graph, warm_start=a.warm_start, precond_fp32=a.precond_fp32,
                     table_mode=a.table_mode)
     if world > 1:

@@ -44,7 +44,8 @@ def lib() -> C.CDLL:
 
 class MgpisOptions(C.Structure):
     _fields_ = [("smoother", C.c_int), ("nu", C.c_int), ("omega", C.c_double), ("iters_per_graph", C.c_int),
-                ("warm_start", C.c_int), ("precond_fp32", C.c_int), ("table_mode", C.c_int)]
+                ("warm_start", C.c_int), ("precond_fp32", C.c_int), ("table_mode", C.c_int),
+                ("coarse_level", C.c_int)]
 
 
 _P = C.c_void_p

@@ -45,6 +45,7 @@ void mgpis_default_options(mgpis_options_t* opt) {
     opt->smoother = 1;
     opt->nu = 1;
     opt->omega = -1.7;  // 1.7 / lambda_max: damping sweep, profiles/r01_sweep_omega.txt
+    opt->coarse_level = -1;
     opt->iters_per_graph = 4;
     opt->warm_start = 0;
     opt->precond_fp32 = 0;

@@ -15,6 +15,9 @@
 #include <thread>
 #include <unordered_map>
 
+#include <rocblas/rocblas.h>
+#include <rocsolver/rocsolver.h>
+
 #include "device_mgpis.hpp"
 
 namespace ddpca {
@@ -613,43 +616,32 @@ __global__ void k_scale_sub(const double* w, const double* scale, double* v, int
 }
 
 // ---- host helpers
-void invert_spd_dense(std::vector<double>& A, int64_t n) {
-    // Cholesky A = L L^T (lower, in place), then A^-1 = L^-T L^-1.
-    for (int64_t j = 0; j < n; ++j) {
-        double d = A[j * n + j];
-        for (int64_t k = 0; k < j; ++k) d -= A[j * n + k] * A[j * n + k];
-        if (!(d > 0.0)) throw ApiError(DDPCA_ENUMERIC, "coarse operator is not positive definite");
-        const double ljj = std::sqrt(d);
-        A[j * n + j] = ljj;
-#pragma omp parallel for schedule(static) if (n - j > 256)
-        for (int64_t i = j + 1; i < n; ++i) {
-            double s = A[i * n + j];
-            const double* ai = &A[i * n];
-            const double* aj = &A[j * n];
-            for (int64_t k = 0; k < j; ++k) s -= ai[k] * aj[k];
-            A[i * n + j] = s / ljj;
-        }
-    }
-    // Linv (lower) by columns
-    std::vector<double> Li(n * n, 0.0);
-#pragma omp parallel for schedule(dynamic, 16)
-    for (int64_t c = 0; c < n; ++c) {
-        Li[c * n + c] = 1.0 / A[c * n + c];
-        for (int64_t i = c + 1; i < n; ++i) {
-            double s = 0.0;
-            for (int64_t k = c; k < i; ++k) s -= A[i * n + k] * Li[k * n + c];
-            Li[i * n + c] = s / A[i * n + i];
-        }
-    }
-    // A^-1 = Li^T Li
-#pragma omp parallel for schedule(dynamic, 16)
-    for (int64_t i = 0; i < n; ++i)
-        for (int64_t j = 0; j <= i; ++j) {
-            double s = 0.0;
-            for (int64_t k = i; k < n; ++k) s += Li[k * n + i] * Li[k * n + j];
-            A[i * n + j] = s;
-            A[j * n + i] = s;
-        }
+__global__ void k_mirror_upper(double* A, int64_t n) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= n * n) return;
+    const int64_t i = idx / n, j = idx % n;
+    if (j < i) A[i * n + j] = A[j * n + i];
+}
+
+// In-place inverse of a dense SPD matrix (row-major = column-major, it is symmetric) with
+// rocSOLVER potrf + potri on the device (setup only).
+void invert_spd_device(std::vector<double>& A, int64_t n, hipStream_t st) {
+    DevBuf<double> d;
+    d.upload(A);
+    DevBuf<rocblas_int> info(2);
+    info.zero(st);
+    rocblas_handle h = nullptr;
+    if (rocblas_create_handle(&h) != rocblas_status_success) throw ApiError(DDPCA_EHIP, "rocblas_create_handle");
+    rocblas_set_stream(h, st);
+    const rocblas_status s1 = rocsolver_dpotrf(h, rocblas_fill_lower, (rocblas_int)n, d.p, (rocblas_int)n, info.p);
+    const rocblas_status s2 = rocsolver_dpotri(h, rocblas_fill_lower, (rocblas_int)n, d.p, (rocblas_int)n, info.p + 1);
+    hipLaunchKernelGGL(k_mirror_upper, dim3(std::max<int64_t>(1, (n * n + 255) / 256)), dim3(256), 0, st, d.p, n);
+    DDPCA_HIP(hipStreamSynchronize(st));
+    rocblas_destroy_handle(h);
+    const auto inf = info.download();
+    if (s1 != rocblas_status_success || s2 != rocblas_status_success) throw ApiError(DDPCA_EHIP, "rocsolver potrf/potri failed");
+    if (inf[0] != 0 || inf[1] != 0) throw ApiError(DDPCA_ENUMERIC, "coarse operator is not positive definite");
+    DDPCA_HIP(hipMemcpy(A.data(), d.p, A.size() * sizeof(double), hipMemcpyDeviceToHost));
 }
 
 bool invert3(const double m[9], double r[9]) {
@@ -1172,31 +1164,52 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
     }
     fine_perm = perm[nlev - 1];
     level_perm = perm;
-    // exact coarse solve: dense inverse of each subdomain's masked level-0 operator
+    // exact coarse solve: dense inverse of each subdomain's masked operator on level clev, in
+    // that level's device order.  clev: the option, or the highest level below the fine one
+    // whose inverses of all members fit in 256 MB (a few-subdomain batch trades the coarse
+    // levels' latency-bound launches for one GEMV over a larger dense inverse)
     {
+        clev = 0;
+        if (opt.coarse_level >= 0) clev = std::min(opt.coarse_level, nlev - 1);
+        else
+            for (int l = nlev - 2; l >= 1; --l) {
+                double bytes = 0.0;
+                int64_t nmax = 0;
+                for (int s = 0; s < nsub; ++s) {
+                    const double n = 3.0 * (double)subs[s].nnodes[l];
+                    bytes += 8.0 * n * n;
+                    nmax = std::max<int64_t>(nmax, 3 * subs[s].nnodes[l]);
+                }
+                if (bytes <= 256.0 * 1024 * 1024 && nmax <= 12288) { clev = l; break; }
+            }
+        if (nlev > 1 && clev == nlev - 1) clev = nlev - 2;
         std::vector<double> packed;
         std::vector<int64_t> ao(nsub), no(nsub), nz(nsub);
         for (int s = 0; s < nsub; ++s) {
-            const Bsr3& A = *subs[s].K[0];
+            const Bsr3& A = *subs[s].K[clev];
             const uint8_t* fr = subs[s].dof_free;
-            const int64_t n0 = 3 * subs[s].nnodes[0];
+            const auto& p = perm[clev][s];
+            const int64_t nc = subs[s].nnodes[clev], n0 = 3 * nc;
             std::vector<double> D(n0 * n0, 0.0);
-            for (int64_t r = 0; r < subs[s].nnodes[0]; ++r)
+            for (int64_t r = 0; r < nc; ++r)
                 for (int64_t k = A.ptr[r]; k < A.ptr[r + 1]; ++k) {
                     const int64_t j = A.col[k];
                     for (int a = 0; a < 3; ++a)
                         for (int b = 0; b < 3; ++b) {
                             double v = A.val[9 * k + 3 * a + b];
                             if (!fr[3 * r + a] || !fr[3 * j + b]) v = (j == r && a == b) ? 1.0 : 0.0;
-                            D[(3 * r + a) * n0 + 3 * j + b] = v;
+                            D[(3 * p[r] + a) * n0 + 3 * p[j] + b] = v;
                         }
                 }
-            invert_spd_dense(D, n0);
-            for (int64_t d = 0; d < n0; ++d)
-                if (!fr[d])
+            invert_spd_device(D, n0, stream);
+            for (int64_t r = 0; r < nc; ++r)
+                for (int a = 0; a < 3; ++a) {
+                    if (fr[3 * r + a]) continue;
+                    const int64_t d = 3 * p[r] + a;
                     for (int64_t e = 0; e < n0; ++e) D[d * n0 + e] = D[e * n0 + d] = 0.0;
+                }
             ao[s] = (int64_t)packed.size();
-            no[s] = lev[0].noff[s];
+            no[s] = lev[clev].noff[s];
             nz[s] = n0;
             packed.insert(packed.end(), D.begin(), D.end());
         }
@@ -1204,6 +1217,8 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
         aoff.upload(ao);
         c_noff.upload(no);
         c_n.upload(nz);
+        if (std::getenv("DDPCA_VERBOSE"))
+            std::fprintf(stderr, "[ddpca] exact coarse solve on level %d (%zu doubles of dense inverses)\n", clev, packed.size());
     }
     // condensed <-> nodal map of the fine level
     const LevelDev& F = lev.back();
@@ -1476,12 +1491,13 @@ void MgpisDevice::vcycle(const double* rin, double* zout, bool dot) {
     const bool cheb = opt.smoother == 2;
     const int nu = opt.nu;
     const PcgScal* scp = sc.p;
-    if (Lf == 0) {
-        hipLaunchKernelGGL(k_coarse, dim3(ceil_div(3 * lev[0].nn, 4)), dim3(kBlock), 0, stream, ainv.p, aoff.p, c_noff.p,
-                           c_n.p, rin, zout, 3 * lev[0].nn, lev[0].csub.p, scp);
+    const int cl = clev;  // the exact dense solve; levels below it are not visited
+    if (Lf == cl) {
+        hipLaunchKernelGGL(k_coarse, dim3(ceil_div(3 * lev[cl].nn, 4)), dim3(kBlock), 0, stream, ainv.p, aoff.p, c_noff.p,
+                           c_n.p, rin, zout, 3 * lev[cl].nn, lev[cl].csub.p, scp);
         if (dot)
-            hipLaunchKernelGGL(k_dot, dim3(ceil_div(lev[0].nn, kBlock)), dim3(kBlock), 0, stream, rin, zout, partial.p,
-                               lev[0].nn, lev[0].csub.p, scp);
+            hipLaunchKernelGGL(k_dot, dim3(ceil_div(lev[cl].nn, kBlock)), dim3(kBlock), 0, stream, rin, zout, partial.p,
+                               lev[cl].nn, lev[cl].csub.p, scp);
         return;
     }
     std::vector<double*> cur(nlev), oth(nlev);
@@ -1524,7 +1540,7 @@ void MgpisDevice::vcycle(const double* rin, double* zout, bool dot) {
         else if (bj) hipLaunchKernelGGL((k_jac0<true, false>), dim3(grid), dim3(kBlock), 0, stream, rin, F.minv.p, coef(Lf, 0), cur[Lf], nullptr, F.nn, F.csub.p, scp);
         else hipLaunchKernelGGL((k_jac0<false, false>), dim3(grid), dim3(kBlock), 0, stream, rin, F.minv.p, coef(Lf, 0), cur[Lf], nullptr, F.nn, F.csub.p, scp);
     }
-    for (int l = Lf; l >= 1; --l) {
+    for (int l = Lf; l >= cl + 1; --l) {
         smooth(l, 1, nu - 1, false);
         {
             SellArgs a = vc_level_args(*this, l);
@@ -1539,7 +1555,7 @@ void MgpisDevice::vcycle(const double* rin, double* zout, bool dot) {
         const LevelDev& C = lev[c];
         const int grid = ceil_div(C.nn, kBlock);
         const double* cf = c > 0 ? coef(c, 0) : nullptr;
-        if (c == 0)
+        if (c == cl)
             hipLaunchKernelGGL((k_restrict<false, false, false>), dim3(grid), dim3(kBlock), 0, stream, F.r.p, F.rslots.p, F.roff.p, F.rcol.p, F.rwt.p, C.mask.p, C.b.p, nullptr, nullptr, nullptr, nullptr, C.nn, C.csub.p, scp);
         else if (cheb)
             hipLaunchKernelGGL((k_restrict<true, true, true>), dim3(grid), dim3(kBlock), 0, stream, F.r.p, F.rslots.p, F.roff.p, F.rcol.p, F.rwt.p, C.mask.p, C.b.p, cur[c], C.d.p, C.minv.p, cf, C.nn, C.csub.p, scp);
@@ -1548,10 +1564,10 @@ void MgpisDevice::vcycle(const double* rin, double* zout, bool dot) {
         else
             hipLaunchKernelGGL((k_restrict<true, false, false>), dim3(grid), dim3(kBlock), 0, stream, F.r.p, F.rslots.p, F.roff.p, F.rcol.p, F.rwt.p, C.mask.p, C.b.p, cur[c], nullptr, C.minv.p, cf, C.nn, C.csub.p, scp);
     }
-    hipLaunchKernelGGL(k_coarse, dim3(ceil_div(3 * lev[0].nn, 4)), dim3(kBlock), 0, stream, ainv.p, aoff.p, c_noff.p, c_n.p,
-                       lev[0].b.p, cur[0], 3 * lev[0].nn, lev[0].csub.p, scp);
+    hipLaunchKernelGGL(k_coarse, dim3(ceil_div(3 * lev[cl].nn, 4)), dim3(kBlock), 0, stream, ainv.p, aoff.p, c_noff.p,
+                       c_n.p, lev[cl].b.p, cur[cl], 3 * lev[cl].nn, lev[cl].csub.p, scp);
     // ---- ascend
-    for (int l = 1; l <= Lf; ++l) {
+    for (int l = cl + 1; l <= Lf; ++l) {
         const LevelDev& F = lev[l];
         hipLaunchKernelGGL(k_prolong, dim3(ceil_div(F.nn, kBlock)), dim3(kBlock), 0, stream, cur[l - 1], F.ppar.p, F.pw.p,
                            F.mask.p, cur[l], F.nn, F.csub.p, scp);

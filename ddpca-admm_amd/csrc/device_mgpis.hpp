@@ -113,7 +113,8 @@ public:
     hipStream_t stream = nullptr;
     mgpis_options_t opt{};
     std::vector<LevelDev> lev;
-    // exact coarse solve: per-subdomain dense inverses, packed
+    // exact coarse solve on level clev: per-subdomain dense inverses, packed
+    int clev = 0;
     DevBuf<double> ainv;
     DevBuf<int64_t> aoff;      // per subdomain offset into ainv
     DevBuf<int64_t> c_noff;    // per subdomain first node of level 0

@@ -55,6 +55,10 @@ typedef struct {
                           block values deduplicate well (structured meshes), keep one copy per
                           distinct row in a cache-resident table and stream only column indices
                           and a row type -- the operator is bit-identical; 2 force (tests) */
+    int coarse_level;  /* level of the exact (dense-inverse) coarse solve of the V-cycle; the reference
+                          factorises level 0 (MGPIS.h:58-62).  -1 (default): the highest level whose
+                          dense inverses of all batch members fit in 256 MB -- fewer, latency-bound
+                          coarse-level launches when a process owns few subdomains */
 } mgpis_options_t;
 
 /* Fill default options. */
