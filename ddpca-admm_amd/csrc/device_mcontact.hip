@@ -31,6 +31,7 @@
 #include <chrono>
 #include <climits>
 #include <cmath>
+#include <cstdio>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -414,6 +415,18 @@ __global__ void k_fill_lower(double* A, int64_t n) {
     if (j < i) A[i * n + j] = A[j * n + i];
 }
 
+// Fused interface update (penalty mass operators proportional to the plain ones, rho = penN =
+// penF): with w = M^-1 T^T u and v = M^-1 I gamma from one batched solve,
+//   aux = (rho M)^-1 (rho T^T u + M lambda + I gamma) = w + (lambda + v) / rho   (MCONTACT.h:2671-2684)
+//   lambda += M^-1 (rho T^T u - rho M aux)             = -v                      (2689-2704)
+__global__ void k_fuse_aux_lambda(double* state, const double* wv, const double* rinv, int64_t R) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= R) return;
+    const double w = wv[i], v = wv[R + i];
+    state[i] = w + (state[R + i] + v) * rinv[i];
+    state[R + i] = -v;
+}
+
 inline int nb256(int64_t n) { return (int)std::max<int64_t>(1, (n + 255) / 256); }
 
 // Row lists -> SELL-64 (rows padded to a multiple of 64; padding slots: column 0, value 0).
@@ -659,6 +672,12 @@ struct ddpca_mcontact {
     DevBuf<double> uo, state_old, gcst, partial, moni;
     SellOp op_gamma, op_aux, op_lam;     // gamma (my halves), aux RHS, lambda RHS
     MassBatch mb_aux, mb_lam;
+    // fused interface update (every owned side has inteMass_pena = rho inteMass and
+    // systTran_pena = rho systTran): one batched solve of M [w | v] = [T^T u | I gamma]
+    bool fused = false;
+    SellOp op_wv;
+    MassBatch mb_wv;
+    DevBuf<double> rinv;
     CoarseDev cs;
     std::vector<double> moni_host;
     hipStream_t main = nullptr;          // == mg->stream
@@ -845,6 +864,56 @@ void build(ddpca_mcontact& H, Problem& P) {
         }
         H.mb_aux.build(Ma, ro, H.R);
         H.mb_lam.build(Ml, ro, H.R);
+        // fused update when the penalty operators are exact multiples of the plain ones
+        // (entries agree to rounding: the penalty operators are accumulated with pen inside the
+        // basis products, e.g. off-diagonal T^T P T entries are rounding noise around 0)
+        auto proportional = [](const Csr& A, const Csr& B, double rho) {
+            if (A.nrow != B.nrow || A.ptr != B.ptr || A.col != B.col) return false;
+            double amax = 0.0;
+            for (double v : A.val) amax = std::max(amax, std::abs(v));
+            for (int64_t k = 0; k < A.nnz(); ++k)
+                if (std::abs(A.val[k] - rho * B.val[k]) > 1e-13 * amax) return false;
+            return true;
+        };
+        const char* env = std::getenv("DDPCA_MASS_FUSED");
+        bool fuse = !H.sides.empty() && (!env || std::atoi(env) != 0);
+        for (const auto& sd : H.sides) {
+            const Interface& itf = mc.searCont[sd.ts];
+            const double rho = itf.penN;
+            fuse = fuse && itf.penN == itf.penF && rho > 0.0 && proportional(itf.inteMass_pena[sd.s], itf.inteMass[sd.s], rho) &&
+                   proportional(itf.systTran_pena[sd.s], itf.systTran[sd.s], rho);
+        }
+        if (fuse) {
+            H.fused = true;
+            Rows rwv(2 * H.R);
+            std::vector<double> ri(std::max<int64_t>(H.R, 1), 0.0);
+            std::vector<const Csr*> M2;
+            std::vector<int64_t> ro2;
+            for (const auto& sd : H.sides) {
+                const Interface& itf = mc.searCont[sd.ts];
+                const auto& I = itf_of(sd.ts);
+                const int64_t u0 = H.subs[sd.sub].dof0;
+                const Csr tT = transpose(itf.systTran[sd.s]);
+                const Csr& Ii = itf.inteInpo[sd.s];
+                for (int64_t r = 0; r < sd.m; ++r) {
+                    for (int64_t k = tT.ptr[r]; k < tT.ptr[r + 1]; ++k) rwv[sd.roff + r].push_back({u0 + tT.col[k], tT.val[k]});
+                    for (int64_t k = Ii.ptr[r]; k < Ii.ptr[r + 1]; ++k)
+                        rwv[H.R + sd.roff + r].push_back({H.oG + I.goff + Ii.col[k], Ii.val[k]});
+                    ri[sd.roff + r] = 1.0 / itf.penN;
+                }
+                M2.push_back(&itf.inteMass[sd.s]);
+                ro2.push_back(sd.roff);
+            }
+            for (const auto& sd : H.sides) {
+                M2.push_back(&mc.searCont[sd.ts].inteMass[sd.s]);
+                ro2.push_back(H.R + sd.roff);
+            }
+            H.op_wv.build(rwv);
+            H.mb_wv.build(M2, ro2, 2 * H.R);
+            H.rinv.upload(ri);
+        }
+        if (std::getenv("DDPCA_VERBOSE"))
+            std::fprintf(stderr, "[ddpca] interface update: %s\n", H.fused ? "fused (one batched mass solve)" : "sequential");
     }
     // ---- coupling rows of the body-balance RHS: sum over incident sides of
     //      [systTran_pena | -systTran] on free dofs, solver dofs x W columns
@@ -1215,8 +1284,12 @@ bool iterate_once(ddpca_mcontact& H, bool check) {
         if (I.mine)
             hipLaunchKernelGGL(k_project, dim3(nb256(I.mip / I.comp)), dim3(256), 0, st, H.gamma + I.goff, I.stat.p,
                                I.mip / I.comp, I.comp, I.fric);
-    // ---- aux = (M^rho)^-1 (T^T u + M lambda + I gamma)
-    if (!H.sides.empty()) {
+    // ---- aux = (M^rho)^-1 (T^T u + M lambda + I gamma), lambda += M^-1 (T^T u - M^rho aux)
+    if (H.fused) {
+        H.op_wv.apply(st, H.W.p, H.mb_wv.b.p, nullptr);
+        H.mb_wv.solve(st, H.mb_wv.x.p, 1.0e-14, 2000);
+        hipLaunchKernelGGL(k_fuse_aux_lambda, dim3(nb256(H.R)), dim3(256), 0, st, H.state, H.mb_wv.x.p, H.rinv.p, H.R);
+    } else if (!H.sides.empty()) {
         H.op_aux.apply(st, H.W.p, H.mb_aux.b.p, nullptr);
         H.mb_aux.solve(st, H.state, 1.0e-14, 2000);
         // ---- lambda += M^-1 (T^T u - M^rho aux)
@@ -1240,6 +1313,7 @@ bool iterate_once(ddpca_mcontact& H, bool check) {
     if (H.mg) H.mg->pcg_check();
     H.mb_aux.check();
     H.mb_lam.check();
+    H.mb_wv.check();
     float a = 0, b = 0;
     (void)hipEventElapsedTime(&a, H.ev[1], H.ev[3]);
     (void)hipEventElapsedTime(&b, H.ev[0], H.ev[2]);
@@ -1247,7 +1321,7 @@ bool iterate_once(ddpca_mcontact& H, bool check) {
     H.timing[1] += t_solve;
     H.timing[2] += a;
     H.timing[3] += any_cross ? b : 0.0;
-    H.mass_iters += (double)(H.mb_aux.last_iters + H.mb_lam.last_iters);
+    H.mass_iters += (double)(H.fused ? H.mb_wv.last_iters : H.mb_aux.last_iters + H.mb_lam.last_iters);
     if (H.mg) {
         MgpisDevice& D = *H.mg;
         for (int s = 0; s < D.nsub; ++s) {

@@ -84,8 +84,8 @@ __device__ __forceinline__ void apply_m(const double* minv, int64_t row, double 
 // fp64, paired (DDPCA_PAIRED_VALUES = 1, default): 16-B lane loads -- four 1-KiB wave runs of
 // (v[2p], v[2p+1]), then a 512-B run of v[8]: 5 load instructions per block instead of 9, the
 // fine PCG SpMV 5-8 % faster (profiles/r01_spmv_ab.json).  fp32 keeps nine 256-B runs, one per
-// entry: its paired form (two 16-B quads + v[8]) measured 7-10 % SLOWER in the smoothing and
-// residual kernels.  Element (ij, lane) of slot base sb:
+// entry: its paired forms -- two 16-B quads + v[8], or four 8-B pairs + v[8] -- measured 4-13 %
+// SLOWER in the smoothing and residual kernels (profiles/r01_spmv_ab.json, _f32pairs.json).  Element (ij, lane) of slot base sb:
 //   paired fp64: sb[(ij < 8 ? 128 * (ij / 2) + 2 * lane + ij % 2 : 512 + lane)]
 //   otherwise:   sb[ij * 64 + lane]
 #ifndef DDPCA_PAIRED_VALUES
@@ -107,7 +107,7 @@ template <bool NT, typename T>
 __device__ __forceinline__ void block_fma_any(const T* v, const double* xj, double& s0, double& s1, double& s2) {
     const double x0 = xj[0], x1 = xj[1], x2 = xj[2];
     auto ldv = [](const auto* p) { if constexpr (NT) return __builtin_nontemporal_load(p); else return *p; };
-    if constexpr (paired_values<T>()) {
+    if constexpr (paired_values<T>() && sizeof(T) == 8) {
         const int lane = threadIdx.x & 63;
         const dbl2_t* p = reinterpret_cast<const dbl2_t*>(v - lane) + lane;
         const dbl2_t a = ldv(p), b = ldv(p + 64), c = ldv(p + 128), d = ldv(p + 192);
