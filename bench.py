@@ -31,6 +31,7 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+VALUE_LAYOUT = "fp64-pairs"  # SELL value layout of the fine Krylov operator (device_mgpis.hip)
 
 
 def parse():
@@ -205,8 +206,9 @@ def main():
 
 
 def traffic_key(a) -> dict:
+    # the roofline launch does not depend on musc / omega / coarse level; it does on the value layout
     return dict(groups=a.groups, nx=a.nx, ny=a.ny, nz=a.nz, gl=a.gl, smoother=a.smoother, nu=a.nu,
-                precond_fp32=a.precond_fp32, table_mode=a.table_mode)  # the SpMV launch is unchanged by musc
+                precond_fp32=a.precond_fp32, table_mode=a.table_mode, value_layout=VALUE_LAYOUT)
 
 
 def cpu_baseline(P, nsub, owner, budget_s=10.0):

@@ -45,6 +45,7 @@ def main():
     for k, d in [("groups", 4), ("nx", 3), ("ny", 2), ("nz", 2), ("gl", 5), ("smoother", 1), ("nu", 1),
                  ("precond-fp32", 1), ("table-mode", 0)]:
         ap.add_argument(f"--{k}", type=int, default=d)
+    ap.add_argument("--value-layout", default="fp64-pairs")
     ap.add_argument("--out", default=str(Path(__file__).resolve().parent / "traffic.json"))
     a = ap.parse_args()
     fetch = full_launches(per_launch(a.fetch_csv, "FETCH_SIZE"))
@@ -53,7 +54,7 @@ def main():
     res = {
         "kernel": "k_sell<kPcg> fine level",
         "config": dict(groups=a.groups, nx=a.nx, ny=a.ny, nz=a.nz, gl=a.gl, smoother=a.smoother, nu=a.nu,
-                       precond_fp32=a.precond_fp32, table_mode=a.table_mode),
+                       precond_fp32=a.precond_fp32, table_mode=a.table_mode, value_layout=a.value_layout),
         "fetch_size_kb_median": fkb,
         "write_size_kb_median": wkb,
         "launches_used": [len(fetch), len(write)],
