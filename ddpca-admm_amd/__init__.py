@@ -78,6 +78,8 @@ def _declare(L: C.CDLL) -> None:
     L.ddpca_problem_set_interface.argtypes = [_P, C.c_int64, C.c_int64, C.c_int64, C.c_double, C.c_int64, C.c_int64,
                                               C.c_int64, _P, _P, C.POINTER(_CsrArg)]
     L.ddpca_problem_finalize.argtypes = [_P]
+    L.ddpca_problem_set_coarse_operators.argtypes = [_P, C.c_int64, _P, _P, C.POINTER(_CsrArg), _P,
+                                                     C.POINTER(_CsrArg), C.POINTER(_CsrArg), C.POINTER(_CsrArg)]
     L.mgpis_gpu_create.argtypes = [C.c_int, C.c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P,
                                    C.POINTER(MgpisOptions), C.POINTER(_P)]
     L.mgpis_gpu_create_bsr3.argtypes = [C.c_int, C.c_int, _P, _P, _P, _P, _P, _P, _P, _P,
@@ -213,14 +215,17 @@ class Problem:
     IFACE_OPS = ("inpoLagr", "pemaInpo_r", "systTran", "systTran_pena", "inteMass", "inteMass_pena", "inteInpo")
 
     @classmethod
-    def from_operators(cls, subdomains: Sequence[dict], interfaces: Sequence[dict]) -> "Problem":
+    def from_operators(cls, subdomains: Sequence[dict], interfaces: Sequence[dict],
+                       coarse: Optional[dict] = None) -> "Problem":
         """Established problem from operators in the reference's layouts (no host restatement).
 
         subdomains[tv]: nnodes (per level), free_dof (per level, increasing nodal dofs), K (per
         level, condensed consStif CSR), S (per level < L, scalar stencil CSR), consForc, and
         optionally presc (3N nodal Dirichlet values) and coords (N x 3).
         interfaces[ts]: body (2), fric, nip, nnc (2), pemaDiag, inpoNgap, ops[s][name] CSR for
-        the names in Problem.IFACE_OPS."""
+        the names in Problem.IFACE_OPS.
+        coarse (optional, the caller's MCONTACT::MULTISCALE_1 output, muscSett = 2): doleMcsc,
+        baseReco, globCoup_1, globForc_1, globTran_1[ts][s], globTran_D_1[tv], accuProl[tv]."""
         self = cls.__new__(cls)
         h = C.c_void_p()
         _check(lib().ddpca_problem_empty(len(subdomains), len(interfaces), C.byref(h)))
@@ -263,6 +268,19 @@ class Problem:
             _check(lib().ddpca_problem_set_interface(
                 self._h, ts, int(f["body"][0]), int(f["body"][1]), float(f["fric"]), int(f["nip"]), int(f["nnc"][0]),
                 int(f["nnc"][1]), _ptr(arr(f["pemaDiag"], np.float64)), _ptr(arr(f["inpoNgap"], np.float64)), ops))
+        if coarse is not None:
+            def csr_arg(m):
+                m = m.tocsr()
+                return _CsrArg(m.shape[0], m.shape[1], _ptr(arr(m.indptr, np.int64)), _ptr(arr(m.indices, np.int32)),
+                               _ptr(arr(m.data, np.float64)))
+            nint = len(interfaces)
+            gt = (_CsrArg * max(1, 2 * nint))(*[csr_arg(coarse["globTran_1"][ts][s]) for ts in range(nint) for s in range(2)])
+            gd = (_CsrArg * len(subdomains))(*[csr_arg(m) for m in coarse["globTran_D_1"]])
+            ap = (_CsrArg * len(subdomains))(*[csr_arg(m) for m in coarse["accuProl"]])
+            gc = csr_arg(coarse["globCoup_1"])
+            _check(lib().ddpca_problem_set_coarse_operators(
+                self._h, 2, _ptr(arr(coarse["doleMcsc"], np.int64)), _ptr(arr(coarse["baseReco"], np.int64)),
+                C.byref(gc), _ptr(arr(coarse["globForc_1"], np.float64)), gt, gd, ap))
         _check(lib().ddpca_problem_finalize(self._h))
         return self
 

@@ -162,6 +162,53 @@ int ddpca_problem_set_interface(ddpca_problem_t h, int64_t ts, int64_t body0, in
     });
 }
 
+int ddpca_problem_set_coarse_operators(ddpca_problem_t h, int64_t muscSett, const int64_t* doleMcsc,
+                                       const int64_t* baseReco, const ddpca_csr_t* globCoup_1, const double* globForc_1,
+                                       const ddpca_csr_t* globTran_1, const ddpca_csr_t* globTran_D_1,
+                                       const ddpca_csr_t* accuProl) {
+    return guarded([&] {
+        Problem& P = builder(h);
+        const int64_t nsub = (int64_t)P.mc.multGrid.size(), nint = (int64_t)P.mc.searCont.size();
+        if (muscSett != 2) throw ApiError(DDPCA_EINVAL, "only muscSett = 2 (MULTISCALE_1) is supported");
+        if (!doleMcsc || !baseReco || !globCoup_1 || !globForc_1 || (nint && !globTran_1) || !globTran_D_1 || !accuProl)
+            throw ApiError(DDPCA_EINVAL, "null argument");
+        CoarseSpace C;
+        C.assembled = true;
+        C.baseReco.assign(baseReco, baseReco + nsub + 1);
+        C.n = C.baseReco[nsub];
+        P.mc.doleMcsc.assign(doleMcsc, doleMcsc + nsub);
+        for (int64_t tv = 0; tv < nsub; ++tv) {
+            const MULTIGRID& g = P.mc.multGrid[tv];
+            if (g.leveCount.empty()) throw ApiError(DDPCA_ESTATE, "set every subdomain before the coarse operators");
+            const int64_t d = P.mc.doleMcsc[tv];
+            if (d < 0 || d > g.maxiLeve) throw ApiError(DDPCA_EINVAL, "doleMcsc out of range");
+            if (C.baseReco[tv + 1] - C.baseReco[tv] != g.freeCount[d]) throw ApiError(DDPCA_EINVAL, "baseReco does not match nfree[doleMcsc]");
+        }
+        C.globCoup_1 = to_csr(*globCoup_1, "globCoup_1");
+        expect_shape(C.globCoup_1, C.n, C.n, "globCoup_1");
+        C.globForc_1.assign(globForc_1, globForc_1 + C.n);
+        C.globTran_1.assign(nint, {});
+        for (int64_t ts = 0; ts < nint; ++ts)
+            for (int s = 0; s < 2; ++s) {
+                const Interface& itf = P.mc.searCont[ts];
+                if (itf.inteMass[s].ptr.empty()) throw ApiError(DDPCA_ESTATE, "set every interface before the coarse operators");
+                C.globTran_1[ts][s] = to_csr(globTran_1[2 * ts + s], "globTran_1");
+                expect_shape(C.globTran_1[ts][s], C.n, itf.mside(s), "globTran_1");
+            }
+        for (int64_t tv = 0; tv < nsub; ++tv) {
+            const MULTIGRID& g = P.mc.multGrid[tv];
+            C.globTran_D_full.push_back(to_csr(globTran_D_1[tv], "globTran_D_1"));
+            expect_shape(C.globTran_D_full.back(), C.n, 3 * g.leveCount.back(), "globTran_D_1");
+            C.accuProl_full.push_back(to_csr(accuProl[tv], "accuProl"));
+            expect_shape(C.accuProl_full.back(), g.freeCount.back(), g.freeCount[P.mc.doleMcsc[tv]], "accuProl");
+        }
+        C.built.assign(nsub, 1);
+        C.ready = true;
+        P.mc.coarse = std::move(C);
+        P.mc.muscSett = muscSett;
+    });
+}
+
 int ddpca_problem_finalize(ddpca_problem_t h) {
     return guarded([&] {
         Problem& P = builder(h);

@@ -374,8 +374,11 @@ int ddpca_problem_view(ddpca_problem_t h, const char* cname, int64_t index, int6
                 if (index < 0 || index >= nsub || !cs.built[index]) throw ApiError(DDPCA_EINVAL, "subdomain index");
                 const std::string ck = b + std::to_string(index);
                 auto it = P.cache_csr.find(ck);
-                if (it == P.cache_csr.end())
-                    it = P.cache_csr.emplace(ck, b[0] == 'g' ? P.mc.globTran_D_1(index) : P.mc.accuProl(index)).first;
+                if (it == P.cache_csr.end()) {
+                    Csr m = cs.assembled ? (b[0] == 'g' ? cs.globTran_D_full[index] : cs.accuProl_full[index])
+                                         : (b[0] == 'g' ? P.mc.globTran_D_1(index) : P.mc.accuProl(index));
+                    it = P.cache_csr.emplace(ck, std::move(m)).first;
+                }
                 put_csr(it->second, name.substr(b.size()));
                 return;
             }

@@ -406,6 +406,23 @@ __global__ void k_cs_prolong(const int32_t* qcol, const double* qw, int64_t nn, 
     }
 }
 
+// assembled accuProl (operator-level builder): u[tgt[r]] += sum_k val[k] xc[col[k]] over the owned
+// subdomains' fine free dofs (one row per thread), then u[cdof[i]] += presc[cdof[i]] on the
+// constrained dofs (OUTP_SUB1 writes their prescribed values again, MCONTACT.h:2606-2608)
+__global__ void k_cs_prolong_csr(const int64_t* ptr, const int32_t* col, const double* val, const int32_t* tgt,
+                                 const double* xc, double* u, int64_t nrow) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= nrow) return;
+    double s = 0.0;
+    for (int64_t k = ptr[r]; k < ptr[r + 1]; ++k) s += val[k] * xc[col[k]];
+    u[tgt[r]] += s;
+}
+
+__global__ void k_cs_presc(const int32_t* cdof, const double* presc, double* u, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) u[cdof[i]] += presc[cdof[i]];
+}
+
 // potri(lower) on the column-major view leaves the inverse in the row-major upper triangle;
 // mirror it into the lower one
 __global__ void k_fill_lower(double* A, int64_t n) {
@@ -622,6 +639,12 @@ struct CoarseDev {
     DevBuf<int32_t> xsrc, qcol;
     DevBuf<double> qw;
     DevBuf<uint8_t> flag;
+    // assembled variant (cs.assembled): accuProl as CSR rows over the owned fine free dofs
+    bool assembled = false;
+    int64_t npr = 0, ncd = 0;
+    DevBuf<int64_t> pptr;
+    DevBuf<int32_t> pcol, ptgt, cdof;
+    DevBuf<double> pval;
     std::vector<int64_t> own_rows;  // global coarse rows of this rank, in xc order
     std::vector<double> dense;      // host, until inverted: this rank's rows of globCoup_1 (n x n, zeros elsewhere)
 };
@@ -998,7 +1021,9 @@ void build_coarse(ddpca_mcontact& H, Problem& P) {
             for (int64_t k = T.ptr[r]; k < T.ptr[r + 1]; ++k) rows[r].push_back({(int32_t)(lam0 + T.col[k]), T.val[k]});
     }
     for (size_t i = 0; i < H.subs.size(); ++i) {
-        const Csr& T = cs.globTran_S[H.subs[i].tv];
+        // factored: the interface part (the stiffness part is the SpMV + restriction chain);
+        // assembled: the caller's whole globTran_D_1
+        const Csr& T = cs.assembled ? cs.globTran_D_full[H.subs[i].tv] : cs.globTran_S[H.subs[i].tv];
         const int64_t u0 = H.subs[i].dof0;
         for (int64_t r = 0; r < T.nrow; ++r)
             for (int64_t k = T.ptr[r]; k < T.ptr[r + 1]; ++k) rows[r].push_back({(int32_t)(u0 + T.col[k]), -T.val[k]});
@@ -1032,6 +1057,37 @@ void build_coarse(ddpca_mcontact& H, Problem& P) {
         for (int64_t k = cs.globCoup_1.ptr[r]; k < cs.globCoup_1.ptr[r + 1]; ++k)
             C.dense[(size_t)r * n + cs.globCoup_1.col[k]] = cs.globCoup_1.val[k];
     if (!H.mg) return;
+    if (cs.assembled) {
+        C.assembled = true;
+        std::vector<int64_t> ptr{0};
+        std::vector<int32_t> col, tgt, cd;
+        std::vector<double> val;
+        for (size_t i = 0; i < H.subs.size(); ++i) {
+            const int64_t tv = H.subs[i].tv;
+            const MULTIGRID& g = mc.multGrid[tv];
+            const Csr& A = cs.accuProl_full[tv];
+            std::vector<int64_t> f2d(g.freeCount.back(), -1);
+            for (int64_t d = 0; d < (int64_t)g.consFlag.size(); ++d)
+                if (g.freeIndex[d] >= 0) f2d[g.freeIndex[d]] = d;
+                else cd.push_back((int32_t)(H.subs[i].dof0 + d));
+            for (int64_t r = 0; r < A.nrow; ++r) {
+                for (int64_t k = A.ptr[r]; k < A.ptr[r + 1]; ++k) {
+                    col.push_back((int32_t)(xoff[i] + A.col[k]));
+                    val.push_back(A.val[k]);
+                }
+                ptr.push_back((int64_t)col.size());
+                tgt.push_back((int32_t)(H.subs[i].dof0 + f2d[r]));
+            }
+        }
+        C.npr = (int64_t)tgt.size();
+        C.ncd = (int64_t)cd.size();
+        C.pptr.upload(ptr);
+        C.pcol.upload(col.empty() ? std::vector<int32_t>{0} : col);
+        C.pval.upload(val.empty() ? std::vector<double>{0.0} : val);
+        C.ptgt.upload(tgt.empty() ? std::vector<int32_t>{0} : tgt);
+        C.cdof.upload(cd.empty() ? std::vector<int32_t>{0} : cd);
+        return;
+    }
     MgpisDevice& D = *H.mg;
     const int L = (int)D.lev.size() - 1;
     // stiffness part: gather level-d device values into the owned coarse rows
@@ -1145,7 +1201,7 @@ void coarse_correct(ddpca_mcontact& H) {
     if (!C.inverted) throw ApiError(DDPCA_ESTATE, "coarse space not factorised (multi-rank runs: comm_init first)");
     hipStream_t st = H.main;
     const int64_t n = C.n;
-    if (H.mg) {
+    if (H.mg && !C.assembled) {
         MgpisDevice& D = *H.mg;
         const int L = (int)D.lev.size() - 1;
         // consStif[L] x on every owned subdomain, then realProl^T down to level doleMcsc
@@ -1154,7 +1210,7 @@ void coarse_correct(ddpca_mcontact& H) {
     }
     hipLaunchKernelGGL(k_csr_wave, dim3(ceil_div(n, 4)), dim3(256), 0, st, C.rptr.p, C.rcol.p, C.rval.p, n, H.W.p,
                        C.g.p, C.f0.p);
-    if (H.mg) {
+    if (H.mg && !C.assembled) {
         MgpisDevice& D = *H.mg;
         const int L = (int)D.lev.size() - 1;
         for (auto& G : C.kg) {
@@ -1166,6 +1222,13 @@ void coarse_correct(ddpca_mcontact& H) {
     if (H.nranks > 1) DDPCA_NCCL(ncclAllReduce(C.g.p, C.g.p, n, ncclDouble, ncclSum, H.comm, st));
     if (!C.nown) return;
     hipLaunchKernelGGL(k_gemv_wave, dim3(ceil_div(C.nown, 4)), dim3(256), 0, st, C.ainv.p, C.g.p, C.xc.p, C.nown, n);
+    if (C.assembled) {
+        if (C.npr)
+            hipLaunchKernelGGL(k_cs_prolong_csr, dim3(nb256(C.npr)), dim3(256), 0, st, C.pptr.p, C.pcol.p, C.pval.p, C.ptgt.p,
+                               C.xc.p, H.u, C.npr);
+        if (C.ncd) hipLaunchKernelGGL(k_cs_presc, dim3(nb256(C.ncd)), dim3(256), 0, st, C.cdof.p, H.presc.p, H.u, C.ncd);
+        return;
+    }
     hipLaunchKernelGGL(k_cs_scatter, dim3(nb256(C.nxn)), dim3(256), 0, st, C.xsrc.p, C.xc.p, C.xn.p, C.nxn);
     hipLaunchKernelGGL(k_cs_prolong, dim3(nb256(C.qnn)), dim3(256), 0, st, C.qcol.p, C.qw.p, C.qnn, C.xn.p, C.flag.p,
                        H.presc.p, H.u);

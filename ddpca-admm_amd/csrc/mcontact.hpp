@@ -52,6 +52,11 @@ struct CoarseSpace {
                                               // (the stiffness part Rc consStif[L] C_L is applied
                                               // in factored form)
     std::vector<Stencil> accuQ;               // [tv] fine node -> level-d node prolongation chain
+    // assembled variant (operator-level builder: the caller's own MULTISCALE_1 output): the full
+    // globTran_D_1[tv] (n x 3N_tv) and accuProl[tv] (nfree_L x nfree_d) replace the factored
+    // stiffness part / globTran_S and accuQ
+    bool assembled = false;
+    std::vector<Csr> globTran_D_full, accuProl_full;
 };
 
 // prolOper[L-1] ... prolOper[d] of one grid as a single scalar stencil (no masks)

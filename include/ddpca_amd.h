@@ -191,6 +191,16 @@ int ddpca_problem_set_subdomain(ddpca_problem_t p, int64_t tv, int nlev, const i
 int ddpca_problem_set_interface(ddpca_problem_t p, int64_t ts, int64_t body0, int64_t body1, double fric,
                                 int64_t nip, int64_t nnc0, int64_t nnc1, const double* pemaDiag,
                                 const double* inpoNgap, const ddpca_csr_t* ops);
+/* The caller's own interface-eliminated coarse space (MCONTACT::MULTISCALE_1, MCONTACT.h:
+ * 1672-2301, muscSett = 2), after every subdomain and interface was set: doleMcsc[nsub],
+ * baseReco[nsub+1], globCoup_1 (n x n), globForc_1 (n), globTran_1[2*ts+s] (n x comp*nnc_s),
+ * globTran_D_1[tv] (n x 3N_tv, columns in the nodal numbering of set_subdomain) and
+ * accuProl[tv] (nfree_L x nfree_doleMcsc) -- the ADMM loop then applies the correction of
+ * MCONTACT.h:2578-2612 every iteration while tc <= MULT_MAXI. */
+int ddpca_problem_set_coarse_operators(ddpca_problem_t p, int64_t muscSett, const int64_t* doleMcsc,
+                                       const int64_t* baseReco, const ddpca_csr_t* globCoup_1,
+                                       const double* globForc_1, const ddpca_csr_t* globTran_1,
+                                       const ddpca_csr_t* globTran_D_1, const ddpca_csr_t* accuProl);
 /* Check that every subdomain and interface was set; mark the problem established. */
 int ddpca_problem_finalize(ddpca_problem_t p);
 

@@ -7,7 +7,7 @@
 // compared with the reference's matrices.  With "gpu", the device ADMM loop then runs on that
 // problem (mcontact_gpu_*) and is compared with the reference's own CONTACT_ANALYSIS in the same
 // process.  Prints JSON lines; exit code 0 = match.
-//   ref_bind fric globLeve [gpu]
+//   ref_bind fric globLeve [gpu [muscSett]]
 #define HARNESS_NO_MAIN
 #include "ref_harness.cpp"
 #include "ref_bind.hpp"
@@ -49,6 +49,10 @@ int main(int argc, char** argv) {
     if (argc < 3) { std::fprintf(stderr, "usage: ref_bind fric globLeve\n"); return 2; }
     MCONTACT mc;
     harness::twoblock_build(mc, std::stod(argv[1]), std::stol(argv[2]));
+    if (argc > 4 && std::stol(argv[4]) == 2) {  // interface-eliminated coarse space (BLOCK.h:38-41 setting)
+        mc.muscSett = 2;
+        mc.doleMcsc.assign(mc.multGrid.size(), 1);
+    }
     std::string log;
     harness::capture_iters([&] { mc.ESTABLISH(); }, &log);
     ddpca_problem_t p = ddpca_bind::from_reference(mc);

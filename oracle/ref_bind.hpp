@@ -98,7 +98,9 @@ inline mgpis_t mgpis_create(MULTIGRID& g, int device, const mgpis_options_t* opt
     return out;
 }
 
-// MCONTACT after ESTABLISH() (muscSett = 0) -> an established device problem.
+// MCONTACT after ESTABLISH() -> an established device problem; with muscSett = 2 its
+// MULTISCALE_1 coarse operators go along (globTran_D_1 columns moved to positions like the
+// systTran rows; accuProl and globTran_1 are in free / contact numbering already).
 inline ddpca_problem_t from_reference(MCONTACT& mc) {
     const int64_t nsub = (int64_t)mc.multGrid.size(), nint = (int64_t)mc.searCont.size();
     ddpca_problem_t p = nullptr;
@@ -129,6 +131,25 @@ inline ddpca_problem_t from_reference(MCONTACT& mc) {
                                           (int64_t)mc.searCont[ts].intePoin.size(), (int64_t)mc.nodeCont[ts][0].size(),
                                           (int64_t)mc.nodeCont[ts][1].size(), pema.data(), mc.inpoNgap[ts].data(),
                                           v.data()));
+    }
+    if ((mc.muscSett >> 1) % 2 == 1) {
+        std::vector<int64_t> dole(mc.doleMcsc.begin(), mc.doleMcsc.end());
+        std::vector<int64_t> base(mc.baseReco.begin(), mc.baseReco.end());
+        std::vector<Csr> gt, gd, ap;
+        for (int64_t ts = 0; ts < nint; ++ts)
+            for (int s = 0; s < 2; ++s) gt.emplace_back(mc.globTran_1[ts][s]);
+        for (int64_t tv = 0; tv < nsub; ++tv) {
+            gd.emplace_back(SpMat(mc.globTran_D_1[tv] * mc.multGrid[tv].earlTran));
+            ap.emplace_back(mc.accuProl[tv]);
+        }
+        Csr gc(mc.globCoup_1);
+        std::vector<ddpca_csr_t> vt, vd, va;
+        for (const auto& o : gt) vt.push_back(o.view());
+        for (const auto& o : gd) vd.push_back(o.view());
+        for (const auto& o : ap) va.push_back(o.view());
+        const ddpca_csr_t vc = gc.view();
+        check(ddpca_problem_set_coarse_operators(p, 2, dole.data(), base.data(), &vc, mc.globForc_1.data(), vt.data(),
+                                                 vd.data(), va.data()));
     }
     check(ddpca_problem_finalize(p));
     return p;
