@@ -80,6 +80,8 @@ def _declare(L: C.CDLL) -> None:
     L.ddpca_problem_finalize.argtypes = [_P]
     L.ddpca_problem_set_coarse_operators.argtypes = [_P, C.c_int64, _P, _P, C.POINTER(_CsrArg), _P,
                                                      C.POINTER(_CsrArg), C.POINTER(_CsrArg), C.POINTER(_CsrArg)]
+    L.ddpca_problem_set_coarse_latin.argtypes = [_P, _P, _P, C.POINTER(_CsrArg), C.POINTER(_CsrArg),
+                                                 C.POINTER(_CsrArg), C.POINTER(_CsrArg), C.POINTER(_CsrArg)]
     L.mgpis_gpu_create.argtypes = [C.c_int, C.c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P,
                                    C.POINTER(MgpisOptions), C.POINTER(_P)]
     L.mgpis_gpu_create_bsr3.argtypes = [C.c_int, C.c_int, _P, _P, _P, _P, _P, _P, _P, _P,
@@ -225,7 +227,9 @@ class Problem:
         interfaces[ts]: body (2), fric, nip, nnc (2), pemaDiag, inpoNgap, ops[s][name] CSR for
         the names in Problem.IFACE_OPS.
         coarse (optional, the caller's MCONTACT::MULTISCALE_1 output, muscSett = 2): doleMcsc,
-        baseReco, globCoup_1, globForc_1, globTran_1[ts][s], globTran_D_1[tv], accuProl[tv]."""
+        baseReco, globCoup_1, globForc_1, globTran_1[ts][s], globTran_D_1[tv], accuProl[tv]; or
+        its MULTISCALE output (muscSett = 1) with latin=True: doleMcsc, baseReco, globCoup,
+        globTran / globTran_pena / globTran_D [ts][s], accuProl[tv]."""
         self = cls.__new__(cls)
         h = C.c_void_p()
         _check(lib().ddpca_problem_empty(len(subdomains), len(interfaces), C.byref(h)))
@@ -268,7 +272,22 @@ class Problem:
             _check(lib().ddpca_problem_set_interface(
                 self._h, ts, int(f["body"][0]), int(f["body"][1]), float(f["fric"]), int(f["nip"]), int(f["nnc"][0]),
                 int(f["nnc"][1]), _ptr(arr(f["pemaDiag"], np.float64)), _ptr(arr(f["inpoNgap"], np.float64)), ops))
-        if coarse is not None:
+        if coarse is not None and coarse.get("latin", False):
+            def csr_arg(m):
+                m = m.tocsr()
+                return _CsrArg(m.shape[0], m.shape[1], _ptr(arr(m.indptr, np.int64)), _ptr(arr(m.indices, np.int32)),
+                               _ptr(arr(m.data, np.float64)))
+            nint = len(interfaces)
+
+            def sides(name):
+                return (_CsrArg * max(1, 2 * nint))(*[csr_arg(coarse[name][ts][s]) for ts in range(nint)
+                                                      for s in range(2)])
+            ap = (_CsrArg * len(subdomains))(*[csr_arg(m) for m in coarse["accuProl"]])
+            gc = csr_arg(coarse["globCoup"])
+            _check(lib().ddpca_problem_set_coarse_latin(
+                self._h, _ptr(arr(coarse["doleMcsc"], np.int64)), _ptr(arr(coarse["baseReco"], np.int64)), C.byref(gc),
+                sides("globTran"), sides("globTran_pena"), sides("globTran_D"), ap))
+        elif coarse is not None:
             def csr_arg(m):
                 m = m.tocsr()
                 return _CsrArg(m.shape[0], m.shape[1], _ptr(arr(m.indptr, np.int64)), _ptr(arr(m.indices, np.int32)),

@@ -209,6 +209,56 @@ int ddpca_problem_set_coarse_operators(ddpca_problem_t h, int64_t muscSett, cons
     });
 }
 
+int ddpca_problem_set_coarse_latin(ddpca_problem_t h, const int64_t* doleMcsc, const int64_t* baseReco,
+                                   const ddpca_csr_t* globCoup, const ddpca_csr_t* globTran,
+                                   const ddpca_csr_t* globTran_pena, const ddpca_csr_t* globTran_D,
+                                   const ddpca_csr_t* accuProl) {
+    return guarded([&] {
+        Problem& P = builder(h);
+        const int64_t nsub = (int64_t)P.mc.multGrid.size(), nint = (int64_t)P.mc.searCont.size();
+        if (!doleMcsc || !baseReco || !globCoup || (nint && (!globTran || !globTran_pena || !globTran_D)) || !accuProl)
+            throw ApiError(DDPCA_EINVAL, "null argument");
+        CoarseSpace C;
+        C.assembled = true;
+        C.latin = true;
+        C.baseReco.assign(baseReco, baseReco + nsub + 1);
+        P.mc.doleMcsc.assign(doleMcsc, doleMcsc + nsub);
+        C.globCoup_1 = to_csr(*globCoup, "globCoup");
+        C.n = C.globCoup_1.nrow;
+        expect_shape(C.globCoup_1, C.n, C.n, "globCoup");
+        if (C.n < C.baseReco[nsub]) throw ApiError(DDPCA_EINVAL, "globCoup smaller than baseReco[nsub]");
+        for (int64_t tv = 0; tv < nsub; ++tv) {
+            const MULTIGRID& g = P.mc.multGrid[tv];
+            if (g.leveCount.empty()) throw ApiError(DDPCA_ESTATE, "set every subdomain before the coarse operators");
+            const int64_t d = P.mc.doleMcsc[tv];
+            if (d < 0 || d > g.maxiLeve) throw ApiError(DDPCA_EINVAL, "doleMcsc out of range");
+            if (C.baseReco[tv + 1] - C.baseReco[tv] != g.freeCount[d]) throw ApiError(DDPCA_EINVAL, "baseReco does not match nfree[doleMcsc]");
+            C.accuProl_full.push_back(to_csr(accuProl[tv], "accuProl"));
+            expect_shape(C.accuProl_full.back(), g.freeCount.back(), g.freeCount[d], "accuProl");
+        }
+        C.globForc_1.assign(C.n, 0.0);
+        C.globTran_L.assign(nint, {});
+        C.globTran_pena_L.assign(nint, {});
+        C.globTran_D_L.assign(nint, {});
+        for (int64_t ts = 0; ts < nint; ++ts)
+            for (int s = 0; s < 2; ++s) {
+                const Interface& itf = P.mc.searCont[ts];
+                if (itf.inteMass[s].ptr.empty()) throw ApiError(DDPCA_ESTATE, "set every interface before the coarse operators");
+                const int64_t n3 = 3 * P.mc.multGrid[itf.body[s]].leveCount.back();
+                C.globTran_L[ts][s] = to_csr(globTran[2 * ts + s], "globTran");
+                C.globTran_pena_L[ts][s] = to_csr(globTran_pena[2 * ts + s], "globTran_pena");
+                C.globTran_D_L[ts][s] = to_csr(globTran_D[2 * ts + s], "globTran_D");
+                expect_shape(C.globTran_L[ts][s], C.n, itf.mside(s), "globTran");
+                expect_shape(C.globTran_pena_L[ts][s], C.n, itf.mside(s), "globTran_pena");
+                expect_shape(C.globTran_D_L[ts][s], C.n, n3, "globTran_D");
+            }
+        C.built.assign(nsub, 1);
+        C.ready = true;
+        P.mc.coarse = std::move(C);
+        P.mc.muscSett = 1;
+    });
+}
+
 int ddpca_problem_finalize(ddpca_problem_t h) {
     return guarded([&] {
         Problem& P = builder(h);

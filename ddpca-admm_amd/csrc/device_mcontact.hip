@@ -640,7 +640,7 @@ struct CoarseDev {
     DevBuf<double> qw;
     DevBuf<uint8_t> flag;
     // assembled variant (cs.assembled): accuProl as CSR rows over the owned fine free dofs
-    bool assembled = false;
+    bool assembled = false, latin = false;
     int64_t npr = 0, ncd = 0;
     DevBuf<int64_t> pptr;
     DevBuf<int32_t> pcol, ptgt, cdof;
@@ -998,8 +998,8 @@ void build_coarse(ddpca_mcontact& H, Problem& P) {
     MCONTACT& mc = P.mc;
     const CoarseSpace& cs = mc.coarse;
     CoarseDev& C = H.cs;
-    if (!(mc.muscSett & 2)) return;
-    if (!cs.ready) throw ApiError(DDPCA_ESTATE, "muscSett = 2 but the coarse space was not built");
+    if (!(mc.muscSett & 3)) return;
+    if (!cs.ready) throw ApiError(DDPCA_ESTATE, "muscSett set but the coarse space was not built");
     C.on = true;
     C.n = cs.n;
     const int64_t n = C.n;
@@ -1014,13 +1014,21 @@ void build_coarse(ddpca_mcontact& H, Problem& P) {
     // RHS rows over W: + globTran_1 (owned sides, lambda columns), - interface part of
     // globTran_D_1 (owned subdomains, u columns)
     std::vector<std::vector<std::pair<int32_t, double>>> rows(n);
-    for (const auto& sd : H.sides) {
-        const Csr& T = cs.globTran_1[sd.ts][sd.s];
-        const int64_t lam0 = H.oS + H.R + sd.roff;
+    auto add_rows = [&](const Csr& T, int64_t c0, double sgn) {
         for (int64_t r = 0; r < T.nrow; ++r)
-            for (int64_t k = T.ptr[r]; k < T.ptr[r + 1]; ++k) rows[r].push_back({(int32_t)(lam0 + T.col[k]), T.val[k]});
+            for (int64_t k = T.ptr[r]; k < T.ptr[r + 1]; ++k) rows[r].push_back({(int32_t)(c0 + T.col[k]), sgn * T.val[k]});
+    };
+    for (const auto& sd : H.sides) {
+        const int64_t lam0 = H.oS + H.R + sd.roff, aux0 = H.oS + sd.roff;
+        if (cs.latin) {  // + globTran lambda - globTran_pena aux + globTran_D u   (MCONTACT.h:2540-2548)
+            add_rows(cs.globTran_L[sd.ts][sd.s], lam0, 1.0);
+            add_rows(cs.globTran_pena_L[sd.ts][sd.s], aux0, -1.0);
+            add_rows(cs.globTran_D_L[sd.ts][sd.s], H.subs[sd.sub].dof0, 1.0);
+        } else {
+            add_rows(cs.globTran_1[sd.ts][sd.s], lam0, 1.0);
+        }
     }
-    for (size_t i = 0; i < H.subs.size(); ++i) {
+    for (size_t i = 0; i < H.subs.size() && !cs.latin; ++i) {
         // factored: the interface part (the stiffness part is the SpMV + restriction chain);
         // assembled: the caller's whole globTran_D_1
         const Csr& T = cs.assembled ? cs.globTran_D_full[H.subs[i].tv] : cs.globTran_S[H.subs[i].tv];
@@ -1053,9 +1061,13 @@ void build_coarse(ddpca_mcontact& H, Problem& P) {
     C.xc.alloc(std::max<int64_t>(C.nown, 1));
     // dense rows of globCoup_1 (inverted once every rank holds all rows)
     C.dense.assign((size_t)n * n, 0.0);
-    for (int64_t r : C.own_rows)
+    std::vector<int64_t> fill_rows = C.own_rows;
+    if (cs.latin && H.rank == 0)  // the coarse contact unknowns' rows: filled by rank 0 only
+        for (int64_t r = cs.baseReco.back(); r < n; ++r) fill_rows.push_back(r);
+    for (int64_t r : fill_rows)
         for (int64_t k = cs.globCoup_1.ptr[r]; k < cs.globCoup_1.ptr[r + 1]; ++k)
             C.dense[(size_t)r * n + cs.globCoup_1.col[k]] = cs.globCoup_1.val[k];
+    C.latin = cs.latin;
     if (!H.mg) return;
     if (cs.assembled) {
         C.assembled = true;
@@ -1173,9 +1185,19 @@ void coarse_invert(ddpca_mcontact& H) {
     DevBuf<rocblas_int> info(2);
     info.zero(st);
     rocblas_set_stream(rh, st);
-    const rocblas_status s1 = rocsolver_dpotrf(rh, rocblas_fill_lower, (rocblas_int)n, A.p, (rocblas_int)n, info.p);
-    const rocblas_status s2 = rocsolver_dpotri(rh, rocblas_fill_lower, (rocblas_int)n, A.p, (rocblas_int)n, info.p + 1);
-    hipLaunchKernelGGL(k_fill_lower, dim3(std::max<int64_t>(1, ((int64_t)n * n + 255) / 256)), dim3(256), 0, st, A.p, n);
+    rocblas_status s1, s2;
+    if (C.latin) {
+        // globCoup (displacements + coarse contact unknowns) is symmetric but indefinite: pivoted
+        // LU, then the inverse (symmetric again, so the row-major copy reads it as it is)
+        DevBuf<rocblas_int> ipiv(std::max<int64_t>(n, 1));
+        s1 = rocsolver_dgetrf(rh, (rocblas_int)n, (rocblas_int)n, A.p, (rocblas_int)n, ipiv.p, info.p);
+        s2 = rocsolver_dgetri(rh, (rocblas_int)n, A.p, (rocblas_int)n, ipiv.p, info.p + 1);
+        DDPCA_HIP(hipStreamSynchronize(st));
+    } else {
+        s1 = rocsolver_dpotrf(rh, rocblas_fill_lower, (rocblas_int)n, A.p, (rocblas_int)n, info.p);
+        s2 = rocsolver_dpotri(rh, rocblas_fill_lower, (rocblas_int)n, A.p, (rocblas_int)n, info.p + 1);
+        hipLaunchKernelGGL(k_fill_lower, dim3(std::max<int64_t>(1, ((int64_t)n * n + 255) / 256)), dim3(256), 0, st, A.p, n);
+    }
     C.ainv.alloc(std::max<int64_t>(C.nown, 1) * n);
     // owned rows are contiguous per subdomain (baseReco blocks)
     for (size_t k = 0; k < C.own_rows.size();) {
@@ -1191,7 +1213,8 @@ void coarse_invert(ddpca_mcontact& H) {
     if (s1 != rocblas_status_success || s2 != rocblas_status_success)
         throw ApiError(DDPCA_EHIP, "rocsolver potrf/potri failed on globCoup_1");
     if (inf[0] != 0 || inf[1] != 0)
-        throw ApiError(DDPCA_ENUMERIC, "globCoup_1 is not positive definite (potrf info " + std::to_string(inf[0]) + ")");
+        throw ApiError(DDPCA_ENUMERIC, std::string(C.latin ? "globCoup is singular (getrf" : "globCoup_1 is not positive definite (potrf") +
+                                           " info " + std::to_string(inf[0]) + ")");
     C.inverted = true;
 }
 

@@ -57,6 +57,11 @@ struct CoarseSpace {
     // stiffness part / globTran_S and accuQ
     bool assembled = false;
     std::vector<Csr> globTran_D_full, accuProl_full;
+    // LATIN-type coarse space (MULTISCALE, muscSett bit 0; assembled only): globCoup_1 holds
+    // globCoup (displacement blocks + coarse contact unknowns, rows >= baseReco[nsub]), the
+    // right-hand side is sum over sides of globTran lambda - globTran_pena aux + globTran_D u
+    bool latin = false;
+    std::vector<std::array<Csr, 2>> globTran_L, globTran_pena_L, globTran_D_L;  // [ts][s]
 };
 
 // prolOper[L-1] ... prolOper[d] of one grid as a single scalar stencil (no masks)

@@ -201,6 +201,17 @@ int ddpca_problem_set_coarse_operators(ddpca_problem_t p, int64_t muscSett, cons
                                        const int64_t* baseReco, const ddpca_csr_t* globCoup_1,
                                        const double* globForc_1, const ddpca_csr_t* globTran_1,
                                        const ddpca_csr_t* globTran_D_1, const ddpca_csr_t* accuProl);
+/* The caller's own LATIN-type coarse space (MCONTACT::MULTISCALE, MCONTACT.h:898-1536,
+ * muscSett = 1, CYLINDER.h:42): doleMcsc[nsub], baseReco[nsub+1], globCoup (n x n: the
+ * displacement blocks plus the coarse contact unknowns, rows >= baseReco[nsub]),
+ * globTran / globTran_pena [2*ts+s] (n x comp*nnc_s), globTran_D[2*ts+s] (n x 3N of body s,
+ * columns in set_subdomain's nodal numbering), accuProl[tv].  Each ADMM iteration then adds
+ * u += OUTP_SUB1(accuProl globCoup^-1 sum(globTran l - globTran_pena aux + globTran_D u))
+ * (MCONTACT.h:2540-2576) while tc <= MULT_MAXI; globCoup is factorised by pivoted LU. */
+int ddpca_problem_set_coarse_latin(ddpca_problem_t p, const int64_t* doleMcsc, const int64_t* baseReco,
+                                   const ddpca_csr_t* globCoup, const ddpca_csr_t* globTran,
+                                   const ddpca_csr_t* globTran_pena, const ddpca_csr_t* globTran_D,
+                                   const ddpca_csr_t* accuProl);
 /* Check that every subdomain and interface was set; mark the problem established. */
 int ddpca_problem_finalize(ddpca_problem_t p);
 

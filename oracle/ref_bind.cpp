@@ -49,8 +49,8 @@ int main(int argc, char** argv) {
     if (argc < 3) { std::fprintf(stderr, "usage: ref_bind fric globLeve\n"); return 2; }
     MCONTACT mc;
     harness::twoblock_build(mc, std::stod(argv[1]), std::stol(argv[2]));
-    if (argc > 4 && std::stol(argv[4]) == 2) {  // interface-eliminated coarse space (BLOCK.h:38-41 setting)
-        mc.muscSett = 2;
+    if (argc > 4 && std::stol(argv[4]) != 0) {  // coarse space: 2 interface-eliminated (BLOCK.h:38-41), 1 LATIN
+        mc.muscSett = std::stol(argv[4]);
         mc.doleMcsc.assign(mc.multGrid.size(), 1);
     }
     std::string log;

@@ -151,6 +151,26 @@ inline ddpca_problem_t from_reference(MCONTACT& mc) {
         check(ddpca_problem_set_coarse_operators(p, 2, dole.data(), base.data(), &vc, mc.globForc_1.data(), vt.data(),
                                                  vd.data(), va.data()));
     }
+    if ((mc.muscSett >> 0) % 2 == 1) {                         // MULTISCALE (LATIN-type) output
+        std::vector<int64_t> dole(mc.doleMcsc.begin(), mc.doleMcsc.end());
+        std::vector<int64_t> base(mc.baseReco.begin(), mc.baseReco.end());
+        std::vector<Csr> gt, gp, gd, ap;
+        for (int64_t ts = 0; ts < nint; ++ts)
+            for (int s = 0; s < 2; ++s) {
+                gt.emplace_back(mc.globTran[ts][s]);
+                gp.emplace_back(mc.globTran_pena[ts][s]);
+                gd.emplace_back(SpMat(mc.globTran_D[ts][s] * mc.multGrid[mc.contBody[ts][s]].earlTran));
+            }
+        for (int64_t tv = 0; tv < nsub; ++tv) ap.emplace_back(mc.accuProl[tv]);
+        Csr gc(mc.globCoup);
+        std::vector<ddpca_csr_t> vt, vp, vd, va;
+        for (const auto& o : gt) vt.push_back(o.view());
+        for (const auto& o : gp) vp.push_back(o.view());
+        for (const auto& o : gd) vd.push_back(o.view());
+        for (const auto& o : ap) va.push_back(o.view());
+        const ddpca_csr_t vc = gc.view();
+        check(ddpca_problem_set_coarse_latin(p, dole.data(), base.data(), &vc, vt.data(), vp.data(), vd.data(), va.data()));
+    }
     check(ddpca_problem_finalize(p));
     return p;
 }

@@ -19,7 +19,9 @@
 //       built from the reference's MULTIGRID/CSEARCH/CURVEDS/MCONTACT API.
 //   With muscSett = 2 (interface-eliminated coarse space, MCONTACT.h:1672-2301) doleMcsc = 1
 //   for every subdomain (the examples' setting, e.g. BLOCK.h:38-41, DEHW.h:2222, 2239) and the
-//   coarse operators globCoup_1 / globForc_1 / globTran_1 / globTran_D_1 / accuProl are dumped.
+//   coarse operators globCoup_1 / globForc_1 / globTran_1 / globTran_D_1 / accuProl are dumped;
+//   with muscSett = 1 (LATIN-type, MULTISCALE, MCONTACT.h:898-1536; CYLINDER.h:42) likewise
+//   globCoup / globTran / globTran_pena / globTran_D / accuProl.
 //   time_cg d0 d1 d2 globLeve reps
 //       wall time of MGPIS::CG_SOLV(1) on the BEAM mesh (CPU baseline calibration).
 #include "examples/BEAM.h"
@@ -293,6 +295,21 @@ void dump_mcontact(MCONTACT& mc, const std::string& moni_path) {
         for (long ts = 0; ts < nint; ++ts)
             for (int s = 0; s < 2; ++s)
                 save_csr("if" + std::to_string(ts) + "_s" + std::to_string(s) + "_globTran_1", mc.globTran_1[ts][s]);
+    }
+    if ((mc.muscSett >> 0) % 2 == 1) {  // LATIN-type coarse space (MULTISCALE, MCONTACT.h:898-1536)
+        save_csr("globCoup", mc.globCoup);
+        std::vector<int64_t> base(mc.baseReco.begin(), mc.baseReco.end());
+        save_ivec("baseReco", base);
+        std::vector<int64_t> dole(mc.doleMcsc.begin(), mc.doleMcsc.end());
+        save_ivec("doleMcsc", dole);
+        for (long tv = 0; tv < nsub; ++tv) save_csr("sd" + std::to_string(tv) + "_accuProl", mc.accuProl[tv]);
+        for (long ts = 0; ts < nint; ++ts)
+            for (int s = 0; s < 2; ++s) {
+                const std::string ps = "if" + std::to_string(ts) + "_s" + std::to_string(s) + "_";
+                save_csr(ps + "globTran", mc.globTran[ts][s]);
+                save_csr(ps + "globTran_pena", mc.globTran_pena[ts][s]);
+                save_csr(ps + "globTran_D", mc.globTran_D[ts][s]);
+            }
     }
     save_ivec("muscSett", {mc.muscSett});
     // resuMoni.txt (MCONTACT.h:2742-2836): one row per ADMM iteration

@@ -47,6 +47,8 @@ CASE_PARAMS = {
     "beam_dd_m2": ("beam", 4, 2, 2, 2, 2, 1, 1),
     "twoblock_f0_m2": ("twoblock", 0.0, 2),
     "twoblock_f3_m2": ("twoblock", 0.3, 2),
+    "twoblock_f0_m1": ("twoblock", 0.0, 2),
+    "twoblock_f3_m1": ("twoblock", 0.3, 2),
 }
 
 

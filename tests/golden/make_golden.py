@@ -38,6 +38,9 @@ CASES = {
     "beam_dd_m2": ["beam_dd", "4", "2", "2", "2", "2", "1", "1", "{out}", "2"],
     "twoblock_f0_m2": ["twoblock", "0", "2", "{out}", "2"],
     "twoblock_f3_m2": ["twoblock", "0.3", "2", "{out}", "2"],
+    # LATIN-type coarse space (muscSett = 1, MULTISCALE, MCONTACT.h:898-1536 / 2540-2576)
+    "twoblock_f0_m1": ["twoblock", "0", "2", "{out}", "1"],
+    "twoblock_f3_m1": ["twoblock", "0.3", "2", "{out}", "1"],
 }
 
 

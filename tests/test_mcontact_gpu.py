@@ -124,11 +124,12 @@ def test_admm_matches_oracle_on_generated_problem(ddpca, oracle, gpu, smoother, 
     assert ok, worst
 
 
-@pytest.mark.parametrize("case", ["twoblock_f0", "twoblock_f3", "twoblock_f0_m2", "twoblock_f3_m2", "beam_dd_m2"])
+@pytest.mark.parametrize("case", ["twoblock_f0", "twoblock_f3", "twoblock_f0_m2", "twoblock_f3_m2", "beam_dd_m2",
+                                  "twoblock_f0_m1", "twoblock_f3_m1"])
 def test_admm_on_reference_operators_via_builder(ddpca, gpu, case):
     """Drop-in path: the reference's OWN ESTABLISH output from the fixture -- fine stiffness
     consStif[L], consForc, inpoNgap and all seven interface operators per side, and for the *_m2
-    cases its MULTISCALE_1 coarse operators -- handed over through the operator-level builder
+    / *_m1 cases its MULTISCALE_1 / MULTISCALE (LATIN) coarse operators -- handed over through the operator-level builder
     (coarse levels as Galerkin products with the stencils, which equal the reference's realProl
     entrywise).  Same bar as the native path."""
     from conftest import ref_csr
@@ -156,10 +157,10 @@ def test_admm_on_reference_operators_via_builder(ddpca, gpu, case):
         for side in range(2):
             for n in ddpca.Problem.IFACE_OPS:
                 f["ops"][side][n] = ref_csr(g, f"if{ts}_s{side}_{n}")
-    coarse = None
-    if "globCoup_1_val" in g.files:  # the reference's own MULTISCALE_1 output (assembled coarse space)
-        from oracle.oracle import coarse_from_golden
-        coarse = coarse_from_golden(g)
+    # the reference's own MULTISCALE_1 (*_m2) or MULTISCALE (*_m1, LATIN-type) output
+    from oracle.oracle import coarse_from_golden
+    coarse = coarse_from_golden(g)
+    if coarse is not None:
         coarse["doleMcsc"] = g["doleMcsc"]
     Q = ddpca.Problem.from_operators(subs, ifaces, coarse=coarse)
     mc = ddpca.MCONTACT(Q)
@@ -215,12 +216,12 @@ def _oracle_problem(P):
     return subs, ifaces
 
 
-@pytest.mark.parametrize("fric,musc", [("0", "0"), ("0.3", "0"), ("0", "2"), ("0.3", "2")])
+@pytest.mark.parametrize("fric,musc", [("0", "0"), ("0.3", "0"), ("0", "2"), ("0.3", "2"), ("0", "1"), ("0.3", "1")])
 def test_reference_binding_end_to_end(gpu, fric, musc):
     """The reference's own classes build and ESTABLISH the two-block problem, oracle/ref_bind.hpp
     hands it to the C ABI, the device loop runs, and the result is compared in the same process
-    with the reference's own CONTACT_ANALYSIS (iterations +-1, resuDisp 1e-6).  musc = 2: with
-    the reference's MULTISCALE_1 coarse space (globLeve 2, doleMcsc 1)."""
+    with the reference's own CONTACT_ANALYSIS (iterations +-1, resuDisp 1e-6).  musc = 2 / 1: with
+    the reference's MULTISCALE_1 / MULTISCALE (LATIN) coarse space (globLeve 2, doleMcsc 1)."""
     import json
     import subprocess
     from pathlib import Path
