@@ -87,6 +87,10 @@ def _declare(L: C.CDLL) -> None:
     L.mgpis_gpu_create_bsr3.argtypes = [C.c_int, C.c_int, _P, _P, _P, _P, _P, _P, _P, _P,
                                         C.POINTER(MgpisOptions), C.POINTER(_P)]
     L.mgpis_gpu_solve.argtypes = [_P, _P, _P, C.c_int, C.c_double, C.c_int64, _I64P, _DP]
+    L.mgpis_gpu_mult_solve.argtypes = [_P, _P, _P, C.c_int64, _I64P, _DP]
+    L.mgpis_gpu_bicgstab.argtypes = [_P, _P, _P, C.c_int, C.c_double, C.c_int64, _I64P, _DP,
+                                     C.POINTER(C.c_int)]
+    L.mgpis_gpu_gmres.argtypes = [_P, _P, _P, C.c_int, C.c_double, C.c_int64, C.c_int64, _I64P, _DP]
     L.mgpis_gpu_spmv.argtypes = [_P, C.c_int, _P, _P]
     L.mgpis_gpu_vcycle.argtypes = [_P, _P, _P]
     L.mgpis_gpu_info.argtypes = [_P, _I64P]
@@ -437,6 +441,34 @@ class MGPIS:
         rr = C.c_double()
         _check(lib().mgpis_gpu_solve(self._h, _ptr(b), _ptr(x), precSwit, rtol, len(b) if maxit is None else maxit,
                                      C.byref(it), C.byref(rr)))
+        return x, it.value, rr.value
+
+    def MULT_SOLV(self, totaForc: np.ndarray, maxit: int = 10000):
+        """MGPIS::MULT_SOLV (MGPIS.h:130-160) -> (x, iterNumb at exit, ||b - Kx|| / ||b||)."""
+        b = np.ascontiguousarray(totaForc, dtype=np.float64)
+        x = np.zeros_like(b)
+        it, rr = C.c_int64(), C.c_double()
+        _check(lib().mgpis_gpu_mult_solve(self._h, _ptr(b), _ptr(x), maxit, C.byref(it), C.byref(rr)))
+        return x, it.value, rr.value
+
+    def BiCGSTAB_SOLV(self, precSwit: int, totaForc: np.ndarray, rtol: float = 1e-14,
+                      maxit: Optional[int] = None):
+        """MGPIS::BiCGSTAB_SOLV (MGPIS.h:350-432) -> (x, iterNumb, recursive ||r|| / ||b||, breakdown)."""
+        b = np.ascontiguousarray(totaForc, dtype=np.float64)
+        x = np.zeros_like(b)
+        it, rr, bd = C.c_int64(), C.c_double(), C.c_int()
+        _check(lib().mgpis_gpu_bicgstab(self._h, _ptr(b), _ptr(x), precSwit, rtol,
+                                        len(b) if maxit is None else maxit, C.byref(it), C.byref(rr), C.byref(bd)))
+        return x, it.value, rr.value, bool(bd.value)
+
+    def GMRES_SOLV(self, precSwit: int, totaForc: np.ndarray, rtol: float = 1e-12, maxit: Optional[int] = None,
+                   restart: int = 10):
+        """MGPIS::GMRES_SOLV (MGPIS.h:228-348) -> (x, iterNumb, true ||b - Kx|| / ||b||)."""
+        b = np.ascontiguousarray(totaForc, dtype=np.float64)
+        x = np.zeros_like(b)
+        it, rr = C.c_int64(), C.c_double()
+        _check(lib().mgpis_gpu_gmres(self._h, _ptr(b), _ptr(x), precSwit, rtol, len(b) if maxit is None else maxit,
+                                     restart, C.byref(it), C.byref(rr)))
         return x, it.value, rr.value
 
     def MULT_VCYC(self, r: np.ndarray) -> np.ndarray:

@@ -152,6 +152,56 @@ int mgpis_gpu_solve(mgpis_t h, const double* b, double* x, int prec, double rtol
     return (maxit > 0 && it >= maxit) ? (int)std::min<int64_t>(it, 1 << 30) : 0;
 }
 
+}  // extern "C"
+namespace {
+// Shared shell of the non-CG drivers: condensed host b -> device nodal layout, run, gather x.
+template <typename F>
+int run_driver(mgpis_t h, const double* b, double* x, int64_t maxit, int64_t* iters, F body) {
+    int64_t it = 0;
+    int rc = guarded([&] {
+        if (!h || !b || !x) throw ApiError(DDPCA_EINVAL, "null argument");
+        if (maxit < 0) throw ApiError(DDPCA_EINVAL, "maxit must be >= 0");
+        MgpisDevice& D = *h->dev;
+        if (D.nsub != 1) throw ApiError(DDPCA_EINVAL, "driver needs a one-subdomain handle");
+        select_device(D.device);
+        DevBuf<double> tmp;
+        tmp.upload(b, D.nfree[0]);
+        D.bs.zero(D.stream);
+        D.scatter_free(0, tmp.p, D.bs.p);
+        it = body(D, D.bs.p, D.xs.p);
+        D.gather_free(0, D.xs.p, tmp.p);
+        DDPCA_HIP(hipMemcpyAsync(x, tmp.p, D.nfree[0] * sizeof(double), hipMemcpyDeviceToHost, D.stream));
+        DDPCA_HIP(hipStreamSynchronize(D.stream));
+        if (iters) *iters = it;
+    });
+    if (rc != 0) return rc;
+    return (maxit > 0 && it >= maxit) ? (int)std::min<int64_t>(it, 1 << 30) : 0;
+}
+}  // namespace
+extern "C" {
+
+int mgpis_gpu_mult_solve(mgpis_t h, const double* b, double* x, int64_t maxit, int64_t* iters, double* relres) {
+    return run_driver(h, b, x, maxit, iters, [&](MgpisDevice& D, const double* bd, double* xd) {
+        return krylov_mult_solv(D, bd, xd, maxit, relres);
+    });
+}
+
+int mgpis_gpu_bicgstab(mgpis_t h, const double* b, double* x, int prec, double rtol, int64_t maxit, int64_t* iters,
+                       double* relres, int* breakdown) {
+    if (prec != 0 && prec != 1) return guarded([] { throw ApiError(DDPCA_EINVAL, "prec must be 0 or 1"); });
+    return run_driver(h, b, x, maxit, iters, [&](MgpisDevice& D, const double* bd, double* xd) {
+        return krylov_bicgstab(D, prec, bd, xd, rtol, maxit, relres, breakdown);
+    });
+}
+
+int mgpis_gpu_gmres(mgpis_t h, const double* b, double* x, int prec, double rtol, int64_t maxit, int64_t restart,
+                    int64_t* iters, double* relres) {
+    if (prec != 0 && prec != 1) return guarded([] { throw ApiError(DDPCA_EINVAL, "prec must be 0 or 1"); });
+    return run_driver(h, b, x, maxit, iters, [&](MgpisDevice& D, const double* bd, double* xd) {
+        return krylov_gmres(D, prec, bd, xd, rtol, maxit, restart, relres);
+    });
+}
+
 int mgpis_gpu_spmv(mgpis_t h, int level, const double* x, double* y) {
     return guarded([&] {
         MgpisDevice& D = *h->dev;

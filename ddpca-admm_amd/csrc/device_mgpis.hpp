@@ -181,4 +181,12 @@ private:
     void estimate_lmax(int level);
 };
 
+// The other drivers of the MGPIS class surface (device_krylov.hip), on member 0 of a one-member
+// batch; b, x: device vectors in the fine level's batch nodal layout.  Return iterNumb at exit.
+int64_t krylov_mult_solv(MgpisDevice& D, const double* b, double* x, int64_t maxit, double* relres);
+int64_t krylov_bicgstab(MgpisDevice& D, int prec, const double* b, double* x, double rtol, int64_t maxit,
+                        double* relres, int* breakdown);
+int64_t krylov_gmres(MgpisDevice& D, int prec, const double* b, double* x, double rtol, int64_t maxit, int64_t restart,
+                     double* relres);
+
 }  // namespace ddpca

@@ -98,6 +98,29 @@ int mgpis_gpu_create_bsr3(int device, int nlev, const int64_t* nnodes,
 int mgpis_gpu_solve(mgpis_t h, const double* b, double* x, int prec, double rtol,
                     int64_t maxit, int64_t* iters, double* relres);
 
+/* Replaces MGPIS::MULT_SOLV(totaForc, resuSolu) (MGPIS.h:130-160): x0 = 0, repeated V-cycles
+ * x <- MULT_VCYC(b, x) until the last five residual norms ||b - Kx|| oscillate by less than 0.1
+ * of their median (VECT_MEDI_OSCI, PREP.h:147-153), or maxit V-cycles (reference 10000).
+ * iters = the reference's iterNumb at exit (the value it prints); relres = ||b - Kx|| / ||b||.
+ * The cycle is the handle's (options): a stagnation rule returns the accuracy the cycle's
+ * contraction allows -- use nu >= 2 (block-Jacobi V(2,2) matches SGS V(1,1), tests).
+ * Returns 0, or maxit (> 0) when the cap was hit. */
+int mgpis_gpu_mult_solve(mgpis_t h, const double* b, double* x, int64_t maxit, int64_t* iters, double* relres);
+/* Replaces MGPIS::BiCGSTAB_SOLV(precSwit, totaForc, resuSolu) (MGPIS.h:350-432): right-
+ * preconditioned BiCGSTAB, x0 = 0, shadow residual b, stop on the recursive residual
+ * ||r|| <= rtol ||b|| (reference 1e-14) or maxit (reference = rows).  *breakdown (may be NULL)
+ * = 1 when rho = 0 ended the run (the reference's "ERROR 1" exit, MGPIS.h:386-389) -- like the
+ * reference, x is then returned as it stands.  Returns 0, maxit on the cap, DDPCA_ENUMERIC on
+ * NaN/Inf. */
+int mgpis_gpu_bicgstab(mgpis_t h, const double* b, double* x, int prec, double rtol, int64_t maxit,
+                       int64_t* iters, double* relres, int* breakdown);
+/* Replaces MGPIS::GMRES_SOLV(precSwit, totaForc, resuSolu) (MGPIS.h:228-348): left-preconditioned
+ * GMRES(restart) (reference restart = iterStag = 10, rtol = 1e-12, maxit = rows), classical
+ * Gram-Schmidt Arnoldi; stop on the true residual: <= rtol ||b||, or <= 100 rtol ||b|| with the
+ * last `restart` residuals oscillating by less than 0.1 of their median.  restart in [1, 24].
+ * iters = iterNumb at exit; relres = ||b - Kx|| / ||b||.  Returns 0, or maxit on the cap. */
+int mgpis_gpu_gmres(mgpis_t h, const double* b, double* x, int prec, double rtol, int64_t maxit,
+                    int64_t restart, int64_t* iters, double* relres);
 /* y = consStif[level] * x (condensed host vectors), for parity tests of the SpMV kernel. */
 int mgpis_gpu_spmv(mgpis_t h, int level, const double* x, double* y);
 /* z = M^-1 r: one V-cycle from zero (MGPIS::MULT_VCYC, MGPIS.h:55-128) on condensed vectors. */

@@ -6,6 +6,10 @@
 // V-cycle application (vcycle_z), CG_SOLV(1) / CG_SOLV(0) solutions and iteration counts.
 //   orc_mult_vcyc   MGPIS::MULT_VCYC  MGPIS.h:55-128  (symmetric Gauss-Seidel V(1,1))
 //   orc_cg_solv     MGPIS::CG_SOLV    MGPIS.h:163-225 (x0 = 0, rtol on the recursive residual)
+//   orc_mult_solv   MGPIS::MULT_SOLV  MGPIS.h:130-160 (V-cycles from x, 5-residual stagnation stop)
+//   orc_bicgstab    MGPIS::BiCGSTAB_SOLV MGPIS.h:350-432
+//   orc_gmres       MGPIS::GMRES_SOLV MGPIS.h:228-348 (left-preconditioned GMRES(10), classical
+//                   Gram-Schmidt Arnoldi, Gram-Schmidt QR of the Hessenberg, true-residual stop)
 // The coarse solve is a dense Cholesky (the reference's SimplicialLDLT, PREP.h:107, agrees to
 // rounding).  SpMV is OpenMP-parallel over rows like Eigen's row-major product
 // (SparseDenseProduct.h:47-57); the SGS sweeps are sequential as in the reference.
@@ -231,6 +235,204 @@ int64_t orc_cg_solv(void* h, int prec, const double* b, double* xout, double rto
     }
     std::copy(x.begin(), x.end(), xout);
     if (relres) *relres = bn > 0 ? std::sqrt(dot(r, r)) / bn : 0.0;
+    return it;
+}
+
+// shared by the three drivers below
+static void orc_precond(const Mgpis& M, int prec, const std::vector<double>& r, std::vector<double>& z) {
+    const int L = (int)M.lev.size() - 1;
+    const Level& F = M.lev[L];
+    if (prec == 0)
+        for (size_t i = 0; i < r.size(); ++i) z[i] = (1.0 / F.D[i]) * r[i];
+    else {
+        std::fill(z.begin(), z.end(), 0.0);
+        M.vcycle(L, r.data(), z);
+    }
+}
+
+// VECT_MEDI_OSCI (PREP.h:147-153): median := (max + min) / 2, oscillation := max - min
+static void medi_osci(const std::vector<double>& v, double& medi, double& osci) {
+    const double mx = *std::max_element(v.begin(), v.end()), mn = *std::min_element(v.begin(), v.end());
+    medi = (mx + mn) / 2.0;
+    osci = mx - mn;
+}
+
+// MGPIS::MULT_SOLV (MGPIS.h:130-160): x0 = 0, repeated V-cycles on (b, x) until the last five
+// residual norms oscillate by less than 0.1 of their median.  Returns iterNumb at exit.
+int64_t orc_mult_solv(void* h, const double* b, double* xout, int64_t maxit, double* relres) {
+    const Mgpis& M = *static_cast<Mgpis*>(h);
+    const int L = (int)M.lev.size() - 1;
+    const Level& F = M.lev[L];
+    const int64_t n = F.K.n;
+    std::vector<double> x(n, 0.0), kx(n), r(n), moni(5, 0.0);
+    int64_t it = 0;
+    double rn = 0.0;
+    while (it < maxit) {
+        M.vcycle(L, b, x);
+        F.K.spmv(x.data(), kx.data());
+        for (int64_t i = 0; i < n; ++i) r[i] = b[i] - kx[i];
+        rn = std::sqrt(dot(r, r));
+        moni[it % 5] = rn;
+        if (it >= 4) {
+            double medi, osci;
+            medi_osci(moni, medi, osci);
+            if (osci < 0.1 * medi) break;
+        }
+        ++it;
+    }
+    std::copy(x.begin(), x.end(), xout);
+    double bn = 0.0;
+    for (int64_t i = 0; i < n; ++i) bn += b[i] * b[i];
+    if (relres) *relres = bn > 0 ? rn / std::sqrt(bn) : 0.0;
+    return it;
+}
+
+// MGPIS::BiCGSTAB_SOLV (MGPIS.h:350-432): right-preconditioned BiCGSTAB, x0 = 0, shadow residual
+// = r0, stop on the recursive residual.  Returns iterNumb at exit.
+int64_t orc_bicgstab(void* h, int prec, const double* b, double* xout, double rtol, int64_t maxit, double* relres,
+                     int* breakdown) {
+    const Mgpis& M = *static_cast<Mgpis*>(h);
+    const Level& F = M.lev.back();
+    const int64_t n = F.K.n;
+    std::vector<double> x(n, 0.0), r(b, b + n), rh(b, b + n), p(n, 0.0), v(n, 0.0), ph(n), s(n), sh(n), t(n);
+    const double tol = rtol * std::sqrt(dot(r, r));
+    double rho[2] = {0.0, 0.0}, alph = 0.0, omeg = 0.0;
+    int64_t it = 0;
+    if (breakdown) *breakdown = 0;
+    while (it < maxit && std::sqrt(dot(r, r)) > tol) {
+        double& rc = rho[(it + 1) % 2];
+        rc = dot(rh, r);
+        if (std::fabs(rc) == 0.0) {  // the reference's "ERROR 1" exit (MGPIS.h:386-389)
+            if (breakdown) *breakdown = 1;
+            break;
+        }
+        if (it == 0)
+            p = r;
+        else {
+            const double beta = (rc / rho[it % 2]) * (alph / omeg);
+            for (int64_t i = 0; i < n; ++i) p[i] = r[i] + beta * (p[i] - omeg * v[i]);
+        }
+        orc_precond(M, prec, p, ph);
+        F.K.spmv(ph.data(), v.data());
+        alph = rc / dot(rh, v);
+        for (int64_t i = 0; i < n; ++i) s[i] = r[i] - alph * v[i];
+        if (std::sqrt(dot(s, s)) <= 0.0) {
+            for (int64_t i = 0; i < n; ++i) x[i] += alph * ph[i];
+            break;
+        }
+        orc_precond(M, prec, s, sh);
+        F.K.spmv(sh.data(), t.data());
+        omeg = dot(t, s) / dot(t, t);
+        for (int64_t i = 0; i < n; ++i) {
+            x[i] += alph * ph[i] + omeg * sh[i];
+            r[i] = s[i] - omeg * t[i];
+        }
+        ++it;
+    }
+    std::copy(x.begin(), x.end(), xout);
+    const double bn = std::sqrt(dot(rh, rh));
+    if (relres) *relres = bn > 0 ? std::sqrt(dot(r, r)) / bn : 0.0;
+    return it;
+}
+
+// MGPIS::GMRES_SOLV (MGPIS.h:228-348): GMRES(restart) on M^-1 K, x0 = 0.  Per restart cycle the
+// basis starts at M^-1 (b - K x0) / ||.||; each step appends one Arnoldi vector (one classical
+// Gram-Schmidt pass), extends the Gram-Schmidt QR of the Hessenberg by one column, solves
+// R y = ||M^-1 r0|| Q(0,:)^T and forms x = x0 + V y; the stop test is on the true residual
+// ||b - K x|| over a window of `restart` values: <= tol, or <= 100 tol with an oscillation below
+// 0.1 of the median.  Returns iterNumb at exit.
+int64_t orc_gmres(void* h, int prec, const double* b, double* xout, double rtol, int64_t maxit, int64_t restart,
+                  double* relres) {
+    const Mgpis& M = *static_cast<Mgpis*>(h);
+    const Level& F = M.lev.back();
+    const int64_t n = F.K.n;
+    const int64_t m = restart;
+    std::vector<double> x(n, 0.0), x0(n), r(n), pr(n), kv(n), pv(n), kx(n), moni(m, 0.0);
+    std::vector<std::vector<double>> V;
+    std::vector<double> H, Q, R;  // column-major, leading dimension m + 1
+    const int64_t ld = m + 1;
+    double bn = 0.0;
+    for (int64_t i = 0; i < n; ++i) bn += b[i] * b[i];
+    bn = std::sqrt(bn);
+    const double tol = rtol * bn;
+    double nr0 = 0.0, rn = 0.0;
+    int64_t it = 0;
+    while (it < maxit) {
+        const int64_t j = it % m;
+        if (j == 0) {
+            x0 = x;
+            F.K.spmv(x0.data(), kx.data());
+            for (int64_t i = 0; i < n; ++i) r[i] = b[i] - kx[i];
+            orc_precond(M, prec, r, pr);
+            nr0 = std::sqrt(dot(pr, pr));
+            V.assign(1, pr);
+            for (double& e : V[0]) e /= nr0;
+            H.assign(ld * m, 0.0);
+            Q.assign(ld * m, 0.0);
+            R.assign(ld * m, 0.0);
+        }
+        F.K.spmv(V[j].data(), kv.data());
+        orc_precond(M, prec, kv, pv);
+        std::vector<double> bi(j + 1);
+        for (int64_t k = 0; k <= j; ++k) bi[k] = dot(V[k], pv);
+        std::vector<double> q(pv);
+        for (int64_t i = 0; i < n; ++i) {
+            double s = 0.0;
+            for (int64_t k = 0; k <= j; ++k) s += V[k][i] * bi[k];
+            q[i] -= s;
+        }
+        const double nq = std::sqrt(dot(q, q));
+        for (int64_t k = 0; k <= j; ++k) H[j * ld + k] = bi[k];
+        H[j * ld + j + 1] = nq;
+        for (double& e : q) e /= nq;
+        V.push_back(q);
+        if (j == 0) {
+            const double hn = std::sqrt(H[0] * H[0] + H[1] * H[1]);
+            Q[0] = H[0] / hn;
+            Q[1] = H[1] / hn;
+            R[0] = hn;
+        } else {
+            // R(0:j, j) = Q(:, 0:j)^T H(:, j) over j + 2 rows (new row of Q is zero)
+            for (int64_t c = 0; c < j; ++c) {
+                double s = 0.0;
+                for (int64_t k = 0; k <= j + 1; ++k) s += Q[c * ld + k] * H[j * ld + k];
+                R[j * ld + c] = s;
+            }
+            double qq = 0.0;
+            for (int64_t k = 0; k <= j + 1; ++k) {
+                double s = 0.0;
+                for (int64_t c = 0; c < j; ++c) s += Q[c * ld + k] * R[j * ld + c];
+                Q[j * ld + k] = H[j * ld + k] - s;
+                qq += Q[j * ld + k] * Q[j * ld + k];
+            }
+            const double rjj = std::sqrt(qq);
+            R[j * ld + j] = rjj;
+            for (int64_t k = 0; k <= j + 1; ++k) Q[j * ld + k] /= rjj;
+        }
+        std::vector<double> y(j + 1, 0.0);
+        for (int64_t t = j; t >= 0; --t) {
+            double s = 0.0;
+            for (int64_t c = t + 1; c <= j; ++c) s += R[c * ld + t] * y[c];
+            y[t] = (nr0 * Q[t * ld + 0] - s) / R[t * ld + t];
+        }
+        for (int64_t i = 0; i < n; ++i) {
+            double s = 0.0;
+            for (int64_t k = 0; k <= j; ++k) s += V[k][i] * y[k];
+            x[i] = x0[i] + s;
+        }
+        F.K.spmv(x.data(), kx.data());
+        for (int64_t i = 0; i < n; ++i) r[i] = b[i] - kx[i];
+        rn = std::sqrt(dot(r, r));
+        moni[it % m] = rn;
+        if (it >= m - 1) {
+            double medi, osci;
+            medi_osci(moni, medi, osci);
+            if (rn <= tol || (rn <= 1e2 * tol && osci < 0.1 * medi)) break;
+        }
+        ++it;
+    }
+    std::copy(x.begin(), x.end(), xout);
+    if (relres) *relres = bn > 0 ? rn / bn : 0.0;
     return it;
 }
 

@@ -22,6 +22,8 @@
 //   coarse operators globCoup_1 / globForc_1 / globTran_1 / globTran_D_1 / accuProl are dumped;
 //   with muscSett = 1 (LATIN-type, MULTISCALE, MCONTACT.h:898-1536; CYLINDER.h:42) likewise
 //   globCoup / globTran / globTran_pena / globTran_D / accuProl.
+//   beam_solv d0 d1 d2 globLeve outdir
+//       the same BEAM -> MULT_SOLV, BiCGSTAB_SOLV(0/1), GMRES_SOLV(0/1) solutions.
 //   time_cg d0 d1 d2 globLeve reps
 //       wall time of MGPIS::CG_SOLV(1) on the BEAM mesh (CPU baseline calibration).
 #include "examples/BEAM.h"
@@ -219,6 +221,41 @@ int beam_nodd(long d0, long d1, long d2, long gl, bool full, bool do_cg) {
     }
     save_dvec("info", info);  // [t_setup, it_mg, t_mg, it_diag, t_diag, true_relres_mg]
     std::printf("beam_nodd n=%ld levels=%ld info:", (long)g.mgpi.consStif[L].rows(), L + 1);
+    for (double v : info) std::printf(" %.6g", v);
+    std::printf("\n");
+    return 0;
+}
+
+// The other drivers of the MGPIS class surface on the BEAM mesh: MULT_SOLV (MGPIS.h:130-160),
+// BiCGSTAB_SOLV(0/1) (MGPIS.h:350-432), GMRES_SOLV(0/1) (MGPIS.h:228-348).  Saves each solution,
+// the last "#Iteration" value each printed and the true relative residual.
+int beam_solv(long d0, long d1, long d2, long gl) {
+    BEAM beam(0);
+    beam.diviNumb = {d0, d1, d2};
+    beam.globLeve = gl;
+    { std::stringstream ss; auto* o = std::cout.rdbuf(ss.rdbuf()); beam.MESH_NODD(0); std::cout.rdbuf(o); }
+    MULTIGRID& g = beam.multGrid[0];
+    { std::stringstream ss; auto* o = std::cout.rdbuf(ss.rdbuf());
+      g.TRANSFER(); g.STIF_MATR(); g.CONSTRAINT(1); std::cout.rdbuf(o); }
+    const long L = g.mgpi.maxiLeve;
+    const Eigen::VectorXd& b = g.consForc;
+    std::vector<double> info;
+    auto run = [&](const char* name, auto fn) {
+        Eigen::VectorXd x;
+        long last = capture_iters([&] { fn(x); }) - 1;  // the printed value
+        save_vec(name, x);
+        Eigen::VectorXd r = b - g.mgpi.consStif[L] * x;
+        info.push_back((double)last);
+        info.push_back(r.norm() / b.norm());
+    };
+    run("x_mult", [&](Eigen::VectorXd& x) { g.mgpi.MULT_SOLV(b, x); });
+    run("x_bicg1", [&](Eigen::VectorXd& x) { g.mgpi.BiCGSTAB_SOLV(1, b, x); });
+    run("x_bicg0", [&](Eigen::VectorXd& x) { g.mgpi.BiCGSTAB_SOLV(0, b, x); });
+    run("x_gmres1", [&](Eigen::VectorXd& x) { g.mgpi.GMRES_SOLV(1, b, x); });
+    run("x_gmres0", [&](Eigen::VectorXd& x) { g.mgpi.GMRES_SOLV(0, b, x); });
+    save_vec("consForc", b);
+    save_dvec("solv_info", info);  // [printed iteration, true relres] per solver, order as above
+    std::printf("beam_solv n=%ld info:", (long)b.size());
     for (double v : info) std::printf(" %.6g", v);
     std::printf("\n");
     return 0;
@@ -527,6 +564,10 @@ int main(int argc, char** argv) {
         return twoblock(std::stod(argv[2]), L(3), argc >= 6 ? L(5) : 0);
     }
     if (mode == "time_cg" && argc >= 7) return time_cg(L(2), L(3), L(4), L(5), L(6));
+    if (mode == "beam_solv" && argc >= 7) {
+        g_out = argv[6];
+        return beam_solv(L(2), L(3), L(4), L(5));
+    }
     std::fprintf(stderr, "bad arguments\n");
     return 2;
 }

@@ -28,6 +28,8 @@ CASES = {
     "beam_s1": ["beam_nodd", "8", "2", "2", "1", "{out}", "1"],
     "beam_s2": ["beam_nodd", "8", "2", "2", "2", "{out}", "0"],
     "beam_gl1": ["beam_nodd", "64", "4", "2", "1", "{out}", "0"],
+    # the other MGPIS drivers (MULT_SOLV, BiCGSTAB_SOLV, GMRES_SOLV) on the beam_s2 mesh
+    "beam_s2_solv": ["beam_solv", "8", "2", "2", "2", "{out}"],
     # DD BEAM, 2 subdomains glued (fricCoef = -1), muscSett = 0: 3000 ADMM iterations
     "beam_dd": ["beam_dd", "8", "2", "2", "1", "2", "1", "1", "{out}"],
     # two stacked blocks: frictionless patch test and Coulomb friction (mu = 0.3)
