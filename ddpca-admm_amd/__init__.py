@@ -92,6 +92,9 @@ def _declare(L: C.CDLL) -> None:
                                      C.POINTER(C.c_int)]
     L.mgpis_gpu_gmres.argtypes = [_P, _P, _P, C.c_int, C.c_double, C.c_int64, C.c_int64, _I64P, _DP]
     L.mgpis_gpu_spmv.argtypes = [_P, C.c_int, _P, _P]
+    L.ddpca_write_resuDisp.argtypes = [C.c_char_p, _P, C.c_int64, C.c_int64, _P, _P]
+    L.ddpca_write_resuCont.argtypes = [C.c_char_p, C.c_double, C.c_int64, _P, _P, _P]
+    L.ddpca_write_resuMoni.argtypes = [C.c_char_p, _P, C.c_int64, C.c_int64]
     L.mgpis_gpu_vcycle.argtypes = [_P, _P, _P]
     L.mgpis_gpu_info.argtypes = [_P, _I64P]
     L.mgpis_gpu_bench_spmv.argtypes = [_P, C.c_int, C.c_int, _DP, _DP]
@@ -486,6 +489,26 @@ class MGPIS:
 
 
 # ============================================================================ device MCONTACT
+def write_resuDisp(path: str, disp: np.ndarray, rot_node=None, rot=None) -> None:
+    d = np.ascontiguousarray(disp, dtype=np.float64)
+    rn = np.ascontiguousarray([] if rot_node is None else rot_node, dtype=np.int64)
+    rm = np.ascontiguousarray(np.zeros((0, 9)) if rot is None else rot, dtype=np.float64).reshape(-1)
+    _check(lib().ddpca_write_resuDisp(str(path).encode(), _ptr(d), len(d) // 3, len(rn), _ptr(rn), _ptr(rm)))
+
+
+def write_resuCont(path: str, fric: float, gamma: np.ndarray, stat=None, basis=None) -> None:
+    g = np.ascontiguousarray(gamma, dtype=np.float64)
+    nip = len(g) if fric == 0.0 else len(g) // 3
+    st = np.ascontiguousarray(np.zeros(nip) if stat is None else stat, dtype=np.int32)
+    bs = np.ascontiguousarray(np.zeros(9 * nip) if basis is None else basis, dtype=np.float64).reshape(-1)
+    _check(lib().ddpca_write_resuCont(str(path).encode(), fric, nip, _ptr(g), _ptr(st), _ptr(bs)))
+
+
+def write_resuMoni(path: str, rows: np.ndarray) -> None:
+    r = np.ascontiguousarray(np.atleast_2d(rows), dtype=np.float64)
+    _check(lib().ddpca_write_resuMoni(str(path).encode(), _ptr(r), r.shape[0], r.shape[1]))
+
+
 class MCONTACT:
     """Device ADMM loop of MCONTACT::CONTACT_ANALYSIS (MCONTACT.h:2493-2845) for one rank."""
 
@@ -530,11 +553,27 @@ class MCONTACT:
 
     def get(self, what: str, index: int = 0) -> np.ndarray:
         n = _check(lib().mcontact_gpu_get(self._h, what.encode(), index, None, 0))
-        dtype = np.int64 if what in ("pcg_iters", "owned", "mass_iters") else np.float64
+        dtype = (np.int64 if what in ("pcg_iters", "owned", "mass_iters")
+                 else np.int32 if what == "fricStat" else np.float64)
         out = np.zeros(n, dtype)
         if n:
             _check(lib().mcontact_gpu_get(self._h, what.encode(), index, _ptr(out), n))
         return out
+
+    # ---- result files in the reference's formats (host writers, include/ddpca_amd.h)
+    def OUTP_SUB2(self, tv: int, path: str) -> None:
+        """resuDisp_<tv>.txt of an owned subdomain (MULTIGRID::OUTP_SUB2, MULTIGRID.h:1288-1307)."""
+        write_resuDisp(path, self.get("resuDisp", tv))
+
+    def OUTPUT_PRTR(self, ts: int, path: str) -> None:
+        """resuCont_<ts>.txt of an interface this rank handles (MCONTACT::OUTPUT_PRTR, MCONTACT.h:97-123)."""
+        fric = float(self.problem.array("iface_param", ts)[0])
+        write_resuCont(path, fric, self.get("inpoGamm", ts), self.get("fricStat", ts),
+                       self.problem.array("ip_basis", ts))
+
+    def write_resuMoni(self, path: str) -> None:
+        """resuMoni.txt (MCONTACT.h:2502, 2742-2836): every MONITOR row recorded so far."""
+        write_resuMoni(path, self.monitor())
 
     def timing(self) -> dict:
         out = (C.c_double * 10)()

@@ -1533,6 +1533,15 @@ int64_t mcontact_gpu_get(mcontact_t h, const char* what, int64_t index, void* ou
                 }
             throw ApiError(DDPCA_EINVAL, "interface not handled by this rank");
         }
+        if (w == "fricStat") {
+            for (auto& I : h->itfs)
+                if (I.ts == index && I.mine) {
+                    n = I.mip / I.comp;
+                    if (out) DDPCA_HIP(hipMemcpy(out, I.stat.p, std::min(n, cap) * sizeof(int32_t), hipMemcpyDeviceToHost));
+                    return;
+                }
+            throw ApiError(DDPCA_EINVAL, "interface not handled by this rank");
+        }
         if (w == "pcg_iters") {
             n = (int64_t)h->subs.size();
             if (out)

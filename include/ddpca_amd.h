@@ -264,6 +264,7 @@ int64_t mcontact_gpu_iterate(mcontact_t h, int64_t maxit, int check);
 int64_t mcontact_gpu_monitor(mcontact_t h, double* out, int64_t cap_rows);
 /* Copy state to host: what = "resuDisp" (index = subdomain, nodal 3N), "inteAuxi"/"inteLagr"
  * (index = 2*ts+side), "inpoGamm" (index = ts, projected gamma of the last iteration),
+ * "fricStat" (index = ts, int32 per integration point: 0 open, 1 slip, 2 stick, MCONTACT.h:2647-2666),
  * "pcg_iters" (int64 per owned subdomain, last iteration). */
 int64_t mcontact_gpu_get(mcontact_t h, const char* what, int64_t index, void* out, int64_t cap);
 /* Timing of the last iterate() call, summed over its iterations: [total_ms (host wall),
@@ -273,6 +274,25 @@ int64_t mcontact_gpu_get(mcontact_t h, const char* what, int64_t index, void* ou
  * spmv_bytes_per_launch (algorithmic), dof_iterations (sum n_free * PCG its), owned_dofs] */
 int mcontact_gpu_timing(mcontact_t h, double* out10);
 int mcontact_gpu_destroy(mcontact_t h);
+
+/* ========================================================================================
+ * Result files in the reference's text formats (host only; std::scientific, precision 20,
+ * width 30).  The reference rewrites resuDisp/resuCont on every ADMM iteration; a caller writes
+ * them from mcontact_gpu_get / mcontact_gpu_monitor output when it wants them.
+ * ======================================================================================== */
+/* MULTIGRID::OUTP_SUB2 (MULTIGRID.h:1288-1307): one line "ux uy uz" per node of the nodal
+ * displacement disp[3*nnodes]; the nrot nodes rot_node[k] (MULTIGRID::nodeRota) are rotated by
+ * rot[9k..9k+8] (row-major) first. */
+int ddpca_write_resuDisp(const char* path, const double* disp, int64_t nnodes, int64_t nrot,
+                         const int64_t* rot_node, const double* rot);
+/* MCONTACT::OUTPUT_PRTR (MCONTACT.h:97-123): fric == 0: one gamma_n per line; otherwise
+ * "gamma_n  (gamma_1 t1 + gamma_2 t2)[0..2]  fricStat" per integration point, with gamma the
+ * projected contact traction (3 per ip), stat the friction state (0 open, 1 slip, 2 stick;
+ * mcontact_gpu_get "fricStat") and basis 9 doubles per ip (n, t1, t2; INTEGRAL_POINT::basiVect). */
+int ddpca_write_resuCont(const char* path, double fric, int64_t nip, const double* gamma,
+                         const int32_t* stat, const double* basis);
+/* resuMoni.txt (MCONTACT.h:2502, 2742-2836): the rows of mcontact_gpu_monitor. */
+int ddpca_write_resuMoni(const char* path, const double* rows, int64_t nrows, int64_t ncols);
 
 #ifdef __cplusplus
 }

@@ -7,10 +7,12 @@ expected outputs of the reference), never reference source.
 
     python tests/golden/make_golden.py            # all cases
     python tests/golden/make_golden.py beam_s1    # one case
+    python tests/golden/make_golden.py --text     # the text-file fixtures (TEXT) only
 """
 from __future__ import annotations
 
 import glob
+import gzip
 import os
 import subprocess
 import sys
@@ -46,8 +48,18 @@ CASES = {
 }
 
 
-def run_case(name: str) -> Path:
+# text-file fixtures: the reference's own result files (MULTIGRID::OUTP_SUB2, MCONTACT::
+# OUTPUT_PRTR, resuMoni.txt) of a case, kept gzip'd under text/<case>/ -- data, for the writers'
+# format tests (tests/test_writers.py).  `make_golden.py --text <case>` writes only these.
+TEXT = {
+    "twoblock_f0_m2": ["resuMoni.txt", "resuDisp_0.txt", "resuDisp_1.txt", "resuCont_0.txt"],
+    "twoblock_f3_m2": ["resuMoni.txt", "resuCont_0.txt"],
+}
+
+
+def run_case(name: str, text_only: bool = False) -> Path:
     argv = CASES[name]
+    here = Path(__file__).resolve().parent
     with tempfile.TemporaryDirectory() as work:
         out = Path(work) / "npy"
         out.mkdir()
@@ -55,16 +67,25 @@ def run_case(name: str) -> Path:
         env = dict(os.environ, OMP_NUM_THREADS=os.environ.get("OMP_NUM_THREADS", "8"))
         subprocess.run(cmd, cwd=work, check=True, env=env)
         arrays = {Path(f).stem: np.load(f) for f in sorted(glob.glob(str(out / "*.npy")))}
-    dest = Path(__file__).resolve().parent / f"{name}.npz"
+        for fname in TEXT.get(name, []):
+            tdir = here / "text" / name
+            tdir.mkdir(parents=True, exist_ok=True)
+            with open(Path(work) / fname, "rb") as src, gzip.GzipFile(tdir / (fname + ".gz"), "wb", mtime=0) as dst:
+                dst.write(src.read())
+    if text_only:
+        return here / "text" / name
+    dest = here / f"{name}.npz"
     np.savez_compressed(dest, **arrays)
     return dest
 
 
 def main() -> None:
     subprocess.run(["make", "-C", str(ROOT / "oracle"), "ref"], check=True)
-    names = sys.argv[1:] or list(CASES)
+    args = sys.argv[1:]
+    text_only = "--text" in args
+    names = [a for a in args if a != "--text"] or (list(TEXT) if text_only else list(CASES))
     for n in names:
-        print("wrote", run_case(n))
+        print("wrote", run_case(n, text_only))
 
 
 if __name__ == "__main__":

@@ -101,6 +101,44 @@ def test_contact_pressure_matches_reference(ddpca, gpu, case):
         assert np.abs(trac - ref[:, 1:4]).max() <= 1e-5 * scale
 
 
+@pytest.mark.parametrize("case", ["twoblock_f0_m2", "twoblock_f3_m2"])
+def test_result_files_match_reference_files(ddpca, gpu, case, tmp_path):
+    """The device run's result files (MCONTACT.OUTP_SUB2 / OUTPUT_PRTR / write_resuMoni, the
+    reference's formats) against the reference's own files (tests/golden/text): same layout
+    line for line, values at the tolerances above (pressures 1e-5 on active points, tangential
+    traction 1e-5 of its scale, friction state equal where the slip margin exceeds 1e-6,
+    displacements 1e-6, resuMoni rows within 1e-7)."""
+    import gzip
+    from conftest import GOLDEN
+    g, P, mc, n = _run(ddpca, case)
+
+    def ref(name):
+        with gzip.open(GOLDEN / "text" / case / (name + ".gz"), "rt") as f:
+            return f.read()
+
+    mc.write_resuMoni(tmp_path / "resuMoni.txt")
+    mc.OUTPUT_PRTR(0, tmp_path / "resuCont_0.txt")
+    mine_m, ref_m = (tmp_path / "resuMoni.txt").read_text(), ref("resuMoni.txt")
+    assert [len(l) for l in mine_m.splitlines()][:1] == [len(l) for l in ref_m.splitlines()][:1]
+    ok, worst = _rows_close(np.loadtxt(tmp_path / "resuMoni.txt", ndmin=2), np.loadtxt(ref("resuMoni.txt").splitlines(), ndmin=2))
+    assert ok, worst
+    got = np.loadtxt(tmp_path / "resuCont_0.txt", ndmin=2)
+    exp = np.loadtxt(ref("resuCont_0.txt").splitlines(), ndmin=2)
+    assert got.shape == exp.shape
+    active = exp[:, 0] > 1e-3 * exp[:, 0].max()
+    assert np.all(np.abs(got[active, 0] - exp[active, 0]) <= 1e-5 * exp[active, 0])
+    if exp.shape[1] == 5:
+        assert np.abs(got[:, 1:4] - exp[:, 1:4]).max() <= 1e-5 * np.abs(exp[:, 1:4]).max()
+        fric = float(g["if0_param"][0])
+        margin = np.abs(np.linalg.norm(exp[:, 1:4], axis=1) - fric * exp[:, 0]) > 1e-6 * exp[:, 0].max()
+        assert np.array_equal(got[margin, 4], exp[margin, 4])
+    else:
+        for tv in range(P.nsub):
+            mc.OUTP_SUB2(tv, tmp_path / f"resuDisp_{tv}.txt")
+            d, dr = np.loadtxt(tmp_path / f"resuDisp_{tv}.txt"), np.loadtxt(ref(f"resuDisp_{tv}.txt").splitlines())
+            assert d.shape == dr.shape and np.linalg.norm(d - dr) <= 1e-6 * np.linalg.norm(dr)
+
+
 def test_patch_test_pressure(ddpca, gpu):
     """BLOCK-style patch test: uniform 1e7 Pa load gives a uniform contact pressure."""
     g, P, mc, n = _run(ddpca, "twoblock_f0")
