@@ -53,8 +53,9 @@ def parse():
     ap.add_argument("--iters-per-graph", type=int, default=4)
     ap.add_argument("--warm-start", type=int, default=0,
                     help="1: each subdomain PCG starts from its previous solution (same 1e-14 stop rule)")
-    ap.add_argument("--precond-fp32", type=int, default=1,
-                    help="1: V-cycle level operators stored in fp32 (arithmetic, Krylov operator and stop rule fp64)")
+    ap.add_argument("--precond-fp32", type=int, default=2,
+                    help="1: V-cycle level operators stored in fp32; 2: and the fine level's V-cycle copy in block-exponent fp16 "
+                         "(arithmetic, Krylov operator and stop rule fp64)")
     ap.add_argument("--table-mode", type=int, default=0,
                     help="1: keep one copy of bit-identical operator rows (pays on regular meshes only; the "
                          "synthetic box mesh is far more regular than DEHW's curved one, so the headline keeps 0)")
@@ -172,7 +173,7 @@ def main():
                 "mg_levels": a.gl + 1,
                 "smoother": {0: "jacobi", 1: "block-jacobi", 2: "chebyshev"}[a.smoother] + f"({a.nu})",
                 "pcg_x0": "previous solution" if a.warm_start else "zero",
-                "vcycle_operator_storage": "fp32" if a.precond_fp32 else "fp64",
+                "vcycle_operator_storage": {0: "fp64", 1: "fp32", 2: "fp32, fine level block-exponent fp16"}[a.precond_fp32],
                 "operator_rows": "deduplicated table" if a.table_mode else "streamed",
                 "coarse_space": f"interface-eliminated (muscSett={a.musc}, doleMcsc={a.dole})" if a.musc else "none",
                 "parallelism": f"dd{world}",

@@ -95,6 +95,30 @@ template <typename T>
 constexpr bool paired_values() { return DDPCA_PAIRED_VALUES != 0 && sizeof(T) == 8; }
 typedef double dbl2_t __attribute__((ext_vector_type(2)));
 
+// Block-exponent fp16 storage (T = uint16_t; precond_fp32 = 2, the fine level's V-cycle copy):
+// each 3x3 block is 2^e times nine fp16 values, e = the binary exponent of the block's largest
+// |entry| (so |values| < 1 and every entry within 2^14 of the block maximum keeps fp16's 11
+// significant bits); the record is ten halves, (v0,v1) (v2,v3) (v4,v5) (v6,v7) (v8,e), one
+// 256-B dword run per pair: a slot is 1280 B, 20 B per block against 36 B for fp32.  A block
+// and its transpose share e and round alike, so the operator stays exactly symmetric.
+template <typename T>
+constexpr int slot_vals() { return sizeof(T) == 2 ? 10 : 9; }
+
+__device__ __forceinline__ double h16_lo(uint32_t w) {
+    return (double)__builtin_bit_cast(_Float16, (uint16_t)(w & 0xFFFFu));
+}
+__device__ __forceinline__ double h16_hi(uint32_t w) { return (double)__builtin_bit_cast(_Float16, (uint16_t)(w >> 16)); }
+
+// host: one block (9 fp64 entries, row-major) -> the ten-half record
+inline void to_h16_block(const double* v, uint16_t* rec) {
+    double m = 0.0;
+    for (int k = 0; k < 9; ++k) m = std::max(m, std::fabs(v[k]));
+    int e = 0;
+    if (m > 0.0) std::frexp(m, &e);
+    for (int k = 0; k < 9; ++k) rec[k] = __builtin_bit_cast(uint16_t, (_Float16)std::ldexp(v[k], -e));
+    rec[9] = (uint16_t)(int16_t)e;
+}
+
 template <typename T>
 __host__ __device__ inline int64_t slot_elem(int ij, int64_t lane) {
     if (!paired_values<T>()) return (int64_t)ij * kChunk + lane;
@@ -107,7 +131,16 @@ template <bool NT, typename T>
 __device__ __forceinline__ void block_fma_any(const T* v, const double* xj, double& s0, double& s1, double& s2) {
     const double x0 = xj[0], x1 = xj[1], x2 = xj[2];
     auto ldv = [](const auto* p) { if constexpr (NT) return __builtin_nontemporal_load(p); else return *p; };
-    if constexpr (paired_values<T>() && sizeof(T) == 8) {
+    if constexpr (sizeof(T) == 2) {
+        // v = slot base + lane in halves; the lane's dword of pair p is at dword 64 p + lane
+        const int lane = threadIdx.x & 63;
+        const uint32_t* p = reinterpret_cast<const uint32_t*>(v - lane) + lane;
+        const uint32_t a = ldv(p), b = ldv(p + 64), c = ldv(p + 128), d = ldv(p + 192), e = ldv(p + 256);
+        const double sc = __builtin_amdgcn_ldexp(1.0, (int)(int16_t)(e >> 16));
+        s0 += sc * (h16_lo(a) * x0 + h16_hi(a) * x1 + h16_lo(b) * x2);
+        s1 += sc * (h16_hi(b) * x0 + h16_lo(c) * x1 + h16_hi(c) * x2);
+        s2 += sc * (h16_lo(d) * x0 + h16_hi(d) * x1 + h16_lo(e) * x2);
+    } else if constexpr (paired_values<T>() && sizeof(T) == 8) {
         const int lane = threadIdx.x & 63;
         const dbl2_t* p = reinterpret_cast<const dbl2_t*>(v - lane) + lane;
         const dbl2_t a = ldv(p), b = ldv(p + 64), c = ldv(p + 128), d = ldv(p + 192);
@@ -144,11 +177,11 @@ __device__ __forceinline__ void sell_rows(const int32_t* colp, const T* valp, co
     if constexpr (V == 0) {
 #pragma unroll 3
         for (int k = 0; k < ns; ++k)
-            block_fma_plain(valp + (int64_t)k * 9 * kChunk, x + 3 * (int64_t)colp[(int64_t)k * kChunk], s0, s1, s2);
+            block_fma_plain(valp + (int64_t)k * slot_vals<T>() * kChunk, x + 3 * (int64_t)colp[(int64_t)k * kChunk], s0, s1, s2);
     } else if constexpr (V == 1) {
 #pragma unroll 3
         for (int k = 0; k < ns; ++k)
-            block_fma(valp + (int64_t)k * 9 * kChunk, x + 3 * (int64_t)__builtin_nontemporal_load(colp + (int64_t)k * kChunk),
+            block_fma(valp + (int64_t)k * slot_vals<T>() * kChunk, x + 3 * (int64_t)__builtin_nontemporal_load(colp + (int64_t)k * kChunk),
                       s0, s1, s2);
     } else if constexpr (V == 3) {
         // diagnostic bound only (wrong product): as 1 but x gathered at the row's own node, i.e.
@@ -156,7 +189,7 @@ __device__ __forceinline__ void sell_rows(const int32_t* colp, const T* valp, co
 #pragma unroll 3
         for (int k = 0; k < ns; ++k) {
             const int32_t j = __builtin_nontemporal_load(colp + (int64_t)k * kChunk);
-            block_fma(valp + (int64_t)k * 9 * kChunk, x + 3 * (row + (j & 0)), s0, s1, s2);
+            block_fma(valp + (int64_t)k * slot_vals<T>() * kChunk, x + 3 * (row + (j & 0)), s0, s1, s2);
         }
     } else {
         int k = 0;
@@ -173,12 +206,12 @@ __device__ __forceinline__ void sell_rows(const int32_t* colp, const T* valp, co
                 c1 = __builtin_nontemporal_load(colp + (int64_t)(k + 4) * kChunk);
                 c2 = __builtin_nontemporal_load(colp + (int64_t)(k + 5) * kChunk);
             }
-            const T* v = valp + (int64_t)k * 9 * kChunk;
+            const T* v = valp + (int64_t)k * slot_vals<T>() * kChunk;
             block_fma(v, x + 3 * j0, s0, s1, s2);
-            block_fma(v + 9 * kChunk, x + 3 * j1, s0, s1, s2);
-            block_fma(v + 18 * kChunk, x + 3 * j2, s0, s1, s2);
+            block_fma(v + slot_vals<T>() * kChunk, x + 3 * j1, s0, s1, s2);
+            block_fma(v + 2 * slot_vals<T>() * kChunk, x + 3 * j2, s0, s1, s2);
         }
-        for (; k < ns; ++k) block_fma(valp + (int64_t)k * 9 * kChunk, x + 3 * (int64_t)colp[(int64_t)k * kChunk], s0, s1, s2);
+        for (; k < ns; ++k) block_fma(valp + (int64_t)k * slot_vals<T>() * kChunk, x + 3 * (int64_t)colp[(int64_t)k * kChunk], s0, s1, s2);
     }
 }
 
@@ -281,7 +314,7 @@ __global__ __launch_bounds__(kBlock) void k_sell(SellArgs a, const double* __res
         else
             sell_rows_tbl(a.col + base * kChunk + lane, tab + (int64_t)a.rtype[row] * a.tstride, a.x, ns, s0, s1, s2);
     } else
-        sell_rows<V>(a.col + base * kChunk + lane, static_cast<const T*>(a.val) + base * 9 * kChunk + lane, a.x, ns,
+        sell_rows<V>(a.col + base * kChunk + lane, static_cast<const T*>(a.val) + base * slot_vals<T>() * kChunk + lane, a.x, ns,
                      row, s0, s1, s2);
     double dotv = 0.0;
     const int64_t o = 3 * row;
@@ -1085,7 +1118,21 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
                         v64[q * 9 * kChunk + slot_elem<double>(ij, lane)] = val[(q * 9 + ij) * kChunk + lane];
             L.val.upload(v64);
         }
-        if (!L.tbl && vc32 && l >= 1) {
+        if (!L.tbl && vc32 && l >= 1 && l == nlev - 1 && opt.precond_fp32 == 2) {
+            // block-exponent fp16 copy of the fine level for the smoother and the V-cycle
+            // residual (symmetric: a block and its transpose round alike); coarser levels fp32
+            std::vector<uint16_t> v16((size_t)nslot * 10 * kChunk);
+#pragma omp parallel for schedule(static)
+            for (int64_t q = 0; q < nslot; ++q)
+                for (int64_t lane = 0; lane < kChunk; ++lane) {
+                    double blk[9];
+                    uint16_t rec[10];
+                    for (int ij = 0; ij < 9; ++ij) blk[ij] = val[(q * 9 + ij) * kChunk + lane];
+                    to_h16_block(blk, rec);
+                    for (int k = 0; k < 10; ++k) v16[q * 10 * kChunk + 128 * (k / 2) + 2 * lane + k % 2] = rec[k];
+                }
+            L.val16.upload(v16);
+        } else if (!L.tbl && vc32 && l >= 1) {
             std::vector<float> v32(val.size());
 #pragma omp parallel for schedule(static)
             for (int64_t q = 0; q < nslot; ++q)
@@ -1359,19 +1406,29 @@ SellArgs level_args(const LevelDev& L) {
 }
 
 // one SELL launch over a level: table mode when the arguments carry a table, else values
-// streamed as fp32 (f32) or fp64
+// streamed in storage type vt (kVal64 / kVal32 / kValH16)
 template <int MODE, bool BJ, bool DOT>
-void launch_sell(bool f32, const SellArgs& a, hipStream_t s) {
+void launch_sell(int vt, const SellArgs& a, hipStream_t s) {
     const int grid = ceil_div(a.nch, 4);
     constexpr int V = default_variant(MODE);
     if (a.tab) hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, double, V, true>), dim3(grid), dim3(kBlock), 0, s, a, a.tab);
-    else if (f32) hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, float>), dim3(grid), dim3(kBlock), 0, s, a, a.tab);
+    else if (vt == kValH16) hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, uint16_t>), dim3(grid), dim3(kBlock), 0, s, a, a.tab);
+    else if (vt == kVal32) hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, float>), dim3(grid), dim3(kBlock), 0, s, a, a.tab);
     else hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, double>), dim3(grid), dim3(kBlock), 0, s, a, a.tab);
 }
 
 template <int MODE, bool BJ, bool DOT>
-void launch_loop(int loop, bool f32, const SellArgs& a, int grid, hipStream_t s) {
-    if (f32) {
+void launch_loop(int loop, int vt, const SellArgs& a, int grid, hipStream_t s) {
+    if (vt == kValH16) {
+        switch (loop) {
+            case 0: hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, uint16_t, 0>), dim3(grid), dim3(kBlock), 0, s, a, a.tab); break;
+            case 1: hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, uint16_t, 1>), dim3(grid), dim3(kBlock), 0, s, a, a.tab); break;
+            case 2: hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, uint16_t, 2>), dim3(grid), dim3(kBlock), 0, s, a, a.tab); break;
+            default: hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, uint16_t, 3>), dim3(grid), dim3(kBlock), 0, s, a, a.tab); break;
+        }
+        return;
+    }
+    if (vt == kVal32) {
         switch (loop) {
             case 0: hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, float, 0>), dim3(grid), dim3(kBlock), 0, s, a, a.tab); break;
             case 1: hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, float, 1>), dim3(grid), dim3(kBlock), 0, s, a, a.tab); break;
@@ -1393,7 +1450,9 @@ namespace {
 // V-cycle-operator arguments of a level: the fp32 copy when the preconditioner stores it
 SellArgs vc_level_args(const MgpisDevice& D, int level) {
     SellArgs a = level_args(D.lev[level]);
-    if (D.vc32() && !D.lev[level].tbl) a.val = D.lev[level].val32.p;
+    const int vt = D.vc_type(level);
+    if (vt == kValH16) a.val = D.lev[level].val16.p;
+    else if (vt == kVal32) a.val = D.lev[level].val32.p;
     return a;
 }
 }  // namespace
@@ -1412,7 +1471,7 @@ void MgpisDevice::spmv(int level, const double* x, double* y, bool vc_op) {
     if (!a.val && !a.tab) throw ApiError(DDPCA_ESTATE, "operator of this level is not stored in the requested precision");
     a.x = x;
     a.y = y;
-    launch_sell<kSpmv, false, false>(vc_op && vc32(), a, stream);
+    launch_sell<kSpmv, false, false>(vc_op ? vc_type(level) : kVal64, a, stream);
 }
 
 double MgpisDevice::bench_spmv(int variant, int reps) {
@@ -1424,14 +1483,15 @@ double MgpisDevice::bench_spmv(int variant, int reps) {
     const LevelDev& L = lev.back();
     const int loop = variant & 3, mode = (variant >> 2) & 3;
     const bool f32 = (variant & 16) != 0;
+    const int vt = !f32 ? kVal64 : L.val16.p ? kValH16 : kVal32;  // the V-cycle's copy
     const int tloop = (variant & 32) ? 4 + (loop & 1) : loop;
     if (variant >= 64 || ((variant & 32) && (!L.tbl || mode != 0 || f32))) throw ApiError(DDPCA_EINVAL, "unknown SpMV variant");
     if (mode == 3 && (lev.size() < 2 || opt.smoother < 1)) throw ApiError(DDPCA_EINVAL, "Chebyshev mode needs block smoothing");
-    if (f32 && !L.val32.p) throw ApiError(DDPCA_EINVAL, "no fp32 operator (precond_fp32 = 0)");
+    if (f32 && !L.val32.p && !L.val16.p) throw ApiError(DDPCA_EINVAL, "no reduced-precision operator (precond_fp32 = 0)");
     DDPCA_HIP(hipMemsetAsync(sc.p, 0, nsub * sizeof(PcgScal), stream));  // done = 0, beta = 0
     SellArgs a = level_args(L);
     if (f32) {
-        a.val = L.val32.p;
+        a.val = vt == kValH16 ? (const void*)L.val16.p : (const void*)L.val32.p;
         a.tab = nullptr;
     }
     a.x = xs.p;
@@ -1463,16 +1523,16 @@ double MgpisDevice::bench_spmv(int variant, int reps) {
             return;
         }
         if (a.tab) {  // table mode: one loop variant
-            if (mode == 0) launch_sell<kSpmv, false, false>(false, a, stream);
-            else if (mode == 1) launch_sell<kPcg, false, true>(false, a, stream);
-            else if (mode == 2) launch_sell<kResid, false, false>(false, a, stream);
-            else launch_sell<kCheb, true, false>(false, a, stream);
+            if (mode == 0) launch_sell<kSpmv, false, false>(kVal64, a, stream);
+            else if (mode == 1) launch_sell<kPcg, false, true>(kVal64, a, stream);
+            else if (mode == 2) launch_sell<kResid, false, false>(kVal64, a, stream);
+            else launch_sell<kCheb, true, false>(kVal64, a, stream);
             return;
         }
-        if (mode == 0) launch_loop<kSpmv, false, false>(loop, f32, a, grid, stream);
-        else if (mode == 1) launch_loop<kPcg, false, true>(loop, f32, a, grid, stream);
-        else if (mode == 2) launch_loop<kResid, false, false>(loop, f32, a, grid, stream);
-        else launch_loop<kCheb, true, false>(loop, f32, a, grid, stream);
+        if (mode == 0) launch_loop<kSpmv, false, false>(loop, vt, a, grid, stream);
+        else if (mode == 1) launch_loop<kPcg, false, true>(loop, vt, a, grid, stream);
+        else if (mode == 2) launch_loop<kResid, false, false>(loop, vt, a, grid, stream);
+        else launch_loop<kCheb, true, false>(loop, vt, a, grid, stream);
     };
     launch();
     DDPCA_HIP(hipEventRecord(ev_k0, stream));
@@ -1507,8 +1567,8 @@ void MgpisDevice::vcycle(const double* rin, double* zout, bool dot) {
     auto bvec = [&](int l) -> const double* { return l == Lf ? rin : lev[l].b.p; };
     auto coef = [&](int l, int sweep) { return lev[l].coef.p + 2 * (int64_t)sweep * nsub; };
     // smoothing sweeps on level l from the current iterate (first: jac0/restrict already did sweep 0)
-    const bool f32 = vc32();
     auto smooth = [&](int l, int first, int count, bool last_dot) {
+        const int f32 = vc_type(l);
         for (int s = first; s < first + count; ++s) {
             SellArgs a = vc_level_args(*this, l);
             a.sc = scp;
@@ -1548,7 +1608,7 @@ void MgpisDevice::vcycle(const double* rin, double* zout, bool dot) {
             a.x = cur[l];
             a.b = bvec(l);
             a.y = lev[l].r.p;
-            launch_sell<kResid, false, false>(f32, a, stream);
+            launch_sell<kResid, false, false>(vc_type(l), a, stream);
         }
         const int c = l - 1;
         const LevelDev& F = lev[l];
@@ -1577,12 +1637,12 @@ void MgpisDevice::vcycle(const double* rin, double* zout, bool dot) {
     if (cur[Lf] != zout) throw ApiError(DDPCA_ESTATE, "V-cycle buffer parity");
 }
 
-double MgpisDevice::fine_matrix_bytes(int s, bool f32) const {
+double MgpisDevice::fine_matrix_bytes(int s, int vt) const {
     // operator bytes one fine-level pass reads for member s: streamed values = 4 B index + 72 B
-    // (fp64) or 36 B (fp32) per stored block; table mode = 4 B index per block + 4 B row type
-    // per node + the member's share of the table (read once per launch)
+    // (fp64), 36 B (fp32) or 20 B (block-exponent fp16) per stored block; table mode = 4 B index per block +
+    // 4 B row type per node + the member's share of the table (read once per launch)
     const LevelDev& L = lev.back();
-    if (!L.tbl) return (f32 ? 40.0 : 76.0) * (double)L.nnzb_sub[s];
+    if (!L.tbl) return (vt == kValH16 ? 24.0 : vt == kVal32 ? 40.0 : 76.0) * (double)L.nnzb_sub[s];
     double nodes = 0.0;
     for (int64_t n : L.nloc) nodes += (double)n;
     return 4.0 * (double)L.nnzb_sub[s] + 4.0 * (double)L.nloc[s] +
@@ -1592,7 +1652,7 @@ double MgpisDevice::fine_matrix_bytes(int s, bool f32) const {
 double MgpisDevice::fine_kernel_bytes(int s) const {
     // algorithmic bytes of one fine-level k_sell<kPcg> for member s: the operator + z gathered
     // once (24 B/node) + p, q read and written (4 x 24 B/node)
-    return fine_matrix_bytes(s, false) + 24.0 * 5.0 * (double)lev.back().nloc[s];
+    return fine_matrix_bytes(s, kVal64) + 24.0 * 5.0 * (double)lev.back().nloc[s];
 }
 
 void MgpisDevice::enqueue_iteration(int prec, bool timed) {
@@ -1605,7 +1665,7 @@ void MgpisDevice::enqueue_iteration(int prec, bool timed) {
     a.partial = partial.p;
     const int nblk = ceil_div(L.nn, kBlock);
     if (timed) DDPCA_HIP(hipEventRecord(ev_k0, stream));
-    launch_sell<kPcg, false, true>(false, a, stream);
+    launch_sell<kPcg, false, true>(kVal64, a, stream);
     if (timed) DDPCA_HIP(hipEventRecord(ev_k1, stream));
     hipLaunchKernelGGL(k_fin, dim3(nsub), dim3(kBlock), 0, stream, (int)kFinAlpha, partial.p, nullptr, fin_cb.p, sc.p, mirror.dev);
     hipLaunchKernelGGL(k_axpy, dim3(nblk), dim3(kBlock), 0, stream, xs.p, rs.p, ps.p, qs.p, sc.p, partial.p, L.nn, L.csub.p);
@@ -1652,7 +1712,7 @@ void MgpisDevice::pcg_begin(int prec, double rtol, const std::vector<int64_t>& m
         a.b = bs.p;
         a.y = rs.p;
         a.partial = partial.p;
-        launch_sell<kResid, false, true>(false, a, stream);
+        launch_sell<kResid, false, true>(kVal64, a, stream);
         hipLaunchKernelGGL(k_fin, dim3(nsub), dim3(kBlock), 0, stream, (int)kFinInitWarm, partial.p, partial2, fin_cb.p, sc.p, mirror.dev);
     }
     if (prec == 1) vcycle(rs.p, zs.p, true);

@@ -42,6 +42,9 @@
 
 namespace ddpca {
 
+// Storage type of streamed operator values (arithmetic is fp64 throughout).
+enum ValType { kVal64 = 0, kVal32 = 1, kValH16 = 2 };  // H16: block-exponent fp16
+
 // Per-subdomain scalar block of the PCG recurrence (device memory, read by every kernel).
 struct PcgScal {
     double delta;     // r^T z
@@ -74,6 +77,7 @@ struct LevelDev {
     DevBuf<double> val;    // fp64 operator: fine level (Krylov operator), or every level when the
                            // V-cycle runs on fp64 operators
     DevBuf<float> val32;   // V-cycle operator rounded once to fp32 (opt.precond_fp32), levels >= 1
+    DevBuf<uint16_t> val16;  // fine level's V-cycle copy in block-exponent fp16 (opt.precond_fp32 = 2)
     // table mode: rows whose block values (in device slot order, masks applied) are bit-identical
     // share one table row; the kernel streams only column indices and a row type, the values
     // come from the cache-resident table (structured meshes: ~30x fewer distinct rows than rows)
@@ -147,6 +151,11 @@ public:
     // y = K_level x (batch nodal layout); vc_op: the V-cycle's copy of the operator
     void spmv(int level, const double* x, double* y, bool vc_op = false);
     bool vc32() const { return opt.precond_fp32 != 0 && lev.size() > 1; }
+    // storage type of the V-cycle's copy of level l (table-mode levels: the table)
+    int vc_type(int l) const {
+        if (!vc32() || lev[l].tbl) return kVal64;
+        return lev[l].val16.p ? kValH16 : kVal32;
+    }
     void vcycle(const double* r, double* z, bool dot);     // z = M^-1 r (fine level)
     // b_{l-1} = realProl[l-1]^T r_l on every member (masked), batch nodal layouts of levels l, l-1
     void restrict_level(int l, const double* rf, double* bc);
@@ -169,7 +178,7 @@ public:
     int64_t timed_kernel_samples = 0;
     bool time_kernel = false;
     double fine_kernel_bytes(int s) const;  // algorithmic bytes of the timed kernel, member s
-    double fine_matrix_bytes(int s, bool f32) const;  // operator bytes of one fine pass, member s
+    double fine_matrix_bytes(int s, int vt) const;  // operator bytes of one fine pass, member s
     double bench_spmv(int variant, int reps);  // ms per launch of a fine-level SpMV loop variant
     int64_t graphs_launched = 0;
 

@@ -50,7 +50,11 @@ typedef struct {
     int precond_fp32;  /* 1: the V-cycle's level operators are stored rounded to fp32 (once, at
                           create; still exactly symmetric, all arithmetic fp64).  The Krylov
                           operator, vectors and the stop rule stay fp64, so the solution meets the
-                          same ||r|| <= rtol ||b||; only the preconditioner differs slightly. */
+                          same ||r|| <= rtol ||b||; only the preconditioner differs slightly.
+                          2: as 1, and the fine level's V-cycle copy (smoothing sweeps and the
+                          V-cycle residual) stored as block-exponent fp16 (2^e x nine fp16 per 3x3
+                          block) -- 24 instead of 40 B per block on the two fine smoother passes
+                          of every PCG iteration. */
     int table_mode;    /* levels >= 1: 0 stream every block value; 1 (default) when the rows'
                           block values deduplicate well (structured meshes), keep one copy per
                           distinct row in a cache-resident table and stream only column indices
