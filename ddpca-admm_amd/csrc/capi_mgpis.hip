@@ -262,7 +262,7 @@ int mgpis_gpu_bench_spmv(mgpis_t h, int variant, int reps, double* ms, double* b
         const double per_node[4] = {24.0, 96.0, 48.0, 24.0 * 5.0 + 72.0};
         const int mode = (variant >> 2) & 3;
         const bool f32 = (variant & 16) != 0;
-        if (bytes) *bytes = D.fine_matrix_bytes(0, !f32 ? kVal64 : D.lev.back().val16.p ? kValH16 : kVal32) + (24.0 + per_node[mode]) * (double)D.lev.back().nloc[0];
+        if (bytes) *bytes = D.fine_matrix_bytes(0, !f32 ? kVal64 : D.lev.back().val16.p ? kValH16 : kVal32, false) + (24.0 + per_node[mode]) * (double)D.lev.back().nloc[0];
     });
 }
 

@@ -32,6 +32,7 @@ struct SellArgs {
     const int32_t* slots;
     const int64_t* off;
     const int32_t* col;
+    const int16_t* col16;  // column offsets from the row node (levels whose offsets fit), or null
     const void* val;       // double (Krylov operator) or float (fp32-stored V-cycle operator)
     const int32_t* csub;   // chunk -> subdomain
     int64_t nch;
@@ -171,47 +172,58 @@ __device__ __forceinline__ void block_fma_plain(const T* v, const double* xj, do
 //   0  slot loop unrolled x3, cached loads
 //   1  as 0 with non-temporal matrix loads
 //   2  groups of 3 slots with the next group's columns prefetched, non-temporal matrix loads
-template <int V, typename T>
-__device__ __forceinline__ void sell_rows(const int32_t* colp, const T* valp, const double* x, int ns, int64_t row,
+// Column of slot k for this lane: CT = int32_t holds the block column, CT = int16_t its offset
+// from the row's own node (col16: every |column - row| of the level < 2^15, which the
+// lexicographic device numbering gives for subdomains up to ~180 x 180 nodes per plane) --
+// 2 B instead of 4 per block.
+template <typename CT>
+__device__ __forceinline__ int64_t col_of(CT c, int64_t row) {
+    if constexpr (sizeof(CT) == 2) return row + (int64_t)c;
+    else return (int64_t)c;
+}
+
+template <int V, typename T, typename CT = int32_t>
+__device__ __forceinline__ void sell_rows(const CT* colp, const T* valp, const double* x, int ns, int64_t row,
                                           double& s0, double& s1, double& s2) {
+    constexpr int64_t SV = slot_vals<T>() * kChunk;
     if constexpr (V == 0) {
 #pragma unroll 3
         for (int k = 0; k < ns; ++k)
-            block_fma_plain(valp + (int64_t)k * slot_vals<T>() * kChunk, x + 3 * (int64_t)colp[(int64_t)k * kChunk], s0, s1, s2);
+            block_fma_plain(valp + (int64_t)k * SV, x + 3 * col_of(colp[(int64_t)k * kChunk], row), s0, s1, s2);
     } else if constexpr (V == 1) {
 #pragma unroll 3
         for (int k = 0; k < ns; ++k)
-            block_fma(valp + (int64_t)k * slot_vals<T>() * kChunk, x + 3 * (int64_t)__builtin_nontemporal_load(colp + (int64_t)k * kChunk),
+            block_fma(valp + (int64_t)k * SV, x + 3 * col_of(__builtin_nontemporal_load(colp + (int64_t)k * kChunk), row),
                       s0, s1, s2);
     } else if constexpr (V == 3) {
         // diagnostic bound only (wrong product): as 1 but x gathered at the row's own node, i.e.
         // perfectly coalesced gathers -- what a locality-optimal node numbering could approach
 #pragma unroll 3
         for (int k = 0; k < ns; ++k) {
-            const int32_t j = __builtin_nontemporal_load(colp + (int64_t)k * kChunk);
-            block_fma(valp + (int64_t)k * slot_vals<T>() * kChunk, x + 3 * (row + (j & 0)), s0, s1, s2);
+            const int64_t j = col_of(__builtin_nontemporal_load(colp + (int64_t)k * kChunk), row);
+            block_fma(valp + (int64_t)k * SV, x + 3 * (row + (j & 0)), s0, s1, s2);
         }
     } else {
         int k = 0;
-        int32_t c0 = 0, c1 = 0, c2 = 0;
+        CT c0 = 0, c1 = 0, c2 = 0;
         if (ns >= 3) {
             c0 = __builtin_nontemporal_load(colp);
             c1 = __builtin_nontemporal_load(colp + kChunk);
             c2 = __builtin_nontemporal_load(colp + 2 * kChunk);
         }
         for (; k + 3 <= ns; k += 3) {
-            const int64_t j0 = c0, j1 = c1, j2 = c2;
+            const int64_t j0 = col_of(c0, row), j1 = col_of(c1, row), j2 = col_of(c2, row);
             if (k + 6 <= ns) {
                 c0 = __builtin_nontemporal_load(colp + (int64_t)(k + 3) * kChunk);
                 c1 = __builtin_nontemporal_load(colp + (int64_t)(k + 4) * kChunk);
                 c2 = __builtin_nontemporal_load(colp + (int64_t)(k + 5) * kChunk);
             }
-            const T* v = valp + (int64_t)k * slot_vals<T>() * kChunk;
+            const T* v = valp + (int64_t)k * SV;
             block_fma(v, x + 3 * j0, s0, s1, s2);
-            block_fma(v + slot_vals<T>() * kChunk, x + 3 * j1, s0, s1, s2);
-            block_fma(v + 2 * slot_vals<T>() * kChunk, x + 3 * j2, s0, s1, s2);
+            block_fma(v + SV, x + 3 * j1, s0, s1, s2);
+            block_fma(v + 2 * SV, x + 3 * j2, s0, s1, s2);
         }
-        for (; k < ns; ++k) block_fma(valp + (int64_t)k * slot_vals<T>() * kChunk, x + 3 * (int64_t)colp[(int64_t)k * kChunk], s0, s1, s2);
+        for (; k < ns; ++k) block_fma(valp + (int64_t)k * SV, x + 3 * col_of(colp[(int64_t)k * kChunk], row), s0, s1, s2);
     }
 }
 
@@ -293,7 +305,8 @@ constexpr int default_variant(int mode) { return (mode == 0 || mode == 1) ? 2 : 
 
 // One wavefront per 64-node chunk, one lane per node row, three accumulators per lane; T is the
 // storage type of streamed operator values (all arithmetic fp64); TBL: values from the table.
-template <int MODE, bool BJ, bool DOT, typename T = double, int V = default_variant(MODE), bool TBL = false>
+template <int MODE, bool BJ, bool DOT, typename T = double, int V = default_variant(MODE), bool TBL = false,
+          typename CT = int32_t>
 __global__ __launch_bounds__(kBlock) void k_sell(SellArgs a, const double* __restrict__ tab) {
     const int lane = threadIdx.x & 63;
     const int64_t c = (int64_t)blockIdx.x * (kBlock / kWave) + (threadIdx.x >> 6);
@@ -313,9 +326,12 @@ __global__ __launch_bounds__(kBlock) void k_sell(SellArgs a, const double* __res
                                                 s0, s1, s2);
         else
             sell_rows_tbl(a.col + base * kChunk + lane, tab + (int64_t)a.rtype[row] * a.tstride, a.x, ns, s0, s1, s2);
-    } else
-        sell_rows<V>(a.col + base * kChunk + lane, static_cast<const T*>(a.val) + base * slot_vals<T>() * kChunk + lane, a.x, ns,
-                     row, s0, s1, s2);
+    } else if constexpr (sizeof(CT) == 2)
+        sell_rows<V, T, CT>(a.col16 + base * kChunk + lane, static_cast<const T*>(a.val) + base * slot_vals<T>() * kChunk + lane,
+                            a.x, ns, row, s0, s1, s2);
+    else
+        sell_rows<V, T, CT>(a.col + base * kChunk + lane, static_cast<const T*>(a.val) + base * slot_vals<T>() * kChunk + lane,
+                            a.x, ns, row, s0, s1, s2);
     double dotv = 0.0;
     const int64_t o = 3 * row;
     if (MODE == kSpmv) {
@@ -1099,6 +1115,20 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
         L.csub.upload(csub);
         L.off.upload(off);
         L.col.upload(col);
+        {
+            // relative 16-bit columns when every offset of the level fits (DDPCA_COL16=0: off)
+            static const bool want16 = !std::getenv("DDPCA_COL16") || std::atoi(std::getenv("DDPCA_COL16")) != 0;
+            bool fits = want16;
+            std::vector<int16_t> col16(want16 ? col.size() : 0);
+            for (int64_t c = 0; c < L.nch && fits; ++c)
+                for (int64_t q = off[c]; q < off[c + 1] && fits; ++q)
+                    for (int64_t lane = 0; lane < kChunk; ++lane) {
+                        const int64_t d = (int64_t)col[q * kChunk + lane] - (c * kChunk + lane);
+                        if (d < INT16_MIN || d > INT16_MAX) { fits = false; break; }
+                        col16[q * kChunk + lane] = (int16_t)d;
+                    }
+            if (fits) L.col16.upload(col16);
+        }
         if (opt.table_mode != 0 && l >= 1) build_table(L, slots, off, val, opt.table_mode == 2 || grouped[l]);
         if (std::getenv("DDPCA_VERBOSE"))
             std::fprintf(stderr, "[ddpca] level %d: %lld nodes, %lld chunks, %lld slots, table %d (%lld types, %lld uniform chunks)\n",
@@ -1118,7 +1148,9 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
                         v64[q * 9 * kChunk + slot_elem<double>(ij, lane)] = val[(q * 9 + ij) * kChunk + lane];
             L.val.upload(v64);
         }
-        if (!L.tbl && vc32 && l >= 1 && l == nlev - 1 && opt.precond_fp32 == 2) {
+        // levels in block-exponent fp16: the finest h16_levels (DDPCA_H16_LEVELS, default 2: +2 % over 1, profiles/r01_sweep_h16.txt)
+        static const int h16_levels = std::getenv("DDPCA_H16_LEVELS") ? std::atoi(std::getenv("DDPCA_H16_LEVELS")) : 2;
+        if (!L.tbl && vc32 && l >= 1 && l >= nlev - h16_levels && opt.precond_fp32 == 2) {
             // block-exponent fp16 copy of the fine level for the smoother and the V-cycle
             // residual (symmetric: a block and its transpose round alike); coarser levels fp32
             std::vector<uint16_t> v16((size_t)nslot * 10 * kChunk);
@@ -1390,6 +1422,7 @@ SellArgs level_args(const LevelDev& L) {
     a.slots = L.slots.p;
     a.off = L.off.p;
     a.col = L.col.p;
+    a.col16 = L.col16.p;
     a.val = L.val.p;
     a.csub = L.csub.p;
     a.nch = L.nch;
@@ -1411,8 +1444,13 @@ template <int MODE, bool BJ, bool DOT>
 void launch_sell(int vt, const SellArgs& a, hipStream_t s) {
     const int grid = ceil_div(a.nch, 4);
     constexpr int V = default_variant(MODE);
+    using I16 = int16_t;
     if (a.tab) hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, double, V, true>), dim3(grid), dim3(kBlock), 0, s, a, a.tab);
-    else if (vt == kValH16) hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, uint16_t>), dim3(grid), dim3(kBlock), 0, s, a, a.tab);
+    else if (a.col16) {
+        if (vt == kValH16) hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, uint16_t, V, false, I16>), dim3(grid), dim3(kBlock), 0, s, a, a.tab);
+        else if (vt == kVal32) hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, float, V, false, I16>), dim3(grid), dim3(kBlock), 0, s, a, a.tab);
+        else hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, double, V, false, I16>), dim3(grid), dim3(kBlock), 0, s, a, a.tab);
+    } else if (vt == kValH16) hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, uint16_t>), dim3(grid), dim3(kBlock), 0, s, a, a.tab);
     else if (vt == kVal32) hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, float>), dim3(grid), dim3(kBlock), 0, s, a, a.tab);
     else hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, double>), dim3(grid), dim3(kBlock), 0, s, a, a.tab);
 }
@@ -1637,12 +1675,14 @@ void MgpisDevice::vcycle(const double* rin, double* zout, bool dot) {
     if (cur[Lf] != zout) throw ApiError(DDPCA_ESTATE, "V-cycle buffer parity");
 }
 
-double MgpisDevice::fine_matrix_bytes(int s, int vt) const {
+double MgpisDevice::fine_matrix_bytes(int s, int vt, bool prod_cols) const {
     // operator bytes one fine-level pass reads for member s: streamed values = 4 B index + 72 B
     // (fp64), 36 B (fp32) or 20 B (block-exponent fp16) per stored block; table mode = 4 B index per block +
     // 4 B row type per node + the member's share of the table (read once per launch)
     const LevelDev& L = lev.back();
-    if (!L.tbl) return (vt == kValH16 ? 24.0 : vt == kVal32 ? 40.0 : 76.0) * (double)L.nnzb_sub[s];
+    // (the production kernels read 2-B column offsets where the level has them, prod_cols)
+    const double cb = (prod_cols && L.col16.p) ? 2.0 : 4.0;
+    if (!L.tbl) return (cb + (vt == kValH16 ? 20.0 : vt == kVal32 ? 36.0 : 72.0)) * (double)L.nnzb_sub[s];
     double nodes = 0.0;
     for (int64_t n : L.nloc) nodes += (double)n;
     return 4.0 * (double)L.nnzb_sub[s] + 4.0 * (double)L.nloc[s] +

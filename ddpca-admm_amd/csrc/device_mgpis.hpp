@@ -73,6 +73,7 @@ struct LevelDev {
     int64_t nn = 0, nch = 0, nslots = 0, nnzb = 0;  // batch totals (nn, nch padded)
     std::vector<int64_t> noff, nloc, nnzb_sub;      // per subdomain: first node, real nodes, blocks
     DevBuf<int32_t> slots, col, csub;               // csub: chunk -> subdomain
+    DevBuf<int16_t> col16;  // col - row node when every offset of the level fits 16 bits (else empty)
     DevBuf<int64_t> off;
     DevBuf<double> val;    // fp64 operator: fine level (Krylov operator), or every level when the
                            // V-cycle runs on fp64 operators
@@ -178,7 +179,9 @@ public:
     int64_t timed_kernel_samples = 0;
     bool time_kernel = false;
     double fine_kernel_bytes(int s) const;  // algorithmic bytes of the timed kernel, member s
-    double fine_matrix_bytes(int s, int vt) const;  // operator bytes of one fine pass, member s
+    // operator bytes of one fine pass, member s (prod_cols: with the 16-bit column offsets the
+    // production kernels use; the mgpis_gpu_bench_spmv variants read 32-bit columns)
+    double fine_matrix_bytes(int s, int vt, bool prod_cols = true) const;
     double bench_spmv(int variant, int reps);  // ms per launch of a fine-level SpMV loop variant
     int64_t graphs_launched = 0;
 
