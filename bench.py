@@ -31,7 +31,7 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
-VALUE_LAYOUT = "fp64-pairs"  # SELL value layout of the fine Krylov operator (device_mgpis.hip)
+VALUE_LAYOUT = "fp64-pairs, col16"  # SELL layout of the fine Krylov operator (device_mgpis.hip)
 
 
 def parse():

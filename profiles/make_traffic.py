@@ -43,9 +43,9 @@ def main():
     ap.add_argument("fetch_csv")
     ap.add_argument("write_csv")
     for k, d in [("groups", 4), ("nx", 3), ("ny", 2), ("nz", 2), ("gl", 5), ("smoother", 1), ("nu", 1),
-                 ("precond-fp32", 1), ("table-mode", 0)]:
+                 ("precond-fp32", 2), ("table-mode", 0)]:
         ap.add_argument(f"--{k}", type=int, default=d)
-    ap.add_argument("--value-layout", default="fp64-pairs")
+    ap.add_argument("--value-layout", default="fp64-pairs, col16")
     ap.add_argument("--out", default=str(Path(__file__).resolve().parent / "traffic.json"))
     a = ap.parse_args()
     fetch = full_launches(per_launch(a.fetch_csv, "FETCH_SIZE"))
