@@ -10,6 +10,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <numeric>
+#include <type_traits>
 #include <omp.h>
 #include <random>
 #include <thread>
@@ -39,7 +40,7 @@ struct SellArgs {
     const double* x;       // gathered operand
     double* y;             // SPMV / RESID output, PCG: q (in place)
     const double* b;       // RESID / JAC / CHEB right-hand side
-    const double* minv;
+    const void* minv;      // smoother inverse: double, or float on reduced-precision levels
     const double* coef;    // per subdomain (c1, c2) of this sweep; JAC uses c2 = omega
     double* xo;            // JAC / CHEB new iterate
     double* p;             // PCG: p (in place), CHEB: direction d (in place)
@@ -65,16 +66,16 @@ __device__ __forceinline__ void chunk_partial(double v, double* partial, int64_t
 
 __device__ __forceinline__ bool stopped(const PcgScal* sc, int sub) { return sc && sc[sub].done; }
 
-template <bool BJ>
-__device__ __forceinline__ void apply_m(const double* minv, int64_t row, double r0, double r1, double r2,
+template <bool BJ, typename MT = double>
+__device__ __forceinline__ void apply_m(const MT* minv, int64_t row, double r0, double r1, double r2,
                                         double& m0, double& m1, double& m2) {
     if (BJ) {
-        const double* m = minv + 9 * row;
+        const MT* m = minv + 9 * row;
         m0 = m[0] * r0 + m[1] * r1 + m[2] * r2;
         m1 = m[3] * r0 + m[4] * r1 + m[5] * r2;
         m2 = m[6] * r0 + m[7] * r1 + m[8] * r2;
     } else {
-        const double* m = minv + 3 * row;
+        const MT* m = minv + 3 * row;
         m0 = m[0] * r0;
         m1 = m[1] * r1;
         m2 = m[2] * r2;
@@ -104,6 +105,11 @@ typedef double dbl2_t __attribute__((ext_vector_type(2)));
 // and its transpose share e and round alike, so the operator stays exactly symmetric.
 template <typename T>
 constexpr int slot_vals() { return sizeof(T) == 2 ? 10 : 9; }
+
+// storage type of the smoother inverse on a level whose operator values are stored as T: fp64
+// with fp64 operators, fp32 on the reduced-precision levels (precond_fp32 >= 1)
+template <typename T>
+using SmoothInv = typename std::conditional<sizeof(T) == 8, double, float>::type;
 
 __device__ __forceinline__ double h16_lo(uint32_t w) {
     return (double)__builtin_bit_cast(_Float16, (uint16_t)(w & 0xFFFFu));
@@ -348,7 +354,7 @@ __global__ __launch_bounds__(kBlock) void k_sell(SellArgs a, const double* __res
         const double om = a.coef[2 * sub + 1];
         const double b0 = a.b[o], b1 = a.b[o + 1], b2 = a.b[o + 2];
         double m0, m1, m2;
-        apply_m<BJ>(a.minv, row, b0 - s0, b1 - s1, b2 - s2, m0, m1, m2);
+        apply_m<BJ>(static_cast<const SmoothInv<T>*>(a.minv), row, b0 - s0, b1 - s1, b2 - s2, m0, m1, m2);
         const double n0 = a.x[o] + om * m0, n1 = a.x[o + 1] + om * m1, n2 = a.x[o + 2] + om * m2;
         a.xo[o] = n0;
         a.xo[o + 1] = n1;
@@ -370,7 +376,7 @@ __global__ __launch_bounds__(kBlock) void k_sell(SellArgs a, const double* __res
         const double c1 = a.coef[2 * sub], c2 = a.coef[2 * sub + 1];
         const double b0 = a.b[o], b1 = a.b[o + 1], b2 = a.b[o + 2];
         double m0, m1, m2;
-        apply_m<BJ>(a.minv, row, b0 - s0, b1 - s1, b2 - s2, m0, m1, m2);
+        apply_m<BJ>(static_cast<const SmoothInv<T>*>(a.minv), row, b0 - s0, b1 - s1, b2 - s2, m0, m1, m2);
         const double d0 = c1 * a.p[o] + c2 * m0, d1 = c1 * a.p[o + 1] + c2 * m1, d2 = c1 * a.p[o + 2] + c2 * m2;
         a.p[o] = d0;
         a.p[o + 1] = d1;
@@ -393,8 +399,8 @@ __global__ __launch_bounds__(kBlock) void k_sell(SellArgs a, const double* __res
     if (stopped((sc), sub)) return;
 
 // x = omega M b  (first smoothing sweep from a zero guess); CHEB: also d = x
-template <bool BJ, bool SETD>
-__global__ __launch_bounds__(kBlock) void k_jac0(const double* b, const double* minv, const double* coef, double* x,
+template <bool BJ, bool SETD, typename MT = double>
+__global__ __launch_bounds__(kBlock) void k_jac0(const double* b, const MT* minv, const double* coef, double* x,
                                                  double* d, int64_t nn, const int32_t* csub, const PcgScal* sc) {
     NODE_PROLOGUE(nn, csub, sc)
     const double om = coef[2 * sub + 1];
@@ -413,10 +419,10 @@ __global__ __launch_bounds__(kBlock) void k_jac0(const double* b, const double* 
 // b_c = mask_c (sum_children w r_f[child]), the coarse node's own fine copy first with w = 1;
 // optionally x_c = omega M b_c (CHEB: d_c too).  Children in SELL-64 layout: slot k of chunk c
 // at (roff[c] + k) * 64 + lane, so index and weight loads are contiguous wave accesses.
-template <bool INIT, bool BJ, bool SETD>
+template <bool INIT, bool BJ, bool SETD, typename MT = double>
 __global__ __launch_bounds__(kBlock) void k_restrict(const double* rf, const int32_t* rslots, const int64_t* roff,
                                                      const int32_t* rcol, const double* rwt, const uint8_t* cmask,
-                                                     double* bc, double* xc, double* dc, const double* minv,
+                                                     double* bc, double* xc, double* dc, const MT* minv,
                                                      const double* coef, int64_t nc, const int32_t* csub,
                                                      const PcgScal* sc) {
     NODE_PROLOGUE(nc, csub, sc)
@@ -644,8 +650,8 @@ __global__ void k_gather(const double* full, const int32_t* free_dof, double* co
 }
 
 // y = M x, partial ||y||^2 per chunk (power iteration for lambda_max(M K) at setup)
-template <bool BJ>
-__global__ void k_apply_m(const double* x, const double* minv, double* y, double* partial, int64_t nn) {
+template <bool BJ, typename MT = double>
+__global__ void k_apply_m(const double* x, const MT* minv, double* y, double* partial, int64_t nn) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= nn) return;
     double m0, m1, m2;
@@ -1175,6 +1181,19 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
         }
         L.dinv.upload(dinv);
         L.minv.upload(minv);
+        if (!L.tbl && vc32 && l >= 1) {
+            // reduced-precision levels smooth with an fp32 inverse, symmetrised before rounding
+            // so the V-cycle stays exactly symmetric (block Jacobi: M_ab = M_ba)
+            std::vector<float> m32(minv.size());
+            const int w = bj ? 9 : 3;
+#pragma omp parallel for schedule(static)
+            for (int64_t g = 0; g < L.nn; ++g) {
+                const double* m = minv.data() + w * g;
+                for (int k = 0; k < w; ++k)
+                    m32[w * g + k] = bj ? (float)(0.5 * (m[k] + m[3 * (k % 3) + k / 3])) : (float)m[k];
+            }
+            L.minv32.upload(m32);
+        }
         L.mask.upload(mask);
         for (auto* v : {&L.x, &L.t, &L.b, &L.r, &L.d}) {
             v->alloc(3 * L.nn);
@@ -1397,7 +1416,10 @@ void MgpisDevice::estimate_lmax(int l) {
         }
     };
     auto apply_m = [&](const double* x) {
-        if (bj) hipLaunchKernelGGL((k_apply_m<true>), dim3(nb), dim3(kBlock), 0, stream, x, L.minv.p, w.p, partial.p, L.nn);
+        if (vc_type(l) != kVal64) {  // the smoother's own (fp32) inverse
+            if (bj) hipLaunchKernelGGL((k_apply_m<true, float>), dim3(nb), dim3(kBlock), 0, stream, x, L.minv32.p, w.p, partial.p, L.nn);
+            else hipLaunchKernelGGL((k_apply_m<false, float>), dim3(nb), dim3(kBlock), 0, stream, x, L.minv32.p, w.p, partial.p, L.nn);
+        } else if (bj) hipLaunchKernelGGL((k_apply_m<true>), dim3(nb), dim3(kBlock), 0, stream, x, L.minv.p, w.p, partial.p, L.nn);
         else hipLaunchKernelGGL((k_apply_m<false>), dim3(nb), dim3(kBlock), 0, stream, x, L.minv.p, w.p, partial.p, L.nn);
     };
     apply_m(v.p);
@@ -1491,6 +1513,7 @@ SellArgs vc_level_args(const MgpisDevice& D, int level) {
     const int vt = D.vc_type(level);
     if (vt == kValH16) a.val = D.lev[level].val16.p;
     else if (vt == kVal32) a.val = D.lev[level].val32.p;
+    if (vt != kVal64) a.minv = D.lev[level].minv32.p;
     return a;
 }
 }  // namespace
@@ -1499,7 +1522,7 @@ void MgpisDevice::restrict_level(int l, const double* rf, double* bc) {
     if (l < 1 || l >= (int)lev.size()) throw ApiError(DDPCA_EINVAL, "restrict_level: level");
     const LevelDev& F = lev[l];
     const LevelDev& C = lev[l - 1];
-    hipLaunchKernelGGL((k_restrict<false, false, false>), dim3(ceil_div(C.nn, kBlock)), dim3(kBlock), 0, stream, rf,
+    hipLaunchKernelGGL((k_restrict<false, false, false, double>), dim3(ceil_div(C.nn, kBlock)), dim3(kBlock), 0, stream, rf,
                        F.rslots.p, F.roff.p, F.rcol.p, F.rwt.p, C.mask.p, bc, nullptr, nullptr, nullptr, nullptr, C.nn,
                        C.csub.p, nullptr);
 }
@@ -1634,7 +1657,12 @@ void MgpisDevice::vcycle(const double* rin, double* zout, bool dot) {
     {
         const LevelDev& F = lev[Lf];
         const int grid = ceil_div(F.nn, kBlock);
-        if (cheb) hipLaunchKernelGGL((k_jac0<true, true>), dim3(grid), dim3(kBlock), 0, stream, rin, F.minv.p, coef(Lf, 0), cur[Lf], F.d.p, F.nn, F.csub.p, scp);
+        if (vc_type(Lf) != kVal64) {
+            const float* m = F.minv32.p;
+            if (cheb) hipLaunchKernelGGL((k_jac0<true, true, float>), dim3(grid), dim3(kBlock), 0, stream, rin, m, coef(Lf, 0), cur[Lf], F.d.p, F.nn, F.csub.p, scp);
+            else if (bj) hipLaunchKernelGGL((k_jac0<true, false, float>), dim3(grid), dim3(kBlock), 0, stream, rin, m, coef(Lf, 0), cur[Lf], nullptr, F.nn, F.csub.p, scp);
+            else hipLaunchKernelGGL((k_jac0<false, false, float>), dim3(grid), dim3(kBlock), 0, stream, rin, m, coef(Lf, 0), cur[Lf], nullptr, F.nn, F.csub.p, scp);
+        } else if (cheb) hipLaunchKernelGGL((k_jac0<true, true>), dim3(grid), dim3(kBlock), 0, stream, rin, F.minv.p, coef(Lf, 0), cur[Lf], F.d.p, F.nn, F.csub.p, scp);
         else if (bj) hipLaunchKernelGGL((k_jac0<true, false>), dim3(grid), dim3(kBlock), 0, stream, rin, F.minv.p, coef(Lf, 0), cur[Lf], nullptr, F.nn, F.csub.p, scp);
         else hipLaunchKernelGGL((k_jac0<false, false>), dim3(grid), dim3(kBlock), 0, stream, rin, F.minv.p, coef(Lf, 0), cur[Lf], nullptr, F.nn, F.csub.p, scp);
     }
@@ -1654,8 +1682,16 @@ void MgpisDevice::vcycle(const double* rin, double* zout, bool dot) {
         const int grid = ceil_div(C.nn, kBlock);
         const double* cf = c > 0 ? coef(c, 0) : nullptr;
         if (c == cl)
-            hipLaunchKernelGGL((k_restrict<false, false, false>), dim3(grid), dim3(kBlock), 0, stream, F.r.p, F.rslots.p, F.roff.p, F.rcol.p, F.rwt.p, C.mask.p, C.b.p, nullptr, nullptr, nullptr, nullptr, C.nn, C.csub.p, scp);
-        else if (cheb)
+            hipLaunchKernelGGL((k_restrict<false, false, false, double>), dim3(grid), dim3(kBlock), 0, stream, F.r.p, F.rslots.p, F.roff.p, F.rcol.p, F.rwt.p, C.mask.p, C.b.p, nullptr, nullptr, nullptr, nullptr, C.nn, C.csub.p, scp);
+        else if (vc_type(c) != kVal64) {
+            const float* m = C.minv32.p;
+            if (cheb)
+                hipLaunchKernelGGL((k_restrict<true, true, true, float>), dim3(grid), dim3(kBlock), 0, stream, F.r.p, F.rslots.p, F.roff.p, F.rcol.p, F.rwt.p, C.mask.p, C.b.p, cur[c], C.d.p, m, cf, C.nn, C.csub.p, scp);
+            else if (bj)
+                hipLaunchKernelGGL((k_restrict<true, true, false, float>), dim3(grid), dim3(kBlock), 0, stream, F.r.p, F.rslots.p, F.roff.p, F.rcol.p, F.rwt.p, C.mask.p, C.b.p, cur[c], nullptr, m, cf, C.nn, C.csub.p, scp);
+            else
+                hipLaunchKernelGGL((k_restrict<true, false, false, float>), dim3(grid), dim3(kBlock), 0, stream, F.r.p, F.rslots.p, F.roff.p, F.rcol.p, F.rwt.p, C.mask.p, C.b.p, cur[c], nullptr, m, cf, C.nn, C.csub.p, scp);
+        } else if (cheb)
             hipLaunchKernelGGL((k_restrict<true, true, true>), dim3(grid), dim3(kBlock), 0, stream, F.r.p, F.rslots.p, F.roff.p, F.rcol.p, F.rwt.p, C.mask.p, C.b.p, cur[c], C.d.p, C.minv.p, cf, C.nn, C.csub.p, scp);
         else if (bj)
             hipLaunchKernelGGL((k_restrict<true, true, false>), dim3(grid), dim3(kBlock), 0, stream, F.r.p, F.rslots.p, F.roff.p, F.rcol.p, F.rwt.p, C.mask.p, C.b.p, cur[c], nullptr, C.minv.p, cf, C.nn, C.csub.p, scp);

@@ -91,6 +91,7 @@ struct LevelDev {
     DevBuf<double> tab;
 
     DevBuf<double> minv;   // point: 3 per node; block: 9 per node
+    DevBuf<float> minv32;  // the same in fp32 (symmetrised) on reduced-precision levels
     DevBuf<double> dinv;   // point Jacobi inverse (diagonal preconditioner at the fine level)
     DevBuf<uint8_t> mask;  // bit a set = dof 3i+a free
     DevBuf<double> coef;   // [(sweep * nsub + sub) * 2 + {0,1}]: Chebyshev (c1, c2) / Jacobi (-, omega)
