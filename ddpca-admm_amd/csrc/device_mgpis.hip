@@ -483,7 +483,8 @@ __global__ __launch_bounds__(kBlock) void k_prolong(const double* ec, const int3
 }
 
 // x0 = A0^-1 b0 per subdomain, one wavefront per coarse dof row
-__global__ __launch_bounds__(kBlock) void k_coarse(const double* ainv, const int64_t* aoff, const int64_t* noff,
+template <typename AT = double>
+__global__ __launch_bounds__(kBlock) void k_coarse(const AT* ainv, const int64_t* aoff, const int64_t* noff,
                                                    const int64_t* n0, const double* b, double* x, int64_t nrow,
                                                    const int32_t* csub, const PcgScal* sc) {
     const int64_t r = (int64_t)blockIdx.x * (kBlock / kWave) + (threadIdx.x >> 6);
@@ -496,10 +497,10 @@ __global__ __launch_bounds__(kBlock) void k_coarse(const double* ainv, const int
         if (lane == 0) x[r] = 0.0;
         return;
     }
-    const double* arow = ainv + aoff[sub] + lr * n;
+    const AT* arow = ainv + aoff[sub] + lr * n;
     const double* bs = b + 3 * noff[sub];
     double s = 0.0;
-    for (int64_t k = lane; k < n; k += kWave) s += arow[k] * bs[k];
+    for (int64_t k = lane; k < n; k += kWave) s += (double)arow[k] * bs[k];
     s = wave_sum(s);
     if (lane == 0) x[r] = s;
 }
@@ -1311,7 +1312,13 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
             nz[s] = n0;
             packed.insert(packed.end(), D.begin(), D.end());
         }
-        ainv.upload(packed);
+        if (vc32()) {
+            // reduced-precision preconditioner storage: the (exactly symmetric) dense inverses in
+            // fp32 -- half the bytes of the coarse GEMV, which dominates small batches' coarse time
+            std::vector<float> p32(packed.begin(), packed.end());
+            ainv32.upload(p32);
+        } else
+            ainv.upload(packed);
         aoff.upload(ao);
         c_noff.upload(no);
         c_n.upload(nz);
@@ -1614,7 +1621,9 @@ void MgpisDevice::vcycle(const double* rin, double* zout, bool dot) {
     const PcgScal* scp = sc.p;
     const int cl = clev;  // the exact dense solve; levels below it are not visited
     if (Lf == cl) {
-        hipLaunchKernelGGL(k_coarse, dim3(ceil_div(3 * lev[cl].nn, 4)), dim3(kBlock), 0, stream, ainv.p, aoff.p, c_noff.p,
+        if (ainv32.p) hipLaunchKernelGGL(k_coarse<float>, dim3(ceil_div(3 * lev[cl].nn, 4)), dim3(kBlock), 0, stream, ainv32.p, aoff.p, c_noff.p,
+                           c_n.p, rin, zout, 3 * lev[cl].nn, lev[cl].csub.p, scp);
+        else hipLaunchKernelGGL(k_coarse<double>, dim3(ceil_div(3 * lev[cl].nn, 4)), dim3(kBlock), 0, stream, ainv.p, aoff.p, c_noff.p,
                            c_n.p, rin, zout, 3 * lev[cl].nn, lev[cl].csub.p, scp);
         if (dot)
             hipLaunchKernelGGL(k_dot, dim3(ceil_div(lev[cl].nn, kBlock)), dim3(kBlock), 0, stream, rin, zout, partial.p,
@@ -1698,7 +1707,9 @@ void MgpisDevice::vcycle(const double* rin, double* zout, bool dot) {
         else
             hipLaunchKernelGGL((k_restrict<true, false, false>), dim3(grid), dim3(kBlock), 0, stream, F.r.p, F.rslots.p, F.roff.p, F.rcol.p, F.rwt.p, C.mask.p, C.b.p, cur[c], nullptr, C.minv.p, cf, C.nn, C.csub.p, scp);
     }
-    hipLaunchKernelGGL(k_coarse, dim3(ceil_div(3 * lev[cl].nn, 4)), dim3(kBlock), 0, stream, ainv.p, aoff.p, c_noff.p,
+    if (ainv32.p) hipLaunchKernelGGL(k_coarse<float>, dim3(ceil_div(3 * lev[cl].nn, 4)), dim3(kBlock), 0, stream, ainv32.p, aoff.p, c_noff.p,
+                           c_n.p, lev[cl].b.p, cur[cl], 3 * lev[cl].nn, lev[cl].csub.p, scp);
+        else hipLaunchKernelGGL(k_coarse<double>, dim3(ceil_div(3 * lev[cl].nn, 4)), dim3(kBlock), 0, stream, ainv.p, aoff.p, c_noff.p,
                        c_n.p, lev[cl].b.p, cur[cl], 3 * lev[cl].nn, lev[cl].csub.p, scp);
     // ---- ascend
     for (int l = cl + 1; l <= Lf; ++l) {

@@ -122,6 +122,7 @@ public:
     // exact coarse solve on level clev: per-subdomain dense inverses, packed
     int clev = 0;
     DevBuf<double> ainv;
+    DevBuf<float> ainv32;      // the same in fp32 (reduced-precision preconditioner storage)
     DevBuf<int64_t> aoff;      // per subdomain offset into ainv
     DevBuf<int64_t> c_noff;    // per subdomain first node of level 0
     DevBuf<int64_t> c_n;       // per subdomain coarse dofs (3 nloc_0)

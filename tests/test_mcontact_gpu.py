@@ -266,8 +266,13 @@ def test_reference_binding_end_to_end(gpu, fric, musc):
     exe = Path(__file__).resolve().parents[1] / "oracle" / "_ref" / "ref_bind"
     if not exe.exists():
         pytest.skip("oracle/_ref/ref_bind is built only where the reference is (travels with the snapshot)")
+    # one host thread: the reference's own OpenMP loops (its CPU run is the checker here) once
+    # crashed this binary (SIGSEGV before any output) on a 16-thread box and never on a rerun;
+    # single-threaded they are deterministic, and this case is small
+    import os
+    env = dict(os.environ, OMP_NUM_THREADS="1")
     out = subprocess.run([str(exe), fric, "1" if musc == "0" else "2", "gpu", musc], capture_output=True, text=True,
-                         timeout=600)
+                         timeout=600, env=env)
     assert out.returncode == 0, out.stdout + out.stderr
     res = json.loads(out.stdout.splitlines()[-1])
     assert res["gpu_ok"], res
