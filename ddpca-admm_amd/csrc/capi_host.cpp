@@ -293,8 +293,7 @@ int ddpca_problem_set_coarse(ddpca_problem_t h, int64_t muscSett, const int64_t*
     return guarded([&] {
         Problem& P = *reinterpret_cast<Problem*>(h);
         if (P.established) throw ApiError(DDPCA_ESTATE, "set_coarse after establish");
-        if (muscSett & 1) throw ApiError(DDPCA_EINVAL, "muscSett bit 0 (MULTISCALE) is not supported; use 2");
-        if (muscSett < 0 || muscSett > 3) throw ApiError(DDPCA_EINVAL, "muscSett");
+        if (muscSett < 0 || muscSett > 2) throw ApiError(DDPCA_EINVAL, "muscSett must be 0, 1 (MULTISCALE) or 2 (MULTISCALE_1)");
         P.mc.muscSett = muscSett;
         const int64_t nsub = (int64_t)P.mc.multGrid.size();
         P.mc.doleMcsc.assign(nsub, 0);
@@ -361,6 +360,17 @@ int ddpca_problem_view(ddpca_problem_t h, const char* cname, int64_t index, int6
             if (name == "globForc_1") { need(); put(cs.globForc_1, data, count, dtype); return; }
             if (name == "doleMcsc") { put(P.mc.doleMcsc, data, count, dtype); return; }
             if (name.rfind("globCoup_1:", 0) == 0) { need(); put_csr(cs.globCoup_1, name.substr(11)); return; }
+            // LATIN-type (MULTISCALE) right-hand-side operators, index = 2*ts + side
+            for (const char* base : {"globTran:", "globTran_pena:", "globTran_D:"}) {
+                const std::string b(base);
+                if (name.rfind(b, 0) != 0) continue;
+                need();
+                if (!cs.latin) throw ApiError(DDPCA_ESTATE, "not a LATIN-type coarse space (muscSett = 1)");
+                if (index < 0 || index >= 2 * nint) throw ApiError(DDPCA_EINVAL, "side index");
+                const auto& M = b == "globTran:" ? cs.globTran_L : b == "globTran_pena:" ? cs.globTran_pena_L : cs.globTran_D_L;
+                put_csr(M[index / 2][index % 2], name.substr(b.size()));
+                return;
+            }
             if (name.rfind("globTran_1:", 0) == 0) {
                 need();
                 if (index < 0 || index >= 2 * nint) throw ApiError(DDPCA_EINVAL, "side index");

@@ -264,8 +264,16 @@ void MCONTACT::ESTABLISH(const std::vector<uint8_t>* owned) {
         }
     }
     // ---- coarse space (MCONTACT.h:858-863)
-    if (muscSett & 1)
-        throw std::invalid_argument("muscSett bit 0 (MULTISCALE, MCONTACT.h:898-1536) is not supported; use bit 1");
+    if ((muscSett & 3) == 3)
+        throw std::invalid_argument("muscSett: choose one coarse space (1 = MULTISCALE, 2 = MULTISCALE_1)");
+    if (muscSett & 1) {
+        if (owned)
+            for (int64_t tv = 0; tv < (int64_t)multGrid.size(); ++tv)
+                if (!(*owned)[tv])
+                    throw std::invalid_argument("muscSett = 1 (MULTISCALE) is built on one process holding every "
+                                                "subdomain; multi-rank runs use ddpca_problem_set_coarse_latin");
+        MULTISCALE();
+    }
     if (muscSett & 2) {
         // the dof bookkeeping of every subdomain (baseReco) and the transfer stencils of the
         // mates of owned interface sides (their restriction chains)

@@ -75,6 +75,7 @@ public:
     std::vector<int64_t> doleMcsc;         // coarse level per subdomain (MCONTACT.h:23)
     CoarseSpace coarse;
     void MULTISCALE_1(const std::vector<uint8_t>* owned = nullptr);
+    void MULTISCALE();  // LATIN-type (muscSett bit 0), every subdomain built on this process
     Csr globTran_D_1(int64_t tv) const;    // assembled (tests)
     Csr accuProl(int64_t tv) const;        // assembled (tests)
     // ESTABLISH: interface operators, systMass added to each body's stiffness, then

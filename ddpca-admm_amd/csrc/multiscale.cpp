@@ -421,3 +421,157 @@ Csr MCONTACT::accuProl(int64_t tv) const {
 }
 
 }  // namespace ddpca
+
+namespace ddpca {
+
+// Host restatement of the LATIN-type coarse space, MCONTACT::MULTISCALE (MCONTACT.h:898-1536,
+// muscSett bit 0, CYLINDER.h:42), for this library's uniformly refined hierarchies (earlTran,
+// prolOper[maxiLeve] and CONT_ROTA identities; prolOper[L-1..d] = Q (x) I3).  Side 0 of every
+// interface carries the coarse contact unknowns: ficoCotr = the columns of Q restricted to
+// side 0's contact nodes that touch any of them (MCONTACT.h:900-959), one unknown per such
+// level-d node (x3 with friction).  Output in the assembled LATIN form the device consumes
+// (CoarseSpace::latin; the same fields ddpca_problem_set_coarse_latin fills from a caller).
+void MCONTACT::MULTISCALE() {
+    const int64_t nsub = (int64_t)multGrid.size(), nint = (int64_t)searCont.size();
+    if ((int64_t)doleMcsc.size() != nsub) doleMcsc.assign(nsub, 0);
+    for (int64_t tv = 0; tv < nsub; ++tv) {
+        const MULTIGRID& g = multGrid[tv];
+        if (g.freeCount.empty() || g.levelStif.empty())
+            throw std::invalid_argument("MULTISCALE (muscSett bit 0) needs every subdomain established on this "
+                                        "process; multi-rank runs hand the caller's operators over with "
+                                        "ddpca_problem_set_coarse_latin");
+        if (doleMcsc[tv] < 0 || doleMcsc[tv] > g.maxiLeve) throw std::invalid_argument("doleMcsc out of range");
+    }
+    CoarseSpace C;
+    C.assembled = true;
+    C.latin = true;
+    C.built.assign(nsub, 1);
+    C.baseReco.assign(nsub + 1, 0);
+    for (int64_t tv = 0; tv < nsub; ++tv) C.baseReco[tv + 1] = C.baseReco[tv] + multGrid[tv].freeCount[doleMcsc[tv]];
+    const int64_t N = C.baseReco[nsub];
+    C.accuQ.assign(nsub, Stencil());
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int64_t tv = 0; tv < nsub; ++tv) C.accuQ[tv] = accumulated_stencil(multGrid[tv], doleMcsc[tv]);
+    // ---- ficoCotr[ts] (side 0): contact index -> selected level-d nodes (MCONTACT.h:900-959)
+    std::vector<Csr> fico(nint);
+    std::vector<int64_t> contReco(nint + 1, 0);
+    for (int64_t ts = 0; ts < nint; ++ts) {
+        const Interface& itf = searCont[ts];
+        const Stencil& Q0 = C.accuQ[itf.body[0]];
+        const auto& nc0 = itf.nodeCont[0];
+        std::vector<int64_t> newc(Q0.nc, -1);
+        for (int64_t k = 0; k < (int64_t)nc0.size(); ++k)
+            for (int64_t q = Q0.ptr[nc0[k]]; q < Q0.ptr[nc0[k] + 1]; ++q) newc[Q0.col[q]] = 0;
+        int64_t ncc = 0;
+        for (int64_t c = 0; c < Q0.nc; ++c)
+            if (newc[c] == 0) newc[c] = ncc++;
+        const int comp = itf.comp();
+        std::vector<Trip> t;
+        for (int64_t k = 0; k < (int64_t)nc0.size(); ++k)
+            for (int64_t q = Q0.ptr[nc0[k]]; q < Q0.ptr[nc0[k] + 1]; ++q)
+                for (int j = 0; j < comp; ++j) t.push_back({comp * k + j, comp * newc[Q0.col[q]] + j, Q0.w[q]});
+        fico[ts] = from_triplets(comp * (int64_t)nc0.size(), comp * ncc, t);
+        contReco[ts + 1] = contReco[ts] + comp * ncc;
+    }
+    const int64_t n = N + contReco[nint];
+    C.n = n;
+    std::vector<Trip> coup;
+    for (int64_t tv = 0; tv < nsub; ++tv) append(coup, multGrid[tv].consStif(doleMcsc[tv]), C.baseReco[tv], C.baseReco[tv]);
+    C.globTran_L.assign(nint, {});
+    C.globTran_pena_L.assign(nint, {});
+    C.globTran_D_L.assign(nint, {});
+    std::vector<std::vector<Trip>> coup_side(2 * nint);
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int64_t task = 0; task < 2 * nint; ++task) {
+        const int64_t ts = task / 2;
+        const int tv = (int)(task % 2);
+        const Interface& itf = searCont[ts];
+        const int64_t b = itf.body[tv];
+        const MULTIGRID& g = multGrid[b];
+        const int comp = itf.comp();
+        const int64_t N3 = 3 * g.numNodes();
+        const int64_t m0 = itf.mside(0), mv = itf.mside(tv);
+        std::vector<int64_t> c0(multGrid[itf.body[0]].numNodes(), -1), cv(g.numNodes(), -1);
+        for (size_t k = 0; k < itf.nodeCont[0].size(); ++k) c0[itf.nodeCont[0][k]] = (int64_t)k;
+        for (size_t k = 0; k < itf.nodeCont[tv].size(); ++k) cv[itf.nodeCont[tv][k]] = (int64_t)k;
+        std::vector<Trip> disp, unba, tran, tranp, tranD;
+        for (const auto& p : itf.ip) {
+            const double* Me = p.shap[tv];
+            const double* M0 = p.shap[0];
+            const double* nv = p.basis[0];
+            double G[9], GP[9];  // T^T T, T^T P T (T rows = basiVect, P = diag(penN, penF, penF))
+            const double pen[3] = {itf.penN, itf.penF, itf.penF};
+            for (int i = 0; i < 3; ++i)
+                for (int j = 0; j < 3; ++j) {
+                    double x = 0.0, y = 0.0;
+                    for (int c = 0; c < 3; ++c) {
+                        x += p.basis[c][i] * p.basis[c][j];
+                        y += p.basis[c][i] * pen[c] * p.basis[c][j];
+                    }
+                    G[3 * i + j] = x;
+                    GP[3 * i + j] = y;
+                }
+            for (int a = 0; a < 4; ++a) {
+                const int64_t node_a = p.node[tv][a], ca0 = c0[p.node[0][a]];
+                for (int bb = 0; bb < 4; ++bb) {
+                    const int64_t cb0 = c0[p.node[0][bb]], cbv = cv[p.node[tv][bb]];
+                    if (comp == 1) {
+                        // inteCoup: w pn N_e^T n^T M_0e (MCONTACT.h:1010-1044), unbaMatr w pn M_0e^T M_0e
+                        for (int k = 0; k < 3; ++k)
+                            disp.push_back({3 * node_a + k, cb0, p.w * itf.penN * Me[a] * nv[k] * M0[bb]});
+                        unba.push_back({ca0, cb0, p.w * itf.penN * M0[a] * M0[bb]});
+                        // globTran: w M_0e^T M_e (MCONTACT.h:1249-1268); globTran_D: w pn M_0e^T n N_e
+                        tran.push_back({ca0, cbv, p.w * M0[a] * Me[bb]});
+                        for (int k = 0; k < 3; ++k)
+                            tranD.push_back({ca0, 3 * p.node[tv][bb] + k, p.w * itf.penN * M0[a] * nv[k] * Me[bb]});
+                    } else {
+                        for (int i = 0; i < 3; ++i)
+                            for (int j = 0; j < 3; ++j) {
+                                disp.push_back({3 * node_a + i, 3 * cb0 + j, p.w * Me[a] * M0[bb] * GP[3 * i + j]});
+                                unba.push_back({3 * ca0 + i, 3 * cb0 + j, p.w * M0[a] * M0[bb] * GP[3 * i + j]});
+                                tran.push_back({3 * ca0 + i, 3 * cbv + j, p.w * M0[a] * Me[bb] * G[3 * i + j]});
+                                tranp.push_back({3 * ca0 + i, 3 * cbv + j, p.w * M0[a] * Me[bb] * GP[3 * i + j]});
+                                tranD.push_back({3 * ca0 + i, 3 * p.node[tv][bb] + j, p.w * M0[a] * Me[bb] * GP[3 * i + j]});
+                            }
+                    }
+                }
+            }
+        }
+        const Csr& F = fico[ts];
+        const Csr FT = transpose_csr(F);
+        // dispUnba -> level-d free rows: C_d (Q (x) I3)^T (MCONTACT.h:1045-1054)
+        const Csr QI = nodal_prolong(g, C.accuQ[b], doleMcsc[b], nullptr);
+        const Csr D = spgemm(transpose_csr(QI), spgemm(from_triplets(N3, m0, disp), F));
+        std::vector<Trip>& out = coup_side[task];
+        const int64_t cr = N + contReco[ts];
+        for (int64_t r = 0; r < D.nrow; ++r)
+            for (int64_t k = D.ptr[r]; k < D.ptr[r + 1]; ++k) {
+                out.push_back({C.baseReco[b] + r, cr + D.col[k], -D.val[k]});
+                out.push_back({cr + D.col[k], C.baseReco[b] + r, -D.val[k]});
+            }
+        append(out, spgemm(FT, spgemm(from_triplets(m0, m0, unba), F)), cr, cr);
+        // globTran / globTran_pena / globTran_D (MCONTACT.h:1235-1534): rows N + contReco[ts] + i
+        auto place = [&](const Csr& A, int64_t ncol) {
+            std::vector<Trip> t;
+            append(t, spgemm(FT, A), cr, 0);
+            return from_triplets(n, ncol, t);
+        };
+        C.globTran_L[ts][tv] = place(from_triplets(m0, mv, tran), mv);
+        if (comp == 1) {
+            C.globTran_pena_L[ts][tv] = C.globTran_L[ts][tv];
+            for (auto& v : C.globTran_pena_L[ts][tv].val) v *= itf.penN;
+        } else
+            C.globTran_pena_L[ts][tv] = place(from_triplets(m0, mv, tranp), mv);
+        C.globTran_D_L[ts][tv] = place(from_triplets(m0, N3, tranD), N3);
+    }
+    for (auto& t : coup_side) coup.insert(coup.end(), t.begin(), t.end());
+    C.globCoup_1 = from_triplets(n, n, coup);
+    C.globForc_1.assign(n, 0.0);
+    // accuProl[tv] = C_L (Q (x) I3) C_d^T (MCONTACT.h:864-872)
+    for (int64_t tv = 0; tv < nsub; ++tv)
+        C.accuProl_full.push_back(rows_to_free(multGrid[tv], nodal_prolong(multGrid[tv], C.accuQ[tv], doleMcsc[tv], nullptr)));
+    C.ready = true;
+    coarse = std::move(C);
+}
+
+}  // namespace ddpca

@@ -69,10 +69,13 @@ def test_oracle_on_host_coarse_operators(ddpca, oracle, case):
         assert np.linalg.norm(u - ur) <= 1e-8 * np.linalg.norm(ur)
 
 
-def test_set_coarse_rejects_multiscale(ddpca):
+def test_set_coarse_rejects_bad_settings(ddpca):
+    """muscSett is 0, 1 (MULTISCALE) or 2 (MULTISCALE_1): both bits at once, or out of range, is
+    refused (the reference's loop applies either correction, MCONTACT.h:2539-2612)."""
     P = ddpca.Problem(*CASE_PARAMS["twoblock_f0_m2"])
-    with pytest.raises(ddpca.DdpcaError):
-        P.set_coarse(1)
+    for bad in (3, 4, -1):
+        with pytest.raises(ddpca.DdpcaError):
+            P.set_coarse(bad)
 
 
 def test_rank_local_build_matches_global(ddpca):
@@ -109,3 +112,37 @@ def test_rank_local_build_matches_global(ddpca):
                 if owner[body[s]] == rank:
                     B = full.csr("globTran_1", 2 * ts + s)
                     assert abs(P.csr("globTran_1", 2 * ts + s) - B).max() <= 1e-12 * abs(B).max()
+
+
+@pytest.mark.parametrize("case", ["twoblock_f0_m1", "twoblock_f3_m1"])
+def test_latin_operators_match_reference(ddpca, case):
+    """LATIN-type coarse space (MCONTACT::MULTISCALE, MCONTACT.h:898-1536, muscSett = 1), host
+    restatement (multiscale.cpp MCONTACT::MULTISCALE) against the reference's own operators:
+    globCoup (displacement blocks + coarse contact unknowns), globTran / globTran_pena /
+    globTran_D per side at 1e-12 of their largest entry, accuProl exactly."""
+    g = golden(case)
+    P = ddpca.Problem(*CASE_PARAMS[case])
+    for ts in range(P.nint):
+        fric, pn, pf = g[f"if{ts}_param"]
+        P.set_ips(ts, g[f"if{ts}_ip_node"], g[f"if{ts}_ip_shap"], g[f"if{ts}_ip_basis"], g[f"if{ts}_ip_gap"],
+                  g[f"if{ts}_ip_w"], fric, pn, pf)
+    P.set_coarse(1, [int(x) for x in g["doleMcsc"]])
+    P.ESTABLISH()
+    assert np.array_equal(P.array("baseReco"), g["baseReco"])
+    assert_close(P.csr("globCoup_1"), ref_csr(g, "globCoup"))
+    for ts in range(P.nint):
+        for s in range(2):
+            for name in ("globTran", "globTran_pena", "globTran_D"):
+                assert_close(P.csr(name, 2 * ts + s), ref_csr(g, f"if{ts}_s{s}_{name}"))
+    for tv in range(P.nsub):
+        A, B = P.csr("accuProl", tv), ref_csr(g, f"sd{tv}_accuProl")
+        assert A.shape == B.shape and abs(A - B).max() == 0.0
+
+
+def test_latin_needs_every_subdomain(ddpca):
+    """The host MULTISCALE is assembled on a process that holds every subdomain; a rank-local
+    build refuses it (multi-rank runs hand the caller's operators over instead)."""
+    P = ddpca.Problem(*CASE_PARAMS["twoblock_f0_m1"])
+    P.set_coarse(1, [1] * P.nsub)
+    with pytest.raises(ddpca.DdpcaError):
+        P.ESTABLISH(owner=[0, 1], rank=0)

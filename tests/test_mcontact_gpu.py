@@ -59,10 +59,11 @@ def test_admm_matches_reference(ddpca, gpu, case, warm, f32):
 
 
 @pytest.mark.parametrize("f32", [0, 1])
-@pytest.mark.parametrize("case", ["twoblock_f0_m2", "twoblock_f3_m2", "beam_dd_m2"])
+@pytest.mark.parametrize("case", ["twoblock_f0_m2", "twoblock_f3_m2", "beam_dd_m2", "twoblock_f0_m1", "twoblock_f3_m1"])
 def test_admm_coarse_space_matches_reference(ddpca, gpu, case, f32):
     """Interface-eliminated coarse space (muscSett = 2, doleMcsc = 1; MCONTACT.h:2578-2612) on
-    the device: converged runs of 2 / 24 / 36 ADMM iterations, same bar as without it."""
+    the device: converged runs of 2 / 24 / 36 ADMM iterations, same bar as without it.  *_m1:
+    the LATIN-type space (muscSett = 1, MCONTACT.h:2540-2576) from the host MULTISCALE."""
     g, P, mc, n = _run(ddpca, case, precond_fp32=f32)
     ref_iters = len(g["resuMoni"])
     assert abs(n - ref_iters) <= 1, (n, ref_iters)
