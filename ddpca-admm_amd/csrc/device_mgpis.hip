@@ -538,18 +538,27 @@ __global__ __launch_bounds__(kBlock) void k_pcg_init_warm(const double* b, doubl
 }
 
 // x += alpha p, r -= alpha q, partial ||r||^2
+// x += alpha p, r -= alpha q, partial ||r||^2.  One wavefront per 64-node chunk walks the chunk's
+// 192 doubles flat (lane, lane + 64, lane + 128): every load is a contiguous 512-B wave access
+// instead of three 24-B-strided ones.
 __global__ __launch_bounds__(kBlock) void k_axpy(double* x, double* r, const double* p, const double* q,
                                                  const PcgScal* sc, double* partial, int64_t nn, const int32_t* csub) {
-    NODE_PROLOGUE(nn, csub, sc)
+    const int64_t c = (int64_t)blockIdx.x * (kBlock / kWave) + (threadIdx.x >> 6);
+    if (c * kChunk >= nn) return;
+    const int sub = csub[c];
+    if (stopped(sc, sub)) return;
     const double al = sc[sub].alpha;
+    const int64_t base = c * 3 * kChunk + (threadIdx.x & 63);
     double s = 0.0;
-    for (int a = 0; a < 3; ++a) {
-        x[3 * i + a] += al * p[3 * i + a];
-        const double v = r[3 * i + a] - al * q[3 * i + a];
-        r[3 * i + a] = v;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        const int64_t k = base + j * kChunk;
+        x[k] += al * p[k];
+        const double v = r[k] - al * q[k];
+        r[k] = v;
         s += v * v;
     }
-    chunk_partial(s, partial, i >> 6);
+    chunk_partial(s, partial, c);
 }
 
 // z = D^-1 r (diagonal preconditioner, DIAG_PREC), partial r^T z
