@@ -257,13 +257,21 @@ __global__ __launch_bounds__(256) void k_mcg_fin(int what, const double* partial
     PcgScal* sc = scv + sys;
     if (what != kMcgInit && sc->done) return;
     __shared__ double r0[4], r1[4];
-    double a = 0.0, b = 0.0;
-    for (int64_t k = cb[sys] + threadIdx.x; k < cb[sys + 1]; k += 256) {
-        a += partial[2 * k];
-        b += partial[2 * k + 1];
+    // four independent accumulator pairs per thread (loads in flight together), fixed order
+    double av[4] = {0.0, 0.0, 0.0, 0.0}, bv[4] = {0.0, 0.0, 0.0, 0.0};
+    const int64_t k1 = cb[sys + 1];
+    for (int64_t k = cb[sys] + threadIdx.x; k < k1; k += 4 * 256) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int64_t q = k + 256 * u;
+            if (q < k1) {
+                av[u] += partial[2 * q];
+                bv[u] += partial[2 * q + 1];
+            }
+        }
     }
-    a = wsum(a);
-    b = wsum(b);
+    double a = wsum((av[0] + av[1]) + (av[2] + av[3]));
+    double b = wsum((bv[0] + bv[1]) + (bv[2] + bv[3]));
     if ((threadIdx.x & 63) == 0) {
         r0[threadIdx.x >> 6] = a;
         r1[threadIdx.x >> 6] = b;

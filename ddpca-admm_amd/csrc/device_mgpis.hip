@@ -585,27 +585,40 @@ __global__ __launch_bounds__(kBlock) void k_dot(const double* x, const double* y
 
 // Scalar updates of the PCG recurrence: one workgroup per subdomain, fixed summation order
 // over that subdomain's chunk partials.  Stop-state changes are mirrored to host memory.
-__global__ __launch_bounds__(kBlock) void k_fin(int what, const double* partial, const double* partial2,
-                                                const int64_t* cb, PcgScal* scv, PcgMirror* mirror) {
+constexpr int kFinT = 1024;  // threads of k_fin: a subdomain's ~6400 fine chunk partials in ~2 loads each
+__global__ __launch_bounds__(kFinT) void k_fin(int what, const double* partial, const double* partial2,
+                                               const int64_t* cb, PcgScal* scv, PcgMirror* mirror) {
     const int sub = blockIdx.x;
     PcgScal* sc = scv + sub;
     if (what != kFinInit && what != kFinInitWarm && sc->done) return;
-    __shared__ double red[kBlock / kWave], red2[kBlock / kWave];
-    double s = 0.0, s2 = 0.0;
-    for (int64_t k = cb[sub] + threadIdx.x; k < cb[sub + 1]; k += kBlock) {
-        s += partial[k];
-        if (what == kFinInitWarm) s2 += partial2[k];
+    __shared__ double red[kFinT / kWave], red2[kFinT / kWave];
+    // four independent accumulators per thread (loads in flight together), fixed combine order
+    double a[4] = {0.0, 0.0, 0.0, 0.0}, b[4] = {0.0, 0.0, 0.0, 0.0};
+    const int64_t k0 = cb[sub], k1 = cb[sub + 1];
+    for (int64_t k = k0 + threadIdx.x; k < k1; k += 4 * kFinT) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int64_t q = k + (int64_t)u * kFinT;
+            if (q < k1) {
+                a[u] += partial[q];
+                if (what == kFinInitWarm) b[u] += partial2[q];
+            }
+        }
     }
-    s = wave_sum(s);
-    s2 = wave_sum(s2);
+    double s = wave_sum((a[0] + a[1]) + (a[2] + a[3]));
+    double s2 = wave_sum((b[0] + b[1]) + (b[2] + b[3]));
     if ((threadIdx.x & 63) == 0) {
         red[threadIdx.x >> 6] = s;
         red2[threadIdx.x >> 6] = s2;
     }
     __syncthreads();
     if (threadIdx.x != 0) return;
-    s = (red[0] + red[1]) + (red[2] + red[3]);
-    s2 = (red2[0] + red2[1]) + (red2[2] + red2[3]);
+    s = 0.0;
+    s2 = 0.0;
+    for (int w = 0; w < kFinT / kWave; w += 4) {
+        s += (red[w] + red[w + 1]) + (red[w + 2] + red[w + 3]);
+        s2 += (red2[w] + red2[w + 1]) + (red2[w + 2] + red2[w + 3]);
+    }
     const int was_done = sc->done;
     if (what == kFinInit || what == kFinInitWarm) {
         const double bb = what == kFinInit ? s : s2;
@@ -1763,12 +1776,12 @@ void MgpisDevice::enqueue_iteration(int prec, bool timed) {
     if (timed) DDPCA_HIP(hipEventRecord(ev_k0, stream));
     launch_sell<kPcg, false, true>(kVal64, a, stream);
     if (timed) DDPCA_HIP(hipEventRecord(ev_k1, stream));
-    hipLaunchKernelGGL(k_fin, dim3(nsub), dim3(kBlock), 0, stream, (int)kFinAlpha, partial.p, nullptr, fin_cb.p, sc.p, mirror.dev);
+    hipLaunchKernelGGL(k_fin, dim3(nsub), dim3(kFinT), 0, stream, (int)kFinAlpha, partial.p, nullptr, fin_cb.p, sc.p, mirror.dev);
     hipLaunchKernelGGL(k_axpy, dim3(nblk), dim3(kBlock), 0, stream, xs.p, rs.p, ps.p, qs.p, sc.p, partial.p, L.nn, L.csub.p);
-    hipLaunchKernelGGL(k_fin, dim3(nsub), dim3(kBlock), 0, stream, (int)kFinRR, partial.p, nullptr, fin_cb.p, sc.p, mirror.dev);
+    hipLaunchKernelGGL(k_fin, dim3(nsub), dim3(kFinT), 0, stream, (int)kFinRR, partial.p, nullptr, fin_cb.p, sc.p, mirror.dev);
     if (prec == 1) vcycle(rs.p, zs.p, true);
     else hipLaunchKernelGGL(k_diag, dim3(nblk), dim3(kBlock), 0, stream, rs.p, L.dinv.p, zs.p, partial.p, L.nn, L.csub.p, sc.p);
-    hipLaunchKernelGGL(k_fin, dim3(nsub), dim3(kBlock), 0, stream, (int)kFinBeta, partial.p, nullptr, fin_cb.p, sc.p, mirror.dev);
+    hipLaunchKernelGGL(k_fin, dim3(nsub), dim3(kFinT), 0, stream, (int)kFinBeta, partial.p, nullptr, fin_cb.p, sc.p, mirror.dev);
 }
 
 // graph_[prec]: iters_per_graph PCG iterations captured once and replayed.
@@ -1799,7 +1812,7 @@ void MgpisDevice::pcg_begin(int prec, double rtol, const std::vector<int64_t>& m
     const int nblk = ceil_div(L.nn, kBlock);
     if (!warm) {
         hipLaunchKernelGGL(k_pcg_init, dim3(nblk), dim3(kBlock), 0, stream, bs.p, xs.p, rs.p, ps.p, qs.p, partial.p, L.nn);
-        hipLaunchKernelGGL(k_fin, dim3(nsub), dim3(kBlock), 0, stream, (int)kFinInit, partial.p, nullptr, fin_cb.p, sc.p, mirror.dev);
+        hipLaunchKernelGGL(k_fin, dim3(nsub), dim3(kFinT), 0, stream, (int)kFinInit, partial.p, nullptr, fin_cb.p, sc.p, mirror.dev);
     } else {
         double* partial2 = partial.p + L.nch;
         hipLaunchKernelGGL(k_pcg_init_warm, dim3(nblk), dim3(kBlock), 0, stream, bs.p, ps.p, qs.p, partial2, L.nn);
@@ -1809,11 +1822,11 @@ void MgpisDevice::pcg_begin(int prec, double rtol, const std::vector<int64_t>& m
         a.y = rs.p;
         a.partial = partial.p;
         launch_sell<kResid, false, true>(kVal64, a, stream);
-        hipLaunchKernelGGL(k_fin, dim3(nsub), dim3(kBlock), 0, stream, (int)kFinInitWarm, partial.p, partial2, fin_cb.p, sc.p, mirror.dev);
+        hipLaunchKernelGGL(k_fin, dim3(nsub), dim3(kFinT), 0, stream, (int)kFinInitWarm, partial.p, partial2, fin_cb.p, sc.p, mirror.dev);
     }
     if (prec == 1) vcycle(rs.p, zs.p, true);
     else hipLaunchKernelGGL(k_diag, dim3(nblk), dim3(kBlock), 0, stream, rs.p, L.dinv.p, zs.p, partial.p, L.nn, L.csub.p, sc.p);
-    hipLaunchKernelGGL(k_fin, dim3(nsub), dim3(kBlock), 0, stream, (int)kFinBeta0, partial.p, nullptr, fin_cb.p, sc.p, mirror.dev);
+    hipLaunchKernelGGL(k_fin, dim3(nsub), dim3(kFinT), 0, stream, (int)kFinBeta0, partial.p, nullptr, fin_cb.p, sc.p, mirror.dev);
     sample_pending_ = false;
     if (time_kernel) {
         // first iteration eagerly, with HIP events around its fine-level SpMV on this stream
