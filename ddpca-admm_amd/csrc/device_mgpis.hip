@@ -419,6 +419,9 @@ __global__ __launch_bounds__(kBlock) void k_jac0(const double* b, const MT* minv
 // b_c = mask_c (sum_children w r_f[child]), the coarse node's own fine copy first with w = 1;
 // optionally x_c = omega M b_c (CHEB: d_c too).  Children in SELL-64 layout: slot k of chunk c
 // at (roff[c] + k) * 64 + lane, so index and weight loads are contiguous wave accesses.
+// 1/k for the uniform-averaging stencils (weight = 1 / number of parents; k_prolong<true>)
+__constant__ double kInvCount[9] = {0.0, 1.0, 0.5, 1.0 / 3.0, 0.25, 0.2, 1.0 / 6.0, 1.0 / 7.0, 0.125};
+
 template <bool INIT, bool BJ, bool SETD, typename MT = double>
 __global__ __launch_bounds__(kBlock) void k_restrict(const double* rf, const int32_t* rslots, const int64_t* roff,
                                                      const int32_t* rcol, const double* rwt, const uint8_t* cmask,
@@ -462,19 +465,28 @@ __global__ __launch_bounds__(kBlock) void k_restrict(const double* rf, const int
 }
 
 // x_f += mask_f (P e_c)
+template <bool UW = false>  // UW: weights 1 / parent count (see k_restrict), pw unread
 __global__ __launch_bounds__(kBlock) void k_prolong(const double* ec, const int32_t* ppar, const double* pw,
                                                     const uint8_t* fmask, double* xf, int64_t nf, const int32_t* csub,
                                                     const PcgScal* sc) {
     NODE_PROLOGUE(nf, csub, sc)
     double e0 = 0.0, e1 = 0.0, e2 = 0.0;
+    int np = 0;
 #pragma unroll
     for (int p = 0; p < 8; ++p) {
         const int32_t c = ppar[p * nf + i];
         if (c < 0) break;
-        const double w = pw[p * nf + i];
+        const double w = UW ? 1.0 : pw[p * nf + i];
         e0 += w * ec[3 * (int64_t)c];
         e1 += w * ec[3 * (int64_t)c + 1];
         e2 += w * ec[3 * (int64_t)c + 2];
+        ++np;
+    }
+    if (UW) {
+        const double w = kInvCount[np];
+        e0 *= w;
+        e1 *= w;
+        e2 *= w;
     }
     const uint8_t m = fmask[i];
     if (m & 1) xf[3 * i] += e0;
@@ -1226,6 +1238,7 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
             const LevelDev& C = lev[l - 1];
             std::vector<int32_t> ppar(8 * L.nn, -1);
             std::vector<double> pw(8 * L.nn, 0.0);
+            bool uw = true;  // every weight == 1 / the node's parent count
             std::vector<std::vector<std::pair<int32_t, double>>> kids(C.nn);
             for (int s = 0; s < nsub; ++s) {
                 const Stencil& st = *subs[s].S[l - 1];
@@ -1247,6 +1260,7 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
                     }
                     if (np > 8) throw ApiError(DDPCA_EINVAL, "more than 8 parents");
                     for (int64_t k = 0; k < np; ++k) {
+                        if (st.w[st.ptr[i] + k] != 1.0 / (double)np) uw = false;
                         const int64_t gc = C.noff[s] + pc[st.col[st.ptr[i] + k]];
                         ppar[k * L.nn + gf] = (int32_t)gc;
                         pw[k * L.nn + gf] = st.w[st.ptr[i] + k];
@@ -1276,7 +1290,8 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
                 }
             }
             L.ppar.upload(ppar);
-            L.pw.upload(pw);
+            L.uw = uw;  // prolongation weights from the parent count (restriction keeps rwt)
+            if (!uw) L.pw.upload(pw);
             L.rslots.upload(rsl);
             L.roff.upload(rof);
             L.rcol.upload(rcol);
@@ -1547,13 +1562,25 @@ SellArgs vc_level_args(const MgpisDevice& D, int level) {
 }
 }  // namespace
 
+namespace {
+// k_restrict over level l -> l-1 with the transfer's weight form (stored or uniform)
+template <bool INIT, bool BJ, bool SETD, typename MT>
+void launch_restrict(const LevelDev& F, int grid, hipStream_t st, const double* rf, const uint8_t* cmask, double* bc,
+                     double* xc, double* dc, const MT* minv, const double* coef, int64_t nc, const int32_t* csub,
+                     const PcgScal* sc) {
+    // stored weights: deriving them from a gathered parent count (as k_prolong<true> does)
+    // measured 58 -> 102 us on the fine level (profiles/r01_transfer_weights.txt)
+    hipLaunchKernelGGL((k_restrict<INIT, BJ, SETD, MT>), dim3(grid), dim3(kBlock), 0, st, rf, F.rslots.p, F.roff.p,
+                       F.rcol.p, F.rwt.p, cmask, bc, xc, dc, minv, coef, nc, csub, sc);
+}
+}  // namespace
+
 void MgpisDevice::restrict_level(int l, const double* rf, double* bc) {
     if (l < 1 || l >= (int)lev.size()) throw ApiError(DDPCA_EINVAL, "restrict_level: level");
     const LevelDev& F = lev[l];
     const LevelDev& C = lev[l - 1];
-    hipLaunchKernelGGL((k_restrict<false, false, false, double>), dim3(ceil_div(C.nn, kBlock)), dim3(kBlock), 0, stream, rf,
-                       F.rslots.p, F.roff.p, F.rcol.p, F.rwt.p, C.mask.p, bc, nullptr, nullptr, nullptr, nullptr, C.nn,
-                       C.csub.p, nullptr);
+    launch_restrict<false, false, false, double>(F, ceil_div(C.nn, kBlock), stream, rf, C.mask.p, bc, nullptr, nullptr,
+                                                 nullptr, nullptr, C.nn, C.csub.p, nullptr);
 }
 
 void MgpisDevice::spmv(int level, const double* x, double* y, bool vc_op) {
@@ -1713,21 +1740,21 @@ void MgpisDevice::vcycle(const double* rin, double* zout, bool dot) {
         const int grid = ceil_div(C.nn, kBlock);
         const double* cf = c > 0 ? coef(c, 0) : nullptr;
         if (c == cl)
-            hipLaunchKernelGGL((k_restrict<false, false, false, double>), dim3(grid), dim3(kBlock), 0, stream, F.r.p, F.rslots.p, F.roff.p, F.rcol.p, F.rwt.p, C.mask.p, C.b.p, nullptr, nullptr, nullptr, nullptr, C.nn, C.csub.p, scp);
+            launch_restrict<false, false, false, double>(F, grid, stream, F.r.p, C.mask.p, C.b.p, nullptr, nullptr, nullptr, nullptr, C.nn, C.csub.p, scp);
         else if (vc_type(c) != kVal64) {
             const float* m = C.minv32.p;
             if (cheb)
-                hipLaunchKernelGGL((k_restrict<true, true, true, float>), dim3(grid), dim3(kBlock), 0, stream, F.r.p, F.rslots.p, F.roff.p, F.rcol.p, F.rwt.p, C.mask.p, C.b.p, cur[c], C.d.p, m, cf, C.nn, C.csub.p, scp);
+                launch_restrict<true, true, true, float>(F, grid, stream, F.r.p, C.mask.p, C.b.p, cur[c], C.d.p, m, cf, C.nn, C.csub.p, scp);
             else if (bj)
-                hipLaunchKernelGGL((k_restrict<true, true, false, float>), dim3(grid), dim3(kBlock), 0, stream, F.r.p, F.rslots.p, F.roff.p, F.rcol.p, F.rwt.p, C.mask.p, C.b.p, cur[c], nullptr, m, cf, C.nn, C.csub.p, scp);
+                launch_restrict<true, true, false, float>(F, grid, stream, F.r.p, C.mask.p, C.b.p, cur[c], nullptr, m, cf, C.nn, C.csub.p, scp);
             else
-                hipLaunchKernelGGL((k_restrict<true, false, false, float>), dim3(grid), dim3(kBlock), 0, stream, F.r.p, F.rslots.p, F.roff.p, F.rcol.p, F.rwt.p, C.mask.p, C.b.p, cur[c], nullptr, m, cf, C.nn, C.csub.p, scp);
+                launch_restrict<true, false, false, float>(F, grid, stream, F.r.p, C.mask.p, C.b.p, cur[c], nullptr, m, cf, C.nn, C.csub.p, scp);
         } else if (cheb)
-            hipLaunchKernelGGL((k_restrict<true, true, true>), dim3(grid), dim3(kBlock), 0, stream, F.r.p, F.rslots.p, F.roff.p, F.rcol.p, F.rwt.p, C.mask.p, C.b.p, cur[c], C.d.p, C.minv.p, cf, C.nn, C.csub.p, scp);
+            launch_restrict<true, true, true, double>(F, grid, stream, F.r.p, C.mask.p, C.b.p, cur[c], C.d.p, C.minv.p, cf, C.nn, C.csub.p, scp);
         else if (bj)
-            hipLaunchKernelGGL((k_restrict<true, true, false>), dim3(grid), dim3(kBlock), 0, stream, F.r.p, F.rslots.p, F.roff.p, F.rcol.p, F.rwt.p, C.mask.p, C.b.p, cur[c], nullptr, C.minv.p, cf, C.nn, C.csub.p, scp);
+            launch_restrict<true, true, false, double>(F, grid, stream, F.r.p, C.mask.p, C.b.p, cur[c], nullptr, C.minv.p, cf, C.nn, C.csub.p, scp);
         else
-            hipLaunchKernelGGL((k_restrict<true, false, false>), dim3(grid), dim3(kBlock), 0, stream, F.r.p, F.rslots.p, F.roff.p, F.rcol.p, F.rwt.p, C.mask.p, C.b.p, cur[c], nullptr, C.minv.p, cf, C.nn, C.csub.p, scp);
+            launch_restrict<true, false, false, double>(F, grid, stream, F.r.p, C.mask.p, C.b.p, cur[c], nullptr, C.minv.p, cf, C.nn, C.csub.p, scp);
     }
     if (ainv32.p) hipLaunchKernelGGL(k_coarse<float>, dim3(ceil_div(3 * lev[cl].nn, 4)), dim3(kBlock), 0, stream, ainv32.p, aoff.p, c_noff.p,
                            c_n.p, lev[cl].b.p, cur[cl], 3 * lev[cl].nn, lev[cl].csub.p, scp);
@@ -1736,7 +1763,9 @@ void MgpisDevice::vcycle(const double* rin, double* zout, bool dot) {
     // ---- ascend
     for (int l = cl + 1; l <= Lf; ++l) {
         const LevelDev& F = lev[l];
-        hipLaunchKernelGGL(k_prolong, dim3(ceil_div(F.nn, kBlock)), dim3(kBlock), 0, stream, cur[l - 1], F.ppar.p, F.pw.p,
+        if (F.uw) hipLaunchKernelGGL(k_prolong<true>, dim3(ceil_div(F.nn, kBlock)), dim3(kBlock), 0, stream, cur[l - 1], F.ppar.p, F.pw.p,
+                           F.mask.p, cur[l], F.nn, F.csub.p, scp);
+        else hipLaunchKernelGGL(k_prolong<false>, dim3(ceil_div(F.nn, kBlock)), dim3(kBlock), 0, stream, cur[l - 1], F.ppar.p, F.pw.p,
                            F.mask.p, cur[l], F.nn, F.csub.p, scp);
         // post-smoothing restarts the smoother (Chebyshev recurrence) from the prolongated iterate
         smooth(l, 0, nu, dot && l == Lf);

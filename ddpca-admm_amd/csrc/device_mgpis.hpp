@@ -98,7 +98,9 @@ struct LevelDev {
     std::vector<double> lmax;  // per subdomain, lambda_max(M K)
     // transfer from level l-1 (batch-global indices)
     DevBuf<int32_t> ppar;  // 8 x nn, slot-major, -1 = unused
-    DevBuf<double> pw;
+    DevBuf<double> pw;     // weights (empty when uw)
+    bool uw = false;       // uniform averaging: prolongation weight = 1 / parent count (nested
+                           // refinement), computed in k_prolong instead of read
     // restriction: SELL-64 over the coarse nodes of level l-1 (chunk = 64 coarse nodes, lane =
     // node, slot k = k-th child: own fine copy first, padding = weight 0)
     DevBuf<int32_t> rslots;  // per coarse chunk
