@@ -1070,7 +1070,9 @@ void build_coarse(ddpca_mcontact& H, Problem& P) {
     // dense rows of globCoup_1 (inverted once every rank holds all rows)
     C.dense.assign((size_t)n * n, 0.0);
     std::vector<int64_t> fill_rows = C.own_rows;
-    if (cs.latin && H.rank == 0)  // the coarse contact unknowns' rows: filled by rank 0 only
+    // the coarse contact unknowns' rows: a caller's full operator is filled by rank 0 only; a
+    // rank-local host build holds each rank's share (the all-reduce sums them)
+    if (cs.latin && (cs.rank_local || H.rank == 0))
         for (int64_t r = cs.baseReco.back(); r < n; ++r) fill_rows.push_back(r);
     for (int64_t r : fill_rows)
         for (int64_t k = cs.globCoup_1.ptr[r]; k < cs.globCoup_1.ptr[r + 1]; ++k)

@@ -267,12 +267,15 @@ void MCONTACT::ESTABLISH(const std::vector<uint8_t>* owned) {
     if ((muscSett & 3) == 3)
         throw std::invalid_argument("muscSett: choose one coarse space (1 = MULTISCALE, 2 = MULTISCALE_1)");
     if (muscSett & 1) {
-        if (owned)
-            for (int64_t tv = 0; tv < (int64_t)multGrid.size(); ++tv)
-                if (!(*owned)[tv])
-                    throw std::invalid_argument("muscSett = 1 (MULTISCALE) is built on one process holding every "
-                                                "subdomain; multi-rank runs use ddpca_problem_set_coarse_latin");
-        MULTISCALE();
+        // the dof bookkeeping and prolongation chains of every subdomain (baseReco, the coarse
+        // contact unknowns of every interface's side 0)
+        for (int64_t tv = 0; tv < (int64_t)multGrid.size(); ++tv) {
+            if (mine(tv)) continue;
+            MULTIGRID& g = multGrid[tv];
+            if (g.scalProl.empty()) g.TRANSFER();
+            g.FLAGS();
+        }
+        MULTISCALE(owned);
     }
     if (muscSett & 2) {
         // the dof bookkeeping of every subdomain (baseReco) and the transfer stencils of the

@@ -61,6 +61,7 @@ struct CoarseSpace {
     // globCoup (displacement blocks + coarse contact unknowns, rows >= baseReco[nsub]), the
     // right-hand side is sum over sides of globTran lambda - globTran_pena aux + globTran_D u
     bool latin = false;
+    bool rank_local = false;  // latin rows of the coarse contact unknowns hold this rank's share only
     std::vector<std::array<Csr, 2>> globTran_L, globTran_pena_L, globTran_D_L;  // [ts][s]
 };
 
@@ -75,7 +76,7 @@ public:
     std::vector<int64_t> doleMcsc;         // coarse level per subdomain (MCONTACT.h:23)
     CoarseSpace coarse;
     void MULTISCALE_1(const std::vector<uint8_t>* owned = nullptr);
-    void MULTISCALE();  // LATIN-type (muscSett bit 0), every subdomain built on this process
+    void MULTISCALE(const std::vector<uint8_t>* owned = nullptr);  // LATIN-type (muscSett bit 0)
     Csr globTran_D_1(int64_t tv) const;    // assembled (tests)
     Csr accuProl(int64_t tv) const;        // assembled (tests)
     // ESTABLISH: interface operators, systMass added to each body's stiffness, then

@@ -16,6 +16,7 @@
 #include <numeric>
 #include <stdexcept>
 #include <string>
+#include <unordered_map>
 
 #include "mcontact.hpp"
 
@@ -431,52 +432,73 @@ namespace ddpca {
 // side 0's contact nodes that touch any of them (MCONTACT.h:900-959), one unknown per such
 // level-d node (x3 with friction).  Output in the assembled LATIN form the device consumes
 // (CoarseSpace::latin; the same fields ddpca_problem_set_coarse_latin fills from a caller).
-void MCONTACT::MULTISCALE() {
+void MCONTACT::MULTISCALE(const std::vector<uint8_t>* owned) {
     const int64_t nsub = (int64_t)multGrid.size(), nint = (int64_t)searCont.size();
+    auto mine = [&](int64_t tv) { return !owned || (*owned)[tv] != 0; };
     if ((int64_t)doleMcsc.size() != nsub) doleMcsc.assign(nsub, 0);
     for (int64_t tv = 0; tv < nsub; ++tv) {
         const MULTIGRID& g = multGrid[tv];
-        if (g.freeCount.empty() || g.levelStif.empty())
-            throw std::invalid_argument("MULTISCALE (muscSett bit 0) needs every subdomain established on this "
-                                        "process; multi-rank runs hand the caller's operators over with "
-                                        "ddpca_problem_set_coarse_latin");
+        if (g.freeCount.empty()) throw std::logic_error("MULTISCALE: every subdomain needs its dof flags (FLAGS)");
+        if (mine(tv) && g.levelStif.empty()) throw std::logic_error("MULTISCALE: owned subdomain not established");
         if (doleMcsc[tv] < 0 || doleMcsc[tv] > g.maxiLeve) throw std::invalid_argument("doleMcsc out of range");
     }
     CoarseSpace C;
     C.assembled = true;
     C.latin = true;
-    C.built.assign(nsub, 1);
+    C.rank_local = owned != nullptr;
+    C.built.assign(nsub, 0);
+    for (int64_t tv = 0; tv < nsub; ++tv) C.built[tv] = mine(tv);
     C.baseReco.assign(nsub + 1, 0);
     for (int64_t tv = 0; tv < nsub; ++tv) C.baseReco[tv + 1] = C.baseReco[tv] + multGrid[tv].freeCount[doleMcsc[tv]];
     const int64_t N = C.baseReco[nsub];
+    // prolongation chains: owned bodies and side 0 of every interface (its coarse contact
+    // unknowns number every rank's columns, so each rank derives all of them)
+    std::vector<uint8_t> needQ(nsub, 0);
+    for (int64_t tv = 0; tv < nsub; ++tv) needQ[tv] = mine(tv);
+    for (const auto& itf : searCont) needQ[itf.body[0]] = 1;
     C.accuQ.assign(nsub, Stencil());
 #pragma omp parallel for schedule(dynamic, 1)
-    for (int64_t tv = 0; tv < nsub; ++tv) C.accuQ[tv] = accumulated_stencil(multGrid[tv], doleMcsc[tv]);
+    for (int64_t tv = 0; tv < nsub; ++tv)
+        if (needQ[tv]) C.accuQ[tv] = accumulated_stencil(multGrid[tv], doleMcsc[tv]);
+    // side-0 contact nodes of interfaces this rank did not build (Interface::BUILD's order)
+    std::vector<std::vector<int64_t>> nc0(nint);
+    for (int64_t ts = 0; ts < nint; ++ts) {
+        const Interface& itf = searCont[ts];
+        if (!itf.nodeCont[0].empty() || itf.ip.empty()) {
+            nc0[ts] = itf.nodeCont[0];
+            continue;
+        }
+        std::unordered_map<int64_t, int64_t> seen;
+        for (const auto& p : itf.ip)
+            for (int k = 0; k < 4; ++k)
+                if (seen.emplace(p.node[0][k], (int64_t)seen.size()).second) nc0[ts].push_back(p.node[0][k]);
+    }
     // ---- ficoCotr[ts] (side 0): contact index -> selected level-d nodes (MCONTACT.h:900-959)
     std::vector<Csr> fico(nint);
     std::vector<int64_t> contReco(nint + 1, 0);
     for (int64_t ts = 0; ts < nint; ++ts) {
         const Interface& itf = searCont[ts];
         const Stencil& Q0 = C.accuQ[itf.body[0]];
-        const auto& nc0 = itf.nodeCont[0];
+        const auto& nc0t = nc0[ts];
         std::vector<int64_t> newc(Q0.nc, -1);
-        for (int64_t k = 0; k < (int64_t)nc0.size(); ++k)
-            for (int64_t q = Q0.ptr[nc0[k]]; q < Q0.ptr[nc0[k] + 1]; ++q) newc[Q0.col[q]] = 0;
+        for (int64_t k = 0; k < (int64_t)nc0t.size(); ++k)
+            for (int64_t q = Q0.ptr[nc0t[k]]; q < Q0.ptr[nc0t[k] + 1]; ++q) newc[Q0.col[q]] = 0;
         int64_t ncc = 0;
         for (int64_t c = 0; c < Q0.nc; ++c)
             if (newc[c] == 0) newc[c] = ncc++;
         const int comp = itf.comp();
         std::vector<Trip> t;
-        for (int64_t k = 0; k < (int64_t)nc0.size(); ++k)
-            for (int64_t q = Q0.ptr[nc0[k]]; q < Q0.ptr[nc0[k] + 1]; ++q)
+        for (int64_t k = 0; k < (int64_t)nc0t.size(); ++k)
+            for (int64_t q = Q0.ptr[nc0t[k]]; q < Q0.ptr[nc0t[k] + 1]; ++q)
                 for (int j = 0; j < comp; ++j) t.push_back({comp * k + j, comp * newc[Q0.col[q]] + j, Q0.w[q]});
-        fico[ts] = from_triplets(comp * (int64_t)nc0.size(), comp * ncc, t);
+        fico[ts] = from_triplets(comp * (int64_t)nc0t.size(), comp * ncc, t);
         contReco[ts + 1] = contReco[ts] + comp * ncc;
     }
     const int64_t n = N + contReco[nint];
     C.n = n;
     std::vector<Trip> coup;
-    for (int64_t tv = 0; tv < nsub; ++tv) append(coup, multGrid[tv].consStif(doleMcsc[tv]), C.baseReco[tv], C.baseReco[tv]);
+    for (int64_t tv = 0; tv < nsub; ++tv)
+        if (mine(tv)) append(coup, multGrid[tv].consStif(doleMcsc[tv]), C.baseReco[tv], C.baseReco[tv]);
     C.globTran_L.assign(nint, {});
     C.globTran_pena_L.assign(nint, {});
     C.globTran_D_L.assign(nint, {});
@@ -487,6 +509,7 @@ void MCONTACT::MULTISCALE() {
         const int tv = (int)(task % 2);
         const Interface& itf = searCont[ts];
         const int64_t b = itf.body[tv];
+        if (!mine(b)) continue;  // the side's owner assembles it (the device sums the ranks)
         const MULTIGRID& g = multGrid[b];
         const int comp = itf.comp();
         const int64_t N3 = 3 * g.numNodes();
@@ -569,7 +592,8 @@ void MCONTACT::MULTISCALE() {
     C.globForc_1.assign(n, 0.0);
     // accuProl[tv] = C_L (Q (x) I3) C_d^T (MCONTACT.h:864-872)
     for (int64_t tv = 0; tv < nsub; ++tv)
-        C.accuProl_full.push_back(rows_to_free(multGrid[tv], nodal_prolong(multGrid[tv], C.accuQ[tv], doleMcsc[tv], nullptr)));
+        C.accuProl_full.push_back(mine(tv) ? rows_to_free(multGrid[tv], nodal_prolong(multGrid[tv], C.accuQ[tv], doleMcsc[tv], nullptr))
+                                           : Csr());
     C.ready = true;
     coarse = std::move(C);
 }

@@ -166,9 +166,9 @@ int ddpca_problem_set_ips(ddpca_problem_t p, int64_t ts, int64_t n, const int64_
  * establish and applied by every ADMM iteration while tc <= MULT_MAXI (MCONTACT.h:2578-2612);
  * doleMcsc[tv] = coarse level of subdomain tv (NULL = 0).  muscSett = 0 (default): none.
  * muscSett = 1 selects the LATIN-type space (MULTISCALE, MCONTACT.h:898-1536, CYLINDER.h:42;
- * applied as MCONTACT.h:2540-2576), assembled by establish on a process that holds every
- * subdomain (a rank-local establish refuses it: multi-rank runs hand the operators over with
- * ddpca_problem_set_coarse_latin).  3 (both) is DDPCA_EINVAL. */
+ * applied as MCONTACT.h:2540-2576), assembled by establish (rank-locally under
+ * ddpca_problem_establish_owned: each rank its own rows and interface sides, summed on the device
+ * by RCCL).  3 (both) is DDPCA_EINVAL. */
 int ddpca_problem_set_coarse(ddpca_problem_t p, int64_t muscSett, const int64_t* doleMcsc);
 /* MCONTACT::ESTABLISH (MCONTACT.h:181-896); single grids just run TRANSFER / STIF_MATR /
  * CONSTRAINT(1). */

@@ -139,10 +139,40 @@ def test_latin_operators_match_reference(ddpca, case):
         assert A.shape == B.shape and abs(A - B).max() == 0.0
 
 
-def test_latin_needs_every_subdomain(ddpca):
-    """The host MULTISCALE is assembled on a process that holds every subdomain; a rank-local
-    build refuses it (multi-rank runs hand the caller's operators over instead)."""
-    P = ddpca.Problem(*CASE_PARAMS["twoblock_f0_m1"])
-    P.set_coarse(1, [1] * P.nsub)
-    with pytest.raises(ddpca.DdpcaError):
-        P.ESTABLISH(owner=[0, 1], rank=0)
+def test_latin_rank_local_build_matches_global(ddpca):
+    """Rank-local MULTISCALE (muscSett = 1) builds: each rank assembles its own subdomains' rows
+    and its own interface sides' contributions (the coarse contact unknowns of every interface
+    are numbered identically on every rank); summed over the ranks -- what the device's RCCL
+    all-reduce of the dense rows does -- they equal the single-process operator."""
+    args = ("dehw", 2, 2, 2, 1, 2, 0.3)
+    full = ddpca.Problem(*args)
+    full.set_coarse(1, [1] * full.nsub)
+    full.ESTABLISH()
+    base = full.array("baseReco")
+    A = full.csr("globCoup_1").toarray()
+    owner = [0, 1, 0, 1]  # every interface crosses ranks
+    total = np.zeros_like(A)
+    for rank in range(2):
+        P = ddpca.Problem(*args)
+        P.set_coarse(1, [1] * P.nsub)
+        P.ESTABLISH(owner, rank)
+        assert np.array_equal(P.array("baseReco"), base)
+        Ar = P.csr("globCoup_1").toarray()
+        assert Ar.shape == A.shape
+        total += Ar
+        for tv in range(P.nsub):
+            rows = slice(base[tv], base[tv + 1])
+            if owner[tv] == rank:
+                assert np.abs(Ar[rows] - A[rows]).max() <= 1e-12 * np.abs(A).max()
+                B = full.csr("accuProl", tv)
+                assert abs(P.csr("accuProl", tv) - B).max() == 0.0
+            else:
+                assert not Ar[rows].any()
+        for ts in range(P.nint):
+            body = P.array("iface_body", ts)
+            for s in range(2):
+                if owner[body[s]] == rank:
+                    for name in ("globTran", "globTran_pena", "globTran_D"):
+                        B = full.csr(name, 2 * ts + s)
+                        assert abs(P.csr(name, 2 * ts + s) - B).max() <= 1e-12 * abs(B).max()
+    assert np.abs(total - A).max() <= 1e-12 * np.abs(A).max()
