@@ -230,6 +230,31 @@ def test_admm_coarse_space_matches_oracle_on_generated_problem(ddpca, oracle, gp
         assert np.linalg.norm(u - ur) <= 1e-7 * np.linalg.norm(ur)
 
 
+def test_admm_latin_matches_oracle_on_generated_problem(ddpca, oracle, gpu):
+    """The same chain with the LATIN-type coarse space built by the host MULTISCALE (muscSett =
+    1): fixed-k trajectory against the CPU oracle applying the same operators (MCONTACT.h:
+    2540-2576)."""
+    P = ddpca.Problem("dehw", 2, 2, 2, 1, 2, 0.3)
+    P.set_coarse(1, [1] * P.nsub)
+    P.ESTABLISH()
+    mc = ddpca.MCONTACT(P)
+    k = 30
+    assert mc.CONTACT_ANALYSIS(k, check=False) == k
+    subs, ifaces = _oracle_problem(P)
+    coarse = dict(latin=True, globCoup=P.csr("globCoup_1"), baseReco=P.array("baseReco"),
+                  doleMcsc=P.array("doleMcsc"),
+                  globTran=[[P.csr("globTran", 2 * ts + s) for s in range(2)] for ts in range(P.nint)],
+                  globTran_pena=[[P.csr("globTran_pena", 2 * ts + s) for s in range(2)] for ts in range(P.nint)],
+                  globTran_D=[[P.csr("globTran_D", 2 * ts + s) for s in range(2)] for ts in range(P.nint)],
+                  accuProl=[P.csr("accuProl", tv) for tv in range(P.nsub)])
+    res = oracle.admm(subs, ifaces, maxit=k, check=False, coarse=coarse)
+    ok, worst = _rows_close(mc.monitor(), res["rows"], k=k, rtol=1e-6)
+    assert ok, worst
+    for tv in range(P.nsub):
+        u, ur = mc.get("resuDisp", tv), res["u"][tv]
+        assert np.linalg.norm(u - ur) <= 1e-7 * np.linalg.norm(ur)
+
+
 def _oracle_coarse(P):
     return dict(globCoup_1=P.csr("globCoup_1"), globForc_1=P.array("globForc_1"), baseReco=P.array("baseReco"),
                 globTran_1=[[P.csr("globTran_1", 2 * ts + s) for s in range(2)] for ts in range(P.nint)],
