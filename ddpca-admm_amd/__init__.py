@@ -84,6 +84,8 @@ def _declare(L: C.CDLL) -> None:
                                                  C.POINTER(_CsrArg), C.POINTER(_CsrArg), C.POINTER(_CsrArg)]
     L.mgpis_gpu_create.argtypes = [C.c_int, C.c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P,
                                    C.POINTER(MgpisOptions), C.POINTER(_P)]
+    L.mgpis_gpu_create_prol.argtypes = [C.c_int, C.c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P,
+                                        C.POINTER(MgpisOptions), C.POINTER(_P)]
     L.mgpis_gpu_create_bsr3.argtypes = [C.c_int, C.c_int, _P, _P, _P, _P, _P, _P, _P, _P,
                                         C.POINTER(MgpisOptions), C.POINTER(_P)]
     L.mgpis_gpu_solve.argtypes = [_P, _P, _P, C.c_int, C.c_double, C.c_int64, _I64P, _DP]
@@ -416,6 +418,36 @@ class MGPIS:
         o = default_options(**opts)
         _check(lib().mgpis_gpu_create(device, nlev, C.c_void_p(nn), C.c_void_p(nf), fd, kp, kc, kv, sp_, sc_, sw_,
                                       C.byref(o), C.byref(h)))
+        return cls(h)
+
+    @classmethod
+    def from_prol(cls, nnodes: Sequence[int], free_dof: Sequence[np.ndarray], K: Sequence, P: Sequence,
+                  device: int = 0, **opts) -> "MGPIS":
+        """The reference's own MGPIS members: consStif[l] and realProl[l] (scipy CSR, condensed,
+        MGPIS.h:8-38), free_dof[l] = consOper[l]'s nodal dofs; realProl may carry rotated-node
+        blocks (MULTIGRID.h:1141-1181)."""
+        nlev = len(nnodes)
+        keep = []
+
+        def arr(a, dt):
+            a = np.ascontiguousarray(a, dtype=dt)
+            keep.append(a)
+            return a.ctypes.data
+
+        nn = arr(nnodes, np.int64)
+        nf = arr([k.shape[0] for k in K], np.int64)
+        fd = (C.c_void_p * nlev)(*[arr(f, np.int32) for f in free_dof])
+        kp = (C.c_void_p * nlev)(*[arr(k.indptr, np.int64) for k in K])
+        kc = (C.c_void_p * nlev)(*[arr(k.indices, np.int32) for k in K])
+        kv = (C.c_void_p * nlev)(*[arr(k.data, np.float64) for k in K])
+        ns = max(nlev - 1, 1)
+        pp = (C.c_void_p * ns)(*[arr(q.indptr, np.int64) for q in P])
+        pc = (C.c_void_p * ns)(*[arr(q.indices, np.int32) for q in P])
+        pv = (C.c_void_p * ns)(*[arr(q.data, np.float64) for q in P])
+        h = C.c_void_p()
+        o = default_options(**opts)
+        _check(lib().mgpis_gpu_create_prol(device, nlev, C.c_void_p(nn), C.c_void_p(nf), fd, kp, kc, kv, pp, pc, pv,
+                                           C.byref(o), C.byref(h)))
         return cls(h)
 
     def __del__(self):

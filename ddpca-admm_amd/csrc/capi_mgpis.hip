@@ -85,6 +85,39 @@ int mgpis_gpu_create(int device, int nlev, const int64_t* nnodes, const int64_t*
     });
 }
 
+int mgpis_gpu_create_prol(int device, int nlev, const int64_t* nnodes, const int64_t* nfree,
+                          const int32_t* const* free_dof, const int64_t* const* K_ptr, const int32_t* const* K_col,
+                          const double* const* K_val, const int64_t* const* P_ptr, const int32_t* const* P_col,
+                          const double* const* P_val, const mgpis_options_t* opt, mgpis_t* out) {
+    return guarded([&] {
+        if (nlev < 1 || !nnodes || !nfree || !free_dof || !K_ptr || !K_col || !K_val || !out)
+            throw ApiError(DDPCA_EINVAL, "null argument");
+        if (nlev > 1 && (!P_ptr || !P_col || !P_val)) throw ApiError(DDPCA_EINVAL, "null realProl");
+        std::vector<Bsr3> B(nlev);
+        std::vector<Stencil> S(nlev - 1);
+        for (int l = 0; l < nlev; ++l) B[l] = condensed_to_bsr3(nnodes[l], nfree[l], free_dof[l], K_ptr[l], K_col[l], K_val[l]);
+        for (int l = 0; l + 1 < nlev; ++l) {
+            try {
+                S[l] = prol_to_stencil(nnodes[l + 1], nnodes[l], nfree[l + 1], free_dof[l + 1], free_dof[l], P_ptr[l],
+                                       P_col[l], P_val[l]);
+            } catch (const std::invalid_argument& e) {
+                throw ApiError(DDPCA_EINVAL, e.what());
+            }
+        }
+        const int64_t nn = nnodes[nlev - 1];
+        std::vector<uint8_t> fr(3 * nn, 0);
+        for (int64_t r = 0; r < nfree[nlev - 1]; ++r) fr[free_dof[nlev - 1][r]] = 1;
+        std::vector<int64_t> nn_v(nnodes, nnodes + nlev);
+        std::vector<const Bsr3*> Bp;
+        std::vector<const Stencil*> Sp;
+        for (auto& b : B) Bp.push_back(&b);
+        for (auto& s : S) Sp.push_back(&s);
+        auto h = std::make_unique<ddpca_mgpis>();
+        h->dev = single(device, nn_v, Bp, fr, Sp, opt);
+        *out = h.release();
+    });
+}
+
 int mgpis_gpu_create_bsr3(int device, int nlev, const int64_t* nnodes, const int64_t* const* B_ptr,
                           const int32_t* const* B_col, const double* const* B_val, const uint8_t* dof_free,
                           const int64_t* const* S_ptr, const int32_t* const* S_col, const double* const* S_w,

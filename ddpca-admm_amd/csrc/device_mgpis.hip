@@ -494,6 +494,55 @@ __global__ __launch_bounds__(kBlock) void k_prolong(const double* ec, const int3
     if (m & 4) xf[3 * i + 2] += e2;
 }
 
+// Block transfer entries (rotated nodes): x_f += mask_f (B e_c) per fine node that owns one
+// (after k_prolong, whose weight for those entries is 0); thread = fine node.
+__global__ __launch_bounds__(kBlock) void k_prolong_rot(const double* ec, const int32_t* row, const int64_t* ptr,
+                                                        const int32_t* par, const double* blk, const uint8_t* fmask,
+                                                        double* xf, int64_t nr, const int32_t* csub,
+                                                        const PcgScal* sc) {
+    const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (t >= nr) return;
+    const int64_t i = row[t];
+    if (stopped(sc, csub[i >> 6])) return;
+    double e0 = 0.0, e1 = 0.0, e2 = 0.0;
+    for (int64_t k = ptr[t]; k < ptr[t + 1]; ++k) {
+        const double* B = blk + 9 * k;
+        const int64_t c = par[k];
+        const double c0 = ec[3 * c], c1 = ec[3 * c + 1], c2 = ec[3 * c + 2];
+        e0 += B[0] * c0 + B[1] * c1 + B[2] * c2;
+        e1 += B[3] * c0 + B[4] * c1 + B[5] * c2;
+        e2 += B[6] * c0 + B[7] * c1 + B[8] * c2;
+    }
+    const uint8_t m = fmask[i];
+    if (m & 1) xf[3 * i] += e0;
+    if (m & 2) xf[3 * i + 1] += e1;
+    if (m & 4) xf[3 * i + 2] += e2;
+}
+
+// ... and b_c += mask_c (B^T r_f) per coarse node that receives one (after k_restrict).
+__global__ __launch_bounds__(kBlock) void k_restrict_rot(const double* rf, const int32_t* row, const int64_t* ptr,
+                                                         const int32_t* kid, const double* blk, const uint8_t* cmask,
+                                                         double* bc, int64_t nr, const int32_t* csub,
+                                                         const PcgScal* sc) {
+    const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (t >= nr) return;
+    const int64_t j = row[t];
+    if (stopped(sc, csub[j >> 6])) return;
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+    for (int64_t k = ptr[t]; k < ptr[t + 1]; ++k) {
+        const double* B = blk + 9 * k;
+        const int64_t f = kid[k];
+        const double r0 = rf[3 * f], r1 = rf[3 * f + 1], r2 = rf[3 * f + 2];
+        s0 += B[0] * r0 + B[3] * r1 + B[6] * r2;
+        s1 += B[1] * r0 + B[4] * r1 + B[7] * r2;
+        s2 += B[2] * r0 + B[5] * r1 + B[8] * r2;
+    }
+    const uint8_t m = cmask[j];
+    if (m & 1) bc[3 * j] += s0;
+    if (m & 2) bc[3 * j + 1] += s1;
+    if (m & 4) bc[3 * j + 2] += s2;
+}
+
 // x0 = A0^-1 b0 per subdomain, one wavefront per coarse dof row
 template <typename AT = double>
 __global__ __launch_bounds__(kBlock) void k_coarse(const AT* ainv, const int64_t* aoff, const int64_t* noff,
@@ -1289,6 +1338,54 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
                     rwt[q] = real ? kids[j][k].second : 0.0;
                 }
             }
+            // block entries: (fine node, coarse node, 3x3) in batch-global indices, as CSR by
+            // fine node (prolongation) and by coarse node (restriction)
+            struct RotEnt {
+                int32_t f, c;
+                const double* b;
+            };
+            std::vector<RotEnt> ents;
+            for (int s = 0; s < nsub; ++s) {
+                const Stencil& st = *subs[s].S[l - 1];
+                if (st.bent.empty()) continue;
+                const auto& pf = perm[l][s];
+                const auto& pc = perm[l - 1][s];
+                int64_t i = 0;
+                for (size_t q = 0; q < st.bent.size(); ++q) {
+                    const int64_t e = st.bent[q];
+                    while (st.ptr[i + 1] <= e) ++i;
+                    if (st.w[e] != 0.0) throw ApiError(DDPCA_EINVAL, "block transfer entry with a scalar weight");
+                    ents.push_back({(int32_t)(L.noff[s] + pf[i]), (int32_t)(C.noff[s] + pc[st.col[e]]), &st.bval[9 * q]});
+                }
+            }
+            if (!ents.empty()) {
+                auto upload_csr = [&](bool by_fine, int64_t& nr, DevBuf<int32_t>& row, DevBuf<int64_t>& ptr_,
+                                      DevBuf<int32_t>& other, DevBuf<double>& blk) {
+                    std::stable_sort(ents.begin(), ents.end(), [by_fine](const RotEnt& a, const RotEnt& b) {
+                        return by_fine ? a.f < b.f : a.c < b.c;
+                    });
+                    std::vector<int32_t> r, o;
+                    std::vector<int64_t> pt{0};
+                    std::vector<double> bv;
+                    for (size_t q = 0; q < ents.size(); ++q) {
+                        const int32_t key = by_fine ? ents[q].f : ents[q].c;
+                        if (r.empty() || r.back() != key) {
+                            if (!r.empty()) pt.push_back((int64_t)q);
+                            r.push_back(key);
+                        }
+                        o.push_back(by_fine ? ents[q].c : ents[q].f);
+                        bv.insert(bv.end(), ents[q].b, ents[q].b + 9);
+                    }
+                    pt.push_back((int64_t)ents.size());
+                    nr = (int64_t)r.size();
+                    row.upload(r);
+                    ptr_.upload(pt);
+                    other.upload(o);
+                    blk.upload(bv);
+                };
+                upload_csr(true, L.nrot, L.rot_row, L.rot_ptr, L.rot_par, L.rot_blk);
+                upload_csr(false, L.nrotc, L.rotc_row, L.rotc_ptr, L.rotc_kid, L.rotc_blk);
+            }
             L.ppar.upload(ppar);
             L.uw = uw;  // prolongation weights from the parent count (restriction keeps rwt)
             if (!uw) L.pw.upload(pw);
@@ -1581,6 +1678,21 @@ void MgpisDevice::restrict_level(int l, const double* rf, double* bc) {
     const LevelDev& C = lev[l - 1];
     launch_restrict<false, false, false, double>(F, ceil_div(C.nn, kBlock), stream, rf, C.mask.p, bc, nullptr, nullptr,
                                                  nullptr, nullptr, C.nn, C.csub.p, nullptr);
+    rot_restrict(l, rf, bc, nullptr);
+}
+
+void MgpisDevice::rot_restrict(int l, const double* rf, double* bc, const PcgScal* scp) {
+    const LevelDev& F = lev[l];
+    if (!F.nrotc) return;
+    hipLaunchKernelGGL(k_restrict_rot, dim3(ceil_div(F.nrotc, kBlock)), dim3(kBlock), 0, stream, rf, F.rotc_row.p,
+                       F.rotc_ptr.p, F.rotc_kid.p, F.rotc_blk.p, lev[l - 1].mask.p, bc, F.nrotc, lev[l - 1].csub.p, scp);
+}
+
+void MgpisDevice::rot_prolong(int l, const double* ec, double* xf, const PcgScal* scp) {
+    const LevelDev& F = lev[l];
+    if (!F.nrot) return;
+    hipLaunchKernelGGL(k_prolong_rot, dim3(ceil_div(F.nrot, kBlock)), dim3(kBlock), 0, stream, ec, F.rot_row.p,
+                       F.rot_ptr.p, F.rot_par.p, F.rot_blk.p, F.mask.p, xf, F.nrot, F.csub.p, scp);
 }
 
 void MgpisDevice::spmv(int level, const double* x, double* y, bool vc_op) {
@@ -1739,22 +1851,39 @@ void MgpisDevice::vcycle(const double* rin, double* zout, bool dot) {
         const LevelDev& C = lev[c];
         const int grid = ceil_div(C.nn, kBlock);
         const double* cf = c > 0 ? coef(c, 0) : nullptr;
-        if (c == cl)
+        if (F.nrot) {
+            // block transfer entries: plain restriction, the blocks' B^T part, then the first
+            // coarse sweep x_c = omega M b_c that k_restrict otherwise fuses
             launch_restrict<false, false, false, double>(F, grid, stream, F.r.p, C.mask.p, C.b.p, nullptr, nullptr, nullptr, nullptr, C.nn, C.csub.p, scp);
-        else if (vc_type(c) != kVal64) {
-            const float* m = C.minv32.p;
-            if (cheb)
-                launch_restrict<true, true, true, float>(F, grid, stream, F.r.p, C.mask.p, C.b.p, cur[c], C.d.p, m, cf, C.nn, C.csub.p, scp);
+            rot_restrict(l, F.r.p, C.b.p, scp);
+            if (c != cl) {
+                const bool f32c = vc_type(c) != kVal64;
+                const float* m32 = C.minv32.p;
+                if (cheb && f32c) hipLaunchKernelGGL((k_jac0<true, true, float>), dim3(grid), dim3(kBlock), 0, stream, C.b.p, m32, cf, cur[c], C.d.p, C.nn, C.csub.p, scp);
+                else if (bj && f32c) hipLaunchKernelGGL((k_jac0<true, false, float>), dim3(grid), dim3(kBlock), 0, stream, C.b.p, m32, cf, cur[c], nullptr, C.nn, C.csub.p, scp);
+                else if (f32c) hipLaunchKernelGGL((k_jac0<false, false, float>), dim3(grid), dim3(kBlock), 0, stream, C.b.p, m32, cf, cur[c], nullptr, C.nn, C.csub.p, scp);
+                else if (cheb) hipLaunchKernelGGL((k_jac0<true, true>), dim3(grid), dim3(kBlock), 0, stream, C.b.p, C.minv.p, cf, cur[c], C.d.p, C.nn, C.csub.p, scp);
+                else if (bj) hipLaunchKernelGGL((k_jac0<true, false>), dim3(grid), dim3(kBlock), 0, stream, C.b.p, C.minv.p, cf, cur[c], nullptr, C.nn, C.csub.p, scp);
+                else hipLaunchKernelGGL((k_jac0<false, false>), dim3(grid), dim3(kBlock), 0, stream, C.b.p, C.minv.p, cf, cur[c], nullptr, C.nn, C.csub.p, scp);
+            }
+        } else {
+            if (c == cl)
+                launch_restrict<false, false, false, double>(F, grid, stream, F.r.p, C.mask.p, C.b.p, nullptr, nullptr, nullptr, nullptr, C.nn, C.csub.p, scp);
+            else if (vc_type(c) != kVal64) {
+                const float* m = C.minv32.p;
+                if (cheb)
+                    launch_restrict<true, true, true, float>(F, grid, stream, F.r.p, C.mask.p, C.b.p, cur[c], C.d.p, m, cf, C.nn, C.csub.p, scp);
+                else if (bj)
+                    launch_restrict<true, true, false, float>(F, grid, stream, F.r.p, C.mask.p, C.b.p, cur[c], nullptr, m, cf, C.nn, C.csub.p, scp);
+                else
+                    launch_restrict<true, false, false, float>(F, grid, stream, F.r.p, C.mask.p, C.b.p, cur[c], nullptr, m, cf, C.nn, C.csub.p, scp);
+            } else if (cheb)
+                launch_restrict<true, true, true, double>(F, grid, stream, F.r.p, C.mask.p, C.b.p, cur[c], C.d.p, C.minv.p, cf, C.nn, C.csub.p, scp);
             else if (bj)
-                launch_restrict<true, true, false, float>(F, grid, stream, F.r.p, C.mask.p, C.b.p, cur[c], nullptr, m, cf, C.nn, C.csub.p, scp);
+                launch_restrict<true, true, false, double>(F, grid, stream, F.r.p, C.mask.p, C.b.p, cur[c], nullptr, C.minv.p, cf, C.nn, C.csub.p, scp);
             else
-                launch_restrict<true, false, false, float>(F, grid, stream, F.r.p, C.mask.p, C.b.p, cur[c], nullptr, m, cf, C.nn, C.csub.p, scp);
-        } else if (cheb)
-            launch_restrict<true, true, true, double>(F, grid, stream, F.r.p, C.mask.p, C.b.p, cur[c], C.d.p, C.minv.p, cf, C.nn, C.csub.p, scp);
-        else if (bj)
-            launch_restrict<true, true, false, double>(F, grid, stream, F.r.p, C.mask.p, C.b.p, cur[c], nullptr, C.minv.p, cf, C.nn, C.csub.p, scp);
-        else
-            launch_restrict<true, false, false, double>(F, grid, stream, F.r.p, C.mask.p, C.b.p, cur[c], nullptr, C.minv.p, cf, C.nn, C.csub.p, scp);
+                launch_restrict<true, false, false, double>(F, grid, stream, F.r.p, C.mask.p, C.b.p, cur[c], nullptr, C.minv.p, cf, C.nn, C.csub.p, scp);
+        }
     }
     if (ainv32.p) hipLaunchKernelGGL(k_coarse<float>, dim3(ceil_div(3 * lev[cl].nn, 4)), dim3(kBlock), 0, stream, ainv32.p, aoff.p, c_noff.p,
                            c_n.p, lev[cl].b.p, cur[cl], 3 * lev[cl].nn, lev[cl].csub.p, scp);
@@ -1767,6 +1896,7 @@ void MgpisDevice::vcycle(const double* rin, double* zout, bool dot) {
                            F.mask.p, cur[l], F.nn, F.csub.p, scp);
         else hipLaunchKernelGGL(k_prolong<false>, dim3(ceil_div(F.nn, kBlock)), dim3(kBlock), 0, stream, cur[l - 1], F.ppar.p, F.pw.p,
                            F.mask.p, cur[l], F.nn, F.csub.p, scp);
+        rot_prolong(l, cur[l - 1], cur[l], scp);
         // post-smoothing restarts the smoother (Chebyshev recurrence) from the prolongated iterate
         smooth(l, 0, nu, dot && l == Lf);
     }

@@ -107,6 +107,13 @@ struct LevelDev {
     DevBuf<int64_t> roff;    // per coarse chunk + 1
     DevBuf<int32_t> rcol;    // fine node
     DevBuf<double> rwt;
+    // block transfer entries (nodal rotations, MULTIGRID.h:1141-1181): P = S (x) I3 + sum of
+    // 3x3 blocks, as CSR over the fine nodes that own one (prolongation) and over the coarse
+    // nodes that receive one (restriction, B^T); nrot = 0 on plain S (x) I3 transfers
+    int64_t nrot = 0, nrotc = 0;
+    DevBuf<int32_t> rot_row, rot_par, rotc_row, rotc_kid;
+    DevBuf<int64_t> rot_ptr, rotc_ptr;
+    DevBuf<double> rot_blk, rotc_blk;
     // vectors (3 nn)
     DevBuf<double> x, t, b, r, d;
 };
@@ -164,6 +171,9 @@ public:
     void vcycle(const double* r, double* z, bool dot);     // z = M^-1 r (fine level)
     // b_{l-1} = realProl[l-1]^T r_l on every member (masked), batch nodal layouts of levels l, l-1
     void restrict_level(int l, const double* rf, double* bc);
+    // block (rotated-node) parts of the transfer from level l-1 to l: b_c += B^T r_f, x_f += B e_c
+    void rot_restrict(int l, const double* rf, double* bc, const PcgScal* scp);
+    void rot_prolong(int l, const double* ec, double* xf, const PcgScal* scp);
     // PCG over every subdomain of the batch; b in bs, result in xs (x0 = xs when warm).
     // begin() enqueues the setup, step() one graph replay (iters_per_graph iterations),
     // wait() paces replays on the host-mapped stop flags until every subdomain is done.

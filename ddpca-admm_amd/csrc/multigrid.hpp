@@ -9,7 +9,8 @@
 //   ADDITIONAL_FORCE     MULTIGRID.h:1257-1261
 //   OUTP_SUB1            MULTIGRID.h:1263-1281
 // Out of scope here: local/anisotropic refinement, hanging nodes, nodal
-// rotations (nodeRota), coupling nodes, stress recovery, text output.
+// rotations (nodeRota), coupling nodes, stress recovery, text output.  (The device solver takes
+// a rotated hierarchy built by the reference itself: mgpis_gpu_create_prol.)
 #pragma once
 #include <array>
 #include <cstdint>

@@ -189,4 +189,77 @@ Stencil make_stencil(int64_t nf, int64_t nc, const int64_t* ptr, const int32_t* 
     return S;
 }
 
+Stencil prol_to_stencil(int64_t nf, int64_t nc, int64_t nfree_f, const int32_t* free_f, const int32_t* free_c,
+                        const int64_t* ptr, const int32_t* col, const double* val) {
+    // blocks per fine node, keyed by coarse node; fm/cm: which rows/columns of the block are free
+    struct Blk {
+        int32_t p;
+        double b[9];
+        uint8_t fm, cm;
+    };
+    std::vector<std::vector<Blk>> rows(nf);
+    std::vector<uint8_t> fmask(nf, 0);
+    for (int64_t r = 0; r < nfree_f; ++r) {
+        const int32_t fd = free_f[r];
+        if (fd < 0 || fd >= 3 * nf) throw std::invalid_argument("realProl: fine free dof out of range");
+        const int64_t i = fd / 3;
+        const int a = fd % 3;
+        fmask[i] |= (uint8_t)(1u << a);
+        for (int64_t k = ptr[r]; k < ptr[r + 1]; ++k) {
+            const int32_t cd = free_c[col[k]];
+            if (cd < 0 || cd >= 3 * nc) throw std::invalid_argument("realProl: coarse free dof out of range");
+            const int32_t p = cd / 3;
+            const int b = cd % 3;
+            auto& v = rows[i];
+            auto it = std::find_if(v.begin(), v.end(), [p](const Blk& x) { return x.p == p; });
+            if (it == v.end()) {
+                v.push_back(Blk{p, {0, 0, 0, 0, 0, 0, 0, 0, 0}, 0, 0});
+                it = v.end() - 1;
+            }
+            it->b[3 * a + b] += val[k];
+            it->cm |= (uint8_t)(1u << b);
+        }
+    }
+    Stencil S;
+    S.nf = nf;
+    S.nc = nc;
+    S.ptr.assign(nf + 1, 0);
+    for (int64_t i = 0; i < nf; ++i) {
+        auto& v = rows[i];
+        if (i < nc) {  // identity rows (MULTIGRID.h:1144-1146): the node itself, weight 1
+            for (const Blk& x : v)
+                for (int a = 0; a < 3; ++a)
+                    for (int b = 0; b < 3; ++b)
+                        if (x.b[3 * a + b] != ((x.p == i && a == b) ? 1.0 : 0.0))
+                            throw std::invalid_argument("realProl: coarse node row is not the identity");
+            S.col.push_back((int32_t)i);
+            S.w.push_back(1.0);
+        } else {
+            std::sort(v.begin(), v.end(), [](const Blk& x, const Blk& y) { return x.p < y.p; });
+            for (const Blk& x : v) {
+                // scalar iff the free part is w*I (the free diagonal entries equal, the rest 0)
+                double w = 0.0;
+                bool have = false, scalar = true;
+                for (int a = 0; a < 3; ++a)
+                    if ((fmask[i] >> a & 1) && (x.cm >> a & 1)) {
+                        if (!have) w = x.b[4 * a], have = true;
+                        else if (x.b[4 * a] != w) scalar = false;
+                    }
+                for (int a = 0; a < 3; ++a)
+                    for (int b = 0; b < 3; ++b)
+                        if (a != b && x.b[3 * a + b] != 0.0) scalar = false;
+                if (!scalar) {
+                    S.bent.push_back((int64_t)S.col.size());
+                    S.bval.insert(S.bval.end(), x.b, x.b + 9);
+                    w = 0.0;
+                }
+                S.col.push_back(x.p);
+                S.w.push_back(w);
+            }
+        }
+        S.ptr[i + 1] = (int64_t)S.col.size();
+    }
+    return S;
+}
+
 }  // namespace ddpca

@@ -42,6 +42,10 @@ struct Stencil {
     std::vector<int64_t> ptr;
     std::vector<int32_t> col;
     std::vector<double> w;
+    // entries whose 3x3 block is not w*I (nodal rotations, MULTIGRID.h:1141-1181): entry index
+    // into col/w (its w is 0) and the full block, row-major, 9 per entry; empty when P = S (x) I3
+    std::vector<int64_t> bent;
+    std::vector<double> bval;
 };
 
 // C = S^T A S for a BSR3 A on the fine nodes and a scalar stencil S (Galerkin product,
@@ -60,5 +64,12 @@ Bsr3 condensed_to_bsr3(int64_t nn, int64_t nfree, const int32_t* free_dof, const
                        const double* val);
 
 Stencil make_stencil(int64_t nf, int64_t nc, const int64_t* ptr, const int32_t* col, const double* w);
+
+// Node stencil of the reference's realProl[l] = consOper[l+1] prolOper[l] consOper[l]^T
+// (MULTIGRID.h:1141-1181, 1246-1249) given as condensed CSR (nfree_f x nfree_c): every
+// (fine node, coarse node) block whose free part is w*I becomes a scalar entry, any other block
+// (rotated nodes, nodeRota) a block entry.  Coarse nodes keep the identity row.
+Stencil prol_to_stencil(int64_t nf, int64_t nc, int64_t nfree_f, const int32_t* free_f, const int32_t* free_c,
+                        const int64_t* ptr, const int32_t* col, const double* val);
 
 }  // namespace ddpca

@@ -85,6 +85,18 @@ int mgpis_gpu_create(int device, int nlev, const int64_t* nnodes, const int64_t*
                      const int64_t* const* S_ptr, const int32_t* const* S_col,
                      const double* const* S_w, const mgpis_options_t* opt, mgpis_t* out);
 
+/* Same as mgpis_gpu_create, with the transfers given as the reference's own
+ * MGPIS::realProl[l] (condensed CSR, nfree[l+1] x nfree[l], MULTIGRID.h:1141-1181, 1246-1249)
+ * instead of the scalar stencil, so hierarchies with rotated nodes (MULTIGRID::nodeRota: CYLINDER,
+ * DEHW hubs) drop in unchanged: every (fine node, coarse node) block whose free part is w*I runs as
+ * a stencil weight, every other 3x3 block as a block entry (k_prolong_rot / k_restrict_rot).
+ * DDPCA_EINVAL when a coarse node's row is not the identity. */
+int mgpis_gpu_create_prol(int device, int nlev, const int64_t* nnodes, const int64_t* nfree,
+                          const int32_t* const* free_dof, const int64_t* const* K_ptr,
+                          const int32_t* const* K_col, const double* const* K_val,
+                          const int64_t* const* P_ptr, const int32_t* const* P_col,
+                          const double* const* P_val, const mgpis_options_t* opt, mgpis_t* out);
+
 /* Same hierarchy in node-block form: B_*[l] is the UNCONSTRAINED Galerkin operator
  * origStif[l] (MULTIGRID.h:1182-1184) as 3x3-block CSR (9 doubles per block, row-major);
  * dof_free[3*nnodes[nlev-1]] marks free dofs (consFlag, MULTIGRID.h:1186-1194). */
