@@ -83,6 +83,9 @@ def main():
 
     torch.cuda.set_device(local)  # the timing syncs below must hit this rank's GPU, not device 0
     if world > 1:
+        # one node: RCCL's bootstrap over loopback (its data path is xGMI peer-to-peer either way);
+        # an interface chosen by the launcher's environment wins
+        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
         # host-side coordination only (barriers, the RCCL unique id, max-over-ranks timing); the
         # data path's exchanges are RCCL calls inside libddpca_amd on the solve stream
         dist.init_process_group("gloo", rank=rank, world_size=world)
