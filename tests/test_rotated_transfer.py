@@ -148,13 +148,16 @@ def test_rotated_prol_dropin_one_rotation(ddpca, oracle, gpu, case):
 
 
 @pytest.mark.gpu
-def test_rotated_prol_dropin_many_rotations(ddpca, oracle, gpu):
+@pytest.mark.parametrize("smoother,nu,fp32", [(1, 1, 0), (0, 1, 0), (2, 2, 0), (1, 1, 1), (1, 1, 2), (2, 2, 2)])
+def test_rotated_prol_dropin_many_rotations(ddpca, oracle, gpu, smoother, nu, fp32):
     """Per-node rotations: the reference's both-rotated rule (w * I) makes the hierarchy a
-    different, still valid preconditioner; the solution must still be x' = Q^T x."""
+    different, still valid preconditioner; the solution must still be x' = Q^T x.  Every smoother
+    (point / block Jacobi, Chebyshev: the first coarse sweep after a block restriction runs as
+    k_jac0) and every V-cycle operator storage (fp64, fp32, fine level block-exponent fp16)."""
     g = golden("beam_s1")
     nn, fd, K, P, Q, b = _hierarchy(ddpca, "many")
     x_ref = Q.T @ g["x_mg"]
-    M = ddpca.MGPIS.from_prol(nn, fd, K, P)
+    M = ddpca.MGPIS.from_prol(nn, fd, K, P, smoother=smoother, nu=nu, precond_fp32=fp32)
     x, it, _ = M.CG_SOLV(1, b)
     assert np.linalg.norm(x - x_ref) <= 1e-8 * np.linalg.norm(x_ref)
     xo, ito, _ = oracle.MgpisOracle(K, P).CG_SOLV(1, b)
