@@ -8,6 +8,10 @@
 // problem (mcontact_gpu_*) and is compared with the reference's own CONTACT_ANALYSIS in the same
 // process.  Prints JSON lines; exit code 0 = match.
 //   ref_bind fric globLeve [gpu [muscSett]]
+// "rot": a BEAM MULTIGRID with nodal rotations (nodeRota) on every fifth node, one rotation
+// ("one") or a node-dependent one ("many"); the reference's CG_SOLV(1) vs mgpis_gpu_create_prol
+// + mgpis_gpu_solve on the same hierarchy.
+//   ref_bind rot globLeve one|many
 #define HARNESS_NO_MAIN
 #include "ref_harness.cpp"
 #include "ref_bind.hpp"
@@ -43,9 +47,56 @@ double maxabs(const ddpca_bind::SpMat& a) {
     return m;
 }
 
+Eigen::Matrix3d axis_rotation(double ax, double ay, double az, double ang) {
+    return Eigen::AngleAxisd(ang, Eigen::Vector3d(ax, ay, az).normalized()).toRotationMatrix();
+}
+
+int rot_mode(long gl, bool many) {
+    BEAM beam(0);
+    beam.diviNumb = {8, 2, 2};
+    beam.globLeve = gl;
+    std::string log;
+    MULTIGRID* gp = nullptr;
+    harness::capture_iters([&] {
+        beam.MESH_NODD(0);
+        gp = &beam.multGrid[0];
+        gp->TRANSFER();
+        gp->STIF_MATR();
+    }, &log);
+    MULTIGRID& g = *gp;
+    long nrot = 0;
+    for (long ti = 0; ti < (long)g.nodeCoor.size(); ti += 5, ++nrot)
+        g.nodeRota.emplace(ti, axis_rotation(1.0, 2.0, 3.0, many ? 0.3 + 0.001 * ti : 0.7));
+    harness::capture_iters([&] { g.CONSTRAINT(1); }, &log);
+    long nblk = 0;  // realProl entries off w*I: the blocks the device runs as block entries
+    for (long l = 0; l < g.mgpi.maxiLeve; ++l)
+        for (int k = 0; k < g.mgpi.realProl[l].outerSize(); ++k)
+            for (ddpca_bind::SpMat::InnerIterator it(g.mgpi.realProl[l], k); it; ++it)
+                if (it.value() != 0.0 && it.value() != 1.0 && it.value() != 0.5 && it.value() != 0.25 &&
+                    it.value() != 0.125)
+                    ++nblk;
+    Eigen::VectorXd x_ref;
+    const long it_ref = harness::capture_iters([&] { g.mgpi.CG_SOLV(1, g.consForc, x_ref); });
+    mgpis_options_t opt;
+    mgpis_default_options(&opt);
+    mgpis_t h = ddpca_bind::mgpis_create_prol(g, 0, &opt);
+    Eigen::VectorXd x(g.consForc.size());
+    int64_t it_gpu = 0;
+    double rr = 0.0;
+    ddpca_bind::check(mgpis_gpu_solve(h, g.consForc.data(), x.data(), 1, 1e-14, g.consForc.size(), &it_gpu, &rr));
+    mgpis_gpu_destroy(h);
+    const double dx = (x - x_ref).norm() / x_ref.norm();
+    const bool ok = dx <= 1e-8 && nblk > 0;
+    std::printf("{\"rot_ok\": %s, \"n\": %ld, \"rotated_nodes\": %ld, \"rotated_prol_entries\": %ld, "
+                "\"iters_ref\": %ld, \"iters_gpu\": %ld, \"x_rel\": %.3g}\n",
+                ok ? "true" : "false", (long)x.size(), nrot, nblk, it_ref, (long)it_gpu, dx);
+    return ok ? 0 : 1;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
+    if (argc >= 4 && std::string(argv[1]) == "rot") return rot_mode(std::stol(argv[2]), std::string(argv[3]) == "many");
     if (argc < 3) { std::fprintf(stderr, "usage: ref_bind fric globLeve\n"); return 2; }
     MCONTACT mc;
     harness::twoblock_build(mc, std::stod(argv[1]), std::stol(argv[2]));

@@ -98,6 +98,27 @@ inline mgpis_t mgpis_create(MULTIGRID& g, int device, const mgpis_options_t* opt
     return out;
 }
 
+// The same drop-in when the hierarchy has rotated nodes (MULTIGRID::nodeRota set before
+// CONSTRAINT(1)): realProl carries w*R_off^T*R_par blocks a scalar stencil cannot hold
+// (MULTIGRID.h:1141-1181), so it is handed over as the reference holds it.
+inline mgpis_t mgpis_create_prol(MULTIGRID& g, int device, const mgpis_options_t* opt) {
+    Hierarchy h(g);
+    std::vector<Csr> P;
+    std::vector<const int64_t*> Pp;
+    std::vector<const int32_t*> Pc;
+    std::vector<const double*> Pv;
+    for (int l = 0; l + 1 < h.nlev; ++l) P.emplace_back(g.mgpi.realProl[l]);
+    for (auto& q : P) {
+        Pp.push_back(q.ptr.data());
+        Pc.push_back(q.m.innerIndexPtr());
+        Pv.push_back(q.m.valuePtr());
+    }
+    mgpis_t out = nullptr;
+    check(mgpis_gpu_create_prol(device, h.nlev, h.nnodes.data(), h.nfree.data(), h.fd_p.data(), h.Kp.data(),
+                                h.Kc.data(), h.Kv.data(), Pp.data(), Pc.data(), Pv.data(), opt, &out));
+    return out;
+}
+
 // MCONTACT after ESTABLISH() -> an established device problem; with muscSett = 2 its
 // MULTISCALE_1 coarse operators go along (globTran_D_1 columns moved to positions like the
 // systTran rows; accuProl and globTran_1 are in free / contact numbering already).

@@ -169,3 +169,24 @@ def test_rotated_prol_dropin_many_rotations(ddpca, oracle, gpu, smoother, nu, fp
     Mu, Mv = M.MULT_VCYC(u), M.MULT_VCYC(v)
     assert abs(v @ Mu - u @ Mv) <= 1e-10 * np.linalg.norm(Mu) * np.linalg.norm(v)
     assert u @ Mu > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("gl,variant", [(1, "one"), (2, "one"), (2, "many")])
+def test_reference_rotated_hierarchy_end_to_end(gpu, gl, variant):
+    """The reference itself builds a rotated hierarchy: oracle/ref_bind sets MULTIGRID::nodeRota
+    on every fifth node of a BEAM mesh before CONSTRAINT(1) (MULTIGRID.h:1102-1181), solves with
+    its own CG_SOLV(1), and hands consStif / realProl over through mgpis_gpu_create_prol
+    (oracle/ref_bind.hpp); the device solution must match to 1e-8."""
+    import json
+    import os
+    import subprocess
+    from pathlib import Path
+    exe = Path(__file__).resolve().parents[1] / "oracle" / "_ref" / "ref_bind"
+    if not exe.exists():
+        pytest.skip("oracle/_ref/ref_bind is built only where the reference is (travels with the snapshot)")
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    out = subprocess.run([str(exe), "rot", str(gl), variant], capture_output=True, text=True, timeout=600, env=env)
+    assert out.returncode == 0, out.stdout + out.stderr
+    res = json.loads(out.stdout.splitlines()[-1])
+    assert res["rot_ok"] and res["rotated_prol_entries"] > 0, res
