@@ -1,0 +1,58 @@
+// ORACLE TEST INFRASTRUCTURE -- NOT PART OF THE PRODUCT.
+//
+// Known-answer check on the reference's own TORSION example (examples/TORSION.h): a hollow
+// shaft under an end torque, whose analytic end-face displacement is T*l/(G*I_p)*R =
+// 1.159111630361142e-06 (TORSION.h:49).  The reference builds the {1,2,2}-subdomain DD problem
+// (globHomo levels, muscSett = 2 interface-eliminated coarse space, TORSION.h:39) and runs its
+// own CONTACT_ANALYSIS; oracle/ref_bind.hpp then hands the same ESTABLISH / MULTISCALE_1 output
+// to the device and the device ADMM loop runs.  Prints one JSON line on stderr:
+// iterations (device, reference), max nodal |u| (device, reference), resuDisp difference.
+//   ref_torsion globHomo
+#include <unistd.h>
+
+#include <cmath>
+#include <cstdio>
+
+#include "examples/TORSION.h"
+#include "ref_bind.hpp"
+
+int main(int argc, char** argv) {
+    const long gh = argc > 1 ? std::atol(argv[1]) : 2;
+    const int saved = dup(1);
+    if (!std::freopen("/dev/null", "w", stdout)) return 2;  // the reference's progress output
+    TORSION t(1);
+    t.domaNumb = {1, 2, 2};
+    t.globHomo = gh;
+    t.doleMcsc.assign(4, 1);
+    t.ESTA_SURF();
+    t.MESH_DD();
+    t.SOLVE_DD(1);  // ESTABLISH + the reference's CONTACT_ANALYSIS
+    std::fflush(stdout);
+    dup2(saved, 1);
+    ddpca_problem_t p = ddpca_bind::from_reference(t);
+    std::vector<int32_t> owner(t.multGrid.size(), 0);
+    mcontact_t h = nullptr;
+    ddpca_bind::check(mcontact_gpu_create(p, 0, 0, 1, owner.data(), nullptr, &h));
+    const int64_t n_gpu = mcontact_gpu_iterate(h, 3000, 1);
+    ddpca_bind::check((int)std::min<int64_t>(n_gpu, 0));
+    double du = 0.0, umax_gpu = 0.0, umax_ref = 0.0;
+    for (size_t tv = 0; tv < t.multGrid.size(); ++tv) {
+        const MULTIGRID& g = t.multGrid[tv];
+        Eigen::VectorXd u_pos(g.earlTran.cols());
+        ddpca_bind::check((int)std::min<int64_t>(mcontact_gpu_get(h, "resuDisp", tv, u_pos.data(), u_pos.size()), 0));
+        const Eigen::VectorXd u = g.earlTran * u_pos;  // position order -> node-id order (OUTP_SUB1)
+        du = std::max(du, (u - t.resuDisp[tv]).norm() / t.resuDisp[tv].norm());
+        for (long i = 0; i < u.size() / 3; ++i) {
+            umax_gpu = std::max(umax_gpu, u.segment<3>(3 * i).norm());
+            umax_ref = std::max(umax_ref, t.resuDisp[tv].segment<3>(3 * i).norm());
+        }
+    }
+    mcontact_gpu_destroy(h);
+    ddpca_problem_destroy(p);
+    std::fprintf(stderr,
+                 "{\"iters_gpu\": %ld, \"iters_ref\": %ld, \"umax_gpu\": %.12g, \"umax_ref\": %.12g, "
+                 "\"analytic\": 1.159111630361142e-06, \"resuDisp_rel\": %.3g, \"dofs\": %ld}\n",
+                 (long)n_gpu, (long)t.iterNumbReco, umax_gpu, umax_ref, du,
+                 (long)[&] { long n = 0; for (auto& g : t.multGrid) n += g.mgpi.consStif[g.mgpi.maxiLeve].rows(); return n; }());
+    return 0;
+}

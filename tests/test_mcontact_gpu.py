@@ -302,3 +302,26 @@ def test_reference_binding_end_to_end(gpu, fric, musc):
     assert out.returncode == 0, out.stdout + out.stderr
     res = json.loads(out.stdout.splitlines()[-1])
     assert res["gpu_ok"], res
+
+
+def test_torsion_known_answer(gpu, tmp_path):
+    """The reference's own TORSION example ({1,2,2} subdomains, globHomo 2, muscSett = 2; built
+    by the reference, handed over by oracle/ref_bind.hpp, oracle/ref_torsion.cpp): the device
+    ADMM loop reaches the reference's iteration count (+-1) and resuDisp (1e-6), and the end
+    face's displacement matches the analytic T*l/(G*I_p)*R = 1.159111630361142e-06
+    (TORSION.h:49) to the discretisation error (1e-3)."""
+    import json
+    import os
+    import subprocess
+    from pathlib import Path
+    exe = Path(__file__).resolve().parents[1] / "oracle" / "_ref" / "ref_torsion"
+    if not exe.exists():
+        pytest.skip("oracle/_ref/ref_torsion is built only where the reference is (travels with the snapshot)")
+    env = dict(os.environ, OMP_NUM_THREADS="8")
+    out = subprocess.run([str(exe), "2"], capture_output=True, text=True, timeout=170, env=env, cwd=tmp_path)
+    assert out.returncode == 0, out.stderr[-2000:]
+    res = json.loads(out.stderr.strip().splitlines()[-1])
+    assert abs(res["iters_gpu"] - res["iters_ref"]) <= 1, res
+    assert res["resuDisp_rel"] <= 1e-6, res
+    assert abs(res["umax_gpu"] - res["umax_ref"]) <= 1e-6 * res["umax_ref"], res
+    assert abs(res["umax_gpu"] - res["analytic"]) <= 1e-3 * res["analytic"], res
