@@ -325,3 +325,30 @@ def test_torsion_known_answer(gpu, tmp_path):
     assert res["resuDisp_rel"] <= 1e-6, res
     assert abs(res["umax_gpu"] - res["umax_ref"]) <= 1e-6 * res["umax_ref"], res
     assert abs(res["umax_gpu"] - res["analytic"]) <= 1e-3 * res["analytic"], res
+
+
+@pytest.mark.parametrize("musc", ["1", "2"])
+def test_block_patch_pressure_known_answer(gpu, tmp_path, musc):
+    """The reference's own BLOCK example (stacked blocks, uniform 1e7 Pa top load; domaNumb
+    {1,1,1}, globLeve 1, 8 interfaces; oracle/ref_block.cpp): the device ADMM loop on the
+    handed-over operators reaches the reference's iteration count (+-1) and resuDisp (1e-6), and
+    every interface carries the patch-test pressure 1e7 at every integration point (1e-5, the
+    contact-pressure tolerance of SURVEY §8 c4; the reference's own run is within 1e-9)."""
+    import json
+    import os
+    import subprocess
+    from pathlib import Path
+    exe = Path(__file__).resolve().parents[1] / "oracle" / "_ref" / "ref_block"
+    if not exe.exists():
+        pytest.skip("oracle/_ref/ref_block is built only where the reference is (travels with the snapshot)")
+    env = dict(os.environ, OMP_NUM_THREADS="8")
+    out = subprocess.run([str(exe), "1", musc], capture_output=True, text=True, timeout=170, env=env, cwd=tmp_path)
+    assert out.returncode == 0, out.stderr[-2000:]
+    res = json.loads(out.stderr.strip().splitlines()[-1])
+    assert abs(res["iters_gpu"] - res["iters_ref"]) <= 1, res
+    assert res["resuDisp_rel"] <= 1e-6, res
+    assert len(res["interfaces"]) == 8
+    for itf in res["interfaces"]:
+        assert itf["nip"] > 0
+        for k in ("mean", "min", "max"):
+            assert abs(itf[k] - 1e7) <= 1e-5 * 1e7, (musc, itf)
