@@ -317,7 +317,7 @@ def test_torsion_known_answer(gpu, tmp_path):
     exe = Path(__file__).resolve().parents[1] / "oracle" / "_ref" / "ref_torsion"
     if not exe.exists():
         pytest.skip("oracle/_ref/ref_torsion is built only where the reference is (travels with the snapshot)")
-    env = dict(os.environ, OMP_NUM_THREADS="8")
+    env = dict(os.environ, OMP_NUM_THREADS="1")  # deterministic reference run, see above
     out = subprocess.run([str(exe), "2"], capture_output=True, text=True, timeout=170, env=env, cwd=tmp_path)
     assert out.returncode == 0, out.stderr[-2000:]
     res = json.loads(out.stderr.strip().splitlines()[-1])
@@ -341,7 +341,7 @@ def test_block_patch_pressure_known_answer(gpu, tmp_path, musc):
     exe = Path(__file__).resolve().parents[1] / "oracle" / "_ref" / "ref_block"
     if not exe.exists():
         pytest.skip("oracle/_ref/ref_block is built only where the reference is (travels with the snapshot)")
-    env = dict(os.environ, OMP_NUM_THREADS="8")
+    env = dict(os.environ, OMP_NUM_THREADS="1")  # deterministic reference run, see above
     out = subprocess.run([str(exe), "1", musc], capture_output=True, text=True, timeout=170, env=env, cwd=tmp_path)
     assert out.returncode == 0, out.stderr[-2000:]
     res = json.loads(out.stderr.strip().splitlines()[-1])
