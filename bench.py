@@ -35,6 +35,8 @@ VALUE_LAYOUT = "fp64-pairs, col16"  # SELL layout of the fine Krylov operator (d
 
 
 def parse():
+    H = importlib.import_module("ddpca-admm_amd").HEADLINE_OPTIONS  # pinned by tests/test_headline_gpu.py
+    M = importlib.import_module("ddpca-admm_amd").HEADLINE_MUSC
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -46,23 +48,23 @@ def parse():
     ap.add_argument("--gl", type=int, default=5, help="uniform refinements (levels = gl + 1)")
     ap.add_argument("--fric", type=float, default=0.2)
     # defaults: the fastest configuration of the round-1 sweep (profiles/r01_sweep.txt)
-    ap.add_argument("--smoother", type=int, default=1, help="0 point Jacobi, 1 block Jacobi, 2 Chebyshev")
-    ap.add_argument("--nu", type=int, default=1)
-    ap.add_argument("--omega-scale", type=float, default=1.7,
+    ap.add_argument("--smoother", type=int, default=H["smoother"], help="0 point Jacobi, 1 block Jacobi, 2 Chebyshev")
+    ap.add_argument("--nu", type=int, default=H["nu"])
+    ap.add_argument("--omega-scale", type=float, default=-H["omega"],
                     help="Jacobi damping = scale / lambda_max(M^-1 K) per level (profiles/r01_sweep_omega.txt)")
-    ap.add_argument("--iters-per-graph", type=int, default=4)
-    ap.add_argument("--warm-start", type=int, default=0,
+    ap.add_argument("--iters-per-graph", type=int, default=H["iters_per_graph"])
+    ap.add_argument("--warm-start", type=int, default=H["warm_start"],
                     help="1: each subdomain PCG starts from its previous solution (same 1e-14 stop rule)")
-    ap.add_argument("--precond-fp32", type=int, default=2,
+    ap.add_argument("--precond-fp32", type=int, default=H["precond_fp32"],
                     help="1: V-cycle level operators stored in fp32; 2: and the fine level's V-cycle copy in block-exponent fp16 "
                          "(arithmetic, Krylov operator and stop rule fp64)")
-    ap.add_argument("--table-mode", type=int, default=0,
+    ap.add_argument("--table-mode", type=int, default=H["table_mode"],
                     help="1: keep one copy of bit-identical operator rows (pays on regular meshes only; the "
                          "synthetic box mesh is far more regular than DEHW's curved one, so the headline keeps 0)")
-    ap.add_argument("--musc", type=int, default=2,
+    ap.add_argument("--musc", type=int, default=M["muscSett"],
                     help="muscSett: 2 = interface-eliminated coarse space every ADMM iteration (DEHW.h:2222), 0 = none")
-    ap.add_argument("--dole", type=int, default=1, help="doleMcsc: coarse-space level of every subdomain (DEHW.h:2239)")
-    ap.add_argument("--coarse-level", type=int, default=-1,
+    ap.add_argument("--dole", type=int, default=M["doleMcsc"], help="doleMcsc: coarse-space level of every subdomain (DEHW.h:2239)")
+    ap.add_argument("--coarse-level", type=int, default=H["coarse_level"],
                     help="V-cycle level of the exact dense coarse solve (-1: auto, 0: the reference's)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=os.environ.get("DDPCA_TRAFFIC_JSON", str(ROOT / "profiles" / "traffic.json")),

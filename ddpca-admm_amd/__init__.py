@@ -48,6 +48,16 @@ class MgpisOptions(C.Structure):
                 ("coarse_level", C.c_int)]
 
 
+# The option set bench.py measures the headline on (its defaults; tests/test_headline_gpu.py pins
+# this exact set against the oracle): 3x3 block-Jacobi V(1,1) with damping 1.7 / lambda_max,
+# V-cycle levels stored fp32 with the two finest as block-exponent fp16, streamed operator rows,
+# automatic exact-solve level, 4 PCG iterations per hipGraph replay, x0 = 0.
+HEADLINE_OPTIONS = dict(smoother=1, nu=1, omega=-1.7, iters_per_graph=4, warm_start=0, precond_fp32=2,
+                        table_mode=0, coarse_level=-1)
+# and the ADMM setting it runs: interface-eliminated coarse space (muscSett = 2) on level 1 of
+# every subdomain (DEHW.h:2222, 2239)
+HEADLINE_MUSC = dict(muscSett=2, doleMcsc=1)
+
 _P = C.c_void_p
 _I64P = C.POINTER(C.c_int64)
 _DP = C.POINTER(C.c_double)
@@ -616,4 +626,4 @@ class MCONTACT:
 
 
 __all__ = ["Problem", "MULTIGRID", "MGPIS", "MCONTACT", "DdpcaError", "lib", "gpu_available", "default_options",
-           "LIBPATH"]
+           "LIBPATH", "HEADLINE_OPTIONS", "HEADLINE_MUSC"]

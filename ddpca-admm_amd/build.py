@@ -11,6 +11,7 @@ import hashlib
 import os
 import subprocess
 import sys
+import threading
 from pathlib import Path
 
 HERE = Path(__file__).resolve().parent
@@ -49,10 +50,15 @@ def _compile(src: Path) -> Path:
         flags = flags + ["-x", "hip"]
     obj = OBJ / f"{src.stem}.{_digest(src, flags)}.o"
     if not obj.exists():
-        cmd = [HIPCC, *flags, "-c", str(src), "-o", str(obj)]
+        # compile to a private name and rename on success: a killed compile never leaves a
+        # truncated object under the cache name, and concurrent builds do not share a file
+        tmp = obj.with_suffix(f".{os.getpid()}.{threading.get_ident()}.tmp")
+        cmd = [HIPCC, *flags, "-c", str(src), "-o", str(tmp)]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
+            tmp.unlink(missing_ok=True)
             raise RuntimeError(f"compile failed: {src.name}\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+        os.replace(tmp, obj)
     return obj
 
 
@@ -66,7 +72,7 @@ def build(verbose: bool = False) -> Path:
     stamp_file = OBJ / f"link.{LIB.name}.stamp"
     if LIB.exists() and stamp_file.exists() and stamp_file.read_text() == stamp:
         return LIB
-    tmp = LIB.with_suffix(".so.tmp")
+    tmp = LIB.with_suffix(f".so.{os.getpid()}.tmp")
     cmd = [HIPCC, *[str(o) for o in objs], *LINK, "-o", str(tmp)]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:

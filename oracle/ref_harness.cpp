@@ -33,7 +33,10 @@
 #include <cstdio>
 #include <random>
 #include <regex>
+#include <stdexcept>
 #include <string>
+
+#include <unistd.h>
 
 namespace harness {
 
@@ -132,21 +135,54 @@ void save_elems(const std::string& name, const MULTIGRID& g) {
     save_npy(P(name), e.data(), {e.size() / 8, 8});
 }
 
-// Run fn with std::cout captured; return the last "#Iteration: N" value + 1 (= loop count of
-// MGPIS::CG_SOLV, which prints iterNumb - 1 at exit, MGPIS.h:221).
+// Run fn with the process's stdout captured at the file-descriptor level and return the last
+// "#Iteration: N" value + 1 (= loop count of MGPIS::CG_SOLV, which prints iterNumb - 1 at exit,
+// MGPIS.h:221).  The reference prints from inside its OpenMP subdomain loop (MCONTACT.h:2511-2537),
+// so the capture must be safe under concurrent writers: std::cout stays on its stdio-synchronised
+// buffer (stdio locks each call) and fd 1 is pointed at an anonymous temp file for the duration;
+// a std::stringbuf swapped into std::cout would be written by several threads unsynchronised.
 template <typename F>
 long capture_iters(F fn, std::string* text = nullptr) {
-    std::stringstream ss;
-    std::streambuf* old = std::cout.rdbuf(ss.rdbuf());
-    fn();
-    std::cout.rdbuf(old);
-    std::string s = ss.str();
+    std::cout.flush();
+    std::fflush(stdout);
+    std::FILE* tmp = std::tmpfile();
+    const int saved = dup(1);
+    if (!tmp || saved < 0 || dup2(fileno(tmp), 1) < 0) {
+        if (tmp) std::fclose(tmp);
+        if (saved >= 0) close(saved);
+        throw std::runtime_error("capture_iters: cannot redirect stdout");
+    }
+    try {
+        fn();
+    } catch (...) {
+        std::cout.flush();
+        std::fflush(stdout);
+        dup2(saved, 1);
+        close(saved);
+        std::fclose(tmp);
+        throw;
+    }
+    std::cout.flush();
+    std::fflush(stdout);
+    dup2(saved, 1);
+    close(saved);
+    std::string s;
+    std::rewind(tmp);
+    char buf[1 << 16];
+    for (size_t k; (k = std::fread(buf, 1, sizeof buf, tmp)) > 0;) s.append(buf, k);
+    std::fclose(tmp);
     if (text) *text = s;
     std::regex re("#Iteration: (-?[0-9]+)");
     long last = -2;
     for (std::sregex_iterator it(s.begin(), s.end(), re), end; it != end; ++it)
         last = std::stol((*it)[1]);
     return last + 1;
+}
+
+// Silence the reference's progress output around setup calls (same fd-level redirection).
+template <typename F>
+void quiet(F fn) {
+    capture_iters(fn);
 }
 
 double now_s() {
@@ -185,11 +221,10 @@ int beam_nodd(long d0, long d1, long d2, long gl, bool full, bool do_cg) {
     BEAM beam(0);
     beam.diviNumb = {d0, d1, d2};
     beam.globLeve = gl;
-    { std::stringstream ss; auto* o = std::cout.rdbuf(ss.rdbuf()); beam.MESH_NODD(0); std::cout.rdbuf(o); }
+    quiet([&] { beam.MESH_NODD(0); });
     MULTIGRID& g = beam.multGrid[0];
     double t0 = now_s();
-    { std::stringstream ss; auto* o = std::cout.rdbuf(ss.rdbuf());
-      g.TRANSFER(); g.STIF_MATR(); g.CONSTRAINT(1); std::cout.rdbuf(o); }
+    quiet([&] { g.TRANSFER(); g.STIF_MATR(); g.CONSTRAINT(1); });
     double t_setup = now_s() - t0;
     dump_grid("", g, full);
     const long L = g.mgpi.maxiLeve;
@@ -233,10 +268,9 @@ int beam_solv(long d0, long d1, long d2, long gl) {
     BEAM beam(0);
     beam.diviNumb = {d0, d1, d2};
     beam.globLeve = gl;
-    { std::stringstream ss; auto* o = std::cout.rdbuf(ss.rdbuf()); beam.MESH_NODD(0); std::cout.rdbuf(o); }
+    quiet([&] { beam.MESH_NODD(0); });
     MULTIGRID& g = beam.multGrid[0];
-    { std::stringstream ss; auto* o = std::cout.rdbuf(ss.rdbuf());
-      g.TRANSFER(); g.STIF_MATR(); g.CONSTRAINT(1); std::cout.rdbuf(o); }
+    quiet([&] { g.TRANSFER(); g.STIF_MATR(); g.CONSTRAINT(1); });
     const long L = g.mgpi.maxiLeve;
     const Eigen::VectorXd& b = g.consForc;
     std::vector<double> info;

@@ -185,7 +185,7 @@ def test_reference_rotated_hierarchy_end_to_end(gpu, gl, variant):
     exe = Path(__file__).resolve().parents[1] / "oracle" / "_ref" / "ref_bind"
     if not exe.exists():
         pytest.skip("oracle/_ref/ref_bind is built only where the reference is (travels with the snapshot)")
-    env = dict(os.environ, OMP_NUM_THREADS="1")
+    env = dict(os.environ)
     out = subprocess.run([str(exe), "rot", str(gl), variant], capture_output=True, text=True, timeout=600, env=env)
     assert out.returncode == 0, out.stdout + out.stderr
     res = json.loads(out.stdout.splitlines()[-1])
