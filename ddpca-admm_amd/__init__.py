@@ -85,6 +85,9 @@ def _declare(L: C.CDLL) -> None:
     L.ddpca_problem_mgpis.argtypes = [_P, C.c_int64, C.c_int, C.POINTER(MgpisOptions), C.POINTER(_P)]
     L.ddpca_problem_empty.argtypes = [C.c_int64, C.c_int64, C.POINTER(_P)]
     L.ddpca_problem_set_subdomain.argtypes = [_P, C.c_int64, C.c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]
+    L.ddpca_problem_set_subdomain_prol.argtypes = [_P, C.c_int64, C.c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
+                                                   _P]
+    L.ddpca_problem_set_hanging.argtypes = [_P, C.c_int64, C.c_int64, C.POINTER(_CsrArg)]
     L.ddpca_problem_set_interface.argtypes = [_P, C.c_int64, C.c_int64, C.c_int64, C.c_double, C.c_int64, C.c_int64,
                                               C.c_int64, _P, _P, C.POINTER(_CsrArg)]
     L.ddpca_problem_finalize.argtypes = [_P]
@@ -241,8 +244,10 @@ class Problem:
         """Established problem from operators in the reference's layouts (no host restatement).
 
         subdomains[tv]: nnodes (per level), free_dof (per level, increasing nodal dofs), K (per
-        level, condensed consStif CSR), S (per level < L, scalar stencil CSR), consForc, and
-        optionally presc (3N nodal Dirichlet values) and coords (N x 3).
+        level, condensed consStif CSR), S (per level < L, scalar stencil CSR) -- or P (per level < L,
+        the reference's condensed realProl, for rotated nodes) --, consForc, and optionally presc
+        (3N nodal Dirichlet values), coords (N x 3) and hang = (nnodes_all, H): the hanging level
+        (rows 3N.. of prolOper[maxiLeve], ddpca_problem_set_hanging).
         interfaces[ts]: body (2), fric, nip, nnc (2), pemaDiag, inpoNgap, ops[s][name] CSR for
         the names in Problem.IFACE_OPS.
         coarse (optional, the caller's MCONTACT::MULTISCALE_1 output, muscSett = 2): doleMcsc,
@@ -269,10 +274,12 @@ class Problem:
         for tv, s in enumerate(subdomains):
             nlev = len(s["nnodes"])
             K = [m.tocsr() for m in s["K"]]
-            S = [m.tocsr() for m in s.get("S", [])]
+            use_p = "P" in s
+            S = [m.tocsr() for m in (s["P"] if use_p else s.get("S", []))]
             presc = s.get("presc")
             coords = s.get("coords")
-            _check(lib().ddpca_problem_set_subdomain(
+            fn = lib().ddpca_problem_set_subdomain_prol if use_p else lib().ddpca_problem_set_subdomain
+            _check(fn(
                 self._h, tv, nlev, _ptr(arr(s["nnodes"], np.int64)), _ptr(arr([m.shape[0] for m in K], np.int64)),
                 ptrs([arr(f, np.int32) for f in s["free_dof"]], None),
                 ptrs([arr(m.indptr, np.int64) for m in K], None), ptrs([arr(m.indices, np.int32) for m in K], None),
@@ -281,6 +288,12 @@ class Problem:
                 ptrs([arr(m.data, np.float64) for m in S], None), _ptr(arr(s["consForc"], np.float64)),
                 None if presc is None else _ptr(arr(presc, np.float64)),
                 None if coords is None else _ptr(arr(np.asarray(coords).reshape(-1), np.float64))))
+            if s.get("hang") is not None:
+                n_all, Hm = s["hang"]
+                Hm = Hm.tocsr()
+                hv = _CsrArg(Hm.shape[0], Hm.shape[1], _ptr(arr(Hm.indptr, np.int64)), _ptr(arr(Hm.indices, np.int32)),
+                             _ptr(arr(Hm.data, np.float64)))
+                _check(lib().ddpca_problem_set_hanging(self._h, tv, int(n_all), C.byref(hv)))
         for ts, f in enumerate(interfaces):
             ops = (_CsrArg * 14)()
             for side in range(2):

@@ -60,6 +60,70 @@ int ddpca_problem_empty(int64_t nsub, int64_t nint, ddpca_problem_t* out) {
     });
 }
 
+}  // extern "C"
+
+namespace {
+
+// Shared body of set_subdomain / set_subdomain_prol: `transfers(g)` fills g.scalProl.
+template <typename Tr>
+void set_subdomain_common(ddpca_problem_t h, int64_t tv, int nlev, const int64_t* nnodes, const int64_t* nfree,
+                          const int32_t* const* free_dof, const int64_t* const* K_ptr, const int32_t* const* K_col,
+                          const double* const* K_val, bool have_transfers, Tr&& transfers, const double* consForc,
+                          const double* presc, const double* coords) {
+    Problem& P = builder(h);
+    if (tv < 0 || tv >= (int64_t)P.mc.multGrid.size()) throw ApiError(DDPCA_EINVAL, "subdomain index");
+    if (nlev < 1 || !nnodes || !nfree || !free_dof || !K_ptr || !K_col || !K_val || !consForc)
+        throw ApiError(DDPCA_EINVAL, "null argument");
+    if (nlev > 1 && !have_transfers) throw ApiError(DDPCA_EINVAL, "transfer operators missing");
+    for (int l = 0; l < nlev; ++l) {
+        if (nnodes[l] < 1 || (l > 0 && nnodes[l] < nnodes[l - 1])) throw ApiError(DDPCA_EINVAL, "nnodes must grow by level");
+        if (nfree[l] < 0 || nfree[l] > 3 * nnodes[l]) throw ApiError(DDPCA_EINVAL, "nfree out of range");
+    }
+    MULTIGRID g;
+    const int64_t N = nnodes[nlev - 1];
+    g.maxiLeve = nlev - 1;
+    g.leveCount.assign(nnodes, nnodes + nlev);
+    g.freeCount.assign(nfree, nfree + nlev);
+    g.levelStif.resize(nlev);
+    for (int l = 0; l < nlev; ++l) {
+        // the level-l free dofs must be the level-(l+1) free dofs of the first nnodes[l] nodes
+        // (level-ordered numbering, MULTIGRID.h:884-910)
+        for (int64_t r = 0; r < nfree[l]; ++r)
+            if (free_dof[l][r] < 0 || free_dof[l][r] >= 3 * nnodes[l] || (r && free_dof[l][r] <= free_dof[l][r - 1]))
+                throw ApiError(DDPCA_EINVAL, "free_dof[" + std::to_string(l) + "] must be increasing nodal dofs of the level");
+        g.levelStif[l] = condensed_to_bsr3(nnodes[l], nfree[l], free_dof[l], K_ptr[l], K_col[l], K_val[l]);
+    }
+    transfers(g);
+    g.consFlag.assign(3 * N, 0);
+    g.freeIndex.assign(3 * N, -1);
+    for (int64_t r = 0; r < nfree[nlev - 1]; ++r) {
+        g.consFlag[free_dof[nlev - 1][r]] = 1;
+        g.freeIndex[free_dof[nlev - 1][r]] = (int32_t)r;
+    }
+    for (int l = 0; l + 1 < nlev; ++l)
+        for (int64_t r = 0; r < nfree[l]; ++r)
+            if (!g.consFlag[free_dof[l][r]]) throw ApiError(DDPCA_EINVAL, "coarse free dof constrained on the fine level");
+    g.consForc.assign(consForc, consForc + nfree[nlev - 1]);
+    g.dispForc.clear();  // constrained dofs' values in dof order (MULTIGRID::CONSTRAINT layout)
+    for (int64_t d = 0; d < 3 * N; ++d)
+        if (!g.consFlag[d]) {
+            const double v = presc ? presc[d] : 0.0;
+            g.consDofv[d] = v;
+            g.dispForc.push_back(v);
+        }
+    if (coords) {
+        g.nodeCoor.resize(N);
+        for (int64_t i = 0; i < N; ++i)
+            for (int a = 0; a < 3; ++a) g.nodeCoor[i][a] = coords[3 * i + a];
+    }
+    P.mc.multGrid[tv] = std::move(g);
+    P.owned[tv] = 1;
+}
+
+}  // namespace
+
+extern "C" {
+
 int ddpca_problem_set_subdomain(ddpca_problem_t h, int64_t tv, int nlev, const int64_t* nnodes, const int64_t* nfree,
                                 const int32_t* const* free_dof, const int64_t* const* K_ptr,
                                 const int32_t* const* K_col, const double* const* K_val,
@@ -67,54 +131,53 @@ int ddpca_problem_set_subdomain(ddpca_problem_t h, int64_t tv, int nlev, const i
                                 const double* const* S_w, const double* consForc, const double* presc,
                                 const double* coords) {
     return guarded([&] {
+        set_subdomain_common(
+            h, tv, nlev, nnodes, nfree, free_dof, K_ptr, K_col, K_val, S_ptr && S_col && S_w,
+            [&](MULTIGRID& g) {
+                for (int l = 0; l + 1 < nlev; ++l)
+                    g.scalProl.push_back(make_stencil(nnodes[l + 1], nnodes[l], S_ptr[l], S_col[l], S_w[l]));
+            },
+            consForc, presc, coords);
+    });
+}
+
+int ddpca_problem_set_subdomain_prol(ddpca_problem_t h, int64_t tv, int nlev, const int64_t* nnodes,
+                                     const int64_t* nfree, const int32_t* const* free_dof,
+                                     const int64_t* const* K_ptr, const int32_t* const* K_col,
+                                     const double* const* K_val, const int64_t* const* P_ptr,
+                                     const int32_t* const* P_col, const double* const* P_val,
+                                     const double* consForc, const double* presc, const double* coords) {
+    return guarded([&] {
+        set_subdomain_common(
+            h, tv, nlev, nnodes, nfree, free_dof, K_ptr, K_col, K_val, P_ptr && P_col && P_val,
+            [&](MULTIGRID& g) {
+                for (int l = 0; l + 1 < nlev; ++l) {
+                    const int64_t nnz = P_ptr[l][nfree[l + 1]];
+                    for (int64_t k = 0; k < nnz; ++k)
+                        if (P_col[l][k] < 0 || P_col[l][k] >= nfree[l]) throw ApiError(DDPCA_EINVAL, "realProl column out of range");
+                    g.scalProl.push_back(prol_to_stencil(nnodes[l + 1], nnodes[l], nfree[l + 1], free_dof[l + 1], free_dof[l],
+                                                         P_ptr[l], P_col[l], P_val[l]));
+                }
+            },
+            consForc, presc, coords);
+    });
+}
+
+int ddpca_problem_set_hanging(ddpca_problem_t h, int64_t tv, int64_t nnodes_all, const ddpca_csr_t* hang) {
+    return guarded([&] {
         Problem& P = builder(h);
-        if (tv < 0 || tv >= (int64_t)P.mc.multGrid.size()) throw ApiError(DDPCA_EINVAL, "subdomain index");
-        if (nlev < 1 || !nnodes || !nfree || !free_dof || !K_ptr || !K_col || !K_val || !consForc)
-            throw ApiError(DDPCA_EINVAL, "null argument");
-        if (nlev > 1 && (!S_ptr || !S_col || !S_w)) throw ApiError(DDPCA_EINVAL, "stencils missing");
-        for (int l = 0; l < nlev; ++l) {
-            if (nnodes[l] < 1 || (l > 0 && nnodes[l] < nnodes[l - 1])) throw ApiError(DDPCA_EINVAL, "nnodes must grow by level");
-            if (nfree[l] < 0 || nfree[l] > 3 * nnodes[l]) throw ApiError(DDPCA_EINVAL, "nfree out of range");
-        }
-        MULTIGRID g;
-        const int64_t N = nnodes[nlev - 1];
-        g.maxiLeve = nlev - 1;
-        g.leveCount.assign(nnodes, nnodes + nlev);
-        g.freeCount.assign(nfree, nfree + nlev);
-        g.levelStif.resize(nlev);
-        for (int l = 0; l < nlev; ++l) {
-            // the level-l free dofs must be the level-(l+1) free dofs of the first nnodes[l] nodes
-            // (level-ordered numbering, MULTIGRID.h:884-910)
-            for (int64_t r = 0; r < nfree[l]; ++r)
-                if (free_dof[l][r] < 0 || free_dof[l][r] >= 3 * nnodes[l] || (r && free_dof[l][r] <= free_dof[l][r - 1]))
-                    throw ApiError(DDPCA_EINVAL, "free_dof[" + std::to_string(l) + "] must be increasing nodal dofs of the level");
-            g.levelStif[l] = condensed_to_bsr3(nnodes[l], nfree[l], free_dof[l], K_ptr[l], K_col[l], K_val[l]);
-        }
-        for (int l = 0; l + 1 < nlev; ++l) g.scalProl.push_back(make_stencil(nnodes[l + 1], nnodes[l], S_ptr[l], S_col[l], S_w[l]));
-        g.consFlag.assign(3 * N, 0);
-        g.freeIndex.assign(3 * N, -1);
-        for (int64_t r = 0; r < nfree[nlev - 1]; ++r) {
-            g.consFlag[free_dof[nlev - 1][r]] = 1;
-            g.freeIndex[free_dof[nlev - 1][r]] = (int32_t)r;
-        }
-        for (int l = 0; l + 1 < nlev; ++l)
-            for (int64_t r = 0; r < nfree[l]; ++r)
-                if (!g.consFlag[free_dof[l][r]]) throw ApiError(DDPCA_EINVAL, "coarse free dof constrained on the fine level");
-        g.consForc.assign(consForc, consForc + nfree[nlev - 1]);
-        g.dispForc.clear();  // constrained dofs' values in dof order (MULTIGRID::CONSTRAINT layout)
-        for (int64_t d = 0; d < 3 * N; ++d)
-            if (!g.consFlag[d]) {
-                const double v = presc ? presc[d] : 0.0;
-                g.consDofv[d] = v;
-                g.dispForc.push_back(v);
-            }
-        if (coords) {
-            g.nodeCoor.resize(N);
-            for (int64_t i = 0; i < N; ++i)
-                for (int a = 0; a < 3; ++a) g.nodeCoor[i][a] = coords[3 * i + a];
-        }
-        P.mc.multGrid[tv] = std::move(g);
-        P.owned[tv] = 1;
+        if (tv < 0 || tv >= (int64_t)P.mc.multGrid.size() || !hang) throw ApiError(DDPCA_EINVAL, "subdomain index / null");
+        MULTIGRID& g = P.mc.multGrid[tv];
+        if (g.leveCount.empty()) throw ApiError(DDPCA_ESTATE, "set the subdomain before its hanging level");
+        for (const Interface& itf : P.mc.searCont)
+            if (!itf.inteMass[0].ptr.empty() && (itf.body[0] == tv || itf.body[1] == tv))
+                throw ApiError(DDPCA_ESTATE, "set the hanging level before the subdomain's interfaces");
+        const int64_t NL = g.leveCount.back();
+        if (nnodes_all < NL) throw ApiError(DDPCA_EINVAL, "nnodes_all below the fine level's node count");
+        Csr H = to_csr(*hang, "hanging prolongation");
+        expect_shape(H, 3 * (nnodes_all - NL), 3 * NL, "hanging prolongation");
+        g.nodeAll = nnodes_all == NL ? 0 : nnodes_all;
+        g.hangProl = std::move(H);
     });
 }
 
@@ -149,7 +212,7 @@ int ddpca_problem_set_interface(ddpca_problem_t h, int64_t ts, int64_t body0, in
             const int64_t m = I.mside(s);
             if (P.mc.multGrid[I.body[s]].leveCount.empty())
                 throw ApiError(DDPCA_ESTATE, "set the interface's subdomains before the interface");
-            const int64_t n3 = 3 * P.mc.multGrid[I.body[s]].leveCount.back();
+            const int64_t n3 = 3 * P.mc.multGrid[I.body[s]].nodalCount();
             expect_shape(I.inpoLagr[s], mip, m, "inpoLagr");
             expect_shape(I.pemaInpo_r[s], mip, n3, "pemaInpo_r");
             expect_shape(I.systTran[s], n3, m, "systTran");
@@ -198,7 +261,7 @@ int ddpca_problem_set_coarse_operators(ddpca_problem_t h, int64_t muscSett, cons
         for (int64_t tv = 0; tv < nsub; ++tv) {
             const MULTIGRID& g = P.mc.multGrid[tv];
             C.globTran_D_full.push_back(to_csr(globTran_D_1[tv], "globTran_D_1"));
-            expect_shape(C.globTran_D_full.back(), C.n, 3 * g.leveCount.back(), "globTran_D_1");
+            expect_shape(C.globTran_D_full.back(), C.n, 3 * g.nodalCount(), "globTran_D_1");
             C.accuProl_full.push_back(to_csr(accuProl[tv], "accuProl"));
             expect_shape(C.accuProl_full.back(), g.freeCount.back(), g.freeCount[P.mc.doleMcsc[tv]], "accuProl");
         }
@@ -244,7 +307,7 @@ int ddpca_problem_set_coarse_latin(ddpca_problem_t h, const int64_t* doleMcsc, c
             for (int s = 0; s < 2; ++s) {
                 const Interface& itf = P.mc.searCont[ts];
                 if (itf.inteMass[s].ptr.empty()) throw ApiError(DDPCA_ESTATE, "set every interface before the coarse operators");
-                const int64_t n3 = 3 * P.mc.multGrid[itf.body[s]].leveCount.back();
+                const int64_t n3 = 3 * P.mc.multGrid[itf.body[s]].nodalCount();
                 C.globTran_L[ts][s] = to_csr(globTran[2 * ts + s], "globTran");
                 C.globTran_pena_L[ts][s] = to_csr(globTran_pena[2 * ts + s], "globTran_pena");
                 C.globTran_D_L[ts][s] = to_csr(globTran_D[2 * ts + s], "globTran_D");

@@ -662,6 +662,10 @@ struct ddpca_mcontact {
     struct Sub {
         int64_t tv = 0, nn = 0;
         int64_t dof0 = 0;  // first dof in the batch's fine layout
+        int64_t nh = 0;    // hanging-level dofs (MULTIGRID::hangProl rows), at W[oH + hoff]
+        int64_t hoff = 0;
+        // workspace index of the subdomain's nodal dof c (position numbering, hanging level last)
+        int64_t wcol(int64_t c, int64_t oH) const { return c < 3 * nn ? dof0 + c : oH + hoff + (c - 3 * nn); }
     };
     struct Side {
         int64_t ts = 0, s = 0, tv = 0, m = 0, mip = 0;
@@ -694,9 +698,10 @@ struct ddpca_mcontact {
     DevBuf<double> cval;
     int64_t ncrow = 0;
     int64_t R = 0;                       // padded rows of all owned sides
-    // workspace W = [u (NU) | aux, lambda (2R) | gamma (G)] and its regions
+    // workspace W = [u (NU) | u on hanging levels (NH) | aux, lambda (2R) | gamma (G)] and its regions
     DevBuf<double> W;
-    int64_t NU = 0, G = 0, oS = 0, oG = 0;
+    int64_t NU = 0, NH = 0, G = 0, oH = 0, oS = 0, oG = 0;
+    SellOp op_hang;                      // hanging-level values: rows of prolOper[maxiLeve] over u
     double* u = nullptr;
     double* state = nullptr;
     double* gamma = nullptr;
@@ -747,6 +752,7 @@ void build(ddpca_mcontact& H, Problem& P) {
         ddpca_mcontact::Sub S;
         S.tv = tv;
         S.nn = g.leveCount.back();
+        S.nh = 3 * (g.nodalCount() - S.nn);
         H.subs.push_back(S);
     }
     if (!ops.empty()) {
@@ -762,6 +768,11 @@ void build(ddpca_mcontact& H, Problem& P) {
     };
     const int64_t NN = H.mg ? H.mg->lev.back().nn : 0;
     H.NU = std::max<int64_t>(3 * NN, 64);
+    for (auto& S : H.subs) {
+        S.hoff = H.NH;
+        H.NH += S.nh;
+    }
+    H.NH = pad64(H.NH);
     {
         std::vector<double> cf(H.NU, 0.0), pr(H.NU, 0.0);
         std::vector<int32_t> on(std::max<int64_t>(NN, 1));
@@ -829,14 +840,15 @@ void build(ddpca_mcontact& H, Problem& P) {
     std::sort(H.itfs.begin(), H.itfs.end(), [](const auto& a, const auto& b) { return a.ts < b.ts; });
     H.G = pad64(std::max<int64_t>(goff, 1));
     // ---- workspace
-    H.oS = H.NU;
-    H.oG = H.NU + 2 * H.R;
+    H.oH = H.NU;
+    H.oS = H.NU + H.NH;
+    H.oG = H.oS + 2 * H.R;
     H.W.alloc(H.oG + H.G);
     H.W.zero(H.main);
     H.u = H.W.p;
     H.state = H.W.p + H.oS;
     H.gamma = H.W.p + H.oG;
-    H.uo.alloc(H.NU);
+    H.uo.alloc(H.NU + H.NH);
     H.uo.zero(H.main);
     H.state_old.alloc(std::max<int64_t>(2 * H.R, 2));
     H.state_old.zero(H.main);
@@ -852,7 +864,7 @@ void build(ddpca_mcontact& H, Problem& P) {
             const auto& I = itf_of(sd.ts);
             const int s = (int)sd.s;
             const double half = s == 0 ? 0.5 : -0.5;
-            const int64_t u0 = H.subs[sd.sub].dof0;
+            const auto& Su = H.subs[sd.sub];
             const int64_t lam0 = H.oS + H.R + sd.roff, aux0 = H.oS + sd.roff;
             // gamma half: +-1/2 (inpoLagr lambda + pemaInpo_r u); side 0 adds -1/2 pema g
             const Csr& Lg = itf.inpoLagr[s];
@@ -860,7 +872,7 @@ void build(ddpca_mcontact& H, Problem& P) {
             for (int64_t i = 0; i < sd.mip; ++i) {
                 auto& row = rg[I.goff + i];
                 for (int64_t k = Lg.ptr[i]; k < Lg.ptr[i + 1]; ++k) row.push_back({lam0 + Lg.col[k], half * Lg.val[k]});
-                for (int64_t k = Rg.ptr[i]; k < Rg.ptr[i + 1]; ++k) row.push_back({u0 + Rg.col[k], half * Rg.val[k]});
+                for (int64_t k = Rg.ptr[i]; k < Rg.ptr[i + 1]; ++k) row.push_back({Su.wcol(Rg.col[k], H.oH), half * Rg.val[k]});
                 if (s == 0) gc[I.goff + i] = -0.5 * (itf.pemaDiag[i] * itf.inpoNgap[i]);
             }
             // aux RHS: systTran_pena^T u + inteMass lambda + inteInpo gamma
@@ -872,8 +884,8 @@ void build(ddpca_mcontact& H, Problem& P) {
                 auto& a = ra[sd.roff + r];
                 auto& l = rl[sd.roff + r];
                 for (int64_t k = tTp.ptr[r]; k < tTp.ptr[r + 1]; ++k) {
-                    a.push_back({u0 + tTp.col[k], tTp.val[k]});
-                    l.push_back({u0 + tTp.col[k], tTp.val[k]});
+                    a.push_back({Su.wcol(tTp.col[k], H.oH), tTp.val[k]});
+                    l.push_back({Su.wcol(tTp.col[k], H.oH), tTp.val[k]});
                 }
                 for (int64_t k = M.ptr[r]; k < M.ptr[r + 1]; ++k) a.push_back({lam0 + M.col[k], M.val[k]});
                 for (int64_t k = Ii.ptr[r]; k < Ii.ptr[r + 1]; ++k) a.push_back({H.oG + I.goff + Ii.col[k], Ii.val[k]});
@@ -923,11 +935,11 @@ void build(ddpca_mcontact& H, Problem& P) {
             for (const auto& sd : H.sides) {
                 const Interface& itf = mc.searCont[sd.ts];
                 const auto& I = itf_of(sd.ts);
-                const int64_t u0 = H.subs[sd.sub].dof0;
+                const auto& Su = H.subs[sd.sub];
                 const Csr tT = transpose(itf.systTran[sd.s]);
                 const Csr& Ii = itf.inteInpo[sd.s];
                 for (int64_t r = 0; r < sd.m; ++r) {
-                    for (int64_t k = tT.ptr[r]; k < tT.ptr[r + 1]; ++k) rwv[sd.roff + r].push_back({u0 + tT.col[k], tT.val[k]});
+                    for (int64_t k = tT.ptr[r]; k < tT.ptr[r + 1]; ++k) rwv[sd.roff + r].push_back({Su.wcol(tT.col[k], H.oH), tT.val[k]});
                     for (int64_t k = Ii.ptr[r]; k < Ii.ptr[r + 1]; ++k)
                         rwv[H.R + sd.roff + r].push_back({H.oG + I.goff + Ii.col[k], Ii.val[k]});
                     ri[sd.roff + r] = 1.0 / itf.penN;
@@ -960,14 +972,27 @@ void build(ddpca_mcontact& H, Problem& P) {
                     const auto& sd = H.sides[side_of.at({ts, s})];
                     const Csr& Tp = itf.systTran_pena[s];
                     const Csr& T = itf.systTran[s];
+                    const int64_t n3 = 3 * S.nn;
                     for (int64_t r = 0; r < Tp.nrow; ++r) {
-                        // only free dofs the interface actually couples (surface rows)
-                        if (!g.consFlag[r] || (Tp.ptr[r] == Tp.ptr[r + 1] && T.ptr[r] == T.ptr[r + 1])) continue;
-                        auto& row = rowmap[H.mg->fine_dof((int)si, r)];  // added into the solver RHS
-                        for (int64_t k = Tp.ptr[r]; k < Tp.ptr[r + 1]; ++k)
-                            row.push_back({(int32_t)(H.oS + sd.roff + Tp.col[k]), Tp.val[k]});
-                        for (int64_t k = T.ptr[r]; k < T.ptr[r + 1]; ++k)
-                            row.push_back({(int32_t)(H.oS + H.R + sd.roff + T.col[k]), -T.val[k]});
+                        // only the rows the interface actually couples (surface rows)
+                        if (Tp.ptr[r] == Tp.ptr[r + 1] && T.ptr[r] == T.ptr[r + 1]) continue;
+                        // a hanging-level row reaches the free dofs through prolOper[maxiLeve]^T
+                        // (ADDITIONAL_FORCE, MULTIGRID.h:1257-1261)
+                        std::vector<std::pair<int64_t, double>> tgt;
+                        if (r < n3) {
+                            tgt.push_back({r, 1.0});
+                        } else {
+                            const Csr& Hp = g.hangProl;
+                            for (int64_t k = Hp.ptr[r - n3]; k < Hp.ptr[r - n3 + 1]; ++k) tgt.push_back({Hp.col[k], Hp.val[k]});
+                        }
+                        for (const auto& [d, w] : tgt) {
+                            if (!g.consFlag[d] || w == 0.0) continue;
+                            auto& row = rowmap[H.mg->fine_dof((int)si, d)];  // added into the solver RHS
+                            for (int64_t k = Tp.ptr[r]; k < Tp.ptr[r + 1]; ++k)
+                                row.push_back({(int32_t)(H.oS + sd.roff + Tp.col[k]), w * Tp.val[k]});
+                            for (int64_t k = T.ptr[r]; k < T.ptr[r + 1]; ++k)
+                                row.push_back({(int32_t)(H.oS + H.R + sd.roff + T.col[k]), -w * T.val[k]});
+                        }
                     }
                 }
             }
@@ -976,11 +1001,18 @@ void build(ddpca_mcontact& H, Problem& P) {
         std::vector<int64_t> cptr{0};
         std::vector<int32_t> ccol;
         std::vector<double> cval;
-        for (const auto& kv : rowmap) {
+        for (auto& kv : rowmap) {
             crow.push_back((int32_t)kv.first);
-            for (const auto& e : kv.second) {
-                ccol.push_back(e.first);
-                cval.push_back(e.second);
+            // merge duplicate columns (hanging rows folded onto the same free dof)
+            std::stable_sort(kv.second.begin(), kv.second.end(),
+                             [](const auto& a, const auto& b) { return a.first < b.first; });
+            for (size_t e = 0; e < kv.second.size();) {
+                size_t f = e;
+                double v = 0.0;
+                for (; f < kv.second.size() && kv.second[f].first == kv.second[e].first; ++f) v += kv.second[f].second;
+                ccol.push_back(kv.second[e].first);
+                cval.push_back(v);
+                e = f;
             }
             cptr.push_back((int64_t)ccol.size());
         }
@@ -990,11 +1022,22 @@ void build(ddpca_mcontact& H, Problem& P) {
         H.ccol.upload(ccol);
         H.cval.upload(cval);
     }
+    // ---- hanging-level values over u: one SELL-64 product (rows of prolOper[maxiLeve])
+    if (H.NH) {
+        Rows rh(H.NH);
+        for (const auto& S : H.subs) {
+            const Csr& Hp = mc.multGrid[S.tv].hangProl;
+            for (int64_t r = 0; r < S.nh; ++r)
+                for (int64_t k = Hp.ptr[r]; k < Hp.ptr[r + 1]; ++k) rh[S.hoff + r].push_back({S.wcol(Hp.col[k], H.oH), Hp.val[k]});
+        }
+        H.op_hang.build(rh);
+    }
     int64_t maxn = 1;
-    for (auto& S : H.subs) maxn = std::max(maxn, 3 * S.nn);
+    for (auto& S : H.subs) maxn = std::max(maxn, std::max(3 * S.nn, S.nh));
     for (auto& sd : H.sides) maxn = std::max(maxn, sd.m);
     H.partial.alloc(2 * nb256(maxn));
-    const int64_t nmon = 2 * H.nsub + 8 * H.nint;
+    // monitor norms [2 nsub u | 8 nint aux, lambda | 2 nsub hanging-level parts of u]
+    const int64_t nmon = 4 * H.nsub + 8 * H.nint;
     H.moni.alloc(nmon);
     H.moni_host.assign(nmon, 0.0);
     H.moniReco.assign(H.nsub + 4 * H.nint, std::vector<double>(10, 0.0));
@@ -1031,7 +1074,10 @@ void build_coarse(ddpca_mcontact& H, Problem& P) {
         if (cs.latin) {  // + globTran lambda - globTran_pena aux + globTran_D u   (MCONTACT.h:2540-2548)
             add_rows(cs.globTran_L[sd.ts][sd.s], lam0, 1.0);
             add_rows(cs.globTran_pena_L[sd.ts][sd.s], aux0, -1.0);
-            add_rows(cs.globTran_D_L[sd.ts][sd.s], H.subs[sd.sub].dof0, 1.0);
+            const auto& Su = H.subs[sd.sub];
+            const Csr& D = cs.globTran_D_L[sd.ts][sd.s];
+            for (int64_t r = 0; r < D.nrow; ++r)
+                for (int64_t k = D.ptr[r]; k < D.ptr[r + 1]; ++k) rows[r].push_back({(int32_t)Su.wcol(D.col[k], H.oH), D.val[k]});
         } else {
             add_rows(cs.globTran_1[sd.ts][sd.s], lam0, 1.0);
         }
@@ -1040,9 +1086,9 @@ void build_coarse(ddpca_mcontact& H, Problem& P) {
         // factored: the interface part (the stiffness part is the SpMV + restriction chain);
         // assembled: the caller's whole globTran_D_1
         const Csr& T = cs.assembled ? cs.globTran_D_full[H.subs[i].tv] : cs.globTran_S[H.subs[i].tv];
-        const int64_t u0 = H.subs[i].dof0;
+        const auto& Su = H.subs[i];
         for (int64_t r = 0; r < T.nrow; ++r)
-            for (int64_t k = T.ptr[r]; k < T.ptr[r + 1]; ++k) rows[r].push_back({(int32_t)(u0 + T.col[k]), -T.val[k]});
+            for (int64_t k = T.ptr[r]; k < T.ptr[r + 1]; ++k) rows[r].push_back({(int32_t)Su.wcol(T.col[k], H.oH), -T.val[k]});
     }
     {
         std::vector<int64_t> ptr(n + 1, 0);
@@ -1277,6 +1323,8 @@ void pair_norm(ddpca_mcontact& H, const double* a, const double* o, int64_t n, i
 bool monitor(ddpca_mcontact& H) {
     const int64_t cyc = 10;
     const int64_t tc = H.tc;
+    const int64_t hb = 2 * H.nsub + 8 * H.nint;  // hanging-level parts of the subdomain norms
+    for (int64_t k = 0; k < 2 * H.nsub; ++k) H.moni_host[k] += H.moni_host[hb + k];
     bool flag0 = tc >= cyc, flag1 = true;
     const double c0 = 0.1, c1 = 1.0e-12;
     double convValu = 0.0, convCrit = 0.0;
@@ -1339,7 +1387,7 @@ bool iterate_once(ddpca_mcontact& H, bool check) {
     hipStream_t st = H.main;
     // snapshot for MONITOR (resuDisp_0 / inteAuxi_0 / inteLagr_0, MCONTACT.h:2507-2509)
     if (H.R) copy_dev(st, H.state_old.p, H.state, 2 * H.R);
-    copy_dev(st, H.uo.p, H.u, H.NU);
+    copy_dev(st, H.uo.p, H.u, H.NU + H.NH);
     // ---- body balance: every owned subdomain in one batched PCG
     if (H.mg) {
         MgpisDevice& D = *H.mg;
@@ -1351,9 +1399,14 @@ bool iterate_once(ddpca_mcontact& H, bool check) {
         D.pcg_wait(1, 0);
         hipLaunchKernelGGL(k_outp, dim3(nb256(D.lev.back().nn)), dim3(256), 0, st, D.xs.p, D.lev.back().mask.p,
                            H.onode.p, H.presc.p, H.u, D.lev.back().nn);
+        if (H.NH) H.op_hang.apply(st, H.W.p, H.W.p + H.oH, nullptr);  // OUTP_SUB1's prolOper[maxiLeve] rows
     }
-    // ---- interface-eliminated coarse-space correction (MCONTACT.h:2578-2612)
-    if (H.cs.on && H.tc <= H.mult_maxi) coarse_correct(H);
+    // ---- coarse-space correction (MCONTACT.h:2540-2612); OUTP_SUB1 of the correction reaches the
+    //      hanging level through the same rows, so they are recomputed from the corrected u
+    if (H.cs.on && H.tc <= H.mult_maxi) {
+        coarse_correct(H);
+        if (H.NH) H.op_hang.apply(st, H.W.p, H.W.p + H.oH, nullptr);
+    }
     DDPCA_HIP(hipEventRecord(H.ev[1], st));
     const double t_solve = ms_since(t0);
     // ---- interface balance: this rank's gamma halves, one launch for every owned side
@@ -1395,7 +1448,11 @@ bool iterate_once(ddpca_mcontact& H, bool check) {
     }
     // ---- MONITOR norms (owned entries; others zero) and their reduction across ranks
     DDPCA_HIP(hipMemsetAsync(H.moni.p, 0, H.moni.n * sizeof(double), st));
-    for (auto& S : H.subs) pair_norm(H, H.u + S.dof0, H.uo.p + S.dof0, 3 * S.nn, 2 * S.tv);
+    for (auto& S : H.subs) {
+        pair_norm(H, H.u + S.dof0, H.uo.p + S.dof0, 3 * S.nn, 2 * S.tv);
+        if (S.nh)
+            pair_norm(H, H.u + H.oH + S.hoff, H.uo.p + H.oH + S.hoff, S.nh, 2 * H.nsub + 8 * H.nint + 2 * S.tv);
+    }
     for (auto& sd : H.sides) {
         const int64_t base = 2 * H.nsub + 8 * sd.ts + 4 * sd.s;
         pair_norm(H, H.state + sd.roff, H.state_old.p + sd.roff, sd.m, base);
@@ -1517,9 +1574,14 @@ int64_t mcontact_gpu_get(mcontact_t h, const char* what, int64_t index, void* ou
         DDPCA_HIP(hipStreamSynchronize(h->main));
         if (w == "resuDisp") {
             for (auto& S : h->subs)
-                if (S.tv == index) {
-                    n = 3 * S.nn;
-                    if (out) DDPCA_HIP(hipMemcpy(out, h->u + S.dof0, std::min(n, cap) * sizeof(double), hipMemcpyDeviceToHost));
+                if (S.tv == index) {  // position numbering: level-maxiLeve nodes, then the hanging level
+                    n = 3 * S.nn + S.nh;
+                    if (out) {
+                        DDPCA_HIP(hipMemcpy(out, h->u + S.dof0, std::min(3 * S.nn, cap) * sizeof(double), hipMemcpyDeviceToHost));
+                        if (cap > 3 * S.nn && S.nh)
+                            DDPCA_HIP(hipMemcpy(static_cast<double*>(out) + 3 * S.nn, h->u + h->oH + S.hoff,
+                                                std::min(S.nh, cap - 3 * S.nn) * sizeof(double), hipMemcpyDeviceToHost));
+                    }
                     return;
                 }
             throw ApiError(DDPCA_EINVAL, "subdomain not owned by this rank");

@@ -49,6 +49,14 @@ public:
     std::vector<int64_t> leveCount;   // nodes of levels <= l  (levels 0..maxiLeve)
     std::vector<Stencil> scalProl;    // level l+1 nodes x level l nodes
     void TRANSFER();
+    // Hanging level (operator-level builder only): the reference puts hanging nodes of local
+    // refinement and coupled nodes on a level maxiLeve + 1 outside the MGPIS hierarchy
+    // (MULTIGRID.h:836-848, 870-875, 884-910); their values are rows of prolOper[maxiLeve] applied
+    // to the level-maxiLeve nodal vector (OUTP_SUB1, MULTIGRID.h:1279).  nodeAll = 0: none.
+    int64_t nodeAll = 0;
+    Csr hangProl;  // 3 (nodeAll - leveCount.back()) x 3 leveCount.back(), position numbering
+    // nodes of the subdomain's nodal vectors (resuDisp, interface operator columns)
+    int64_t nodalCount() const { return nodeAll ? nodeAll : leveCount.back(); }
 
     // ---------------------------------------------------------------- stiffness
     double mateElas = 210.0e9;

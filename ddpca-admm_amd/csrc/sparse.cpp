@@ -227,10 +227,13 @@ Stencil prol_to_stencil(int64_t nf, int64_t nc, int64_t nfree_f, const int32_t* 
     for (int64_t i = 0; i < nf; ++i) {
         auto& v = rows[i];
         if (i < nc) {  // identity rows (MULTIGRID.h:1144-1146): the node itself, weight 1
+            // realProl = consOper_f·prolOper·consOper_cᵀ (MULTIGRID.h:1248): a constrained dof has
+            // no row (fine side) or no column (coarse side), so only free×free entries are checked
             for (const Blk& x : v)
                 for (int a = 0; a < 3; ++a)
                     for (int b = 0; b < 3; ++b)
-                        if (x.b[3 * a + b] != ((x.p == i && a == b) ? 1.0 : 0.0))
+                        if ((fmask[i] >> a & 1) && (x.cm >> b & 1) &&
+                            x.b[3 * a + b] != ((x.p == i && a == b) ? 1.0 : 0.0))
                             throw std::invalid_argument("realProl: coarse node row is not the identity");
             S.col.push_back((int32_t)i);
             S.w.push_back(1.0);

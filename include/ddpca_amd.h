@@ -222,6 +222,26 @@ int ddpca_problem_set_subdomain(ddpca_problem_t p, int64_t tv, int nlev, const i
                                 const double* const* K_val, const int64_t* const* S_ptr,
                                 const int32_t* const* S_col, const double* const* S_w,
                                 const double* consForc, const double* presc, const double* coords);
+/* Same, with the transfers as the reference's MGPIS::realProl[l] (condensed CSR, nfree[l+1] x
+ * nfree[l], MULTIGRID.h:1141-1181, 1246-1249) instead of scalProl -- hierarchies with rotated nodes
+ * (MULTIGRID::nodeRota: DEHW hubs) whose w R_off^T R_par blocks a scalar stencil cannot hold; the
+ * blocks run as block entries (as mgpis_gpu_create_prol). */
+int ddpca_problem_set_subdomain_prol(ddpca_problem_t p, int64_t tv, int nlev, const int64_t* nnodes,
+                                     const int64_t* nfree, const int32_t* const* free_dof,
+                                     const int64_t* const* K_ptr, const int32_t* const* K_col,
+                                     const double* const* K_val, const int64_t* const* P_ptr,
+                                     const int32_t* const* P_col, const double* const* P_val,
+                                     const double* consForc, const double* presc, const double* coords);
+/* The hanging level of subdomain tv (after set_subdomain, before its interfaces): locally refined
+ * meshes (CYLINDER) put hanging nodes -- and coupled nodes -- on a level maxiLeve + 1 outside the
+ * MGPIS hierarchy (MULTIGRID.h:836-848, 884-910); OUTP_SUB1 gives them prolOper[maxiLeve] of the
+ * level-maxiLeve vector (MULTIGRID.h:1279).  nnodes_all = all nodes of the subdomain (the
+ * interface operators' 3 N columns / rows); hang = rows 3 nnodes[nlev-1] .. 3 nnodes_all - 1 of
+ * prolOper[maxiLeve] in the position numbering (3 (nnodes_all - nnodes[nlev-1]) x
+ * 3 nnodes[nlev-1]).  The device keeps those values in u as well: MONITOR's norms, resuDisp and the
+ * interface products see every node, and the body-balance RHS folds the hanging rows in
+ * (ADDITIONAL_FORCE's prolOper^T, MULTIGRID.h:1257-1261). */
+int ddpca_problem_set_hanging(ddpca_problem_t p, int64_t tv, int64_t nnodes_all, const ddpca_csr_t* hang);
 /* Interface ts between contBody {body0, body1} with fricCoef fric (< 0 glued, 0 frictionless,
  * > 0 Coulomb; comp = 1 if fric == 0 else 3), nip integration points, nnc_s contact nodes per
  * side; pemaDiag / inpoNgap have comp*nip entries.  ops[7*s + k] is side s's

@@ -10,8 +10,11 @@
 // posiNode, MULTIGRID.h:884-910) and maps to node ids with earlTran (OUTP_SUB1,
 // MULTIGRID.h:1263-1281).  The device problem uses ONE nodal numbering per subdomain -- the
 // position numbering -- so the interface operators that act on node-id vectors are moved to it:
-// systTran(_pena) rows by earlTran^T, pemaInpo_r columns by earlTran.  Hanging-node prolOper and
-// nodal rotations are identities on uniformly refined meshes (the scope of this path).
+// systTran(_pena) rows by earlTran^T, pemaInpo_r columns by earlTran.  Positions past the MGPIS
+// fine level are the hanging level (hanging nodes of local refinement, coupled nodes; MULTIGRID.h:
+// 836-848, 884-910): their rows of prolOper[maxiLeve] go along (ddpca_problem_set_hanging).  A
+// subdomain with rotated nodes (nodeRota) hands its realProl over instead of scalProl: its
+// transfers carry w R_off^T R_par blocks (MULTIGRID.h:1141-1181) a scalar stencil cannot hold.
 #pragma once
 #include <stdexcept>
 #include <string>
@@ -129,9 +132,32 @@ inline ddpca_problem_t from_reference(MCONTACT& mc) {
     for (int64_t tv = 0; tv < nsub; ++tv) {
         MULTIGRID& g = mc.multGrid[tv];
         Hierarchy h(g);
-        check(ddpca_problem_set_subdomain(p, tv, h.nlev, h.nnodes.data(), h.nfree.data(), h.fd_p.data(), h.Kp.data(),
-                                          h.Kc.data(), h.Kv.data(), h.Sp.data(), h.Sc.data(), h.Sv.data(),
-                                          g.consForc.data(), h.presc.data(), h.coords.data()));
+        if (g.nodeRota.empty()) {
+            check(ddpca_problem_set_subdomain(p, tv, h.nlev, h.nnodes.data(), h.nfree.data(), h.fd_p.data(), h.Kp.data(),
+                                              h.Kc.data(), h.Kv.data(), h.Sp.data(), h.Sc.data(), h.Sv.data(),
+                                              g.consForc.data(), h.presc.data(), h.coords.data()));
+        } else {
+            std::vector<Csr> P;
+            std::vector<const int64_t*> Pp;
+            std::vector<const int32_t*> Pc;
+            std::vector<const double*> Pv;
+            for (int l = 0; l + 1 < h.nlev; ++l) P.emplace_back(g.mgpi.realProl[l]);
+            for (auto& q : P) {
+                Pp.push_back(q.ptr.data());
+                Pc.push_back(q.m.innerIndexPtr());
+                Pv.push_back(q.m.valuePtr());
+            }
+            check(ddpca_problem_set_subdomain_prol(p, tv, h.nlev, h.nnodes.data(), h.nfree.data(), h.fd_p.data(),
+                                                   h.Kp.data(), h.Kc.data(), h.Kv.data(), Pp.data(), Pc.data(), Pv.data(),
+                                                   g.consForc.data(), h.presc.data(), h.coords.data()));
+        }
+        const int64_t NL = h.nnodes.back(), Nall = (int64_t)g.nodeCoor.size();
+        if (Nall > NL) {  // hanging level: rows 3 NL.. of prolOper[maxiLeve] (positions x positions)
+            const SpMat& Pm = g.prolOper[g.mgpi.maxiLeve];
+            const Csr hang(SpMat(Pm.bottomRows(Pm.rows() - 3 * NL)));
+            const ddpca_csr_t hv = hang.view();
+            check(ddpca_problem_set_hanging(p, tv, Nall, &hv));
+        }
     }
     for (int64_t ts = 0; ts < nint; ++ts) {
         std::vector<Csr> ops;

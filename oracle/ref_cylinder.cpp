@@ -1,0 +1,125 @@
+// ORACLE TEST INFRASTRUCTURE -- NOT PART OF THE PRODUCT.
+//
+// The reference's own CYLINDER example (examples/CYLINDER_1.h: a stack of four cylinder bodies
+// in Hertz contact, locally refined towards the contact lines -- hanging nodes on a level past
+// the MGPIS hierarchy, MULTIGRID.h:836-848 -- contact search on the curved surfaces, LATIN-type
+// coarse space muscSett = 1 with doleMcsc = 2).  The reference builds it at a reduced size and
+// runs its own CONTACT_ANALYSIS; oracle/ref_bind.hpp hands the same operators (with the hanging
+// level, ddpca_problem_set_hanging) to the device, whose ADMM loop then runs.  One JSON line on
+// stderr: iterations, resuDisp difference (node-id order, every node incl. the hanging ones), the
+// resuMoni trajectory and the contact pressures against the reference's last resuCont files.
+//   ref_cylinder copyNumb locaLeve globInho bandWidt
+#include <unistd.h>
+
+#include <cstdio>
+#include <fstream>
+#include <sstream>
+
+#include "examples/CYLINDER_1.h"
+#include "ref_bind.hpp"
+
+namespace {
+
+std::vector<std::vector<double>> read_rows(const std::string& path) {
+    std::vector<std::vector<double>> rows;
+    std::ifstream f(path);
+    std::string line;
+    while (std::getline(f, line)) {
+        std::istringstream is(line);
+        std::vector<double> r;
+        double v;
+        while (is >> v) r.push_back(v);
+        if (!r.empty()) rows.push_back(r);
+    }
+    return rows;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    const long copyNumb = argc > 1 ? std::atol(argv[1]) : 1;
+    const long locaLeve = argc > 2 ? std::atol(argv[2]) : 4;
+    const long globInho = argc > 3 ? std::atol(argv[3]) : 2;
+    const double bandWidt = argc > 4 ? std::atof(argv[4]) : 2.0e-4;
+    const int saved = dup(1);
+    if (!std::freopen("/dev/null", "w", stdout)) return 2;  // the reference's progress output
+    CYLINDER_1 c;  // creates ./Cylinder/ for the reference's result files
+    c.copyNumb = copyNumb;
+    c.locaLeve = locaLeve;
+    c.globInho = globInho;
+    c.bandWidt = bandWidt;
+    c.SOLVE(1);  // MESH, contact search, ESTABLISH and the reference's CONTACT_ANALYSIS
+    std::fflush(stdout);
+    dup2(saved, 1);
+    long nhang = 0, nnodes = 0;
+    for (auto& g : c.multGrid) {
+        nnodes += (long)g.nodeCoor.size();
+        nhang += (long)g.leveNode[g.mgpi.maxiLeve + 1].size();
+    }
+    ddpca_problem_t p = ddpca_bind::from_reference(c);
+    std::vector<int32_t> owner(c.multGrid.size(), 0);
+    mcontact_t h = nullptr;
+    ddpca_bind::check(mcontact_gpu_create(p, 0, 0, 1, owner.data(), nullptr, &h));
+    const int64_t n_gpu = mcontact_gpu_iterate(h, 3000, 1);
+    ddpca_bind::check((int)std::min<int64_t>(n_gpu, 0));
+    // displacements: position order (hanging level last) -> node-id order
+    double du = 0.0;
+    for (size_t tv = 0; tv < c.multGrid.size(); ++tv) {
+        const MULTIGRID& g = c.multGrid[tv];
+        Eigen::VectorXd u_pos(g.earlTran.cols());
+        const int64_t n = mcontact_gpu_get(h, "resuDisp", tv, u_pos.data(), u_pos.size());
+        ddpca_bind::check((int)std::min<int64_t>(n, 0));
+        if (n != u_pos.size()) {
+            std::fprintf(stderr, "resuDisp of %zu has %ld entries, expected %ld\n", tv, (long)n, (long)u_pos.size());
+            return 1;
+        }
+        const Eigen::VectorXd u = g.earlTran * u_pos;
+        du = std::max(du, (u - c.resuDisp[tv]).norm() / c.resuDisp[tv].norm());
+    }
+    // resuMoni rows (the reference's file, scientific 20 digits) vs the device's monitor rows
+    const auto ref_moni = read_rows(DIRECTORY("resuMoni.txt"));
+    const int64_t ncol = 2 * (int64_t)c.multGrid.size() + 8 * (int64_t)c.searCont.size() + 2;
+    const int64_t nrows = mcontact_gpu_monitor(h, nullptr, 0);
+    std::vector<double> moni(nrows * ncol);
+    mcontact_gpu_monitor(h, moni.data(), nrows);
+    double dmoni = 0.0;  // rows k <= 50, the columns of the squared norms (even columns), relative
+    const int64_t kmax = std::min<int64_t>(std::min<int64_t>(50, nrows), (int64_t)ref_moni.size());
+    for (int64_t k = 0; k < kmax; ++k)
+        for (int64_t j = 1; j < ncol; j += 2) {  // odd columns: ||u||^2, ||aux||^2, ...: well scaled
+            const double r = ref_moni[k][j], d = moni[k * ncol + j];
+            if (r != 0.0) dmoni = std::max(dmoni, std::abs(d - r) / std::abs(r));
+        }
+    // contact pressures (frictionless: one gamma_n per ip) vs the reference's last resuCont
+    std::string itf = "[";
+    std::vector<double> gam(1 << 22);
+    double dp_all = 0.0;
+    for (size_t ts = 0; ts < c.searCont.size(); ++ts) {
+        const int64_t n = mcontact_gpu_get(h, "inpoGamm", ts, gam.data(), (int64_t)gam.size());
+        ddpca_bind::check((int)std::min<int64_t>(n, 0));
+        const auto ref = read_rows(DIRECTORY("resuCont_" + std::to_string(ts) + ".txt"));
+        const int comp = c.fricCoef[ts] == 0.0 ? 1 : 3;
+        double pmax = 0.0, dp = 0.0, gmax = 0.0;
+        int64_t active = 0;
+        for (size_t i = 0; i < ref.size(); ++i) pmax = std::max(pmax, ref[i][0]);
+        for (int64_t i = 0; i < n / comp && i < (int64_t)ref.size(); ++i) {
+            const double g = gam[comp * i], r = ref[i][0];
+            gmax = std::max(gmax, g);
+            if (r > 0.0) ++active;
+            dp = std::max(dp, std::abs(g - r) / std::max(pmax, 1e-300));
+        }
+        dp_all = std::max(dp_all, dp);
+        char buf[200];
+        std::snprintf(buf, sizeof(buf), "%s{\"ts\": %zu, \"nip\": %ld, \"active\": %ld, \"pmax_ref\": %.9g, \"pmax_gpu\": %.9g, \"dp\": %.3g}",
+                      ts ? ", " : "", ts, (long)(n / comp), (long)active, pmax, gmax, dp);
+        itf += buf;
+    }
+    itf += "]";
+    mcontact_gpu_destroy(h);
+    ddpca_problem_destroy(p);
+    std::fprintf(stderr,
+                 "{\"subdomains\": %zu, \"nodes\": %ld, \"hanging_nodes\": %ld, \"iters_gpu\": %ld, \"iters_ref\": %ld, "
+                 "\"resuDisp_rel\": %.3g, \"moni_rows\": %ld, \"moni_rel\": %.3g, \"pressure_rel\": %.3g, \"interfaces\": %s}\n",
+                 c.multGrid.size(), nnodes, nhang, (long)n_gpu, (long)c.iterNumbReco, du, (long)kmax, dmoni, dp_all,
+                 itf.c_str());
+    return 0;
+}

@@ -54,3 +54,36 @@ def test_unset_members_are_reported(ddpca):
         L.ddpca_problem_destroy(h)
     with pytest.raises(ddpca.DdpcaError):
         ddpca.Problem.from_operators([], [])
+
+
+def test_realprol_handover_equals_stencils(ddpca, pair):
+    """ddpca_problem_set_subdomain_prol (the reference's realProl instead of scalProl, for rotated
+    hierarchies) rebuilds the same stencils on a plain hierarchy: realProl read back is exact."""
+    P, subs, ifaces = pair
+    subs_p = []
+    for tv, s in enumerate(subs):
+        G = P.grid(tv)
+        d = {k: v for k, v in s.items() if k != "S"}
+        d["P"] = [G.realProl(l) for l in range(G.maxiLeve)]
+        subs_p.append(d)
+    Q = ddpca.Problem.from_operators(subs_p, ifaces)
+    for tv in range(P.nsub):
+        G, H = P.grid(tv), Q.grid(tv)
+        for l in range(G.maxiLeve):
+            assert abs(G.realProl(l) - H.realProl(l)).max() == 0.0
+
+
+def test_hanging_level_shapes(ddpca, pair):
+    """The hanging level widens the subdomain's nodal space: interface operators must then have
+    3 nnodes_all rows / columns, and the hanging prolongation 3 (nnodes_all - N) x 3 N."""
+    import scipy.sparse as sp
+    P, subs, ifaces = pair
+    nL = int(subs[0]["nnodes"][-1])
+    H = sp.csr_matrix((np.full(3, 1.0), (np.arange(3), np.arange(3))), shape=(3, 3 * nL))
+    s2 = [dict(s) for s in subs]
+    s2[0]["hang"] = (nL + 1, H)
+    with pytest.raises(ddpca.DdpcaError, match="pemaInpo_r|systTran"):
+        ddpca.Problem.from_operators(s2, ifaces)  # operators still 3N wide
+    s2[0]["hang"] = (nL + 2, H)
+    with pytest.raises(ddpca.DdpcaError, match="hanging prolongation"):
+        ddpca.Problem.from_operators(s2, ifaces)

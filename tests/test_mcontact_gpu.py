@@ -351,3 +351,32 @@ def test_block_patch_pressure_known_answer(gpu, tmp_path, musc):
         assert itf["nip"] > 0
         for k in ("mean", "min", "max"):
             assert abs(itf[k] - 1e7) <= 1e-5 * 1e7, (musc, itf)
+
+
+def test_cylinder_known_answer(gpu, tmp_path):
+    """The reference's own CYLINDER example (CYLINDER_1.h, copyNumb 1: four cylinder bodies in
+    Hertz contact, locally refined towards the contact lines -- 35 % of the nodes on the hanging
+    level past the MGPIS hierarchy -- contact search on the curved surfaces, LATIN-type coarse
+    space muscSett = 1, doleMcsc = 2; oracle/ref_cylinder.cpp, reduced locaLeve 4, globInho 2,
+    contact band 2e-4): the reference builds and solves it, oracle/ref_bind.hpp hands the
+    operators over with the hanging level, and the device ADMM loop reaches the reference's
+    iteration count (+-1), resuDisp on every node (1e-6), the resuMoni norm columns of rows
+    k <= 50 (1e-7) and the contact pressures of its last resuCont files (1e-5 of the peak)."""
+    import json
+    import os
+    import subprocess
+    from pathlib import Path
+    exe = Path(__file__).resolve().parents[1] / "oracle" / "_ref" / "ref_cylinder"
+    if not exe.exists():
+        pytest.skip("oracle/_ref/ref_cylinder is built only where the reference is (travels with the snapshot)")
+    out = subprocess.run([str(exe), "1", "4", "2", "2e-4"], capture_output=True, text=True, timeout=170,
+                         env=dict(os.environ), cwd=tmp_path)
+    assert out.returncode == 0, out.stderr[-2000:]
+    res = json.loads(out.stderr.strip().splitlines()[-1])
+    assert res["hanging_nodes"] > 0, res
+    assert abs(res["iters_gpu"] - res["iters_ref"]) <= 1, res
+    assert res["resuDisp_rel"] <= 1e-6, res
+    assert res["moni_rel"] <= 1e-7, res
+    assert res["pressure_rel"] <= 1e-5, res
+    for itf in res["interfaces"]:
+        assert itf["active"] > 0, itf
