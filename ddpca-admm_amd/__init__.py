@@ -118,6 +118,7 @@ def _declare(L: C.CDLL) -> None:
         L.mcontact_gpu_create.argtypes = [_P, C.c_int, C.c_int, C.c_int, _P, C.POINTER(MgpisOptions),
                                           C.POINTER(_P)]
         L.mcontact_gpu_comm_init.argtypes = [_P, _P]
+        L.mcontact_gpu_comm_local.argtypes = [_P, C.c_int]
         L.mcontact_gpu_unique_id.argtypes = [_P]
         L.mcontact_gpu_iterate.argtypes = [_P, C.c_int64, C.c_int]
         L.mcontact_gpu_iterate.restype = C.c_int64
@@ -594,6 +595,13 @@ class MCONTACT:
     def comm_init(self, uid: bytes) -> None:
         buf = (C.c_char * 128).from_buffer_copy(uid)
         _check(lib().mcontact_gpu_comm_init(self._h, buf))
+
+    @staticmethod
+    def comm_local(ranks: Sequence["MCONTACT"]) -> None:
+        """Connect the rank handles of ONE process (ranks[r] = rank r) through the in-process test
+        transport (mcontact_gpu_comm_local); run each rank's CONTACT_ANALYSIS on its own thread."""
+        arr = (C.c_void_p * len(ranks))(*[m._h.value for m in ranks])
+        _check(lib().mcontact_gpu_comm_local(arr, len(ranks)))
 
     def CONTACT_ANALYSIS(self, maxit: int = 3000, check: bool = True) -> int:
         return _check(lib().mcontact_gpu_iterate(self._h, maxit, 1 if check else 0))

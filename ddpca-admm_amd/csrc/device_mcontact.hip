@@ -31,11 +31,15 @@
 #include <chrono>
 #include <climits>
 #include <cmath>
+#include <condition_variable>
 #include <cstdio>
 #include <cstring>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <numeric>
+#include <thread>
+#include <tuple>
 
 #include "../../include/ddpca_amd.h"
 #include "device_mgpis.hpp"
@@ -657,6 +661,111 @@ struct CoarseDev {
     std::vector<double> dense;      // host, until inverted: this rank's rows of globCoup_1 (n x n, zeros elsewhere)
 };
 
+// ============================================================================= transport
+// The exchanges of a multi-rank run, all stream-ordered on the rank's stream:
+//   exchange()      the gamma halves of cross-rank interfaces (one grouped send/recv per peer)
+//   allreduce_sum() the MONITOR norms and the coarse right-hand side every iteration, the dense
+//                   coarse matrix once at setup
+// RcclTransport is the production path (RCCL over xGMI); LocalTransport connects the handles of
+// ONE process through host-staged copies (mcontact_gpu_comm_local) so the multi-rank bookkeeping
+// (owner maps, gamma offsets, rank-local coarse rows) runs on a single GPU in the tests.
+struct Transport {
+    struct Msg {
+        int peer;
+        int64_t tag;  // interface index
+        const double* send;
+        double* recv;
+        int64_t n;
+    };
+    virtual ~Transport() = default;
+    virtual void allreduce_sum(double* buf, int64_t n, hipStream_t st) = 0;
+    virtual void exchange(const std::vector<Msg>& msgs, hipStream_t st) = 0;
+};
+
+struct RcclTransport : Transport {
+    ncclComm_t comm = nullptr;
+    ~RcclTransport() override {
+        if (comm) (void)ncclCommDestroy(comm);
+    }
+    void allreduce_sum(double* buf, int64_t n, hipStream_t st) override {
+        DDPCA_NCCL(ncclAllReduce(buf, buf, (size_t)n, ncclDouble, ncclSum, comm, st));
+    }
+    void exchange(const std::vector<Msg>& msgs, hipStream_t st) override {
+        DDPCA_NCCL(ncclGroupStart());
+        for (const Msg& m : msgs) {
+            DDPCA_NCCL(ncclSend(m.send, (size_t)m.n, ncclDouble, m.peer, comm, st));
+            DDPCA_NCCL(ncclRecv(m.recv, (size_t)m.n, ncclDouble, m.peer, comm, st));
+        }
+        DDPCA_NCCL(ncclGroupEnd());
+    }
+};
+
+// Rendezvous of the ranks of one process (each rank's calls come from its own host thread).
+struct LocalHub {
+    int n = 0;
+    std::mutex mu;
+    std::condition_variable cv;
+    int arrived = 0;
+    int64_t generation = 0;
+    bool broken = false;
+    std::vector<std::vector<double>> slot;                       // allreduce staging per rank
+    std::map<std::tuple<int, int, int64_t>, const double*> post;  // (src, dst, tag) -> device send buffer
+    void barrier() {
+        std::unique_lock<std::mutex> lk(mu);
+        if (broken) throw ApiError(DDPCA_ECOMM, "local transport: a peer failed");
+        const int64_t g = generation;
+        if (++arrived == n) {
+            arrived = 0;
+            ++generation;
+            cv.notify_all();
+        } else if (!cv.wait_for(lk, std::chrono::seconds(120), [&] { return generation != g || broken; }) || broken) {
+            broken = true;
+            cv.notify_all();
+            throw ApiError(DDPCA_ECOMM, "local transport: peers did not arrive");
+        }
+    }
+};
+
+struct LocalTransport : Transport {
+    std::shared_ptr<LocalHub> hub;
+    int rank = 0;
+    void allreduce_sum(double* buf, int64_t n, hipStream_t st) override {
+        auto& mine = hub->slot[rank];
+        mine.resize(n);
+        DDPCA_HIP(hipMemcpyAsync(mine.data(), buf, n * sizeof(double), hipMemcpyDeviceToHost, st));
+        DDPCA_HIP(hipStreamSynchronize(st));
+        hub->barrier();
+        std::vector<double> sum(n, 0.0);
+        for (int q = 0; q < hub->n; ++q)  // rank order: every rank gets the same bits
+            for (int64_t i = 0; i < n; ++i) sum[i] += hub->slot[q][i];
+        DDPCA_HIP(hipMemcpyAsync(buf, sum.data(), n * sizeof(double), hipMemcpyHostToDevice, st));
+        DDPCA_HIP(hipStreamSynchronize(st));
+        hub->barrier();  // nobody restages before every rank has read the slots
+    }
+    void exchange(const std::vector<Msg>& msgs, hipStream_t st) override {
+        DDPCA_HIP(hipStreamSynchronize(st));
+        {
+            std::lock_guard<std::mutex> lk(hub->mu);
+            for (const Msg& m : msgs) hub->post[{rank, m.peer, m.tag}] = m.send;
+        }
+        hub->barrier();
+        for (const Msg& m : msgs) {
+            const double* src = nullptr;
+            {
+                std::lock_guard<std::mutex> lk(hub->mu);
+                auto it = hub->post.find({m.peer, rank, m.tag});
+                if (it == hub->post.end()) throw ApiError(DDPCA_ECOMM, "local transport: unmatched receive");
+                src = it->second;
+            }
+            DDPCA_HIP(hipMemcpyAsync(m.recv, src, m.n * sizeof(double), hipMemcpyDeviceToDevice, st));
+        }
+        DDPCA_HIP(hipStreamSynchronize(st));
+        hub->barrier();  // the peers' send buffers stay untouched until every copy has landed
+        std::lock_guard<std::mutex> lk(hub->mu);
+        for (const Msg& m : msgs) hub->post.erase({rank, m.peer, m.tag});
+    }
+};
+
 // ================================================================================ handle
 struct ddpca_mcontact {
     struct Sub {
@@ -717,7 +826,7 @@ struct ddpca_mcontact {
     CoarseDev cs;
     std::vector<double> moni_host;
     hipStream_t main = nullptr;          // == mg->stream
-    ncclComm_t comm = nullptr;
+    std::unique_ptr<Transport> comm;     // nranks > 1: RCCL, or the in-process test transport
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     // reference MONITOR state (MCONTACT.h:2494-2498, 2725-2845)
     int64_t tc = 0;
@@ -1234,7 +1343,7 @@ void coarse_invert(ddpca_mcontact& H) {
     hipStream_t st = H.main;
     if (H.nranks > 1) {
         if (!H.comm) throw ApiError(DDPCA_ESTATE, "the coarse space of a multi-rank run needs mcontact_gpu_comm_init");
-        DDPCA_NCCL(ncclAllReduce(A.p, A.p, (size_t)n * n, ncclDouble, ncclSum, H.comm, st));
+        H.comm->allreduce_sum(A.p, n * n, st);
     }
     rocblas_handle rh = nullptr;
     if (rocblas_create_handle(&rh) != rocblas_status_success) throw ApiError(DDPCA_EHIP, "rocblas_create_handle");
@@ -1298,7 +1407,7 @@ void coarse_correct(ddpca_mcontact& H) {
                                (int64_t)G.rows.n);
         }
     }
-    if (H.nranks > 1) DDPCA_NCCL(ncclAllReduce(C.g.p, C.g.p, n, ncclDouble, ncclSum, H.comm, st));
+    if (H.nranks > 1) H.comm->allreduce_sum(C.g.p, n, st);
     if (!C.nown) return;
     hipLaunchKernelGGL(k_gemv_wave, dim3(ceil_div(C.nown, 4)), dim3(256), 0, st, C.ainv.p, C.g.p, C.xc.p, C.nown, n);
     if (C.assembled) {
@@ -1416,14 +1525,13 @@ bool iterate_once(ddpca_mcontact& H, bool check) {
     DDPCA_HIP(hipEventRecord(H.ev[0], st));
     if (any_cross) {
         if (!H.comm) throw ApiError(DDPCA_ESTATE, "cross-rank interfaces need mcontact_gpu_comm_init");
-        DDPCA_NCCL(ncclGroupStart());
+        std::vector<Transport::Msg> msgs;
         for (auto& I : H.itfs) {
             if (!(I.cross && I.mine)) continue;
             const int peer = I.owner[0] == H.rank ? I.owner[1] : I.owner[0];
-            DDPCA_NCCL(ncclSend(H.gamma + I.goff, I.mip, ncclDouble, peer, H.comm, st));
-            DDPCA_NCCL(ncclRecv(I.recv.p, I.mip, ncclDouble, peer, H.comm, st));
+            msgs.push_back({peer, I.ts, H.gamma + I.goff, I.recv.p, I.mip});
         }
-        DDPCA_NCCL(ncclGroupEnd());
+        H.comm->exchange(msgs, st);
         for (auto& I : H.itfs)
             if (I.cross && I.mine)
                 hipLaunchKernelGGL(k_add, dim3(nb256(I.mip)), dim3(256), 0, st, H.gamma + I.goff, I.recv.p, I.mip);
@@ -1458,7 +1566,7 @@ bool iterate_once(ddpca_mcontact& H, bool check) {
         pair_norm(H, H.state + sd.roff, H.state_old.p + sd.roff, sd.m, base);
         pair_norm(H, H.state + H.R + sd.roff, H.state_old.p + H.R + sd.roff, sd.m, base + 2);
     }
-    if (H.nranks > 1) DDPCA_NCCL(ncclAllReduce(H.moni.p, H.moni.p, H.moni.n, ncclDouble, ncclSum, H.comm, st));
+    if (H.nranks > 1) H.comm->allreduce_sum(H.moni.p, H.moni.n, st);
     DDPCA_HIP(hipEventRecord(H.ev[3], st));
     DDPCA_HIP(hipMemcpyAsync(H.moni_host.data(), H.moni.p, H.moni.n * sizeof(double), hipMemcpyDeviceToHost, st));
     if (H.mg) H.mg->pcg_fetch();
@@ -1537,8 +1645,45 @@ int mcontact_gpu_comm_init(mcontact_t h, const void* uid) {
         if (h->nranks == 1) return;
         ncclUniqueId id;
         std::memcpy(&id, uid, sizeof(id));
-        DDPCA_NCCL(ncclCommInitRank(&h->comm, h->nranks, id, h->rank));
+        auto t = std::make_unique<RcclTransport>();
+        DDPCA_NCCL(ncclCommInitRank(&t->comm, h->nranks, id, h->rank));
+        h->comm = std::move(t);
         coarse_invert(*h);
+    });
+}
+
+int mcontact_gpu_comm_local(mcontact_t* handles, int n) {
+    return guarded([&] {
+        if (!handles || n < 1) throw ApiError(DDPCA_EINVAL, "handles");
+        for (int r = 0; r < n; ++r) {
+            if (!handles[r] || handles[r]->nranks != n || handles[r]->rank != r)
+                throw ApiError(DDPCA_EINVAL, "handles[r] must be rank r of n");
+            if (handles[r]->comm) throw ApiError(DDPCA_ESTATE, "handle already has a communicator");
+        }
+        auto hub = std::make_shared<LocalHub>();
+        hub->n = n;
+        hub->slot.resize(n);
+        for (int r = 0; r < n; ++r) {
+            auto t = std::make_unique<LocalTransport>();
+            t->hub = hub;
+            t->rank = r;
+            handles[r]->comm = std::move(t);
+        }
+        // the setup all-reduce of the coarse matrix is collective: one host thread per rank
+        std::vector<std::thread> th;
+        std::vector<int> rc(n, 0);
+        std::vector<std::string> msg(n);
+        for (int r = 0; r < n; ++r)
+            th.emplace_back([&, r] {
+                rc[r] = guarded([&] {
+                    select_device(handles[r]->device);
+                    coarse_invert(*handles[r]);
+                });
+                if (rc[r] < 0) msg[r] = ddpca_last_error();
+            });
+        for (auto& t : th) t.join();
+        for (int r = 0; r < n; ++r)
+            if (rc[r] < 0) throw ApiError(rc[r], "rank " + std::to_string(r) + ": " + msg[r]);
     });
 }
 
@@ -1651,7 +1796,7 @@ int mcontact_gpu_destroy(mcontact_t h) {
         if (!h) return;
         (void)hipSetDevice(h->device);
         if (h->main) (void)hipStreamSynchronize(h->main);
-        if (h->comm) (void)ncclCommDestroy(h->comm);
+        h->comm.reset();
         for (auto& e : h->ev)
             if (e) (void)hipEventDestroy(e);
         const bool own_stream = !h->mg && h->main;

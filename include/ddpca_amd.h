@@ -294,6 +294,12 @@ int mcontact_gpu_create(ddpca_problem_t p, int device, int rank, int nranks,
 int mcontact_gpu_comm_init(mcontact_t h, const void* nccl_unique_id);
 /* 128-byte ncclUniqueId for rank 0 to broadcast. */
 int mcontact_gpu_unique_id(void* out128);
+/* Test transport (no reference counterpart): connects the n handles of ONE process, handles[r] =
+ * rank r of n, through host-staged copies instead of RCCL -- the same exchanges (gamma halves of
+ * cross-rank interfaces, MONITOR and coarse-RHS all-reduces, the setup all-reduce of the coarse
+ * matrix) with the same multi-rank bookkeeping, so a multi-rank run can be checked on one GPU.
+ * Each handle's mcontact_gpu_iterate must then be called from its own host thread. */
+int mcontact_gpu_comm_local(mcontact_t* handles, int n);
 /* Run up to maxit ADMM iterations (reference maxiIter = 3000) from the current state;
  * stop on MONITOR convergence (MCONTACT.h:2725-2845) when check != 0.
  * Returns the number of iterations run (>= 0) or a negative error. */

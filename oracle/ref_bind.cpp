@@ -10,8 +10,10 @@
 //   ref_bind fric globLeve [gpu [muscSett]]
 // "rot": a BEAM MULTIGRID with nodal rotations (nodeRota) on every fifth node, one rotation
 // ("one") or a node-dependent one ("many"); the reference's CG_SOLV(1) vs mgpis_gpu_create_prol
-// + mgpis_gpu_solve on the same hierarchy.
-//   ref_bind rot globLeve one|many
+// + mgpis_gpu_solve on the same hierarchy.  "roller": "one" plus a roller support on the tip face
+// (local dof 0 of every tip node constrained): coarse nodes with partly constrained dofs, whose
+// realProl rows/columns lack those dofs (consOper, MULTIGRID.h:1248).
+//   ref_bind rot globLeve one|many|roller
 #define HARNESS_NO_MAIN
 #include "ref_harness.cpp"
 #include "ref_bind.hpp"
@@ -51,7 +53,7 @@ Eigen::Matrix3d axis_rotation(double ax, double ay, double az, double ang) {
     return Eigen::AngleAxisd(ang, Eigen::Vector3d(ax, ay, az).normalized()).toRotationMatrix();
 }
 
-int rot_mode(long gl, bool many) {
+int rot_mode(long gl, bool many, bool roller) {
     BEAM beam(0);
     beam.diviNumb = {8, 2, 2};
     beam.globLeve = gl;
@@ -67,6 +69,13 @@ int rot_mode(long gl, bool many) {
     long nrot = 0;
     for (long ti = 0; ti < (long)g.nodeCoor.size(); ti += 5, ++nrot)
         g.nodeRota.emplace(ti, axis_rotation(1.0, 2.0, 3.0, many ? 0.3 + 0.001 * ti : 0.7));
+    long nroll = 0;
+    if (roller) {
+        double xmax = -1e300;
+        for (const auto& nc : g.nodeCoor) xmax = std::max(xmax, nc.second[0]);
+        for (const auto& nc : g.nodeCoor)
+            if (nc.second[0] >= xmax - 1e-9 * std::abs(xmax) && g.consDofv.emplace(3 * nc.first, 0.0).second) ++nroll;
+    }
     harness::capture_iters([&] { g.CONSTRAINT(1); }, &log);
     long nblk = 0;  // realProl entries off w*I: the blocks the device runs as block entries
     for (long l = 0; l < g.mgpi.maxiLeve; ++l)
@@ -86,17 +95,18 @@ int rot_mode(long gl, bool many) {
     ddpca_bind::check(mgpis_gpu_solve(h, g.consForc.data(), x.data(), 1, 1e-14, g.consForc.size(), &it_gpu, &rr));
     mgpis_gpu_destroy(h);
     const double dx = (x - x_ref).norm() / x_ref.norm();
-    const bool ok = dx <= 1e-8 && nblk > 0;
+    const bool ok = dx <= 1e-8 && nblk > 0 && (!roller || nroll > 0);
     std::printf("{\"rot_ok\": %s, \"n\": %ld, \"rotated_nodes\": %ld, \"rotated_prol_entries\": %ld, "
-                "\"iters_ref\": %ld, \"iters_gpu\": %ld, \"x_rel\": %.3g}\n",
-                ok ? "true" : "false", (long)x.size(), nrot, nblk, it_ref, (long)it_gpu, dx);
+                "\"roller_dofs\": %ld, \"iters_ref\": %ld, \"iters_gpu\": %ld, \"x_rel\": %.3g}\n",
+                ok ? "true" : "false", (long)x.size(), nrot, nblk, nroll, it_ref, (long)it_gpu, dx);
     return ok ? 0 : 1;
 }
 
 }  // namespace
 
 int main(int argc, char** argv) {
-    if (argc >= 4 && std::string(argv[1]) == "rot") return rot_mode(std::stol(argv[2]), std::string(argv[3]) == "many");
+    if (argc >= 4 && std::string(argv[1]) == "rot")
+        return rot_mode(std::stol(argv[2]), std::string(argv[3]) == "many", std::string(argv[3]) == "roller");
     if (argc < 3) { std::fprintf(stderr, "usage: ref_bind fric globLeve\n"); return 2; }
     MCONTACT mc;
     harness::twoblock_build(mc, std::stod(argv[1]), std::stol(argv[2]));

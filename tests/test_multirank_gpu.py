@@ -1,0 +1,74 @@
+"""The multi-rank device path on one GPU: two mcontact_gpu handles (ranks 0 and 1 of 2) in one
+process, connected by the in-process test transport (mcontact_gpu_comm_local) instead of RCCL.
+
+Everything but the wire is the production code: rank-local ESTABLISH(owner, rank), each rank's
+batch of owned subdomains, the gamma offsets and the halves exchanged for cross-rank interfaces,
+the MONITOR all-reduce, and with a coarse space the rank-local coarse operators, the setup
+all-reduce of the dense coarse matrix (coarse_invert after comm init) and the per-iteration
+coarse right-hand side all-reduce.  The two-rank run must reproduce the single-rank run: same
+iteration count and stopping decision, resuMoni rows and displacements to the PCG accuracy (each
+rank's batch holds different members, so the V-cycle's exact-solve level and the rounding of the
+batched launches differ; 1e-8 is far below any bookkeeping error, which would be O(1)).  The CPU
+counterpart over gloo is tests/test_distributed_cpu.py."""
+import threading
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ARGS = ("dehw", 2, 2, 2, 1, 2, 0.3)  # 4 subdomains (2 worm/wheel groups), 3 levels, mu = 0.3
+
+
+def _problem(ddpca, musc, owner=None, rank=0):
+    P = ddpca.Problem(*ARGS)
+    if musc:
+        P.set_coarse(musc, [1] * P.nsub)
+    return P.ESTABLISH(owner, rank) if owner is not None else P.ESTABLISH()
+
+
+@pytest.mark.parametrize("musc", [0, 2, 1])
+@pytest.mark.parametrize("owner", [[0, 1, 0, 1], [0, 0, 1, 1]])
+def test_two_ranks_in_one_process_match_single_rank(ddpca, gpu, owner, musc):
+    """owner [0,1,0,1] puts every worm/wheel contact across the ranks (gamma halves exchanged),
+    [0,0,1,1] the glued chain links; musc 2 / 1: interface-eliminated / LATIN coarse space built
+    rank-locally."""
+    maxit = 300
+    ref = ddpca.MCONTACT(_problem(ddpca, musc))
+    n_ref = ref.CONTACT_ANALYSIS(maxit)
+    rows_ref = ref.monitor()
+    probs = [_problem(ddpca, musc, owner, r) for r in range(2)]
+    ranks = [ddpca.MCONTACT(probs[r], rank=r, nranks=2, owner=owner) for r in range(2)]
+    ddpca.MCONTACT.comm_local(ranks)
+    out, err = [None, None], [None, None]
+
+    def run(r):
+        try:
+            out[r] = ranks[r].CONTACT_ANALYSIS(maxit)
+        except Exception as e:  # noqa: BLE001 -- reported below
+            err[r] = e
+
+    th = [threading.Thread(target=run, args=(r,)) for r in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=240)
+    assert not any(t.is_alive() for t in th), "a rank hung"
+    assert err == [None, None], err
+    assert out[0] == out[1] == n_ref, (out, n_ref)
+    for r in range(2):
+        rows = ranks[r].monitor()
+        assert rows.shape == rows_ref.shape
+        scale = np.abs(rows_ref).max(axis=0, keepdims=True)
+        bad = np.abs(rows - rows_ref) > 1e-8 * np.abs(rows_ref) + 1e-12 * scale
+        assert not bad.any(), (r, np.argwhere(bad)[:5])
+        for tv in range(4):
+            if owner[tv] != r:
+                continue
+            u, ur = ranks[r].get("resuDisp", tv), ref.get("resuDisp", tv)
+            assert np.linalg.norm(u - ur) <= 1e-8 * np.linalg.norm(ur)
+        for ts in range(probs[r].nint):
+            body = [int(b) for b in probs[r].array("iface_body", ts)]
+            if r in (owner[body[0]], owner[body[1]]):
+                g, gr = ranks[r].get("inpoGamm", ts), ref.get("inpoGamm", ts)
+                assert np.abs(g - gr).max() <= 1e-7 * np.abs(gr).max()
