@@ -2,7 +2,10 @@
 
 Workload (BASELINE.json configs[4]): 8 subdomains of 1.23M DOF each
 (9.8M DOF), 4 worm/wheel groups -- each a frictional contact (mu = 0.2) between a worm block and
-a wheel block -- glued into two chains along x, 6 multigrid levels per subdomain.  One ADMM
+a wheel block -- glued into two chains along x, 6 multigrid levels per subdomain, and M3's
+interface density: 7.9M integration points (0.80 per DOF, DEHW's 3.37M ip / 4.18M DOF) -- contact
+faces integrated over 4 x 4 polygons each, glued faces over 2 x 2 (what CSEARCH's intersection
+yields against a slave surface mesh 4x / 2x finer, as DEHW's adaptively refined contact bands).  One ADMM
 iteration = every subdomain's MGPIS PCG solve (1e-14 recursive residual, x0 = 0, as
 MGPIS::CG_SOLV) + the interface-eliminated coarse-space correction (muscSett = 2, doleMcsc = 1:
 DEHW's own setting, DEHW.h:2222, 2239) + the interface step + MONITOR.  The global problem is fixed and its subdomains
@@ -47,6 +50,9 @@ def parse():
     ap.add_argument("--nz", type=int, default=2)
     ap.add_argument("--gl", type=int, default=5, help="uniform refinements (levels = gl + 1)")
     ap.add_argument("--fric", type=float, default=0.2)
+    ap.add_argument("--ip-contact", type=int, default=2,
+                    help="contact faces integrated over 2^k x 2^k polygons (k = 2: M3's 0.8 ip per DOF with --ip-glued 1)")
+    ap.add_argument("--ip-glued", type=int, default=1, help="the same for the glued faces")
     # defaults: the fastest configuration of the round-1 sweep (profiles/r01_sweep.txt)
     ap.add_argument("--smoother", type=int, default=H["smoother"], help="0 point Jacobi, 1 block Jacobi, 2 Chebyshev")
     ap.add_argument("--nu", type=int, default=H["nu"])
@@ -96,7 +102,8 @@ def main():
     part = import_module("ddpca-admm_amd.partition")
 
     t_setup = time.perf_counter()
-    P = D.Problem("dehw", a.groups, a.nx, a.ny, a.nz, a.gl, a.fric)
+    P = D.Problem("dehw", a.groups, a.nx, a.ny, a.nz, a.gl, a.fric, a.ip_contact, a.ip_glued)
+    nip = sum(len(P.array("ip_w", ts)) for ts in range(P.nint))
     nsub = P.nsub
     owner = part.block_owner(nsub, world)
     if a.musc:
@@ -171,10 +178,13 @@ def main():
             "config": {
                 "workload": f"dehw-synthetic: {nsub} subdomains x {total_dofs // nsub} DOF = {total_dofs} DOF, "
                             f"{a.groups} frictional contacts (mu={a.fric}) + {2 * (a.groups - 1)} glued interfaces, "
+                            f"{nip} integration points ({nip / total_dofs:.2f} per DOF), "
                             f"{a.gl + 1} MG levels, MGPIS-PCG rtol 1e-14",
                 "subdomains": nsub,
                 "dof": total_dofs,
                 "interfaces": P.nint,
+                "integration_points": nip,
+                "ip_per_dof": nip / total_dofs,
                 "mg_levels": a.gl + 1,
                 "smoother": {0: "jacobi", 1: "block-jacobi", 2: "chebyshev"}[a.smoother] + f"({a.nu})",
                 "pcg_x0": "previous solution" if a.warm_start else "zero",
@@ -187,6 +197,10 @@ def main():
             "pcg_iters_per_solve": pcg_its / max(n * nsub, 1),
             "setup_s": t_setup,
             "mass_cg_iters_per_admm_iter": int(mc.get("mass_iters")[0]) / max(n, 1),
+            # device time per ADMM iteration of the interface step (gamma, projection, aux / lambda
+            # mass solves, MONITOR norms) and of the body balance (host wall, PCG + coarse space)
+            "iface_ms_per_iter": tm["iface_ms"] / max(n, 1),
+            "solve_ms_per_iter": tm["solve_ms"] / max(n, 1),
             "roofline": {
                 "bound": "hbm",
                 "kernel": "k_sell<kPcg> fine level (SELL-BSR3 SpMV q=Kz+beta q, p=z+beta p, p.q)",

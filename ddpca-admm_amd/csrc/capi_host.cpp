@@ -41,7 +41,7 @@ std::vector<std::array<int64_t, 4>> plane_faces(const MULTIGRID& g, int axis, in
 // Conforming interface on a shared lattice plane: master faces of body m, slave faces of body
 // s; integration points in CONTACT_SEARCH order (slave segments, CSEARCH.h:777-817).
 void conforming_interface(const MULTIGRID& gm, const MULTIGRID& gs, int axis, int64_t value,
-                          std::vector<IntegralPoint>& ips) {
+                          std::vector<IntegralPoint>& ips, int sub = 1) {
     auto key = [](const MULTIGRID& g, const std::array<int64_t, 4>& f) {
         std::array<std::array<int64_t, 3>, 4> k;
         for (int i = 0; i < 4; ++i) k[i] = g.nodeLatt[f[i]];
@@ -53,7 +53,7 @@ void conforming_interface(const MULTIGRID& gm, const MULTIGRID& gs, int axis, in
     for (const auto& f : plane_faces(gs, axis, value)) {
         auto it = mast.find(key(gs, f));
         if (it == mast.end()) continue;
-        conforming_face_ips(gm, it->second.data(), gs, f.data(), ips);
+        conforming_face_ips(gm, it->second.data(), gs, f.data(), ips, sub);
     }
 }
 
@@ -169,12 +169,17 @@ void make_twoblock(Problem& P, const double* q) {
 // (interfaces G + g), wheel blocks glued along x (interfaces 2G - 1 + g).  Worm bottom on
 // rollers (uz = 0), both chains clamped at x = 0, wheel tops loaded by pressure p and shear
 // 0.5 fric p (partial slip).  E = 210e9 (worm) / 110e9 (wheel) as in DEHW.h:2248.
-void make_dehw(Problem& P, const double* q) {
+// q[6], q[7] (optional, default 0): integration density of the contact / glued faces -- each face
+// integrated over 2^k x 2^k polygons, as against a slave surface mesh 2^k times finer (DEHW's
+// adaptively refined contact bands, DEHW.h:1562, 2079, carry ~0.8 integration points per DOF).
+void make_dehw(Problem& P, const double* q, int nq) {
     const int64_t G = (int64_t)q[0];
     const int64_t n[3] = {(int64_t)q[1], (int64_t)q[2], (int64_t)q[3]};
     const int64_t gl = (int64_t)q[4];
     const double fric = q[5];
+    const int kc = nq > 6 ? (int)q[6] : 0, kg = nq > 7 ? (int)q[7] : 0;
     if (G < 1) throw std::invalid_argument("dehw: ngroups >= 1");
+    if (kc < 0 || kc > 4 || kg < 0 || kg > 4) throw std::invalid_argument("dehw: integration refinement in [0, 4]");
     const double h = 0.01;  // cubic coarse elements
     const double Lx = n[0] * h, Ly = n[1] * h, H = n[2] * h, p = 1.0e7;
     P.mc.multGrid.resize(2 * G);
@@ -218,7 +223,9 @@ void make_dehw(Problem& P, const double* q) {
 #pragma omp parallel for schedule(dynamic, 1)
     for (int64_t ts = 0; ts < nint; ++ts) {
         Interface& itf = P.mc.searCont[ts];
-        conforming_interface(P.mc.multGrid[itf.body[0]], P.mc.multGrid[itf.body[1]], (int)plane[ts][0], plane[ts][1], itf.ip);
+        const int k = ts < G ? kc : kg;
+        conforming_interface(P.mc.multGrid[itf.body[0]], P.mc.multGrid[itf.body[1]], (int)plane[ts][0], plane[ts][1], itf.ip,
+                             1 << k);
     }
     set_penalty(P);
 }
@@ -254,7 +261,7 @@ int ddpca_problem_create(const char* kind, const double* params, int nparams, dd
             make_twoblock(*P, params);
         } else if (k == "dehw") {
             if (nparams < 6) throw ApiError(DDPCA_EINVAL, "dehw needs 6 params");
-            make_dehw(*P, params);
+            make_dehw(*P, params, nparams);
         } else {
             throw ApiError(DDPCA_EINVAL, "unknown problem kind " + k);
         }

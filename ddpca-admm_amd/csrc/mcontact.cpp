@@ -299,7 +299,7 @@ double MCONTACT::GET_CHAR_LENG() const {
 
 // ------------------------------------------------------------------------------------------
 void conforming_face_ips(const MULTIGRID& gm, const int64_t mast[4], const MULTIGRID& gs,
-                         const int64_t slav[4], std::vector<IntegralPoint>& out) {
+                         const int64_t slav[4], std::vector<IntegralPoint>& out, int sub) {
     static const double nacoCorn[4][2] = {{-1, -1}, {1, -1}, {1, 1}, {-1, 1}};
     double X[4][3], Y[4][3];
     for (int k = 0; k < 4; ++k)
@@ -320,56 +320,67 @@ void conforming_face_ips(const MULTIGRID& gm, const int64_t mast[4], const MULTI
         sxi[k][0] = nacoCorn[hit][0];
         sxi[k][1] = nacoCorn[hit][1];
     }
-    // polygon = master square, vertices sorted by angle about the centroid: (-1,-1),(1,-1),(1,1),(-1,1)
-    const double poly[4][2] = {{-1, -1}, {1, -1}, {1, 1}, {-1, 1}};
+    // polygons = the sub x sub cells of the master square (sub = 1: the square itself, the
+    // intersection with a coincident slave face; sub = 2^k: what SEGMENT_INTERSECT clips against a
+    // slave face mesh 2^k times finer), vertices sorted by angle about the cell centroid, each
+    // triangulated from that centroid (CSEARCH.h:614-775)
+    // one integration point at master natural coordinates (xi, et) with weight factor wgt
+    auto emit = [&](double xi, double et, double wgt) {
+        IntegralPoint p;
+        double dx[3] = {0, 0, 0}, de[3] = {0, 0, 0};
+        for (int k = 0; k < 4; ++k) {
+            p.node[0][k] = mast[k];
+            p.node[1][k] = slav[k];
+            p.shap[0][k] = (1.0 + nacoCorn[k][0] * xi) * (1.0 + nacoCorn[k][1] * et) / 4.0;
+            for (int a = 0; a < 3; ++a) {
+                dx[a] += X[k][a] * (nacoCorn[k][0] / 4.0 + nacoCorn[k][0] * nacoCorn[k][1] * et / 4.0);
+                de[a] += X[k][a] * (nacoCorn[k][1] / 4.0 + nacoCorn[k][0] * nacoCorn[k][1] * xi / 4.0);
+            }
+        }
+        // slave shape functions: the projected point coincides with the master point,
+        // so slave corner k (sitting on master corner m) carries master weight m
+        for (int k = 0; k < 4; ++k) {
+            int m = 0;
+            for (; m < 4; ++m)
+                if (nacoCorn[m][0] == sxi[k][0] && nacoCorn[m][1] == sxi[k][1]) break;
+            p.shap[1][k] = p.shap[0][m];
+        }
+        double n[3] = {dx[1] * de[2] - dx[2] * de[1], dx[2] * de[0] - dx[0] * de[2], dx[0] * de[1] - dx[1] * de[0]};
+        const double jac = std::sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
+        const double lx = std::sqrt(dx[0] * dx[0] + dx[1] * dx[1] + dx[2] * dx[2]);
+        const double le = std::sqrt(de[0] * de[0] + de[1] * de[1] + de[2] * de[2]);
+        for (int a = 0; a < 3; ++a) {
+            p.basis[0][a] = n[a] / jac;
+            p.basis[1][a] = dx[a] / lx;
+            p.basis[2][a] = de[a] / le;
+        }
+        p.gap = 0.0;
+        p.w = wgt * jac;
+        out.push_back(p);
+    };
     const double g = std::sqrt(1.0 / 3.0);
     const double gl[2] = {-g, g};
-    for (int t = 0; t < 4; ++t) {
-        const double* v1 = poly[t];
-        const double* v2 = poly[(t + 1) % 4];
-        const double area = std::abs((v1[0] - 0.0) * (v2[1] - 0.0) - (v1[1] - 0.0) * (v2[0] - 0.0)) / 2.0;
-        for (int i = 0; i < 2; ++i)
-            for (int j = 0; j < 2; ++j) {
-                // PREP.h:336-361 triangle rule, CSEARCH.h:468-483
-                const double b0 = (1.0 + gl[i]) / 2.0;
-                const double b1 = (1.0 - gl[i]) * (1.0 + gl[j]) / 4.0;
-                const double b2 = 1.0 - b0 - b1;
-                const double wq = (1.0 - gl[i]) / 8.0;
-                const double xi = b0 * 0.0 + b1 * v1[0] + b2 * v2[0];
-                const double et = b0 * 0.0 + b1 * v1[1] + b2 * v2[1];
-                IntegralPoint p;
-                double dx[3] = {0, 0, 0}, de[3] = {0, 0, 0};
-                for (int k = 0; k < 4; ++k) {
-                    p.node[0][k] = mast[k];
-                    p.node[1][k] = slav[k];
-                    p.shap[0][k] = (1.0 + nacoCorn[k][0] * xi) * (1.0 + nacoCorn[k][1] * et) / 4.0;
-                    for (int a = 0; a < 3; ++a) {
-                        dx[a] += X[k][a] * (nacoCorn[k][0] / 4.0 + nacoCorn[k][0] * nacoCorn[k][1] * et / 4.0);
-                        de[a] += X[k][a] * (nacoCorn[k][1] / 4.0 + nacoCorn[k][0] * nacoCorn[k][1] * xi / 4.0);
+    const double hc = 2.0 / sub;
+    for (int cy = 0; cy < sub; ++cy)
+        for (int cx = 0; cx < sub; ++cx) {
+            const double x0 = -1.0 + cx * hc, y0 = -1.0 + cy * hc;
+            const double poly[4][2] = {{x0, y0}, {x0 + hc, y0}, {x0 + hc, y0 + hc}, {x0, y0 + hc}};
+            const double c0 = x0 + 0.5 * hc, c1 = y0 + 0.5 * hc;  // sub = 1: the origin
+            for (int t = 0; t < 4; ++t) {
+                const double* v1 = poly[t];
+                const double* v2 = poly[(t + 1) % 4];
+                const double area = std::abs((v1[0] - c0) * (v2[1] - c1) - (v1[1] - c1) * (v2[0] - c0)) / 2.0;
+                for (int i = 0; i < 2; ++i)
+                    for (int j = 0; j < 2; ++j) {
+                        // PREP.h:336-361 triangle rule, CSEARCH.h:468-483
+                        const double b0 = (1.0 + gl[i]) / 2.0;
+                        const double b1 = (1.0 - gl[i]) * (1.0 + gl[j]) / 4.0;
+                        const double b2 = 1.0 - b0 - b1;
+                        const double wq = (1.0 - gl[i]) / 8.0;
+                        emit(b0 * c0 + b1 * v1[0] + b2 * v2[0], b0 * c1 + b1 * v1[1] + b2 * v2[1], 2.0 * area * wq);
                     }
-                }
-                // slave shape functions: the projected point coincides with the master point,
-                // so slave corner k (sitting on master corner m) carries master weight m
-                for (int k = 0; k < 4; ++k) {
-                    int m = 0;
-                    for (; m < 4; ++m)
-                        if (nacoCorn[m][0] == sxi[k][0] && nacoCorn[m][1] == sxi[k][1]) break;
-                    p.shap[1][k] = p.shap[0][m];
-                }
-                double n[3] = {dx[1] * de[2] - dx[2] * de[1], dx[2] * de[0] - dx[0] * de[2], dx[0] * de[1] - dx[1] * de[0]};
-                const double jac = std::sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
-                const double lx = std::sqrt(dx[0] * dx[0] + dx[1] * dx[1] + dx[2] * dx[2]);
-                const double le = std::sqrt(de[0] * de[0] + de[1] * de[1] + de[2] * de[2]);
-                for (int a = 0; a < 3; ++a) {
-                    p.basis[0][a] = n[a] / jac;
-                    p.basis[1][a] = dx[a] / lx;
-                    p.basis[2][a] = de[a] / le;
-                }
-                p.gap = 0.0;
-                p.w = 2.0 * area * wq * jac;
-                out.push_back(p);
             }
-    }
+        }
 }
 
 }  // namespace ddpca

@@ -90,8 +90,9 @@ public:
 // Conforming-face integration points (restatement of CSEARCH::SEGMENT_INTERSECT for two
 // coincident quadrilateral faces: polygon = master face, 4 centroid triangles x 4-point
 // triangle rule, CSEARCH.h:614-775).  mast/slav: 4 node ids of matching faces, oriented as
-// EFACE_SURFACE returns them.
+// EFACE_SURFACE returns them.  sub > 1: the master face in sub x sub polygons (the intersection
+// with a slave face mesh sub times finer), 16 points each.
 void conforming_face_ips(const MULTIGRID& gm, const int64_t mast[4], const MULTIGRID& gs,
-                         const int64_t slav[4], std::vector<IntegralPoint>& out);
+                         const int64_t slav[4], std::vector<IntegralPoint>& out, int sub = 1);
 
 }  // namespace ddpca

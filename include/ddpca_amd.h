@@ -163,9 +163,13 @@ typedef struct ddpca_problem* ddpca_problem_t;
  *   "beam"     d0 d1 d2 globLeve D0 D1 D2       BEAM.h (D = 1,1,1: MESH_NODD; else MESH_DD,
  *                                              glued interfaces fricCoef = -1, BEAM.h:424-470)
  *   "twoblock" fric globLeve                    two stacked blocks, one contact interface
- *   "dehw"     ngroups nx ny nz globLeve fric   synthetic DEHW-shaped chain: per group one
+ *   "dehw"     ngroups nx ny nz globLeve fric [kc kg]
+ *                                              synthetic DEHW-shaped chain: per group one
  *                                              worm and one wheel block in frictional contact,
- *                                              groups glued along x (worm-worm, wheel-wheel) */
+ *                                              groups glued along x (worm-worm, wheel-wheel);
+ *                                              kc / kg (default 0): contact / glued faces
+ *                                              integrated over 2^k x 2^k polygons each (the
+ *                                              intersection with a 2^k times finer slave mesh) */
 int ddpca_problem_create(const char* kind, const double* params, int nparams, ddpca_problem_t* out);
 /* Replace the integration points of interface ts (CSEARCH::intePoin, CSEARCH.h:19-32):
  * node[n][2][4], shap[n][2][4], basis[n][3][3], gap[n], w[n]. */
