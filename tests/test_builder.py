@@ -87,3 +87,22 @@ def test_hanging_level_shapes(ddpca, pair):
     s2[0]["hang"] = (nL + 2, H)
     with pytest.raises(ddpca.DdpcaError, match="hanging prolongation"):
         ddpca.Problem.from_operators(s2, ifaces)
+
+
+@pytest.mark.parametrize("kc,kg", [(1, 0), (2, 1)])
+def test_refined_face_integration(ddpca, kc, kg):
+    """Contact / glued faces integrated over 2^k x 2^k polygons each (bench.py's M3 density):
+    4^k times the points of the conforming rule, weights summing to the face area, and the
+    mortar mass of a contact side equal to the conforming one to the quadrature's accuracy (the
+    triangle rule is not exact for the xi^2 eta^2 term of bilinear x bilinear: 0.5 %)."""
+    P0 = ddpca.Problem("dehw", 2, 2, 1, 1, 1, 0.2)
+    P1 = ddpca.Problem("dehw", 2, 2, 1, 1, 1, 0.2, kc, kg)
+    for ts in range(P0.nint):
+        k = kc if ts < 2 else kg
+        w0, w1 = P0.array("ip_w", ts), P1.array("ip_w", ts)
+        assert len(w1) == 4 ** k * len(w0)
+        assert abs(w1.sum() - w0.sum()) <= 1e-14 * w0.sum()
+    P0.ESTABLISH()
+    P1.ESTABLISH()
+    M0, M1 = P0.csr("inteMass", 0), P1.csr("inteMass", 0)
+    assert abs(M1 - M0).max() <= 1e-2 * abs(M0).max()
