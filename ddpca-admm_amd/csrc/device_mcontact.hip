@@ -435,6 +435,17 @@ __global__ void k_cs_presc(const int32_t* cdof, const double* presc, double* u, 
     if (i < n) u[cdof[i]] += presc[cdof[i]];
 }
 
+// coarse right-hand side into the coarse MGPIS's fine layout / its solution back to the own rows
+__global__ void k_perm_scatter(const int32_t* perm, const double* g, double* b, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) b[perm[i]] = g[i];
+}
+
+__global__ void k_perm_gather(const int32_t* perm, const int32_t* rows, const double* x, double* xc, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) xc[i] = x[perm[rows[i]]];
+}
+
 // potri(lower) on the column-major view leaves the inverse in the row-major upper triangle;
 // mirror it into the lower one
 __global__ void k_fill_lower(double* A, int64_t n) {
@@ -659,6 +670,18 @@ struct CoarseDev {
     DevBuf<double> pval;
     std::vector<int64_t> own_rows;  // global coarse rows of this rank, in xc order
     std::vector<double> dense;      // host, until inverted: this rank's rows of globCoup_1 (n x n, zeros elsewhere)
+    // DOUBLE_M_1 (MCONTACT.h:2303-2341; the reference's choice once globCoup_1 has DIRE_MAXI rows,
+    // 1857-1865): the coarse problem solved by its own MGPIS-PCG, redundantly on every rank, on a
+    // hierarchy whose transfers are every subdomain's realProl below doleMcsc, block-diagonal
+    bool mg = false;
+    std::unique_ptr<MgpisDevice> cmg;
+    DevBuf<int32_t> cperm;  // coarse row -> dof of cmg's fine level (device layout)
+    DevBuf<int32_t> cown;   // xc index -> coarse row
+    hipEvent_t ev_in = nullptr, ev_out = nullptr;
+    ~CoarseDev() {
+        if (ev_in) (void)hipEventDestroy(ev_in);
+        if (ev_out) (void)hipEventDestroy(ev_out);
+    }
 };
 
 // ============================================================================= transport
@@ -1153,6 +1176,92 @@ void build(ddpca_mcontact& H, Problem& P) {
     DDPCA_HIP(hipStreamSynchronize(H.main));
 }
 
+// ---- DOUBLE_M_1 (MCONTACT.h:2303-2341): level l of the coarse hierarchy (l = Lc = max doleMcsc is
+// globCoup_1 itself) holds level max(0, doleMcsc[tv] - (Lc - l)) of every subdomain; the transfer
+// below it is each subdomain's realProl at that level (identity where a subdomain has reached its
+// level 0), and the level operators are Galerkin products.  Nodes are numbered so that every level
+// is a prefix of the next (the layout MgpisDevice takes): level l = level l-1's nodes, then the new
+// nodes of every subdomain in order.  Needs every subdomain's coarse rows on this rank.
+void build_coarse_mg(ddpca_mcontact& H, const MCONTACT& mc, CoarseDev& C) {
+    const CoarseSpace& cs = mc.coarse;
+    const int64_t nsub = (int64_t)mc.multGrid.size(), n = C.n;
+    for (int64_t tv = 0; tv < nsub; ++tv)
+        if (!cs.built[tv])
+            throw ApiError(DDPCA_ESTATE, "DOUBLE_M coarse solve: every subdomain's rows of globCoup_1 are needed on each rank "
+                                         "(a single-rank run or the caller's full MULTISCALE_1 output)");
+    const int64_t Lc = *std::max_element(mc.doleMcsc.begin(), mc.doleMcsc.end());
+    auto lev = [&](int64_t tv, int64_t l) { return std::max<int64_t>(0, mc.doleMcsc[tv] - (Lc - l)); };
+    std::vector<std::vector<std::vector<int64_t>>> gid(Lc + 1, std::vector<std::vector<int64_t>>(nsub));
+    std::vector<int64_t> nglob(Lc + 1, 0);
+    for (int64_t l = 0; l <= Lc; ++l) {
+        int64_t cnt = l ? nglob[l - 1] : 0;
+        for (int64_t tv = 0; tv < nsub; ++tv) {
+            auto& v = gid[l][tv];
+            v.resize(mc.multGrid[tv].leveCount[lev(tv, l)]);
+            int64_t keep = 0;
+            if (l) {
+                keep = (int64_t)gid[l - 1][tv].size();
+                std::copy(gid[l - 1][tv].begin(), gid[l - 1][tv].end(), v.begin());
+            }
+            for (int64_t j = keep; j < (int64_t)v.size(); ++j) v[j] = cnt++;
+        }
+        nglob[l] = cnt;
+    }
+    std::vector<Stencil> S(Lc);
+    for (int64_t l = 1; l <= Lc; ++l) {
+        std::vector<std::vector<std::pair<int32_t, double>>> rows(nglob[l]);
+        for (int64_t i = 0; i < nglob[l - 1]; ++i) rows[i].push_back({(int32_t)i, 1.0});
+        for (int64_t tv = 0; tv < nsub; ++tv) {
+            if (lev(tv, l) == lev(tv, l - 1)) continue;  // identity (MCONTACT.h:2325-2331)
+            const Stencil& Sp = mc.multGrid[tv].scalProl[lev(tv, l - 1)];
+            if (!Sp.bent.empty()) throw ApiError(DDPCA_EINVAL, "DOUBLE_M coarse solve with rotated-node transfers");
+            for (int64_t j = (int64_t)gid[l - 1][tv].size(); j < (int64_t)gid[l][tv].size(); ++j)
+                for (int64_t k = Sp.ptr[j]; k < Sp.ptr[j + 1]; ++k)
+                    rows[gid[l][tv][j]].push_back({(int32_t)gid[l - 1][tv][Sp.col[k]], Sp.w[k]});
+        }
+        Stencil& T = S[l - 1];
+        T.nf = nglob[l];
+        T.nc = nglob[l - 1];
+        T.ptr.assign(1, 0);
+        for (const auto& r : rows) {
+            for (const auto& e : r) {
+                T.col.push_back(e.first);
+                T.w.push_back(e.second);
+            }
+            T.ptr.push_back((int64_t)T.col.size());
+        }
+    }
+    // globCoup_1 rows: subdomain tv's level-doleMcsc free dofs in increasing order (consOper)
+    std::vector<int32_t> fdg(n);
+    for (int64_t tv = 0; tv < nsub; ++tv) {
+        const MULTIGRID& g = mc.multGrid[tv];
+        int64_t r = cs.baseReco[tv];
+        for (int64_t dof = 0; dof < 3 * g.leveCount[mc.doleMcsc[tv]]; ++dof)
+            if (g.consFlag[dof]) fdg[r++] = (int32_t)(3 * gid[Lc][tv][dof / 3] + dof % 3);
+        if (r != cs.baseReco[tv + 1]) throw ApiError(DDPCA_EINVAL, "DOUBLE_M: baseReco does not match the free dofs");
+    }
+    std::vector<Bsr3> K(Lc + 1);
+    K[Lc] = condensed_to_bsr3(nglob[Lc], n, fdg.data(), cs.globCoup_1.ptr.data(), cs.globCoup_1.col.data(),
+                              cs.globCoup_1.val.data());
+    for (int64_t l = Lc - 1; l >= 0; --l) K[l] = galerkin_rap(K[l + 1], S[l]);  // MCONTACT.h:2337-2338
+    std::vector<uint8_t> flag(3 * nglob[Lc], 0);
+    for (int32_t d : fdg) flag[d] = 1;
+    SubdomainOps o;
+    o.nnodes = nglob;
+    for (const auto& k : K) o.K.push_back(&k);
+    for (const auto& s : S) o.S.push_back(&s);
+    o.dof_free = flag.data();
+    C.cmg = std::make_unique<MgpisDevice>(H.device, std::vector<SubdomainOps>{o}, H.opt);
+    std::vector<int32_t> perm(n), own(C.own_rows.begin(), C.own_rows.end());
+    for (int64_t r = 0; r < n; ++r) perm[r] = (int32_t)C.cmg->fine_dof(0, fdg[r]);
+    C.cperm.upload(perm);
+    C.cown.upload(own.empty() ? std::vector<int32_t>{0} : own);
+    DDPCA_HIP(hipEventCreateWithFlags(&C.ev_in, hipEventDisableTiming));
+    DDPCA_HIP(hipEventCreateWithFlags(&C.ev_out, hipEventDisableTiming));
+    if (std::getenv("DDPCA_VERBOSE"))
+        std::fprintf(stderr, "[ddpca] DOUBLE_M coarse solve: %ld rows, %ld levels\n", (long)n, (long)(Lc + 1));
+}
+
 // ---- coarse space: device operands from the host MULTISCALE_1 output
 void build_coarse(ddpca_mcontact& H, Problem& P) {
     MCONTACT& mc = P.mc;
@@ -1222,17 +1331,25 @@ void build_coarse(ddpca_mcontact& H, Problem& P) {
     C.f0.upload(f0);
     C.g.alloc(std::max<int64_t>(n, 1));
     C.xc.alloc(std::max<int64_t>(C.nown, 1));
-    // dense rows of globCoup_1 (inverted once every rank holds all rows)
-    C.dense.assign((size_t)n * n, 0.0);
-    std::vector<int64_t> fill_rows = C.own_rows;
-    // the coarse contact unknowns' rows: a caller's full operator is filled by rank 0 only; a
-    // rank-local host build holds each rank's share (the all-reduce sums them)
-    if (cs.latin && (cs.rank_local || H.rank == 0))
-        for (int64_t r = cs.baseReco.back(); r < n; ++r) fill_rows.push_back(r);
-    for (int64_t r : fill_rows)
-        for (int64_t k = cs.globCoup_1.ptr[r]; k < cs.globCoup_1.ptr[r + 1]; ++k)
-            C.dense[(size_t)r * n + cs.globCoup_1.col[k]] = cs.globCoup_1.val[k];
+    // the reference solves globCoup_1 directly below DIRE_MAXI = 120000 rows and with its DOUBLE_M_1
+    // MGPIS above (PREP.h:69, MCONTACT.h:1857-1865); DDPCA_COARSE_MG_MIN moves the switch (tests)
+    const char* mg_env = std::getenv("DDPCA_COARSE_MG_MIN");
+    C.mg = !cs.latin && n >= (mg_env ? std::atoll(mg_env) : 120000);
     C.latin = cs.latin;
+    if (C.mg) {
+        if (H.mg && C.nown) build_coarse_mg(H, mc, C);
+    } else {
+        // dense rows of globCoup_1 (inverted once every rank holds all rows)
+        C.dense.assign((size_t)n * n, 0.0);
+        std::vector<int64_t> fill_rows = C.own_rows;
+        // the coarse contact unknowns' rows: a caller's full operator is filled by rank 0 only; a
+        // rank-local host build holds each rank's share (the all-reduce sums them)
+        if (cs.latin && (cs.rank_local || H.rank == 0))
+            for (int64_t r = cs.baseReco.back(); r < n; ++r) fill_rows.push_back(r);
+        for (int64_t r : fill_rows)
+            for (int64_t k = cs.globCoup_1.ptr[r]; k < cs.globCoup_1.ptr[r + 1]; ++k)
+                C.dense[(size_t)r * n + cs.globCoup_1.col[k]] = cs.globCoup_1.val[k];
+    }
     if (!H.mg) return;
     if (cs.assembled) {
         C.assembled = true;
@@ -1335,6 +1452,10 @@ void build_coarse(ddpca_mcontact& H, Problem& P) {
 void coarse_invert(ddpca_mcontact& H) {
     CoarseDev& C = H.cs;
     if (!C.on || C.inverted) return;
+    if (C.mg) {  // DOUBLE_M: nothing to factorise (the same decision on every rank: n is global)
+        C.inverted = true;
+        return;
+    }
     const int64_t n = C.n;
     if (n > 46000) throw ApiError(DDPCA_EINVAL, "coarse space too large for the dense inverse (n > 46000)");
     DevBuf<double> A;
@@ -1409,7 +1530,20 @@ void coarse_correct(ddpca_mcontact& H) {
     }
     if (H.nranks > 1) H.comm->allreduce_sum(C.g.p, n, st);
     if (!C.nown) return;
-    hipLaunchKernelGGL(k_gemv_wave, dim3(ceil_div(C.nown, 4)), dim3(256), 0, st, C.ainv.p, C.g.p, C.xc.p, C.nown, n);
+    if (C.mg) {  // mgpi_1.CG_SOLV(1, globForc, globSolu) (MCONTACT.h:2594), on the coarse solver's stream
+        MgpisDevice& M = *C.cmg;
+        DDPCA_HIP(hipEventRecord(C.ev_in, st));
+        DDPCA_HIP(hipStreamWaitEvent(M.stream, C.ev_in, 0));
+        DDPCA_HIP(hipMemsetAsync(M.bs.p, 0, M.bs.n * sizeof(double), M.stream));
+        hipLaunchKernelGGL(k_perm_scatter, dim3(nb256(n)), dim3(256), 0, M.stream, C.cperm.p, C.g.p, M.bs.p, n);
+        M.pcg_solve(1, 1.0e-14, std::vector<int64_t>{n});
+        hipLaunchKernelGGL(k_perm_gather, dim3(nb256(C.nown)), dim3(256), 0, M.stream, C.cperm.p, C.cown.p, M.xs.p, C.xc.p,
+                           C.nown);
+        DDPCA_HIP(hipEventRecord(C.ev_out, M.stream));
+        DDPCA_HIP(hipStreamWaitEvent(st, C.ev_out, 0));
+    } else {
+        hipLaunchKernelGGL(k_gemv_wave, dim3(ceil_div(C.nown, 4)), dim3(256), 0, st, C.ainv.p, C.g.p, C.xc.p, C.nown, n);
+    }
     if (C.assembled) {
         if (C.npr)
             hipLaunchKernelGGL(k_cs_prolong_csr, dim3(nb256(C.npr)), dim3(256), 0, st, C.pptr.p, C.pcol.p, C.pval.p, C.ptgt.p,
