@@ -17,8 +17,8 @@ are spread over the ranks (strong scaling); N = 1 runs all 8 on one MI355X.
 Rank 0 prints one JSON line.  `roofline` is the fine-level SELL-BSR3 SpMV kernel (the dominant
 kernel family, one launch covers every owned subdomain), timed by HIP events around its launch in
 the eager first PCG iteration of every batched solve, on the solve stream;
-`cpu_baseline` is the CPU oracle (oracle/, SGS-faithful restatement of MGPIS) on one subdomain
-solve of the same workload, scaled to one ADMM iteration.
+`cpu_baseline` is the CPU port (oracle/cpu_admm.py: SGS-faithful MGPIS + the interface step) pricing
+one full ADMM iteration of the same workload at the device run's final state.
 """
 from __future__ import annotations
 
@@ -215,7 +215,7 @@ def main():
             },
         }
         if world == 1 and not a.no_cpu_baseline:
-            result["cpu_baseline"] = cpu_baseline(P, nsub, owner)
+            result["cpu_baseline"] = cpu_baseline(P, mc)
     # release device state before the process group
     del mc
     if world > 1:
@@ -231,40 +231,21 @@ def traffic_key(a) -> dict:
                 precond_fp32=a.precond_fp32, table_mode=a.table_mode, value_layout=VALUE_LAYOUT)
 
 
-def cpu_baseline(P, nsub, owner, budget_s=10.0):
-    """SGS-faithful CPU restatement (oracle/, MGPIS.h) of the subdomain solves of this workload:
-    CG_SOLV(1) on the wheel subdomains (their RHS at ADMM iteration 0 is consForc; the worms'
-    is zero there) until about `budget_s` seconds of solve time; one ADMM iteration is priced as
-    nsub times the mean solve time (the interface step, < 5 % on the GPU, is left out)."""
-    from oracle import oracle as O
-    times, its, ndof = [], [], 0
-    for tv in range(1, nsub, 2):
-        G = P.grid(tv)
-        L = G.maxiLeve
-        K = [G.consStif(l) for l in range(L + 1)]
-        Pr = [G.realProl(l) for l in range(L)]
-        M = O.MgpisOracle(K, Pr)
-        del K, Pr
-        b = G.consForc
-        ndof = len(b)
-        t0 = time.perf_counter()
-        x, it, rr = M.CG_SOLV(1, b)
-        times.append(time.perf_counter() - t0)
-        its.append(it)
-        del M
-        if sum(times) >= budget_s:
-            break
-    t = sum(times) / len(times)
-    return {
-        "value": 1.0 / (nsub * t),
-        "unit": "ADMM it/s",
-        "cores": O.threads(),
-        "kind": "port",
-        "sample": f"{len(times)} SGS-V-cycle CG_SOLV(1) solves of wheel subdomains ({ndof} DOF each, "
-                  f"{its} iterations, {sum(times):.1f} s) at ADMM iteration 0; one ADMM iteration = "
-                  f"{nsub} solves at the mean time {t:.2f} s (interface step left out)",
-        "dof_iter_per_s": ndof * sum(its) / sum(times),
-    }
+def cpu_baseline(P, mc, budget_s=20.0):
+    """SGS-faithful CPU port (oracle/cpu_admm.py, MGPIS.h + MCONTACT.h) pricing one full ADMM
+    iteration at the state the device run reached: sampled subdomain CG_SOLV(1) solves, the whole
+    coarse-space correction and interface step.  `reference_equivalent` rescales it by the
+    container measurement of the reference's own CG_SOLV against the port on the same mesh and
+    cores (profiles/cpu_calibration.py), since the reference never travels to the GPU box."""
+    from oracle import cpu_admm
+    res = cpu_admm.price_iteration(P, mc, budget_s)
+    cal = ROOT / "profiles" / "r02_cpu_calibration.json"
+    if cal.exists():
+        c = json.loads(cal.read_text())
+        res["calibration"] = {"ref_over_port": c["ref_over_port"], "mesh": c["mesh"], "threads": c["threads"],
+                              "source": str(cal.relative_to(ROOT))}
+        res["reference_equivalent"] = res["value"] / c["ref_over_port"]
+    return res
 
 
 if __name__ == "__main__":

@@ -438,4 +438,17 @@ int64_t orc_gmres(void* h, int prec, const double* b, double* xout, double rtol,
 
 int orc_num_threads(void) { return omp_get_max_threads(); }
 
+// y (+)= A x for a scalar CSR, OpenMP over rows like Eigen's row-major product
+// (SparseDenseProduct.h:47-57): the interface-step products of bench.py's CPU baseline
+// (MCONTACT.h:2520-2521, 2632-2704)
+void orc_csr_matvec(int64_t nrow, const int64_t* ptr, const int32_t* col, const double* val, const double* x,
+                    double* y, int accumulate) {
+#pragma omp parallel for schedule(static, 1024)
+    for (int64_t r = 0; r < nrow; ++r) {
+        double s = 0.0;
+        for (int64_t k = ptr[r]; k < ptr[r + 1]; ++k) s += val[k] * x[col[k]];
+        y[r] = accumulate ? y[r] + s : s;
+    }
+}
+
 }  // extern "C"
