@@ -118,6 +118,7 @@ def main():
         dist.broadcast_object_list(obj, src=0)
         mc.comm_init(obj[0])
     t_setup = time.perf_counter() - t_setup
+    log(rank, f"setup {t_setup:.1f} s ({nip} integration points)")
 
     def barrier():
         if world > 1:
@@ -125,6 +126,7 @@ def main():
 
     if a.warmup > 0:
         mc.CONTACT_ANALYSIS(a.warmup, check=False)
+    log(rank, "warmup done")
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -132,6 +134,7 @@ def main():
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
+    log(rank, f"{n} ADMM iterations in {elapsed:.3f} s")
     tm = mc.timing()
     if world > 1:
         t = torch.tensor([elapsed, tm["dof_iterations"], tm["pcg_iterations"]], dtype=torch.float64)
@@ -223,6 +226,12 @@ def main():
         dist.destroy_process_group()
     if result is not None:
         print(json.dumps(result), flush=True)
+
+
+def log(rank: int, msg: str) -> None:
+    """Progress on stderr (stdout carries the one JSON line)."""
+    if rank == 0:
+        print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
 
 def traffic_key(a) -> dict:

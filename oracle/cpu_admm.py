@@ -4,21 +4,23 @@ CPU price of one full ADMM iteration of MCONTACT::CONTACT_ANALYSIS (MCONTACT.h:2
 bench.py's `cpu_baseline` leg, computed by the SGS-faithful port (oracle.cpp: MGPIS::CG_SOLV with
 SGS V(1,1), OpenMP SpMV) on the bench's own operators, at the state the device run reached (its
 u / aux / lambda after the timed iterations), so the subdomain solves see a late-iteration
-right-hand side, not iteration 0's:
+right-hand side, not iteration 0's.  Bounded sample:
 
-  body balance   (2511-2533)  CG_SOLV(1) of each subdomain with consForc + consOper
-                              (systTran_pena aux - systTran lambda) -- sampled: solves run until
-                              `budget_s` is spent (>= 2 of them), priced as nsub x their mean
-  coarse space   (2578-2612)  globTran_1 lambda, globTran_D_1 u, the factorised globCoup_1 solve
-                              (scipy SuperLU; the reference's SimplicialLDLT is factorised at setup
-                              too), accuProl -- all of them, timed
-  interface      (2629-2704)  gamma, projection, aux and lambda with the factorised surface mass
-                              matrices (the reference's LDLT below 120000 rows) -- all interfaces,
-                              timed
+  per subdomain (sampled: a wheel and a worm, more while `budget_s` lasts; priced x nsub / sample)
+    body balance (2511-2533)  CG_SOLV(1) with consForc + consOper (systTran_pena aux - systTran lambda)
+    coarse space (2578-2612)  its part of globTran_D_1 u in factored form -- consStif[L] u (one SpMV;
+                              the reference multiplies the assembled globTran_D_1, more entries, so
+                              this is favourable to the CPU) -- and accuProl x_c
+  once (timed in full)
+    coarse space              globTran_1 lambda, the globCoup_1 solve (scipy SuperLU, factorised
+                              beforehand like the reference's SimplicialLDLT)
+    interface    (2629-2704)  gamma, projection, aux and lambda with the factorised surface mass
+                              matrices (the reference's LDLT below 120000 rows), every interface
 Text output (OUTP_SUB2 / OUTPUT_PRTR every iteration in the reference) is left out.
 """
 from __future__ import annotations
 
+import sys
 import time
 
 import numpy as np
@@ -28,17 +30,26 @@ import scipy.sparse.linalg as spla
 from oracle import oracle as O
 
 
+def _log(msg: str) -> None:
+    print(f"[cpu_baseline] {msg}", file=sys.stderr, flush=True)
+
+
 def price_iteration(P, mc, budget_s: float = 20.0) -> dict:
     nsub, nint = P.nsub, P.nint
+    body = [tuple(int(b) for b in P.array("iface_body", ts)) for ts in range(nint)]
+    fric = [float(P.array("iface_param", ts)[0]) for ts in range(nint)]
     u = [mc.get("resuDisp", tv) for tv in range(nsub)]
     aux = [[mc.get("inteAuxi", 2 * ts + s) for s in range(2)] for ts in range(nint)]
     lam = [[mc.get("inteLagr", 2 * ts + s) for s in range(2)] for ts in range(nint)]
-    ops = [[{n: O.csr64(P.csr(n, 2 * ts + s)) for n in P.IFACE_OPS} for s in range(2)] for ts in range(nint)]
-    body = [tuple(int(b) for b in P.array("iface_body", ts)) for ts in range(nint)]
-    fric = [float(P.array("iface_param", ts)[0]) for ts in range(nint)]
-    # ---- body balance: sampled subdomain solves (wheels first: they carry the load)
-    order = [tv for tv in range(1, nsub, 2)] + [tv for tv in range(0, nsub, 2)]
-    solve_s, iters, ndof, used = [], [], 0, []
+    try:
+        has_coarse = P.csr("globCoup_1").shape[0] > 0
+    except Exception:  # noqa: BLE001 -- no coarse space in this problem
+        has_coarse = False
+    base = P.array("baseReco") if has_coarse else None
+    # ---- per-subdomain work, sampled (wheels carry the load: a wheel, a worm, then alternate)
+    order = [x for pair in zip(range(1, nsub, 2), range(0, nsub, 2)) for x in pair]
+    solve_s, spmv_s, prol_s, iters, used, ndof = [], [], [], [], [], 0
+    t_sample0 = time.perf_counter()
     for tv in order:
         G = P.grid(tv)
         L = G.maxiLeve
@@ -48,46 +59,47 @@ def price_iteration(P, mc, budget_s: float = 20.0) -> dict:
         for ts in range(nint):
             for s in range(2):
                 if body[ts][s] == tv:  # ADDITIONAL_FORCE, MCONTACT.h:2520-2524
-                    O.csr_matvec(ops[ts][s]["systTran_pena"], aux[ts][s], f)
-                    f -= O.csr_matvec(ops[ts][s]["systTran"], lam[ts][s])
+                    O.csr_matvec(O.csr64(P.csr("systTran_pena", 2 * ts + s)), aux[ts][s], f)
+                    f -= O.csr_matvec(O.csr64(P.csr("systTran", 2 * ts + s)), lam[ts][s])
         b = G.consForc + f[flag]
         t = time.perf_counter()
         x, it, _ = M.CG_SOLV(1, b)
         solve_s.append(time.perf_counter() - t)
         iters.append(int(it))
+        if has_coarse:
+            t = time.perf_counter()
+            M.SPMV(L, x)
+            spmv_s.append(time.perf_counter() - t)
+            A = O.csr64(P.csr("accuProl", tv))
+            xc = np.ones(A.shape[1])
+            t = time.perf_counter()
+            O.csr_matvec(A, xc)
+            prol_s.append(time.perf_counter() - t)
         used.append(tv)
         ndof = len(b)
         del M
-        if len(solve_s) >= 2 and sum(solve_s) >= budget_s:
+        _log(f"subdomain {tv}: CG_SOLV(1) {iters[-1]} iterations, {solve_s[-1]:.2f} s")
+        if len(solve_s) >= 2 and time.perf_counter() - t_sample0 >= budget_s:
             break
-    t_body = nsub * float(np.mean(solve_s))
-    # ---- coarse-space correction (muscSett = 2)
-    t_coarse = 0.0
-    try:
-        gc = P.csr("globCoup_1")
-    except Exception:  # noqa: BLE001 -- no coarse space in this problem
-        gc = None
-    if gc is not None and gc.shape[0] > 0:
-        lu = spla.splu(sp.csc_matrix(gc))
+    scale = nsub / len(solve_s)
+    t_body = scale * sum(solve_s)
+    t_coarse = scale * (sum(spmv_s) + sum(prol_s))
+    # ---- coarse solve and globTran_1 lambda, once
+    if has_coarse:
+        lu = spla.splu(sp.csc_matrix(P.csr("globCoup_1")))
         gt = [[O.csr64(P.csr("globTran_1", 2 * ts + s)) for s in range(2)] for ts in range(nint)]
-        gd = [O.csr64(P.csr("globTran_D_1", tv)) for tv in range(nsub)]
-        ap = [O.csr64(P.csr("accuProl", tv)) for tv in range(nsub)]
-        base = P.array("baseReco")
         t = time.perf_counter()
         g = P.array("globForc_1").copy()
         for ts in range(nint):
             for s in range(2):
                 O.csr_matvec(gt[ts][s], lam[ts][s], g)
-        for tv in range(nsub):
-            g -= O.csr_matvec(gd[tv], u[tv])
-        xc = lu.solve(g)
-        for tv in range(nsub):
-            O.csr_matvec(ap[tv], xc[base[tv]:base[tv + 1]])
-        t_coarse = time.perf_counter() - t
+        lu.solve(g)
+        t_coarse += time.perf_counter() - t
     # ---- interface step, every interface
+    ops = [[{n: O.csr64(P.csr(n, 2 * ts + s)) for n in P.IFACE_OPS} for s in range(2)] for ts in range(nint)]
     mfac = [[(spla.factorized(sp.csc_matrix(ops[ts][s]["inteMass_pena"])), spla.factorized(sp.csc_matrix(ops[ts][s]["inteMass"])))
              for s in range(2)] for ts in range(nint)]
-    tTp = [[O.csr64(ops[ts][s]["systTran_pena"].T) for s in range(2)] for ts in range(nint)]
+    tTp = [[O.csr64(ops[ts][s]["systTran_pena"].T.tocsr()) for s in range(2)] for ts in range(nint)]
     t = time.perf_counter()
     nip = 0
     for ts in range(nint):
@@ -103,16 +115,18 @@ def price_iteration(P, mc, budget_s: float = 20.0) -> dict:
             a = mfac[ts][s][0](Tt_u + O.csr_matvec(op[s]["inteMass"], lam[ts][s]) + O.csr_matvec(op[s]["inteInpo"], gam))
             lam[ts][s] = lam[ts][s] + mfac[ts][s][1](Tt_u - O.csr_matvec(op[s]["inteMass_pena"], a))
     t_iface = time.perf_counter() - t
+    _log(f"interface step {t_iface:.2f} s ({nip} integration points)")
     total = t_body + t_coarse + t_iface
     return {
         "value": 1.0 / total,
         "unit": "ADMM it/s",
         "cores": O.threads(),
         "kind": "port",
-        "sample": f"one ADMM iteration at the device run's final state: {len(solve_s)} of {nsub} subdomain "
-                  f"CG_SOLV(1) solves sampled (subdomains {used}, {ndof} DOF each, {iters} SGS-MGPIS iterations, "
-                  f"{sum(solve_s):.1f} s; body balance priced {t_body:.1f} s), coarse-space correction {t_coarse:.2f} s, "
-                  f"interface step over all {nint} interfaces / {nip} integration points {t_iface:.2f} s",
+        "sample": f"one ADMM iteration at the device run's final state: {len(solve_s)} of {nsub} subdomains sampled "
+                  f"(subdomains {used}, {ndof} DOF each: CG_SOLV(1) {iters} SGS-MGPIS iterations in "
+                  f"{sum(solve_s):.1f} s, priced x{scale:g} = {t_body:.1f} s), coarse-space correction {t_coarse:.2f} s "
+                  f"(fine SpMV + accuProl sampled, globTran_1 and the coarse solve in full), interface step over all "
+                  f"{nint} interfaces / {nip} integration points {t_iface:.2f} s",
         "body_s": t_body,
         "coarse_s": t_coarse,
         "iface_s": t_iface,
