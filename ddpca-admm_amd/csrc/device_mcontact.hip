@@ -40,6 +40,7 @@
 #include <numeric>
 #include <thread>
 #include <tuple>
+#include <unordered_map>
 
 #include "../../include/ddpca_amd.h"
 #include "device_mgpis.hpp"
@@ -119,6 +120,12 @@ __global__ void k_outp(const double* x, const uint8_t* mask, const int32_t* onod
     for (int a = 0; a < 3; ++a) u[3 * o + a] = ((m >> a) & 1) ? x[3 * i + a] : presc[3 * o + a];
 }
 
+// y = a - b
+__global__ void k_sub(const double* a, const double* b, double* y, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) y[i] = a[i] - b[i];
+}
+
 __global__ void k_add(double* y, const double* x, int64_t n) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) y[i] += x[i];
@@ -175,6 +182,109 @@ __global__ void k_project(double* g, int32_t* stat, int64_t nip, int comp, doubl
         v[1] = 0.0;
         v[2] = 0.0;
         stat[q] = 0;
+    }
+}
+
+// ---- factored per-ip interface operators (host-built interfaces, Interface::factored).  Every
+// row of inpoLagr, pemaInpo_r and inteInpo is an outer product of ONE integration point's shape
+// values, basis and weight (mcontact.cpp BUILD, MCONTACT.h:570-714), so the gamma product and the
+// inteInpo product are applied from the ip data -- 4 shape values, 4 + 4 node indices per side and
+// the 3x3 basis per ip -- instead of streaming the 24 (frictional: 24 per row, 3 rows) stored
+// entries of every gamma row.  Per-ip arrays are slot-major (x[slot * nip + q]).
+struct IpSide {
+    const double* M;     // 4 x nip shape values
+    const int32_t* lam;  // 4 x nip: workspace index of the contact node's first lambda component
+    const int32_t* u;    // 4 x nip: workspace index of the body node's first dof
+};
+
+// gamma[C q + m] = gcst + sum over owned sides s of h_s (inpoLagr_s lambda_s + pemaInpo_r_s u_s),
+// h_0 = 1/2, h_1 = -1/2 (MCONTACT.h:2632-2636); one thread per ip
+__global__ __launch_bounds__(256) void k_gamma_ip(const double* B, IpSide s0, IpSide s1, int own0, int own1, double p0,
+                                                  double p1, double p2, int C, int64_t nip, const double* W,
+                                                  double* gamma, const double* gcst) {
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= nip) return;
+    double b[3][3];
+#pragma unroll
+    for (int j = 0; j < 9; ++j) b[j / 3][j % 3] = B[(int64_t)j * nip + q];
+    const double pen[3] = {p0, p1, p2};
+    double g[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        if (!(s ? own1 : own0)) continue;
+        const IpSide& S = s ? s1 : s0;
+        const double h = s ? -0.5 : 0.5;
+        double l[3] = {0.0, 0.0, 0.0}, u[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+            const double m = S.M[(int64_t)a * nip + q];
+            const double* lp = W + S.lam[(int64_t)a * nip + q];
+            const double* up = W + S.u[(int64_t)a * nip + q];
+            l[0] += m * lp[0];
+            if (C == 3) {
+                l[1] += m * lp[1];
+                l[2] += m * lp[2];
+            }
+            u[0] += m * up[0];
+            u[1] += m * up[1];
+            u[2] += m * up[2];
+        }
+        if (C == 1) {
+            g[0] += h * (l[0] + pen[0] * (b[0][0] * u[0] + b[0][1] * u[1] + b[0][2] * u[2]));
+        } else {
+#pragma unroll
+            for (int m = 0; m < 3; ++m)
+                g[m] += h * ((b[m][0] * l[0] + b[m][1] * l[1] + b[m][2] * l[2]) +
+                             pen[m] * (b[m][0] * u[0] + b[m][1] * u[1] + b[m][2] * u[2]));
+        }
+    }
+    for (int m = 0; m < C; ++m) gamma[C * q + m] = gcst[C * q + m] + g[m];
+}
+
+// the projected traction in global components, T[3 q + k] = sum_m basis[m][k] gamma[3 q + m]
+// (C = 1: T[q] = gamma[q]) -- what inteInpo's rows contract gamma with
+__global__ void k_traction_ip(const double* B, const double* gamma, double* T, int C, int64_t nip) {
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= nip) return;
+    if (C == 1) {
+        T[q] = gamma[q];
+        return;
+    }
+    const double g0 = gamma[3 * q], g1 = gamma[3 * q + 1], g2 = gamma[3 * q + 2];
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+        T[3 * q + k] = B[(int64_t)k * nip + q] * g0 + B[(int64_t)(3 + k) * nip + q] * g1 + B[(int64_t)(6 + k) * nip + q] * g2;
+}
+
+// out[C a + k] = sum over the ips q touching contact node a of coef (= sgn w_q M_a(q)) T[C q + k]:
+// inteInpo gamma (MCONTACT.h:2671-2684) node-major; a contact node collects up to ~1000 ips on
+// refined contact faces, so one wavefront per node splits its list over the lanes
+__global__ __launch_bounds__(256) void k_inpo_node(const int64_t* ptr, const int32_t* iq, const double* coef,
+                                                   const double* T, int C, int64_t nnc, double* out) {
+    const int64_t a = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (a >= nnc) return;
+    const int lane = threadIdx.x & 63;
+    double v0 = 0.0, v1 = 0.0, v2 = 0.0;
+    for (int64_t e = ptr[a] + lane; e < ptr[a + 1]; e += 64) {
+        const double c = coef[e];
+        const double* t = T + (int64_t)C * iq[e];
+        v0 += c * t[0];
+        if (C == 3) {
+            v1 += c * t[1];
+            v2 += c * t[2];
+        }
+    }
+    v0 = wsum(v0);
+    if (C == 3) {
+        v1 = wsum(v1);
+        v2 = wsum(v2);
+    }
+    if (lane == 0) {
+        out[C * a] = v0;
+        if (C == 3) {
+            out[C * a + 1] = v1;
+            out[C * a + 2] = v2;
+        }
     }
 }
 
@@ -839,6 +949,19 @@ struct ddpca_mcontact {
     double* gamma = nullptr;
     DevBuf<double> uo, state_old, gcst, partial, moni;
     SellOp op_gamma, op_aux, op_lam;     // gamma (my halves), aux RHS, lambda RHS
+    // interfaces whose per-ip operators are applied in factored form (Interface::factored)
+    struct FactItf {
+        int64_t ts = 0, nip = 0, goff = 0;
+        int C = 1, own[2] = {0, 0};
+        double pen[3] = {0.0, 0.0, 0.0};
+        DevBuf<double> B, M[2], T;
+        DevBuf<int32_t> lam[2], u[2];
+        int64_t nnc[2] = {0, 0}, roff[2] = {0, 0};  // node-major inteInpo (fused update)
+        DevBuf<int64_t> nptr[2];
+        DevBuf<int32_t> niq[2];
+        DevBuf<double> ncoef[2];
+    };
+    std::vector<FactItf> fitfs;
     MassBatch mb_aux, mb_lam;
     // fused interface update (every owned side has inteMass_pena = rho inteMass and
     // systTran_pena = rho systTran): one batched solve of M [w | v] = [T^T u | I gamma]
@@ -987,6 +1110,64 @@ void build(ddpca_mcontact& H, Problem& P) {
     auto itf_of = [&](int64_t ts) -> const ddpca_mcontact::Itf& {
         return *std::find_if(H.itfs.begin(), H.itfs.end(), [&](const auto& x) { return x.ts == ts; });
     };
+    // ---- factored per-ip operators of host-built interfaces this rank handles
+    for (const auto& I : H.itfs) {
+        const Interface& itf = mc.searCont[I.ts];
+        if (!I.mine || !itf.factored) continue;
+        ddpca_mcontact::FactItf F;
+        F.ts = I.ts;
+        F.nip = (int64_t)itf.ip.size();
+        F.goff = I.goff;
+        F.C = itf.comp();
+        for (int m = 0; m < F.C; ++m) F.pen[m] = itf.pemaDiag[m];  // pemaDiag[C q + m] = pen[m] for every q
+        const int64_t nip = F.nip;
+        std::vector<double> B(9 * std::max<int64_t>(nip, 1));
+        for (int64_t q = 0; q < nip; ++q)
+            for (int j = 0; j < 9; ++j) B[j * nip + q] = itf.ip[q].basis[j / 3][j % 3];
+        F.B.upload(B);
+        F.T.alloc(std::max<int64_t>(F.C * nip, 1));
+        for (int s = 0; s < 2; ++s) {
+            if (H.owner[itf.body[s]] != H.rank) continue;
+            F.own[s] = 1;
+            const auto& sd = H.sides[side_of.at({I.ts, s})];
+            const auto& Su = H.subs[sd.sub];
+            const int64_t lam0 = H.oS + H.R + sd.roff;
+            std::unordered_map<int64_t, int32_t> cidx;
+            for (size_t a = 0; a < itf.nodeCont[s].size(); ++a) cidx.emplace(itf.nodeCont[s][a], (int32_t)a);
+            std::vector<double> M(4 * std::max<int64_t>(nip, 1));
+            std::vector<int32_t> lam(4 * std::max<int64_t>(nip, 1)), u(4 * std::max<int64_t>(nip, 1));
+            std::vector<std::vector<std::pair<int32_t, double>>> bynode(itf.nodeCont[s].size());
+            const double sgn = s == 0 ? -1.0 : 1.0;  // inteInpo's sign (mcontact.cpp BUILD)
+            for (int64_t q = 0; q < nip; ++q)
+                for (int a = 0; a < 4; ++a) {
+                    const int64_t node = itf.ip[q].node[s][a];
+                    const int32_t c = cidx.at(node);
+                    M[a * nip + q] = itf.ip[q].shap[s][a];
+                    lam[a * nip + q] = (int32_t)(lam0 + F.C * c);
+                    u[a * nip + q] = (int32_t)Su.wcol(3 * node, H.oH);
+                    bynode[c].push_back({(int32_t)q, sgn * (itf.ip[q].w * itf.ip[q].shap[s][a])});
+                }
+            F.M[s].upload(M);
+            F.lam[s].upload(lam);
+            F.u[s].upload(u);
+            std::vector<int64_t> ptr{0};
+            std::vector<int32_t> iq;
+            std::vector<double> coef;
+            for (const auto& v : bynode) {
+                for (const auto& e : v) {
+                    iq.push_back(e.first);
+                    coef.push_back(e.second);
+                }
+                ptr.push_back((int64_t)iq.size());
+            }
+            F.nnc[s] = (int64_t)bynode.size();
+            F.roff[s] = sd.roff;
+            F.nptr[s].upload(ptr);
+            F.niq[s].upload(iq.empty() ? std::vector<int32_t>{0} : iq);
+            F.ncoef[s].upload(coef.empty() ? std::vector<double>{0.0} : coef);
+        }
+        H.fitfs.push_back(std::move(F));
+    }
     // ---- interface operators over W (MCONTACT.h:2632-2636, 2671-2704)
     {
         Rows rg(H.G), ra(H.R), rl(H.R);
@@ -1002,9 +1183,11 @@ void build(ddpca_mcontact& H, Problem& P) {
             const Csr& Lg = itf.inpoLagr[s];
             const Csr& Rg = itf.pemaInpo_r[s];
             for (int64_t i = 0; i < sd.mip; ++i) {
-                auto& row = rg[I.goff + i];
-                for (int64_t k = Lg.ptr[i]; k < Lg.ptr[i + 1]; ++k) row.push_back({lam0 + Lg.col[k], half * Lg.val[k]});
-                for (int64_t k = Rg.ptr[i]; k < Rg.ptr[i + 1]; ++k) row.push_back({Su.wcol(Rg.col[k], H.oH), half * Rg.val[k]});
+                if (!itf.factored) {  // factored interfaces: k_gamma_ip
+                    auto& row = rg[I.goff + i];
+                    for (int64_t k = Lg.ptr[i]; k < Lg.ptr[i + 1]; ++k) row.push_back({lam0 + Lg.col[k], half * Lg.val[k]});
+                    for (int64_t k = Rg.ptr[i]; k < Rg.ptr[i + 1]; ++k) row.push_back({Su.wcol(Rg.col[k], H.oH), half * Rg.val[k]});
+                }
                 if (s == 0) gc[I.goff + i] = -0.5 * (itf.pemaDiag[i] * itf.inpoNgap[i]);
             }
             // aux RHS: systTran_pena^T u + inteMass lambda + inteInpo gamma
@@ -1072,8 +1255,9 @@ void build(ddpca_mcontact& H, Problem& P) {
                 const Csr& Ii = itf.inteInpo[sd.s];
                 for (int64_t r = 0; r < sd.m; ++r) {
                     for (int64_t k = tT.ptr[r]; k < tT.ptr[r + 1]; ++k) rwv[sd.roff + r].push_back({Su.wcol(tT.col[k], H.oH), tT.val[k]});
-                    for (int64_t k = Ii.ptr[r]; k < Ii.ptr[r + 1]; ++k)
-                        rwv[H.R + sd.roff + r].push_back({H.oG + I.goff + Ii.col[k], Ii.val[k]});
+                    if (!itf.factored)  // factored interfaces: k_traction_ip + k_inpo_node
+                        for (int64_t k = Ii.ptr[r]; k < Ii.ptr[r + 1]; ++k)
+                            rwv[H.R + sd.roff + r].push_back({H.oG + I.goff + Ii.col[k], Ii.val[k]});
                     ri[sd.roff + r] = 1.0 / itf.penN;
                 }
                 M2.push_back(&itf.inteMass[sd.s]);
@@ -1513,8 +1697,12 @@ void coarse_correct(ddpca_mcontact& H) {
     if (H.mg && !C.assembled) {
         MgpisDevice& D = *H.mg;
         const int L = (int)D.lev.size() - 1;
-        // consStif[L] x on every owned subdomain, then realProl^T down to level doleMcsc
-        D.spmv(L, D.xs.p, D.lev[L].r.p);
+        // consStif[L] x on every owned subdomain, then realProl^T down to level doleMcsc.  K x is
+        // b - r with PCG's recursive residual r: it meets the true one to the PCG accuracy (the
+        // reference's own CG_SOLV leaves a true residual of 1e-10 |b| behind its 1e-14 recursive
+        // one), and it saves a full fine-level fp64 SpMV per ADMM iteration
+        hipLaunchKernelGGL(k_sub, dim3(nb256(3 * D.lev[L].nn)), dim3(256), 0, st, D.bs.p, D.rs.p, D.lev[L].r.p,
+                           3 * D.lev[L].nn);
         for (int l = L; l > C.dmin; --l) D.restrict_level(l, l == L ? D.lev[L].r.p : D.lev[l].b.p, D.lev[l - 1].b.p);
     }
     hipLaunchKernelGGL(k_csr_wave, dim3(ceil_div(n, 4)), dim3(256), 0, st, C.rptr.p, C.rcol.p, C.rval.p, n, H.W.p,
@@ -1654,6 +1842,12 @@ bool iterate_once(ddpca_mcontact& H, bool check) {
     const double t_solve = ms_since(t0);
     // ---- interface balance: this rank's gamma halves, one launch for every owned side
     H.op_gamma.apply(st, H.W.p, H.gamma, H.gcst.p);
+    for (auto& F : H.fitfs) {
+        const IpSide s0{F.M[0].p, F.lam[0].p, F.u[0].p}, s1{F.M[1].p, F.lam[1].p, F.u[1].p};
+        if (F.nip)
+            hipLaunchKernelGGL(k_gamma_ip, dim3(nb256(F.nip)), dim3(256), 0, st, F.B.p, s0, s1, F.own[0], F.own[1], F.pen[0],
+                               F.pen[1], F.pen[2], F.C, F.nip, H.W.p, H.gamma + F.goff, H.gcst.p + F.goff);
+    }
     bool any_cross = false;
     for (auto& I : H.itfs) any_cross |= (I.cross && I.mine);
     DDPCA_HIP(hipEventRecord(H.ev[0], st));
@@ -1678,6 +1872,15 @@ bool iterate_once(ddpca_mcontact& H, bool check) {
     // ---- aux = (M^rho)^-1 (T^T u + M lambda + I gamma), lambda += M^-1 (T^T u - M^rho aux)
     if (H.fused) {
         H.op_wv.apply(st, H.W.p, H.mb_wv.b.p, nullptr);
+        for (auto& F : H.fitfs) {  // the inteInpo gamma half of the factored interfaces
+            if (!F.nip) continue;
+            hipLaunchKernelGGL(k_traction_ip, dim3(nb256(F.nip)), dim3(256), 0, st, F.B.p, H.gamma + F.goff, F.T.p, F.C,
+                               F.nip);
+            for (int s = 0; s < 2; ++s)
+                if (F.own[s] && F.nnc[s])
+                    hipLaunchKernelGGL(k_inpo_node, dim3(ceil_div(F.nnc[s], 4)), dim3(256), 0, st, F.nptr[s].p, F.niq[s].p,
+                                       F.ncoef[s].p, F.T.p, F.C, F.nnc[s], H.mb_wv.b.p + H.R + F.roff[s]);
+        }
         H.mb_wv.solve(st, H.mb_wv.x.p, 1.0e-14, 2000);
         hipLaunchKernelGGL(k_fuse_aux_lambda, dim3(nb256(H.R)), dim3(256), 0, st, H.state, H.mb_wv.x.p, H.rinv.p, H.R);
     } else if (!H.sides.empty()) {

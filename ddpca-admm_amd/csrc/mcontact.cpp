@@ -226,6 +226,7 @@ void Interface::BUILD(const MULTIGRID& g0, const MULTIGRID& g1) {
         inpoNgap[C * q] = ip[q].gap;
         for (int m = 0; m < C; ++m) pemaDiag[C * q + m] = pen[m];
     }
+    factored = true;
     for (int s = 0; s < 2; ++s) {
         pemaInpo_r[s] = inpoDisp[s];
         for (int64_t r = 0; r < pemaInpo_r[s].nrow; ++r)

@@ -35,6 +35,10 @@ struct Interface {
     int comp() const { return fric == 0.0 ? 1 : 3; }
     int64_t mip() const { return comp() * (int64_t)ip.size(); }
     int64_t mside(int s) const { return comp() * (int64_t)nodeCont[s].size(); }
+    // the per-ip operators were assembled here from `ip` (BUILD): every row of inpoLagr /
+    // pemaInpo_r / inteInpo is an outer product of one ip's shape values and basis, so the device
+    // may apply them in that factored form (operators handed over by a caller are not assumed so)
+    bool factored = false;
     void BUILD(const MULTIGRID& g0, const MULTIGRID& g1);
 };
 
