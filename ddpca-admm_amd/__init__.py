@@ -78,6 +78,12 @@ def _declare(L: C.CDLL) -> None:
                                         C.c_double]
     L.ddpca_problem_establish.argtypes = [_P]
     L.ddpca_problem_set_coarse.argtypes = [_P, C.c_int64, _P]
+    L.ddpca_contact_search.argtypes = [_P, C.c_int64, _P, C.c_int64, C.c_int64, _P, _P, C.c_int64, _P, _P, _P,
+                                       C.c_double, C.POINTER(_P)]
+    L.ddpca_ips_count.argtypes = [_P]
+    L.ddpca_ips_count.restype = C.c_int64
+    L.ddpca_ips_get.argtypes = [_P, _P, _P, _P, _P, _P]
+    L.ddpca_ips_destroy.argtypes = [_P]
     L.ddpca_problem_establish_owned.argtypes = [_P, _P, C.c_int]
     L.ddpca_problem_view.argtypes = [_P, C.c_char_p, C.c_int64, C.c_int64, C.POINTER(_P), _I64P,
                                      C.POINTER(C.c_int)]
@@ -364,6 +370,32 @@ class Problem:
         return subs, ifaces
 
 
+def contact_search(mast_xyz, mast_segm, mast_2d, slav_xyz, slav_segm, slav_2d, buck, maxiDist: float = 1.0e12) -> dict:
+    """CSEARCH::BUCKET_SORT + CONTACT_SEARCH (CSEARCH.h:205-230, 777-817): integration points of
+    the contact between master faces (mast_segm, 4 node ids each, coordinates mast_xyz by node id,
+    2-D bucket coordinates mast_2d) and slave faces, in the reference's order.  Returns node
+    (n, 2, 4), shap (n, 2, 4), basis (n, 3, 3), gap (n), w (n) -- Problem.set_ips' arguments."""
+    def a(x, dt):
+        return np.ascontiguousarray(x, dtype=dt)
+    mx, sx = a(mast_xyz, np.float64).reshape(-1), a(slav_xyz, np.float64).reshape(-1)
+    ms, ss = a(mast_segm, np.int64).reshape(-1), a(slav_segm, np.int64).reshape(-1)
+    m2, s2 = a(mast_2d, np.float64).reshape(-1), a(slav_2d, np.float64).reshape(-1)
+    bk = a(buck, np.int64)
+    h = C.c_void_p()
+    _check(lib().ddpca_contact_search(_ptr(mx), len(mx) // 3, _ptr(sx), len(sx) // 3, len(ms) // 4, _ptr(ms), _ptr(m2),
+                                      len(ss) // 4, _ptr(ss), _ptr(s2), _ptr(bk), float(maxiDist), C.byref(h)))
+    try:
+        n = int(lib().ddpca_ips_count(h))
+        out = dict(node=np.zeros((n, 2, 4), np.int64), shap=np.zeros((n, 2, 4)), basis=np.zeros((n, 3, 3)),
+                   gap=np.zeros(n), w=np.zeros(n))
+        if n:
+            _check(lib().ddpca_ips_get(h, _ptr(out["node"]), _ptr(out["shap"]), _ptr(out["basis"]), _ptr(out["gap"]),
+                                       _ptr(out["w"])))
+        return out
+    finally:
+        lib().ddpca_ips_destroy(h)
+
+
 class MULTIGRID:
     """Read-only view of one subdomain's operators (MULTIGRID.h public members)."""
 
@@ -647,4 +679,5 @@ class MCONTACT:
 
 
 __all__ = ["Problem", "MULTIGRID", "MGPIS", "MCONTACT", "DdpcaError", "lib", "gpu_available", "default_options",
+           "contact_search",
            "LIBPATH", "HEADLINE_OPTIONS", "HEADLINE_MUSC"]

@@ -176,6 +176,26 @@ int ddpca_problem_create(const char* kind, const double* params, int nparams, dd
 int ddpca_problem_set_ips(ddpca_problem_t p, int64_t ts, int64_t n, const int64_t* node,
                           const double* shap, const double* basis, const double* gap,
                           const double* w, double fric, double penN, double penF);
+/* CSEARCH::BUCKET_SORT + CONTACT_SEARCH (CSEARCH.h:205-230, 777-817; per face pair
+ * SEGMENT_INTERSECT / SI_SUB 614-775): the integration points of the contact between a master and
+ * a slave face set, in the reference's order.
+ *   mast_xyz[3 * mast_nnode], slav_xyz[3 * slav_nnode]  node coordinates by node id
+ *   mast_segm[4 nm], slav_segm[4 ns]                     4 node ids per face (EFACE_SURFACE order)
+ *   mast_2d[2 nm], slav_2d[2 ns]                         the faces' 2-D bucket coordinates (the
+ *                                                        examples' mastCoor / slavCoor)
+ *   buck[2]                                              bucket counts (buckNumb)
+ *   maxiDist                                             keep a face pair when one of its points has
+ *                                                        initial gap <= maxiDist (reference 1e12)
+ * The result feeds ddpca_problem_set_ips (ddpca_ips_get's layout is set_ips'). */
+typedef struct ddpca_ips* ddpca_ips_t;
+int ddpca_contact_search(const double* mast_xyz, int64_t mast_nnode, const double* slav_xyz, int64_t slav_nnode,
+                         int64_t nm, const int64_t* mast_segm, const double* mast_2d, int64_t ns,
+                         const int64_t* slav_segm, const double* slav_2d, const int64_t* buck, double maxiDist,
+                         ddpca_ips_t* out);
+int64_t ddpca_ips_count(ddpca_ips_t h);
+/* node[n][2][4], shap[n][2][4], basis[n][3][3] (n, t1, t2), gap[n], w[n]; any pointer may be NULL */
+int ddpca_ips_get(ddpca_ips_t h, int64_t* node, double* shap, double* basis, double* gap, double* w);
+int ddpca_ips_destroy(ddpca_ips_t h);
 /* Coarse-space setting of MCONTACT (muscSett / doleMcsc, MCONTACT.h:22-23), before establish.
  * muscSett = 2 selects the interface-eliminated coarse space (MULTISCALE_1, MCONTACT.h:
  * 1672-2301; the examples' choice, e.g. BLOCK.h:38, TORSION.h:39, DEHW.h:2222), built by
