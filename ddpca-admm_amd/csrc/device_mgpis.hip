@@ -422,26 +422,11 @@ __global__ __launch_bounds__(kBlock) void k_jac0(const double* b, const MT* minv
 // 1/k for the uniform-averaging stencils (weight = 1 / number of parents; k_prolong<true>)
 __constant__ double kInvCount[9] = {0.0, 1.0, 0.5, 1.0 / 3.0, 0.25, 0.2, 1.0 / 6.0, 1.0 / 7.0, 0.125};
 
-template <bool INIT, bool BJ, bool SETD, typename MT = double>
-__global__ __launch_bounds__(kBlock) void k_restrict(const double* rf, const int32_t* rslots, const int64_t* roff,
-                                                     const int32_t* rcol, const double* rwt, const uint8_t* cmask,
-                                                     double* bc, double* xc, double* dc, const MT* minv,
-                                                     const double* coef, int64_t nc, const int32_t* csub,
-                                                     const PcgScal* sc) {
-    NODE_PROLOGUE(nc, csub, sc)
-    const int64_t j = i, c = j >> 6;
-    const int ns = rslots[c];
-    const int32_t* cp = rcol + roff[c] * kChunk + (j & 63);
-    const double* wp = rwt + roff[c] * kChunk + (j & 63);
-    double s0 = 0.0, s1 = 0.0, s2 = 0.0;
-#pragma unroll 4
-    for (int k = 0; k < ns; ++k) {
-        const int64_t f = __builtin_nontemporal_load(cp + (int64_t)k * kChunk);
-        const double w = __builtin_nontemporal_load(wp + (int64_t)k * kChunk);
-        s0 += w * rf[3 * f];
-        s1 += w * rf[3 * f + 1];
-        s2 += w * rf[3 * f + 2];
-    }
+// restriction epilogue: b_c = mask s; INIT: x_c = omega M b_c (SETD: d_c = x_c)
+template <bool INIT, bool BJ, bool SETD, typename MT>
+__device__ __forceinline__ void restrict_store(const uint8_t* cmask, double* bc, double* xc, double* dc, const MT* minv,
+                                               const double* coef, int64_t j, int sub, double s0, double s1,
+                                               double s2) {
     const uint8_t m = cmask[j];
     s0 = (m & 1) ? s0 : 0.0;
     s1 = (m & 2) ? s1 : 0.0;
@@ -462,6 +447,57 @@ __global__ __launch_bounds__(kBlock) void k_restrict(const double* rf, const int
             dc[3 * j + 2] = om * m2;
         }
     }
+}
+
+template <bool INIT, bool BJ, bool SETD, typename MT = double>
+__global__ __launch_bounds__(kBlock) void k_restrict(const double* rf, const int32_t* rslots, const int64_t* roff,
+                                                     const int32_t* rcol, const double* rwt, const uint8_t* cmask,
+                                                     double* bc, double* xc, double* dc, const MT* minv,
+                                                     const double* coef, int64_t nc, const int32_t* csub,
+                                                     const PcgScal* sc) {
+    NODE_PROLOGUE(nc, csub, sc)
+    const int64_t j = i, c = j >> 6;
+    const int ns = rslots[c];
+    const int32_t* cp = rcol + roff[c] * kChunk + (j & 63);
+    const double* wp = rwt + roff[c] * kChunk + (j & 63);
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+#pragma unroll 4
+    for (int k = 0; k < ns; ++k) {
+        const int64_t f = __builtin_nontemporal_load(cp + (int64_t)k * kChunk);
+        const double w = __builtin_nontemporal_load(wp + (int64_t)k * kChunk);
+        s0 += w * rf[3 * f];
+        s1 += w * rf[3 * f + 1];
+        s2 += w * rf[3 * f + 2];
+    }
+    restrict_store<INIT, BJ, SETD>(cmask, bc, xc, dc, minv, coef, j, sub, s0, s1, s2);
+}
+
+// Lattice restriction (LevelDev::lat): children f0 + d0 t0 + d1 t1 + d2 t2 for the bits of the
+// coarse node's 27-bit mask, weight 2^-(|d0|+|d1|+|d2|); every index is computed, the 27 gathers
+// are independent (no index / weight stream)
+template <bool INIT, bool BJ, bool SETD, typename MT = double>
+__global__ __launch_bounds__(kBlock) void k_restrict_lat(const double* rf, const uint32_t* rmsk, const int32_t* rf0,
+                                                         const int32_t* rstr, const uint8_t* cmask, double* bc,
+                                                         double* xc, double* dc, const MT* minv, const double* coef,
+                                                         int64_t nc, const int32_t* csub, const PcgScal* sc) {
+    NODE_PROLOGUE(nc, csub, sc)
+    const int64_t j = i;
+    const uint32_t msk = rmsk[j];
+    const int64_t f0 = rf0[j];
+    const int64_t t0 = rstr[3 * sub], t1 = rstr[3 * sub + 1], t2 = rstr[3 * sub + 2];
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+#pragma unroll
+    for (int q = 0; q < 27; ++q) {
+        const int d0 = q % 3 - 1, d1 = (q / 3) % 3 - 1, d2 = q / 9 - 1;
+        const double w = 1.0 / (double)(1 << ((d0 != 0) + (d1 != 0) + (d2 != 0)));
+        const int64_t f = f0 + d0 * t0 + d1 * t1 + d2 * t2;
+        if ((msk >> q) & 1u) {
+            s0 += w * rf[3 * f];
+            s1 += w * rf[3 * f + 1];
+            s2 += w * rf[3 * f + 2];
+        }
+    }
+    restrict_store<INIT, BJ, SETD>(cmask, bc, xc, dc, minv, coef, j, sub, s0, s1, s2);
 }
 
 // x_f += mask_f (P e_c)
@@ -492,6 +528,34 @@ __global__ __launch_bounds__(kBlock) void k_prolong(const double* ec, const int3
     if (m & 1) xf[3 * i] += e0;
     if (m & 2) xf[3 * i + 1] += e1;
     if (m & 4) xf[3 * i + 2] += e2;
+}
+
+// Lattice prolongation (LevelDev::lat): parents p0 + the subset sums of the coarse strides the
+// node's code selects, weight 1 / 2^popcount(code); one 4-B word per fine node, the (up to 8)
+// parent gathers independent of each other
+__global__ __launch_bounds__(kBlock) void k_prolong_lat(const double* ec, const uint32_t* ppk, const int32_t* pstr,
+                                                        const uint8_t* fmask, double* xf, int64_t nf,
+                                                        const int32_t* csub, const PcgScal* sc) {
+    NODE_PROLOGUE(nf, csub, sc)
+    const uint32_t w = ppk[i];
+    const int64_t p0 = w & 0x1fffffffu;
+    const uint32_t code = w >> 29;
+    const int64_t s0 = pstr[3 * sub], s1 = pstr[3 * sub + 1], s2 = pstr[3 * sub + 2];
+    double e0 = 0.0, e1 = 0.0, e2 = 0.0;
+#pragma unroll
+    for (uint32_t q = 0; q < 8; ++q) {
+        const int64_t c = p0 + ((q & 1) ? s0 : 0) + ((q & 2) ? s1 : 0) + ((q & 4) ? s2 : 0);
+        if ((q & ~code) == 0) {
+            e0 += ec[3 * c];
+            e1 += ec[3 * c + 1];
+            e2 += ec[3 * c + 2];
+        }
+    }
+    const double wt = 1.0 / (double)(1 << __popc(code));
+    const uint8_t m = fmask[i];
+    if (m & 1) xf[3 * i] += wt * e0;
+    if (m & 2) xf[3 * i + 1] += wt * e1;
+    if (m & 4) xf[3 * i + 2] += wt * e2;
 }
 
 // Block transfer entries (rotated nodes): x_f += mask_f (B e_c) per fine node that owns one
@@ -1067,6 +1131,109 @@ int64_t pace_until_done(hipStream_t stream, hipGraphExec_t graph, const MirrorBu
 }
 
 // ============================================================================== setup
+namespace {
+using KidList = std::vector<std::vector<std::pair<int32_t, double>>>;
+
+// Lattice form of a uniformly averaging transfer l-1 -> l (LevelDev::lat): accepted only when it
+// reproduces the explicit lists exactly, per subdomain: every fine node's parent set is p0 plus
+// the subset sums of three coarse strides (the differences of the two-parent nodes), every coarse
+// node's child set is its fine copy plus d . t for d in {-1,0,1}^3 (t from the half-weight
+// children) with weight 2^-|d|, the 27 offsets distinct.  Box lattices numbered lexicographically
+// (the device renumbering of levels >= 1) pass; anything else keeps the explicit lists.
+bool lattice_transfer(LevelDev& L, const LevelDev& C, const std::vector<int32_t>& ppar, const KidList& kids) {
+    const size_t ns = L.noff.size();
+    std::vector<uint32_t> ppk(L.nn, 0u), rmsk(C.nn, 0u);
+    std::vector<int32_t> pstr(3 * ns, 0), rstr(3 * ns, 0), rf0(C.nn, 0);
+    if (C.nn >= (int64_t)1 << 29 || L.nn >= (int64_t)1 << 31) return false;
+    auto three = [](std::vector<int64_t>& d, int32_t* out, int64_t fill) {
+        std::sort(d.begin(), d.end());
+        d.erase(std::unique(d.begin(), d.end()), d.end());
+        if (d.size() > 3 || (!d.empty() && d[0] <= 0)) return false;
+        for (int k = 0; k < 3; ++k) out[k] = (int32_t)(k < (int)d.size() ? d[k] : fill + k);
+        return true;
+    };
+    for (size_t s = 0; s < ns; ++s) {
+        // prolongation
+        std::vector<int64_t> d;
+        int32_t P[8];
+        auto parents = [&](int64_t gf) {
+            int np = 0;
+            while (np < 8 && ppar[np * L.nn + gf] >= 0) {
+                P[np] = ppar[np * L.nn + gf];
+                ++np;
+            }
+            std::sort(P, P + np);
+            return np;
+        };
+        const int64_t f_lo = L.noff[s], f_hi = f_lo + L.nloc[s];
+        for (int64_t gf = f_lo; gf < f_hi; ++gf)
+            if (parents(gf) == 2) d.push_back((int64_t)P[1] - P[0]);
+        int32_t* st = &pstr[3 * s];
+        if (!three(d, st, (int64_t)1 << 28)) return false;
+        for (int64_t gf = f_lo; gf < f_hi; ++gf) {
+            const int np = parents(gf);
+            if (np != 1 && np != 2 && np != 4 && np != 8) return false;
+            bool found = false;
+            for (uint32_t code = 0; code < 8 && !found; ++code) {
+                if ((1 << __builtin_popcount(code)) != np) continue;
+                int64_t set[8];
+                int m = 0;
+                for (uint32_t q = 0; q < 8; ++q)
+                    if ((q & ~code) == 0)
+                        set[m++] = P[0] + ((q & 1) ? st[0] : 0) + ((q & 2) ? st[1] : 0) + ((q & 4) ? (int64_t)st[2] : 0);
+                std::sort(set, set + m);
+                bool eq = true;
+                for (int k = 0; k < m; ++k) eq &= set[k] == P[k];
+                if (eq) {
+                    ppk[gf] = (uint32_t)P[0] | (code << 29);
+                    found = true;
+                }
+            }
+            if (!found) return false;
+        }
+        // restriction
+        const int64_t c_lo = C.noff[s], c_hi = c_lo + C.nloc[s];
+        d.clear();
+        for (int64_t j = c_lo; j < c_hi; ++j) {
+            if (kids[j].empty() || kids[j][0].second != 1.0) return false;
+            for (const auto& k : kids[j])
+                if (k.second == 0.5) d.push_back(std::abs((int64_t)k.first - kids[j][0].first));
+        }
+        int32_t* t = &rstr[3 * s];
+        if (!three(d, t, (int64_t)1 << 29)) return false;
+        std::vector<std::pair<int64_t, int>> offs;  // offset -> bit
+        for (int q = 0; q < 27; ++q)
+            offs.push_back({(int64_t)(q % 3 - 1) * t[0] + (int64_t)((q / 3) % 3 - 1) * t[1] + (int64_t)(q / 9 - 1) * t[2], q});
+        std::sort(offs.begin(), offs.end());
+        for (int q = 1; q < 27; ++q)
+            if (offs[q].first == offs[q - 1].first) return false;
+        for (int64_t j = c_lo; j < c_hi; ++j) {
+            const int64_t f0 = kids[j][0].first;
+            uint32_t msk = 0;
+            for (const auto& k : kids[j]) {
+                const int64_t o = (int64_t)k.first - f0;
+                auto it = std::lower_bound(offs.begin(), offs.end(), std::make_pair(o, -1));
+                if (it == offs.end() || it->first != o) return false;
+                const int q = it->second;
+                const int nz = (q % 3 != 1) + ((q / 3) % 3 != 1) + (q / 9 != 1);
+                if (k.second != 1.0 / (double)(1 << nz) || ((msk >> q) & 1u)) return false;
+                msk |= 1u << q;
+            }
+            rmsk[j] = msk;
+            rf0[j] = (int32_t)f0;
+        }
+    }
+    L.lat = true;
+    L.uw = true;
+    L.ppk.upload(ppk);
+    L.pstr.upload(pstr);
+    L.rmsk.upload(rmsk);
+    L.rf0.upload(rf0);
+    L.rstr.upload(rstr);
+    return true;
+}
+}  // namespace
+
 MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const mgpis_options_t& o)
     : device(dev), opt(o) {
     select_device(device);
@@ -1386,6 +1553,11 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
                 upload_csr(true, L.nrot, L.rot_row, L.rot_ptr, L.rot_par, L.rot_blk);
                 upload_csr(false, L.nrotc, L.rotc_row, L.rotc_ptr, L.rotc_kid, L.rotc_blk);
             }
+            static const bool want_lat = !std::getenv("DDPCA_LATTICE") || std::atoi(std::getenv("DDPCA_LATTICE")) != 0;
+            if (want_lat && uw && ents.empty() && lattice_transfer(L, C, ppar, kids)) {
+                if (std::getenv("DDPCA_VERBOSE")) std::fprintf(stderr, "[ddpca] level %d: lattice transfers\n", l);
+                continue;
+            }
             L.ppar.upload(ppar);
             L.uw = uw;  // prolongation weights from the parent count (restriction keeps rwt)
             if (!uw) L.pw.upload(pw);
@@ -1667,6 +1839,11 @@ void launch_restrict(const LevelDev& F, int grid, hipStream_t st, const double* 
                      const PcgScal* sc) {
     // stored weights: deriving them from a gathered parent count (as k_prolong<true> does)
     // measured 58 -> 102 us on the fine level (profiles/r01_transfer_weights.txt)
+    if (F.lat) {
+        hipLaunchKernelGGL((k_restrict_lat<INIT, BJ, SETD, MT>), dim3(grid), dim3(kBlock), 0, st, rf, F.rmsk.p, F.rf0.p,
+                           F.rstr.p, cmask, bc, xc, dc, minv, coef, nc, csub, sc);
+        return;
+    }
     hipLaunchKernelGGL((k_restrict<INIT, BJ, SETD, MT>), dim3(grid), dim3(kBlock), 0, st, rf, F.rslots.p, F.roff.p,
                        F.rcol.p, F.rwt.p, cmask, bc, xc, dc, minv, coef, nc, csub, sc);
 }
@@ -1892,7 +2069,9 @@ void MgpisDevice::vcycle(const double* rin, double* zout, bool dot) {
     // ---- ascend
     for (int l = cl + 1; l <= Lf; ++l) {
         const LevelDev& F = lev[l];
-        if (F.uw) hipLaunchKernelGGL(k_prolong<true>, dim3(ceil_div(F.nn, kBlock)), dim3(kBlock), 0, stream, cur[l - 1], F.ppar.p, F.pw.p,
+        if (F.lat) hipLaunchKernelGGL(k_prolong_lat, dim3(ceil_div(F.nn, kBlock)), dim3(kBlock), 0, stream, cur[l - 1], F.ppk.p,
+                                      F.pstr.p, F.mask.p, cur[l], F.nn, F.csub.p, scp);
+        else if (F.uw) hipLaunchKernelGGL(k_prolong<true>, dim3(ceil_div(F.nn, kBlock)), dim3(kBlock), 0, stream, cur[l - 1], F.ppar.p, F.pw.p,
                            F.mask.p, cur[l], F.nn, F.csub.p, scp);
         else hipLaunchKernelGGL(k_prolong<false>, dim3(ceil_div(F.nn, kBlock)), dim3(kBlock), 0, stream, cur[l - 1], F.ppar.p, F.pw.p,
                            F.mask.p, cur[l], F.nn, F.csub.p, scp);

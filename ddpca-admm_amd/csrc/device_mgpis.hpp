@@ -107,6 +107,16 @@ struct LevelDev {
     DevBuf<int64_t> roff;    // per coarse chunk + 1
     DevBuf<int32_t> rcol;    // fine node
     DevBuf<double> rwt;
+    // lattice transfers (uniform averaging on a lexicographically numbered box lattice, detected
+    // at create, off with DDPCA_LATTICE=0): a fine node's parents are p0 + subset sums of three
+    // coarse strides, a coarse node's children its fine copy f0 + sum d_k t_k (d in {-1,0,1}^3)
+    // with weight 2^-|d|; the kernels compute the indices instead of streaming ppar / rcol / rwt
+    bool lat = false;
+    DevBuf<uint32_t> ppk;   // per fine node: p0 | (stride-subset code << 29)
+    DevBuf<int32_t> pstr;   // per subdomain: 3 coarse strides
+    DevBuf<uint32_t> rmsk;  // per coarse node: 27-bit mask of the children present, bit (d0+1) + 3(d1+1) + 9(d2+1)
+    DevBuf<int32_t> rf0;    // per coarse node: its fine copy
+    DevBuf<int32_t> rstr;   // per subdomain: 3 fine strides
     // block transfer entries (nodal rotations, MULTIGRID.h:1141-1181): P = S (x) I3 + sum of
     // 3x3 blocks, as CSR over the fine nodes that own one (prolongation) and over the coarse
     // nodes that receive one (restriction, B^T); nrot = 0 on plain S (x) I3 transfers

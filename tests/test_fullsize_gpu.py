@@ -87,3 +87,37 @@ def test_column_offsets_are_exact(ddpca, gpu, tmp_path):
     n = len(P.grid(0).consForc)
     v = ((np.arange(n) * 7919 + 13) % 2003) / 2003.0 - 0.5
     assert np.array_equal(M.spmv(v), np.load(tmp_path / "y.npy"))
+
+
+def test_lattice_transfers_are_the_explicit_ones(ddpca, gpu, tmp_path):
+    """Lattice transfers (indices computed from three strides per subdomain, LevelDev::lat) against
+    the explicit parent / child lists (DDPCA_LATTICE=0), each in its own process: the V-cycle
+    output agrees to rounding (the parents are summed in another order) and the PCG solves to
+    solver accuracy; the lattice process must report that it took the lattice form."""
+    import os
+    import subprocess
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    outs = {}
+    for lat in ("0", "1"):
+        code = (
+            "import importlib, sys, numpy as np\n"
+            f"sys.path.insert(0, {str(root)!r})\n"
+            "D = importlib.import_module('ddpca-admm_amd')\n"
+            "P = D.Problem('beam', 8, 2, 2, 2, 1, 1, 1).ESTABLISH()\n"
+            "M = D.MGPIS.from_problem(P, 0)\n"
+            "b = P.grid(0).consForc\n"
+            "r = ((np.arange(len(b)) * 7919 + 13) % 2003) / 2003.0 - 0.5\n"
+            "x, it, rr = M.CG_SOLV(1, b)\n"
+            f"np.savez({str(tmp_path / ('o' + lat + '.npz'))!r}, z=M.MULT_VCYC(r), x=x, it=it)\n"
+        )
+        env = dict(os.environ, DDPCA_LATTICE=lat, DDPCA_VERBOSE="1")
+        out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+        assert out.returncode == 0, out.stderr
+        outs[lat] = (np.load(tmp_path / f"o{lat}.npz"), out.stderr.count("lattice transfers"))
+    (e, n_e), (t, n_t) = outs["0"], outs["1"]
+    assert n_e == 0 and n_t >= 1
+    assert np.linalg.norm(t["z"] - e["z"]) <= 1e-13 * np.linalg.norm(e["z"])
+    assert abs(int(t["it"]) - int(e["it"])) <= 1
+    assert np.linalg.norm(t["x"] - e["x"]) <= 1e-10 * np.linalg.norm(e["x"])
