@@ -1140,15 +1140,20 @@ using KidList = std::vector<std::vector<std::pair<int32_t, double>>>;
 // node's child set is its fine copy plus d . t for d in {-1,0,1}^3 (t from the half-weight
 // children) with weight 2^-|d|, the 27 offsets distinct.  Box lattices numbered lexicographically
 // (the device renumbering of levels >= 1) pass; anything else keeps the explicit lists.
+bool lattice_reject(int why) {
+    if (std::getenv("DDPCA_VERBOSE")) std::fprintf(stderr, "[ddpca] lattice transfer rejected (check %d)\n", why);
+    return false;
+}
+
 bool lattice_transfer(LevelDev& L, const LevelDev& C, const std::vector<int32_t>& ppar, const KidList& kids) {
     const size_t ns = L.noff.size();
     std::vector<uint32_t> ppk(L.nn, 0u), rmsk(C.nn, 0u);
     std::vector<int32_t> pstr(3 * ns, 0), rstr(3 * ns, 0), rf0(C.nn, 0);
-    if (C.nn >= (int64_t)1 << 29 || L.nn >= (int64_t)1 << 31) return false;
+    if (C.nn >= (int64_t)1 << 29 || L.nn >= (int64_t)1 << 31) return lattice_reject(0);
     auto three = [](std::vector<int64_t>& d, int32_t* out, int64_t fill) {
         std::sort(d.begin(), d.end());
         d.erase(std::unique(d.begin(), d.end()), d.end());
-        if (d.size() > 3 || (!d.empty() && d[0] <= 0)) return false;
+        if (d.size() > 3 || (!d.empty() && d[0] <= 0)) return lattice_reject(1);
         for (int k = 0; k < 3; ++k) out[k] = (int32_t)(k < (int)d.size() ? d[k] : fill + k);
         return true;
     };
@@ -1169,10 +1174,10 @@ bool lattice_transfer(LevelDev& L, const LevelDev& C, const std::vector<int32_t>
         for (int64_t gf = f_lo; gf < f_hi; ++gf)
             if (parents(gf) == 2) d.push_back((int64_t)P[1] - P[0]);
         int32_t* st = &pstr[3 * s];
-        if (!three(d, st, (int64_t)1 << 28)) return false;
+        if (!three(d, st, (int64_t)1 << 28)) return lattice_reject(2);
         for (int64_t gf = f_lo; gf < f_hi; ++gf) {
             const int np = parents(gf);
-            if (np != 1 && np != 2 && np != 4 && np != 8) return false;
+            if (np != 1 && np != 2 && np != 4 && np != 8) return lattice_reject(3);
             bool found = false;
             for (uint32_t code = 0; code < 8 && !found; ++code) {
                 if ((1 << __builtin_popcount(code)) != np) continue;
@@ -1189,34 +1194,34 @@ bool lattice_transfer(LevelDev& L, const LevelDev& C, const std::vector<int32_t>
                     found = true;
                 }
             }
-            if (!found) return false;
+            if (!found) return lattice_reject(4);
         }
         // restriction
         const int64_t c_lo = C.noff[s], c_hi = c_lo + C.nloc[s];
         d.clear();
         for (int64_t j = c_lo; j < c_hi; ++j) {
-            if (kids[j].empty() || kids[j][0].second != 1.0) return false;
+            if (kids[j].empty() || kids[j][0].second != 1.0) return lattice_reject(5);
             for (const auto& k : kids[j])
                 if (k.second == 0.5) d.push_back(std::abs((int64_t)k.first - kids[j][0].first));
         }
         int32_t* t = &rstr[3 * s];
-        if (!three(d, t, (int64_t)1 << 29)) return false;
+        if (!three(d, t, (int64_t)1 << 29)) return lattice_reject(6);
         std::vector<std::pair<int64_t, int>> offs;  // offset -> bit
         for (int q = 0; q < 27; ++q)
             offs.push_back({(int64_t)(q % 3 - 1) * t[0] + (int64_t)((q / 3) % 3 - 1) * t[1] + (int64_t)(q / 9 - 1) * t[2], q});
         std::sort(offs.begin(), offs.end());
         for (int q = 1; q < 27; ++q)
-            if (offs[q].first == offs[q - 1].first) return false;
+            if (offs[q].first == offs[q - 1].first) return lattice_reject(7);
         for (int64_t j = c_lo; j < c_hi; ++j) {
             const int64_t f0 = kids[j][0].first;
             uint32_t msk = 0;
             for (const auto& k : kids[j]) {
                 const int64_t o = (int64_t)k.first - f0;
                 auto it = std::lower_bound(offs.begin(), offs.end(), std::make_pair(o, -1));
-                if (it == offs.end() || it->first != o) return false;
+                if (it == offs.end() || it->first != o) return lattice_reject(8);
                 const int q = it->second;
                 const int nz = (q % 3 != 1) + ((q / 3) % 3 != 1) + (q / 9 != 1);
-                if (k.second != 1.0 / (double)(1 << nz) || ((msk >> q) & 1u)) return false;
+                if (k.second != 1.0 / (double)(1 << nz) || ((msk >> q) & 1u)) return lattice_reject(9);
                 msk |= 1u << q;
             }
             rmsk[j] = msk;
@@ -1558,6 +1563,9 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
                 if (std::getenv("DDPCA_VERBOSE")) std::fprintf(stderr, "[ddpca] level %d: lattice transfers\n", l);
                 continue;
             }
+            if (std::getenv("DDPCA_VERBOSE"))
+                std::fprintf(stderr, "[ddpca] level %d: explicit transfer lists (uniform averaging %d, block entries %zu)\n", l,
+                             (int)uw, ents.size());
             L.ppar.upload(ppar);
             L.uw = uw;  // prolongation weights from the parent count (restriction keeps rwt)
             if (!uw) L.pw.upload(pw);
