@@ -85,6 +85,16 @@ def _declare(L: C.CDLL) -> None:
     L.ddpca_ips_get.argtypes = [_P, _P, _P, _P, _P, _P]
     L.ddpca_ips_destroy.argtypes = [_P]
     L.ddpca_problem_establish_owned.argtypes = [_P, _P, C.c_int]
+    L.ddpca_lagrange_create.argtypes = [C.c_int64, C.c_int64, C.POINTER(_P)]
+    L.ddpca_lagrange_set_subdomain.argtypes = [_P, C.c_int64, C.c_int, _P, _P, _P, C.POINTER(_CsrArg),
+                                               C.POINTER(_CsrArg), _P, C.c_int64, C.POINTER(_CsrArg), _P]
+    L.ddpca_lagrange_set_interface.argtypes = [_P, C.c_int64, C.c_int64, C.c_int64, C.c_double, C.c_int64, _P, _P,
+                                               _P, _P, _P]
+    L.ddpca_lagrange_solve.argtypes = [_P, C.c_int, C.c_int, C.POINTER(MgpisOptions), C.c_int64]
+    L.ddpca_lagrange_solve.restype = C.c_int64
+    L.ddpca_lagrange_get.argtypes = [_P, C.c_char_p, C.c_int64, _P, C.c_int64]
+    L.ddpca_lagrange_get.restype = C.c_int64
+    L.ddpca_lagrange_destroy.argtypes = [_P]
     L.ddpca_problem_view.argtypes = [_P, C.c_char_p, C.c_int64, C.c_int64, C.POINTER(_P), _I64P,
                                      C.POINTER(C.c_int)]
     L.ddpca_problem_destroy.argtypes = [_P]
@@ -394,6 +404,90 @@ def contact_search(mast_xyz, mast_segm, mast_2d, slav_xyz, slav_segm, slav_2d, b
         return out
     finally:
         lib().ddpca_ips_destroy(h)
+
+
+class LAGRANGE:
+    """MCONTACT::LAGRANGE (MCONTACT.h:2847-3701): dual mortar + semi-smooth Newton, every Newton
+    step's condensed system solved on the device by MGPIS-preconditioned BiCGSTAB (precType 1) or
+    diagonal-preconditioned BiCGSTAB (precType 2).  Inputs as LAGRANGE reads them from MCONTACT
+    (include/ddpca_amd.h, ddpca_lagrange_*); ``from_problem`` takes them from a host Problem."""
+
+    def __init__(self, nsub: int, nint: int):
+        h = C.c_void_p()
+        _check(lib().ddpca_lagrange_create(nsub, nint, C.byref(h)))
+        self._h, self.nsub, self.nint, self._keep = h, nsub, nint, []
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h and _lib is not None:
+            _lib.ddpca_lagrange_destroy(h)
+            self._h = None
+
+    def _arr(self, a, dt):
+        a = np.ascontiguousarray(a, dtype=dt)
+        self._keep.append(a)
+        return a
+
+    def _csr(self, m):
+        m = m.tocsr()
+        m.sort_indices()
+        ptr, col, val = self._arr(m.indptr, np.int64), self._arr(m.indices, np.int32), self._arr(m.data, np.float64)
+        return _CsrArg(m.shape[0], m.shape[1], ptr.ctypes.data, col.ctypes.data, val.ctypes.data)
+
+    def set_subdomain(self, tv: int, nnodes, free_dof, K, P, consForc, nnodes_all: int, G, hanging=None):
+        nlev = len(nnodes)
+        fd = [self._arr(f, np.int32) for f in free_dof]
+        fdp = (C.c_void_p * nlev)(*[f.ctypes.data for f in fd])
+        Ka = (_CsrArg * nlev)(*[self._csr(k) for k in K])
+        Pa = (_CsrArg * max(1, nlev - 1))(*[self._csr(q) for q in P])
+        Ga = self._csr(G)
+        hg = None if hanging is None else self._arr(hanging, np.uint8)
+        _check(lib().ddpca_lagrange_set_subdomain(
+            self._h, tv, nlev, _ptr(self._arr(nnodes, np.int64)), _ptr(self._arr([len(f) for f in fd], np.int64)),
+            C.cast(fdp, C.c_void_p), Ka, Pa, _ptr(self._arr(consForc, np.float64)), int(nnodes_all), C.byref(Ga),
+            None if hg is None else _ptr(hg)))
+        return self
+
+    def set_interface(self, ts: int, body, fric: float, node, shap, basis, gap, w):
+        n = len(w)
+        _check(lib().ddpca_lagrange_set_interface(
+            self._h, ts, int(body[0]), int(body[1]), float(fric), n, _ptr(self._arr(node, np.int64)),
+            _ptr(self._arr(shap, np.float64)), _ptr(self._arr(basis, np.float64)), _ptr(self._arr(gap, np.float64)),
+            _ptr(self._arr(w, np.float64))))
+        return self
+
+    @classmethod
+    def from_problem(cls, problem: "Problem") -> "LAGRANGE":
+        """The inputs of an established host Problem (its MULTIGRID hierarchies and integration
+        points; no hanging level, no rotations there: the node-id map is consOper^T)."""
+        import scipy.sparse as sp
+        lg = cls(problem.nsub, problem.nint)
+        for tv in range(problem.nsub):
+            g = problem.grid(tv)
+            L = g.maxiLeve
+            nn = [int(x) for x in problem.array("leveCount", tv)]
+            flag = np.asarray(g.consFlag)
+            fd = [np.flatnonzero(flag[: 3 * nn[l]]) for l in range(L + 1)]
+            G = sp.csr_matrix((np.ones(len(fd[L])), (fd[L], np.arange(len(fd[L])))), shape=(3 * nn[L], len(fd[L])))
+            lg.set_subdomain(tv, nn, fd, [g.consStif(l) for l in range(L + 1)], [g.realProl(l) for l in range(L)],
+                             g.consForc, nn[L], G)
+        for ts in range(problem.nint):
+            lg.set_interface(ts, problem.array("iface_body", ts), float(problem.array("iface_param", ts)[0]),
+                             problem.array("ip_node", ts), problem.array("ip_shap", ts), problem.array("ip_basis", ts),
+                             problem.array("ip_gap", ts), problem.array("ip_w", ts))
+        return lg
+
+    def solve(self, precType: int = 1, device: int = 0, max_newton: int = 50, **opts) -> int:
+        """Returns tc, the reference's "Converge after tc-th iteration"."""
+        o = default_options(**opts)
+        return int(_check(lib().ddpca_lagrange_solve(self._h, device, precType, C.byref(o), max_newton)))
+
+    def get(self, what: str, index: int = 0) -> np.ndarray:
+        n = _check(lib().ddpca_lagrange_get(self._h, what.encode(), index, None, 0))
+        out = np.zeros(n)
+        if n:
+            _check(lib().ddpca_lagrange_get(self._h, what.encode(), index, _ptr(out), n))
+        return out
 
 
 class MULTIGRID:

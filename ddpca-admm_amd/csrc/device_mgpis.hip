@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <deque>
 #include <array>
 #include <climits>
 #include <cmath>
@@ -847,6 +848,26 @@ void invert_spd_device(std::vector<double>& A, int64_t n, hipStream_t st) {
     DDPCA_HIP(hipMemcpy(A.data(), d.p, A.size() * sizeof(double), hipMemcpyDeviceToHost));
 }
 
+// In-place inverse of a dense general matrix (rocSOLVER getrf + getri; the row-major buffer read
+// as column-major is A^T, whose inverse read back row-major is A^-1).  Setup only.
+void invert_general_device(std::vector<double>& A, int64_t n, hipStream_t st) {
+    DevBuf<double> d;
+    d.upload(A);
+    DevBuf<rocblas_int> info(2), ipiv(std::max<int64_t>(n, 1));
+    info.zero(st);
+    rocblas_handle h = nullptr;
+    if (rocblas_create_handle(&h) != rocblas_status_success) throw ApiError(DDPCA_EHIP, "rocblas_create_handle");
+    rocblas_set_stream(h, st);
+    const rocblas_status s1 = rocsolver_dgetrf(h, (rocblas_int)n, (rocblas_int)n, d.p, (rocblas_int)n, ipiv.p, info.p);
+    const rocblas_status s2 = rocsolver_dgetri(h, (rocblas_int)n, d.p, (rocblas_int)n, ipiv.p, info.p + 1);
+    DDPCA_HIP(hipStreamSynchronize(st));
+    rocblas_destroy_handle(h);
+    const auto inf = info.download();
+    if (s1 != rocblas_status_success || s2 != rocblas_status_success) throw ApiError(DDPCA_EHIP, "rocsolver getrf/getri failed");
+    if (inf[0] != 0 || inf[1] != 0) throw ApiError(DDPCA_ENUMERIC, "coarse operator is singular");
+    DDPCA_HIP(hipMemcpy(A.data(), d.p, A.size() * sizeof(double), hipMemcpyDeviceToHost));
+}
+
 bool invert3(const double m[9], double r[9]) {
     const double det = m[0] * (m[4] * m[8] - m[5] * m[7]) - m[1] * (m[3] * m[8] - m[5] * m[6]) +
                        m[2] * (m[3] * m[7] - m[4] * m[6]);
@@ -863,7 +884,7 @@ bool invert3(const double m[9], double r[9]) {
     return true;
 }
 
-constexpr int64_t kMaxRowBlocks = 128;  // node-block row length bound of the setup sort
+constexpr int64_t kMaxRowBlocks = 128;  // longest node-block row the table mode types (longer: streamed)
 
 // Quantised (z, y, x) keys of a level's nodes: coordinates quantised to 1e-9 of the bounding
 // box, so nodes of one mesh plane share a key despite rounding in their coordinates.
@@ -1239,8 +1260,8 @@ bool lattice_transfer(LevelDev& L, const LevelDev& C, const std::vector<int32_t>
 }
 }  // namespace
 
-MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const mgpis_options_t& o)
-    : device(dev), opt(o) {
+MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const mgpis_options_t& o, bool gen)
+    : general(gen), device(dev), opt(o) {
     select_device(device);
     nsub = (int)subs.size();
     if (nsub < 1) throw ApiError(DDPCA_EINVAL, "empty subdomain batch");
@@ -1278,7 +1299,7 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
             if (opt.table_mode == 0) continue;
             int64_t nt = 0, tmax = 0;
             for (int64_t r = 0; r < A.nb; ++r) tmax = std::max<int64_t>(tmax, A.ptr[r + 1] - A.ptr[r]);
-            if (tmax > kMaxRowBlocks) continue;  // reported by the SELL build below
+            if (tmax > kMaxRowBlocks) continue;  // long rows: no table for this subdomain
             types[s] = row_types(A, subs[s].dof_free, keys[l][s], nt);
             tab_blocks += (double)nt * (double)tmax;
             blocks += (double)A.nnzb();
@@ -1310,7 +1331,6 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
             for (int64_t r = 0; r < L.nloc[s]; ++r) {
                 int32_t& sl = slots[c0 + p[r] / kChunk];
                 sl = std::max<int32_t>(sl, (int32_t)(A.ptr[r + 1] - A.ptr[r]));
-                if (A.ptr[r + 1] - A.ptr[r] > kMaxRowBlocks) throw ApiError(DDPCA_EINVAL, "too many blocks in an operator row");
             }
             L.nnzb += A.nnzb();
             L.nnzb_sub.push_back(A.nnzb());
@@ -1339,8 +1359,10 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
                 mask[g] = m;
                 // this row's blocks in canonical order (= increasing device column under the
                 // lexicographic numbering), else in increasing device column
-                int64_t ord[kMaxRowBlocks];
                 const int64_t len = A.ptr[r + 1] - A.ptr[r];
+                thread_local std::vector<int64_t> ordv;  // rows of any length (LAGRANGE's condensed systems)
+                ordv.resize(len);
+                int64_t* ord = ordv.data();
                 if (!keys[l][s].empty()) {
                     canonical_slots(A, r, keys[l][s], ord);
                 } else {
@@ -1446,7 +1468,7 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
             for (int64_t g = 0; g < L.nn; ++g) {
                 const double* m = minv.data() + w * g;
                 for (int k = 0; k < w; ++k)
-                    m32[w * g + k] = bj ? (float)(0.5 * (m[k] + m[3 * (k % 3) + k / 3])) : (float)m[k];
+                    m32[w * g + k] = bj && !general ? (float)(0.5 * (m[k] + m[3 * (k % 3) + k / 3])) : (float)m[k];
             }
             L.minv32.upload(m32);
         }
@@ -1461,14 +1483,25 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
             std::vector<double> pw(8 * L.nn, 0.0);
             bool uw = true;  // every weight == 1 / the node's parent count
             std::vector<std::vector<std::pair<int32_t, double>>> kids(C.nn);
+            struct ExtraEnt {
+                int32_t f, c;
+                double b[9];
+            };
+            std::deque<ExtraEnt> extra;  // scalar parents past the eighth, as blocks
             for (int s = 0; s < nsub; ++s) {
                 const Stencil& st = *subs[s].S[l - 1];
                 const auto& pf = perm[l][s];
                 const auto& pc = perm[l - 1][s];
                 const int64_t nc = C.nloc[s];
                 if (st.nf != L.nloc[s] || st.nc != nc) throw ApiError(DDPCA_EINVAL, "stencil shape");
+                // block entries (weight 0 in the scalar stencil) run in k_prolong_rot / k_restrict_rot
+                // only: they take no parent slot (a node may have any number of them)
+                std::vector<uint8_t> isblk(st.col.size(), 0);
+                for (int64_t e : st.bent) isblk[e] = 1;
+                if (!st.bent.empty()) uw = false;
                 for (int64_t i = 0; i < L.nloc[s]; ++i) {
-                    const int64_t np = st.ptr[i + 1] - st.ptr[i];
+                    int64_t np = 0;
+                    for (int64_t e = st.ptr[i]; e < st.ptr[i + 1]; ++e) np += !isblk[e];
                     const int64_t gf = L.noff[s] + pf[i];
                     if (i < nc) {
                         if (np != 1 || st.col[st.ptr[i]] != i || st.w[st.ptr[i]] != 1.0)
@@ -1479,13 +1512,22 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
                         kids[gc].insert(kids[gc].begin(), {(int32_t)gf, 1.0});
                         continue;
                     }
-                    if (np > 8) throw ApiError(DDPCA_EINVAL, "more than 8 parents");
-                    for (int64_t k = 0; k < np; ++k) {
-                        if (st.w[st.ptr[i] + k] != 1.0 / (double)np) uw = false;
-                        const int64_t gc = C.noff[s] + pc[st.col[st.ptr[i] + k]];
+                    // parents past the eighth (LAGRANGE's condensed transfers) run as w*I blocks
+                    if (np > 8) uw = false;
+                    int64_t k = 0;
+                    for (int64_t e = st.ptr[i]; e < st.ptr[i + 1]; ++e) {
+                        if (isblk[e]) continue;
+                        if (k == 8) {
+                            extra.push_back({(int32_t)gf, (int32_t)(C.noff[s] + pc[st.col[e]]), {}});
+                            for (int q = 0; q < 9; ++q) extra.back().b[q] = q % 4 == 0 ? st.w[e] : 0.0;
+                            continue;
+                        }
+                        if (st.w[e] != 1.0 / (double)np) uw = false;
+                        const int64_t gc = C.noff[s] + pc[st.col[e]];
                         ppar[k * L.nn + gf] = (int32_t)gc;
-                        pw[k * L.nn + gf] = st.w[st.ptr[i] + k];
-                        kids[gc].push_back({(int32_t)gf, st.w[st.ptr[i] + k]});
+                        pw[k * L.nn + gf] = st.w[e];
+                        kids[gc].push_back({(int32_t)gf, st.w[e]});
+                        ++k;
                     }
                 }
             }
@@ -1530,6 +1572,7 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
                     ents.push_back({(int32_t)(L.noff[s] + pf[i]), (int32_t)(C.noff[s] + pc[st.col[e]]), &st.bval[9 * q]});
                 }
             }
+            for (const ExtraEnt& x : extra) ents.push_back({x.f, x.c, x.b});
             if (!ents.empty()) {
                 auto upload_csr = [&](bool by_fine, int64_t& nr, DevBuf<int32_t>& row, DevBuf<int64_t>& ptr_,
                                       DevBuf<int32_t>& other, DevBuf<double>& blk) {
@@ -1596,6 +1639,13 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
                 if (bytes <= 256.0 * 1024 * 1024 && nmax <= 12288) { clev = l; break; }
             }
         if (nlev > 1 && clev == nlev - 1) clev = nlev - 2;
+        int64_t n0max = 0;
+        for (int s = 0; s < nsub; ++s) n0max = std::max<int64_t>(n0max, 3 * subs[s].nnodes[clev]);
+        // a one-level handle too large for a dense inverse serves the diagonal-preconditioned
+        // drivers only (precSwit 0; the V-cycle then reports DDPCA_ESTATE)
+        no_coarse = nlev == 1 && n0max > 12288;
+    }
+    if (!no_coarse) {
         std::vector<double> packed;
         std::vector<int64_t> ao(nsub), no(nsub), nz(nsub);
         for (int s = 0; s < nsub; ++s) {
@@ -1614,7 +1664,8 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
                             D[(3 * p[r] + a) * n0 + 3 * p[j] + b] = v;
                         }
                 }
-            invert_spd_device(D, n0, stream);
+            if (general) invert_general_device(D, n0, stream);
+            else invert_spd_device(D, n0, stream);
             for (int64_t r = 0; r < nc; ++r)
                 for (int a = 0; a < 3; ++a) {
                     if (fr[3 * r + a]) continue;
@@ -1959,6 +2010,7 @@ double MgpisDevice::bench_spmv(int variant, int reps) {
 }
 
 void MgpisDevice::vcycle(const double* rin, double* zout, bool dot) {
+    if (no_coarse) throw ApiError(DDPCA_ESTATE, "one-level handle without a coarse inverse: diagonal preconditioner only");
     const int nlev = (int)lev.size();
     const int Lf = nlev - 1;
     const bool bj = opt.smoother >= 1;

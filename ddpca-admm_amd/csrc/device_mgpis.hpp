@@ -130,7 +130,11 @@ struct LevelDev {
 
 class MgpisDevice {
 public:
-    MgpisDevice(int device, const std::vector<SubdomainOps>& subs, const mgpis_options_t& opt);
+    // general: the operators may be nonsymmetric (LAGRANGE's condensed systems under Coulomb
+    // friction): LU coarse inverse, no symmetrised fp32 smoother copy
+    MgpisDevice(int device, const std::vector<SubdomainOps>& subs, const mgpis_options_t& opt, bool general = false);
+    bool general = false;
+    bool no_coarse = false;  // one-level handle without the dense inverse (diagonal drivers only)
     ~MgpisDevice();
 
     int device = 0;

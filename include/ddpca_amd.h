@@ -27,6 +27,7 @@ extern "C" {
 #define DDPCA_ESTATE (-4)   /* call sequence error */
 #define DDPCA_ECOMM (-5)    /* RCCL error */
 #define DDPCA_ENUMERIC (-6) /* NaN/Inf or breakdown in a Krylov scalar */
+#define DDPCA_ENOCONV (-7)  /* iteration cap reached before convergence (LAGRANGE's Newton loop) */
 
 /* last error message of the calling thread (never NULL) */
 const char* ddpca_last_error(void);
@@ -343,6 +344,48 @@ int64_t mcontact_gpu_get(mcontact_t h, const char* what, int64_t index, void* ou
  * spmv_bytes_per_launch (algorithmic), dof_iterations (sum n_free * PCG its), owned_dofs] */
 int mcontact_gpu_timing(mcontact_t h, double* out10);
 int mcontact_gpu_destroy(mcontact_t h);
+
+/* ========================================================================================
+ * LAGRANGE path: MCONTACT::LAGRANGE (MCONTACT.h:2847-3701) -- dual mortar basis (2894-2947),
+ * nodal normal / tangent frames (2968-3038), normal-tangential mortar coupling (3040-3109),
+ * static condensation of the non-mortar dofs (3281-3416) and the semi-smooth Newton active set
+ * (stick / slip / open, 3637-3698); each Newton step's condensed system is solved on the device
+ * by BiCGSTAB (MGPIS::BiCGSTAB_SOLV, MGPIS.h:350-432, stop ||r|| <= 1e-14 ||b||) preconditioned
+ * with the MGPIS V-cycle of the hierarchy LAGRANGE builds for it (precType 1, 3419-3563) or the
+ * diagonal (precType 2, the reference's Eigen::BiCGSTAB, 3565-3578).
+ * ======================================================================================== */
+typedef struct ddpca_lagrange* ddpca_lagrange_t;
+int ddpca_lagrange_create(int64_t nsub, int64_t nint, ddpca_lagrange_t* out);
+/* Subdomain tv as LAGRANGE reads it after TRANSFER / STIF_MATR / CONSTRAINT(precType == 1 ? 1 : -1)
+ * (MCONTACT.h:2851-2860): nlev levels of mgpi.consStif K[l] (condensed, nfree[l] square), mgpi.realProl
+ * P[l] (nfree[l+1] x nfree[l]), free_dof[l] (consOper[l]: condensed index -> position dof,
+ * increasing, each level's a prefix of the next's), consForc; the node-id map
+ * G = earlTran prolOper[maxiLeve] consOper[maxiLeve]^T (3 nnodes_all x nfree[nlev-1],
+ * MCONTACT.h:3086-3088) and hanging[nnodes_all] (node id on level maxiLeve + 1, nodeLepo; may be
+ * NULL: none). */
+int ddpca_lagrange_set_subdomain(ddpca_lagrange_t h, int64_t tv, int nlev, const int64_t* nnodes,
+                                 const int64_t* nfree, const int32_t* const* free_dof,
+                                 const ddpca_csr_t* K, const ddpca_csr_t* P, const double* consForc,
+                                 int64_t nnodes_all, const ddpca_csr_t* G, const uint8_t* hanging);
+/* Interface ts: contBody {body0 (non-mortar), body1}, fricCoef (< 0 glued, 0 frictionless, > 0
+ * Coulomb) and its integration points in ddpca_problem_set_ips's layout (node ids). */
+int ddpca_lagrange_set_interface(ddpca_lagrange_t h, int64_t ts, int64_t body0, int64_t body1, double fric,
+                                 int64_t n, const int64_t* node, const double* shap, const double* basis,
+                                 const double* gap, const double* w);
+/* Run the Newton loop; returns the reference's "Converge after tc-th iteration" tc (>= 0),
+ * DDPCA_ENOCONV after max_newton steps, or another negative code.  opt: the V-cycle's smoother
+ * settings (NULL: defaults); operators are kept fp64 (the system may be nonsymmetric). */
+int64_t ddpca_lagrange_solve(ddpca_lagrange_t h, int device, int prec_type, const mgpis_options_t* opt,
+                             int64_t max_newton);
+/* Results of the last Newton step (doubles): "u" (index = subdomain: condensed displacement,
+ * the subdomain's block of slidDisp, MCONTACT.h:3589), per interface (index = ts) over the
+ * non-mortar nodes in the reference's (body, node) key order: "node" (node ids), "status"
+ * (0 open, 1 slip, 2 stick: the active set the step solved with), "lambda" (3 per node,
+ * resuLagr: normal, t1, t2), "wedi" (3 per node, nmnoWedi: weighted gap / relative
+ * displacement); "solver_iters" and "changes" (per Newton step: BiCGSTAB iterations, seneNumb).
+ * Returns the count (copies min(count, cap) when out != NULL). */
+int64_t ddpca_lagrange_get(ddpca_lagrange_t h, const char* what, int64_t index, double* out, int64_t cap);
+int ddpca_lagrange_destroy(ddpca_lagrange_t h);
 
 /* ========================================================================================
  * Result files in the reference's text formats (host only; std::scientific, precision 20,

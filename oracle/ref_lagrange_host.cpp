@@ -1,0 +1,176 @@
+// ORACLE TEST INFRASTRUCTURE -- NOT PART OF THE PRODUCT.
+//
+// CPU check of the LAGRANGE host assembly (ddpca-admm_amd/csrc/lagrange.cpp, compiled in here)
+// against the reference's own MCONTACT::LAGRANGE on BLOCK, with an exact sparse LU (Eigen) in
+// place of the device BiCGSTAB: the Newton decisions, multipliers and displacements must follow
+// the reference's to its BiCGSTAB accuracy.  Runs without a GPU (tests/test_lagrange.py); the
+// device path is checked by oracle/ref_lagrange.cpp (tests/test_lagrange_gpu.py).
+//   ref_lagrange_host globLeve fric tangential_load
+#include <unistd.h>
+
+#include <Eigen/SparseLU>
+#include <cstdio>
+#include <fstream>
+#include <sstream>
+
+#include "examples/BLOCK.h"
+#include "lagrange.hpp"
+
+namespace {
+
+using SpMat = Eigen::SparseMatrix<double, Eigen::RowMajor>;
+
+ddpca::Csr to_csr(SpMat m) {
+    m.makeCompressed();
+    ddpca::Csr c;
+    c.nrow = m.rows();
+    c.ncol = m.cols();
+    c.ptr.assign(m.outerIndexPtr(), m.outerIndexPtr() + m.rows() + 1);
+    c.col.assign(m.innerIndexPtr(), m.innerIndexPtr() + m.nonZeros());
+    c.val.assign(m.valuePtr(), m.valuePtr() + m.nonZeros());
+    return c;
+}
+
+SpMat from_csr(const ddpca::Csr& c) {
+    std::vector<Eigen::Triplet<double>> t;
+    for (int64_t r = 0; r < c.nrow; ++r)
+        for (int64_t k = c.ptr[r]; k < c.ptr[r + 1]; ++k) t.emplace_back(r, c.col[k], c.val[k]);
+    SpMat m(c.nrow, c.ncol);
+    m.setFromTriplets(t.begin(), t.end());
+    return m;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    const long gl = argc > 1 ? std::atol(argv[1]) : 1;
+    const double fric = argc > 2 ? std::atof(argv[2]) : 0.0;
+    const double tang = argc > 3 ? std::atof(argv[3]) : 0.0;
+    const std::string log = "Block/ref_lagrange_stdout.txt";
+    BLOCK b;
+    const int saved = dup(1);
+    if (!std::freopen(log.c_str(), "w", stdout)) return 2;
+    b.domaNumb = {1, 1, 1};
+    b.globLeve = gl;
+    b.muscSett = 0;
+    b.doleMcsc.assign(3 * 1 + 6, 1);
+    b.loadPres << tang, 0.0, -1.0E7;
+    b.ESTA_SURF();
+    if (fric == 0.0 && tang == 0.0) {
+        b.SOLVE(1 + 1);  // MESH, contact searches, the reference's LAGRANGE(1)
+    } else {
+        b.SOLVE(0);
+        for (size_t ts = 0; ts < b.fricCoef.size(); ++ts)
+            if (b.fricCoef[ts] == 0.0) b.fricCoef[ts] = fric;  // the contact (not glued) interfaces
+        // LAGRANGE re-runs TRANSFER, which appends to leveNode (MULTIGRID.h:884-900): start it
+        // from the state MESH left, as SOLVE(2) does
+        for (auto& g : b.multGrid) g.leveNode.clear();
+        b.LAGRANGE(1);
+    }
+    std::fflush(stdout);
+    dup2(saved, 1);
+    long tc_ref = -1;
+    {
+        std::ifstream f(log);
+        std::string line;
+        while (std::getline(f, line)) {
+            const auto p = line.find("Converge after ");
+            if (p != std::string::npos) tc_ref = std::atol(line.c_str() + p + 15);
+        }
+    }
+    std::vector<ddpca::LagrangeSub> subs(b.multGrid.size());
+    for (size_t tv = 0; tv < subs.size(); ++tv) {
+        MULTIGRID& g = b.multGrid[tv];
+        ddpca::LagrangeSub& s = subs[tv];
+        const long L = g.mgpi.maxiLeve;
+        s.nlev = (int)L + 1;
+        int64_t acc = 0;
+        for (long l = 0; l <= L; ++l) {
+            acc += (int64_t)g.leveNode[l].size();
+            s.nnodes.push_back(acc);
+            SpMat C = g.consOper[l];
+            C.makeCompressed();
+            s.free_dof.emplace_back(C.innerIndexPtr(), C.innerIndexPtr() + C.rows());
+            s.nfree.push_back(C.rows());
+            s.K.push_back(to_csr(g.mgpi.consStif[l]));
+            if (l < L) s.P.push_back(to_csr(g.mgpi.realProl[l]));
+        }
+        s.consForc.assign(g.consForc.data(), g.consForc.data() + g.consForc.size());
+        s.nall = (int64_t)g.nodeCoor.size();
+        s.G = to_csr(SpMat(g.earlTran * g.prolOper[L] * SpMat(g.consOper[L].transpose())));
+        s.hanging.assign(s.nall, 0);
+        for (int64_t n = 0; n < s.nall; ++n) s.hanging[n] = g.nodeLepo[n][0] == L + 1;
+    }
+    std::vector<ddpca::LagrangeItf> itfs(b.searCont.size());
+    for (size_t ts = 0; ts < itfs.size(); ++ts) {
+        itfs[ts].body[0] = b.contBody[ts][0];
+        itfs[ts].body[1] = b.contBody[ts][1];
+        itfs[ts].fric = b.fricCoef[ts];
+        for (const auto& p : b.searCont[ts].intePoin) {
+            ddpca::LagrangeIp q;
+            for (int s = 0; s < 2; ++s)
+                for (int k = 0; k < 4; ++k) {
+                    q.node[s][k] = p.node[s][k];
+                    q.shap[s][k] = p.shapFunc[s][k];
+                }
+            for (int a = 0; a < 3; ++a)
+                for (int c = 0; c < 3; ++c) q.basis[a][c] = p.basiVect[a](c);
+            q.gap = p.initNgap;
+            q.w = p.quadWeig;
+            itfs[ts].ips.push_back(q);
+        }
+    }
+    const ddpca::LagrangeResult r = ddpca::run_lagrange(subs, itfs, 50, [](const ddpca::LagrangeSystem& sys, std::vector<double>& x) {
+        Eigen::SparseMatrix<double> K = from_csr(sys.K.back());
+        Eigen::SparseLU<Eigen::SparseMatrix<double>> lu(K);
+        Eigen::Map<const Eigen::VectorXd> F(sys.F.data(), (Eigen::Index)sys.F.size());
+        const Eigen::VectorXd u = lu.solve(F);
+        x.assign(u.data(), u.data() + u.size());
+        return (int64_t)0;
+    });
+    double du = 0.0;
+    for (size_t tv = 0; tv < subs.size(); ++tv) {
+        MULTIGRID& g = b.multGrid[tv];
+        Eigen::Map<const Eigen::VectorXd> u(r.u[tv].data(), (Eigen::Index)r.u[tv].size());
+        Eigen::VectorXd disp;
+        g.OUTP_SUB1(Eigen::VectorXd(u), disp);
+        du = std::max(du, (disp - b.resuDisp[tv]).norm() / std::max(b.resuDisp[tv].norm(), 1e-300));
+    }
+    bool nodes_equal = true, stat_equal = true;
+    double dl = 0.0;
+    for (size_t ts = 0; ts < itfs.size(); ++ts) {
+        std::ifstream f(DIRECTORY("resuLagr_" + std::to_string(ts) + ".txt"));
+        std::string line;
+        size_t i = 0;
+        double scale = 0.0, d = 0.0;
+        while (std::getline(f, line)) {
+            std::istringstream is(line);
+            long n, s;
+            double a, c, e;
+            if (!(is >> n >> s >> a >> c >> e)) continue;
+            if (i >= r.node[ts].size()) {
+                nodes_equal = false;
+                break;
+            }
+            nodes_equal = nodes_equal && r.node[ts][i] == n;
+            stat_equal = stat_equal && r.status[ts][i] == s;
+            const double l0 = r.lambda[ts][3 * i];
+            const double l1 = s == 1 ? b.fricCoef[ts] * l0 : r.lambda[ts][3 * i + 1];
+            const double l2 = s == 1 ? 0.0 : r.lambda[ts][3 * i + 2];
+            scale = std::max({scale, std::abs(a), std::abs(c), std::abs(e)});
+            d = std::max({d, std::abs(l0 - a), std::abs(l1 - c), std::abs(l2 - e)});
+            ++i;
+        }
+        nodes_equal = nodes_equal && i == r.node[ts].size();
+        dl = std::max(dl, scale > 0 ? d / scale : d);
+    }
+    std::string ch = "[";
+    for (size_t k = 0; k < r.changes.size(); ++k) ch += (k ? ", " : "") + std::to_string(r.changes[k]);
+    ch += "]";
+    std::fprintf(stderr,
+                 "{\"newton\": %ld, \"newton_ref\": %ld, \"converged\": %s, \"changes\": %s, \"resuDisp_rel\": %.3g, \"lambda_rel\": %.3g, "
+                 "\"nodes_equal\": %s, \"status_equal\": %s}\n",
+                 (long)r.newton, tc_ref, r.converged ? "true" : "false", ch.c_str(), du, dl, nodes_equal ? "true" : "false",
+                 stat_equal ? "true" : "false");
+    return 0;
+}

@@ -1,0 +1,60 @@
+"""LAGRANGE on the device (ddpca_lagrange_*: host assembly + BiCGSTAB on the GPU, MGPIS V-cycle
+of the condensed hierarchy for precType 1, the diagonal for precType 2) against the reference's
+own MCONTACT::LAGRANGE run on its BLOCK example (oracle/_ref/ref_lagrange: domaNumb {1,1,1},
+globLeve 1, 8 interfaces; the reference's stdout and resuLagr_<ts>.txt files are its output).
+
+Tolerances: Newton step count, non-mortar node order and final active-set states equal;
+multipliers within 1e-6 of the largest and displacements within 1e-6 relative (both BiCGSTABs stop
+at ||r|| <= 1e-14 ||b|| with different preconditioners; SURVEY §8 c4's displacement tolerance).
+"""
+import json
+import os
+import subprocess
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+EXE = Path(__file__).resolve().parents[1] / "oracle" / "_ref" / "ref_lagrange"
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("prec,fric,tang", [("1", "0", "0"), ("1", "0.2", "2e6"), ("2", "0", "0")],
+                         ids=["mgpis-frictionless", "mgpis-coulomb-slip", "diagonal-frictionless"])
+def test_lagrange_matches_reference(gpu, tmp_path, prec, fric, tang):
+    if not EXE.exists():
+        pytest.skip("oracle/_ref/ref_lagrange is built where the reference is (travels with the snapshot)")
+    out = subprocess.run([str(EXE), "1", prec, fric, tang], capture_output=True, text=True, timeout=840, cwd=tmp_path,
+                         env=dict(os.environ))
+    assert out.returncode == 0, out.stderr[-2000:]
+    res = json.loads(out.stderr.strip().splitlines()[-1])
+    print(res)
+    assert res["newton"] == res["newton_ref"], res
+    assert res["nodes_equal"] and res["status_equal"], res
+    assert res["lambda_rel"] <= 1e-6 and res["resuDisp_rel"] <= 1e-6, res
+    assert len(res["bicgstab_iters"]) == res["newton"] + 1
+    if fric == "0":  # the patch test: every active node carries the 1e7 load pressure
+        for itf in res["interfaces"]:
+            if itf["fric"] == 0.0 and itf["nodes"]:
+                assert abs(itf["lambda_max"] - 1e7) <= 1e-5 * 1e7, itf
+
+
+def test_lagrange_preconditioners_agree(ddpca, gpu):
+    """A synthetic contact (the host-built two-block problem, frictionless): the Newton loop with the
+    MGPIS-preconditioned and with the diagonal-preconditioned BiCGSTAB takes the same steps to the
+    same active set and multipliers (1e-8), and the multigrid preconditioner needs fewer
+    iterations."""
+    P = ddpca.Problem("twoblock", 0.0, 2).ESTABLISH()
+    runs = {}
+    for prec in (1, 2):
+        lg = ddpca.LAGRANGE.from_problem(P)
+        tc = lg.solve(prec)
+        runs[prec] = (tc, lg.get("status", 0), lg.get("lambda", 0), lg.get("solver_iters"), lg.get("u", 0))
+    (t1, s1, l1, i1, u1), (t2, s2, l2, i2, u2) = runs[1], runs[2]
+    print("newton", t1, t2, "iters", i1, i2)
+    assert t1 == t2 and np.array_equal(s1, s2)
+    assert np.abs(l1 - l2).max() <= 1e-8 * np.abs(l2).max()
+    assert np.linalg.norm(u1 - u2) <= 1e-8 * np.linalg.norm(u2)
+    assert i1.sum() < i2.sum()
