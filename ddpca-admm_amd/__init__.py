@@ -80,6 +80,8 @@ def _declare(L: C.CDLL) -> None:
     L.ddpca_problem_set_coarse.argtypes = [_P, C.c_int64, _P]
     L.ddpca_contact_search.argtypes = [_P, C.c_int64, _P, C.c_int64, C.c_int64, _P, _P, C.c_int64, _P, _P, _P,
                                        C.c_double, C.POINTER(_P)]
+    L.ddpca_refine_select.argtypes = [_P, C.c_int64, _P, C.c_int64, C.c_int64, _P, _P, C.c_int64, _P, _P, _P,
+                                      C.c_double, C.c_int64, _P, C.c_int64, _P, _P, _P]
     L.ddpca_ips_count.argtypes = [_P]
     L.ddpca_ips_count.restype = C.c_int64
     L.ddpca_ips_get.argtypes = [_P, _P, _P, _P, _P, _P]

@@ -313,6 +313,62 @@ void segment_intersect(const V3 mc[4], const V3 sc[4], const int64_t mn[4], cons
     }
 }
 
+// BUCKET_SORT (CSEARCH.h:205-230) + CONTACT_SEARCH (CSEARCH.h:777-817): every (master, slave) face
+// pair of the 3 x 3 buckets around the slave face whose intersection has a point within maxiDist;
+// per slave face, in the reference's order
+std::vector<std::vector<IntegralPoint>> search(const double* mast_xyz, int64_t mast_nnode, const double* slav_xyz,
+                                               int64_t slav_nnode, int64_t nm, const int64_t* mast_segm, const double* mast_2d,
+                                               int64_t ns, const int64_t* slav_segm, const double* slav_2d, const int64_t* buck,
+                                               double maxiDist) {
+    if (!mast_xyz || !slav_xyz || !mast_segm || !slav_segm || !mast_2d || !slav_2d || !buck || nm < 1 || ns < 0)
+        throw ApiError(DDPCA_EINVAL, "null argument / no master faces");
+    if (buck[0] < 1 || buck[1] < 1) throw ApiError(DDPCA_EINVAL, "bucket counts >= 1");
+    for (int64_t i = 0; i < 4 * nm; ++i)
+        if (mast_segm[i] < 0 || mast_segm[i] >= mast_nnode) throw ApiError(DDPCA_EINVAL, "master face node out of range");
+    for (int64_t i = 0; i < 4 * ns; ++i)
+        if (slav_segm[i] < 0 || slav_segm[i] >= slav_nnode) throw ApiError(DDPCA_EINVAL, "slave face node out of range");
+    double lo[2], step[2];
+    for (int a = 0; a < 2; ++a) {
+        double mn = mast_2d[a], mx = mast_2d[a];
+        for (int64_t i = 0; i < nm; ++i) mn = std::min(mn, mast_2d[2 * i + a]), mx = std::max(mx, mast_2d[2 * i + a]);
+        double inc = (mx - mn) / (double)buck[a];
+        if (std::abs(inc) < 1.0e-10) inc = 1.0e-10;
+        lo[a] = mn - inc;
+        step[a] = ((mx + inc) - lo[a]) / (double)buck[a];
+    }
+    std::vector<std::vector<int64_t>> bucket(buck[0] * buck[1]);
+    for (int64_t i = 0; i < nm; ++i) {
+        const long r = (long)((mast_2d[2 * i] - lo[0]) / step[0]), c = (long)((mast_2d[2 * i + 1] - lo[1]) / step[1]);
+        bucket[r * buck[1] + c].push_back(i);
+    }
+    auto corners = [](const double* xyz, const int64_t* seg, V3 c[4]) {
+        for (int k = 0; k < 4; ++k)
+            for (int a = 0; a < 3; ++a) c[k][a] = xyz[3 * seg[k] + a];
+    };
+    // CONTACT_SEARCH (CSEARCH.h:777-817): slave faces in order, each over its 3 x 3 buckets
+    std::vector<std::vector<IntegralPoint>> per(ns);
+#pragma omp parallel for schedule(dynamic, 64)
+    for (int64_t t = 0; t < ns; ++t) {
+        const long r = (long)((slav_2d[2 * t] - lo[0]) / step[0]), c = (long)((slav_2d[2 * t + 1] - lo[1]) / step[1]);
+        if (r < 0 || r > buck[0] - 1 || c < 0 || c > buck[1] - 1) continue;
+        V3 sc[4];
+        corners(slav_xyz, slav_segm + 4 * t, sc);
+        std::vector<IntegralPoint> e;
+        for (long j = std::max(r - 1, 0L); j <= std::min(r + 1, (long)buck[0] - 1); ++j)
+            for (long k = std::max(c - 1, 0L); k <= std::min(c + 1, (long)buck[1] - 1); ++k)
+                for (int64_t m : bucket[j * buck[1] + k]) {
+                    V3 mc[4];
+                    corners(mast_xyz, mast_segm + 4 * m, mc);
+                    e.clear();
+                    segment_intersect(mc, sc, mast_segm + 4 * m, slav_segm + 4 * t, e);
+                    bool keep = false;
+                    for (const auto& p : e) keep |= p.gap <= maxiDist;
+                    if (keep) per[t].insert(per[t].end(), e.begin(), e.end());
+                }
+    }
+    return per;
+}
+
 }  // namespace
 
 struct ddpca_ips {
@@ -326,53 +382,9 @@ int ddpca_contact_search(const double* mast_xyz, int64_t mast_nnode, const doubl
                          const int64_t* slav_segm, const double* slav_2d, const int64_t* buck, double maxiDist,
                          ddpca_ips_t* out) {
     return guarded([&] {
-        if (!mast_xyz || !slav_xyz || !mast_segm || !slav_segm || !mast_2d || !slav_2d || !buck || !out || nm < 1 || ns < 0)
-            throw ApiError(DDPCA_EINVAL, "null argument / no master faces");
-        if (buck[0] < 1 || buck[1] < 1) throw ApiError(DDPCA_EINVAL, "bucket counts >= 1");
-        for (int64_t i = 0; i < 4 * nm; ++i)
-            if (mast_segm[i] < 0 || mast_segm[i] >= mast_nnode) throw ApiError(DDPCA_EINVAL, "master face node out of range");
-        for (int64_t i = 0; i < 4 * ns; ++i)
-            if (slav_segm[i] < 0 || slav_segm[i] >= slav_nnode) throw ApiError(DDPCA_EINVAL, "slave face node out of range");
-        // BUCKET_SORT (CSEARCH.h:205-230)
-        double lo[2], step[2];
-        for (int a = 0; a < 2; ++a) {
-            double mn = mast_2d[a], mx = mast_2d[a];
-            for (int64_t i = 0; i < nm; ++i) mn = std::min(mn, mast_2d[2 * i + a]), mx = std::max(mx, mast_2d[2 * i + a]);
-            double inc = (mx - mn) / (double)buck[a];
-            if (std::abs(inc) < 1.0e-10) inc = 1.0e-10;
-            lo[a] = mn - inc;
-            step[a] = ((mx + inc) - lo[a]) / (double)buck[a];
-        }
-        std::vector<std::vector<int64_t>> bucket(buck[0] * buck[1]);
-        for (int64_t i = 0; i < nm; ++i) {
-            const long r = (long)((mast_2d[2 * i] - lo[0]) / step[0]), c = (long)((mast_2d[2 * i + 1] - lo[1]) / step[1]);
-            bucket[r * buck[1] + c].push_back(i);
-        }
-        auto corners = [](const double* xyz, const int64_t* seg, V3 c[4]) {
-            for (int k = 0; k < 4; ++k)
-                for (int a = 0; a < 3; ++a) c[k][a] = xyz[3 * seg[k] + a];
-        };
-        // CONTACT_SEARCH (CSEARCH.h:777-817): slave faces in order, each over its 3 x 3 buckets
-        std::vector<std::vector<IntegralPoint>> per(ns);
-#pragma omp parallel for schedule(dynamic, 64)
-        for (int64_t t = 0; t < ns; ++t) {
-            const long r = (long)((slav_2d[2 * t] - lo[0]) / step[0]), c = (long)((slav_2d[2 * t + 1] - lo[1]) / step[1]);
-            if (r < 0 || r > buck[0] - 1 || c < 0 || c > buck[1] - 1) continue;
-            V3 sc[4];
-            corners(slav_xyz, slav_segm + 4 * t, sc);
-            std::vector<IntegralPoint> e;
-            for (long j = std::max(r - 1, 0L); j <= std::min(r + 1, (long)buck[0] - 1); ++j)
-                for (long k = std::max(c - 1, 0L); k <= std::min(c + 1, (long)buck[1] - 1); ++k)
-                    for (int64_t m : bucket[j * buck[1] + k]) {
-                        V3 mc[4];
-                        corners(mast_xyz, mast_segm + 4 * m, mc);
-                        e.clear();
-                        segment_intersect(mc, sc, mast_segm + 4 * m, slav_segm + 4 * t, e);
-                        bool keep = false;
-                        for (const auto& p : e) keep |= p.gap <= maxiDist;
-                        if (keep) per[t].insert(per[t].end(), e.begin(), e.end());
-                    }
-        }
+        if (!out) throw ApiError(DDPCA_EINVAL, "null argument");
+        auto per = search(mast_xyz, mast_nnode, slav_xyz, slav_nnode, nm, mast_segm, mast_2d, ns, slav_segm, slav_2d, buck,
+                          maxiDist);
         auto R = std::make_unique<ddpca_ips>();
         size_t total = 0;
         for (const auto& v : per) total += v.size();
@@ -380,6 +392,45 @@ int ddpca_contact_search(const double* mast_xyz, int64_t mast_nnode, const doubl
         for (auto& v : per) R->ip.insert(R->ip.end(), v.begin(), v.end());
         *out = R.release();
     });
+}
+
+int ddpca_refine_select(const double* mast_xyz, int64_t mast_nnode, const double* slav_xyz, int64_t slav_nnode,
+                        int64_t nm, const int64_t* mast_segm, const double* mast_2d, int64_t ns, const int64_t* slav_segm,
+                        const double* slav_2d, const int64_t* buck, double distCrit, int64_t ne_m, const int64_t* mast_elem,
+                        int64_t ne_s, const int64_t* slav_elem, uint8_t* mast_split, uint8_t* slav_split) {
+    int any = 0;
+    const int rc = guarded([&] {
+        if ((ne_m > 0 && (!mast_elem || !mast_split)) || (ne_s > 0 && (!slav_elem || !slav_split)) || ne_m < 0 || ne_s < 0)
+            throw ApiError(DDPCA_EINVAL, "null argument");
+        // the face pairs whose intersection comes within distCrit (ADAPTIVE_REFINE's miniNgap <=
+        // distCrit is CONTACT_SEARCH's keep rule): every node of their points is a split node
+        const auto per = search(mast_xyz, mast_nnode, slav_xyz, slav_nnode, nm, mast_segm, mast_2d, ns, slav_segm, slav_2d,
+                                buck, distCrit);
+        std::vector<uint8_t> split[2] = {std::vector<uint8_t>(mast_nnode, 0), std::vector<uint8_t>(slav_nnode, 0)};
+        for (const auto& v : per)
+            for (const auto& p : v)
+                for (int s = 0; s < 2; ++s)
+                    for (int k = 0; k < 4; ++k) {
+                        split[s][p.node[s][k]] = 1;
+                        any = 1;
+                    }
+        // candidate elements with a split corner node are refined (CSEARCH.h:927-952)
+        const int64_t ne[2] = {ne_m, ne_s};
+        const int64_t* el[2] = {mast_elem, slav_elem};
+        uint8_t* fl[2] = {mast_split, slav_split};
+        const int64_t nn[2] = {mast_nnode, slav_nnode};
+        for (int s = 0; s < 2; ++s)
+            for (int64_t e = 0; e < ne[s]; ++e) {
+                uint8_t f = 0;
+                for (int k = 0; k < 8; ++k) {
+                    const int64_t n = el[s][8 * e + k];
+                    if (n < 0 || n >= nn[s]) throw ApiError(DDPCA_EINVAL, "element corner node out of range");
+                    f |= split[s][n];
+                }
+                fl[s][e] = f;
+            }
+    });
+    return rc != 0 ? rc : any;
 }
 
 int64_t ddpca_ips_count(ddpca_ips_t h) { return h ? (int64_t)h->ip.size() : -1; }

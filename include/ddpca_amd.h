@@ -193,6 +193,17 @@ int ddpca_contact_search(const double* mast_xyz, int64_t mast_nnode, const doubl
                          int64_t nm, const int64_t* mast_segm, const double* mast_2d, int64_t ns,
                          const int64_t* slav_segm, const double* slav_2d, const int64_t* buck, double maxiDist,
                          ddpca_ips_t* out);
+/* CSEARCH::ADAPTIVE_REFINE (CSEARCH.h:839-956), the selection: with the same face / bucket input as
+ * ddpca_contact_search, every node of the integration points of face pairs that come within
+ * distCrit is a split node, and a candidate element (8 corner node ids; the caller passes the leaf
+ * elements of level tempLeve) with a split corner is flagged in mast_split / slav_split.  Returns
+ * 1 when any node was selected (the reference's isnoRefi), 0 otherwise.  Refining the flagged
+ * elements (CURVEDS::REFINE + MULTIGRID::REFINE, refiPatt 0) is the caller's mesh operation. */
+int ddpca_refine_select(const double* mast_xyz, int64_t mast_nnode, const double* slav_xyz, int64_t slav_nnode,
+                        int64_t nm, const int64_t* mast_segm, const double* mast_2d, int64_t ns,
+                        const int64_t* slav_segm, const double* slav_2d, const int64_t* buck, double distCrit,
+                        int64_t ne_m, const int64_t* mast_elem, int64_t ne_s, const int64_t* slav_elem,
+                        uint8_t* mast_split, uint8_t* slav_split);
 int64_t ddpca_ips_count(ddpca_ips_t h);
 /* node[n][2][4], shap[n][2][4], basis[n][3][3] (n, t1, t2), gap[n], w[n]; any pointer may be NULL */
 int ddpca_ips_get(ddpca_ips_t h, int64_t* node, double* shap, double* basis, double* gap, double* w);

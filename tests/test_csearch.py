@@ -49,3 +49,24 @@ def test_reference_curved_contact_search(tmp_path):
     assert res["ok"], res
     for itf in res["interfaces"]:
         assert itf["ips"] == itf["ips_ref"] > 0 and itf["nodes_equal"], itf
+
+
+@pytest.mark.parametrize("dist", ["1e-5", "0"])
+def test_adaptive_refine_selection_matches_reference(tmp_path, dist):
+    """CSEARCH::ADAPTIVE_REFINE's selection (CSEARCH.h:839-956) against the reference's own run on
+    its CYLINDER example (oracle/ref_refine.cpp): of the 4096 finest leaf elements per side of the
+    first curved contact pair, exactly the elements the reference refines (1024 per side, the band
+    within distCrit = 1e-5 of the other surface; none at 0) are the ones ddpca_refine_select flags,
+    and isnoRefi agrees."""
+    exe = Path(__file__).resolve().parents[1] / "oracle" / "_ref" / "ref_refine"
+    if not exe.exists():
+        pytest.skip("oracle/_ref/ref_refine is built where the reference is (oracle/Makefile)")
+    out = subprocess.run([str(exe), dist], capture_output=True, text=True, timeout=600, cwd=tmp_path)
+    assert out.returncode == 0, out.stderr[-2000:]
+    res = json.loads(out.stderr.strip().splitlines()[-1])
+    print(res)
+    assert res["equal"], res
+    if dist != "0":
+        assert res["isnoRefi"] and min(res["refined_ref"]) > 0, res
+    else:
+        assert not res["isnoRefi"], res
