@@ -848,24 +848,51 @@ void invert_spd_device(std::vector<double>& A, int64_t n, hipStream_t st) {
     DDPCA_HIP(hipMemcpy(A.data(), d.p, A.size() * sizeof(double), hipMemcpyDeviceToHost));
 }
 
-// In-place inverse of a dense general matrix (rocSOLVER getrf + getri; the row-major buffer read
-// as column-major is A^T, whose inverse read back row-major is A^-1).  Setup only.
-void invert_general_device(std::vector<double>& A, int64_t n, hipStream_t st) {
-    DevBuf<double> d;
+// Scale row i of the column-major n x n matrix Vt by 1 / s_i, or 0 when s_i <= tol (pseudo-inverse)
+__global__ void k_pinv_rows(double* Vt, const double* S, int64_t n, double tol) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= n * n) return;
+    const double sv = S[idx % n];
+    Vt[idx] *= sv > tol ? 1.0 / sv : 0.0;
+}
+
+// In-place pseudo-inverse of a dense general matrix (setup only): rocSOLVER gesvd of the buffer
+// read column-major (M = A^T = U S Vt), then C = Vt^T S+ U^T (rocBLAS gemm) = (A^+)^T column-major,
+// i.e. A^+ row-major.  Singular values below 1e-11 of the largest are dropped: the coarse operator
+// of LAGRANGE's condensed system is singular when a frictionless contact leaves a body free to
+// slide (the reference's LDLT meets the same zero pivots); the V-cycle then solves on the range.
+void pinv_general_device(std::vector<double>& A, int64_t n, hipStream_t st, int64_t* dropped) {
+    DevBuf<double> d, S(std::max<int64_t>(n, 1)), U(std::max<int64_t>(n * n, 1)), Vt(std::max<int64_t>(n * n, 1)),
+        E(std::max<int64_t>(n, 1)), C(std::max<int64_t>(n * n, 1));
     d.upload(A);
-    DevBuf<rocblas_int> info(2), ipiv(std::max<int64_t>(n, 1));
+    DevBuf<rocblas_int> info(1);
     info.zero(st);
     rocblas_handle h = nullptr;
     if (rocblas_create_handle(&h) != rocblas_status_success) throw ApiError(DDPCA_EHIP, "rocblas_create_handle");
     rocblas_set_stream(h, st);
-    const rocblas_status s1 = rocsolver_dgetrf(h, (rocblas_int)n, (rocblas_int)n, d.p, (rocblas_int)n, ipiv.p, info.p);
-    const rocblas_status s2 = rocsolver_dgetri(h, (rocblas_int)n, d.p, (rocblas_int)n, ipiv.p, info.p + 1);
+    const rocblas_status s1 = rocsolver_dgesvd(h, rocblas_svect_all, rocblas_svect_all, (rocblas_int)n, (rocblas_int)n, d.p,
+                                               (rocblas_int)n, S.p, U.p, (rocblas_int)n, Vt.p, (rocblas_int)n, E.p,
+                                               rocblas_outofplace, info.p);
+    std::vector<double> sv(n);
+    DDPCA_HIP(hipMemcpyAsync(sv.data(), S.p, n * sizeof(double), hipMemcpyDeviceToHost, st));
+    DDPCA_HIP(hipStreamSynchronize(st));
+    const auto inf = info.download();
+    if (s1 != rocblas_status_success || inf[0] != 0) {
+        rocblas_destroy_handle(h);
+        throw ApiError(DDPCA_EHIP, "rocsolver gesvd failed on the coarse operator");
+    }
+    const double tol = 1e-11 * (n ? sv[0] : 0.0);
+    *dropped = 0;
+    for (double x : sv) *dropped += !(x > tol);
+    hipLaunchKernelGGL(k_pinv_rows, dim3(std::max<int64_t>(1, (n * n + 255) / 256)), dim3(256), 0, st, Vt.p, S.p, n, tol);
+    const double one = 1.0, zero = 0.0;
+    const rocblas_status s2 = rocblas_dgemm(h, rocblas_operation_transpose, rocblas_operation_transpose, (rocblas_int)n,
+                                            (rocblas_int)n, (rocblas_int)n, &one, Vt.p, (rocblas_int)n, U.p, (rocblas_int)n,
+                                            &zero, C.p, (rocblas_int)n);
     DDPCA_HIP(hipStreamSynchronize(st));
     rocblas_destroy_handle(h);
-    const auto inf = info.download();
-    if (s1 != rocblas_status_success || s2 != rocblas_status_success) throw ApiError(DDPCA_EHIP, "rocsolver getrf/getri failed");
-    if (inf[0] != 0 || inf[1] != 0) throw ApiError(DDPCA_ENUMERIC, "coarse operator is singular");
-    DDPCA_HIP(hipMemcpy(A.data(), d.p, A.size() * sizeof(double), hipMemcpyDeviceToHost));
+    if (s2 != rocblas_status_success) throw ApiError(DDPCA_EHIP, "rocblas gemm failed");
+    DDPCA_HIP(hipMemcpy(A.data(), C.p, A.size() * sizeof(double), hipMemcpyDeviceToHost));
 }
 
 bool invert3(const double m[9], double r[9]) {
@@ -1664,8 +1691,14 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
                             D[(3 * p[r] + a) * n0 + 3 * p[j] + b] = v;
                         }
                 }
-            if (general) invert_general_device(D, n0, stream);
-            else invert_spd_device(D, n0, stream);
+            if (general) {
+                int64_t dropped = 0;
+                pinv_general_device(D, n0, stream, &dropped);
+                if (std::getenv("DDPCA_VERBOSE"))
+                    std::fprintf(stderr, "[ddpca] coarse pseudo-inverse: %ld of %ld singular values dropped\n", (long)dropped, (long)n0);
+            } else {
+                invert_spd_device(D, n0, stream);
+            }
             for (int64_t r = 0; r < nc; ++r)
                 for (int a = 0; a < 3; ++a) {
                     if (fr[3 * r + a]) continue;

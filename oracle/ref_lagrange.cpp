@@ -18,7 +18,10 @@
 #include <fstream>
 #include <sstream>
 
+#include <memory>
+
 #include "examples/BLOCK.h"
+#include "examples/CYLINDER_1.h"
 #include "ref_bind.hpp"
 
 namespace {
@@ -59,31 +62,48 @@ void on_fault(int sig) {  // a crash names its frames (no debugger on the GPU bo
 int main(int argc, char** argv) {
     std::signal(SIGSEGV, on_fault);
     std::signal(SIGABRT, on_fault);
-    const long gl = argc > 1 ? std::atol(argv[1]) : 1;
-    const long prec = argc > 2 ? std::atol(argv[2]) : 1;
-    const double fric = argc > 3 ? std::atof(argv[3]) : 0.0;
-    const double tang = argc > 4 ? std::atof(argv[4]) : 0.0;
-    const std::string log = "Block/ref_lagrange_stdout.txt";
-    BLOCK b;  // creates ./Block/
+    // ref_lagrange [cylinder] globLeve precType fric tangential_load
+    const bool cyl = argc > 1 && std::string(argv[1]) == "cylinder";
+    const int a0 = cyl ? 2 : 1;
+    const long gl = argc > a0 ? std::atol(argv[a0]) : 1;
+    const long prec = argc > a0 + 1 ? std::atol(argv[a0 + 1]) : 1;
+    const double fric = argc > a0 + 2 ? std::atof(argv[a0 + 2]) : 0.0;
+    const double tang = argc > a0 + 3 ? std::atof(argv[a0 + 3]) : 0.0;
+    std::unique_ptr<BLOCK> blk;
+    std::unique_ptr<CYLINDER_1> cy;
+    if (cyl) cy = std::make_unique<CYLINDER_1>();  // creates ./Cylinder/
+    else blk = std::make_unique<BLOCK>();           // creates ./Block/
+    MCONTACT& b = cyl ? static_cast<MCONTACT&>(*cy) : static_cast<MCONTACT&>(*blk);
+    const std::string log = std::string(cyl ? "Cylinder" : "Block") + "/ref_lagrange_stdout.txt";
     const int saved = dup(1);
     if (!std::freopen(log.c_str(), "w", stdout)) return 2;  // the reference's progress output, parsed below
-    b.domaNumb = {1, 1, 1};
-    b.globLeve = gl;
-    b.muscSett = 0;  // no coarse space: ESTABLISH stays cheap and APPS returns at once
-    b.doleMcsc.assign(3 * 1 + 6, 1);
-    b.loadPres << tang, 0.0, -1.0E7;
-    b.ESTA_SURF();
-    if (fric == 0.0 && tang == 0.0) {
-        b.SOLVE(1 + prec);  // MESH, contact searches, the reference's LAGRANGE(prec)
+    if (cyl) {
+        // CYLINDER_1 (locally refined: hanging non-mortar nodes are dropped, MCONTACT.h:2870-2893),
+        // reduced locaLeve as in ref_cylinder; frictionless as the example sets it
+        cy->copyNumb = 1;
+        cy->locaLeve = 3 + gl;
+        cy->globInho = 2;
+        cy->bandWidt = 2.0e-4;
+        cy->SOLVE(1 + prec);
     } else {
-        b.SOLVE(0);  // MESH, contact searches, ESTABLISH
-        for (size_t ts = 0; ts < b.fricCoef.size(); ++ts)
-            if (b.fricCoef[ts] == 0.0) b.fricCoef[ts] = fric;  // the contact (not glued) interfaces
-        // LAGRANGE re-runs TRANSFER, which appends to leveNode (MULTIGRID.h:884-900): start it
-        // from the state MESH left, as SOLVE(2) does
-        for (auto& g : b.multGrid) g.leveNode.clear();
-        b.LAGRANGE(prec);
-    }  // the contact (not glued) interfaces
+        blk->domaNumb = {1, 1, 1};
+        blk->globLeve = gl;
+        blk->muscSett = 0;  // no coarse space: ESTABLISH stays cheap and APPS returns at once
+        blk->doleMcsc.assign(3 * 1 + 6, 1);
+        blk->loadPres << tang, 0.0, -1.0E7;
+        blk->ESTA_SURF();
+        if (fric == 0.0 && tang == 0.0) {
+            blk->SOLVE(1 + prec);  // MESH, contact searches, the reference's LAGRANGE(prec)
+        } else {
+            blk->SOLVE(0);  // MESH, contact searches, ESTABLISH
+            for (size_t ts = 0; ts < b.fricCoef.size(); ++ts)
+                if (b.fricCoef[ts] == 0.0) b.fricCoef[ts] = fric;  // the contact (not glued) interfaces
+            // LAGRANGE re-runs TRANSFER, which appends to leveNode (MULTIGRID.h:884-900): start it
+            // from the state MESH left, as SOLVE(2) does
+            for (auto& g : b.multGrid) g.leveNode.clear();
+            b.LAGRANGE(prec);
+        }
+    }
     std::fflush(stdout);
     dup2(saved, 1);
     // the reference's Newton count and BiCGSTAB iterations from its progress output

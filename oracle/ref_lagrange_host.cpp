@@ -5,7 +5,7 @@
 // place of the device BiCGSTAB: the Newton decisions, multipliers and displacements must follow
 // the reference's to its BiCGSTAB accuracy.  Runs without a GPU (tests/test_lagrange.py); the
 // device path is checked by oracle/ref_lagrange.cpp (tests/test_lagrange_gpu.py).
-//   ref_lagrange_host globLeve fric tangential_load
+//   ref_lagrange_host [cylinder] globLeve fric tangential_load
 #include <unistd.h>
 
 #include <Eigen/SparseLU>
@@ -13,7 +13,10 @@
 #include <fstream>
 #include <sstream>
 
+#include <memory>
+
 #include "examples/BLOCK.h"
+#include "examples/CYLINDER_1.h"
 #include "lagrange.hpp"
 
 namespace {
@@ -43,29 +46,42 @@ SpMat from_csr(const ddpca::Csr& c) {
 }  // namespace
 
 int main(int argc, char** argv) {
-    const long gl = argc > 1 ? std::atol(argv[1]) : 1;
-    const double fric = argc > 2 ? std::atof(argv[2]) : 0.0;
-    const double tang = argc > 3 ? std::atof(argv[3]) : 0.0;
-    const std::string log = "Block/ref_lagrange_stdout.txt";
-    BLOCK b;
+    // ref_lagrange_host [cylinder] globLeve fric tangential_load
+    const bool cyl = argc > 1 && std::string(argv[1]) == "cylinder";
+    const int a0 = cyl ? 2 : 1;
+    const long gl = argc > a0 ? std::atol(argv[a0]) : 1;
+    const double fric = argc > a0 + 1 ? std::atof(argv[a0 + 1]) : 0.0;
+    const double tang = argc > a0 + 2 ? std::atof(argv[a0 + 2]) : 0.0;
+    std::unique_ptr<BLOCK> blk;
+    std::unique_ptr<CYLINDER_1> cy;
+    if (cyl) cy = std::make_unique<CYLINDER_1>();
+    else blk = std::make_unique<BLOCK>();
+    MCONTACT& b = cyl ? static_cast<MCONTACT&>(*cy) : static_cast<MCONTACT&>(*blk);
+    const std::string log = std::string(cyl ? "Cylinder" : "Block") + "/ref_lagrange_stdout.txt";
     const int saved = dup(1);
     if (!std::freopen(log.c_str(), "w", stdout)) return 2;
-    b.domaNumb = {1, 1, 1};
-    b.globLeve = gl;
-    b.muscSett = 0;
-    b.doleMcsc.assign(3 * 1 + 6, 1);
-    b.loadPres << tang, 0.0, -1.0E7;
-    b.ESTA_SURF();
-    if (fric == 0.0 && tang == 0.0) {
-        b.SOLVE(1 + 1);  // MESH, contact searches, the reference's LAGRANGE(1)
+    if (cyl) {
+        cy->copyNumb = 1;
+        cy->locaLeve = 3 + gl;
+        cy->globInho = 2;
+        cy->bandWidt = 2.0e-4;
+        cy->SOLVE(2);
     } else {
-        b.SOLVE(0);
-        for (size_t ts = 0; ts < b.fricCoef.size(); ++ts)
-            if (b.fricCoef[ts] == 0.0) b.fricCoef[ts] = fric;  // the contact (not glued) interfaces
-        // LAGRANGE re-runs TRANSFER, which appends to leveNode (MULTIGRID.h:884-900): start it
-        // from the state MESH left, as SOLVE(2) does
-        for (auto& g : b.multGrid) g.leveNode.clear();
-        b.LAGRANGE(1);
+        blk->domaNumb = {1, 1, 1};
+        blk->globLeve = gl;
+        blk->muscSett = 0;
+        blk->doleMcsc.assign(3 * 1 + 6, 1);
+        blk->loadPres << tang, 0.0, -1.0E7;
+        blk->ESTA_SURF();
+        if (fric == 0.0 && tang == 0.0) {
+            blk->SOLVE(1 + 1);  // MESH, contact searches, the reference's LAGRANGE(1)
+        } else {
+            blk->SOLVE(0);
+            for (size_t ts = 0; ts < b.fricCoef.size(); ++ts)
+                if (b.fricCoef[ts] == 0.0) b.fricCoef[ts] = fric;  // the contact (not glued) interfaces
+            for (auto& g : b.multGrid) g.leveNode.clear();  // LAGRANGE re-runs TRANSFER (MULTIGRID.h:884-900)
+            b.LAGRANGE(1);
+        }
     }
     std::fflush(stdout);
     dup2(saved, 1);

@@ -1,7 +1,8 @@
 """LAGRANGE on the device (ddpca_lagrange_*: host assembly + BiCGSTAB on the GPU, MGPIS V-cycle
 of the condensed hierarchy for precType 1, the diagonal for precType 2) against the reference's
 own MCONTACT::LAGRANGE run on its BLOCK example (oracle/_ref/ref_lagrange: domaNumb {1,1,1},
-globLeve 1, 8 interfaces; the reference's stdout and resuLagr_<ts>.txt files are its output).
+globLeve 1, 8 interfaces) and its CYLINDER example (hanging nodes, curved surfaces); the
+reference's stdout and resuLagr_<ts>.txt files are its output.
 
 Tolerances: Newton step count, non-mortar node order and final active-set states equal;
 multipliers within 1e-6 of the largest and displacements within 1e-6 relative (both BiCGSTABs stop
@@ -21,21 +22,33 @@ EXE = Path(__file__).resolve().parents[1] / "oracle" / "_ref" / "ref_lagrange"
 
 
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("prec,fric,tang", [("1", "0", "0"), ("1", "0.2", "2e6"), ("2", "0", "0")],
-                         ids=["mgpis-frictionless", "mgpis-coulomb-slip", "diagonal-frictionless"])
-def test_lagrange_matches_reference(gpu, tmp_path, prec, fric, tang):
+@pytest.mark.parametrize("example,prec,fric,tang", [("block", "1", "0", "0"), ("block", "1", "0.2", "2e6"),
+                                                    ("block", "2", "0", "0"), ("cylinder", "1", "0", "0")],
+                         ids=["mgpis-frictionless", "mgpis-coulomb-slip", "diagonal-frictionless", "cylinder-hanging"])
+def test_lagrange_matches_reference(gpu, tmp_path, example, prec, fric, tang):
+    """block: BLOCK as above.  cylinder: the reference's CYLINDER_1 (copyNumb 1, locaLeve 4: four
+    cylinders, locally refined contact bands, 35 % hanging nodes -- integration points whose
+    non-mortar face holds a hanging node are dropped, MCONTACT.h:2870-2893; curved contact search);
+    the reference opens 1028 non-mortar nodes at step 0 and converges after step 1."""
     if not EXE.exists():
         pytest.skip("oracle/_ref/ref_lagrange is built where the reference is (travels with the snapshot)")
-    out = subprocess.run([str(EXE), "1", prec, fric, tang], capture_output=True, text=True, timeout=840, cwd=tmp_path,
+    args = ([example] if example != "block" else []) + ["1", prec, fric, tang]
+    out = subprocess.run([str(EXE), *args], capture_output=True, text=True, timeout=840, cwd=tmp_path,
                          env=dict(os.environ))
     assert out.returncode == 0, out.stderr[-2000:]
     res = json.loads(out.stderr.strip().splitlines()[-1])
     print(res)
     assert res["newton"] == res["newton_ref"], res
     assert res["nodes_equal"] and res["status_equal"], res
-    assert res["lambda_rel"] <= 1e-6 and res["resuDisp_rel"] <= 1e-6, res
+    assert res["lambda_rel"] <= 1e-6, res
+    if example == "block":
+        assert res["resuDisp_rel"] <= 1e-6, res
+    # cylinder: frictionless contact leaves the middle cylinders free to slide, the condensed system
+    # is singular (the coarse solve drops those modes) and the displacements are unique only up to
+    # that rigid motion -- the reference's BiCGSTAB and an exact LU already differ there by 5 %
+    # (tests/test_lagrange.py) -- while the multipliers and the active set are unique
     assert len(res["bicgstab_iters"]) == res["newton"] + 1
-    if fric == "0":  # the patch test: every active node carries the 1e7 load pressure
+    if example == "block" and fric == "0":  # the patch test: every active node carries the 1e7 load pressure
         for itf in res["interfaces"]:
             if itf["fric"] == 0.0 and itf["nodes"]:
                 assert abs(itf["lambda_max"] - 1e7) <= 1e-5 * 1e7, itf
