@@ -136,12 +136,12 @@ __host__ __device__ inline int64_t slot_elem(int ij, int64_t lane) {
 // 3x3 block times x_j, accumulated in fp64; v = slot base + lane.  The matrix is streamed once
 // per launch (NT: non-temporal loads, leaving the caches to the x gathers).
 template <bool NT, typename T>
-__device__ __forceinline__ void block_fma_any(const T* v, const double* xj, double& s0, double& s1, double& s2) {
+__device__ __forceinline__ void block_fma_any(const T* v, const double* xj, double& s0, double& s1, double& s2,
+                                              int lane) {
     const double x0 = xj[0], x1 = xj[1], x2 = xj[2];
     auto ldv = [](const auto* p) { if constexpr (NT) return __builtin_nontemporal_load(p); else return *p; };
     if constexpr (sizeof(T) == 2) {
         // v = slot base + lane in halves; the lane's dword of pair p is at dword 64 p + lane
-        const int lane = threadIdx.x & 63;
         const uint32_t* p = reinterpret_cast<const uint32_t*>(v - lane) + lane;
         const uint32_t a = ldv(p), b = ldv(p + 64), c = ldv(p + 128), d = ldv(p + 192), e = ldv(p + 256);
         const double sc = __builtin_amdgcn_ldexp(1.0, (int)(int16_t)(e >> 16));
@@ -149,7 +149,6 @@ __device__ __forceinline__ void block_fma_any(const T* v, const double* xj, doub
         s1 += sc * (h16_hi(b) * x0 + h16_lo(c) * x1 + h16_hi(c) * x2);
         s2 += sc * (h16_lo(d) * x0 + h16_hi(d) * x1 + h16_lo(e) * x2);
     } else if constexpr (paired_values<T>() && sizeof(T) == 8) {
-        const int lane = threadIdx.x & 63;
         const dbl2_t* p = reinterpret_cast<const dbl2_t*>(v - lane) + lane;
         const dbl2_t a = ldv(p), b = ldv(p + 64), c = ldv(p + 128), d = ldv(p + 192);
         const double v8 = ldv(v + 512);
@@ -166,12 +165,12 @@ __device__ __forceinline__ void block_fma_any(const T* v, const double* xj, doub
 
 template <typename T>
 __device__ __forceinline__ void block_fma(const T* v, const double* xj, double& s0, double& s1, double& s2) {
-    block_fma_any<true>(v, xj, s0, s1, s2);
+    block_fma_any<true>(v, xj, s0, s1, s2, threadIdx.x & 63);
 }
 
 template <typename T>
 __device__ __forceinline__ void block_fma_plain(const T* v, const double* xj, double& s0, double& s1, double& s2) {
-    block_fma_any<false>(v, xj, s0, s1, s2);
+    block_fma_any<false>(v, xj, s0, s1, s2, threadIdx.x & 63);
 }
 
 // Row sums of one chunk, loop variant V (the production kernels use default_variant; the others
@@ -389,6 +388,56 @@ __global__ __launch_bounds__(kBlock) void k_sell(SellArgs a, const double* __res
         if (DOT) dotv = b0 * n0 + b1 * n1 + b2 * n2;
     }
     if (DOT) chunk_partial(dotv, a.partial, c);
+}
+
+// Small levels (fewer chunks than the chip has SIMDs): one workgroup per chunk, each of its four
+// waves 16 of the chunk's rows, each lane a quarter of its row's slots (k = g, g + 4, ...), the
+// quarters summed by lane shuffles -- four times the waves and a quarter of the dependent
+// column -> x chain per lane.  Same operator bytes; y = Kx, residual and Jacobi-sweep epilogues
+// (the V-cycle's small-level launches carry no dot product).
+template <int MODE, bool BJ, typename T, typename CT>
+__global__ __launch_bounds__(kBlock) void k_sell_split(SellArgs a) {
+    const int64_t c = blockIdx.x;
+    const int sub = a.csub[c];
+    if (stopped(a.sc, sub)) return;
+    const int lane = threadIdx.x & 63;
+    const int rin = (threadIdx.x >> 6) * 16 + (lane & 15), g = lane >> 4;
+    const int64_t row = c * kChunk + rin;
+    const int ns = a.slots[c];
+    const int64_t base = a.off[c];
+    constexpr int64_t SV = slot_vals<T>() * kChunk;
+    const T* valp = static_cast<const T*>(a.val) + base * SV + rin;
+    const CT* colp;
+    if constexpr (sizeof(CT) == 2) colp = a.col16 + base * kChunk + rin;
+    else colp = a.col + base * kChunk + rin;
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+#pragma unroll 2
+    for (int k = g; k < ns; k += 4)
+        block_fma_any<true>(valp + (int64_t)k * SV, a.x + 3 * col_of(colp[(int64_t)k * kChunk], row), s0, s1, s2, rin);
+    s0 += __shfl_xor(s0, 16, 64);
+    s1 += __shfl_xor(s1, 16, 64);
+    s2 += __shfl_xor(s2, 16, 64);
+    s0 += __shfl_xor(s0, 32, 64);
+    s1 += __shfl_xor(s1, 32, 64);
+    s2 += __shfl_xor(s2, 32, 64);
+    if (g != 0) return;
+    const int64_t o = 3 * row;
+    if (MODE == kSpmv) {
+        a.y[o] = s0;
+        a.y[o + 1] = s1;
+        a.y[o + 2] = s2;
+    } else if (MODE == kResid) {
+        a.y[o] = a.b[o] - s0;
+        a.y[o + 1] = a.b[o + 1] - s1;
+        a.y[o + 2] = a.b[o + 2] - s2;
+    } else if (MODE == kJac) {
+        const double om = a.coef[2 * sub + 1];
+        double m0, m1, m2;
+        apply_m<BJ>(static_cast<const SmoothInv<T>*>(a.minv), row, a.b[o] - s0, a.b[o + 1] - s1, a.b[o + 2] - s2, m0, m1, m2);
+        a.xo[o] = a.x[o] + om * m0;
+        a.xo[o + 1] = a.x[o + 1] + om * m1;
+        a.xo[o + 2] = a.x[o + 2] + om * m2;
+    }
 }
 
 // Node-parallel kernels: thread = node, 256 nodes per workgroup; a wavefront is one chunk, so
@@ -1872,6 +1921,22 @@ void launch_sell(int vt, const SellArgs& a, hipStream_t s) {
     const int grid = ceil_div(a.nch, 4);
     constexpr int V = default_variant(MODE);
     using I16 = int16_t;
+    // small levels: the row-split kernel (DDPCA_SPLIT_CHUNKS = the largest level it takes, in chunks)
+    static const int64_t split_max = std::getenv("DDPCA_SPLIT_CHUNKS") ? std::atoll(std::getenv("DDPCA_SPLIT_CHUNKS")) : 2048;
+    // (V-cycle modes only: y = Kx keeps the slot order the table mode reproduces bit for bit)
+    if constexpr (!DOT && (MODE == kResid || MODE == kJac)) {
+        if (!a.tab && a.nch <= split_max) {
+            const dim3 gs((unsigned)a.nch);
+            if (a.col16) {
+                if (vt == kValH16) hipLaunchKernelGGL((k_sell_split<MODE, BJ, uint16_t, I16>), gs, dim3(kBlock), 0, s, a);
+                else if (vt == kVal32) hipLaunchKernelGGL((k_sell_split<MODE, BJ, float, I16>), gs, dim3(kBlock), 0, s, a);
+                else hipLaunchKernelGGL((k_sell_split<MODE, BJ, double, I16>), gs, dim3(kBlock), 0, s, a);
+            } else if (vt == kValH16) hipLaunchKernelGGL((k_sell_split<MODE, BJ, uint16_t, int32_t>), gs, dim3(kBlock), 0, s, a);
+            else if (vt == kVal32) hipLaunchKernelGGL((k_sell_split<MODE, BJ, float, int32_t>), gs, dim3(kBlock), 0, s, a);
+            else hipLaunchKernelGGL((k_sell_split<MODE, BJ, double, int32_t>), gs, dim3(kBlock), 0, s, a);
+            return;
+        }
+    }
     if (a.tab) hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, double, V, true>), dim3(grid), dim3(kBlock), 0, s, a, a.tab);
     else if (a.col16) {
         if (vt == kValH16) hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, uint16_t, V, false, I16>), dim3(grid), dim3(kBlock), 0, s, a, a.tab);
