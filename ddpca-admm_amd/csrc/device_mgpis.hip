@@ -592,14 +592,17 @@ __global__ __launch_bounds__(kBlock) void k_prolong_lat(const double* ec, const 
     const uint32_t code = w >> 29;
     const int64_t s0 = pstr[3 * sub], s1 = pstr[3 * sub + 1], s2 = pstr[3 * sub + 2];
     double e0 = 0.0, e1 = 0.0, e2 = 0.0;
+    // every lane issues all eight parent loads (a parent outside the node's subset reads p0 and
+    // weighs 0): no divergent branches, the loads issue back to back (47.8 -> 46.0 us per fine
+    // launch against the branching form, profiles/r02m_prolong_ab.txt)
 #pragma unroll
     for (uint32_t q = 0; q < 8; ++q) {
-        const int64_t c = p0 + ((q & 1) ? s0 : 0) + ((q & 2) ? s1 : 0) + ((q & 4) ? s2 : 0);
-        if ((q & ~code) == 0) {
-            e0 += ec[3 * c];
-            e1 += ec[3 * c + 1];
-            e2 += ec[3 * c + 2];
-        }
+        const bool in = (q & ~code) == 0;
+        const int64_t c = in ? p0 + ((q & 1) ? s0 : 0) + ((q & 2) ? s1 : 0) + ((q & 4) ? s2 : 0) : p0;
+        const double w = in ? 1.0 : 0.0;
+        e0 += w * ec[3 * c];
+        e1 += w * ec[3 * c + 1];
+        e2 += w * ec[3 * c + 2];
     }
     const double wt = 1.0 / (double)(1 << __popc(code));
     const uint8_t m = fmask[i];
