@@ -1376,6 +1376,39 @@ void build_coarse_mg(ddpca_mcontact& H, const MCONTACT& mc, CoarseDev& C) {
     const int64_t Lc = *std::max_element(mc.doleMcsc.begin(), mc.doleMcsc.end());
     auto lev = [&](int64_t tv, int64_t l) { return std::max<int64_t>(0, mc.doleMcsc[tv] - (Lc - l)); };
     std::vector<std::vector<std::vector<int64_t>>> gid(Lc + 1, std::vector<std::vector<int64_t>>(nsub));
+    // LATIN (DOUBLE_M, MCONTACT.h:1538-1670): the coarse contact unknowns of every interface are a
+    // group of their own -- at level Lc the level-doleMcsc nodes coarNode[ts] of contBody[ts][0],
+    // one level down the columns its scalProl rows touch (ficoCotr), comp unknowns per node
+    // (the node's first dof for frictionless contact)
+    const int64_t nint = cs.latin ? (int64_t)mc.searCont.size() : 0;
+    if (cs.latin && (int64_t)cs.coarNode.size() != nint)
+        throw ApiError(DDPCA_EINVAL, "DOUBLE_M for the LATIN coarse space needs the coarse contact nodes (coarNode)");
+    std::vector<std::vector<std::vector<int64_t>>> cset(Lc + 1, std::vector<std::vector<int64_t>>(nint));
+    for (int64_t ts = 0; ts < nint; ++ts) {
+        const int64_t b0 = mc.searCont[ts].body[0];
+        const MULTIGRID& g = mc.multGrid[b0];
+        cset[Lc][ts] = cs.coarNode[ts];
+        for (int64_t l = Lc; l >= 1; --l) {
+            const int64_t fl = mc.doleMcsc[b0] - (Lc - l);  // the group's node level at l
+            if (fl - 1 < 0) {
+                cset[l - 1][ts] = cset[l][ts];
+                continue;
+            }
+            const Stencil& Sp = g.scalProl[fl - 1];
+            if (!Sp.bent.empty()) throw ApiError(DDPCA_EINVAL, "DOUBLE_M coarse solve with rotated-node transfers");
+            std::vector<int64_t> cols;
+            for (int64_t f : cset[l][ts])
+                for (int64_t k = Sp.ptr[f]; k < Sp.ptr[f + 1]; ++k) cols.push_back(Sp.col[k]);
+            std::sort(cols.begin(), cols.end());
+            cols.erase(std::unique(cols.begin(), cols.end()), cols.end());
+            cset[l - 1][ts] = cols;
+            // the hierarchy keeps each level's nodes on the next (MgpisDevice's prefix layout)
+            for (int64_t c : cols)
+                if (!std::binary_search(cset[l][ts].begin(), cset[l][ts].end(), c))
+                    throw ApiError(DDPCA_EINVAL, "DOUBLE_M: a coarse contact node is not a contact node of the finer level");
+        }
+    }
+    std::vector<std::unordered_map<int64_t, int64_t>> cg(nint);  // (interface, node) -> global node
     std::vector<int64_t> nglob(Lc + 1, 0);
     for (int64_t l = 0; l <= Lc; ++l) {
         int64_t cnt = l ? nglob[l - 1] : 0;
@@ -1389,6 +1422,9 @@ void build_coarse_mg(ddpca_mcontact& H, const MCONTACT& mc, CoarseDev& C) {
             }
             for (int64_t j = keep; j < (int64_t)v.size(); ++j) v[j] = cnt++;
         }
+        for (int64_t ts = 0; ts < nint; ++ts)
+            for (int64_t node : cset[l][ts])
+                if (cg[ts].emplace(node, cnt).second) ++cnt;
         nglob[l] = cnt;
     }
     std::vector<Stencil> S(Lc);
@@ -1403,6 +1439,17 @@ void build_coarse_mg(ddpca_mcontact& H, const MCONTACT& mc, CoarseDev& C) {
                 for (int64_t k = Sp.ptr[j]; k < Sp.ptr[j + 1]; ++k)
                     rows[gid[l][tv][j]].push_back({(int32_t)gid[l - 1][tv][Sp.col[k]], Sp.w[k]});
         }
+        for (int64_t ts = 0; ts < nint; ++ts) {  // ficoCotr rows of the nodes new on level l
+            const int64_t b0 = mc.searCont[ts].body[0];
+            const int64_t fl = mc.doleMcsc[b0] - (Lc - l);
+            if (fl - 1 < 0) continue;
+            const Stencil& Sp = mc.multGrid[b0].scalProl[fl - 1];
+            for (int64_t f : cset[l][ts]) {
+                if (std::binary_search(cset[l - 1][ts].begin(), cset[l - 1][ts].end(), f)) continue;  // coarse copy
+                auto& row = rows[cg[ts].at(f)];
+                for (int64_t k = Sp.ptr[f]; k < Sp.ptr[f + 1]; ++k) row.push_back({(int32_t)cg[ts].at(Sp.col[k]), Sp.w[k]});
+            }
+        }
         Stencil& T = S[l - 1];
         T.nf = nglob[l];
         T.nc = nglob[l - 1];
@@ -1415,7 +1462,8 @@ void build_coarse_mg(ddpca_mcontact& H, const MCONTACT& mc, CoarseDev& C) {
             T.ptr.push_back((int64_t)T.col.size());
         }
     }
-    // globCoup_1 rows: subdomain tv's level-doleMcsc free dofs in increasing order (consOper)
+    // globCoup(_1) rows: subdomain tv's level-doleMcsc free dofs in increasing order (consOper),
+    // then (LATIN) every interface's coarse contact unknowns, comp per node
     std::vector<int32_t> fdg(n);
     for (int64_t tv = 0; tv < nsub; ++tv) {
         const MULTIGRID& g = mc.multGrid[tv];
@@ -1424,10 +1472,19 @@ void build_coarse_mg(ddpca_mcontact& H, const MCONTACT& mc, CoarseDev& C) {
             if (g.consFlag[dof]) fdg[r++] = (int32_t)(3 * gid[Lc][tv][dof / 3] + dof % 3);
         if (r != cs.baseReco[tv + 1]) throw ApiError(DDPCA_EINVAL, "DOUBLE_M: baseReco does not match the free dofs");
     }
+    {
+        int64_t r = cs.baseReco[nsub];
+        for (int64_t ts = 0; ts < nint; ++ts) {
+            const int comp = mc.searCont[ts].comp();
+            for (int64_t node : cset[Lc][ts])
+                for (int j = 0; j < comp; ++j) fdg[r++] = (int32_t)(3 * cg[ts].at(node) + j);
+        }
+        if (r != n) throw ApiError(DDPCA_EINVAL, "DOUBLE_M: coarse contact unknowns do not match the coarse rows");
+    }
     std::vector<Bsr3> K(Lc + 1);
     K[Lc] = condensed_to_bsr3(nglob[Lc], n, fdg.data(), cs.globCoup_1.ptr.data(), cs.globCoup_1.col.data(),
                               cs.globCoup_1.val.data());
-    for (int64_t l = Lc - 1; l >= 0; --l) K[l] = galerkin_rap(K[l + 1], S[l]);  // MCONTACT.h:2337-2338
+    for (int64_t l = Lc - 1; l >= 0; --l) K[l] = galerkin_rap(K[l + 1], S[l]);  // MCONTACT.h:2337-2338, 1664-1665
     std::vector<uint8_t> flag(3 * nglob[Lc], 0);
     for (int32_t d : fdg) flag[d] = 1;
     SubdomainOps o;
@@ -1443,7 +1500,7 @@ void build_coarse_mg(ddpca_mcontact& H, const MCONTACT& mc, CoarseDev& C) {
     DDPCA_HIP(hipEventCreateWithFlags(&C.ev_in, hipEventDisableTiming));
     DDPCA_HIP(hipEventCreateWithFlags(&C.ev_out, hipEventDisableTiming));
     if (std::getenv("DDPCA_VERBOSE"))
-        std::fprintf(stderr, "[ddpca] DOUBLE_M coarse solve: %ld rows, %ld levels\n", (long)n, (long)(Lc + 1));
+        std::fprintf(stderr, "[ddpca] DOUBLE_M%s coarse solve: %ld rows, %ld levels\n", cs.latin ? "" : "_1", (long)n, (long)(Lc + 1));
 }
 
 // ---- coarse space: device operands from the host MULTISCALE_1 output
@@ -1518,7 +1575,8 @@ void build_coarse(ddpca_mcontact& H, Problem& P) {
     // the reference solves globCoup_1 directly below DIRE_MAXI = 120000 rows and with its DOUBLE_M_1
     // MGPIS above (PREP.h:69, MCONTACT.h:1857-1865); DDPCA_COARSE_MG_MIN moves the switch (tests)
     const char* mg_env = std::getenv("DDPCA_COARSE_MG_MIN");
-    C.mg = !cs.latin && n >= (mg_env ? std::atoll(mg_env) : 120000);
+    // LATIN: DOUBLE_M (MCONTACT.h:1236) with the host MULTISCALE's coarse contact nodes, one rank
+    C.mg = n >= (mg_env ? std::atoll(mg_env) : 120000) && (!cs.latin || (!cs.rank_local && !cs.coarNode.empty()));
     C.latin = cs.latin;
     if (C.mg) {
         if (H.mg && C.nown) build_coarse_mg(H, mc, C);

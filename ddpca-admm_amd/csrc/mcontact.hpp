@@ -67,6 +67,10 @@ struct CoarseSpace {
     bool latin = false;
     bool rank_local = false;  // latin rows of the coarse contact unknowns hold this rank's share only
     std::vector<std::array<Csr, 2>> globTran_L, globTran_pena_L, globTran_D_L;  // [ts][s]
+    // coarse contact unknowns of interface ts: level-doleMcsc node positions of contBody[ts][0]
+    // (MULTISCALE's coarNode, MCONTACT.h:903-957), comp unknowns each -- DOUBLE_M's hierarchy
+    // coarsens them (empty: not known, e.g. a caller's operators without them)
+    std::vector<std::vector<int64_t>> coarNode;
 };
 
 // prolOper[L-1] ... prolOper[d] of one grid as a single scalar stencil (no masks)

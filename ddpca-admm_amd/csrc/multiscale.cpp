@@ -476,6 +476,7 @@ void MCONTACT::MULTISCALE(const std::vector<uint8_t>* owned) {
     // ---- ficoCotr[ts] (side 0): contact index -> selected level-d nodes (MCONTACT.h:900-959)
     std::vector<Csr> fico(nint);
     std::vector<int64_t> contReco(nint + 1, 0);
+    C.coarNode.assign(nint, {});
     for (int64_t ts = 0; ts < nint; ++ts) {
         const Interface& itf = searCont[ts];
         const Stencil& Q0 = C.accuQ[itf.body[0]];
@@ -493,6 +494,8 @@ void MCONTACT::MULTISCALE(const std::vector<uint8_t>* owned) {
                 for (int j = 0; j < comp; ++j) t.push_back({comp * k + j, comp * newc[Q0.col[q]] + j, Q0.w[q]});
         fico[ts] = from_triplets(comp * (int64_t)nc0t.size(), comp * ncc, t);
         contReco[ts + 1] = contReco[ts] + comp * ncc;
+        for (int64_t c = 0; c < Q0.nc; ++c)
+            if (newc[c] >= 0) C.coarNode[ts].push_back(c);
     }
     const int64_t n = N + contReco[nint];
     C.n = n;

@@ -58,3 +58,34 @@ def test_double_m_reference_torsion(gpu, tmp_path):
     assert abs(res["iters_gpu"] - res["iters_ref"]) <= 1, res
     assert res["resuDisp_rel"] <= 1e-6, res
     assert abs(res["umax_gpu"] - res["umax_ref"]) <= 1e-6 * res["umax_ref"], res
+
+
+@pytest.mark.parametrize("fric", [0.3, 0.0])
+def test_double_m_latin_matches_oracle(ddpca, oracle, gpu, monkeypatch, fric):
+    """DOUBLE_M (MCONTACT.h:1538-1670), the LATIN coarse space's multilevel solve (the reference
+    switches to it at DIRE_MAXI = 120000 rows, 1229-1237, and calls mgpi.CG_SOLV(1) every
+    iteration, 2558-2559): the coarse contact unknowns coarsen with the slave body's scalProl
+    (ficoCotr at every level, 1 unknown per node frictionless, 3 otherwise), the displacement
+    blocks with the subdomains' realProl.  Forced on the synthetic chain (LATIN coarse space at
+    level 1) against the oracle's exact coarse solves: fixed-k trajectory 1e-6, displacements 1e-7."""
+    from test_mcontact_gpu import _oracle_problem, _rows_close
+    monkeypatch.setenv("DDPCA_COARSE_MG_MIN", "1")
+    P = ddpca.Problem("dehw", 2, 2, 2, 1, 2, fric)
+    P.set_coarse(1, [1] * P.nsub)
+    P.ESTABLISH()
+    mc = ddpca.MCONTACT(P)
+    k = 30
+    assert mc.CONTACT_ANALYSIS(k, check=False) == k
+    subs, ifaces = _oracle_problem(P)
+    coarse = dict(latin=True, globCoup=P.csr("globCoup_1"), baseReco=P.array("baseReco"),
+                  doleMcsc=P.array("doleMcsc"),
+                  globTran=[[P.csr("globTran", 2 * ts + s) for s in range(2)] for ts in range(P.nint)],
+                  globTran_pena=[[P.csr("globTran_pena", 2 * ts + s) for s in range(2)] for ts in range(P.nint)],
+                  globTran_D=[[P.csr("globTran_D", 2 * ts + s) for s in range(2)] for ts in range(P.nint)],
+                  accuProl=[P.csr("accuProl", tv) for tv in range(P.nsub)])
+    res = oracle.admm(subs, ifaces, maxit=k, check=False, coarse=coarse)
+    ok, worst = _rows_close(mc.monitor(), res["rows"], k=k, rtol=1e-6)
+    assert ok, worst
+    for tv in range(P.nsub):
+        u, ur = mc.get("resuDisp", tv), res["u"][tv]
+        assert np.linalg.norm(u - ur) <= 1e-7 * np.linalg.norm(ur)
