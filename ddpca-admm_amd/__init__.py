@@ -111,6 +111,7 @@ def _declare(L: C.CDLL) -> None:
     L.ddpca_problem_finalize.argtypes = [_P]
     L.ddpca_problem_set_coarse_operators.argtypes = [_P, C.c_int64, _P, _P, C.POINTER(_CsrArg), _P,
                                                      C.POINTER(_CsrArg), C.POINTER(_CsrArg), C.POINTER(_CsrArg)]
+    L.ddpca_problem_set_coarse_nodes.argtypes = [_P, C.c_int64, C.c_int64, _P]
     L.ddpca_problem_set_coarse_latin.argtypes = [_P, _P, _P, C.POINTER(_CsrArg), C.POINTER(_CsrArg),
                                                  C.POINTER(_CsrArg), C.POINTER(_CsrArg), C.POINTER(_CsrArg)]
     L.mgpis_gpu_create.argtypes = [C.c_int, C.c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P,

@@ -272,6 +272,24 @@ int ddpca_problem_set_coarse_operators(ddpca_problem_t h, int64_t muscSett, cons
     });
 }
 
+int ddpca_problem_set_coarse_nodes(ddpca_problem_t h, int64_t ts, int64_t n, const int64_t* nodes) {
+    return guarded([&] {
+        Problem& P = builder(h);
+        CoarseSpace& C = P.mc.coarse;
+        if (!C.latin) throw ApiError(DDPCA_ESTATE, "set_coarse_nodes after set_coarse_latin");
+        const int64_t nint = (int64_t)P.mc.searCont.size();
+        if (ts < 0 || ts >= nint) throw ApiError(DDPCA_EINVAL, "interface index");
+        if (n < 0 || (n > 0 && !nodes)) throw ApiError(DDPCA_EINVAL, "null argument");
+        const int64_t b0 = P.mc.searCont[ts].body[0];
+        const int64_t lim = P.mc.multGrid[b0].leveCount[P.mc.doleMcsc[b0]];
+        for (int64_t k = 0; k < n; ++k)
+            if (nodes[k] < 0 || nodes[k] >= lim || (k && nodes[k] <= nodes[k - 1]))
+                throw ApiError(DDPCA_EINVAL, "coarse contact nodes: increasing level-doleMcsc positions of the slave body");
+        if ((int64_t)C.coarNode.size() != nint) C.coarNode.assign(nint, {});
+        C.coarNode[ts].assign(nodes, nodes + n);
+    });
+}
+
 int ddpca_problem_set_coarse_latin(ddpca_problem_t h, const int64_t* doleMcsc, const int64_t* baseReco,
                                    const ddpca_csr_t* globCoup, const ddpca_csr_t* globTran,
                                    const ddpca_csr_t* globTran_pena, const ddpca_csr_t* globTran_D,

@@ -310,6 +310,12 @@ int ddpca_problem_set_coarse_latin(ddpca_problem_t p, const int64_t* doleMcsc, c
                                    const ddpca_csr_t* globCoup, const ddpca_csr_t* globTran,
                                    const ddpca_csr_t* globTran_pena, const ddpca_csr_t* globTran_D,
                                    const ddpca_csr_t* accuProl);
+/* The coarse contact unknowns of interface ts of a LATIN coarse space (MULTISCALE's local coarNode,
+ * MCONTACT.h:903-957: the level-doleMcsc positions of contBody[ts][0] whose scalEarl * scalProl
+ * chain reaches a contact node, increasing), after ddpca_problem_set_coarse_latin.  Optional:
+ * with them a coarse problem of DIRE_MAXI = 120000 rows or more is solved by DOUBLE_M's MGPIS
+ * (MCONTACT.h:1538-1670, 2558-2559) as the reference does; without them only the dense solve. */
+int ddpca_problem_set_coarse_nodes(ddpca_problem_t p, int64_t ts, int64_t n, const int64_t* nodes);
 /* Check that every subdomain and interface was set; mark the problem established. */
 int ddpca_problem_finalize(ddpca_problem_t p);
 

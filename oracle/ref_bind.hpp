@@ -217,6 +217,20 @@ inline ddpca_problem_t from_reference(MCONTACT& mc) {
         for (const auto& o : ap) va.push_back(o.view());
         const ddpca_csr_t vc = gc.view();
         check(ddpca_problem_set_coarse_latin(p, dole.data(), base.data(), &vc, vt.data(), vp.data(), vd.data(), va.data()));
+        // MULTISCALE's coarNode (a local there, MCONTACT.h:903-957): the level-doleMcsc positions
+        // of the slave body that scalEarl * scalProl[maxiLeve..doleMcsc] reaches from a contact node
+        for (int64_t ts = 0; ts < nint; ++ts) {
+            const MULTIGRID& g = mc.multGrid[mc.contBody[ts][0]];
+            SpMat F = g.scalEarl;
+            for (long l = g.mgpi.maxiLeve; l >= mc.doleMcsc[mc.contBody[ts][0]]; --l) F = SpMat(F * g.scalProl[l]);
+            std::vector<char> used(F.cols(), 0);
+            for (const auto& nc : mc.nodeCont[ts][0])
+                for (SpMat::InnerIterator it(F, nc.first); it; ++it) used[it.col()] = 1;
+            std::vector<int64_t> nodes;
+            for (int64_t c = 0; c < (int64_t)used.size(); ++c)
+                if (used[c]) nodes.push_back(c);
+            check(ddpca_problem_set_coarse_nodes(p, ts, (int64_t)nodes.size(), nodes.data()));
+        }
     }
     check(ddpca_problem_finalize(p));
     return p;

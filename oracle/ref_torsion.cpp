@@ -10,7 +10,8 @@
 // dole = -1: doleMcsc = the fine level of every subdomain, so globCoup_1 has every free dof
 // (126,750 rows at globHomo 2 >= DIRE_MAXI) and the reference solves it with its DOUBLE_M_1 MGPIS
 // (MCONTACT.h:1857-1865, 2303-2341, 2593-2594) -- as the device does above that size.
-//   ref_torsion globHomo [dole]
+// musc = 1: the LATIN coarse space instead (globCoup, DOUBLE_M past the same row count).
+//   ref_torsion globHomo [dole] [musc]
 #include <unistd.h>
 
 #include <cmath>
@@ -22,6 +23,7 @@
 int main(int argc, char** argv) {
     const long gh = argc > 1 ? std::atol(argv[1]) : 2;
     const long dole = argc > 2 ? std::atol(argv[2]) : 1;
+    const long musc = argc > 3 ? std::atol(argv[3]) : 2;
     const int saved = dup(1);
     if (!std::freopen("/dev/null", "w", stdout)) return 2;  // the reference's progress output
     TORSION t(1);
@@ -31,6 +33,7 @@ int main(int argc, char** argv) {
     t.ESTA_SURF();
     t.MESH_DD();
     if (dole < 0) t.doleMcsc.assign(4, t.multGrid[0].mgpi.maxiLeve);
+    t.muscSett = musc;
     t.SOLVE_DD(1);  // ESTABLISH + the reference's CONTACT_ANALYSIS
     std::fflush(stdout);
     dup2(saved, 1);
@@ -57,7 +60,7 @@ int main(int argc, char** argv) {
     std::fprintf(stderr,
                  "{\"iters_gpu\": %ld, \"iters_ref\": %ld, \"umax_gpu\": %.12g, \"umax_ref\": %.12g, "
                  "\"analytic\": 1.159111630361142e-06, \"resuDisp_rel\": %.3g, \"coarse_rows\": %ld, \"dofs\": %ld}\n",
-                 (long)n_gpu, (long)t.iterNumbReco, umax_gpu, umax_ref, du, (long)t.globCoup_1.rows(),
+                 (long)n_gpu, (long)t.iterNumbReco, umax_gpu, umax_ref, du, (long)(musc == 1 ? t.globCoup.rows() : t.globCoup_1.rows()),
                  (long)[&] { long n = 0; for (auto& g : t.multGrid) n += g.mgpi.consStif[g.mgpi.maxiLeve].rows(); return n; }());
     return 0;
 }

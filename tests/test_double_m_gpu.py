@@ -89,3 +89,23 @@ def test_double_m_latin_matches_oracle(ddpca, oracle, gpu, monkeypatch, fric):
     for tv in range(P.nsub):
         u, ur = mc.get("resuDisp", tv), res["u"][tv]
         assert np.linalg.norm(u - ur) <= 1e-7 * np.linalg.norm(ur)
+
+
+@pytest.mark.timeout(700)
+def test_double_m_latin_reference_torsion(gpu, tmp_path):
+    """The reference's TORSION with the LATIN coarse space (muscSett 1) at the fine level: globCoup
+    has 130,680 rows (126,750 displacement dofs + the coarse contact unknowns), the reference
+    builds DOUBLE_M and solves it with mgpi.CG_SOLV(1) every iteration; oracle/ref_bind.hpp hands
+    over the MULTISCALE output with its coarNode (ddpca_problem_set_coarse_nodes) and the device
+    takes its DOUBLE_M MGPIS at the same switch.  Measured: 11 vs 10 iterations, resuDisp 4.9e-13."""
+    exe = Path(__file__).resolve().parents[1] / "oracle" / "_ref" / "ref_torsion"
+    if not exe.exists():
+        pytest.skip("oracle/_ref/ref_torsion is built only where the reference is (travels with the snapshot)")
+    env = {k: v for k, v in os.environ.items() if k != "DDPCA_COARSE_MG_MIN"}
+    out = subprocess.run([str(exe), "2", "-1", "1"], capture_output=True, text=True, timeout=640, env=env, cwd=tmp_path)
+    assert out.returncode == 0, out.stderr[-2000:]
+    res = json.loads(out.stderr.strip().splitlines()[-1])
+    assert res["coarse_rows"] >= 120000, res
+    assert abs(res["iters_gpu"] - res["iters_ref"]) <= 1, res
+    assert res["resuDisp_rel"] <= 1e-6, res
+    assert abs(res["umax_gpu"] - res["umax_ref"]) <= 1e-6 * res["umax_ref"], res
