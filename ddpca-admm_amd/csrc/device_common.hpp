@@ -107,5 +107,8 @@ struct MirrorBuf {
 // about one replay queued ahead of the slowest unfinished solve.  `launched` = iterations
 // already enqueued (eager + pre-enqueued replays).  Returns the number of replays launched.
 int64_t pace_until_done(hipStream_t stream, hipGraphExec_t graph, const MirrorBuf& m, int64_t k, int64_t launched);
+// the same for a batch split into two halves (half[s] = 0 or 1), each half's graph on its stream
+int64_t pace_halves(hipStream_t st[2], hipGraphExec_t g[2], const MirrorBuf& m, const std::vector<int>& half, int64_t k,
+                    int64_t launched0);
 
 }  // namespace ddpca

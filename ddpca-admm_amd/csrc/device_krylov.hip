@@ -12,6 +12,8 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 #include "device_mgpis.hpp"
@@ -246,6 +248,7 @@ int64_t krylov_bicgstab(MgpisDevice& D, int prec, const double* b, double* x, do
     double rho[2] = {0.0, 0.0}, alph = 0.0, omeg = 0.0;
     int64_t it = 0;
     if (breakdown) *breakdown = 0;
+    static const bool trace = std::getenv("DDPCA_KRYLOV_TRACE") != nullptr;  // per-iteration scalars on stderr
     while (it < maxit && std::sqrt(rr) > tol) {
         double& rc = rho[(it + 1) % 2];
         rc = rhr;
@@ -261,7 +264,11 @@ int64_t krylov_bicgstab(MgpisDevice& D, int prec, const double* b, double* x, do
         }
         w.precond(prec, p, ph);
         w.spmv(ph, v);
-        alph = rc / w.dots({{rh, v}})[0];
+        const double rhv = w.dots({{rh, v}})[0];
+        alph = rc / rhv;
+        if (trace)
+            std::fprintf(stderr, "[ddpca bicgstab] it %lld  |r|/|b| %.3e  rho %.3e  rh.v %.3e  alpha %.3e  omega %.3e\n",
+                         (long long)it, std::sqrt(rr) / bn, rc, rhv, alph, omeg);
         check_finite(alph, "alpha (BiCGSTAB)");
         w.xpay(r, -alph, v, s);
         w.precond(prec, s, sh);

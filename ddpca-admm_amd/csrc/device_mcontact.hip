@@ -618,6 +618,27 @@ struct SellOp {
     }
 };
 
+// DDPCA_STREAMS=1: the batched PCG and the mass CG on one stream each (A/B runs); default two
+bool two_streams() {
+    const char* v = std::getenv("DDPCA_STREAMS");
+    return !(v && v[0] == '1');
+}
+
+// scs[h][i] = sc[i] with done forced on the other half's systems / sc[i] = its half's copy
+__global__ void k_scal_split(const PcgScal* sc, PcgScal* scs, const int32_t* half, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    for (int h = 0; h < 2; ++h) {
+        PcgScal v = sc[i];
+        if (half[i] != h) v.done = 1;
+        scs[h * n + i] = v;
+    }
+}
+__global__ void k_scal_merge(PcgScal* sc, const PcgScal* scs, const int32_t* half, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) sc[i] = scs[half[i] * n + i];
+}
+
 // Batched surface-mass solver: one graph of `k` CG iterations over every system, replayed
 // until every system reports done through the host-mapped mirror.
 class MassBatch {
@@ -677,6 +698,7 @@ public:
         val.upload(va);
         dinv.upload(di);
         cb.upload(c0);
+        cb_host_ = c0;
         for (auto* v : {&b, &x, &r, &z, &p, &q}) {
             v->alloc(std::max<int64_t>(nrow, 2));
             v->zero();
@@ -687,7 +709,13 @@ public:
         mirror.alloc(nsys);
     }
     ~MassBatch() {
-        if (graph_) (void)hipGraphExecDestroy(graph_);
+        if (s2_) (void)hipStreamSynchronize(s2_);
+        if (graph_ && !split_) (void)hipGraphExecDestroy(graph_);
+        for (auto& g : graph_h_)
+            if (g) (void)hipGraphExecDestroy(g);
+        if (ev_fork_) (void)hipEventDestroy(ev_fork_);
+        if (ev_join_) (void)hipEventDestroy(ev_join_);
+        if (s2_) (void)hipStreamDestroy(s2_);
         if (sc_host) (void)hipHostFree(sc_host);
     }
 
@@ -695,7 +723,13 @@ public:
     void solve(hipStream_t s, double* x_out, double rtol, int64_t maxit) {
         if (nsys == 0) return;
         if (x_out != x_target_) {
-            if (graph_) (void)hipGraphExecDestroy(graph_);
+            if (split_) {
+                for (auto& g : graph_h_)
+                    if (g) (void)hipGraphExecDestroy(g);
+                graph_h_[0] = graph_h_[1] = nullptr;
+            } else if (graph_) {
+                (void)hipGraphExecDestroy(graph_);
+            }
             graph_ = nullptr;
             x_target_ = x_out;
         }
@@ -710,7 +744,55 @@ public:
         hipLaunchKernelGGL(k_mcg_init, dim3(nb256(nrow)), dim3(256), 0, s, b.p, dinv.p, x_out, r.p, z.p, p.p, q.p,
                            partial.p, nrow);
         hipLaunchKernelGGL(k_mcg_fin, dim3(nsys), dim3(256), 0, s, (int)kMcgInit, partial.p, cb.p, sc.p, mirror.dev);
+        if (split_) {
+            // fork into the two halves' streams, pace both, join and merge the scalars back
+            hipLaunchKernelGGL(k_scal_split, dim3(ceil_div(nsys, 64)), dim3(64), 0, s, sc.p, sc_half_.p, half_.p, nsys);
+            DDPCA_HIP(hipEventRecord(ev_fork_, s));
+            DDPCA_HIP(hipStreamWaitEvent(s2_, ev_fork_, 0));
+            hipStream_t st[2] = {s, s2_};
+            pace_halves(st, graph_h_, mirror, half_host_, k, 0);
+            DDPCA_HIP(hipEventRecord(ev_join_, s2_));
+            DDPCA_HIP(hipStreamWaitEvent(s, ev_join_, 0));
+            hipLaunchKernelGGL(k_scal_merge, dim3(ceil_div(nsys, 64)), dim3(64), 0, s, sc.p, sc_half_.p, half_.p, nsys);
+            return;
+        }
         pace_until_done(s, graph_, mirror, k, 0);
+    }
+
+    // Two-stream split of the systems (as MgpisDevice::set_split): two halves of equal rows, each
+    // half's CG iterations a graph of its own on its own stream, on a copy of the scalars where
+    // the other half's systems are done -- the latency-bound launches of the two halves overlap.
+    void set_split(bool on) {
+        on = on && nsys >= 2;
+        if (on && !s2_) {
+            DDPCA_HIP(hipStreamCreateWithFlags(&s2_, hipStreamNonBlocking));
+            DDPCA_HIP(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
+            DDPCA_HIP(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
+            sc_half_.alloc(2 * nsys);
+            std::vector<int64_t> rows(nsys);
+            std::vector<int> ord(nsys);
+            for (int i = 0; i < nsys; ++i) {
+                rows[i] = cb_host_[i + 1] - cb_host_[i];
+                ord[i] = i;
+            }
+            std::stable_sort(ord.begin(), ord.end(), [&](int a, int c) { return rows[a] > rows[c]; });
+            half_host_.assign(nsys, 0);
+            int64_t w[2] = {0, 0};
+            for (int i : ord) {
+                const int h = w[1] < w[0] ? 1 : 0;
+                half_host_[i] = h;
+                w[h] += rows[i];
+            }
+            half_.upload(half_host_);
+        }
+        if (on != split_) {
+            for (auto& g : graph_h_)
+                if (g) (void)hipGraphExecDestroy(g);
+            graph_h_[0] = graph_h_[1] = nullptr;
+            if (graph_ && !split_) (void)hipGraphExecDestroy(graph_);
+            graph_ = nullptr;
+        }
+        split_ = on;
     }
 
     // after the stream synchronised: iterations of the last solve, breakdown check
@@ -724,20 +806,37 @@ public:
 
 private:
     hipGraphExec_t graph_ = nullptr;
+    hipGraphExec_t graph_h_[2] = {nullptr, nullptr};
     double* x_target_ = nullptr;
+    bool split_ = false;
+    hipStream_t s2_ = nullptr;
+    hipEvent_t ev_fork_ = nullptr, ev_join_ = nullptr;
+    DevBuf<PcgScal> sc_half_;
+    DevBuf<int32_t> half_;
+    std::vector<int> half_host_;
+    std::vector<int64_t> cb_host_;
     void capture(hipStream_t s) {
+        if (split_) {
+            capture_one(s, sc_half_.p, &graph_h_[0]);
+            capture_one(s, sc_half_.p + nsys, &graph_h_[1]);
+            graph_ = graph_h_[0];  // marks the capture done (destroyed through graph_h_)
+            return;
+        }
+        capture_one(s, sc.p, &graph_);
+    }
+    void capture_one(hipStream_t s, PcgScal* scp, hipGraphExec_t* out) {
         EllArgs e{slots.p, off.p, col.p, val.p, csys.p, dinv.p, nch};
         hipGraph_t g;
         DDPCA_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
         for (int64_t it = 0; it < k; ++it) {
-            hipLaunchKernelGGL(k_mcg_spmv, dim3(ceil_div(nch, 4)), dim3(256), 0, s, e, sc.p, z.p, q.p, p.p, partial.p);
-            hipLaunchKernelGGL(k_mcg_fin, dim3(nsys), dim3(256), 0, s, (int)kMcgAlpha, partial.p, cb.p, sc.p, mirror.dev);
-            hipLaunchKernelGGL(k_mcg_axpy, dim3(nb256(nrow)), dim3(256), 0, s, e, sc.p, x_target_, r.p, z.p, p.p, q.p,
+            hipLaunchKernelGGL(k_mcg_spmv, dim3(ceil_div(nch, 4)), dim3(256), 0, s, e, scp, z.p, q.p, p.p, partial.p);
+            hipLaunchKernelGGL(k_mcg_fin, dim3(nsys), dim3(256), 0, s, (int)kMcgAlpha, partial.p, cb.p, scp, mirror.dev);
+            hipLaunchKernelGGL(k_mcg_axpy, dim3(nb256(nrow)), dim3(256), 0, s, e, scp, x_target_, r.p, z.p, p.p, q.p,
                                partial.p);
-            hipLaunchKernelGGL(k_mcg_fin, dim3(nsys), dim3(256), 0, s, (int)kMcgBeta, partial.p, cb.p, sc.p, mirror.dev);
+            hipLaunchKernelGGL(k_mcg_fin, dim3(nsys), dim3(256), 0, s, (int)kMcgBeta, partial.p, cb.p, scp, mirror.dev);
         }
         DDPCA_HIP(hipStreamEndCapture(s, &g));
-        DDPCA_HIP(hipGraphInstantiate(&graph_, g, nullptr, nullptr, 0));
+        DDPCA_HIP(hipGraphInstantiate(out, g, nullptr, nullptr, 0));
         DDPCA_HIP(hipGraphDestroy(g));
     }
 };
@@ -1013,6 +1112,9 @@ void build(ddpca_mcontact& H, Problem& P) {
     if (!ops.empty()) {
         H.mg = std::make_unique<MgpisDevice>(H.device, ops, H.opt);
         H.main = H.mg->stream;
+        // the body balance's batch on two streams (MgpisDevice::set_split); DDPCA_STREAMS=1 keeps
+        // the single-stream graph for A/B runs
+        H.mg->set_split(two_streams());
     } else {
         DDPCA_HIP(hipStreamCreateWithFlags(&H.main, hipStreamNonBlocking));
     }
@@ -1222,6 +1324,8 @@ void build(ddpca_mcontact& H, Problem& P) {
         }
         H.mb_aux.build(Ma, ro, H.R);
         H.mb_lam.build(Ml, ro, H.R);
+        H.mb_aux.set_split(two_streams());
+        H.mb_lam.set_split(two_streams());
         // fused update when the penalty operators are exact multiples of the plain ones
         // (entries agree to rounding: the penalty operators are accumulated with pen inside the
         // basis products, e.g. off-diagonal T^T P T entries are rounding noise around 0)
@@ -1269,6 +1373,7 @@ void build(ddpca_mcontact& H, Problem& P) {
             }
             H.op_wv.build(rwv);
             H.mb_wv.build(M2, ro2, 2 * H.R);
+            H.mb_wv.set_split(two_streams());
             H.rinv.upload(ri);
         }
         if (std::getenv("DDPCA_VERBOSE"))

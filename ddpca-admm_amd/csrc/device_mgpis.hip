@@ -1837,8 +1837,15 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
 MgpisDevice::~MgpisDevice() {
     (void)hipSetDevice(device);
     if (stream) (void)hipStreamSynchronize(stream);
+    if (stream2_) (void)hipStreamSynchronize(stream2_);
     for (auto& g : graph_)
         if (g) (void)hipGraphExecDestroy(g);
+    for (auto& gp : graph_h_)
+        for (auto& g : gp)
+            if (g) (void)hipGraphExecDestroy(g);
+    if (ev_fork_) (void)hipEventDestroy(ev_fork_);
+    if (ev_join_) (void)hipEventDestroy(ev_join_);
+    if (stream2_) (void)hipStreamDestroy(stream2_);
     if (sc_host) (void)hipHostFree(sc_host);
     if (ev_k0) (void)hipEventDestroy(ev_k0);
     if (ev_k1) (void)hipEventDestroy(ev_k1);
@@ -2117,7 +2124,7 @@ void MgpisDevice::vcycle(const double* rin, double* zout, bool dot) {
     const bool bj = opt.smoother >= 1;
     const bool cheb = opt.smoother == 2;
     const int nu = opt.nu;
-    const PcgScal* scp = sc.p;
+    const PcgScal* scp = sc_cur_ ? sc_cur_ : sc.p;
     const int cl = clev;  // the exact dense solve; levels below it are not visited
     if (Lf == cl) {
         if (ainv32.p) hipLaunchKernelGGL(k_coarse<float>, dim3(ceil_div(3 * lev[cl].nn, 4)), dim3(kBlock), 0, stream, ainv32.p, aoff.p, c_noff.p,
@@ -2265,26 +2272,32 @@ double MgpisDevice::fine_kernel_bytes(int s) const {
 
 void MgpisDevice::enqueue_iteration(int prec, bool timed) {
     LevelDev& L = lev.back();
+    PcgScal* scp = sc_cur_ ? sc_cur_ : sc.p;
     SellArgs a = level_args(L);
     a.x = zs.p;
     a.y = qs.p;
     a.p = ps.p;
-    a.sc = sc.p;
+    a.sc = scp;
     a.partial = partial.p;
     const int nblk = ceil_div(L.nn, kBlock);
     if (timed) DDPCA_HIP(hipEventRecord(ev_k0, stream));
     launch_sell<kPcg, false, true>(kVal64, a, stream);
     if (timed) DDPCA_HIP(hipEventRecord(ev_k1, stream));
-    hipLaunchKernelGGL(k_fin, dim3(nsub), dim3(kFinT), 0, stream, (int)kFinAlpha, partial.p, nullptr, fin_cb.p, sc.p, mirror.dev);
-    hipLaunchKernelGGL(k_axpy, dim3(nblk), dim3(kBlock), 0, stream, xs.p, rs.p, ps.p, qs.p, sc.p, partial.p, L.nn, L.csub.p);
-    hipLaunchKernelGGL(k_fin, dim3(nsub), dim3(kFinT), 0, stream, (int)kFinRR, partial.p, nullptr, fin_cb.p, sc.p, mirror.dev);
+    hipLaunchKernelGGL(k_fin, dim3(nsub), dim3(kFinT), 0, stream, (int)kFinAlpha, partial.p, nullptr, fin_cb.p, scp, mirror.dev);
+    hipLaunchKernelGGL(k_axpy, dim3(nblk), dim3(kBlock), 0, stream, xs.p, rs.p, ps.p, qs.p, scp, partial.p, L.nn, L.csub.p);
+    hipLaunchKernelGGL(k_fin, dim3(nsub), dim3(kFinT), 0, stream, (int)kFinRR, partial.p, nullptr, fin_cb.p, scp, mirror.dev);
     if (prec == 1) vcycle(rs.p, zs.p, true);
-    else hipLaunchKernelGGL(k_diag, dim3(nblk), dim3(kBlock), 0, stream, rs.p, L.dinv.p, zs.p, partial.p, L.nn, L.csub.p, sc.p);
-    hipLaunchKernelGGL(k_fin, dim3(nsub), dim3(kFinT), 0, stream, (int)kFinBeta, partial.p, nullptr, fin_cb.p, sc.p, mirror.dev);
+    else hipLaunchKernelGGL(k_diag, dim3(nblk), dim3(kBlock), 0, stream, rs.p, L.dinv.p, zs.p, partial.p, L.nn, L.csub.p, scp);
+    hipLaunchKernelGGL(k_fin, dim3(nsub), dim3(kFinT), 0, stream, (int)kFinBeta, partial.p, nullptr, fin_cb.p, scp, mirror.dev);
 }
 
 // graph_[prec]: iters_per_graph PCG iterations captured once and replayed.
 void MgpisDevice::build_graph(int prec) {
+    if (split_) {
+        build_half_graph(prec, 0);
+        build_half_graph(prec, 1);
+        return;
+    }
     if (graph_[prec]) return;
     hipGraph_t g;
     DDPCA_HIP(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
@@ -2292,6 +2305,111 @@ void MgpisDevice::build_graph(int prec) {
     DDPCA_HIP(hipStreamEndCapture(stream, &g));
     DDPCA_HIP(hipGraphInstantiate(&graph_[prec], g, nullptr, nullptr, 0));
     DDPCA_HIP(hipGraphDestroy(g));
+}
+
+// the same iterations bound to half h's copy of the scalars (captured on `stream`, replayed on
+// the half's own stream)
+void MgpisDevice::build_half_graph(int prec, int h) {
+    if (graph_h_[prec][h]) return;
+    sc_cur_ = sc_half_.p + (int64_t)h * nsub;
+    hipGraph_t g;
+    DDPCA_HIP(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
+    for (int k = 0; k < opt.iters_per_graph; ++k) enqueue_iteration(prec, false);
+    DDPCA_HIP(hipStreamEndCapture(stream, &g));
+    sc_cur_ = nullptr;
+    DDPCA_HIP(hipGraphInstantiate(&graph_h_[prec][h], g, nullptr, nullptr, 0));
+    DDPCA_HIP(hipGraphDestroy(g));
+}
+
+// scs[h][s] = sc[s], with done forced on the members of the other half
+__global__ void k_split_sc(const PcgScal* sc, PcgScal* scs, const int32_t* half, int nsub) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= nsub) return;
+    for (int h = 0; h < 2; ++h) {
+        PcgScal v = sc[s];
+        if (half[s] != h) v.done = 1;
+        scs[h * nsub + s] = v;
+    }
+}
+
+// sc[s] = the copy of the half that ran member s
+__global__ void k_merge_sc(PcgScal* sc, const PcgScal* scs, const int32_t* half, int nsub) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s < nsub) sc[s] = scs[half[s] * nsub + s];
+}
+
+void MgpisDevice::set_split(bool on) {
+    select_device(device);
+    on = on && nsub >= 2 && !no_coarse;
+    if (on == split_) return;
+    DDPCA_HIP(hipStreamSynchronize(stream));
+    if (on && !stream2_) {
+        DDPCA_HIP(hipStreamCreateWithFlags(&stream2_, hipStreamNonBlocking));
+        DDPCA_HIP(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
+        DDPCA_HIP(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
+        sc_half_.alloc(2 * nsub);
+        // deal the members into two halves of equal fine-level work (largest first)
+        std::vector<int> ord(nsub);
+        for (int s = 0; s < nsub; ++s) ord[s] = s;
+        std::stable_sort(ord.begin(), ord.end(), [&](int x, int y) { return lev.back().nnzb_sub[x] > lev.back().nnzb_sub[y]; });
+        half_host_.assign(nsub, 0);
+        double w[2] = {0.0, 0.0};
+        for (int s : ord) {
+            const int h = w[1] < w[0] ? 1 : 0;
+            half_host_[s] = h;
+            w[h] += (double)lev.back().nnzb_sub[s];
+        }
+        half_.upload(half_host_);
+    }
+    split_ = on;
+}
+
+// Host pacing of the two halves' replays (pace_until_done per half, one loop): a half gets its
+// next replay when its slowest member has entered the last one enqueued for it.
+int64_t pace_halves(hipStream_t st[2], hipGraphExec_t g[2], const MirrorBuf& m, const std::vector<int>& half, int64_t k,
+                    int64_t launched0) {
+    int64_t launched[2] = {launched0, launched0}, replays = 0;
+    for (int64_t spin = 0;; ++spin) {
+        bool all = true;
+        int64_t slowest[2] = {INT64_MAX, INT64_MAX};
+        bool busy[2] = {false, false};
+        for (int s = 0; s < m.n; ++s) {
+            if (__atomic_load_n(&m.host[s].done, __ATOMIC_ACQUIRE)) continue;
+            all = false;
+            busy[half[s]] = true;
+            slowest[half[s]] = std::min<int64_t>(slowest[half[s]], __atomic_load_n(&m.host[s].iter, __ATOMIC_RELAXED));
+        }
+        if (all) return replays;
+        bool launched_now = false;
+        for (int h = 0; h < 2; ++h)
+            if (busy[h] && launched[h] - slowest[h] <= k) {
+                DDPCA_HIP(hipGraphLaunch(g[h], st[h]));
+                launched[h] += k;
+                ++replays;
+                launched_now = true;
+            }
+        if (launched_now) continue;
+        if ((spin & 255) == 255) {
+            for (int h = 0; h < 2; ++h) {
+                if (!busy[h]) continue;
+                const hipError_t q = hipStreamQuery(st[h]);
+                if (q == hipSuccess) {
+                    // this half's stream drained: its mirror entries are final for what it ran
+                    bool done_now = true;
+                    for (int s = 0; s < m.n; ++s)
+                        if (half[s] == h) done_now &= __atomic_load_n(&m.host[s].done, __ATOMIC_ACQUIRE) != 0;
+                    if (!done_now) {
+                        DDPCA_HIP(hipGraphLaunch(g[h], st[h]));
+                        launched[h] += k;
+                        ++replays;
+                    }
+                } else if (q != hipErrorNotReady) {
+                    DDPCA_HIP(q);
+                }
+            }
+        }
+        std::this_thread::yield();
+    }
 }
 
 void MgpisDevice::pcg_begin(int prec, double rtol, const std::vector<int64_t>& maxit, bool warm) {
@@ -2332,9 +2450,21 @@ void MgpisDevice::pcg_begin(int prec, double rtol, const std::vector<int64_t>& m
         enqueue_iteration(prec, true);
         sample_pending_ = true;
     }
+    if (split_) {
+        // fork: each half continues on its own stream from its own copy of the scalars
+        hipLaunchKernelGGL(k_split_sc, dim3(ceil_div(nsub, 64)), dim3(64), 0, stream, sc.p, sc_half_.p, half_.p, nsub);
+        DDPCA_HIP(hipEventRecord(ev_fork_, stream));
+        DDPCA_HIP(hipStreamWaitEvent(stream2_, ev_fork_, 0));
+    }
 }
 
 void MgpisDevice::pcg_step(int prec) {
+    if (split_) {
+        DDPCA_HIP(hipGraphLaunch(graph_h_[prec][0], stream));
+        DDPCA_HIP(hipGraphLaunch(graph_h_[prec][1], stream2_));
+        graphs_launched += 2;
+        return;
+    }
     DDPCA_HIP(hipGraphLaunch(graph_[prec], stream));
     ++graphs_launched;
 }
@@ -2342,6 +2472,16 @@ void MgpisDevice::pcg_step(int prec) {
 void MgpisDevice::pcg_wait(int prec, int64_t pre_enqueued) {
     const int64_t k = opt.iters_per_graph;
     const int64_t launched = (sample_pending_ ? 1 : 0) + pre_enqueued * k;
+    if (split_) {
+        hipStream_t st[2] = {stream, stream2_};
+        hipGraphExec_t g[2] = {graph_h_[prec][0], graph_h_[prec][1]};
+        graphs_launched += pace_halves(st, g, mirror, half_host_, k, launched);
+        // join: `stream` continues after the second half's replays; the scalars merge back
+        DDPCA_HIP(hipEventRecord(ev_join_, stream2_));
+        DDPCA_HIP(hipStreamWaitEvent(stream, ev_join_, 0));
+        hipLaunchKernelGGL(k_merge_sc, dim3(ceil_div(nsub, 64)), dim3(64), 0, stream, sc.p, sc_half_.p, half_.p, nsub);
+        return;
+    }
     graphs_launched += pace_until_done(stream, graph_[prec], mirror, k, launched);
 }
 

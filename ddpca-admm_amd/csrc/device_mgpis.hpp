@@ -213,8 +213,28 @@ public:
     double bench_spmv(int variant, int reps);  // ms per launch of a fine-level SpMV loop variant
     int64_t graphs_launched = 0;
 
+    // Two-stream split of the batch (set_split before the first solve): the members are dealt
+    // into two halves of equal fine work, each half's PCG iterations are a graph of their own
+    // replayed on its own stream, so one half's latency-bound coarse levels and kernel
+    // boundaries overlap the other half's fine-level streaming.  Each half runs on its own copy
+    // of the scalars in which the other half's members are marked done (the kernels already skip
+    // done members), so the two graphs touch disjoint chunks; pcg_wait joins the streams and
+    // merges the copies back into `sc`.  Setup and the eagerly timed first iteration stay on
+    // `stream` over the whole batch.
+    void set_split(bool on);
+    bool split() const { return split_; }
+
 private:
     hipGraphExec_t graph_[2] = {nullptr, nullptr};
+    hipGraphExec_t graph_h_[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};  // [prec][half]
+    bool split_ = false;
+    hipStream_t stream2_ = nullptr;
+    hipEvent_t ev_fork_ = nullptr, ev_join_ = nullptr;
+    DevBuf<PcgScal> sc_half_;   // 2 x nsub: the scalars each half's graph runs on
+    DevBuf<int32_t> half_;      // per member: its half
+    std::vector<int> half_host_;
+    PcgScal* sc_cur_ = nullptr; // the scalars enqueue_iteration / vcycle bind (sc, or a half's copy)
+    void build_half_graph(int prec, int h);
     bool sample_pending_ = false;
     void build_graph(int prec);
     void enqueue_iteration(int prec, bool timed);

@@ -103,3 +103,25 @@ def test_headline_fullsize_batched_solves_match_oracle(ddpca, oracle, gpu):
         err = np.linalg.norm(x - xo) / np.linalg.norm(xo)
         print(f"subdomain {tv}: device {its[tv]} PCG its (oracle SGS {ito}), rel err {err:.2e}")
         assert err <= 1e-8, (tv, err)
+
+
+def test_split_streams_reproduce_single_stream(ddpca, gpu, monkeypatch):
+    """The two-stream split of the body-balance batch (MgpisDevice::set_split, the default) runs
+    the same kernels on the same data per subdomain, only on two streams: the ADMM trajectory,
+    displacements and PCG iteration counts must equal the single-stream graph's bit for bit."""
+    H, M = ddpca.HEADLINE_OPTIONS, ddpca.HEADLINE_MUSC
+    out = {}
+    for streams in ("1", "2"):
+        monkeypatch.setenv("DDPCA_STREAMS", streams)
+        P = ddpca.Problem("dehw", 4, 3, 2, 2, 3, 0.2)
+        P.set_coarse(M["muscSett"], [M["doleMcsc"]] * P.nsub)
+        P.ESTABLISH()
+        mc = ddpca.MCONTACT(P, **H)
+        assert mc.CONTACT_ANALYSIS(8, check=False) == 8
+        out[streams] = (mc.monitor().copy(), [mc.get("resuDisp", tv).copy() for tv in range(P.nsub)],
+                         np.array(mc.get("pcg_iters")).copy())
+        del mc
+    assert np.array_equal(out["1"][0], out["2"][0])
+    for a, b in zip(out["1"][1], out["2"][1]):
+        assert np.array_equal(a, b)
+    assert np.array_equal(out["1"][2], out["2"][2])
