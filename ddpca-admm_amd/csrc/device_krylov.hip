@@ -230,7 +230,8 @@ int64_t krylov_mult_solv(MgpisDevice& D, const double* b, double* x, int64_t max
 
 // MGPIS::BiCGSTAB_SOLV (MGPIS.h:350-432): right-preconditioned BiCGSTAB from x0 = 0 with the
 // shadow residual r^ = r0 = b; stop on the recursive residual ||r|| <= rtol ||b||, on
-// rho = 0 (the reference's "ERROR 1" exit, reported through *breakdown) or after maxit.
+// rho = 0 (the reference's "ERROR 1" exit, reported through *breakdown), after maxit, or --
+// deviation -- at the attainable accuracy: ||r|| <= 100 rtol ||b|| and flat over five iterations.
 // The dot products that share operands are fused into one pass: (r^ v), (t s) + (t t),
 // (r r) + (r^ r) for the next iteration.  Returns iterNumb at exit.
 int64_t krylov_bicgstab(MgpisDevice& D, int prec, const double* b, double* x, double rtol, int64_t maxit,
@@ -249,6 +250,7 @@ int64_t krylov_bicgstab(MgpisDevice& D, int prec, const double* b, double* x, do
     int64_t it = 0;
     if (breakdown) *breakdown = 0;
     static const bool trace = std::getenv("DDPCA_KRYLOV_TRACE") != nullptr;  // per-iteration scalars on stderr
+    std::vector<double> moni(5, 0.0);
     while (it < maxit && std::sqrt(rr) > tol) {
         double& rc = rho[(it + 1) % 2];
         rc = rhr;
@@ -287,6 +289,16 @@ int64_t krylov_bicgstab(MgpisDevice& D, int prec, const double* b, double* x, do
         rhr = d[1];
         check_finite(rr, "residual (BiCGSTAB)");
         ++it;
+        // attainable-accuracy stop (the reference's GMRES_SOLV rule, MGPIS.h:228-348): within
+        // 100 tol and the last five residual norms flat to 10 % of their median.  On singular
+        // systems (LAGRANGE, frictionless sliding modes) the recursive residual can stall just
+        // above tol; BiCGSTAB then loses r^ . r to rounding and diverges (profiles/r02q_*)
+        moni[(it - 1) % 5] = std::sqrt(rr);
+        if (it >= 5 && std::sqrt(rr) <= 100.0 * tol) {
+            double medi, osci;
+            medi_osci(moni, medi, osci);
+            if (osci < 0.1 * medi) break;
+        }
     }
     DDPCA_HIP(hipStreamSynchronize(w.st));
     if (relres) *relres = bn > 0 ? std::sqrt(rr) / bn : 0.0;

@@ -21,4 +21,5 @@ python3 profiles/pmc_kernels.py $(find $OUT/pmc_vc_fetch -name "*counter_collect
 timeout -k 10 300 python3 -u bench.py > $OUT/bench.json.log 2>&1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline > $OUT/trace.log 2>&1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace_g1 -o run -- python3 bench.py --groups 1 --steps 5 --warmup 1 --no-cpu-baseline > $OUT/trace_g1.log 2>&1
+cp profiles/traffic.json $OUT/traffic.json
 echo done > $OUT/DONE
