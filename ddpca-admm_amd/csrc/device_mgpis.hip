@@ -739,6 +739,46 @@ __global__ __launch_bounds__(kBlock) void k_axpy(double* x, double* r, const dou
     chunk_partial(s, partial, c);
 }
 
+// k_axpy fused with the V-cycle's first fine-level sweep x0 = omega M r_new (k_jac0 from a zero
+// guess, block Jacobi with the fp32 3x3 inverses): the new residual goes through LDS from the
+// chunk-flat layout to one node per lane, so r is not read again.  Same arithmetic on the same
+// values as k_axpy + k_jac0, bit for bit.  (Members that converge in this iteration compute an
+// x0 nobody reads: the V-cycle's launches skip them.)
+__global__ __launch_bounds__(kBlock) void k_axpy_jac0(double* x, double* r, const double* p, const double* q,
+                                                      const PcgScal* sc, double* partial, int64_t nn,
+                                                      const int32_t* csub, const float* minv, const double* coef,
+                                                      double* x0) {
+    __shared__ double rl[kBlock / kWave][3 * kChunk];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t c = (int64_t)blockIdx.x * (kBlock / kWave) + w;
+    const int sub = c * kChunk < nn ? csub[c] : 0;
+    const bool live = c * kChunk < nn && !stopped(sc, sub);  // wave-uniform
+    if (live) {
+        const double al = sc[sub].alpha;
+        const int64_t base = c * 3 * kChunk + lane;
+        double s = 0.0;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const int64_t k = base + j * kChunk;
+            x[k] += al * p[k];
+            const double v = r[k] - al * q[k];
+            r[k] = v;
+            s += v * v;
+            rl[w][lane + j * kChunk] = v;
+        }
+        chunk_partial(s, partial, c);
+    }
+    __syncthreads();
+    if (!live) return;
+    const int64_t i = c * kChunk + lane;
+    const double om = coef[2 * sub + 1];
+    double m0, m1, m2;
+    apply_m<true>(minv, i, rl[w][3 * lane], rl[w][3 * lane + 1], rl[w][3 * lane + 2], m0, m1, m2);
+    x0[3 * i] = om * m0;
+    x0[3 * i + 1] = om * m1;
+    x0[3 * i + 2] = om * m2;
+}
+
 // z = D^-1 r (diagonal preconditioner, DIAG_PREC), partial r^T z
 __global__ __launch_bounds__(kBlock) void k_diag(const double* r, const double* dinv, double* z, double* partial,
                                                  int64_t nn, const int32_t* csub, const PcgScal* sc) {
@@ -2117,7 +2157,16 @@ double MgpisDevice::bench_spmv(int variant, int reps) {
     return (double)ms / std::max(reps, 1);
 }
 
-void MgpisDevice::vcycle(const double* rin, double* zout, bool dot) {
+// the first fine sweep can ride on k_axpy (k_axpy_jac0): block Jacobi from the fp32 inverses on
+// a level with a coarser one (DDPCA_FUSE_JAC0=0 keeps the separate k_jac0)
+bool MgpisDevice::fuse_jac0() const {
+    const char* e = std::getenv("DDPCA_FUSE_JAC0");  // read at graph capture, per handle
+    const bool on = !(e && e[0] == '0');
+    const int Lf = (int)lev.size() - 1;
+    return on && !no_coarse && opt.smoother == 1 && Lf > clev && vc_type(Lf) != kVal64 && lev[Lf].minv32.p;
+}
+
+void MgpisDevice::vcycle(const double* rin, double* zout, bool dot, bool first_done) {
     if (no_coarse) throw ApiError(DDPCA_ESTATE, "one-level handle without a coarse inverse: diagonal preconditioner only");
     const int nlev = (int)lev.size();
     const int Lf = nlev - 1;
@@ -2169,7 +2218,10 @@ void MgpisDevice::vcycle(const double* rin, double* zout, bool dot) {
         }
     };
     // ---- descend
-    {
+    if (first_done) {
+        // k_axpy_jac0 wrote x0 = omega M rin into the fine level's first iterate buffer
+        if (cur[Lf] != lev[Lf].t.p || !fuse_jac0()) throw ApiError(DDPCA_ESTATE, "fused first sweep");
+    } else {
         const LevelDev& F = lev[Lf];
         const int grid = ceil_div(F.nn, kBlock);
         if (vc_type(Lf) != kVal64) {
@@ -2284,9 +2336,14 @@ void MgpisDevice::enqueue_iteration(int prec, bool timed) {
     launch_sell<kPcg, false, true>(kVal64, a, stream);
     if (timed) DDPCA_HIP(hipEventRecord(ev_k1, stream));
     hipLaunchKernelGGL(k_fin, dim3(nsub), dim3(kFinT), 0, stream, (int)kFinAlpha, partial.p, nullptr, fin_cb.p, scp, mirror.dev);
-    hipLaunchKernelGGL(k_axpy, dim3(nblk), dim3(kBlock), 0, stream, xs.p, rs.p, ps.p, qs.p, scp, partial.p, L.nn, L.csub.p);
+    const bool fuse0 = prec == 1 && fuse_jac0();
+    if (fuse0)
+        hipLaunchKernelGGL(k_axpy_jac0, dim3(nblk), dim3(kBlock), 0, stream, xs.p, rs.p, ps.p, qs.p, scp, partial.p, L.nn,
+                           L.csub.p, L.minv32.p, L.coef.p, L.t.p);
+    else
+        hipLaunchKernelGGL(k_axpy, dim3(nblk), dim3(kBlock), 0, stream, xs.p, rs.p, ps.p, qs.p, scp, partial.p, L.nn, L.csub.p);
     hipLaunchKernelGGL(k_fin, dim3(nsub), dim3(kFinT), 0, stream, (int)kFinRR, partial.p, nullptr, fin_cb.p, scp, mirror.dev);
-    if (prec == 1) vcycle(rs.p, zs.p, true);
+    if (prec == 1) vcycle(rs.p, zs.p, true, fuse0);
     else hipLaunchKernelGGL(k_diag, dim3(nblk), dim3(kBlock), 0, stream, rs.p, L.dinv.p, zs.p, partial.p, L.nn, L.csub.p, scp);
     hipLaunchKernelGGL(k_fin, dim3(nsub), dim3(kFinT), 0, stream, (int)kFinBeta, partial.p, nullptr, fin_cb.p, scp, mirror.dev);
 }

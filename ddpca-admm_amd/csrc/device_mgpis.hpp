@@ -182,7 +182,10 @@ public:
         if (!vc32() || lev[l].tbl) return kVal64;
         return lev[l].val16.p ? kValH16 : kVal32;
     }
-    void vcycle(const double* r, double* z, bool dot);     // z = M^-1 r (fine level)
+    // z = M^-1 r (fine level); first_done: the first fine sweep is already in lev.back().t
+    // (k_axpy_jac0, only when fuse_jac0())
+    void vcycle(const double* r, double* z, bool dot, bool first_done = false);
+    bool fuse_jac0() const;
     // b_{l-1} = realProl[l-1]^T r_l on every member (masked), batch nodal layouts of levels l, l-1
     void restrict_level(int l, const double* rf, double* bc);
     // block (rotated-node) parts of the transfer from level l-1 to l: b_c += B^T r_f, x_f += B e_c

@@ -105,23 +105,29 @@ def test_headline_fullsize_batched_solves_match_oracle(ddpca, oracle, gpu):
         assert err <= 1e-8, (tv, err)
 
 
-def test_split_streams_reproduce_single_stream(ddpca, gpu, monkeypatch):
-    """The two-stream split of the body-balance batch (MgpisDevice::set_split, the default) runs
-    the same kernels on the same data per subdomain, only on two streams: the ADMM trajectory,
-    displacements and PCG iteration counts must equal the single-stream graph's bit for bit."""
+@pytest.mark.parametrize("env", [("DDPCA_STREAMS", "1"), ("DDPCA_FUSE_JAC0", "0")], ids=["one-stream", "separate-jac0"])
+def test_schedule_variants_are_bit_identical(ddpca, gpu, monkeypatch, env):
+    """Schedule-only variants of the headline path must not change a bit: the two-stream split of
+    the body-balance batch and of the mass CG (MgpisDevice / MassBatch ::set_split, default on)
+    against one stream, and the V-cycle's first fine sweep fused into k_axpy (k_axpy_jac0, default
+    on) against the separate k_jac0.  ADMM trajectory, displacements and PCG iteration counts equal
+    bit for bit (8 ADMM iterations, reduced chain, headline option set)."""
     H, M = ddpca.HEADLINE_OPTIONS, ddpca.HEADLINE_MUSC
     out = {}
-    for streams in ("1", "2"):
-        monkeypatch.setenv("DDPCA_STREAMS", streams)
+    for variant in ("default", "alt"):
+        if variant == "alt":
+            monkeypatch.setenv(*env)
+        else:
+            monkeypatch.delenv(env[0], raising=False)
         P = ddpca.Problem("dehw", 4, 3, 2, 2, 3, 0.2)
         P.set_coarse(M["muscSett"], [M["doleMcsc"]] * P.nsub)
         P.ESTABLISH()
         mc = ddpca.MCONTACT(P, **H)
         assert mc.CONTACT_ANALYSIS(8, check=False) == 8
-        out[streams] = (mc.monitor().copy(), [mc.get("resuDisp", tv).copy() for tv in range(P.nsub)],
-                         np.array(mc.get("pcg_iters")).copy())
+        out[variant] = (mc.monitor().copy(), [mc.get("resuDisp", tv).copy() for tv in range(P.nsub)],
+                        np.array(mc.get("pcg_iters")).copy())
         del mc
-    assert np.array_equal(out["1"][0], out["2"][0])
-    for a, b in zip(out["1"][1], out["2"][1]):
+    assert np.array_equal(out["default"][0], out["alt"][0])
+    for a, b in zip(out["default"][1], out["alt"][1]):
         assert np.array_equal(a, b)
-    assert np.array_equal(out["1"][2], out["2"][2])
+    assert np.array_equal(out["default"][2], out["alt"][2])
