@@ -803,7 +803,10 @@ __global__ __launch_bounds__(kBlock) void k_dot(const double* x, const double* y
 
 // Scalar updates of the PCG recurrence: one workgroup per subdomain, fixed summation order
 // over that subdomain's chunk partials.  Stop-state changes are mirrored to host memory.
-constexpr int kFinT = 1024;  // threads of k_fin: a subdomain's ~6400 fine chunk partials in ~2 loads each
+// kFinT threads: 1024 reads a subdomain's ~6400 fine chunk partials in ~2 loads each; 256 (the
+// two-stream split's choice) needs only four free wave slots on one CU, so it is placed while the
+// other half's streaming kernel holds the chip instead of waiting for a CU to drain
+template <int kFinT>
 __global__ __launch_bounds__(kFinT) void k_fin(int what, const double* partial, const double* partial2,
                                                const int64_t* cb, PcgScal* scv, PcgMirror* mirror) {
     const int sub = blockIdx.x;
@@ -2322,6 +2325,22 @@ double MgpisDevice::fine_kernel_bytes(int s) const {
     return fine_matrix_bytes(s, kVal64) + 24.0 * 5.0 * (double)lev.back().nloc[s];
 }
 
+// k_fin over every member (fin_threads_: 1024, or 256 under the two-stream split; DDPCA_FIN_THREADS)
+void MgpisDevice::launch_fin(hipStream_t st, int what, const double* part, const double* part2, const int64_t* cb,
+                             PcgScal* scp, PcgMirror* mir) {
+    if (fin_threads() == 256)
+        hipLaunchKernelGGL(k_fin<256>, dim3(nsub), dim3(256), 0, st, what, part, part2, cb, scp, mir);
+    else
+        hipLaunchKernelGGL(k_fin<1024>, dim3(nsub), dim3(1024), 0, st, what, part, part2, cb, scp, mir);
+}
+
+int MgpisDevice::fin_threads() const {
+    const char* e = std::getenv("DDPCA_FIN_THREADS");
+    if (e && std::atoi(e) == 1024) return 1024;
+    if (e && std::atoi(e) == 256) return 256;
+    return split_ ? 256 : 1024;
+}
+
 void MgpisDevice::enqueue_iteration(int prec, bool timed) {
     LevelDev& L = lev.back();
     PcgScal* scp = sc_cur_ ? sc_cur_ : sc.p;
@@ -2335,17 +2354,17 @@ void MgpisDevice::enqueue_iteration(int prec, bool timed) {
     if (timed) DDPCA_HIP(hipEventRecord(ev_k0, stream));
     launch_sell<kPcg, false, true>(kVal64, a, stream);
     if (timed) DDPCA_HIP(hipEventRecord(ev_k1, stream));
-    hipLaunchKernelGGL(k_fin, dim3(nsub), dim3(kFinT), 0, stream, (int)kFinAlpha, partial.p, nullptr, fin_cb.p, scp, mirror.dev);
+    launch_fin(stream, (int)kFinAlpha, partial.p, nullptr, fin_cb.p, scp, mirror.dev);
     const bool fuse0 = prec == 1 && fuse_jac0();
     if (fuse0)
         hipLaunchKernelGGL(k_axpy_jac0, dim3(nblk), dim3(kBlock), 0, stream, xs.p, rs.p, ps.p, qs.p, scp, partial.p, L.nn,
                            L.csub.p, L.minv32.p, L.coef.p, L.t.p);
     else
         hipLaunchKernelGGL(k_axpy, dim3(nblk), dim3(kBlock), 0, stream, xs.p, rs.p, ps.p, qs.p, scp, partial.p, L.nn, L.csub.p);
-    hipLaunchKernelGGL(k_fin, dim3(nsub), dim3(kFinT), 0, stream, (int)kFinRR, partial.p, nullptr, fin_cb.p, scp, mirror.dev);
+    launch_fin(stream, (int)kFinRR, partial.p, nullptr, fin_cb.p, scp, mirror.dev);
     if (prec == 1) vcycle(rs.p, zs.p, true, fuse0);
     else hipLaunchKernelGGL(k_diag, dim3(nblk), dim3(kBlock), 0, stream, rs.p, L.dinv.p, zs.p, partial.p, L.nn, L.csub.p, scp);
-    hipLaunchKernelGGL(k_fin, dim3(nsub), dim3(kFinT), 0, stream, (int)kFinBeta, partial.p, nullptr, fin_cb.p, scp, mirror.dev);
+    launch_fin(stream, (int)kFinBeta, partial.p, nullptr, fin_cb.p, scp, mirror.dev);
 }
 
 // graph_[prec]: iters_per_graph PCG iterations captured once and replayed.
@@ -2486,7 +2505,7 @@ void MgpisDevice::pcg_begin(int prec, double rtol, const std::vector<int64_t>& m
     const int nblk = ceil_div(L.nn, kBlock);
     if (!warm) {
         hipLaunchKernelGGL(k_pcg_init, dim3(nblk), dim3(kBlock), 0, stream, bs.p, xs.p, rs.p, ps.p, qs.p, partial.p, L.nn);
-        hipLaunchKernelGGL(k_fin, dim3(nsub), dim3(kFinT), 0, stream, (int)kFinInit, partial.p, nullptr, fin_cb.p, sc.p, mirror.dev);
+        launch_fin(stream, (int)kFinInit, partial.p, nullptr, fin_cb.p, sc.p, mirror.dev);
     } else {
         double* partial2 = partial.p + L.nch;
         hipLaunchKernelGGL(k_pcg_init_warm, dim3(nblk), dim3(kBlock), 0, stream, bs.p, ps.p, qs.p, partial2, L.nn);
@@ -2496,11 +2515,11 @@ void MgpisDevice::pcg_begin(int prec, double rtol, const std::vector<int64_t>& m
         a.y = rs.p;
         a.partial = partial.p;
         launch_sell<kResid, false, true>(kVal64, a, stream);
-        hipLaunchKernelGGL(k_fin, dim3(nsub), dim3(kFinT), 0, stream, (int)kFinInitWarm, partial.p, partial2, fin_cb.p, sc.p, mirror.dev);
+        launch_fin(stream, (int)kFinInitWarm, partial.p, partial2, fin_cb.p, sc.p, mirror.dev);
     }
     if (prec == 1) vcycle(rs.p, zs.p, true);
     else hipLaunchKernelGGL(k_diag, dim3(nblk), dim3(kBlock), 0, stream, rs.p, L.dinv.p, zs.p, partial.p, L.nn, L.csub.p, sc.p);
-    hipLaunchKernelGGL(k_fin, dim3(nsub), dim3(kFinT), 0, stream, (int)kFinBeta0, partial.p, nullptr, fin_cb.p, sc.p, mirror.dev);
+    launch_fin(stream, (int)kFinBeta0, partial.p, nullptr, fin_cb.p, sc.p, mirror.dev);
     sample_pending_ = false;
     if (time_kernel) {
         // first iteration eagerly, with HIP events around its fine-level SpMV on this stream

@@ -238,6 +238,9 @@ private:
     std::vector<int> half_host_;
     PcgScal* sc_cur_ = nullptr; // the scalars enqueue_iteration / vcycle bind (sc, or a half's copy)
     void build_half_graph(int prec, int h);
+    int fin_threads() const;
+    void launch_fin(hipStream_t st, int what, const double* part, const double* part2, const int64_t* cb, PcgScal* scp,
+                    PcgMirror* mir);
     bool sample_pending_ = false;
     void build_graph(int prec);
     void enqueue_iteration(int prec, bool timed);
