@@ -803,9 +803,9 @@ __global__ __launch_bounds__(kBlock) void k_dot(const double* x, const double* y
 
 // Scalar updates of the PCG recurrence: one workgroup per subdomain, fixed summation order
 // over that subdomain's chunk partials.  Stop-state changes are mirrored to host memory.
-// kFinT threads: 1024 reads a subdomain's ~6400 fine chunk partials in ~2 loads each; 256 (the
-// two-stream split's choice) needs only four free wave slots on one CU, so it is placed while the
-// other half's streaming kernel holds the chip instead of waiting for a CU to drain
+// kFinT threads: 1024 (default) reads a subdomain's ~6400 fine chunk partials in ~2 loads each;
+// 256 needs only four free wave slots on one CU (placed sooner while the other half of a split
+// batch streams) -- measured 0.2-0.6 % slower overall, kept for A/B (DDPCA_FIN_THREADS=256)
 template <int kFinT>
 __global__ __launch_bounds__(kFinT) void k_fin(int what, const double* partial, const double* partial2,
                                                const int64_t* cb, PcgScal* scv, PcgMirror* mirror) {
@@ -2161,10 +2161,12 @@ double MgpisDevice::bench_spmv(int variant, int reps) {
 }
 
 // the first fine sweep can ride on k_axpy (k_axpy_jac0): block Jacobi from the fp32 inverses on
-// a level with a coarser one (DDPCA_FUSE_JAC0=0 keeps the separate k_jac0)
+// a level with a coarser one
 bool MgpisDevice::fuse_jac0() const {
+    // opt-in (DDPCA_FUSE_JAC0=1): measured 0.4 % slower at 8 subdomains per GPU, as in round 1
+    // (profiles/r02u_ab.json, r01_sweep_fuse_axpy.txt) -- the wider k_axpy costs what k_jac0 did
     const char* e = std::getenv("DDPCA_FUSE_JAC0");  // read at graph capture, per handle
-    const bool on = !(e && e[0] == '0');
+    const bool on = e && e[0] == '1';
     const int Lf = (int)lev.size() - 1;
     return on && !no_coarse && opt.smoother == 1 && Lf > clev && vc_type(Lf) != kVal64 && lev[Lf].minv32.p;
 }
@@ -2325,7 +2327,7 @@ double MgpisDevice::fine_kernel_bytes(int s) const {
     return fine_matrix_bytes(s, kVal64) + 24.0 * 5.0 * (double)lev.back().nloc[s];
 }
 
-// k_fin over every member (fin_threads_: 1024, or 256 under the two-stream split; DDPCA_FIN_THREADS)
+// k_fin over every member (1024 threads, or 256 with DDPCA_FIN_THREADS=256)
 void MgpisDevice::launch_fin(hipStream_t st, int what, const double* part, const double* part2, const int64_t* cb,
                              PcgScal* scp, PcgMirror* mir) {
     if (fin_threads() == 256)
@@ -2336,9 +2338,8 @@ void MgpisDevice::launch_fin(hipStream_t st, int what, const double* part, const
 
 int MgpisDevice::fin_threads() const {
     const char* e = std::getenv("DDPCA_FIN_THREADS");
-    if (e && std::atoi(e) == 1024) return 1024;
-    if (e && std::atoi(e) == 256) return 256;
-    return split_ ? 256 : 1024;
+    // measured (profiles/r02u_ab.json): 1024 is 0.2-0.6 % faster with and without the split
+    return (e && std::atoi(e) == 256) ? 256 : 1024;
 }
 
 void MgpisDevice::enqueue_iteration(int prec, bool timed) {

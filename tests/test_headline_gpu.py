@@ -105,12 +105,12 @@ def test_headline_fullsize_batched_solves_match_oracle(ddpca, oracle, gpu):
         assert err <= 1e-8, (tv, err)
 
 
-@pytest.mark.parametrize("env", [("DDPCA_STREAMS", "1"), ("DDPCA_FUSE_JAC0", "0")], ids=["one-stream", "separate-jac0"])
+@pytest.mark.parametrize("env", [("DDPCA_STREAMS", "1"), ("DDPCA_FUSE_JAC0", "1")], ids=["one-stream", "fused-jac0"])
 def test_schedule_variants_are_bit_identical(ddpca, gpu, monkeypatch, env):
     """Schedule-only variants of the headline path must not change a bit: the two-stream split of
     the body-balance batch and of the mass CG (MgpisDevice / MassBatch ::set_split, default on)
-    against one stream, and the V-cycle's first fine sweep fused into k_axpy (k_axpy_jac0, default
-    on) against the separate k_jac0.  ADMM trajectory, displacements and PCG iteration counts equal
+    against one stream, and the V-cycle's first fine sweep fused into k_axpy (k_axpy_jac0, opt-in)
+    against the separate k_jac0 (default).  ADMM trajectory, displacements and PCG iteration counts equal
     bit for bit (8 ADMM iterations, reduced chain, headline option set)."""
     H, M = ddpca.HEADLINE_OPTIONS, ddpca.HEADLINE_MUSC
     out = {}
