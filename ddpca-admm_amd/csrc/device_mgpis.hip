@@ -440,6 +440,14 @@ __global__ __launch_bounds__(kBlock) void k_sell_split(SellArgs a) {
     }
 }
 
+// Workgroup b is dispatched to XCD b % 8: the logical block that makes XCD x own the x-th
+// contiguous run of the grid (runs of q+1 blocks for the first r XCDs, q for the rest; G = 8q + r)
+__device__ __forceinline__ int64_t xcd_slab_block() {
+    const int64_t G = gridDim.x, b = blockIdx.x, q = G / 8, r = G % 8, x = b % 8, k = b / 8;
+    const int64_t start = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q;
+    return start + k;
+}
+
 // Node-parallel kernels: thread = node, 256 nodes per workgroup; a wavefront is one chunk, so
 // the subdomain (and its stop flag) is uniform per wavefront.  nn is a multiple of 64.
 #define NODE_PROLOGUE(nn, csub, sc)                         \
@@ -529,8 +537,14 @@ template <bool INIT, bool BJ, bool SETD, typename MT = double>
 __global__ __launch_bounds__(kBlock) void k_restrict_lat(const double* rf, const uint32_t* rmsk, const int32_t* rf0,
                                                          const int32_t* rstr, const uint8_t* cmask, double* bc,
                                                          double* xc, double* dc, const MT* minv, const double* coef,
-                                                         int64_t nc, const int32_t* csub, const PcgScal* sc) {
-    NODE_PROLOGUE(nc, csub, sc)
+                                                         int64_t nc, const int32_t* csub, const PcgScal* sc, int xcd) {
+    // xcd: each XCD takes one contiguous eighth of the coarse nodes (workgroup b runs on XCD
+    // b % 8), so the fine planes two neighbouring coarse planes share are fetched into one L2
+    const int64_t blk = xcd ? xcd_slab_block() : (int64_t)blockIdx.x;
+    const int64_t i = blk * kBlock + threadIdx.x;
+    if (i >= nc) return;
+    const int sub = csub[i >> 6];
+    if (stopped(sc, sub)) return;
     const int64_t j = i;
     const uint32_t msk = rmsk[j];
     const int64_t f0 = rf0[j];
@@ -2050,8 +2064,9 @@ void launch_restrict(const LevelDev& F, int grid, hipStream_t st, const double* 
     // stored weights: deriving them from a gathered parent count (as k_prolong<true> does)
     // measured 58 -> 102 us on the fine level (profiles/r01_transfer_weights.txt)
     if (F.lat) {
+        static const int xcd = std::getenv("DDPCA_XCD_RESTRICT") ? std::atoi(std::getenv("DDPCA_XCD_RESTRICT")) : 0;
         hipLaunchKernelGGL((k_restrict_lat<INIT, BJ, SETD, MT>), dim3(grid), dim3(kBlock), 0, st, rf, F.rmsk.p, F.rf0.p,
-                           F.rstr.p, cmask, bc, xc, dc, minv, coef, nc, csub, sc);
+                           F.rstr.p, cmask, bc, xc, dc, minv, coef, nc, csub, sc, xcd);
         return;
     }
     hipLaunchKernelGGL((k_restrict<INIT, BJ, SETD, MT>), dim3(grid), dim3(kBlock), 0, st, rf, F.rslots.p, F.roff.p,
