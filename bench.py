@@ -44,15 +44,16 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--groups", type=int, default=4, help="worm/wheel groups (2 subdomains each)")
-    ap.add_argument("--nx", type=int, default=3)
-    ap.add_argument("--ny", type=int, default=2)
-    ap.add_argument("--nz", type=int, default=2)
-    ap.add_argument("--gl", type=int, default=5, help="uniform refinements (levels = gl + 1)")
-    ap.add_argument("--fric", type=float, default=0.2)
-    ap.add_argument("--ip-contact", type=int, default=2,
+    W = importlib.import_module("ddpca-admm_amd").HEADLINE_WORKLOAD  # the same parity tests pin it
+    ap.add_argument("--groups", type=int, default=W["groups"], help="worm/wheel groups (2 subdomains each)")
+    ap.add_argument("--nx", type=int, default=W["nx"])
+    ap.add_argument("--ny", type=int, default=W["ny"])
+    ap.add_argument("--nz", type=int, default=W["nz"])
+    ap.add_argument("--gl", type=int, default=W["gl"], help="uniform refinements (levels = gl + 1)")
+    ap.add_argument("--fric", type=float, default=W["fric"])
+    ap.add_argument("--ip-contact", type=int, default=W["ip_contact"],
                     help="contact faces integrated over 2^k x 2^k polygons (k = 2: M3's 0.8 ip per DOF with --ip-glued 1)")
-    ap.add_argument("--ip-glued", type=int, default=1, help="the same for the glued faces")
+    ap.add_argument("--ip-glued", type=int, default=W["ip_glued"], help="the same for the glued faces")
     # defaults: the fastest configuration of the round-1 sweep (profiles/r01_sweep.txt)
     ap.add_argument("--smoother", type=int, default=H["smoother"], help="0 point Jacobi, 1 block Jacobi, 2 Chebyshev")
     ap.add_argument("--nu", type=int, default=H["nu"])
@@ -102,7 +103,8 @@ def main():
     part = import_module("ddpca-admm_amd.partition")
 
     t_setup = time.perf_counter()
-    P = D.Problem("dehw", a.groups, a.nx, a.ny, a.nz, a.gl, a.fric, a.ip_contact, a.ip_glued)
+    P = D.headline_problem(groups=a.groups, nx=a.nx, ny=a.ny, nz=a.nz, gl=a.gl, fric=a.fric,
+                           ip_contact=a.ip_contact, ip_glued=a.ip_glued)
     nip = sum(len(P.array("ip_w", ts)) for ts in range(P.nint))
     nsub = P.nsub
     owner = part.block_owner(nsub, world)

@@ -57,6 +57,22 @@ HEADLINE_OPTIONS = dict(smoother=1, nu=1, omega=-1.7, iters_per_graph=4, warm_st
 # and the ADMM setting it runs: interface-eliminated coarse space (muscSett = 2) on level 1 of
 # every subdomain (DEHW.h:2222, 2239)
 HEADLINE_MUSC = dict(muscSett=2, doleMcsc=1)
+# and the workload: the synthetic DEHW chain of bench.py (4 worm/wheel groups = 8 subdomains,
+# 3x2x2 coarse hexes refined gl = 5 times, Coulomb mu = 0.2) at SURVEY §8 d2 M3's interface
+# density -- contact faces integrated over 2^2 x 2^2 polygons, glued faces over 2^1 x 2^1
+# (0.80 integration points per DOF at gl = 5).  bench.py's defaults and the headline parity tests
+# (tests/test_headline_gpu.py, at gl = 3 for the oracle trajectory) both take it from here.
+HEADLINE_WORKLOAD = dict(groups=4, nx=3, ny=2, nz=2, gl=5, fric=0.2, ip_contact=2, ip_glued=1)
+
+
+def headline_problem(gl: int | None = None, **override) -> "Problem":
+    """The bench's DEHW-synthetic Problem (HEADLINE_WORKLOAD), optionally at another refinement
+    depth or with other workload parameters."""
+    w = dict(HEADLINE_WORKLOAD, **override)
+    if gl is not None:
+        w["gl"] = gl
+    return Problem("dehw", w["groups"], w["nx"], w["ny"], w["nz"], w["gl"], w["fric"], w["ip_contact"],
+                   w["ip_glued"])
 
 _P = C.c_void_p
 _I64P = C.POINTER(C.c_int64)
@@ -777,4 +793,5 @@ class MCONTACT:
 
 __all__ = ["Problem", "MULTIGRID", "MGPIS", "MCONTACT", "DdpcaError", "lib", "gpu_available", "default_options",
            "contact_search",
-           "LIBPATH", "HEADLINE_OPTIONS", "HEADLINE_MUSC"]
+           "LIBPATH", "HEADLINE_OPTIONS", "HEADLINE_MUSC", "HEADLINE_WORKLOAD",
+           "headline_problem"]

@@ -30,10 +30,15 @@ struct ddpca_lagrange {
     std::vector<LagrangeItf> itfs;
     std::vector<uint8_t> have_sub, have_itf;
     LagrangeResult res;
+    std::vector<double> solver_relres;   // per Newton step: BiCGSTAB's ||r|| / ||b|| at exit
+    std::vector<double> solver_brk;      // per Newton step: 0, 1 (rho = 0), 2 (attainable-accuracy stop)
     bool solved = false;
 };
 
 namespace {
+
+// the largest BiCGSTAB ||r|| / ||b|| a Newton step may continue from (else DDPCA_ENUMERIC)
+constexpr double kLagrangeMaxRelres = 1e-10;
 
 Csr csr_in(const ddpca_csr_t& m, const char* what) {
     if (m.nrow < 0 || m.ncol < 0 || (m.nrow > 0 && !m.ptr)) throw ApiError(DDPCA_EINVAL, std::string(what) + ": bad CSR");
@@ -57,8 +62,9 @@ Csr csr_in(const ddpca_csr_t& m, const char* what) {
 }
 
 // BiCGSTAB on the device for one Newton step's system (levels lo..L of the hierarchy)
+// relres / brk: the solve's ||r|| / ||b|| and breakdown code (1 rho = 0, 2 attainable-accuracy stop)
 int64_t device_solve(int device, int prec_type, const mgpis_options_t& o, const std::vector<LagrangeSub>& subs,
-                     const LagrangeSystem& sys, std::vector<double>& x) {
+                     const LagrangeSystem& sys, std::vector<double>& x, double& relres, int& brk) {
     const int L = (int)sys.K.size() - 1;
     const int lo = prec_type == 1 ? 0 : L;
     const int nl = L - lo + 1;
@@ -108,7 +114,8 @@ int64_t device_solve(int device, int prec_type, const mgpis_options_t& o, const 
     oo.precond_fp32 = 0;  // the symmetric fp32 / fp16 copies assume K = K^T
     oo.table_mode = 0;
     oo.warm_start = 0;
-    MgpisDevice D(device, std::vector<SubdomainOps>{ops}, oo, true);
+    // precType 2 runs the diagonal preconditioner only: no dense coarse pseudo-inverse
+    MgpisDevice D(device, std::vector<SubdomainOps>{ops}, oo, true, prec_type != 1);
     // the device's condensed order is increasing nodal dof; the hierarchy's is subdomain-major
     const int64_t n = (int64_t)fd[L].size();
     if (D.nfree[0] != n) throw ApiError(DDPCA_ESTATE, "LAGRANGE: device dof count");
@@ -122,9 +129,11 @@ int64_t device_solve(int device, int prec_type, const mgpis_options_t& o, const 
     tmp.upload(b);
     D.bs.zero(D.stream);
     D.scatter_free(0, tmp.p, D.bs.p);
-    double relres = 0.0;
-    int brk = 0;
-    const int64_t it = krylov_bicgstab(D, prec_type == 1 ? 1 : 0, D.bs.p, D.xs.p, 1e-14, n, &relres, &brk);
+    relres = 0.0;
+    brk = 0;
+    // the singular frictionless systems can stall just above 1e-14: the
+    // attainable-accuracy stop is on for LAGRANGE's steps only
+    const int64_t it = krylov_bicgstab(D, prec_type == 1 ? 1 : 0, D.bs.p, D.xs.p, 1e-14, n, &relres, &brk, true);
     D.gather_free(0, D.xs.p, tmp.p);
     DDPCA_HIP(hipMemcpyAsync(xd.data(), tmp.p, n * sizeof(double), hipMemcpyDeviceToHost, D.stream));
     DDPCA_HIP(hipStreamSynchronize(D.stream));
@@ -174,6 +183,7 @@ int ddpca_lagrange_set_subdomain(ddpca_lagrange_t h, int64_t tv, int nlev, const
             for (int64_t r = 0; r < nfree[l]; ++r)
                 if (free_dof[l][r] < 0 || free_dof[l][r] >= 3 * nnodes[l] || (r && free_dof[l][r] <= free_dof[l][r - 1]))
                     throw ApiError(DDPCA_EINVAL, "free_dof must be increasing nodal dofs of the level");
+            if (l && nfree[l] < nfree[l - 1]) throw ApiError(DDPCA_EINVAL, "nfree must not shrink from one level to the next");
             if (l && nfree[l - 1] > 0 && !std::equal(free_dof[l - 1], free_dof[l - 1] + nfree[l - 1], free_dof[l]))
                 throw ApiError(DDPCA_EINVAL, "the free dofs of a level must be a prefix of the next level's");
             s.K.push_back(csr_in(K[l], "consStif"));
@@ -249,10 +259,25 @@ int64_t ddpca_lagrange_solve(ddpca_lagrange_t h, int device, int prec_type, cons
         // run_lagrange drops hanging non-mortar points and sets the dual basis in place: work on copies
         std::vector<LagrangeSub> subs = h->subs;
         std::vector<LagrangeItf> itfs = h->itfs;
+        h->solver_relres.clear();
+        h->solver_brk.clear();
         try {
             h->res = run_lagrange(subs, itfs, max_newton, [&](const LagrangeSystem& sys, std::vector<double>& x) {
-                return device_solve(device, prec_type, o, subs, sys, x);
+                double relres = 0.0;
+                int brk = 0;
+                const int64_t it = device_solve(device, prec_type, o, subs, sys, x, relres, brk);
+                h->solver_relres.push_back(relres);
+                h->solver_brk.push_back((double)brk);
+                // a Newton step must not continue from a solve that did not converge: the
+                // reference's own stop is 1e-14, the attainable-accuracy stop 1e-12
+                if (!(relres <= kLagrangeMaxRelres))
+                    throw std::runtime_error("BiCGSTAB of Newton step " + std::to_string(h->solver_relres.size()) +
+                                             " ended at ||r||/||b|| = " + std::to_string(relres) + " after " +
+                                             std::to_string(it) + " iterations (breakdown " + std::to_string(brk) + ")");
+                return it;
             });
+        } catch (const ApiError&) {
+            throw;  // device errors keep their own code
         } catch (const std::invalid_argument& e) {
             throw ApiError(DDPCA_EINVAL, e.what());
         } catch (const std::runtime_error& e) {
@@ -285,6 +310,8 @@ int64_t ddpca_lagrange_get(ddpca_lagrange_t h, const char* what, int64_t index, 
         else if (w == "wedi") itf(), n = copy_out(r.wedi[index], out, cap);
         else if (w == "solver_iters") n = copy_out(r.solver_iters, out, cap);
         else if (w == "changes") n = copy_out(r.changes, out, cap);
+        else if (w == "solver_relres") n = copy_out(h->solver_relres, out, cap);
+        else if (w == "solver_breakdown") n = copy_out(h->solver_brk, out, cap);
         else throw ApiError(DDPCA_EINVAL, "unknown quantity: " + w);
     });
     return rc != 0 ? rc : n;

@@ -230,12 +230,14 @@ int64_t krylov_mult_solv(MgpisDevice& D, const double* b, double* x, int64_t max
 
 // MGPIS::BiCGSTAB_SOLV (MGPIS.h:350-432): right-preconditioned BiCGSTAB from x0 = 0 with the
 // shadow residual r^ = r0 = b; stop on the recursive residual ||r|| <= rtol ||b||, on
-// rho = 0 (the reference's "ERROR 1" exit, reported through *breakdown), after maxit, or --
-// deviation -- at the attainable accuracy: ||r|| <= 100 rtol ||b|| and flat over five iterations.
+// rho = 0 (the reference's "ERROR 1" exit, reported through *breakdown = 1), after maxit, or --
+// only when `attainable` is set (LAGRANGE's Newton steps; the public MGPIS entry point keeps the
+// reference's rules) -- at the attainable accuracy: ||r|| <= 100 rtol ||b|| and flat over five
+// iterations, reported through *breakdown = 2.
 // The dot products that share operands are fused into one pass: (r^ v), (t s) + (t t),
 // (r r) + (r^ r) for the next iteration.  Returns iterNumb at exit.
 int64_t krylov_bicgstab(MgpisDevice& D, int prec, const double* b, double* x, double rtol, int64_t maxit,
-                        double* relres, int* breakdown) {
+                        double* relres, int* breakdown, bool attainable) {
     Work w(D, 8);
     double *r = w.vec(0), *rh = w.vec(1), *p = w.vec(2), *v = w.vec(3), *ph = w.vec(4), *s = w.vec(5),
            *sh = w.vec(6), *t = w.vec(7);
@@ -294,10 +296,13 @@ int64_t krylov_bicgstab(MgpisDevice& D, int prec, const double* b, double* x, do
         // systems (LAGRANGE, frictionless sliding modes) the recursive residual can stall just
         // above tol; BiCGSTAB then loses r^ . r to rounding and diverges (profiles/r02q_*)
         moni[(it - 1) % 5] = std::sqrt(rr);
-        if (it >= 5 && std::sqrt(rr) <= 100.0 * tol) {
+        if (attainable && it >= 5 && std::sqrt(rr) > tol && std::sqrt(rr) <= 100.0 * tol) {
             double medi, osci;
             medi_osci(moni, medi, osci);
-            if (osci < 0.1 * medi) break;
+            if (osci < 0.1 * medi) {
+                if (breakdown) *breakdown = 2;
+                break;
+            }
         }
     }
     DDPCA_HIP(hipStreamSynchronize(w.st));

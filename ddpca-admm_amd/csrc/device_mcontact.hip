@@ -1863,9 +1863,14 @@ void coarse_correct(ddpca_mcontact& H) {
         // consStif[L] x on every owned subdomain, then realProl^T down to level doleMcsc.  K x is
         // b - r with PCG's recursive residual r: it meets the true one to the PCG accuracy (the
         // reference's own CG_SOLV leaves a true residual of 1e-10 |b| behind its 1e-14 recursive
-        // one), and it saves a full fine-level fp64 SpMV per ADMM iteration
-        hipLaunchKernelGGL(k_sub, dim3(nb256(3 * D.lev[L].nn)), dim3(256), 0, st, D.bs.p, D.rs.p, D.lev[L].r.p,
-                           3 * D.lev[L].nn);
+        // one), and it saves a full fine-level fp64 SpMV per ADMM iteration.  DDPCA_CS_SPMV=1 takes
+        // the reference's explicit product instead (consStif * resuSolu, MCONTACT.h:2585-2587);
+        // tests/test_headline_gpu.py bounds the difference on the headline option set
+        const bool explicit_kx = std::getenv("DDPCA_CS_SPMV") && std::getenv("DDPCA_CS_SPMV")[0] == '1';
+        if (explicit_kx) D.spmv(L, D.xs.p, D.lev[L].r.p);
+        else
+            hipLaunchKernelGGL(k_sub, dim3(nb256(3 * D.lev[L].nn)), dim3(256), 0, st, D.bs.p, D.rs.p, D.lev[L].r.p,
+                               3 * D.lev[L].nn);
         for (int l = L; l > C.dmin; --l) D.restrict_level(l, l == L ? D.lev[L].r.p : D.lev[l].b.p, D.lev[l - 1].b.p);
     }
     hipLaunchKernelGGL(k_csr_wave, dim3(ceil_div(n, 4)), dim3(256), 0, st, C.rptr.p, C.rcol.p, C.rval.p, n, H.W.p,

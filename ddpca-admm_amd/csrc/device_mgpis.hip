@@ -1396,7 +1396,8 @@ bool lattice_transfer(LevelDev& L, const LevelDev& C, const std::vector<int32_t>
 }
 }  // namespace
 
-MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const mgpis_options_t& o, bool gen)
+MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const mgpis_options_t& o, bool gen,
+                         bool diag_only)
     : general(gen), device(dev), opt(o) {
     select_device(device);
     nsub = (int)subs.size();
@@ -1779,7 +1780,7 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
         for (int s = 0; s < nsub; ++s) n0max = std::max<int64_t>(n0max, 3 * subs[s].nnodes[clev]);
         // a one-level handle too large for a dense inverse serves the diagonal-preconditioned
         // drivers only (precSwit 0; the V-cycle then reports DDPCA_ESTATE)
-        no_coarse = nlev == 1 && n0max > 12288;
+        no_coarse = diag_only || (nlev == 1 && n0max > 12288);
     }
     if (!no_coarse) {
         std::vector<double> packed;

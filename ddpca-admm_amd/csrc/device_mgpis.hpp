@@ -132,7 +132,9 @@ class MgpisDevice {
 public:
     // general: the operators may be nonsymmetric (LAGRANGE's condensed systems under Coulomb
     // friction): LU coarse inverse, no symmetrised fp32 smoother copy
-    MgpisDevice(int device, const std::vector<SubdomainOps>& subs, const mgpis_options_t& opt, bool general = false);
+    // diag_only: a handle for the diagonal-preconditioned drivers only (no dense coarse inverse)
+    MgpisDevice(int device, const std::vector<SubdomainOps>& subs, const mgpis_options_t& opt, bool general = false,
+                bool diag_only = false);
     bool general = false;
     bool no_coarse = false;  // one-level handle without the dense inverse (diagonal drivers only)
     ~MgpisDevice();
@@ -250,8 +252,9 @@ private:
 // The other drivers of the MGPIS class surface (device_krylov.hip), on member 0 of a one-member
 // batch; b, x: device vectors in the fine level's batch nodal layout.  Return iterNumb at exit.
 int64_t krylov_mult_solv(MgpisDevice& D, const double* b, double* x, int64_t maxit, double* relres);
+// attainable: also stop within 100 rtol once the residual is flat (LAGRANGE only, *breakdown = 2)
 int64_t krylov_bicgstab(MgpisDevice& D, int prec, const double* b, double* x, double rtol, int64_t maxit,
-                        double* relres, int* breakdown);
+                        double* relres, int* breakdown, bool attainable = false);
 int64_t krylov_gmres(MgpisDevice& D, int prec, const double* b, double* x, double rtol, int64_t maxit, int64_t restart,
                      double* relres);
 

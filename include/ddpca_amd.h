@@ -127,8 +127,9 @@ int mgpis_gpu_mult_solve(mgpis_t h, const double* b, double* x, int64_t maxit, i
  * preconditioned BiCGSTAB, x0 = 0, shadow residual b, stop on the recursive residual
  * ||r|| <= rtol ||b|| (reference 1e-14) or maxit (reference = rows).  *breakdown (may be NULL)
  * = 1 when rho = 0 ended the run (the reference's "ERROR 1" exit, MGPIS.h:386-389) -- like the
- * reference, x is then returned as it stands.  Returns 0, maxit on the cap, DDPCA_ENUMERIC on
- * NaN/Inf. */
+ * reference, x is then returned as it stands.  These are the only stop rules of this entry point
+ * (LAGRANGE's Newton steps add an attainable-accuracy stop, see ddpca_lagrange_get).  Returns 0,
+ * maxit on the cap, DDPCA_ENUMERIC on NaN/Inf. */
 int mgpis_gpu_bicgstab(mgpis_t h, const double* b, double* x, int prec, double rtol, int64_t maxit,
                        int64_t* iters, double* relres, int* breakdown);
 /* Replaces MGPIS::GMRES_SOLV(precSwit, totaForc, resuSolu) (MGPIS.h:228-348): left-preconditioned
@@ -399,7 +400,11 @@ int64_t ddpca_lagrange_solve(ddpca_lagrange_t h, int device, int prec_type, cons
  * non-mortar nodes in the reference's (body, node) key order: "node" (node ids), "status"
  * (0 open, 1 slip, 2 stick: the active set the step solved with), "lambda" (3 per node,
  * resuLagr: normal, t1, t2), "wedi" (3 per node, nmnoWedi: weighted gap / relative
- * displacement); "solver_iters" and "changes" (per Newton step: BiCGSTAB iterations, seneNumb).
+ * displacement); "solver_iters" and "changes" (per Newton step: BiCGSTAB iterations, seneNumb);
+ * "solver_relres" (per Newton step: BiCGSTAB's recursive ||r|| / ||b|| at exit) and
+ * "solver_breakdown" (0 converged to 1e-14, 1 rho = 0, 2 stopped at the attainable accuracy:
+ * ||r|| <= 1e-12 ||b|| and flat over five iterations -- the singular frictionless systems).  A step
+ * whose solve ends above 1e-10 makes ddpca_lagrange_solve return DDPCA_ENUMERIC.
  * Returns the count (copies min(count, cap) when out != NULL). */
 int64_t ddpca_lagrange_get(ddpca_lagrange_t h, const char* what, int64_t index, double* out, int64_t cap);
 int ddpca_lagrange_destroy(ddpca_lagrange_t h);

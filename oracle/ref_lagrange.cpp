@@ -188,6 +188,9 @@ int main(int argc, char** argv) {
     ddpca_bind::check((int)std::min<int64_t>(tc, 0));
     std::vector<double> its(64);
     const int64_t nst = ddpca_lagrange_get(h, "solver_iters", 0, its.data(), (int64_t)its.size());
+    std::vector<double> rel(64), brk(64);
+    ddpca_lagrange_get(h, "solver_relres", 0, rel.data(), (int64_t)rel.size());
+    ddpca_lagrange_get(h, "solver_breakdown", 0, brk.data(), (int64_t)brk.size());
     // displacements: OUTP_SUB1 of the device's condensed solution vs the reference's resuDisp
     double du = 0.0;
     for (int64_t tv = 0; tv < nsub; ++tv) {
@@ -232,16 +235,25 @@ int main(int argc, char** argv) {
         itf += buf;
     }
     itf += "]";
-    std::string sit = "[", rit = "[";
-    for (int64_t k = 0; k < nst; ++k) sit += (k ? ", " : "") + std::to_string((long)its[k]);
+    std::string sit = "[", rit = "[", srel = "[", sbrk = "[";
+    for (int64_t k = 0; k < nst; ++k) {
+        char nb[32];
+        std::snprintf(nb, sizeof(nb), "%.3e", rel[k]);
+        sit += (k ? ", " : "") + std::to_string((long)its[k]);
+        srel += (k ? ", " : "") + std::string(nb);
+        sbrk += (k ? ", " : "") + std::to_string((int)brk[k]);
+    }
+    srel += "]";
+    sbrk += "]";
     for (size_t k = 0; k < its_ref.size(); ++k) rit += (k ? ", " : "") + std::to_string(its_ref[k]);
     sit += "]";
     rit += "]";
     ddpca_lagrange_destroy(h);
     std::fprintf(stderr,
-                 "{\"newton\": %ld, \"newton_ref\": %ld, \"bicgstab_iters\": %s, \"bicgstab_iters_ref\": %s, \"resuDisp_rel\": %.3g, "
+                 "{\"newton\": %ld, \"newton_ref\": %ld, \"bicgstab_iters\": %s, \"bicgstab_iters_ref\": %s, "
+                 "\"bicgstab_relres\": %s, \"bicgstab_breakdown\": %s, \"resuDisp_rel\": %.3g, "
                  "\"lambda_rel\": %.3g, \"nodes_equal\": %s, \"status_equal\": %s, \"interfaces\": %s}\n",
-                 (long)tc, tc_ref, sit.c_str(), rit.c_str(), du, dl, nodes_equal ? "true" : "false", stat_equal ? "true" : "false",
+                 (long)tc, tc_ref, sit.c_str(), rit.c_str(), srel.c_str(), sbrk.c_str(), du, dl, nodes_equal ? "true" : "false", stat_equal ? "true" : "false",
                  itf.c_str());
     return 0;
 }

@@ -6,10 +6,11 @@ fp16 on the two finest, streamed rows (table_mode 0), automatic exact-solve leve
 iterations per hipGraph replay) and ``HEADLINE_MUSC`` (interface-eliminated coarse space,
 muscSett = 2, doleMcsc = 1).  These tests run that same set:
 
-* reduced chain: ``Problem("dehw", 4, 3, 2, 2, 3, 0.2)`` -- the bench's 8-subdomain batch, 4
-  frictional contacts and 6 glued interfaces, 4 MG levels (21k dof per subdomain), so the automatic
-  exact-solve level lands on level 1 exactly as at the bench's size, and the fine and next level
-  run the fp16 smoother copies.  A fixed-k trajectory (20 ADMM iterations) against the CPU oracle
+* reduced chain: ``headline_problem(gl=3)`` -- the bench's workload (``HEADLINE_WORKLOAD``: 8-subdomain
+  batch, 4 frictional contacts and 6 glued interfaces, contact faces integrated over 4 x 4
+  polygons and glued faces over 2 x 2, i.e. the same integration points per contact node as the
+  bench) at 4 MG levels (21k dof per subdomain), so the automatic exact-solve level lands on level 1
+  exactly as at the bench's size, and the fine and next level run the fp16 smoother copies.  A fixed-k trajectory (20 ADMM iterations) against the CPU oracle
   (oracle.admm, MCONTACT.h:2493-2845, with exact subdomain solves: the SGS-faithful oracle CG to
   1e-14) on the same host operators: resuMoni rows within 1e-6 relative, displacements 1e-7.
 * full size: the bench's own problem (8 x 1.22M dof, 6 levels), one batched ADMM iteration without
@@ -58,10 +59,11 @@ def _oracle_problem(P, oracle):
 
 def test_headline_options_trajectory_matches_oracle(ddpca, oracle, gpu):
     H, M = ddpca.HEADLINE_OPTIONS, ddpca.HEADLINE_MUSC
-    P = ddpca.Problem("dehw", 4, 3, 2, 2, 3, 0.2)
+    P = ddpca.headline_problem(gl=3)
     P.set_coarse(M["muscSett"], [M["doleMcsc"]] * P.nsub)
     P.ESTABLISH()
     assert P.nsub == 8 and P.nint == 10
+    assert len(P.array("ip_w", 0)) == 16 * 6144  # 4 x 4 polygons per contact face
     mc = ddpca.MCONTACT(P, **H)
     k = 20
     assert mc.CONTACT_ANALYSIS(k, check=False) == k
@@ -79,9 +81,61 @@ def test_headline_options_trajectory_matches_oracle(ddpca, oracle, gpu):
         assert np.linalg.norm(g - gr) <= 1e-6 * max(np.linalg.norm(gr), 1e-300), ts
 
 
+def test_headline_density_interface_step_matches_operators(ddpca, oracle, gpu):
+    """The per-ip interface kernels at the bench's integration-point density (k_gamma_ip,
+    k_traction_ip, the wave-per-node k_inpo_node with its multi-pass lane loop: a contact node
+    carries 16 ips per face at ip_contact = 2) against the reference's stored operators
+    (MCONTACT.h:2632-2704) on the device's own state: after iteration 1 read lambda^1, after
+    iteration 2 read u^2, gamma^2, aux^2, lambda^2 and recompute
+      gamma = P(1/2 (inpoLagr_0 lam_0 - inpoLagr_1 lam_1 + pemaInpo_r_0 u_0 - pemaInpo_r_1 u_1)
+                - 1/2 pemaDiag inpoNgap)                                        (2632-2668)
+      aux   = inteMass_pena^-1 (systTran_pena^T u + inteMass lam + inteInpo gamma) (2671-2684)
+      lam'  = lam + inteMass^-1 (systTran_pena^T u - inteMass_pena aux)            (2689-2704)
+    with scipy's sparse products and exact sparse LU solves."""
+    import scipy.sparse.linalg as spla
+    H, M = ddpca.HEADLINE_OPTIONS, ddpca.HEADLINE_MUSC
+    P = ddpca.headline_problem(gl=3)
+    P.set_coarse(M["muscSett"], [M["doleMcsc"]] * P.nsub)
+    P.ESTABLISH()
+    mc = ddpca.MCONTACT(P, **H)
+    assert mc.CONTACT_ANALYSIS(1, check=False) == 1
+    lam1 = {k: mc.get("inteLagr", k) for k in range(2 * P.nint)}
+    assert mc.CONTACT_ANALYSIS(1, check=False) == 1
+    u = [mc.get("resuDisp", tv) for tv in range(P.nsub)]
+    worst = dict(gamma=0.0, aux=0.0, lam=0.0)
+    for ts in range(P.nint):
+        fric = float(P.array("iface_param", ts)[0])
+        comp = 1 if fric == 0.0 else 3
+        body = [int(b) for b in P.array("iface_body", ts)]
+        c = -0.5 * P.array("pemaDiag", ts) * P.array("inpoNgap", ts)
+        for s, sgn in ((0, 1.0), (1, -1.0)):
+            c = c + 0.5 * sgn * (P.csr("inpoLagr", 2 * ts + s) @ lam1[2 * ts + s]
+                                 + P.csr("pemaInpo_r", 2 * ts + s) @ u[body[s]])
+        gr, _ = oracle._project(c, comp, fric)
+        g = mc.get("inpoGamm", ts)
+        assert g.shape == gr.shape
+        eg = np.linalg.norm(g - gr) / max(np.linalg.norm(gr), 1e-300)
+        worst["gamma"] = max(worst["gamma"], eg)
+        assert eg <= 1e-12, (ts, eg)
+        for s in range(2):
+            k = 2 * ts + s
+            St, Mm, Mp = P.csr("systTran_pena", k), P.csr("inteMass", k), P.csr("inteMass_pena", k)
+            rhs = St.T @ u[body[s]] + Mm @ lam1[k] + P.csr("inteInpo", k) @ g
+            ar = spla.spsolve(Mp.tocsc(), rhs)
+            a = mc.get("inteAuxi", k)
+            ea = np.linalg.norm(a - ar) / max(np.linalg.norm(ar), 1e-300)
+            lr = lam1[k] + spla.spsolve(Mm.tocsc(), St.T @ u[body[s]] - Mp @ a)
+            el = np.linalg.norm(mc.get("inteLagr", k) - lr) / max(np.linalg.norm(lr), 1e-300)
+            worst["aux"], worst["lam"] = max(worst["aux"], ea), max(worst["lam"], el)
+            assert ea <= 1e-10, (k, ea)
+            assert el <= 1e-8, (k, el)
+    print(f"headline density ({len(P.array('ip_w', 0))} ips on contact 0): worst rel. gamma {worst['gamma']:.2e}, "
+          f"aux {worst['aux']:.2e}, lambda {worst['lam']:.2e}")
+
+
 def test_headline_fullsize_batched_solves_match_oracle(ddpca, oracle, gpu):
     H = ddpca.HEADLINE_OPTIONS
-    P = ddpca.Problem("dehw", 4, 3, 2, 2, 5, 0.2).ESTABLISH()  # the bench's problem, muscSett = 0
+    P = ddpca.headline_problem().ESTABLISH()  # the bench's problem, muscSett = 0
     assert P.nsub == 8
     mc = ddpca.MCONTACT(P, **H)
     assert mc.CONTACT_ANALYSIS(1, check=False) == 1
@@ -119,7 +173,7 @@ def test_schedule_variants_are_bit_identical(ddpca, gpu, monkeypatch, env):
             monkeypatch.setenv(*env)
         else:
             monkeypatch.delenv(env[0], raising=False)
-        P = ddpca.Problem("dehw", 4, 3, 2, 2, 3, 0.2)
+        P = ddpca.headline_problem(gl=3)
         P.set_coarse(M["muscSett"], [M["doleMcsc"]] * P.nsub)
         P.ESTABLISH()
         mc = ddpca.MCONTACT(P, **H)
@@ -131,3 +185,27 @@ def test_schedule_variants_are_bit_identical(ddpca, gpu, monkeypatch, env):
     for a, b in zip(out["default"][1], out["alt"][1]):
         assert np.array_equal(a, b)
     assert np.array_equal(out["default"][2], out["alt"][2])
+
+
+def test_coarse_correction_kx_from_recursive_residual(ddpca, gpu, monkeypatch):
+    """The coarse-space correction takes consStif[L] x as b - r from PCG's recursive residual
+    (device_mcontact.hip coarse_correct) instead of the reference's explicit product
+    (MCONTACT.h:2585-2587).  On the headline option set (fp16 / fp32 V-cycle copies) the two
+    schedules must agree: resuMoni rows within 1e-8 relative and displacements within 1e-9 after
+    10 ADMM iterations (DDPCA_CS_SPMV=1 forces the explicit fp64 SpMV)."""
+    H, M = ddpca.HEADLINE_OPTIONS, ddpca.HEADLINE_MUSC
+    out = {}
+    for v in ("0", "1"):
+        monkeypatch.setenv("DDPCA_CS_SPMV", v)
+        P = ddpca.headline_problem(gl=3)
+        P.set_coarse(M["muscSett"], [M["doleMcsc"]] * P.nsub)
+        P.ESTABLISH()
+        mc = ddpca.MCONTACT(P, **H)
+        assert mc.CONTACT_ANALYSIS(10, check=False) == 10
+        out[v] = (mc.monitor().copy(), [mc.get("resuDisp", tv).copy() for tv in range(P.nsub)])
+        del mc
+    ok, worst = _rows_close(out["0"][0], out["1"][0], k=10, rtol=1e-8)
+    du = max(np.linalg.norm(a - b) / np.linalg.norm(b) for a, b in zip(out["0"][1], out["1"][1]) if np.any(b))
+    print(f"b - r vs explicit K x: worst resuMoni rel {worst:.2e}, displacements {du:.2e}")
+    assert ok, worst
+    assert du <= 1e-9, du

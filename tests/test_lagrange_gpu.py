@@ -48,6 +48,11 @@ def test_lagrange_matches_reference(gpu, tmp_path, example, prec, fric, tang):
     # that rigid motion -- the reference's BiCGSTAB and an exact LU already differ there by 5 %
     # (tests/test_lagrange.py) -- while the multipliers and the active set are unique
     assert len(res["bicgstab_iters"]) == res["newton"] + 1
+    # every Newton step continued from a converged BiCGSTAB: the reference's 1e-14, or the
+    # attainable-accuracy stop (breakdown code 2, <= 1e-12) on the singular frictionless systems
+    assert len(res["bicgstab_relres"]) == len(res["bicgstab_iters"])
+    for rel, brk in zip(res["bicgstab_relres"], res["bicgstab_breakdown"]):
+        assert brk in (0, 2) and rel <= (1e-14 if brk == 0 else 1e-12) * 1.0001, res
     if example == "block" and fric == "0":  # the patch test: every active node carries the 1e7 load pressure
         for itf in res["interfaces"]:
             if itf["fric"] == 0.0 and itf["nodes"]:
@@ -65,6 +70,9 @@ def test_lagrange_preconditioners_agree(ddpca, gpu):
         lg = ddpca.LAGRANGE.from_problem(P)
         tc = lg.solve(prec)
         runs[prec] = (tc, lg.get("status", 0), lg.get("lambda", 0), lg.get("solver_iters"), lg.get("u", 0))
+        rel, brk = lg.get("solver_relres"), lg.get("solver_breakdown")
+        assert len(rel) == len(brk) == len(runs[prec][3]) == tc + 1
+        assert np.all((brk == 0) & (rel <= 1e-14 * 1.0001) | (brk == 2) & (rel <= 1e-12 * 1.0001)), (prec, rel, brk)
     (t1, s1, l1, i1, u1), (t2, s2, l2, i2, u2) = runs[1], runs[2]
     print("newton", t1, t2, "iters", i1, i2)
     assert t1 == t2 and np.array_equal(s1, s2)
