@@ -246,15 +246,20 @@ def cpu_baseline(P, mc, budget_s=20.0):
     """SGS-faithful CPU port (oracle/cpu_admm.py, MGPIS.h + MCONTACT.h) pricing one full ADMM
     iteration at the state the device run reached: sampled subdomain CG_SOLV(1) solves, the whole
     coarse-space correction and interface step.  `reference_equivalent` rescales it by the
-    container measurement of the reference's own CG_SOLV against the port on the same mesh and
-    cores (profiles/cpu_calibration.py), since the reference never travels to the GPU box."""
+    measured ratio of the reference's own CG_SOLV (oracle/_ref/ref_harness_portable, compiled from
+    /root/reference's headers) to the port on the same BEAM mesh (profiles/cpu_calibration.py),
+    timed ON THE GPU HOST at its 16 threads (profiles/r03_cpu_calibration_host.json); the
+    container's 8-thread ratio is the fallback."""
     from oracle import cpu_admm
     res = cpu_admm.price_iteration(P, mc, budget_s)
-    cal = ROOT / "profiles" / "r02_cpu_calibration.json"
+    cal = ROOT / "profiles" / "r03_cpu_calibration_host.json"
+    if not cal.exists():
+        cal = ROOT / "profiles" / "r02_cpu_calibration.json"
     if cal.exists():
         c = json.loads(cal.read_text())
         res["calibration"] = {"ref_over_port": c["ref_over_port"], "mesh": c["mesh"], "threads": c["threads"],
-                              "source": str(cal.relative_to(ROOT))}
+                              "cpu": c.get("cpu"), "reference_s": c["reference"]["median_s"],
+                              "port_s": c["port"]["median_s"], "source": str(cal.relative_to(ROOT))}
         res["reference_equivalent"] = res["value"] / c["ref_over_port"]
     return res
 
