@@ -138,6 +138,12 @@ def main():
     elapsed = time.perf_counter() - t0
     log(rank, f"{n} ADMM iterations in {elapsed:.3f} s")
     tm = mc.timing()
+    by = mc.bytes()  # algorithmic bytes of the timed iterations per phase (mcontact_gpu_bytes)
+    phases = list(mc.BYTE_PHASES)
+    if world > 1:
+        t = torch.tensor([by[k] for k in phases], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        by.update({k: float(v) for k, v in zip(phases, t)})
     if world > 1:
         t = torch.tensor([elapsed, tm["dof_iterations"], tm["pcg_iterations"]], dtype=torch.float64)
         tmax = t.clone()
@@ -219,6 +225,21 @@ def main():
                 "samples": int(tm["spmv_samples"]),
             },
         }
+        # whole-step roofline: the algorithmic bytes of EVERY kernel
+        # of an ADMM iteration (byte model per kernel, DESIGN.md §3, summed over the members'
+        # actual iteration counts) / the measured time per ADMM iteration / the HBM peak
+        step_bytes = sum(by[k] for k in phases) / max(n, 1)
+        step_s = elapsed / max(n, 1)
+        split = {"fine_level_pcg": by["pcg_fine"], "coarse_levels_and_scalars": by["pcg_coarse"],
+                 "coarse_space": by["coarse_space"], "mass_cg": by["mass_cg"],
+                 "interface_rhs_monitor": by["interface"] + by["body_rhs"] + by["monitor"]}
+        result["roofline"].update({
+            "step_bytes": step_bytes,
+            "step_achieved": step_bytes / step_s / 1e9,
+            "step_frac": step_bytes / step_s / 1e9 / HBM_PEAK_GBS,
+            "step_split_bytes": {k: v / max(n, 1) for k, v in split.items()},
+            "pcg_launches_per_admm_iter": by["pcg_launches"] / max(n, 1),
+        })
         if world == 1 and not a.no_cpu_baseline:
             result["cpu_baseline"] = cpu_baseline(P, mc)
     # release device state before the process group

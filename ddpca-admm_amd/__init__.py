@@ -162,6 +162,8 @@ def _declare(L: C.CDLL) -> None:
         L.mcontact_gpu_get.argtypes = [_P, C.c_char_p, C.c_int64, _P, C.c_int64]
         L.mcontact_gpu_get.restype = C.c_int64
         L.mcontact_gpu_timing.argtypes = [_P, _DP]
+        L.mcontact_gpu_bytes.argtypes = [_P, _DP, C.c_int64]
+        L.mcontact_gpu_bytes.restype = C.c_int64
         L.mcontact_gpu_destroy.argtypes = [_P]
 
 
@@ -789,6 +791,17 @@ class MCONTACT:
         keys = ["total_ms", "solve_ms", "iface_ms", "comm_ms", "spmv_kernel_ms", "spmv_samples", "pcg_iterations",
                 "spmv_bytes_per_launch", "dof_iterations", "owned_dofs"]
         return dict(zip(keys, list(out)))
+
+    BYTE_PHASES = ("pcg_fine", "pcg_coarse", "coarse_space", "body_rhs", "interface", "mass_cg", "monitor")
+
+    def bytes(self) -> dict:
+        """Algorithmic HBM bytes of the last CONTACT_ANALYSIS call per phase (mcontact_gpu_bytes),
+        plus the body-balance PCG's kernel launches."""
+        out = (C.c_double * 8)()
+        _check(lib().mcontact_gpu_bytes(self._h, out, 8))
+        d = dict(zip(self.BYTE_PHASES, list(out)[:7]))
+        d["pcg_launches"] = out[7]
+        return d
 
 
 __all__ = ["Problem", "MULTIGRID", "MGPIS", "MCONTACT", "DdpcaError", "lib", "gpu_available", "default_options",

@@ -587,6 +587,9 @@ struct SellOp {
     DevBuf<int32_t> slots, col;
     DevBuf<int64_t> off;
     DevBuf<double> val;
+    // algorithmic bytes of one apply: the stored entries (8 B value + 4 B column), each distinct
+    // gathered W entry once, every real row written once (an `add` operand adds 8 B per row)
+    double bytes = 0.0;
     void build(const Rows& rows) {
         nrow = pad64((int64_t)rows.size());
         nch = nrow / 64;
@@ -612,6 +615,15 @@ struct SellOp {
         off.upload(of);
         col.upload(co);
         val.upload(va);
+        int64_t ent = 0;
+        std::vector<int64_t> cols;
+        for (const auto& r : rows) {
+            ent += (int64_t)r.size();
+            for (const auto& e : r) cols.push_back(e.first);
+        }
+        std::sort(cols.begin(), cols.end());
+        const int64_t uniq = (int64_t)(std::unique(cols.begin(), cols.end()) - cols.begin());
+        bytes = 12.0 * (double)ent + 8.0 * (double)uniq + 8.0 * (double)rows.size();
     }
     void apply(hipStream_t s, const double* W, double* y, const double* add) const {
         if (nch) hipLaunchKernelGGL(k_sell_w, dim3(ceil_div(nch, 4)), dim3(256), 0, s, slots.p, off.p, col.p, val.p, nch, W, y, add);
@@ -653,6 +665,7 @@ public:
     MirrorBuf mirror;
     int64_t k = 8;
     int64_t last_iters = 0;
+    double alg_bytes = 0.0;  // accumulated by check(): init + iterations of every system
 
     // A[i] = system i (rows m_i), placed at rows roff[i] (multiples of 64) of nrow_total.
     void build(const std::vector<const Csr*>& A, const std::vector<int64_t>& roff, int64_t nrow_total) {
@@ -699,6 +712,16 @@ public:
         dinv.upload(di);
         cb.upload(c0);
         cb_host_ = c0;
+        // algorithmic bytes per system: init (b, D^-1 read; x r z p q written: 56 B per row) and
+        // per CG iteration -- k_mcg_spmv: stored entries (12 B), z gathered once, z, q, p read
+        // and q, p written; k_mcg_axpy: x, r read + written, z written, p, q, D^-1 read (112 B per row)
+        init_bytes_.assign(nsys, 0.0);
+        it_bytes_.assign(nsys, 0.0);
+        for (int s = 0; s < nsys; ++s) {
+            const double rows = (double)A[s]->nrow, ent = (double)A[s]->nnz();
+            init_bytes_[s] = 56.0 * rows;
+            it_bytes_[s] = 12.0 * ent + 8.0 * rows + 40.0 * rows + 64.0 * rows;
+        }
         for (auto* v : {&b, &x, &r, &z, &p, &q}) {
             v->alloc(std::max<int64_t>(nrow, 2));
             v->zero();
@@ -722,6 +745,7 @@ public:
     // x_out (nrow) = A^-1 b.  Asynchronous on `s` except for the host pacing of replays.
     void solve(hipStream_t s, double* x_out, double rtol, int64_t maxit) {
         if (nsys == 0) return;
+        solved_ = true;
         if (x_out != x_target_) {
             if (split_) {
                 for (auto& g : graph_h_)
@@ -801,7 +825,9 @@ public:
         for (int i = 0; i < nsys; ++i) {
             if (mirror.host[i].fail) throw ApiError(DDPCA_ENUMERIC, "surface mass CG breakdown");
             last_iters = std::max<int64_t>(last_iters, mirror.host[i].iter);
+            if (solved_) alg_bytes += init_bytes_[i] + (double)mirror.host[i].iter * it_bytes_[i];
         }
+        solved_ = false;
     }
 
 private:
@@ -815,6 +841,8 @@ private:
     DevBuf<int32_t> half_;
     std::vector<int> half_host_;
     std::vector<int64_t> cb_host_;
+    std::vector<double> init_bytes_, it_bytes_;
+    bool solved_ = false;
     void capture(hipStream_t s) {
         if (split_) {
             capture_one(s, sc_half_.p, &graph_h_[0]);
@@ -878,6 +906,7 @@ struct CoarseDev {
     DevBuf<int32_t> pcol, ptgt, cdof;
     DevBuf<double> pval;
     std::vector<int64_t> own_rows;  // global coarse rows of this rank, in xc order
+    double bytes_iter = 0.0;        // algorithmic bytes of one correction (without DOUBLE_M's PCG)
     std::vector<double> dense;      // host, until inverted: this rank's rows of globCoup_1 (n x n, zeros elsewhere)
     // DOUBLE_M_1 (MCONTACT.h:2303-2341; the reference's choice once globCoup_1 has DIRE_MAXI rows,
     // 1857-1865): the coarse problem solved by its own MGPIS-PCG, redundantly on every rank, on a
@@ -1059,6 +1088,7 @@ struct ddpca_mcontact {
         DevBuf<int64_t> nptr[2];
         DevBuf<int32_t> niq[2];
         DevBuf<double> ncoef[2];
+        double bytes_gamma = 0.0, bytes_inpo = 0.0;  // algorithmic bytes of k_gamma_ip / k_traction_ip + k_inpo_node
     };
     std::vector<FactItf> fitfs;
     MassBatch mb_aux, mb_lam;
@@ -1080,6 +1110,13 @@ struct ddpca_mcontact {
     std::vector<std::vector<double>> rows;
     double timing[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     double mass_iters = 0.0;
+    // algorithmic HBM bytes since the last mcontact_gpu_iterate started (include/ddpca_amd.h,
+    // mcontact_gpu_bytes): [0] fine-level PCG kernels, [1] PCG kernels below the fine level + the
+    // scalar kernels, [2] coarse-space correction, [3] body-balance RHS + OUTP_SUB1, [4] interface
+    // products and projection, [5] batched surface-mass CG, [6] MONITOR snapshot + norms,
+    // [7] body-balance PCG launches
+    double bytes[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    double bytes_rhs = 0.0, bytes_iface = 0.0, bytes_moni = 0.0;  // per ADMM iteration (model, build)
     mgpis_options_t opt{};
 };
 
@@ -1264,10 +1301,19 @@ void build(ddpca_mcontact& H, Problem& P) {
             }
             F.nnc[s] = (int64_t)bynode.size();
             F.roff[s] = sd.roff;
+            // k_gamma_ip's share of this side: shape values, lambda and u indices per ip, the
+            // side's contact-node lambda (C per node) and body-node u (3 per node) once;
+            // k_inpo_node: index + coefficient per (node, ip) entry, the node's C outputs
+            F.bytes_gamma += 48.0 * (double)nip + (double)F.nnc[s] * 8.0 * (F.C + 3);
+            F.bytes_inpo += 12.0 * (double)iq.size() + 8.0 * F.C * (double)nip + 8.0 * F.C * (double)F.nnc[s];
             F.nptr[s].upload(ptr);
             F.niq[s].upload(iq.empty() ? std::vector<int32_t>{0} : iq);
             F.ncoef[s].upload(coef.empty() ? std::vector<double>{0.0} : coef);
         }
+        // per ip: the 3x3 basis, gamma written and the constant part read (k_gamma_ip); basis,
+        // gamma read and the traction written (k_traction_ip)
+        F.bytes_gamma += (double)nip * (72.0 + 16.0 * F.C);
+        F.bytes_inpo += (double)nip * ((F.C == 3 ? 72.0 : 0.0) + 16.0 * F.C);
         H.fitfs.push_back(std::move(F));
     }
     // ---- interface operators over W (MCONTACT.h:2632-2636, 2671-2704)
@@ -1438,6 +1484,14 @@ void build(ddpca_mcontact& H, Problem& P) {
             cptr.push_back((int64_t)ccol.size());
         }
         H.ncrow = (int64_t)crow.size();
+        {
+            // k_cpl: entries, the row's target index and pointer, b read + written, W's aux and
+            // lambda entries once
+            std::vector<int32_t> uc(ccol);
+            std::sort(uc.begin(), uc.end());
+            const double uniq = (double)(std::unique(uc.begin(), uc.end()) - uc.begin());
+            H.bytes_rhs += 12.0 * (double)ccol.size() + 28.0 * (double)H.ncrow + 8.0 * uniq;
+        }
         H.crow.upload(crow);
         H.cptr.upload(cptr);
         H.ccol.upload(ccol);
@@ -1452,6 +1506,27 @@ void build(ddpca_mcontact& H, Problem& P) {
                 for (int64_t k = Hp.ptr[r]; k < Hp.ptr[r + 1]; ++k) rh[S.hoff + r].push_back({S.wcol(Hp.col[k], H.oH), Hp.val[k]});
         }
         H.op_hang.build(rh);
+    }
+    // per-ADMM-iteration byte model of the launches outside the PCG, mass CG and coarse space
+    {
+        double nu = 0.0, rows = 0.0;
+        for (auto& S : H.subs) nu += 3.0 * (double)S.nn + (double)S.nh;
+        for (auto& sd : H.sides) rows += (double)sd.m;
+        double fine_nodes = 0.0;
+        for (auto& S : H.subs) fine_nodes += (double)S.nn;
+        // consForc copied into b (16 B per dof), k_outp (x, presc read, u written, mask, node map:
+        // 77 B per node), the hanging rows
+        H.bytes_rhs += 16.0 * 3.0 * fine_nodes + 77.0 * fine_nodes + (H.NH ? H.op_hang.bytes : 0.0);
+        // interface: gamma (stored rows + the constant), factored per-ip kernels, projection,
+        // the aux / lambda right-hand sides, the fused update (or the lambda add)
+        H.bytes_iface += H.op_gamma.nch ? H.op_gamma.bytes + 8.0 * (double)H.op_gamma.nrow : 0.0;
+        for (auto& F : H.fitfs) H.bytes_iface += F.bytes_gamma + (H.fused ? F.bytes_inpo : 0.0);
+        for (auto& I : H.itfs)
+            if (I.mine) H.bytes_iface += (double)(I.mip / I.comp) * (16.0 * I.comp + 4.0) + (I.cross ? 24.0 * I.mip : 0.0);
+        if (H.fused) H.bytes_iface += H.op_wv.bytes + 56.0 * rows;
+        else if (!H.sides.empty()) H.bytes_iface += H.op_aux.bytes + H.op_lam.bytes + 24.0 * rows;
+        // MONITOR: snapshots of u and [aux, lambda] (read + written), the pair norms (16 B per entry)
+        H.bytes_moni = 16.0 * (nu + 2.0 * rows) + 16.0 * (nu + 2.0 * rows);
     }
     int64_t maxn = 1;
     for (auto& S : H.subs) maxn = std::max(maxn, std::max(3 * S.nn, S.nh));
@@ -1671,6 +1746,11 @@ void build_coarse(ddpca_mcontact& H, Problem& P) {
         C.rptr.upload(ptr);
         C.rcol.upload(col.empty() ? std::vector<int32_t>{0} : col);
         C.rval.upload(val.empty() ? std::vector<double>{0.0} : val);
+        // right-hand side CSR over W: entries, each distinct W entry once, f0 read and g written
+        std::vector<int32_t> uc(col);
+        std::sort(uc.begin(), uc.end());
+        const double uniq = (double)(std::unique(uc.begin(), uc.end()) - uc.begin());
+        C.bytes_iter = 12.0 * (double)col.size() + 8.0 * uniq + 16.0 * (double)n;
     }
     std::vector<double> f0(n, 0.0);
     for (int64_t r : C.own_rows) f0[r] = cs.globForc_1[r];
@@ -1683,6 +1763,10 @@ void build_coarse(ddpca_mcontact& H, Problem& P) {
     // LATIN: DOUBLE_M (MCONTACT.h:1236) with the host MULTISCALE's coarse contact nodes, one rank
     C.mg = n >= (mg_env ? std::atoll(mg_env) : 120000) && (!cs.latin || (!cs.rank_local && !cs.coarNode.empty()));
     C.latin = cs.latin;
+    // coarse solve: the owned rows of the dense inverse against g, or (DOUBLE_M) g scattered into
+    // the coarse MGPIS and its owned rows gathered back (its PCG is counted by its own model)
+    C.bytes_iter += C.mg ? 20.0 * (double)n + 24.0 * (double)C.nown
+                         : 8.0 * (double)C.nown * (double)n + 8.0 * (double)n + 8.0 * (double)C.nown;
     if (C.mg) {
         if (H.mg && C.nown) build_coarse_mg(H, mc, C);
     } else {
@@ -1722,6 +1806,9 @@ void build_coarse(ddpca_mcontact& H, Problem& P) {
         }
         C.npr = (int64_t)tgt.size();
         C.ncd = (int64_t)cd.size();
+        // u += accuProl x_c on the free rows (entries, target index, u read + written), the
+        // constrained rows' prescribed values again
+        C.bytes_iter += 12.0 * (double)col.size() + 20.0 * (double)C.npr + 28.0 * (double)C.ncd;
         C.pptr.upload(ptr);
         C.pcol.upload(col.empty() ? std::vector<int32_t>{0} : col);
         C.pval.upload(val.empty() ? std::vector<double>{0.0} : val);
@@ -1792,6 +1879,24 @@ void build_coarse(ddpca_mcontact& H, Problem& P) {
     C.qcol.upload(qcol);
     C.qw.upload(qw);
     C.flag.upload(flag);
+    // factored stiffness part and prolongation: K x = b - r (b, r read, the difference written:
+    // 72 B per fine node), the plain restriction chain down to dmin (r_f once, mask + b_c per
+    // coarse node, the lattice's child mask + fine copy or the stencil's index + weight), the
+    // gather of level-d values into g, x_c scattered to nodal xn, and u += (Q (x) I3) xn: Q's
+    // entries, flags, u read + written, xn once
+    double nf = 0.0, qent = 0.0, kp = 0.0;
+    for (size_t i = 0; i < H.subs.size(); ++i) {
+        nf += (double)H.subs[i].nn;
+        qent += (double)cs.accuQ[H.subs[i].tv].col.size();
+        for (int l = L; l > C.dmin; --l) {
+            const LevelDev& F = D.lev[l];
+            kp += 24.0 * (double)F.nloc[i] + (25.0 + (F.lat ? 8.0 : 0.0)) * (double)D.lev[l - 1].nloc[i] +
+                  (F.lat ? 0.0 : 12.0 * (double)F.tent_sub[i]);
+        }
+    }
+    double krows = 0.0;
+    for (auto& kv : groups) krows += (double)kv.second.first.size();
+    C.bytes_iter += 72.0 * nf + kp + 36.0 * krows + 20.0 * (double)nxn + 12.0 * qent + 51.0 * nf + 8.0 * (double)nxn;
 }
 
 // globCoup_1^-1 rows of the owned subdomains: every rank's rows are summed into a full dense
@@ -2002,7 +2107,8 @@ bool iterate_once(ddpca_mcontact& H, bool check) {
     }
     // ---- coarse-space correction (MCONTACT.h:2540-2612); OUTP_SUB1 of the correction reaches the
     //      hanging level through the same rows, so they are recomputed from the corrected u
-    if (H.cs.on && H.tc <= H.mult_maxi) {
+    const bool cs_ran = H.cs.on && H.tc <= H.mult_maxi;
+    if (cs_ran) {
         coarse_correct(H);
         if (H.NH) H.op_hang.apply(st, H.W.p, H.W.p + H.oH, nullptr);
     }
@@ -2103,6 +2209,27 @@ bool iterate_once(ddpca_mcontact& H, bool check) {
             D.timed_kernel_samples = 0;
         }
     }
+    if (H.mg) {
+        MgpisDevice& D = *H.mg;
+        H.bytes[0] += D.alg_bytes[0];
+        H.bytes[1] += D.alg_bytes[1];
+        H.bytes[7] += D.alg_bytes[2];
+        D.alg_bytes[0] = D.alg_bytes[1] = D.alg_bytes[2] = 0.0;
+    }
+    if (cs_ran) {
+        H.bytes[2] += H.cs.bytes_iter;
+        if (H.cs.cmg) {
+            H.bytes[2] += H.cs.cmg->alg_bytes[0] + H.cs.cmg->alg_bytes[1];
+            H.cs.cmg->alg_bytes[0] = H.cs.cmg->alg_bytes[1] = H.cs.cmg->alg_bytes[2] = 0.0;
+        }
+    }
+    H.bytes[3] += H.bytes_rhs;
+    H.bytes[4] += H.bytes_iface;
+    for (MassBatch* mb : {&H.mb_aux, &H.mb_lam, &H.mb_wv}) {
+        H.bytes[5] += mb->alg_bytes;
+        mb->alg_bytes = 0.0;
+    }
+    H.bytes[6] += H.bytes_moni;
     const bool conv = monitor(H);
     H.tc += 1;
     return check && conv;
@@ -2197,6 +2324,7 @@ int64_t mcontact_gpu_iterate(mcontact_t h, int64_t maxit, int check) {
     const int rc = guarded([&] {
         select_device(h->device);
         for (double& t : h->timing) t = 0.0;
+        for (double& b : h->bytes) b = 0.0;
         h->mass_iters = 0.0;
         if (h->mg) h->mg->time_kernel = true;
         for (; n < maxit;) {
@@ -2294,6 +2422,13 @@ int mcontact_gpu_timing(mcontact_t h, double* out10) {
         for (int64_t nf : h->mg->nfree) dofs += (double)nf;
     out10[9] = dofs;
     return DDPCA_OK;
+}
+
+int64_t mcontact_gpu_bytes(mcontact_t h, double* out, int64_t cap) {
+    const int64_t n = (int64_t)(sizeof(h->bytes) / sizeof(double));
+    if (out)
+        for (int64_t i = 0; i < std::min(n, cap); ++i) out[i] = h->bytes[i];
+    return n;
 }
 
 int mcontact_gpu_destroy(mcontact_t h) {

@@ -1625,12 +1625,16 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
                 double b[9];
             };
             std::deque<ExtraEnt> extra;  // scalar parents past the eighth, as blocks
+            L.tent_sub.assign(nsub, 0);
+            L.tblk_sub.assign(nsub, 0);
             for (int s = 0; s < nsub; ++s) {
                 const Stencil& st = *subs[s].S[l - 1];
                 const auto& pf = perm[l][s];
                 const auto& pc = perm[l - 1][s];
                 const int64_t nc = C.nloc[s];
                 if (st.nf != L.nloc[s] || st.nc != nc) throw ApiError(DDPCA_EINVAL, "stencil shape");
+                L.tblk_sub[s] = (int64_t)st.bent.size();
+                L.tent_sub[s] = (int64_t)st.col.size() - L.tblk_sub[s];
                 // block entries (weight 0 in the scalar stencil) run in k_prolong_rot / k_restrict_rot
                 // only: they take no parent slot (a node may have any number of them)
                 std::vector<uint8_t> isblk(st.col.size(), 0);
@@ -2343,6 +2347,85 @@ double MgpisDevice::fine_kernel_bytes(int s) const {
     return fine_matrix_bytes(s, kVal64) + 24.0 * 5.0 * (double)lev.back().nloc[s];
 }
 
+// ---- algorithmic byte model of the solve path (per member s; bytes every kernel must move at
+// least once: streamed operator values + column indices, each vector read / written once, a
+// gathered vector counted once per element).  The launch sequence is the one vcycle() and
+// enqueue_iteration() issue; the sizes are the member's real (unpadded) nodes.
+namespace {
+double vbytes(int vt) { return vt == kValH16 ? 20.0 : vt == kVal32 ? 36.0 : 72.0; }
+}  // namespace
+
+void MgpisDevice::vcycle_bytes(int s, double out[2]) const {
+    out[0] = out[1] = 0.0;
+    const int nlev = (int)lev.size(), Lf = nlev - 1, cl = clev;
+    const bool bj = opt.smoother >= 1, cheb = opt.smoother == 2;
+    auto n = [&](int l) { return (double)lev[l].nloc[s]; };
+    auto mat = [&](int l) {  // one pass over the V-cycle's copy of level l
+        const LevelDev& L = lev[l];
+        if (L.tbl) return 4.0 * (double)L.nnzb_sub[s] + 4.0 * n(l);
+        return (vbytes(vc_type(l)) + (L.col16.p ? 2.0 : 4.0)) * (double)L.nnzb_sub[s];
+    };
+    auto minv = [&](int l) { return (bj ? 9.0 : 3.0) * (vc_type(l) != kVal64 ? 4.0 : 8.0); };
+    auto put = [&](int l, double b) { out[l == Lf ? 0 : 1] += b; };
+    // x' = x + w M (b - K x): operator, x gathered, b, M^-1, x' (Chebyshev: d read + written)
+    auto sweep = [&](int l) { return mat(l) + n(l) * (24.0 * 3 + minv(l) + (cheb ? 48.0 : 0.0)); };
+    const double n0 = 3.0 * (double)lev[cl].nloc[s];
+    const double coarse = (ainv32.p ? 4.0 : 8.0) * n0 * n0 + 16.0 * n0;  // dense inverse + b in, x out
+    if (Lf == cl) {
+        out[0] += coarse + 16.0 * n0;  // + the dot product's second read
+        return;
+    }
+    put(Lf, n(Lf) * (48.0 + minv(Lf) + (cheb ? 24.0 : 0.0)));  // k_jac0: b in, x out
+    for (int l = Lf; l >= cl + 1; --l) {
+        for (int k = 1; k < opt.nu; ++k) put(l, sweep(l));
+        put(l, mat(l) + 72.0 * n(l));  // residual: x gathered, b, r
+        const LevelDev& F = lev[l];
+        const int c = l - 1;
+        const bool init = c != cl;
+        // coarse node: mask + b_c written (+ x_c = w M b_c: M^-1 read, x_c written; Chebyshev d_c)
+        double cn = 1.0 + 24.0 + (init ? minv(c) + 24.0 + (cheb ? 24.0 : 0.0) : 0.0);
+        double tr = 24.0 * n(l);  // r_f read once
+        if (F.lat) cn += 8.0;     // 27-bit child mask + fine copy
+        else tr += 12.0 * (double)F.tent_sub[s];  // child index + weight per stencil entry
+        tr += 4.0 * 8.0 * (double)F.tblk_sub[s] + (F.tblk_sub[s] ? 24.0 * n(c) : 0.0);  // block entries (B^T r_f)
+        put(l, tr + cn * n(c));
+    }
+    put(cl, coarse);
+    for (int l = cl + 1; l <= Lf; ++l) {
+        const LevelDev& F = lev[l];
+        // x_f += mask P e_c: e_c read once, mask, x_f read + written, the parent encoding
+        double pb = 24.0 * n(l - 1) + n(l) * (1.0 + 48.0);
+        if (F.lat) pb += 4.0 * n(l);
+        else pb += (F.uw ? 4.0 : 12.0) * (double)F.tent_sub[s];
+        pb += 4.0 * 8.0 * (double)F.tblk_sub[s];
+        put(l, pb);
+        for (int k = 0; k < opt.nu; ++k) put(l, sweep(l));
+    }
+}
+
+void MgpisDevice::iteration_bytes(int s, double out[2]) const {
+    vcycle_bytes(s, out);
+    const LevelDev& F = lev.back();
+    const double n = (double)F.nloc[s], nch = (double)pad64(F.nloc[s]) / kChunk;
+    out[0] += fine_kernel_bytes(s) + 144.0 * n;  // k_sell<kPcg> + k_axpy (x, r read + written, p, q read)
+    out[1] += 3.0 * 8.0 * nch;                   // three k_fin passes over the chunk partials
+}
+
+void MgpisDevice::setup_bytes(int s, double out[2]) const {
+    vcycle_bytes(s, out);
+    const LevelDev& F = lev.back();
+    const double n = (double)F.nloc[s], nch = (double)pad64(F.nloc[s]) / kChunk;
+    out[0] += 120.0 * n;  // k_pcg_init: b read, x r p q written
+    out[1] += 2.0 * 8.0 * nch;
+}
+
+int64_t MgpisDevice::iteration_launches() const {
+    // k_sell<kPcg>, k_axpy, 3 x k_fin, and the V-cycle: jac0 + per descended level (nu - 1 sweeps,
+    // residual, restriction) + coarse + per ascended level (prolongation, nu sweeps)
+    const int64_t nd = (int64_t)lev.size() - 1 - clev;
+    return 5 + (nd == 0 ? 2 : 1 + nd * (opt.nu + 1) + 1 + nd * (1 + opt.nu));
+}
+
 // k_fin over every member (1024 threads, or 256 with DDPCA_FIN_THREADS=256)
 void MgpisDevice::launch_fin(hipStream_t st, int what, const double* part, const double* part2, const int64_t* cb,
                              PcgScal* scp, PcgMirror* mir) {
@@ -2507,6 +2590,7 @@ int64_t pace_halves(hipStream_t st[2], hipGraphExec_t g[2], const MirrorBuf& m, 
 
 void MgpisDevice::pcg_begin(int prec, double rtol, const std::vector<int64_t>& maxit, bool warm) {
     select_device(device);
+    solve_accounted_ = prec != 1 || warm;  // the byte model covers the V-cycle PCG from x0 = 0
     if ((int)maxit.size() != nsub) throw ApiError(DDPCA_EINVAL, "maxit per subdomain");
     build_graph(prec);
     LevelDev& L = lev.back();
@@ -2605,6 +2689,30 @@ void MgpisDevice::pcg_check() {
     }
     for (int s = 0; s < nsub; ++s)
         if (sc_host[s].fail) throw ApiError(DDPCA_ENUMERIC, "PCG breakdown (non-finite or non-positive curvature) in batch member " + std::to_string(s));
+    if (!no_coarse && !solve_accounted_) {
+        // algorithmic bytes of the solve that just finished: members done at initialisation moved
+        // only k_pcg_init's share; the others ran iter SpMVs and iter V-cycles (the setup's
+        // first one and iter - 1 more: the converging iteration skips its V-cycle)
+        for (int s = 0; s < nsub; ++s) {
+            const double n = (double)lev.back().nloc[s];
+            if (sc_host[s].iter == 0) {
+                alg_bytes[0] += 120.0 * n;
+                continue;
+            }
+            double a[2], b[2];
+            setup_bytes(s, a);
+            iteration_bytes(s, b);
+            double v[2];
+            vcycle_bytes(s, v);
+            const double it = (double)sc_host[s].iter;
+            alg_bytes[0] += a[0] + it * b[0] - v[0];
+            alg_bytes[1] += a[1] + it * b[1] - v[1];
+        }
+        int64_t itmax = 0;
+        for (int s = 0; s < nsub; ++s) itmax = std::max<int64_t>(itmax, sc_host[s].iter);
+        alg_bytes[2] += (double)(itmax * iteration_launches());
+        solve_accounted_ = true;
+    }
 }
 
 void MgpisDevice::pcg_solve(int prec, double rtol, const std::vector<int64_t>& maxit, bool warm) {

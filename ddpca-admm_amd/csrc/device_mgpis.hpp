@@ -97,6 +97,7 @@ struct LevelDev {
     DevBuf<double> coef;   // [(sweep * nsub + sub) * 2 + {0,1}]: Chebyshev (c1, c2) / Jacobi (-, omega)
     std::vector<double> lmax;  // per subdomain, lambda_max(M K)
     // transfer from level l-1 (batch-global indices)
+    std::vector<int64_t> tent_sub, tblk_sub;  // per subdomain: scalar stencil entries, 3x3 block entries
     DevBuf<int32_t> ppar;  // 8 x nn, slot-major, -1 = unused
     DevBuf<double> pw;     // weights (empty when uw)
     bool uw = false;       // uniform averaging: prolongation weight = 1 / parent count (nested
@@ -212,6 +213,19 @@ public:
     int64_t timed_kernel_samples = 0;
     bool time_kernel = false;
     double fine_kernel_bytes(int s) const;  // algorithmic bytes of the timed kernel, member s
+    // Algorithmic HBM bytes of the solve path (every input read once, every output
+    // written once, gathered operands counted once per unique element), accumulated by pcg_check
+    // over the members' iteration counts: [0] fine-level kernels (the Krylov SpMV, k_axpy and the
+    // V-cycle's launches on the fine level, including the transfers to and from it), [1] every
+    // launch below the fine level (coarser sweeps, residuals, transfers, the dense coarse solve)
+    // and the scalar kernels, [2] launches counted
+    double alg_bytes[3] = {0.0, 0.0, 0.0};
+    // model per member s: one PCG iteration (SpMV + axpy + V-cycle + scalars), split as above;
+    // setup: x0 = 0 initialisation + the first V-cycle
+    void iteration_bytes(int s, double out[2]) const;
+    void setup_bytes(int s, double out[2]) const;
+    void vcycle_bytes(int s, double out[2]) const;
+    int64_t iteration_launches() const;
     // operator bytes of one fine pass, member s (prod_cols: with the 16-bit column offsets the
     // production kernels use; the mgpis_gpu_bench_spmv variants read 32-bit columns)
     double fine_matrix_bytes(int s, int vt, bool prod_cols = true) const;
@@ -244,6 +258,7 @@ private:
     void launch_fin(hipStream_t st, int what, const double* part, const double* part2, const int64_t* cb, PcgScal* scp,
                     PcgMirror* mir);
     bool sample_pending_ = false;
+    bool solve_accounted_ = true;
     void build_graph(int prec);
     void enqueue_iteration(int prec, bool timed);
     void estimate_lmax(int level);

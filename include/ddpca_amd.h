@@ -361,6 +361,15 @@ int64_t mcontact_gpu_get(mcontact_t h, const char* what, int64_t index, void* ou
  * SpMV launches), spmv_samples, pcg_iterations (summed over owned subdomain solves),
  * spmv_bytes_per_launch (algorithmic), dof_iterations (sum n_free * PCG its), owned_dofs] */
 int mcontact_gpu_timing(mcontact_t h, double* out10);
+/* Algorithmic HBM bytes of the last iterate() call, summed over its iterations (SURVEY §8 d4:
+ * streamed operators and every vector read / written once, gathered operands once per distinct
+ * element; each kernel's model in DESIGN.md §3).  out[0] fine-level PCG kernels (Krylov SpMV,
+ * k_axpy, the V-cycle's fine-level sweeps, residuals and transfers), [1] V-cycle launches below
+ * the fine level + the PCG scalar kernels, [2] coarse-space correction, [3] body-balance RHS and
+ * OUTP_SUB1, [4] interface products + projection, [5] batched surface-mass CG, [6] MONITOR
+ * snapshots and norms, [7] body-balance PCG kernel launches (not bytes).  Returns the count (8);
+ * copies min(8, cap) when out != NULL.  No equivalent in the reference (measurement only). */
+int64_t mcontact_gpu_bytes(mcontact_t h, double* out, int64_t cap);
 int mcontact_gpu_destroy(mcontact_t h);
 
 /* ========================================================================================
