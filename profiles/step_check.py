@@ -55,7 +55,8 @@ def split_iterations(seq):
             seen_red = True
     if cur:
         its.append(cur)
-    return its
+    # ADMM iterations only (trailing read-backs and setup launches carry no PCG)
+    return [it for it in its if any(short(r[0]).startswith("k_pcg_init") for r in it)]
 
 
 def classify(it):
