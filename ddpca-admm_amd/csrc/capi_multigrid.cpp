@@ -1,0 +1,292 @@
+// C ABI: the MULTIGRID operator pipeline on a caller's element tree (MULTIGRID::TRANSFER + PATCH +
+// STIF_MATR + CONSTRAINT(1), MULTIGRID.h:722-1255), for meshes the host generators do not make --
+// locally refined octrees with any refinement pattern (hanging nodes on the level past maxiLeve),
+// coupled nodes, nodal rotations (nodeRota).  The tree is what the reference's REFINE leaves in
+// MULTIGRID::elemVect / nodeCoor; its outputs are the reference's operators in its own layouts
+// (position numbering, condensed CSR), and ddpca_problem_set_subdomain_multigrid hands them to the
+// operator-level problem builder exactly as the reference binding does with the reference's own
+// MULTIGRID (oracle/ref_bind.hpp from_reference).
+#include <cstring>
+#include <memory>
+#include <string>
+
+#include "../../include/ddpca_amd.h"
+#include "common.hpp"
+#include "problem.hpp"
+
+using namespace ddpca;
+
+struct ddpca_multigrid {
+    MULTIGRID g;
+    int64_t nnode = 0;                 // node ids of the input (before TRANSFER's renumbering)
+    bool built = false;
+    std::vector<double> coords_by_id;  // after PATCH, by original node id
+    std::vector<int64_t> i64;
+    std::vector<uint8_t> u8;
+    std::vector<double> f64;
+    Csr csr;
+    std::vector<int64_t> shape;
+};
+
+namespace {
+
+template <typename T>
+int dtype_code();
+template <>
+int dtype_code<double>() { return 0; }
+template <>
+int dtype_code<int64_t>() { return 1; }
+template <>
+int dtype_code<int32_t>() { return 2; }
+template <>
+int dtype_code<uint8_t>() { return 3; }
+
+template <typename T>
+void put(const std::vector<T>& v, const void** data, int64_t* count, int* dtype) {
+    *data = v.data();
+    *count = (int64_t)v.size();
+    *dtype = dtype_code<T>();
+}
+
+ddpca_multigrid& open(ddpca_multigrid_t h, bool want_built) {
+    if (!h) throw ApiError(DDPCA_EINVAL, "null handle");
+    if (h->built != want_built)
+        throw ApiError(DDPCA_ESTATE, want_built ? "ddpca_multigrid_build has not run" : "the operators are already built");
+    return *h;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ddpca_multigrid_create(int64_t nnode, const double* coords, int64_t nelem, const int64_t* corner,
+                           const int64_t* parent, const int64_t* level, const int64_t* refiPatt,
+                           const int64_t* child_ptr, const int64_t* child, ddpca_multigrid_t* out) {
+    return guarded([&] {
+        if (nnode < 8 || nelem < 1 || !coords || !corner || !parent || !level || !refiPatt || !child_ptr || !out)
+            throw ApiError(DDPCA_EINVAL, "null argument or empty tree");
+        if (nnode >= (int64_t)1 << 31) throw ApiError(DDPCA_EINVAL, "node ids must fit int32");
+        auto h = std::make_unique<ddpca_multigrid>();
+        MULTIGRID& g = h->g;
+        h->nnode = nnode;
+        g.nodeCoor.resize(nnode);
+        for (int64_t i = 0; i < nnode; ++i)
+            for (int a = 0; a < 3; ++a) g.nodeCoor[i][a] = coords[3 * i + a];
+        g.nodeLevel.assign(nnode, 0);
+        g.nodeParents.assign(nnode, {});
+        g.maxiLeve = 0;
+        g.elemVect.resize(nelem);
+        if (child_ptr[0] != 0) throw ApiError(DDPCA_EINVAL, "child_ptr[0] must be 0");
+        for (int64_t e = 0; e < nelem; ++e) {
+            TreeElem& t = g.elemVect[e];
+            for (int k = 0; k < 8; ++k) {
+                t.cornNode[k] = corner[8 * e + k];
+                if (t.cornNode[k] < 0 || t.cornNode[k] >= nnode) throw ApiError(DDPCA_EINVAL, "corner node out of range");
+            }
+            t.parent = parent[e];
+            t.level = (int)level[e];
+            t.refiPatt = (int)refiPatt[e];
+            if (t.parent < -1 || t.parent >= nelem || t.level < 0) throw ApiError(DDPCA_EINVAL, "parent / level out of range");
+            const int64_t c0 = child_ptr[e], c1 = child_ptr[e + 1];
+            if (c1 < c0 || (c1 > c0 && !child)) throw ApiError(DDPCA_EINVAL, "child_ptr not monotone");
+            for (int64_t c = c0; c < c1; ++c) {
+                if (child[c] <= e || child[c] >= nelem) throw ApiError(DDPCA_EINVAL, "child index out of range");
+                t.children.push_back(child[c]);
+            }
+            if (!t.children.empty() && (t.refiPatt < 0 || t.refiPatt > 6))
+                throw ApiError(DDPCA_EINVAL, "refined element needs a refinement pattern 0..6");
+            g.maxiLeve = std::max<int64_t>(g.maxiLeve, t.level);  // ADD_ELEMENT, MULTIGRID.h:371
+        }
+        *out = h.release();
+    });
+}
+
+int ddpca_multigrid_set(ddpca_multigrid_t h, const char* what, int64_t n, const int64_t* idx, const double* val) {
+    return guarded([&] {
+        ddpca_multigrid& M = open(h, false);
+        MULTIGRID& g = M.g;
+        if (!what || n < 0) throw ApiError(DDPCA_EINVAL, "null argument");
+        const std::string w(what);
+        auto need = [&](bool i, bool v) {
+            if (n > 0 && ((i && !idx) || (v && !val))) throw ApiError(DDPCA_EINVAL, w + ": null array");
+        };
+        auto node = [&](int64_t v) {
+            if (v < 0 || v >= M.nnode) throw ApiError(DDPCA_EINVAL, w + ": node out of range");
+            return v;
+        };
+        if (w == "consDofv") {  // MULTIGRID::consDofv.emplace (first value of a dof wins)
+            need(true, true);
+            for (int64_t k = 0; k < n; ++k) {
+                node(idx[k] / 3);
+                g.consDofv.emplace(idx[k], val[k]);
+            }
+        } else if (w == "exteForc") {  // LOAD_ACCU in the given order (MULTIGRID.h:1084-1100)
+            need(true, true);
+            for (int64_t k = 0; k < n; ++k) {
+                node(idx[k] / 3);
+                g.LOAD_ACCU(idx[k], val[k]);
+            }
+        } else if (w == "nodeRota") {
+            need(true, true);
+            for (int64_t k = 0; k < n; ++k) {
+                std::array<double, 9> R;
+                for (int q = 0; q < 9; ++q) R[q] = val[9 * k + q];
+                g.nodeRota.emplace(node(idx[k]), R);
+            }
+        } else if (w == "coupNode") {
+            need(true, false);
+            for (int64_t k = 0; k < n; ++k) g.coupNode.insert(node(idx[k]));
+        } else if (w == "coupReps") {
+            need(true, false);
+            if (n != 1) throw ApiError(DDPCA_EINVAL, "coupReps: one node (or -1)");
+            g.coupReps = idx[0] < 0 ? -1 : node(idx[0]);
+        } else if (w == "material") {
+            need(false, true);
+            if (n != 2 || !(val[0] > 0.0) || !(val[1] > -1.0 && val[1] < 0.5)) throw ApiError(DDPCA_EINVAL, "material: E > 0, -1 < nu < 0.5");
+            g.mateElas = val[0];
+            g.matePois = val[1];
+        } else {
+            throw ApiError(DDPCA_EINVAL, "unknown input " + w);
+        }
+    });
+}
+
+int ddpca_multigrid_build(ddpca_multigrid_t h, const ddpca_csr_t* extra) {
+    return guarded([&] {
+        ddpca_multigrid& M = open(h, false);
+        MULTIGRID& g = M.g;
+        if (!g.coupNode.empty() && g.coupReps < 0) throw ApiError(DDPCA_EINVAL, "coupled nodes need coupReps");
+        try {
+            g.force_general = true;
+            g.TRANSFER();  // TRANSFER + PATCH; node ids become positions (g.posiNode = earlTran)
+            g.STIF_MATR();
+            if (extra) {
+                // origStif[maxiLeve + 1] += extra in the node-id numbering (MCONTACT.h:816-822:
+                // the contact interfaces' systMass), moved to positions
+                if (extra->nrow != 3 * M.nnode || extra->ncol != 3 * M.nnode || (extra->nrow && !extra->ptr))
+                    throw ApiError(DDPCA_EINVAL, "extra stiffness: 3N x 3N in node ids");
+                std::vector<int64_t> pos(M.nnode);
+                for (int64_t p = 0; p < M.nnode; ++p) pos[g.posiNode[p]] = p;
+                Csr A;
+                A.nrow = A.ncol = 3 * M.nnode;
+                std::vector<std::vector<std::pair<int32_t, double>>> rows(A.nrow);
+                for (int64_t r = 0; r < extra->nrow; ++r)
+                    for (int64_t k = extra->ptr[r]; k < extra->ptr[r + 1]; ++k) {
+                        const int32_t c = extra->col[k];
+                        if (c < 0 || c >= A.ncol) throw ApiError(DDPCA_EINVAL, "extra stiffness: column out of range");
+                        rows[3 * pos[r / 3] + r % 3].push_back({(int32_t)(3 * pos[c / 3] + c % 3), extra->val[k]});
+                    }
+                A.ptr.assign(A.nrow + 1, 0);
+                for (int64_t r = 0; r < A.nrow; ++r) {
+                    for (const auto& e : rows[r]) {
+                        A.col.push_back(e.first);
+                        A.val.push_back(e.second);
+                    }
+                    A.ptr[r + 1] = (int64_t)A.col.size();
+                }
+                g.ADD_NODAL(A);
+            }
+            g.CONSTRAINT();
+        } catch (const ApiError&) {
+            throw;
+        } catch (const std::invalid_argument& e) {
+            throw ApiError(DDPCA_EINVAL, e.what());
+        } catch (const std::runtime_error& e) {
+            throw ApiError(DDPCA_EINVAL, e.what());
+        }
+        M.coords_by_id.assign(3 * M.nnode, 0.0);
+        for (int64_t p = 0; p < M.nnode; ++p)
+            for (int a = 0; a < 3; ++a) M.coords_by_id[3 * g.posiNode[p] + a] = g.nodeCoor[p][a];
+        M.built = true;
+    });
+}
+
+int ddpca_multigrid_view(ddpca_multigrid_t h, const char* what, int64_t level, const void** data, int64_t* count,
+                         int* dtype) {
+    return guarded([&] {
+        ddpca_multigrid& M = open(h, true);
+        const MULTIGRID& g = M.g;
+        if (!what || !data || !count || !dtype) throw ApiError(DDPCA_EINVAL, "null argument");
+        const std::string w(what);
+        const int64_t L = g.maxiLeve;
+        auto lev = [&](int64_t lo, int64_t hi) {
+            if (level < lo || level > hi) throw ApiError(DDPCA_EINVAL, w + ": level out of range");
+        };
+        auto csr_part = [&](const std::string& part) {
+            if (part == "ptr") put(M.csr.ptr, data, count, dtype);
+            else if (part == "col") put(M.csr.col, data, count, dtype);
+            else if (part == "val") put(M.csr.val, data, count, dtype);
+            else if (part == "shape") {
+                M.shape = {M.csr.nrow, M.csr.ncol};
+                put(M.shape, data, count, dtype);
+            } else throw ApiError(DDPCA_EINVAL, "CSR part must be ptr, col, val or shape");
+        };
+        if (w == "posiNode") put(g.posiNode, data, count, dtype);
+        else if (w == "nodeCoor") put(M.coords_by_id, data, count, dtype);
+        else if (w == "leveCount") {
+            M.i64.assign(g.leveCount.begin(), g.leveCount.end());
+            M.i64.push_back(g.numNodes());  // the hanging level's end: every position
+            put(M.i64, data, count, dtype);
+        } else if (w == "freeCount") put(g.freeCount, data, count, dtype);
+        else if (w == "consFlag") put(g.consFlag, data, count, dtype);
+        else if (w == "consForc") put(g.consForc, data, count, dtype);
+        else if (w == "dispForc") put(g.dispForc, data, count, dtype);
+        else if (w.rfind("K:", 0) == 0) {  // MGPIS::consStif[level]
+            lev(0, L);
+            M.csr = g.consStif(level);
+            csr_part(w.substr(2));
+        } else if (w.rfind("P:", 0) == 0) {  // MGPIS::realProl[level] (level + 1 <- level)
+            lev(0, L - 1);
+            M.csr = g.realProl(level);
+            csr_part(w.substr(2));
+        } else if (w.rfind("H:", 0) == 0) {  // prolOper[maxiLeve]'s rows past the fine level
+            M.csr = g.hangRows();
+            csr_part(w.substr(2));
+        } else {
+            throw ApiError(DDPCA_EINVAL, "unknown quantity " + w);
+        }
+    });
+}
+
+int ddpca_problem_set_subdomain_multigrid(ddpca_problem_t p, int64_t tv, ddpca_multigrid_t h) {
+    return guarded([&] {
+        Problem& P = *reinterpret_cast<Problem*>(p);
+        if (P.established) throw ApiError(DDPCA_ESTATE, "problem already established");
+        if (tv < 0 || tv >= (int64_t)P.mc.multGrid.size()) throw ApiError(DDPCA_EINVAL, "subdomain index");
+        ddpca_multigrid& M = open(h, true);
+        const MULTIGRID& s = M.g;
+        // what set_subdomain(_prol) + set_hanging build from the reference's MULTIGRID: the fine
+        // level's nodes, the level operators (unconstrained: the device masks constrained dofs),
+        // prolOper's stencils with their rotation blocks, the hanging rows
+        MULTIGRID g;
+        const int64_t L = s.maxiLeve, NL = s.leveCount[L];
+        g.maxiLeve = L;
+        g.leveCount = s.leveCount;
+        g.freeCount = s.freeCount;
+        g.levelStif = s.levelStif;
+        g.scalProl = s.prolOper;
+        g.consFlag.assign(s.consFlag.begin(), s.consFlag.begin() + 3 * NL);
+        g.freeIndex.assign(s.freeIndex.begin(), s.freeIndex.begin() + 3 * NL);
+        g.consForc = s.consForc;
+        for (int64_t d = 0; d < 3 * NL; ++d)
+            if (!g.consFlag[d]) {
+                const auto it = s.consDofv.find(d);
+                const double v = it == s.consDofv.end() ? 0.0 : it->second;
+                g.consDofv[d] = v;
+                g.dispForc.push_back(v);
+            }
+        g.nodeCoor.assign(s.nodeCoor.begin(), s.nodeCoor.begin() + NL);
+        g.nodeLevel.assign(s.nodeLevel.begin(), s.nodeLevel.begin() + NL);
+        g.nodeAll = s.nodeAll;
+        g.hangProl = s.hangRows();
+        P.mc.multGrid[tv] = std::move(g);
+        P.owned[tv] = 1;
+    });
+}
+
+int ddpca_multigrid_destroy(ddpca_multigrid_t h) {
+    delete h;
+    return DDPCA_OK;
+}
+
+}  // extern "C"

@@ -143,7 +143,7 @@ int64_t MULTIGRID::ADD_ELEMENT(const TreeElem& e) {
 void MULTIGRID::REFINE_ALL() {
     const int64_t ne = (int64_t)elemVect.size();
     for (int64_t e = 0; e < ne; ++e) {
-        if (elemVect[e].firstChild >= 0) continue;
+        if (!elemVect[e].leaf()) continue;
         const std::array<int64_t, 8> corn = elemVect[e].cornNode;
         const int lev = elemVect[e].level;
         int64_t grid[3][3][3];
@@ -178,6 +178,8 @@ void MULTIGRID::REFINE_ALL() {
             grid[q[0]][q[1]][q[2]] = id;
         }
         elemVect[e].firstChild = (int64_t)elemVect.size();
+        elemVect[e].refiPatt = 0;
+        for (int c = 0; c < 8; ++c) elemVect[e].children.push_back((int64_t)elemVect.size() + c);
         for (int c = 0; c < 8; ++c) {
             TreeElem ch;
             ch.parent = e;
@@ -192,12 +194,19 @@ void MULTIGRID::REFINE_ALL() {
 // ---------------------------------------------------------------------------------- transfer
 void MULTIGRID::TRANSFER() {
     const int64_t N = numNodes();
-    leveCount.assign(maxiLeve + 1, 0);
-    for (int64_t i = 0; i < N; ++i) {
-        if (i > 0 && nodeLevel[i] < nodeLevel[i - 1])
-            throw std::runtime_error("node ids are not level ordered (non-uniform refinement)");
-        leveCount[nodeLevel[i]]++;
+    // uniform refinement of a generator (REFINE_ALL, no coupling): node ids are already the
+    // reference's positions and every new node's parents are recorded -- the fast path below is
+    // the general algorithm's result on such a tree (tests/test_host_operators.py checks that)
+    bool fast = !force_general && coupNode.empty() && coupReps < 0 && (int64_t)nodeLevel.size() == N;
+    for (int64_t i = 1; i < N && fast; ++i) fast = nodeLevel[i] >= nodeLevel[i - 1];
+    for (const auto& e : elemVect) fast = fast && (e.leaf() ? e.level == maxiLeve : e.firstChild >= 0);
+    if (!fast) {
+        TRANSFER_GENERAL();
+        return;
     }
+    general = false;
+    leveCount.assign(maxiLeve + 1, 0);
+    for (int64_t i = 0; i < N; ++i) leveCount[nodeLevel[i]]++;
     for (int64_t l = 1; l <= maxiLeve; ++l) leveCount[l] += leveCount[l - 1];
     scalProl.assign(maxiLeve, Stencil());
     for (int64_t l = 0; l < maxiLeve; ++l) {
@@ -221,6 +230,227 @@ void MULTIGRID::TRANSFER() {
     }
 }
 
+namespace {
+
+// The 12 edges and 6 faces every element registers (PREP.h hexaLine / hexaFace; ADD_ELEMENT,
+// MULTIGRID.h:335-373) and, per refinement pattern, the edges / faces of a refined element whose
+// midpoint / centre node the refinement created: {corner a, corner b, child, child corner} and
+// {4 corners, child, child corner} (TRANSFER's elemLine / elemFace, MULTIGRID.h:759-792).
+const int kHexLine[12][2] = {{0, 1}, {1, 2}, {2, 3}, {3, 0}, {0, 4}, {1, 5}, {2, 6}, {3, 7}, {4, 5}, {5, 6}, {6, 7}, {7, 4}};
+const int kHexFace[6][4] = {{0, 3, 2, 1}, {4, 5, 6, 7}, {0, 4, 7, 3}, {1, 2, 6, 5}, {0, 1, 5, 4}, {3, 7, 6, 2}};
+struct LineNew { int a, b, child, corner; };
+struct FaceNew { int c[4], child, corner; };
+const std::vector<std::vector<LineNew>> kPattLine = {
+    {{0, 1, 0, 1}, {1, 2, 1, 2}, {2, 3, 3, 3}, {3, 0, 2, 0}, {0, 4, 0, 4}, {1, 5, 1, 5}, {2, 6, 3, 6}, {3, 7, 2, 7},
+     {4, 5, 4, 5}, {5, 6, 5, 6}, {6, 7, 7, 7}, {7, 4, 6, 4}},
+    {{0, 1, 0, 1}, {1, 2, 1, 2}, {2, 3, 3, 3}, {3, 0, 2, 0}, {4, 5, 0, 5}, {5, 6, 1, 6}, {6, 7, 3, 7}, {7, 4, 2, 4}},
+    {{0, 3, 0, 3}, {3, 7, 1, 7}, {7, 4, 3, 4}, {4, 0, 2, 0}, {1, 2, 0, 2}, {2, 6, 1, 6}, {6, 5, 3, 5}, {5, 1, 2, 1}},
+    {{0, 4, 0, 4}, {4, 5, 1, 5}, {5, 1, 3, 1}, {1, 0, 2, 0}, {3, 7, 0, 7}, {7, 6, 1, 6}, {6, 2, 3, 2}, {2, 3, 2, 3}},
+    {{0, 1, 0, 1}, {2, 3, 0, 2}, {4, 5, 0, 5}, {6, 7, 0, 6}},
+    {{0, 3, 0, 3}, {1, 2, 0, 2}, {4, 7, 0, 7}, {5, 6, 0, 6}},
+    {{0, 4, 0, 4}, {1, 5, 0, 5}, {3, 7, 0, 7}, {2, 6, 0, 6}}};
+const std::vector<std::vector<FaceNew>> kPattFace = {
+    {{{0, 1, 2, 3}, 0, 2}, {{4, 5, 6, 7}, 4, 6}, {{0, 3, 7, 4}, 0, 7}, {{1, 2, 6, 5}, 3, 5}, {{0, 4, 5, 1}, 0, 5},
+     {{3, 7, 6, 2}, 3, 7}},
+    {{{0, 1, 2, 3}, 0, 2}, {{4, 5, 6, 7}, 0, 6}},
+    {{{0, 3, 7, 4}, 0, 7}, {{1, 2, 6, 5}, 0, 6}},
+    {{{0, 4, 5, 1}, 0, 5}, {{3, 7, 6, 2}, 0, 6}},
+    {}, {}, {}};
+
+struct KeyHash {
+    size_t operator()(const std::array<int64_t, 4>& k) const {
+        uint64_t h = 1469598103934665603ull;
+        for (int64_t v : k) h = (h ^ (uint64_t)v) * 1099511628211ull;
+        return (size_t)h;
+    }
+};
+
+}  // namespace
+
+// TRANSFER on any octree (MULTIGRID.h:756-948) + PATCH (722-754), then the node ids are moved to
+// the reference's positions.
+//   * every edge / face midpoint a refinement created (the pattern's elemLine / elemFace rows) is
+//     a node of level (element level + 1) with the edge's 2 / face's 4 corners as parents -- or,
+//     when an element using that edge / face is still a leaf (a hanging node), a node of the
+//     hanging level maxiLeve + 1 with the parents in prolOper[maxiLeve]; a pattern-0 element's
+//     body centre has its 8 corners; the first insertion of a parent set wins (std::map insert)
+//   * PATCH moves every hanging node to the average of its parents (the refined surface's
+//     position would break the patch test)
+//   * positions: level by level, node ids ascending inside a level (std::set order); coupReps on
+//     level 0, the other coupled nodes on the hanging level
+//   * scalProl[l] (level l+1 <- l): identity on the level-l positions, parents' weights 1/count
+//     (duplicates summed: a coupled parent becomes coupReps); prolOper[maxiLeve]'s stencil also
+//     maps every coupled node to coupReps
+void MULTIGRID::TRANSFER_GENERAL() {
+    const int64_t N = numNodes(), L = maxiLeve;
+    const int64_t ne = (int64_t)elemVect.size();
+    for (auto& e : elemVect)
+        if (e.firstChild >= 0 && e.children.empty())
+            for (int c = 0; c < 8; ++c) e.children.push_back(e.firstChild + c);
+    // does a leaf element use this edge / face (lineUsed / faceUsed, MULTIGRID.h:338-369)?
+    std::unordered_map<std::array<int64_t, 4>, bool, KeyHash> leafUse;
+    leafUse.reserve((size_t)ne * 10);
+    auto reg = [&](std::array<int64_t, 4> k, bool leaf) {
+        auto it = leafUse.emplace(k, leaf);
+        if (!it.second) it.first->second = it.first->second || leaf;
+    };
+    for (const auto& e : elemVect) {
+        for (const auto& ln : kHexLine) {
+            std::array<int64_t, 4> k{std::min(e.cornNode[ln[0]], e.cornNode[ln[1]]), std::max(e.cornNode[ln[0]], e.cornNode[ln[1]]), -1, -1};
+            reg(k, e.leaf());
+        }
+        for (const auto& f : kHexFace) {
+            std::array<int64_t, 4> k{e.cornNode[f[0]], e.cornNode[f[1]], e.cornNode[f[2]], e.cornNode[f[3]]};
+            std::sort(k.begin(), k.end());
+            reg(k, e.leaf());
+        }
+    }
+    std::vector<std::map<std::vector<int64_t>, int64_t>> ininTran(L + 1);
+    std::vector<std::set<int64_t>> leveNode_s(L + 2);
+    auto child_corner = [&](const TreeElem& e, int child, int corner) {
+        if (child >= (int)e.children.size()) throw std::invalid_argument("TRANSFER: refined element without that child");
+        const int64_t c = e.children[child];
+        if (c < 0 || c >= ne) throw std::invalid_argument("TRANSFER: child index out of range");
+        return elemVect[c].cornNode[corner];
+    };
+    for (const auto& e : elemVect) {
+        if (e.level == 0)
+            for (int k = 0; k < 8; ++k) leveNode_s[0].insert(e.cornNode[k]);
+        if (e.leaf()) continue;
+        const int s = e.refiPatt;
+        if (s < 0 || s > 6) throw std::invalid_argument("TRANSFER: refined element with refinement pattern outside 0..6");
+        if (e.level + 1 > L + 1 || e.level < 0) throw std::invalid_argument("TRANSFER: element level beyond maxiLeve");
+        if (s == 0) {
+            std::vector<int64_t> corn(e.cornNode.begin(), e.cornNode.end());
+            std::sort(corn.begin(), corn.end());
+            const int64_t nd = child_corner(e, 0, 6);
+            ininTran[e.level].emplace(corn, nd);
+            leveNode_s[e.level + 1].insert(nd);
+        }
+        for (const LineNew& ln : kPattLine[s]) {
+            std::vector<int64_t> key{e.cornNode[ln.a], e.cornNode[ln.b]};
+            std::sort(key.begin(), key.end());
+            const auto it = leafUse.find({key[0], key[1], -1, -1});
+            const bool hang = it != leafUse.end() && it->second;
+            const int64_t nd = child_corner(e, ln.child, ln.corner);
+            const int64_t lv = hang ? L : e.level;
+            ininTran[lv].emplace(key, nd);
+            leveNode_s[lv + 1].insert(nd);
+        }
+        for (const FaceNew& fc : kPattFace[s]) {
+            std::vector<int64_t> key{e.cornNode[fc.c[0]], e.cornNode[fc.c[1]], e.cornNode[fc.c[2]], e.cornNode[fc.c[3]]};
+            std::sort(key.begin(), key.end());
+            const auto it = leafUse.find({key[0], key[1], key[2], key[3]});
+            const bool hang = it != leafUse.end() && it->second;
+            const int64_t nd = child_corner(e, fc.child, fc.corner);
+            const int64_t lv = hang ? L : e.level;
+            ininTran[lv].emplace(key, nd);
+            leveNode_s[lv + 1].insert(nd);
+        }
+    }
+    // PATCH (MULTIGRID.h:722-754): in the map's key order, coordinates summed from zero in the
+    // parents' order, then divided by their count
+    for (const auto& kv : ininTran[L]) {
+        std::array<double, 3> c{0.0, 0.0, 0.0};
+        for (int64_t p : kv.first)
+            for (int a = 0; a < 3; ++a) c[a] = c[a] + nodeCoor[p][a];
+        for (int a = 0; a < 3; ++a) c[a] = c[a] / (double)kv.first.size();
+        nodeCoor[kv.second] = c;
+    }
+    // positions (MULTIGRID.h:884-910)
+    std::vector<std::vector<int64_t>> leveNode(L + 2);
+    for (int64_t t = 0; t <= L + 1; ++t)
+        for (int64_t nd : leveNode_s[t]) {
+            if (nd == coupReps) leveNode[0].push_back(nd);
+            else if (coupNode.count(nd)) leveNode[L + 1].push_back(nd);
+            else leveNode[t].push_back(nd);
+        }
+    std::vector<int64_t> pos(N, -1);
+    posiNode.clear();
+    std::vector<int> plev;
+    for (int64_t t = 0; t <= L + 1; ++t)
+        for (int64_t nd : leveNode[t]) {
+            if (nd < 0 || nd >= N) throw std::invalid_argument("TRANSFER: node id out of range");
+            if (pos[nd] >= 0) throw std::invalid_argument("TRANSFER: node " + std::to_string(nd) + " on two levels");
+            pos[nd] = (int64_t)posiNode.size();
+            posiNode.push_back(nd);
+            plev.push_back((int)t);
+        }
+    if ((int64_t)posiNode.size() != N) throw std::invalid_argument("TRANSFER: nodes used by no element");
+    const int64_t repPos = coupReps >= 0 ? pos.at(coupReps) : -1;
+    // stencils in positions: identity on the level-t positions, the parents with 1/count
+    scalProl.assign(L, Stencil());
+    int64_t accu = 0;
+    for (int64_t t = 0; t <= L; ++t) {
+        const int64_t nc = accu + (int64_t)leveNode[t].size(), nf = nc + (int64_t)leveNode[t + 1].size();
+        std::vector<std::vector<std::pair<int64_t, double>>> rows(nf);
+        for (int64_t r = 0; r < nc; ++r) rows[r].push_back({r, 1.0});
+        for (const auto& kv : ininTran[t]) {
+            if (coupNode.count(kv.second)) continue;
+            const int64_t r = pos[kv.second];
+            const double w = 1.0 / (double)kv.first.size();
+            for (int64_t p : kv.first) rows.at(r).push_back({coupNode.count(p) ? repPos : pos[p], w});
+        }
+        if (t == L)
+            for (int64_t c : coupNode) rows.at(pos[c]).push_back({repPos, 1.0});
+        Stencil S;
+        S.nf = nf;
+        S.nc = nc;
+        S.ptr.assign(nf + 1, 0);
+        for (int64_t r = 0; r < nf; ++r) {
+            // setFromTriplets: duplicates summed in insertion order, columns ascending
+            auto& v = rows[r];
+            std::stable_sort(v.begin(), v.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
+            for (size_t k = 0; k < v.size();) {
+                size_t q = k;
+                double w = 0.0;
+                for (; q < v.size() && v[q].first == v[k].first; ++q) w += v[q].second;
+                if (v[k].first < 0 || v[k].first >= nc) throw std::invalid_argument("TRANSFER: parent outside the coarser levels");
+                S.col.push_back((int32_t)v[k].first);
+                S.w.push_back(w);
+                k = q;
+            }
+            S.ptr[r + 1] = (int64_t)S.col.size();
+        }
+        if (t < L) scalProl[t] = std::move(S);
+        else hangStencil = std::move(S);
+        accu = nc;
+    }
+    leveCount.assign(L + 1, 0);
+    for (int64_t t = 0, acc = 0; t <= L; ++t) leveCount[t] = (acc += (int64_t)leveNode[t].size());
+    nodeAll = N > leveCount[L] ? N : 0;
+    if (!nodeAll) hangStencil = Stencil();
+    // move every node-indexed member to positions (earlTran, MULTIGRID.h:1126-1139)
+    auto perm_dofmap = [&](std::map<int64_t, double>& m) {
+        std::map<int64_t, double> o;
+        for (const auto& kv : m) o.emplace(3 * pos[kv.first / 3] + kv.first % 3, kv.second);
+        m.swap(o);
+    };
+    perm_dofmap(consDofv);
+    perm_dofmap(exteForc);
+    std::map<int64_t, std::array<double, 9>> rot;
+    for (const auto& kv : nodeRota) rot.emplace(pos.at(kv.first), kv.second);
+    nodeRota.swap(rot);
+    std::set<int64_t> cp;
+    for (int64_t c : coupNode) cp.insert(pos[c]);
+    coupNode.swap(cp);
+    if (coupReps >= 0) coupReps = repPos;
+    std::vector<std::array<double, 3>> xyz(N);
+    for (int64_t p = 0; p < N; ++p) xyz[p] = nodeCoor[posiNode[p]];
+    nodeCoor.swap(xyz);
+    if ((int64_t)nodeLatt.size() == N) {
+        std::vector<std::array<int64_t, 3>> lt(N);
+        for (int64_t p = 0; p < N; ++p) lt[p] = nodeLatt[posiNode[p]];
+        nodeLatt.swap(lt);
+    }
+    nodeLevel = plev;
+    nodeParents.assign(N, {});
+    lattNode.clear();
+    for (auto& e : elemVect)
+        for (auto& c : e.cornNode) c = pos[c];
+    general = true;
+}
+
 // ---------------------------------------------------------------------------------- stiffness
 void MULTIGRID::STIF_MATR() {
     const int64_t N = numNodes();
@@ -232,11 +462,12 @@ void MULTIGRID::STIF_MATR() {
     D[3][3] = D[4][4] = D[5][5] = mu;
     std::vector<int64_t> leaves;
     for (int64_t e = 0; e < (int64_t)elemVect.size(); ++e)
-        if (elemVect[e].firstChild < 0) leaves.push_back(e);
+        if (elemVect[e].leaf()) leaves.push_back(e);
     // colour leaf elements so that one colour shares no node (uniform octree: lattice parity)
     int64_t h = -1;
-    bool uniform = true;
+    bool uniform = !nodeLatt.empty() && !general;
     for (int64_t e : leaves) {
+        if (!uniform) break;
         const auto& c0 = nodeLatt[elemVect[e].cornNode[0]];
         int64_t ext = 0;
         for (int k = 1; k < 8; ++k)
@@ -336,7 +567,7 @@ double MULTIGRID::GET_VOLUME() const {
 #pragma omp parallel for schedule(static)
     for (int64_t p = 0; p < np; ++p)
         for (int64_t e = p * part; e < std::min(ne, (p + 1) * part); ++e) {
-            if (elemVect[e].firstChild >= 0) continue;
+            if (!elemVect[e].leaf()) continue;
             double X[8][3], J[3][3];
             for (int k = 0; k < 8; ++k)
                 for (int a = 0; a < 3; ++a) X[k][a] = nodeCoor[elemVect[e].cornNode[k]][a];
@@ -370,6 +601,10 @@ void MULTIGRID::LOAD_ACCU(int64_t dof, double v) {
 void MULTIGRID::FLAGS() {
     const int64_t N = numNodes();
     const int64_t L = maxiLeve;
+    // consFlag over every position (the hanging level's too); the condensed numbering and the
+    // prescribed values cover the MGPIS fine level only (consOper[maxiLeve], dispForc:
+    // MULTIGRID.h:1186-1204)
+    const int64_t NL = leveCount.empty() ? N : leveCount[L];
     consFlag.assign(3 * N, 1);
     std::vector<double> dfull(3 * N, 0.0);
     for (const auto& kv : consDofv) {
@@ -380,7 +615,7 @@ void MULTIGRID::FLAGS() {
     freeCount.assign(L + 1, 0);
     int64_t nf = 0;
     dispForc.clear();
-    for (int64_t d = 0; d < 3 * N; ++d) {
+    for (int64_t d = 0; d < 3 * NL; ++d) {
         if (consFlag[d]) freeIndex[d] = (int32_t)nf++;
         else dispForc.push_back(dfull[d]);
     }
@@ -391,34 +626,165 @@ void MULTIGRID::FLAGS() {
     }
 }
 
+namespace {
+// prolOper's blocks from a position stencil (MULTIGRID.h:1147-1178): an entry between a fine node
+// and a parent of which exactly one is rotated becomes w R_off^T (fine node rotated) or w R_par
+// (parent rotated); both rotated: w I ("only one pattern of nodeRota"); the coupled nodes' map to
+// coupReps stays w I.  Identity rows of the coarse nodes are never rotated.
+Stencil rotate_stencil(const Stencil& S, const std::map<int64_t, std::array<double, 9>>& rot,
+                       const std::set<int64_t>& coup, int64_t reps) {
+    Stencil P = S;
+    P.bent.clear();
+    P.bval.clear();
+    if (rot.empty()) return P;
+    for (int64_t r = S.nc; r < S.nf; ++r)
+        for (int64_t k = S.ptr[r]; k < S.ptr[r + 1]; ++k) {
+            const int64_t c = S.col[k];
+            const auto ro = rot.find(r), rp = rot.find(c);
+            if (ro == rot.end() && rp == rot.end()) continue;
+            if (c == reps && coup.count(r)) continue;
+            if (ro != rot.end() && rp != rot.end()) continue;
+            const double w = S.w[k];
+            double B[9];
+            for (int a = 0; a < 3; ++a)
+                for (int b = 0; b < 3; ++b)
+                    B[3 * a + b] = ro != rot.end() ? w * ro->second[3 * b + a] : w * rp->second[3 * a + b];
+            P.w[k] = 0.0;
+            P.bent.push_back(k);
+            P.bval.insert(P.bval.end(), B, B + 9);
+        }
+    return P;
+}
+
+// y (nc nodes) = P^T x (nf nodes), P = S (x) I3 + block entries
+void stencil_apply_t(const Stencil& S, const double* x, double* y) {
+    std::vector<int64_t> blk_of(S.col.size(), -1);
+    for (size_t q = 0; q < S.bent.size(); ++q) blk_of[S.bent[q]] = (int64_t)q;
+    for (int64_t r = 0; r < S.nf; ++r)
+        for (int64_t k = S.ptr[r]; k < S.ptr[r + 1]; ++k) {
+            const int64_t c = S.col[k];
+            if (blk_of[k] >= 0) {
+                const double* B = &S.bval[9 * blk_of[k]];
+                for (int b = 0; b < 3; ++b) y[3 * c + b] += B[b] * x[3 * r] + B[3 + b] * x[3 * r + 1] + B[6 + b] * x[3 * r + 2];
+            } else {
+                for (int a = 0; a < 3; ++a) y[3 * c + a] += S.w[k] * x[3 * r + a];
+            }
+        }
+}
+}  // namespace
+
 void MULTIGRID::CONSTRAINT() {
     const int64_t N = numNodes();
     const int64_t L = maxiLeve;
+    const int64_t NL = leveCount[L];
+    // R^T K R on the rotated nodes (MULTIGRID.h:1105-1124)
+    Bsr3 K = origStif;
+    if (!nodeRota.empty()) {
+        auto R = [&](int64_t i) -> const double* {
+            auto it = nodeRota.find(i);
+            return it == nodeRota.end() ? nullptr : it->second.data();
+        };
+        static const double I3[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+#pragma omp parallel for schedule(static)
+        for (int64_t i = 0; i < K.nb; ++i) {
+            const double* Ri = R(i);
+            for (int64_t k = K.ptr[i]; k < K.ptr[i + 1]; ++k) {
+                const double* Rj = R(K.col[k]);
+                if (!Ri && !Rj) continue;
+                const double* A = Ri ? Ri : I3;
+                const double* Bm = Rj ? Rj : I3;
+                double* blk = K.block(k);
+                double T[9], O[9];
+                for (int a = 0; a < 3; ++a)
+                    for (int b = 0; b < 3; ++b) T[3 * a + b] = blk[3 * a] * Bm[b] + blk[3 * a + 1] * Bm[3 + b] + blk[3 * a + 2] * Bm[6 + b];
+                for (int a = 0; a < 3; ++a)
+                    for (int b = 0; b < 3; ++b) O[3 * a + b] = A[a] * T[b] + A[3 + a] * T[3 + b] + A[6 + a] * T[6 + b];
+                std::copy(O, O + 9, blk);
+            }
+        }
+    }
+    prolOper.clear();
+    for (int64_t l = 0; l < L; ++l) prolOper.push_back(rotate_stencil(scalProl[l], nodeRota, coupNode, coupReps));
+    prolHang = nodeAll ? rotate_stencil(hangStencil, nodeRota, coupNode, coupReps) : Stencil();
+    // the hanging level's Galerkin step, then the hierarchy (MULTIGRID.h:1182-1184)
     levelStif.assign(L + 1, Bsr3());
-    levelStif[L] = origStif;
-    for (int64_t l = L - 1; l >= 0; --l) levelStif[l] = galerkin_rap(levelStif[l + 1], scalProl[l]);
+    levelStif[L] = nodeAll ? galerkin_rap(K, prolHang) : std::move(K);
+    for (int64_t l = L - 1; l >= 0; --l) levelStif[l] = galerkin_rap(levelStif[l + 1], prolOper[l]);
     FLAGS();
-    std::vector<double> dfull(3 * N, 0.0);
-    for (const auto& kv : consDofv) dfull[kv.first] = kv.second;
+    // consForc = consOper (prolOper[maxiLeve]^T f - K_L d), loads not rotated, d the prescribed
+    // values of the fine level's constrained dofs (MULTIGRID.h:1186-1243)
     std::vector<double> f(3 * N, 0.0);
     for (const auto& kv : exteForc) f[kv.first] += kv.second;
-    std::vector<double> Kd(3 * N, 0.0);
-    if (!consDofv.empty()) levelStif[L].apply(dfull.data(), Kd.data());
+    std::vector<double> fL(3 * NL, 0.0);
+    if (nodeAll) stencil_apply_t(prolHang, f.data(), fL.data());
+    else fL = f;
+    std::vector<double> dL(3 * NL, 0.0);
+    for (const auto& kv : consDofv)
+        if (kv.first < 3 * NL) dL[kv.first] = kv.second;
+    std::vector<double> Kd(3 * NL, 0.0);
+    if (!consDofv.empty()) levelStif[L].apply(dL.data(), Kd.data());
     consForc.assign(freeCount[L], 0.0);
-    for (int64_t d = 0; d < 3 * N; ++d)
-        if (consFlag[d]) consForc[freeIndex[d]] = f[d] - Kd[d];
+    for (int64_t d = 0; d < 3 * NL; ++d)
+        if (freeIndex[d] >= 0) consForc[freeIndex[d]] = fL[d] - Kd[d];
 }
 
 void MULTIGRID::ADDITIONAL_FORCE(const double* f_nodal, double* f_free) const {
-    const int64_t n = 3 * numNodes();
-    for (int64_t d = 0; d < n; ++d)
-        if (consFlag[d]) f_free[freeIndex[d]] = f_nodal[d];
+    // consOper prolOper[maxiLeve]^T f (position numbering: earlTran is the identity here)
+    const int64_t n = 3 * numNodes(), nL = 3 * leveCount[maxiLeve];
+    std::vector<double> fL(f_nodal, f_nodal + nL);
+    if (nodeAll) {
+        std::fill(fL.begin(), fL.end(), 0.0);
+        stencil_apply_t(prolHang, f_nodal, fL.data());
+    }
+    (void)n;
+    for (int64_t d = 0; d < nL; ++d)
+        if (freeIndex[d] >= 0) f_free[freeIndex[d]] = fL[d];
 }
 
 void MULTIGRID::OUTP_SUB1(const double* x_free, double* u_nodal) const {
-    const int64_t n = 3 * numNodes();
-    for (int64_t d = 0; d < n; ++d) u_nodal[d] = consFlag[d] ? x_free[freeIndex[d]] : 0.0;
-    for (const auto& kv : consDofv) u_nodal[kv.first] = kv.second;
+    // the fine level: free values and the prescribed ones; the hanging level: prolOper[maxiLeve]'s rows
+    const int64_t nL = 3 * leveCount[maxiLeve];
+    for (int64_t d = 0; d < nL; ++d) u_nodal[d] = freeIndex[d] >= 0 ? x_free[freeIndex[d]] : 0.0;
+    for (const auto& kv : consDofv)
+        if (kv.first < nL) u_nodal[kv.first] = kv.second;
+    if (nodeAll) {
+        const Csr Hr = hangRows();
+        for (int64_t r = 0; r < Hr.nrow; ++r) {
+            double s = 0.0;
+            for (int64_t k = Hr.ptr[r]; k < Hr.ptr[r + 1]; ++k) s += Hr.val[k] * u_nodal[Hr.col[k]];
+            u_nodal[nL + r] = s;
+        }
+    }
+}
+
+Csr MULTIGRID::hangRows() const {
+    Csr H;
+    const int64_t NL = leveCount[maxiLeve], N = nodeAll ? nodeAll : NL;
+    H.nrow = 3 * (N - NL);
+    H.ncol = 3 * NL;
+    H.ptr.assign(H.nrow + 1, 0);
+    if (!nodeAll) return H;
+    const Stencil& S = prolHang.nf ? prolHang : hangStencil;
+    std::vector<int64_t> blk_of(S.col.size(), -1);
+    for (size_t q = 0; q < S.bent.size(); ++q) blk_of[S.bent[q]] = (int64_t)q;
+    for (int64_t i = NL; i < N; ++i)
+        for (int a = 0; a < 3; ++a) {
+            std::vector<std::pair<int32_t, double>> row;
+            for (int64_t k = S.ptr[i]; k < S.ptr[i + 1]; ++k) {
+                const int64_t c = S.col[k];
+                if (blk_of[k] >= 0)
+                    for (int b = 0; b < 3; ++b) row.push_back({(int32_t)(3 * c + b), S.bval[9 * blk_of[k] + 3 * a + b]});
+                else
+                    row.push_back({(int32_t)(3 * c + a), S.w[k]});
+            }
+            std::sort(row.begin(), row.end());
+            for (const auto& e : row) {
+                H.col.push_back(e.first);
+                H.val.push_back(e.second);
+            }
+            H.ptr[3 * (i - NL) + a + 1] = (int64_t)H.col.size();
+        }
+    return H;
 }
 
 Csr MULTIGRID::consStif(int64_t level) const {
@@ -426,20 +792,36 @@ Csr MULTIGRID::consStif(int64_t level) const {
 }
 
 Csr MULTIGRID::realProl(int64_t level) const {
-    const Stencil& S = scalProl[level];
+    // consOper[l+1] prolOper[l] consOper[l]^T (MULTIGRID.h:1246-1249); rotated blocks expanded
+    const Stencil& S = (int64_t)prolOper.size() > level ? prolOper[level] : scalProl[level];
+    std::vector<int64_t> blk_of(S.col.size(), -1);
+    for (size_t q = 0; q < S.bent.size(); ++q) blk_of[S.bent[q]] = (int64_t)q;
     Csr P;
     P.nrow = freeCount[level + 1];
     P.ncol = freeCount[level];
     P.ptr.assign(P.nrow + 1, 0);
+    std::vector<std::pair<int32_t, double>> row;
     for (int64_t i = 0; i < S.nf; ++i)
         for (int a = 0; a < 3; ++a) {
             const int32_t r = freeIndex[3 * i + a];
             if (r < 0) continue;
+            row.clear();
             for (int64_t k = S.ptr[i]; k < S.ptr[i + 1]; ++k) {
-                const int32_t c = freeIndex[3 * (int64_t)S.col[k] + a];
-                if (c < 0) continue;
-                P.col.push_back(c);
-                P.val.push_back(S.w[k]);
+                const int64_t j = S.col[k];
+                if (blk_of[k] >= 0) {
+                    for (int b = 0; b < 3; ++b) {
+                        const int32_t c = freeIndex[3 * j + b];
+                        if (c >= 0) row.push_back({c, S.bval[9 * blk_of[k] + 3 * a + b]});
+                    }
+                } else {
+                    const int32_t c = freeIndex[3 * j + a];
+                    if (c >= 0) row.push_back({c, S.w[k]});
+                }
+            }
+            std::sort(row.begin(), row.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
+            for (const auto& e : row) {
+                P.col.push_back(e.first);
+                P.val.push_back(e.second);
             }
             P.ptr[r + 1] = (int64_t)P.col.size();
         }

@@ -1,20 +1,28 @@
-// MULTIGRID: host restatement of the reference's operator-producing subset
-// (MULTIGRID.h:10-95) for uniformly refined hexahedral octrees:
-//   REFINE (pattern 0)   MULTIGRID.h:375-545   node creation order reproduced exactly, so the
+// MULTIGRID: host restatement of the reference's operator-producing subset (MULTIGRID.h:10-95):
+//   REFINE (pattern 0)   MULTIGRID.h:375-545   uniform refinement of the generators; node
+//                                              creation order reproduced exactly, so the
 //                                              level-ordered numbering equals the reference's
-//   TRANSFER             MULTIGRID.h:756-948   level sets + scalar prolongation stencils
+//   TRANSFER             MULTIGRID.h:756-948   level sets + scalar prolongation stencils; on any
+//                                              octree (every refinement pattern, locally refined
+//                                              meshes): the hanging level past maxiLeve, coupled
+//                                              nodes (coupNode / coupReps), the position numbering
+//   PATCH                MULTIGRID.h:722-754   hanging nodes moved to their parents' average
 //   STIF_MATR            MULTIGRID.h:950-1039  8-node hex, 3x3x3 Gauss, isotropic
 //   GET_VOLUME           MULTIGRID.h:1041-1082
-//   CONSTRAINT(1)        MULTIGRID.h:1102-1255 Galerkin hierarchy, Dirichlet condensation
+//   CONSTRAINT(1)        MULTIGRID.h:1102-1255 nodal rotations (nodeRota: R^T K R and the rotated
+//                                              prolongation blocks), the hanging level's Galerkin
+//                                              step, the hierarchy, Dirichlet condensation
 //   ADDITIONAL_FORCE     MULTIGRID.h:1257-1261
 //   OUTP_SUB1            MULTIGRID.h:1263-1281
-// Out of scope here: local/anisotropic refinement, hanging nodes, nodal
-// rotations (nodeRota), coupling nodes, stress recovery, text output.  (The device solver takes
-// a rotated hierarchy built by the reference itself: mgpis_gpu_create_prol.)
+// A general tree comes in through the C ABI (ddpca_multigrid_*, capi_multigrid.cpp) with the
+// element tree the caller's REFINE produced; TRANSFER then renumbers the nodes to the reference's
+// positions (posiNode keeps the original ids: earlTran).  Out of scope here:
+// the refinement edit itself on curved surfaces (CURVEDS), stress recovery, text output.
 #pragma once
 #include <array>
 #include <cstdint>
 #include <map>
+#include <set>
 #include <unordered_map>
 #include <vector>
 
@@ -26,7 +34,11 @@ struct TreeElem {
     int64_t parent = -1;
     std::array<int64_t, 8> cornNode{};
     int level = 0;
-    int64_t firstChild = -1;  // 8 children are consecutive (ADD_ELEMENT order)
+    int64_t firstChild = -1;  // REFINE_ALL: the 8 children are consecutive (ADD_ELEMENT order)
+    int refiPatt = 7;         // PREP.h TREE_ELEM: 0 xi-eta-zeta, 1 xi-eta, 2 eta-zeta, 3 zeta-xi,
+                              // 4 xi, 5 eta, 6 zeta (the pattern the element WAS refined with), 7 leaf
+    std::vector<int64_t> children;  // general trees (capi_multigrid.cpp); REFINE_ALL fills it too
+    bool leaf() const { return firstChild < 0 && children.empty(); }
 };
 
 class MULTIGRID {
@@ -49,6 +61,19 @@ public:
     std::vector<int64_t> leveCount;   // nodes of levels <= l  (levels 0..maxiLeve)
     std::vector<Stencil> scalProl;    // level l+1 nodes x level l nodes
     void TRANSFER();
+    // general trees (MULTIGRID.h:49-58, 84): coupled nodes represented by coupReps, nodal rotations
+    std::set<int64_t> coupNode;
+    int64_t coupReps = -1;
+    std::map<int64_t, std::array<double, 9>> nodeRota;  // node -> 3x3 row-major
+    // after TRANSFER on a general tree: node ids ARE positions (MULTIGRID.h:884-910); posiNode[p] =
+    // the node's original id (earlTran), hangStencil = prolOper[maxiLeve]'s stencil (all nodes x
+    // level-maxiLeve nodes, identity on the latter), empty without a hanging level
+    bool general = false;
+    std::vector<int64_t> posiNode;
+    Stencil hangStencil;
+    // the reference's algorithm on any tree (forced on uniform trees too with force_general, tests)
+    void TRANSFER_GENERAL();
+    bool force_general = false;
     // Hanging level (operator-level builder only): the reference puts hanging nodes of local
     // refinement and coupled nodes on a level maxiLeve + 1 outside the MGPIS hierarchy
     // (MULTIGRID.h:836-848, 870-875, 884-910); their values are rows of prolOper[maxiLeve] applied
@@ -72,6 +97,10 @@ public:
     std::map<int64_t, double> exteForc;  // external nodal forces
     void LOAD_ACCU(int64_t dof, double v);
     std::vector<Bsr3> levelStif;          // unconstrained Galerkin operators origStif[l]
+    // prolOper[l] (MULTIGRID.h:1141-1181): scalProl[l] with the nodal rotations' 3x3 blocks as
+    // block entries (== scalProl without nodeRota), and the hanging level's prolOper[maxiLeve]
+    std::vector<Stencil> prolOper;
+    Stencil prolHang;
     std::vector<uint8_t> consFlag;        // 3N: 1 free, 0 constrained
     std::vector<int32_t> freeIndex;       // 3N: condensed index or -1
     std::vector<int64_t> freeCount;       // free dofs on level l
@@ -89,6 +118,9 @@ public:
     // reference-layout operators (MGPIS::consStif / realProl, condensed scalar CSR)
     Csr consStif(int64_t level) const;
     Csr realProl(int64_t level) const;  // level+1 <- level
+    // rows of prolOper[maxiLeve] past the MGPIS fine level (positions x level-maxiLeve positions),
+    // the hanging level's values (OUTP_SUB1, MULTIGRID.h:1279)
+    Csr hangRows() const;
 };
 
 // Coarse-mesh builders used by the examples (node creation order as in the reference).

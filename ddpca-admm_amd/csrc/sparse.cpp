@@ -25,7 +25,101 @@ void Bsr3::apply(const double* x, double* y) const {
     }
 }
 
+namespace {
+// C = P^T A P with P = S (x) I3 plus S's 3x3 block entries (rotated nodes): per coarse node, the
+// blocks B1^T A_f1f2 B2 over the entries (f1 -> c1) and (f2 -> c2), a scalar entry being w I
+Bsr3 galerkin_rap_blocks(const Bsr3& A, const Stencil& S) {
+    const int64_t nc = S.nc;
+    std::vector<int64_t> blk_of(S.col.size(), -1);
+    for (size_t q = 0; q < S.bent.size(); ++q) blk_of[S.bent[q]] = (int64_t)q;
+    std::vector<int64_t> tptr(nc + 1, 0);
+    for (int64_t f = 0; f < S.nf; ++f)
+        for (int64_t k = S.ptr[f]; k < S.ptr[f + 1]; ++k) tptr[S.col[k] + 1]++;
+    for (int64_t c = 0; c < nc; ++c) tptr[c + 1] += tptr[c];
+    std::vector<int64_t> tent(tptr[nc]);  // S^T: coarse node -> entry index
+    std::vector<int32_t> tfine(tptr[nc]);
+    {
+        std::vector<int64_t> fill(tptr.begin(), tptr.end() - 1);
+        for (int64_t f = 0; f < S.nf; ++f)
+            for (int64_t k = S.ptr[f]; k < S.ptr[f + 1]; ++k) {
+                const int64_t p = fill[S.col[k]]++;
+                tent[p] = k;
+                tfine[p] = (int32_t)f;
+            }
+    }
+    auto block = [&](int64_t k, double B[9]) {
+        if (blk_of[k] >= 0) std::copy(&S.bval[9 * blk_of[k]], &S.bval[9 * blk_of[k]] + 9, B);
+        else
+            for (int q = 0; q < 9; ++q) B[q] = q % 4 == 0 ? S.w[k] : 0.0;
+    };
+    std::vector<std::vector<int32_t>> rcol(nc);
+    std::vector<std::vector<double>> rval(nc);
+#pragma omp parallel
+    {
+        std::vector<int32_t> mark(nc, -1);
+        std::vector<int32_t> cols;
+        std::vector<double> acc;
+#pragma omp for schedule(dynamic, 64)
+        for (int64_t c1 = 0; c1 < nc; ++c1) {
+            cols.clear();
+            acc.clear();
+            for (int64_t t = tptr[c1]; t < tptr[c1 + 1]; ++t) {
+                const int64_t f1 = tfine[t];
+                double B1[9];
+                block(tent[t], B1);
+                for (int64_t k = A.ptr[f1]; k < A.ptr[f1 + 1]; ++k) {
+                    const int64_t f2 = A.col[k];
+                    const double* Ak = A.block(k);
+                    double T[9];  // B1^T A_f1f2
+                    for (int a = 0; a < 3; ++a)
+                        for (int b = 0; b < 3; ++b)
+                            T[3 * a + b] = B1[a] * Ak[b] + B1[3 + a] * Ak[3 + b] + B1[6 + a] * Ak[6 + b];
+                    for (int64_t s = S.ptr[f2]; s < S.ptr[f2 + 1]; ++s) {
+                        const int32_t c2 = S.col[s];
+                        double B2[9];
+                        block(s, B2);
+                        int32_t pos = mark[c2];
+                        if (pos < 0) {
+                            pos = (int32_t)cols.size();
+                            mark[c2] = pos;
+                            cols.push_back(c2);
+                            acc.resize(acc.size() + 9, 0.0);
+                        }
+                        double* o = &acc[9 * (size_t)pos];
+                        for (int a = 0; a < 3; ++a)
+                            for (int b = 0; b < 3; ++b)
+                                o[3 * a + b] += T[3 * a] * B2[b] + T[3 * a + 1] * B2[3 + b] + T[3 * a + 2] * B2[6 + b];
+                    }
+                }
+            }
+            std::vector<int32_t> order(cols.size());
+            std::iota(order.begin(), order.end(), 0);
+            std::sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return cols[a] < cols[b]; });
+            rcol[c1].resize(cols.size());
+            rval[c1].resize(9 * cols.size());
+            for (size_t q = 0; q < order.size(); ++q) {
+                rcol[c1][q] = cols[order[q]];
+                std::copy(&acc[9 * (size_t)order[q]], &acc[9 * (size_t)order[q]] + 9, &rval[c1][9 * q]);
+            }
+            for (int32_t c2 : cols) mark[c2] = -1;
+        }
+    }
+    Bsr3 C;
+    C.nb = C.mb = nc;
+    C.ptr.assign(nc + 1, 0);
+    for (int64_t c = 0; c < nc; ++c) C.ptr[c + 1] = C.ptr[c] + (int64_t)rcol[c].size();
+    C.col.resize(C.ptr[nc]);
+    C.val.resize(9 * C.ptr[nc]);
+    for (int64_t c = 0; c < nc; ++c) {
+        std::copy(rcol[c].begin(), rcol[c].end(), C.col.begin() + C.ptr[c]);
+        std::copy(rval[c].begin(), rval[c].end(), C.val.begin() + 9 * C.ptr[c]);
+    }
+    return C;
+}
+}  // namespace
+
 Bsr3 galerkin_rap(const Bsr3& A, const Stencil& S) {
+    if (!S.bent.empty()) return galerkin_rap_blocks(A, S);
     const int64_t nc = S.nc;
     // S^T: coarse node -> list of (fine node, weight)
     std::vector<int64_t> tptr(nc + 1, 0);

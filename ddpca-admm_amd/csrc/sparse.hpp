@@ -48,8 +48,8 @@ struct Stencil {
     std::vector<double> bval;
 };
 
-// C = S^T A S for a BSR3 A on the fine nodes and a scalar stencil S (Galerkin product,
-// MULTIGRID.h:1182-1184 with prolOper = S (x) I3).
+// C = P^T A P for a BSR3 A on the fine nodes and P = S (x) I3 (Galerkin product,
+// MULTIGRID.h:1182-1184), S's block entries (rotated nodes) taken as their 3x3 blocks.
 Bsr3 galerkin_rap(const Bsr3& A, const Stencil& S);
 
 // Expand to scalar CSR keeping only dofs with keep[dof] != 0 (consOper * A * consOper^T,

@@ -279,6 +279,42 @@ int ddpca_problem_set_subdomain_prol(ddpca_problem_t p, int64_t tv, int nlev, co
  * interface products see every node, and the body-balance RHS folds the hanging rows in
  * (ADDITIONAL_FORCE's prolOper^T, MULTIGRID.h:1257-1261). */
 int ddpca_problem_set_hanging(ddpca_problem_t p, int64_t tv, int64_t nnodes_all, const ddpca_csr_t* hang);
+
+/* ---- the MULTIGRID operator pipeline on a caller's element tree (host only, capi_multigrid.cpp)
+ * Replaces MULTIGRID::TRANSFER + PATCH + STIF_MATR + CONSTRAINT(1) (MULTIGRID.h:722-1255) for any
+ * octree the reference's REFINE / GRLE_CHECK produced: every refinement pattern, local refinement
+ * (hanging nodes on the level maxiLeve + 1, moved to their parents' average by PATCH), coupled
+ * nodes (coupNode / coupReps), nodal rotations (nodeRota).
+ *   create: nnode node ids 0..nnode-1 with coordinates (3 per node: nodeCoor); per element e
+ *     (elemVect order): corner[8e..8e+7] (cornNode), parent[e] (-1 at level 0), level[e],
+ *     refiPatt[e] (the pattern a refined element was split with, 0..6; 7 = leaf), children
+ *     child[child_ptr[e] .. child_ptr[e+1]) (TREE_ELEM::children, empty = leaf).
+ *   set: "consDofv" (n node-id dofs 3 node + comp, val = prescribed value; set BEFORE the loads,
+ *     as the reference requires), "exteForc" (n dofs, val: LOAD_ACCU in order; loads on
+ *     constrained dofs are dropped), "nodeRota" (n nodes, val = 9 n, row-major 3x3 each),
+ *     "coupNode" (n nodes), "coupReps" (n = 1: the representative node or -1), "material"
+ *     (n = 2: val = {mateElas, matePois}; default 210e9, 0.3).
+ *   build: TRANSFER, PATCH, STIF_MATR, origStif += extra (nullable: 3 nnode x 3 nnode CSR in
+ *     node ids, e.g. the contact interfaces' systMass, MCONTACT.h:816-822), CONSTRAINT(1).
+ *   view (after build; same dtype codes as ddpca_problem_view): "posiNode" (int64 per position:
+ *     the node id, i.e. earlTran), "nodeCoor" (3 per node id, after PATCH), "leveCount" (int64,
+ *     cumulative positions per level 0..maxiLeve, then the total incl. the hanging level),
+ *     "freeCount", "consFlag" (uint8 per position dof), "consForc", "dispForc", and CSR parts
+ *     ("<X>:ptr|col|val|shape") of "K" (MGPIS::consStif[level]), "P" (MGPIS::realProl[level],
+ *     level+1 <- level) and "H" (rows 3 NL.. of prolOper[maxiLeve], positions: the hanging level).
+ *   set_subdomain_multigrid: subdomain tv of an operator-level problem from the built tree (what
+ *     set_subdomain(_prol) + set_hanging take from the reference's own MULTIGRID); interface
+ *     operators handed over afterwards are in the position numbering (posiNode maps them). */
+typedef struct ddpca_multigrid* ddpca_multigrid_t;
+int ddpca_multigrid_create(int64_t nnode, const double* coords, int64_t nelem, const int64_t* corner,
+                           const int64_t* parent, const int64_t* level, const int64_t* refiPatt,
+                           const int64_t* child_ptr, const int64_t* child, ddpca_multigrid_t* out);
+int ddpca_multigrid_set(ddpca_multigrid_t g, const char* what, int64_t n, const int64_t* idx, const double* val);
+int ddpca_multigrid_build(ddpca_multigrid_t g, const ddpca_csr_t* extra);
+int ddpca_multigrid_view(ddpca_multigrid_t g, const char* what, int64_t level, const void** data, int64_t* count,
+                         int* dtype);
+int ddpca_problem_set_subdomain_multigrid(ddpca_problem_t p, int64_t tv, ddpca_multigrid_t g);
+int ddpca_multigrid_destroy(ddpca_multigrid_t g);
 /* Interface ts between contBody {body0, body1} with fricCoef fric (< 0 glued, 0 frictionless,
  * > 0 Coulomb; comp = 1 if fric == 0 else 3), nip integration points, nnc_s contact nodes per
  * side; pemaDiag / inpoNgap have comp*nip entries.  ops[7*s + k] is side s's

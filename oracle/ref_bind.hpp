@@ -16,6 +16,7 @@
 // subdomain with rotated nodes (nodeRota) hands its realProl over instead of scalProl: its
 // transfers carry w R_off^T R_par blocks (MULTIGRID.h:1141-1181) a scalar stencil cannot hold.
 #pragma once
+#include <functional>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -122,14 +123,98 @@ inline mgpis_t mgpis_create_prol(MULTIGRID& g, int device, const mgpis_options_t
     return out;
 }
 
+// Read an operator back from a problem (ddpca_problem_view's CSR parts) as an Eigen matrix.
+inline SpMat problem_csr(ddpca_problem_t p, const std::string& base, int64_t index, int64_t level) {
+    auto get = [&](const std::string& part, const void** d, int64_t* n) {
+        int dt = -1;
+        check(ddpca_problem_view(p, (base + ":" + part).c_str(), index, level, d, n, &dt));
+    };
+    const void *sh, *pt, *cl, *vl;
+    int64_t n0, n1, n2, n3;
+    get("shape", &sh, &n0);
+    const int64_t rows = ((const int64_t*)sh)[0], cols = ((const int64_t*)sh)[1];
+    get("ptr", &pt, &n1);
+    get("col", &cl, &n2);
+    get("val", &vl, &n3);
+    std::vector<Eigen::Triplet<double>> t;
+    for (int64_t r = 0; r < rows; ++r)
+        for (int64_t k = ((const int64_t*)pt)[r]; k < ((const int64_t*)pt)[r + 1]; ++k)
+            t.emplace_back(r, ((const int32_t*)cl)[k], ((const double*)vl)[k]);
+    SpMat m(rows, cols);
+    m.setFromTriplets(t.begin(), t.end());
+    return m;
+}
+
+// A MULTIGRID's element tree as REFINE left it (before TRANSFER) -> the library's operator
+// pipeline (ddpca_multigrid_*), built with `extra` added to origStif (node ids; ESTABLISH adds the
+// contact interfaces' systMass there, MCONTACT.h:816-822).  REFINE sizes children to 8 and fills
+// the pattern's 8 / 4 / 2 (MULTIGRID.h:515-533): only those go over.
+inline ddpca_multigrid_t tree_build(const MULTIGRID& g, const SpMat* extra = nullptr) {
+    const int64_t nn = (int64_t)g.nodeCoor.size(), ne = (int64_t)g.elemVect.size();
+    std::vector<double> xyz(3 * nn);
+    for (const auto& nc : g.nodeCoor)
+        for (int a = 0; a < 3; ++a) xyz[3 * nc.first + a] = nc.second[a];
+    std::vector<int64_t> corner(8 * ne), parent(ne), level(ne), patt(ne), cptr{0}, child;
+    for (int64_t e = 0; e < ne; ++e) {
+        const TREE_ELEM& t = g.elemVect[e];
+        for (int k = 0; k < 8; ++k) corner[8 * e + k] = t.cornNode[k];
+        parent[e] = t.parent;
+        level[e] = t.level;
+        patt[e] = t.refiPatt;
+        const size_t nch = t.children.empty() ? 0 : t.refiPatt == 0 ? 8 : t.refiPatt <= 3 ? 4 : 2;
+        for (size_t q = 0; q < nch; ++q) child.push_back(t.children[q]);
+        cptr.push_back((int64_t)child.size());
+    }
+    ddpca_multigrid_t h = nullptr;
+    check(ddpca_multigrid_create(nn, xyz.data(), ne, corner.data(), parent.data(), level.data(), patt.data(), cptr.data(),
+                                 child.data(), &h));
+    std::vector<int64_t> idx;
+    std::vector<double> val;
+    auto put = [&](const char* what) {
+        check(ddpca_multigrid_set(h, what, (int64_t)idx.size(), idx.data(), val.data()));
+        idx.clear();
+        val.clear();
+    };
+    for (const auto& kv : g.consDofv) idx.push_back(kv.first), val.push_back(kv.second);
+    put("consDofv");  // before the loads, as the reference sets them
+    for (const auto& kv : g.exteForc) idx.push_back(kv.first), val.push_back(kv.second);
+    put("exteForc");
+    for (const auto& kv : g.nodeRota) {
+        idx.push_back(kv.first);
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) val.push_back(kv.second(i, j));
+    }
+    put("nodeRota");
+    for (long c : g.coupNode) idx.push_back(c);
+    check(ddpca_multigrid_set(h, "coupNode", (int64_t)idx.size(), idx.data(), nullptr));
+    idx.clear();
+    const int64_t reps = g.coupReps;
+    check(ddpca_multigrid_set(h, "coupReps", 1, &reps, nullptr));
+    const double mat[2] = {g.mateElas, g.matePois};
+    check(ddpca_multigrid_set(h, "material", 2, nullptr, mat));
+    if (extra) {
+        const Csr e(*extra);
+        const ddpca_csr_t v = e.view();
+        check(ddpca_multigrid_build(h, &v));
+    } else {
+        check(ddpca_multigrid_build(h, nullptr));
+    }
+    return h;
+}
+
 // MCONTACT after ESTABLISH() -> an established device problem; with muscSett = 2 its
 // MULTISCALE_1 coarse operators go along (globTran_D_1 columns moved to positions like the
 // systTran rows; accuProl and globTran_1 are in free / contact numbering already).
-inline ddpca_problem_t from_reference(MCONTACT& mc) {
+// set_sub (optional): sets subdomain tv itself (e.g. from the element tree through
+// ddpca_multigrid_* + ddpca_problem_set_subdomain_multigrid) and returns true, or false to let the
+// reference's MULTIGRID operators go.
+inline ddpca_problem_t from_reference(MCONTACT& mc,
+                                      const std::function<bool(ddpca_problem_t, int64_t)>& set_sub = {}) {
     const int64_t nsub = (int64_t)mc.multGrid.size(), nint = (int64_t)mc.searCont.size();
     ddpca_problem_t p = nullptr;
     check(ddpca_problem_empty(nsub, nint, &p));
     for (int64_t tv = 0; tv < nsub; ++tv) {
+        if (set_sub && set_sub(p, tv)) continue;
         MULTIGRID& g = mc.multGrid[tv];
         Hierarchy h(g);
         if (g.nodeRota.empty()) {

@@ -8,10 +8,15 @@
 // level, ddpca_problem_set_hanging) to the device, whose ADMM loop then runs.  One JSON line on
 // stderr: iterations, resuDisp difference (node-id order, every node incl. the hanging ones), the
 // resuMoni trajectory and the contact pressures against the reference's last resuCont files.
-//   ref_cylinder copyNumb locaLeve globInho bandWidt
+// "native": every subdomain's operators come from the library's own pipeline on the element tree
+// (ddpca_multigrid_*: TRANSFER with the hanging level, PATCH, STIF_MATR + the contact systMass,
+// CONSTRAINT(1)) instead of the reference's MULTIGRID; the interface and coarse operators stay the
+// reference's.
+//   ref_cylinder copyNumb locaLeve globInho bandWidt [native]
 #include <unistd.h>
 
 #include <cstdio>
+#include <memory>
 #include <fstream>
 #include <sstream>
 
@@ -56,7 +61,42 @@ int main(int argc, char** argv) {
         nnodes += (long)g.nodeCoor.size();
         nhang += (long)g.leveNode[g.mgpi.maxiLeve + 1].size();
     }
-    ddpca_problem_t p = ddpca_bind::from_reference(c);
+    const bool native = argc > 5 && std::string(argv[5]) == "native";
+    std::unique_ptr<CYLINDER_1> trees;  // the same meshes again, before any TRANSFER / PATCH
+    if (native) {
+        if (!std::freopen("/dev/null", "w", stdout)) return 2;
+        trees.reset(new CYLINDER_1);
+        trees->copyNumb = copyNumb;
+        trees->locaLeve = locaLeve;
+        trees->globInho = globInho;
+        trees->bandWidt = bandWidt;
+        trees->MESH();
+        std::fflush(stdout);
+        dup2(saved, 1);
+    }
+    double dK = 0.0;  // native: our consStif vs the reference's, relative to the level maximum
+    ddpca_problem_t p = ddpca_bind::from_reference(c, [&](ddpca_problem_t prob, int64_t tv) {
+        if (!native) return false;
+        ddpca_bind::SpMat extra(3 * c.multGrid[tv].nodeCoor.size(), 3 * c.multGrid[tv].nodeCoor.size());
+        for (size_t ts = 0; ts < c.searCont.size(); ++ts)
+            for (int s = 0; s < 2; ++s)
+                if (c.contBody[ts][s] == tv) extra += c.systMass[ts][s];
+        ddpca_multigrid_t h = ddpca_bind::tree_build(trees->multGrid[tv], &extra);
+        ddpca_bind::check(ddpca_problem_set_subdomain_multigrid(prob, tv, h));
+        ddpca_multigrid_destroy(h);
+        const MULTIGRID& g = c.multGrid[tv];
+        for (long l = 0; l <= g.mgpi.maxiLeve; ++l) {
+            const ddpca_bind::SpMat K = ddpca_bind::problem_csr(prob, "K", tv, l);
+            const ddpca_bind::SpMat D = K - g.mgpi.consStif[l];
+            double m = 0.0, r = 0.0;
+            for (int k = 0; k < D.outerSize(); ++k)
+                for (ddpca_bind::SpMat::InnerIterator it(D, k); it; ++it) m = std::max(m, std::abs(it.value()));
+            for (int k = 0; k < g.mgpi.consStif[l].outerSize(); ++k)
+                for (ddpca_bind::SpMat::InnerIterator it(g.mgpi.consStif[l], k); it; ++it) r = std::max(r, std::abs(it.value()));
+            dK = std::max(dK, m / r);
+        }
+        return true;
+    });
     std::vector<int32_t> owner(c.multGrid.size(), 0);
     mcontact_t h = nullptr;
     ddpca_bind::check(mcontact_gpu_create(p, 0, 0, 1, owner.data(), nullptr, &h));
@@ -117,9 +157,10 @@ int main(int argc, char** argv) {
     mcontact_gpu_destroy(h);
     ddpca_problem_destroy(p);
     std::fprintf(stderr,
-                 "{\"subdomains\": %zu, \"nodes\": %ld, \"hanging_nodes\": %ld, \"iters_gpu\": %ld, \"iters_ref\": %ld, "
+                 "{\"native\": %s, \"K_rel\": %.3g, \"subdomains\": %zu, \"nodes\": %ld, \"hanging_nodes\": %ld, \"iters_gpu\": %ld, \"iters_ref\": %ld, "
                  "\"resuDisp_rel\": %.3g, \"moni_rows\": %ld, \"moni_rel\": %.3g, \"pressure_rel\": %.3g, \"interfaces\": %s}\n",
-                 c.multGrid.size(), nnodes, nhang, (long)n_gpu, (long)c.iterNumbReco, du, (long)kmax, dmoni, dp_all,
+                 native ? "true" : "false", dK, c.multGrid.size(), nnodes, nhang, (long)n_gpu, (long)c.iterNumbReco, du,
+                 (long)kmax, dmoni, dp_all,
                  itf.c_str());
     return 0;
 }

@@ -6,6 +6,10 @@ Tolerances: coordinates 1e-15 absolute (same arithmetic), operator fingerprints 
 different order than Eigen's, which moves entries at the 1e-16 level; structures (nnz, node
 ordering, constrained dofs, contact-node numbering) must be identical.
 """
+import json
+import subprocess
+from pathlib import Path
+
 import numpy as np
 import pytest
 
@@ -118,3 +122,32 @@ def test_bad_arguments_raise(ddpca):
     P = ddpca.Problem("beam", 8, 2, 2, 1, 1, 1, 1)
     with pytest.raises(ddpca.DdpcaError):
         P.array("consForc", 5)
+
+
+@pytest.mark.parametrize("args", [("cylinder", "2", "1"), ("cylinder", "4", "2"), ("cylinder", "2", "1", "rot"),
+                                  ("beam", "2"), ("beam", "2", "rot")],
+                         ids=["cylinder", "cylinder-locaLeve4", "cylinder-rotated", "beam-uniform", "beam-rotated"])
+def test_general_tree_pipeline_matches_reference(tmp_path, args):
+    """The host operator pipeline on general octrees (ddpca_multigrid_*: TRANSFER with the hanging
+    level and coupled nodes, PATCH, STIF_MATR, CONSTRAINT(1) with nodeRota; MULTIGRID.h:722-1255)
+    against the reference's own pipeline on the same element trees (oracle/ref_multigrid.cpp).
+    CYLINDER_1's meshes: curved cylinders, 4-way inhomogeneous refinement, local refinement towards
+    the contact lines (632 / 3136 hanging nodes per subdomain); "rot" puts nodal rotations on every
+    seventh node (fine, coarse and hanging ones); BEAM is a uniform tree through the same general
+    path.  Positions, level counts, consFlag, dispForc and the PATCHed coordinates must be identical,
+    realProl and the hanging rows of prolOper[maxiLeve] exact, consStif within 1e-13 of the level's
+    largest entry (element stiffness and Galerkin products summed in another order), consForc 1e-12."""
+    exe = Path(__file__).resolve().parents[1] / "oracle" / "_ref" / "ref_multigrid"
+    if not exe.exists():
+        pytest.skip("oracle/_ref/ref_multigrid is built where the reference is (oracle/Makefile)")
+    out = subprocess.run([str(exe), *args], capture_output=True, text=True, timeout=600, cwd=tmp_path)
+    lines = [json.loads(l) for l in out.stdout.splitlines() if l.startswith("{")]
+    assert out.returncode == 0 and lines and lines[-1]["ok"], (out.stdout[-3000:], out.stderr[-2000:])
+    for sub in lines[:-1]:
+        assert sub["positions_equal"] and sub["levels_equal"] and sub["consFlag_equal"] and sub["dispForc_equal"], sub
+        assert sub["coords"] == 0.0 and sub["realProl"] == 0.0 and sub["hang"] == 0.0, sub
+        assert sub["K_rel"] <= 1e-13 and sub["consForc_rel"] <= 1e-12, sub
+    if args[0] == "cylinder":
+        assert lines[-1]["hanging_nodes"] > 0
+    if "rot" in args:
+        assert all(sub["rotated"] > 0 for sub in lines[:-1])

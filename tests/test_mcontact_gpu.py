@@ -353,8 +353,14 @@ def test_block_patch_pressure_known_answer(gpu, tmp_path, musc):
             assert abs(itf[k] - 1e7) <= 1e-5 * 1e7, (musc, itf)
 
 
-def test_cylinder_known_answer(gpu, tmp_path):
-    """The reference's own CYLINDER example (CYLINDER_1.h, copyNumb 1: four cylinder bodies in
+@pytest.mark.parametrize("native", [False, True], ids=["reference-operators", "native-operators"])
+def test_cylinder_known_answer(gpu, tmp_path, native):
+    """native: every subdomain's MGPIS hierarchy, consForc and hanging rows come from the library's
+    own pipeline on the reference's element trees (ddpca_multigrid_*: TRANSFER with the hanging
+    level, PATCH, STIF_MATR + the contact systMass, CONSTRAINT(1)) instead of the
+    reference's MULTIGRID; consStif within 1e-13 of the reference's, the same answers required.
+
+    The reference's own CYLINDER example (CYLINDER_1.h, copyNumb 1: four cylinder bodies in
     Hertz contact, locally refined towards the contact lines -- 35 % of the nodes on the hanging
     level past the MGPIS hierarchy -- contact search on the curved surfaces, LATIN-type coarse
     space muscSett = 1, doleMcsc = 2; oracle/ref_cylinder.cpp, reduced locaLeve 4, globInho 2,
@@ -369,11 +375,13 @@ def test_cylinder_known_answer(gpu, tmp_path):
     exe = Path(__file__).resolve().parents[1] / "oracle" / "_ref" / "ref_cylinder"
     if not exe.exists():
         pytest.skip("oracle/_ref/ref_cylinder is built only where the reference is (travels with the snapshot)")
-    out = subprocess.run([str(exe), "1", "4", "2", "2e-4"], capture_output=True, text=True, timeout=170,
-                         env=dict(os.environ), cwd=tmp_path)
+    out = subprocess.run([str(exe), "1", "4", "2", "2e-4"] + (["native"] if native else []), capture_output=True,
+                         text=True, timeout=170, env=dict(os.environ), cwd=tmp_path)
     assert out.returncode == 0, out.stderr[-2000:]
     res = json.loads(out.stderr.strip().splitlines()[-1])
+    print(res)
     assert res["hanging_nodes"] > 0, res
+    assert res["native"] == native and res["K_rel"] <= 1e-13, res
     assert abs(res["iters_gpu"] - res["iters_ref"]) <= 1, res
     assert res["resuDisp_rel"] <= 1e-6, res
     assert res["moni_rel"] <= 1e-7, res
