@@ -11,12 +11,18 @@
 // "native": every subdomain's operators come from the library's own pipeline on the element tree
 // (ddpca_multigrid_*: TRANSFER with the hanging level, PATCH, STIF_MATR + the contact systMass,
 // CONSTRAINT(1)) instead of the reference's MULTIGRID; the interface and coarse operators stay the
-// reference's.
-//   ref_cylinder copyNumb locaLeve globInho bandWidt [native]
+// reference's.  owners (e.g. 0011): the same problem on two device ranks in one process, connected
+// by the in-process test transport (mcontact_gpu_comm_local), subdomain tv owned by rank
+// owners[tv]: rank-local batches with the hanging level, the gamma halves of the cross-rank
+// curved contacts exchanged, the LATIN coarse space's operator rows filled by rank 0 and summed,
+// the MONITOR all-reduce -- compared with the single-rank device run (iterations equal, resuMoni
+// 1e-8, displacements 1e-8, contact tractions 1e-7 of the largest).
+//   ref_cylinder copyNumb locaLeve globInho bandWidt [native|ref] [owners]
 #include <unistd.h>
 
 #include <cstdio>
 #include <memory>
+#include <thread>
 #include <fstream>
 #include <sstream>
 
@@ -154,13 +160,75 @@ int main(int argc, char** argv) {
         itf += buf;
     }
     itf += "]";
+    // ---- the same problem on two ranks (in-process transport)
+    std::string ranks2 = "null";
+    if (argc > 6) {
+        const std::string own = argv[6];
+        if (own.size() != c.multGrid.size()) {
+            std::fprintf(stderr, "owners: one digit per subdomain\n");
+            return 2;
+        }
+        std::vector<int32_t> ow(own.size());
+        for (size_t tv = 0; tv < own.size(); ++tv) ow[tv] = own[tv] - '0';
+        mcontact_t hr[2] = {nullptr, nullptr};
+        for (int r = 0; r < 2; ++r) ddpca_bind::check(mcontact_gpu_create(p, 0, r, 2, ow.data(), nullptr, &hr[r]));
+        ddpca_bind::check(mcontact_gpu_comm_local(hr, 2));
+        int64_t nr[2] = {0, 0};
+        std::thread th[2];
+        for (int r = 0; r < 2; ++r) th[r] = std::thread([&, r] { nr[r] = mcontact_gpu_iterate(hr[r], 3000, 1); });
+        for (auto& t : th) t.join();
+        for (int r = 0; r < 2; ++r) ddpca_bind::check((int)std::min<int64_t>(nr[r], 0));
+        double dm = 0.0, du2 = 0.0, dg = 0.0;
+        int64_t cross = 0;
+        for (int r = 0; r < 2; ++r) {
+            const int64_t rows = mcontact_gpu_monitor(hr[r], nullptr, 0);
+            std::vector<double> m(rows * ncol);
+            mcontact_gpu_monitor(hr[r], m.data(), rows);
+            if (rows != nrows) dm = 1e300;
+            for (int64_t j = 0; j < ncol && rows == nrows; ++j) {
+                double scale = 0.0;
+                for (int64_t k = 0; k < rows; ++k) scale = std::max(scale, std::abs(moni[k * ncol + j]));
+                for (int64_t k = 0; k < rows; ++k) {
+                    const double a = m[k * ncol + j], b = moni[k * ncol + j];
+                    dm = std::max(dm, std::abs(a - b) / (std::abs(b) + 1e-12 * scale + 1e-300));
+                }
+            }
+        }
+        for (size_t tv = 0; tv < c.multGrid.size(); ++tv) {
+            const int64_t n = mcontact_gpu_get(h, "resuDisp", tv, nullptr, 0);
+            std::vector<double> a(n), b(n);
+            mcontact_gpu_get(h, "resuDisp", tv, b.data(), n);
+            ddpca_bind::check((int)std::min<int64_t>(mcontact_gpu_get(hr[ow[tv]], "resuDisp", tv, a.data(), n), 0));
+            double d = 0.0, s = 0.0;
+            for (int64_t i = 0; i < n; ++i) d += (a[i] - b[i]) * (a[i] - b[i]), s += b[i] * b[i];
+            du2 = std::max(du2, std::sqrt(d / s));
+        }
+        for (size_t ts = 0; ts < c.searCont.size(); ++ts) {
+            const int r = ow[c.contBody[ts][0]];
+            cross += ow[c.contBody[ts][0]] != ow[c.contBody[ts][1]];
+            const int64_t n = mcontact_gpu_get(h, "inpoGamm", ts, nullptr, 0);
+            std::vector<double> a(n), b(n);
+            mcontact_gpu_get(h, "inpoGamm", ts, b.data(), n);
+            ddpca_bind::check((int)std::min<int64_t>(mcontact_gpu_get(hr[r], "inpoGamm", ts, a.data(), n), 0));
+            double gm = 0.0, d = 0.0;
+            for (int64_t i = 0; i < n; ++i) gm = std::max(gm, std::abs(b[i])), d = std::max(d, std::abs(a[i] - b[i]));
+            dg = std::max(dg, gm > 0 ? d / gm : d);
+        }
+        for (auto& x : hr) mcontact_gpu_destroy(x);
+        char buf[300];
+        std::snprintf(buf, sizeof(buf), "{\"owners\": \"%s\", \"cross_interfaces\": %ld, \"iters\": [%ld, %ld], \"moni_rel\": %.3g, "
+                      "\"resuDisp_rel\": %.3g, \"gamma_rel\": %.3g}",
+                      own.c_str(), (long)cross, (long)nr[0], (long)nr[1], dm, du2, dg);
+        ranks2 = buf;
+    }
     mcontact_gpu_destroy(h);
     ddpca_problem_destroy(p);
     std::fprintf(stderr,
                  "{\"native\": %s, \"K_rel\": %.3g, \"subdomains\": %zu, \"nodes\": %ld, \"hanging_nodes\": %ld, \"iters_gpu\": %ld, \"iters_ref\": %ld, "
-                 "\"resuDisp_rel\": %.3g, \"moni_rows\": %ld, \"moni_rel\": %.3g, \"pressure_rel\": %.3g, \"interfaces\": %s}\n",
+                 "\"resuDisp_rel\": %.3g, \"moni_rows\": %ld, \"moni_rel\": %.3g, \"pressure_rel\": %.3g, \"interfaces\": %s, "
+                 "\"ranks2\": %s}\n",
                  native ? "true" : "false", dK, c.multGrid.size(), nnodes, nhang, (long)n_gpu, (long)c.iterNumbReco, du,
                  (long)kmax, dmoni, dp_all,
-                 itf.c_str());
+                 itf.c_str(), ranks2.c_str());
     return 0;
 }

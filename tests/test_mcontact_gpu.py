@@ -388,3 +388,35 @@ def test_cylinder_known_answer(gpu, tmp_path, native):
     assert res["pressure_rel"] <= 1e-5, res
     for itf in res["interfaces"]:
         assert itf["active"] > 0, itf
+
+
+@pytest.mark.parametrize("owners", ["0011", "0101"])
+def test_cylinder_two_ranks_in_one_process(gpu, tmp_path, owners):
+    """The locally refined path across ranks (MCONTACT.h:2511-2537, 2539-2576): the reference's
+    CYLINDER_1 (hanging level, curved contacts, LATIN coarse space) on two device ranks of one
+    process connected by the in-process transport (mcontact_gpu_comm_local).  0011: cylinders
+    {0, 1} | {2, 3}, the middle contact crosses the ranks; 0101: all three contacts cross.  Each
+    rank batches its own subdomains with their hanging rows, the cross-rank gamma halves are
+    exchanged, rank 0 fills the LATIN operator's coarse contact rows and the setup all-reduce sums
+    them.  Must reproduce the single-rank device run: the same iteration count on both ranks,
+    resuMoni rows within 1e-8 (relative, floor 1e-12 of the column), displacements 1e-8, contact
+    tractions 1e-7 of the largest -- and the single-rank run the reference (as
+    test_cylinder_known_answer)."""
+    import json
+    import os
+    import subprocess
+    from pathlib import Path
+    exe = Path(__file__).resolve().parents[1] / "oracle" / "_ref" / "ref_cylinder"
+    if not exe.exists():
+        pytest.skip("oracle/_ref/ref_cylinder is built only where the reference is (travels with the snapshot)")
+    out = subprocess.run([str(exe), "1", "4", "2", "2e-4", "ref", owners], capture_output=True, text=True, timeout=240,
+                         env=dict(os.environ), cwd=tmp_path)
+    assert out.returncode == 0, out.stderr[-2000:]
+    res = json.loads(out.stderr.strip().splitlines()[-1])
+    print(res["ranks2"], res["iters_gpu"], res["iters_ref"])
+    r2 = res["ranks2"]
+    assert r2["cross_interfaces"] == (1 if owners == "0011" else 3), r2
+    assert r2["iters"] == [res["iters_gpu"], res["iters_gpu"]], (r2, res["iters_gpu"])
+    assert r2["moni_rel"] <= 1e-8 and r2["resuDisp_rel"] <= 1e-8 and r2["gamma_rel"] <= 1e-7, r2
+    assert abs(res["iters_gpu"] - res["iters_ref"]) <= 1 and res["resuDisp_rel"] <= 1e-6, res
+
