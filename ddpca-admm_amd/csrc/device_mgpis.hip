@@ -674,26 +674,48 @@ __global__ __launch_bounds__(kBlock) void k_restrict_rot(const double* rf, const
     if (m & 4) bc[3 * j + 2] += s2;
 }
 
-// x0 = A0^-1 b0 per subdomain, one wavefront per coarse dof row
+// x0 = A0^-1 b0 per subdomain, one wavefront per coarse dof row.  Rows are padded to a multiple of
+// 4 entries (ld, zero-filled), so every lane loads 16 B of the inverse per instruction (four fp32
+// or two fp64 entries) and the matching b entries as fp64 pairs; two such loads in flight per lane.
+// The padding reads b of the member's padding nodes, which the masked restriction keeps at zero.
 template <typename AT = double>
 __global__ __launch_bounds__(kBlock) void k_coarse(const AT* ainv, const int64_t* aoff, const int64_t* noff,
-                                                   const int64_t* n0, const double* b, double* x, int64_t nrow,
-                                                   const int32_t* csub, const PcgScal* sc) {
+                                                   const int64_t* n0, const int64_t* ldv, const double* b, double* x,
+                                                   int64_t nrow, const int32_t* csub, const PcgScal* sc) {
     const int64_t r = (int64_t)blockIdx.x * (kBlock / kWave) + (threadIdx.x >> 6);
     if (r >= nrow) return;
     const int sub = csub[(r / 3) >> 6];
     if (stopped(sc, sub)) return;
     const int lane = threadIdx.x & 63;
-    const int64_t lr = r - 3 * noff[sub], n = n0[sub];
+    const int64_t lr = r - 3 * noff[sub], n = n0[sub], ld = ldv[sub];
     if (lr >= n) {
         if (lane == 0) x[r] = 0.0;
         return;
     }
-    const AT* arow = ainv + aoff[sub] + lr * n;
+    const AT* arow = ainv + aoff[sub] + lr * ld;
     const double* bs = b + 3 * noff[sub];
-    double s = 0.0;
-    for (int64_t k = lane; k < n; k += kWave) s += (double)arow[k] * bs[k];
-    s = wave_sum(s);
+    constexpr int V = 16 / sizeof(AT);  // entries per 16-B load
+    double s0 = 0.0, s1 = 0.0;
+    auto chunk = [&](int64_t k) {
+        double acc = 0.0;
+        if constexpr (V == 4) {
+            const float4 a = *reinterpret_cast<const float4*>(arow + k);
+            const double2 b0 = *reinterpret_cast<const double2*>(bs + k), b1 = *reinterpret_cast<const double2*>(bs + k + 2);
+            acc = (double)a.x * b0.x + (double)a.y * b0.y + (double)a.z * b1.x + (double)a.w * b1.y;
+        } else {
+            const double2 a = *reinterpret_cast<const double2*>(arow + k);
+            const double2 b0 = *reinterpret_cast<const double2*>(bs + k);
+            acc = a.x * b0.x + a.y * b0.y;
+        }
+        return acc;
+    };
+    int64_t k = (int64_t)V * lane;
+    for (; k + V * kWave < ld; k += 2 * V * kWave) {
+        s0 += chunk(k);
+        s1 += chunk(k + V * kWave);
+    }
+    if (k < ld) s0 += chunk(k);
+    const double s = wave_sum(s0 + s1);
     if (lane == 0) x[r] = s;
 }
 
@@ -1788,7 +1810,7 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
     }
     if (!no_coarse) {
         std::vector<double> packed;
-        std::vector<int64_t> ao(nsub), no(nsub), nz(nsub);
+        std::vector<int64_t> ao(nsub), no(nsub), nz(nsub), ldv(nsub);
         for (int s = 0; s < nsub; ++s) {
             const Bsr3& A = *subs[s].K[clev];
             const uint8_t* fr = subs[s].dof_free;
@@ -1822,7 +1844,13 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
             ao[s] = (int64_t)packed.size();
             no[s] = lev[clev].noff[s];
             nz[s] = n0;
-            packed.insert(packed.end(), D.begin(), D.end());
+            const int64_t ld = (n0 + 3) / 4 * 4;  // rows padded for 16-B loads (k_coarse)
+            if (ld > 3 * pad64(lev[clev].nloc[s])) throw ApiError(DDPCA_ESTATE, "coarse row padding beyond the member");
+            ldv[s] = ld;
+            for (int64_t r = 0; r < n0; ++r) {
+                packed.insert(packed.end(), D.begin() + r * n0, D.begin() + (r + 1) * n0);
+                packed.insert(packed.end(), ld - n0, 0.0);
+            }
         }
         if (vc32()) {
             // reduced-precision preconditioner storage: the (exactly symmetric) dense inverses in
@@ -1834,6 +1862,7 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
         aoff.upload(ao);
         c_noff.upload(no);
         c_n.upload(nz);
+        c_ld.upload(ldv);
         if (std::getenv("DDPCA_VERBOSE"))
             std::fprintf(stderr, "[ddpca] exact coarse solve on level %d (%zu doubles of dense inverses)\n", clev, packed.size());
     }
@@ -2202,9 +2231,9 @@ void MgpisDevice::vcycle(const double* rin, double* zout, bool dot, bool first_d
     const int cl = clev;  // the exact dense solve; levels below it are not visited
     if (Lf == cl) {
         if (ainv32.p) hipLaunchKernelGGL(k_coarse<float>, dim3(ceil_div(3 * lev[cl].nn, 4)), dim3(kBlock), 0, stream, ainv32.p, aoff.p, c_noff.p,
-                           c_n.p, rin, zout, 3 * lev[cl].nn, lev[cl].csub.p, scp);
+                           c_n.p, c_ld.p, rin, zout, 3 * lev[cl].nn, lev[cl].csub.p, scp);
         else hipLaunchKernelGGL(k_coarse<double>, dim3(ceil_div(3 * lev[cl].nn, 4)), dim3(kBlock), 0, stream, ainv.p, aoff.p, c_noff.p,
-                           c_n.p, rin, zout, 3 * lev[cl].nn, lev[cl].csub.p, scp);
+                           c_n.p, c_ld.p, rin, zout, 3 * lev[cl].nn, lev[cl].csub.p, scp);
         if (dot)
             hipLaunchKernelGGL(k_dot, dim3(ceil_div(lev[cl].nn, kBlock)), dim3(kBlock), 0, stream, rin, zout, partial.p,
                                lev[cl].nn, lev[cl].csub.p, scp);
@@ -2308,9 +2337,9 @@ void MgpisDevice::vcycle(const double* rin, double* zout, bool dot, bool first_d
         }
     }
     if (ainv32.p) hipLaunchKernelGGL(k_coarse<float>, dim3(ceil_div(3 * lev[cl].nn, 4)), dim3(kBlock), 0, stream, ainv32.p, aoff.p, c_noff.p,
-                           c_n.p, lev[cl].b.p, cur[cl], 3 * lev[cl].nn, lev[cl].csub.p, scp);
+                           c_n.p, c_ld.p, lev[cl].b.p, cur[cl], 3 * lev[cl].nn, lev[cl].csub.p, scp);
         else hipLaunchKernelGGL(k_coarse<double>, dim3(ceil_div(3 * lev[cl].nn, 4)), dim3(kBlock), 0, stream, ainv.p, aoff.p, c_noff.p,
-                       c_n.p, lev[cl].b.p, cur[cl], 3 * lev[cl].nn, lev[cl].csub.p, scp);
+                       c_n.p, c_ld.p, lev[cl].b.p, cur[cl], 3 * lev[cl].nn, lev[cl].csub.p, scp);
     // ---- ascend
     for (int l = cl + 1; l <= Lf; ++l) {
         const LevelDev& F = lev[l];

@@ -152,6 +152,7 @@ public:
     DevBuf<int64_t> aoff;      // per subdomain offset into ainv
     DevBuf<int64_t> c_noff;    // per subdomain first node of level 0
     DevBuf<int64_t> c_n;       // per subdomain coarse dofs (3 nloc_0)
+    DevBuf<int64_t> c_ld;      // per subdomain row stride of its inverse (c_n padded to 4)
     // device node numbering: fine_perm[s][i] = device position (inside member s's segment of
     // the fine level) of the member's node i in the reference (level-ordered) numbering
     std::vector<std::vector<int32_t>> fine_perm;
