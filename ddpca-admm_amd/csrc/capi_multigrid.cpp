@@ -6,8 +6,10 @@
 // (position numbering, condensed CSR), and ddpca_problem_set_subdomain_multigrid hands them to the
 // operator-level problem builder exactly as the reference binding does with the reference's own
 // MULTIGRID (oracle/ref_bind.hpp from_reference).
+#include <algorithm>
 #include <cstring>
 #include <memory>
+#include <set>
 #include <string>
 
 #include "../../include/ddpca_amd.h"
@@ -26,6 +28,7 @@ struct ddpca_multigrid {
     std::vector<double> f64;
     Csr csr;
     std::vector<int64_t> shape;
+    std::vector<int64_t> next_split;   // the children spliFlag selected in the last refine
 };
 
 namespace {
@@ -148,6 +151,81 @@ int ddpca_multigrid_set(ddpca_multigrid_t h, const char* what, int64_t n, const 
         } else {
             throw ApiError(DDPCA_EINVAL, "unknown input " + w);
         }
+    });
+}
+
+int ddpca_multigrid_refine(ddpca_multigrid_t h, int64_t n, const int64_t* elem, const int64_t* patt, int64_t nplan,
+                           const int64_t* plan_ptr, const int64_t* plan_node, const double* plan_xyz, int64_t nflag,
+                           const int64_t* flag_elem, const int64_t* flag_child) {
+    return guarded([&] {
+        ddpca_multigrid& M = open(h, false);
+        MULTIGRID& g = M.g;
+        if (n < 0 || (n > 0 && (!elem || !patt)) || nplan < 0 || (nplan > 0 && (!plan_ptr || !plan_node || !plan_xyz)) ||
+            nflag < 0 || (nflag > 0 && (!flag_elem || !flag_child)))
+            throw ApiError(DDPCA_EINVAL, "null argument");
+        const int64_t ne = (int64_t)g.elemVect.size();
+        std::set<int64_t> split;
+        for (int64_t k = 0; k < n; ++k) {
+            if (elem[k] < 0 || elem[k] >= ne || !g.elemVect[elem[k]].leaf()) throw ApiError(DDPCA_EINVAL, "refine: not a leaf element");
+            if (patt[k] < 0 || patt[k] > 6) throw ApiError(DDPCA_EINVAL, "refine: pattern must be 0..6");
+            g.elemVect[elem[k]].refiPatt = (int)patt[k];
+            split.insert(elem[k]);
+        }
+        std::map<std::vector<int64_t>, std::array<double, 3>> plan;
+        if (nplan > 0 && plan_ptr[0] != 0) throw ApiError(DDPCA_EINVAL, "plan_ptr[0] must be 0");
+        for (int64_t q = 0; q < nplan; ++q) {
+            std::vector<int64_t> key(plan_node + plan_ptr[q], plan_node + plan_ptr[q + 1]);
+            if (key.size() < 2) throw ApiError(DDPCA_EINVAL, "refine: planSurf key of fewer than 2 nodes");
+            std::sort(key.begin(), key.end());
+            plan.emplace(key, std::array<double, 3>{plan_xyz[3 * q], plan_xyz[3 * q + 1], plan_xyz[3 * q + 2]});
+        }
+        std::map<int64_t, std::set<int>> flag;
+        for (int64_t k = 0; k < nflag; ++k) flag[flag_elem[k]].insert((int)flag_child[k]);
+        try {
+            g.REFINE(split, flag, plan);
+        } catch (const std::invalid_argument& e) {
+            throw ApiError(DDPCA_EINVAL, e.what());
+        }
+        M.next_split.assign(split.begin(), split.end());
+        M.nnode = g.numNodes();
+        g.nodeLevel.assign(M.nnode, 0);
+        g.nodeParents.assign(M.nnode, {});
+    });
+}
+
+int ddpca_multigrid_tree(ddpca_multigrid_t h, const char* what, const void** data, int64_t* count, int* dtype) {
+    return guarded([&] {
+        ddpca_multigrid& M = open(h, false);
+        const MULTIGRID& g = M.g;
+        if (!what || !data || !count || !dtype) throw ApiError(DDPCA_EINVAL, "null argument");
+        const std::string w(what);
+        M.i64.clear();
+        if (w == "nodeCoor") {
+            M.f64.resize(3 * M.nnode);
+            for (int64_t i = 0; i < M.nnode; ++i)
+                for (int a = 0; a < 3; ++a) M.f64[3 * i + a] = g.nodeCoor[i][a];
+            put(M.f64, data, count, dtype);
+            return;
+        }
+        if (w == "corner") {
+            for (const auto& e : g.elemVect) M.i64.insert(M.i64.end(), e.cornNode.begin(), e.cornNode.end());
+        } else if (w == "parent") {
+            for (const auto& e : g.elemVect) M.i64.push_back(e.parent);
+        } else if (w == "level") {
+            for (const auto& e : g.elemVect) M.i64.push_back(e.level);
+        } else if (w == "refiPatt") {
+            for (const auto& e : g.elemVect) M.i64.push_back(e.refiPatt);
+        } else if (w == "child_ptr") {
+            M.i64.push_back(0);
+            for (const auto& e : g.elemVect) M.i64.push_back(M.i64.back() + (int64_t)e.children.size());
+        } else if (w == "child") {
+            for (const auto& e : g.elemVect) M.i64.insert(M.i64.end(), e.children.begin(), e.children.end());
+        } else if (w == "nextSplit") {
+            M.i64 = M.next_split;
+        } else {
+            throw ApiError(DDPCA_EINVAL, "unknown tree quantity " + w);
+        }
+        put(M.i64, data, count, dtype);
     });
 }
 

@@ -191,6 +191,179 @@ void MULTIGRID::REFINE_ALL() {
     }
 }
 
+// ---------------------------------------------------------------------------------- local refinement
+namespace {
+
+// The 12 edges and 6 faces every element registers (PREP.h hexaLine / hexaFace; ADD_ELEMENT,
+// MULTIGRID.h:335-373)
+const int kHexLine[12][2] = {{0, 1}, {1, 2}, {2, 3}, {3, 0}, {0, 4}, {1, 5}, {2, 6}, {3, 7}, {4, 5}, {5, 6}, {6, 7}, {7, 4}};
+const int kHexFace[6][4] = {{0, 3, 2, 1}, {4, 5, 6, 7}, {0, 4, 7, 3}, {1, 2, 6, 5}, {0, 1, 5, 4}, {3, 7, 6, 2}};
+
+// Refinement patterns (PREP.h TREE_ELEM::refiPatt; MULTIGRID.h:382-478): the positions on the
+// element's 3x3x3 subdivision grid (corners at 0 / 2) of the nodes a pattern creates, in creation
+// order -- a node's parents are the corners matching it on every coordinate that is not 1 -- and
+// the children: corner grid position + (0/1 per kHexOff) x the child's extent, children in order.
+const std::vector<std::vector<std::array<int, 3>>> kPattNew = {
+    {{1, 0, 0}, {2, 1, 0}, {1, 2, 0}, {0, 1, 0}, {0, 0, 1}, {2, 0, 1}, {2, 2, 1}, {0, 2, 1}, {1, 0, 2}, {2, 1, 2},
+     {1, 2, 2}, {0, 1, 2}, {0, 1, 1}, {2, 1, 1}, {1, 0, 1}, {1, 2, 1}, {1, 1, 0}, {1, 1, 2}, {1, 1, 1}},
+    {{1, 0, 0}, {2, 1, 0}, {1, 2, 0}, {0, 1, 0}, {1, 0, 2}, {2, 1, 2}, {1, 2, 2}, {0, 1, 2}, {1, 1, 0}, {1, 1, 2}},
+    {{0, 1, 0}, {0, 2, 1}, {0, 1, 2}, {0, 0, 1}, {2, 1, 0}, {2, 2, 1}, {2, 1, 2}, {2, 0, 1}, {0, 1, 1}, {2, 1, 1}},
+    {{0, 0, 1}, {1, 0, 2}, {2, 0, 1}, {1, 0, 0}, {0, 2, 1}, {1, 2, 2}, {2, 2, 1}, {1, 2, 0}, {1, 0, 1}, {1, 2, 1}},
+    {{1, 0, 0}, {1, 2, 0}, {1, 0, 2}, {1, 2, 2}},
+    {{0, 1, 0}, {2, 1, 0}, {0, 1, 2}, {2, 1, 2}},
+    {{0, 0, 1}, {2, 0, 1}, {0, 2, 1}, {2, 2, 1}}};
+const std::vector<std::vector<std::array<int, 3>>> kPattChild = {
+    {{0, 0, 0}, {1, 0, 0}, {0, 1, 0}, {1, 1, 0}, {0, 0, 1}, {1, 0, 1}, {0, 1, 1}, {1, 1, 1}},
+    {{0, 0, 0}, {1, 0, 0}, {0, 1, 0}, {1, 1, 0}},
+    {{0, 0, 0}, {0, 1, 0}, {0, 0, 1}, {0, 1, 1}},
+    {{0, 0, 0}, {0, 0, 1}, {1, 0, 0}, {1, 0, 1}},
+    {{0, 0, 0}, {1, 0, 0}},
+    {{0, 0, 0}, {0, 1, 0}},
+    {{0, 0, 0}, {0, 0, 1}}};
+const std::array<int, 3> kPattExtent[7] = {{1, 1, 1}, {1, 1, 2}, {2, 1, 1}, {1, 2, 1}, {1, 2, 2}, {2, 1, 2}, {2, 2, 1}};
+// GRLE_CHECK (MULTIGRID.h:551-614): per parent pattern and child, the parent's edges / faces (corner
+// indices) the child lies on -- a leaf neighbour using one of them must be refined too
+const std::vector<std::vector<std::vector<std::array<int, 2>>>> kPareLine = {
+    {{{0, 1}, {0, 3}, {0, 4}}, {{1, 0}, {1, 2}, {1, 5}}, {{3, 0}, {3, 2}, {3, 7}}, {{2, 1}, {2, 3}, {2, 6}},
+     {{4, 0}, {4, 5}, {4, 7}}, {{5, 1}, {5, 4}, {5, 6}}, {{7, 3}, {7, 6}, {7, 4}}, {{6, 2}, {6, 5}, {6, 7}}},
+    {{{0, 1}, {0, 3}, {4, 5}, {4, 7}}, {{1, 0}, {1, 2}, {5, 4}, {5, 6}}, {{3, 0}, {3, 2}, {7, 4}, {7, 6}},
+     {{2, 1}, {2, 3}, {6, 5}, {6, 7}}},
+    {{{0, 3}, {0, 4}, {1, 2}, {1, 5}}, {{3, 0}, {3, 7}, {2, 1}, {2, 6}}, {{4, 0}, {4, 7}, {5, 1}, {5, 6}},
+     {{7, 3}, {7, 4}, {6, 2}, {6, 5}}},
+    {{{0, 1}, {0, 4}, {3, 2}, {3, 7}}, {{4, 0}, {4, 5}, {7, 3}, {7, 6}}, {{1, 0}, {1, 5}, {2, 3}, {2, 6}},
+     {{5, 1}, {5, 4}, {6, 2}, {6, 7}}},
+    {{{0, 1}, {4, 5}, {2, 3}, {7, 6}}, {{0, 1}, {4, 5}, {2, 3}, {7, 6}}},
+    {{{0, 3}, {1, 2}, {4, 7}, {5, 6}}, {{0, 3}, {1, 2}, {4, 7}, {5, 6}}},
+    {{{0, 4}, {1, 5}, {3, 7}, {2, 6}}, {{0, 4}, {1, 5}, {3, 7}, {2, 6}}}};
+const std::vector<std::vector<std::vector<std::array<int, 4>>>> kPareFace = {
+    {{{0, 1, 2, 3}, {0, 3, 7, 4}, {0, 4, 5, 1}}, {{1, 2, 3, 0}, {1, 2, 6, 5}, {1, 0, 4, 5}},
+     {{3, 0, 1, 2}, {3, 7, 4, 0}, {3, 7, 6, 2}}, {{2, 3, 0, 1}, {2, 6, 5, 1}, {2, 3, 7, 6}},
+     {{4, 5, 6, 7}, {4, 0, 3, 7}, {4, 5, 1, 0}}, {{5, 6, 7, 4}, {5, 1, 2, 6}, {5, 1, 0, 4}},
+     {{7, 4, 5, 6}, {7, 4, 0, 3}, {7, 6, 2, 3}}, {{6, 7, 4, 5}, {6, 5, 1, 2}, {6, 2, 3, 7}}},
+    {{{0, 1, 2, 3}, {0, 3, 7, 4}, {0, 4, 5, 1}, {4, 5, 6, 7}}, {{1, 2, 3, 0}, {1, 2, 6, 5}, {1, 0, 4, 5}, {5, 6, 7, 4}},
+     {{3, 0, 1, 2}, {3, 7, 4, 0}, {3, 7, 6, 2}, {7, 4, 5, 6}}, {{2, 3, 0, 1}, {2, 6, 5, 1}, {2, 3, 7, 6}, {6, 7, 4, 5}}},
+    {{{0, 3, 7, 4}, {1, 2, 6, 5}, {0, 4, 5, 1}, {0, 1, 2, 3}}, {{3, 7, 4, 0}, {2, 6, 5, 1}, {3, 7, 6, 2}, {3, 0, 1, 2}},
+     {{4, 0, 3, 7}, {5, 1, 2, 6}, {4, 5, 6, 7}, {4, 5, 1, 0}}, {{7, 4, 0, 3}, {6, 5, 1, 2}, {7, 6, 2, 3}, {7, 4, 5, 6}}},
+    {{{0, 4, 5, 1}, {3, 7, 6, 2}, {0, 3, 7, 4}, {0, 1, 2, 3}}, {{4, 5, 1, 0}, {7, 6, 2, 3}, {4, 5, 6, 7}, {4, 0, 3, 7}},
+     {{1, 0, 4, 5}, {2, 3, 7, 6}, {1, 2, 3, 0}, {1, 2, 6, 5}}, {{5, 1, 0, 4}, {6, 2, 3, 7}, {5, 6, 7, 4}, {5, 1, 2, 6}}},
+    {{{0, 1, 2, 3}, {0, 4, 5, 1}, {4, 5, 6, 7}, {3, 7, 6, 2}}, {{0, 1, 2, 3}, {0, 4, 5, 1}, {4, 5, 6, 7}, {3, 7, 6, 2}}},
+    {{{0, 3, 7, 4}, {4, 5, 6, 7}, {1, 2, 6, 5}, {0, 1, 2, 3}}, {{0, 3, 7, 4}, {4, 5, 6, 7}, {1, 2, 6, 5}, {0, 1, 2, 3}}},
+    {{{0, 4, 5, 1}, {3, 7, 6, 2}, {0, 3, 7, 4}, {1, 2, 6, 5}}, {{0, 4, 5, 1}, {3, 7, 6, 2}, {0, 3, 7, 4}, {1, 2, 6, 5}}}};
+
+}  // namespace
+
+int64_t MULTIGRID::TRY_ADD_COOR(const std::array<double, 3>& xyz) {
+    if (coorNode.empty())
+        for (int64_t i = 0; i < numNodes(); ++i) coorNode.emplace(nodeCoor[i], i);
+    auto it = coorNode.find(xyz);
+    if (it != coorNode.end()) return it->second;
+    const int64_t id = numNodes();
+    coorNode.emplace(xyz, id);
+    nodeCoor.push_back(xyz);
+    nodeLatt.clear();  // a general tree has no lattice
+    nodeLevel.push_back(0);
+    nodeParents.emplace_back();
+    return id;
+}
+
+void MULTIGRID::GRLE_CHECK(std::set<int64_t>& split) {
+    // lineUsed / faceUsed (ADD_ELEMENT, MULTIGRID.h:338-369): every element using an edge / face
+    std::map<std::vector<int64_t>, std::vector<int64_t>> used;
+    for (int64_t e = 0; e < (int64_t)elemVect.size(); ++e) {
+        const auto& c = elemVect[e].cornNode;
+        for (const auto& ln : kHexLine) {
+            std::vector<int64_t> k{c[ln[0]], c[ln[1]]};
+            std::sort(k.begin(), k.end());
+            used[k].push_back(e);
+        }
+        for (const auto& f : kHexFace) {
+            std::vector<int64_t> k{c[f[0]], c[f[1]], c[f[2]], c[f[3]]};
+            std::sort(k.begin(), k.end());
+            used[k].push_back(e);
+        }
+    }
+    std::set<int64_t> front = split;
+    for (;;) {
+        std::set<int64_t> added;
+        auto visit = [&](std::vector<int64_t> key) {
+            std::sort(key.begin(), key.end());
+            const auto it = used.find(key);
+            if (it == used.end()) return;
+            for (int64_t n : it->second)
+                if (elemVect[n].leaf() && !split.count(n)) {
+                    added.insert(n);
+                    elemVect[n].refiPatt = 0;
+                }
+        };
+        for (int64_t e : front) {
+            const TreeElem& t = elemVect[e];
+            if (t.parent < 0) continue;
+            const TreeElem& P = elemVect[t.parent];
+            const int p = P.refiPatt;
+            const auto pos = std::find(P.children.begin(), P.children.end(), e);
+            if (p < 0 || p > 6 || pos == P.children.end()) throw std::invalid_argument("GRLE_CHECK: child not in its parent");
+            const size_t isub = (size_t)(pos - P.children.begin());
+            if (isub >= kPareLine[p].size()) throw std::invalid_argument("GRLE_CHECK: child index beyond the pattern");
+            for (const auto& ln : kPareLine[p][isub]) visit({P.cornNode[ln[0]], P.cornNode[ln[1]]});
+            for (const auto& f : kPareFace[p][isub]) visit({P.cornNode[f[0]], P.cornNode[f[1]], P.cornNode[f[2]], P.cornNode[f[3]]});
+        }
+        if (added.empty()) break;
+        front = added;
+        split.insert(added.begin(), added.end());
+    }
+}
+
+void MULTIGRID::REFINE(std::set<int64_t>& split, const std::map<int64_t, std::set<int>>& spliFlag,
+                       const std::map<std::vector<int64_t>, std::array<double, 3>>& planSurf) {
+    for (int64_t e : split)
+        if (e < 0 || e >= (int64_t)elemVect.size() || !elemVect[e].leaf()) throw std::invalid_argument("REFINE: not a leaf element");
+    GRLE_CHECK(split);
+    std::set<int64_t> next;
+    for (int64_t e : split) {
+        const std::array<int64_t, 8> corn = elemVect[e].cornNode;
+        const int s = elemVect[e].refiPatt;
+        if (s < 0 || s > 6) throw std::invalid_argument("REFINE: element without a refinement pattern 0..6");
+        int64_t grid[3][3][3];
+        for (int k = 0; k < 8; ++k) grid[kCornerPos[k][0]][kCornerPos[k][1]][kCornerPos[k][2]] = corn[k];
+        for (const auto& q : kPattNew[s]) {
+            std::vector<int64_t> par;
+            for (int k = 0; k < 8; ++k) {
+                bool on = true;
+                for (int a = 0; a < 3; ++a) on &= (q[a] == 1 || q[a] == kCornerPos[k][a]);
+                if (on) par.push_back(corn[k]);
+            }
+            std::sort(par.begin(), par.end());
+            const auto ps = planSurf.find(par);
+            std::array<double, 3> xyz{0.0, 0.0, 0.0};
+            if (ps != planSurf.end()) {
+                xyz = ps->second;
+            } else {
+                for (int64_t p : par)
+                    for (int a = 0; a < 3; ++a) xyz[a] = xyz[a] + nodeCoor[p][a];
+                for (int a = 0; a < 3; ++a) xyz[a] = xyz[a] / (double)par.size();
+            }
+            grid[q[0]][q[1]][q[2]] = TRY_ADD_COOR(xyz);
+        }
+        const auto& ext = kPattExtent[s];
+        for (const auto& b : kPattChild[s]) {
+            TreeElem ch;
+            ch.parent = e;
+            ch.level = elemVect[e].level + 1;
+            for (int m = 0; m < 8; ++m)
+                ch.cornNode[m] = grid[b[0] + kHexOff[m][0] * ext[0]][b[1] + kHexOff[m][1] * ext[1]][b[2] + kHexOff[m][2] * ext[2]];
+            const int64_t id = ADD_ELEMENT(ch);  // may reallocate elemVect
+            elemVect[e].children.push_back(id);
+        }
+        const auto fl = spliFlag.find(e);
+        if (fl != spliFlag.end())
+            for (int c : fl->second) {
+                if (c < 0 || c >= (int)elemVect[e].children.size()) throw std::invalid_argument("REFINE: spliFlag child out of range");
+                next.insert(elemVect[e].children[c]);
+            }
+    }
+    split.swap(next);
+}
+
 // ---------------------------------------------------------------------------------- transfer
 void MULTIGRID::TRANSFER() {
     const int64_t N = numNodes();
@@ -232,12 +405,9 @@ void MULTIGRID::TRANSFER() {
 
 namespace {
 
-// The 12 edges and 6 faces every element registers (PREP.h hexaLine / hexaFace; ADD_ELEMENT,
-// MULTIGRID.h:335-373) and, per refinement pattern, the edges / faces of a refined element whose
+// Per refinement pattern, the edges / faces of a refined element whose
 // midpoint / centre node the refinement created: {corner a, corner b, child, child corner} and
 // {4 corners, child, child corner} (TRANSFER's elemLine / elemFace, MULTIGRID.h:759-792).
-const int kHexLine[12][2] = {{0, 1}, {1, 2}, {2, 3}, {3, 0}, {0, 4}, {1, 5}, {2, 6}, {3, 7}, {4, 5}, {5, 6}, {6, 7}, {7, 4}};
-const int kHexFace[6][4] = {{0, 3, 2, 1}, {4, 5, 6, 7}, {0, 4, 7, 3}, {1, 2, 6, 5}, {0, 1, 5, 4}, {3, 7, 6, 2}};
 struct LineNew { int a, b, child, corner; };
 struct FaceNew { int c[4], child, corner; };
 const std::vector<std::vector<LineNew>> kPattLine = {

@@ -1,7 +1,11 @@
 // MULTIGRID: host restatement of the reference's operator-producing subset (MULTIGRID.h:10-95):
-//   REFINE (pattern 0)   MULTIGRID.h:375-545   uniform refinement of the generators; node
-//                                              creation order reproduced exactly, so the
-//                                              level-ordered numbering equals the reference's
+//   REFINE_ALL           MULTIGRID.h:375-545   pattern 0 on every leaf (the generators' uniform
+//                                              rounds, lattice-keyed nodes); node creation order
+//                                              reproduced exactly, so the level-ordered numbering
+//                                              equals the reference's
+//   REFINE + GRLE_CHECK  MULTIGRID.h:375-678   local refinement of any leaf set with patterns 0-6,
+//                                              level balancing, planSurf (curved faces), spliFlag;
+//                                              coordinate-keyed nodes (TRY_ADD_NODE(COOR))
 //   TRANSFER             MULTIGRID.h:756-948   level sets + scalar prolongation stencils; on any
 //                                              octree (every refinement pattern, locally refined
 //                                              meshes): the hanging level past maxiLeve, coupled
@@ -15,9 +19,10 @@
 //   ADDITIONAL_FORCE     MULTIGRID.h:1257-1261
 //   OUTP_SUB1            MULTIGRID.h:1263-1281
 // A general tree comes in through the C ABI (ddpca_multigrid_*, capi_multigrid.cpp) with the
-// element tree the caller's REFINE produced; TRANSFER then renumbers the nodes to the reference's
-// positions (posiNode keeps the original ids: earlTran).  Out of scope here:
-// the refinement edit itself on curved surfaces (CURVEDS), stress recovery, text output.
+// element tree the caller built or refined (ddpca_multigrid_refine); TRANSFER then renumbers the
+// nodes to the reference's positions (posiNode keeps the original ids: earlTran).  Out of scope
+// here: the curved-surface projection itself (CURVEDS: the caller supplies its
+// planSurf), stress recovery, text output.
 #pragma once
 #include <array>
 #include <cstdint>
@@ -50,11 +55,32 @@ public:
     std::vector<std::vector<int64_t>> nodeParents;  // parents of a refined node (sorted ids)
     std::vector<TreeElem> elemVect;
     std::unordered_map<uint64_t, int64_t> lattNode;  // lattice key -> node (TRY_ADD_NODE lookup)
+    // coordinate -> node (the reference's coorNode, COOR's 1e-10 lexicographic order), general trees
+    struct CoorLess {
+        bool operator()(const std::array<double, 3>& a, const std::array<double, 3>& b) const {
+            for (int i = 0; i < 3; ++i) {
+                if (a[i] < b[i] - 1.0e-10) return true;
+                if (a[i] > b[i] + 1.0e-10) return false;
+            }
+            return false;
+        }
+    };
+    std::map<std::array<double, 3>, int64_t, CoorLess> coorNode;
     int64_t maxiLeve = -1;
     int64_t TRY_ADD_NODE(const std::array<int64_t, 3>& latt, const std::array<double, 3>& xyz);
     int64_t ADD_ELEMENT(const TreeElem& e);
     // One uniform refinement round: MULTIGRID::REFINE with refiPatt = 0 on every leaf element.
     void REFINE_ALL();
+    // MULTIGRID::REFINE (MULTIGRID.h:375-545) on a general tree: GRLE_CHECK's level balancing
+    // (547-678: the leaf neighbours across the refined elements' parent edges / faces join with
+    // pattern 0), then every element of `split` (each with its refiPatt set) is cut with its
+    // pattern; a new node sits at planSurf's position for its corner set (a curved surface) or at
+    // the corners' average, nodes deduplicated by coordinates as TRY_ADD_NODE does (1e-10).
+    // `split` returns the children spliFlag selects (element -> child indices) for the next round.
+    void REFINE(std::set<int64_t>& split, const std::map<int64_t, std::set<int>>& spliFlag,
+                const std::map<std::vector<int64_t>, std::array<double, 3>>& planSurf);
+    void GRLE_CHECK(std::set<int64_t>& split);
+    int64_t TRY_ADD_COOR(const std::array<double, 3>& xyz);  // coordinate-keyed TRY_ADD_NODE
     int64_t numNodes() const { return (int64_t)nodeCoor.size(); }
 
     // ---------------------------------------------------------------- transfer

@@ -310,6 +310,21 @@ int ddpca_multigrid_create(int64_t nnode, const double* coords, int64_t nelem, c
                            const int64_t* parent, const int64_t* level, const int64_t* refiPatt,
                            const int64_t* child_ptr, const int64_t* child, ddpca_multigrid_t* out);
 int ddpca_multigrid_set(ddpca_multigrid_t g, const char* what, int64_t n, const int64_t* idx, const double* val);
+/* refine (before build): MULTIGRID::REFINE (MULTIGRID.h:375-545) -- GRLE_CHECK's level balancing
+ * (the leaf neighbours across the refined elements' parent edges / faces join with pattern 0),
+ * then the n leaf elements elem[] are cut with patterns patt[] (0 xi-eta-zeta 8-way, 1 xi-eta,
+ * 2 eta-zeta, 3 zeta-xi 4-way, 4 xi, 5 eta, 6 zeta 2-way).  A new node takes planSurf's position
+ * when its corner set is a key there (nplan keys: plan_node[plan_ptr[q] .. plan_ptr[q+1]), position
+ * plan_xyz[3q..3q+2]: the caller's curved surface, CURVEDS::REFINE's output), else the corners'
+ * average; nodes are deduplicated by coordinates as TRY_ADD_NODE does (1e-10).  spliFlag (nflag
+ * pairs: element, child index) selects children for the next round: ddpca_multigrid_tree
+ * "nextSplit". */
+int ddpca_multigrid_refine(ddpca_multigrid_t g, int64_t n, const int64_t* elem, const int64_t* patt, int64_t nplan,
+                           const int64_t* plan_ptr, const int64_t* plan_node, const double* plan_xyz, int64_t nflag,
+                           const int64_t* flag_elem, const int64_t* flag_child);
+/* The tree before build (int64 unless noted): "nodeCoor" (f64, 3 per node), "corner" (8 per element),
+ * "parent", "level", "refiPatt", "child_ptr" (elements + 1), "child", "nextSplit". */
+int ddpca_multigrid_tree(ddpca_multigrid_t g, const char* what, const void** data, int64_t* count, int* dtype);
 int ddpca_multigrid_build(ddpca_multigrid_t g, const ddpca_csr_t* extra);
 int ddpca_multigrid_view(ddpca_multigrid_t g, const char* what, int64_t level, const void** data, int64_t* count,
                          int* dtype);

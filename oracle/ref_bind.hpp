@@ -149,7 +149,7 @@ inline SpMat problem_csr(ddpca_problem_t p, const std::string& base, int64_t ind
 // pipeline (ddpca_multigrid_*), built with `extra` added to origStif (node ids; ESTABLISH adds the
 // contact interfaces' systMass there, MCONTACT.h:816-822).  REFINE sizes children to 8 and fills
 // the pattern's 8 / 4 / 2 (MULTIGRID.h:515-533): only those go over.
-inline ddpca_multigrid_t tree_build(const MULTIGRID& g, const SpMat* extra = nullptr) {
+inline ddpca_multigrid_t tree_create(const MULTIGRID& g) {
     const int64_t nn = (int64_t)g.nodeCoor.size(), ne = (int64_t)g.elemVect.size();
     std::vector<double> xyz(3 * nn);
     for (const auto& nc : g.nodeCoor)
@@ -168,6 +168,11 @@ inline ddpca_multigrid_t tree_build(const MULTIGRID& g, const SpMat* extra = nul
     ddpca_multigrid_t h = nullptr;
     check(ddpca_multigrid_create(nn, xyz.data(), ne, corner.data(), parent.data(), level.data(), patt.data(), cptr.data(),
                                  child.data(), &h));
+    return h;
+}
+
+// the MULTIGRID's constraints, loads, rotations, coupled nodes and material onto an unbuilt handle, then build
+inline void tree_inputs(ddpca_multigrid_t h, const MULTIGRID& g, const SpMat* extra = nullptr) {
     std::vector<int64_t> idx;
     std::vector<double> val;
     auto put = [&](const char* what) {
@@ -199,6 +204,11 @@ inline ddpca_multigrid_t tree_build(const MULTIGRID& g, const SpMat* extra = nul
     } else {
         check(ddpca_multigrid_build(h, nullptr));
     }
+}
+
+inline ddpca_multigrid_t tree_build(const MULTIGRID& g, const SpMat* extra = nullptr) {
+    ddpca_multigrid_t h = tree_create(g);
+    tree_inputs(h, g, extra);
     return h;
 }
 

@@ -1,10 +1,11 @@
-# Round 3, call c: the GPU tests touched this round -- LAGRANGE (BiCGSTAB relres / breakdown per
-# Newton step, diag-only handles), the CYLINDER known answer on the library's own operator
-# pipeline, the headline coarse-correction Kx switch -- then the whole GPU suite
+# Round 3, call c: the groups-1 line after the k_coarse change, then the whole GPU suite (which
+# holds the tests touched this round: LAGRANGE relres / breakdown per Newton step and diag-only
+# handles, CYLINDER on the library's own operator pipeline and on two ranks of one process, the
+# headline coarse-correction Kx switch)
 set -eo pipefail
 OUT=gpurun_out/r03c
 mkdir -p $OUT
 export TMPDIR=/tmp
-timeout -k 10 900 python -u -m pytest tests/test_lagrange_gpu.py tests/test_mcontact_gpu.py::test_cylinder_known_answer tests/test_mcontact_gpu.py::test_cylinder_two_ranks_in_one_process "tests/test_headline_gpu.py::test_coarse_correction_kx_from_recursive_residual" -v -s --timeout 600 --timeout-method thread > $OUT/gputest_touched.log 2>&1
-timeout -k 10 1000 python -u -m pytest tests -m gpu -v --timeout 600 --timeout-method thread > $OUT/gputest.log 2>&1
+timeout -k 10 200 python3 -u bench.py --groups 1 --no-cpu-baseline > $OUT/bench_g1.json 2> $OUT/bench_g1.err
+timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 600 --timeout-method thread > $OUT/gputest.log 2>&1
 echo done > $OUT/DONE

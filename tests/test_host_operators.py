@@ -151,3 +151,49 @@ def test_general_tree_pipeline_matches_reference(tmp_path, args):
         assert lines[-1]["hanging_nodes"] > 0
     if "rot" in args:
         assert all(sub["rotated"] > 0 for sub in lines[:-1])
+
+
+@pytest.mark.parametrize("rounds", [4])
+def test_local_refinement_matches_reference(tmp_path, rounds):
+    """MULTIGRID::REFINE (MULTIGRID.h:375-545) through ddpca_multigrid_refine against the
+    reference's REFINE on the same box, round by round (oracle/ref_multigrid.cpp "refine"): every
+    pattern 0-6 mixed in one round, spliFlag chains (the children a round selects are refined in the
+    next), GRLE_CHECK's level balancing (MULTIGRID.h:547-678), planSurf moving the new nodes of a
+    curved face (CURVEDS::REFINE's role).  Node ids and coordinates must be bitwise equal, every
+    element's corners, parent, level, pattern and children identical, the next split set equal."""
+    exe = Path(__file__).resolve().parents[1] / "oracle" / "_ref" / "ref_multigrid"
+    if not exe.exists():
+        pytest.skip("oracle/_ref/ref_multigrid is built where the reference is (oracle/Makefile)")
+    out = subprocess.run([str(exe), "refine", str(rounds)], capture_output=True, text=True, timeout=600, cwd=tmp_path)
+    lines = [json.loads(l) for l in out.stdout.splitlines() if l.startswith("{")]
+    assert out.returncode == 0 and lines and lines[-1]["ok"], (out.stdout[-3000:], out.stderr[-2000:])
+    rr = [l for l in lines if "round" in l]
+    assert len(rr) == rounds and all(r["nodes_equal"] and r["elements_equal"] and r["next_split_equal"] for r in rr), rr
+    assert any(r["planSurf"] > 0 for r in rr) and rr[-1]["new_elements"] > 0
+
+
+@pytest.mark.parametrize("args", [("1", "1", "2"), ("0", "1", "3", "rot")], ids=["cylinder-schedule", "rotated"])
+def test_refined_tree_pipeline_matches_reference(tmp_path, args):
+    """CYLINDER_1's refinement schedule (MESH, CYLINDER_1.h:346-443: globInho rounds of pattern 1,
+    globHomo of pattern 0, locaLeve local rounds of pattern 0 along a band of the curved face) run
+    through ddpca_multigrid_refine, then the operator pipeline built on the library's own refined
+    tree against the reference's REFINE + TRANSFER + STIF_MATR + CONSTRAINT(1): trees identical each
+    round, then positions, levels, PATCHed coordinates, consFlag and dispForc identical, realProl and
+    the hanging rows exact, consStif 1e-13.  consForc (1e-12) is compared whenever the reference's
+    own dispForc is intact: its MULTIGRID.h:1204 shrinks the vector onto a block of itself (an
+    Eigen aliasing resize that reads the freed buffer) when consDofv holds more dofs than the fine
+    level's constrained rows, so on such inputs its consForc is not defined (reported -1)."""
+    exe = Path(__file__).resolve().parents[1] / "oracle" / "_ref" / "ref_multigrid"
+    if not exe.exists():
+        pytest.skip("oracle/_ref/ref_multigrid is built where the reference is (oracle/Makefile)")
+    out = subprocess.run([str(exe), "refine_pipeline", *args], capture_output=True, text=True, timeout=600, cwd=tmp_path)
+    lines = [json.loads(l) for l in out.stdout.splitlines() if l.startswith("{")]
+    assert out.returncode == 0 and lines and lines[-1]["ok"], (out.stdout[-3000:], out.stderr[-2000:])
+    assert all(l["nodes_equal"] and l["elements_equal"] for l in lines if "round" in l)
+    sub = [l for l in lines if "subdomain" in l][0]
+    assert sub["positions_equal"] and sub["levels_equal"] and sub["consFlag_equal"] and sub["dispForc_equal"], sub
+    assert sub["coords"] == 0.0 and sub["realProl"] == 0.0 and sub["hang"] == 0.0 and sub["K_rel"] <= 1e-13, sub
+    assert sub["consForc_rel"] <= 1e-12 and (sub["consForc_rel"] >= 0 or not sub["reference_dispForc_intact"]), sub
+    assert sub["hanging"] > 0 and lines[-1]["hanging_nodes"] > 0
+    if "rot" in args:
+        assert sub["rotated"] > 0
