@@ -55,7 +55,8 @@ def parse():
                     help="contact faces integrated over 2^k x 2^k polygons (k = 2: M3's 0.8 ip per DOF with --ip-glued 1)")
     ap.add_argument("--ip-glued", type=int, default=W["ip_glued"], help="the same for the glued faces")
     # defaults: the fastest configuration of the round-1 sweep (profiles/r01_sweep.txt)
-    ap.add_argument("--smoother", type=int, default=H["smoother"], help="0 point Jacobi, 1 block Jacobi, 2 Chebyshev")
+    ap.add_argument("--smoother", type=int, default=H["smoother"], help="0 point Jacobi, 1 block Jacobi, 2 Chebyshev, "
+                    "3 multicolour block Gauss-Seidel on the fine level (block Jacobi below, --nu sweeps)")
     ap.add_argument("--nu", type=int, default=H["nu"])
     ap.add_argument("--omega-scale", type=float, default=-H["omega"],
                     help="Jacobi damping = scale / lambda_max(M^-1 K) per level (profiles/r01_sweep_omega.txt)")
@@ -197,7 +198,8 @@ def main():
                 "integration_points": nip,
                 "ip_per_dof": nip / total_dofs,
                 "mg_levels": a.gl + 1,
-                "smoother": {0: "jacobi", 1: "block-jacobi", 2: "chebyshev"}[a.smoother] + f"({a.nu})",
+                "smoother": {0: "jacobi", 1: "block-jacobi", 2: "chebyshev"}[a.smoother] + f"({a.nu})" if a.smoother != 3
+                else f"fine: multicolour block Gauss-Seidel (1 forward, 1 backward); below: block-jacobi({a.nu})",
                 "pcg_x0": "previous solution" if a.warm_start else "zero",
                 "vcycle_operator_storage": {0: "fp64", 1: "fp32", 2: "fp32, fine level block-exponent fp16"}[a.precond_fp32],
                 "operator_rows": "deduplicated table" if a.table_mode else "streamed",

@@ -1174,7 +1174,9 @@ void build(ddpca_mcontact& H, Problem& P) {
         for (size_t i = 0; i < H.subs.size(); ++i) {
             auto& S = H.subs[i];
             S.dof0 = H.mg->fine_dof_offset((int)i);
-            H.maxit.push_back(H.mg->nfree[i]);
+            // DDPCA_PCG_MAXIT (diagnostics only): cap the body solves below the reference's maxit = rows
+            static const int64_t cap = std::getenv("DDPCA_PCG_MAXIT") ? std::atoll(std::getenv("DDPCA_PCG_MAXIT")) : 0;
+            H.maxit.push_back(cap > 0 ? std::min<int64_t>(cap, H.mg->nfree[i]) : H.mg->nfree[i]);
             const MULTIGRID& g = mc.multGrid[S.tv];
             for (int64_t d = 0; d < 3 * S.nn; ++d)
                 if (g.consFlag[d]) cf[H.mg->fine_dof((int)i, d)] = g.consForc[g.freeIndex[d]];

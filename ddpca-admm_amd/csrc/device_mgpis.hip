@@ -440,6 +440,78 @@ __global__ __launch_bounds__(kBlock) void k_sell_split(SellArgs a) {
     }
 }
 
+// Multicolour block Gauss-Seidel on the fine level (GsFine): one wavefront per colour chunk,
+// lane = one row of that colour.  PH 0: forward sweep from zero over the L part, x_i = M_i (b_i -
+// L_i x); PH 1: the residual after the forward sweep, r_i = -U_i x (every chunk, one launch);
+// PH 2: backward sweep, x_i = M_i (b_i - L_i x - U_i x), DOT: partial = b . x_new per chunk.
+// In place: rows of one colour are never each other's neighbours.
+struct GsArgs {
+    const int32_t* list;  // chunk ids of this launch (nullptr: chunks 0 .. n-1)
+    int64_t n;
+    const int32_t* rowidx;
+    const int32_t* csub;
+    const int32_t* nsl;
+    const int32_t* nsu;
+    const int64_t* offl;
+    const int64_t* offu;
+    const int32_t* col;
+    const int16_t* col16;
+    const void* val;
+    const void* minv;
+    double* x;
+    const double* b;
+    double* r;
+    const PcgScal* sc;
+    double* partial;
+};
+
+template <int PH, bool DOT, typename T, typename CT, int V = 1>
+__global__ __launch_bounds__(kBlock) void k_gs(GsArgs a) {
+    const int lane = threadIdx.x & 63;
+    const int64_t li = (int64_t)blockIdx.x * (kBlock / kWave) + (threadIdx.x >> 6);
+    if (li >= a.n) return;
+    const int64_t c = a.list ? (int64_t)a.list[li] : li;
+    const int sub = a.csub[c];
+    if (stopped(a.sc, sub)) return;
+    const int32_t rr = a.rowidx[c * kChunk + lane];
+    const bool real = rr >= 0;
+    const int64_t row = real ? rr : ~rr;  // pad lanes gather at a real row with zero blocks
+    constexpr int64_t SV = slot_vals<T>() * kChunk;
+    const T* val = static_cast<const T*>(a.val);
+    const CT* colp;
+    if constexpr (sizeof(CT) == 2) colp = a.col16;
+    else colp = a.col;
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+    if (PH != 1) {
+        const int64_t o = a.offl[c];
+        sell_rows<V, T, CT>(colp + o * kChunk + lane, val + o * SV + lane, a.x, a.nsl[c], row, s0, s1, s2);
+    }
+    if (PH != 0) {
+        const int64_t o = a.offu[c];
+        sell_rows<V, T, CT>(colp + o * kChunk + lane, val + o * SV + lane, a.x, a.nsu[c], row, s0, s1, s2);
+    }
+    const int64_t o = 3 * row;
+    double dotv = 0.0;
+    if (PH == 1) {
+        if (real) {
+            a.r[o] = -s0;
+            a.r[o + 1] = -s1;
+            a.r[o + 2] = -s2;
+        }
+    } else {
+        const double b0 = a.b[o], b1 = a.b[o + 1], b2 = a.b[o + 2];
+        double m0, m1, m2;
+        apply_m<true>(static_cast<const SmoothInv<T>*>(a.minv), row, b0 - s0, b1 - s1, b2 - s2, m0, m1, m2);
+        if (real) {
+            a.x[o] = m0;
+            a.x[o + 1] = m1;
+            a.x[o + 2] = m2;
+            if (DOT) dotv = b0 * m0 + b1 * m1 + b2 * m2;
+        }
+    }
+    if (DOT) chunk_partial(dotv, a.partial, c);
+}
+
 // Workgroup b is dispatched to XCD b % 8: the logical block that makes XCD x own the x-th
 // contiguous run of the grid (runs of q+1 blocks for the first r XCDs, q for the rest; G = 8q + r)
 __device__ __forceinline__ int64_t xcd_slab_block() {
@@ -1416,6 +1488,154 @@ bool lattice_transfer(LevelDev& L, const LevelDev& C, const std::vector<int32_t>
     L.rstr.upload(rstr);
     return true;
 }
+
+// The fine level's colour structure (GsFine) from its host SELL arrays (col: batch device
+// columns, val: masked fp64 blocks val[(q * 9 + ij) * 64 + lane]); vt: the V-cycle copy's type.
+void build_gs(GsFine& G, const LevelDev& L, int nsub, const std::vector<int64_t>& off, const std::vector<int32_t>& col,
+              const std::vector<double>& val, int vt) {
+    // greedy colouring in device order, per member
+    std::vector<int8_t> colour(L.nn, -1);
+    std::vector<int> ncol_sub(nsub, 0);
+    int too_many = 0;
+#pragma omp parallel for schedule(dynamic, 1) reduction(max : too_many)
+    for (int s = 0; s < nsub; ++s) {
+        for (int64_t g = L.noff[s]; g < L.noff[s] + L.nloc[s]; ++g) {
+            const int64_t c = g / kChunk, lane = g % kChunk;
+            uint64_t used = 0;
+            for (int64_t q = off[c]; q < off[c + 1]; ++q) {
+                const int64_t j = col[q * kChunk + lane];
+                if (j != g && colour[j] >= 0) used |= 1ull << colour[j];
+            }
+            if (used == ~0ull) {
+                too_many = 1;
+                break;
+            }
+            const int k = __builtin_ctzll(~used);
+            colour[g] = (int8_t)k;
+            ncol_sub[s] = std::max(ncol_sub[s], k + 1);
+        }
+    }
+    if (too_many) throw ApiError(DDPCA_EINVAL, "multicolour smoother: a node graph needing more than 64 colours");
+    const int K = *std::max_element(ncol_sub.begin(), ncol_sub.end());
+    // colour chunks, member-major and colour-minor
+    std::vector<std::vector<int64_t>> rows((size_t)nsub * K);
+    for (int s = 0; s < nsub; ++s)
+        for (int64_t g = L.noff[s]; g < L.noff[s] + L.nloc[s]; ++g) rows[(size_t)s * K + colour[g]].push_back(g);
+    std::vector<int32_t> rowidx, csub, nsl, nsu;
+    std::vector<int64_t> offl, offu, cb(nsub + 1, 0);
+    std::vector<std::vector<int32_t>> bycol(K);
+    std::vector<int64_t> base;  // first row of each chunk in its (s, k) list
+    std::vector<size_t> lists;
+    G.nnzb_sub.assign(nsub, 0);
+    G.slots_sub.assign(nsub, 0);
+    int64_t nslot = 0;
+    for (int s = 0; s < nsub; ++s) {
+        cb[s] = (int64_t)csub.size();
+        for (int k = 0; k < K; ++k) {
+            const auto& R = rows[(size_t)s * K + k];
+            for (size_t r0 = 0; r0 < R.size(); r0 += kChunk) {
+                const int64_t c = (int64_t)csub.size();
+                bycol[k].push_back((int32_t)c);
+                csub.push_back(s);
+                base.push_back((int64_t)r0);
+                lists.push_back((size_t)s * K + k);
+                int32_t ml = 0, mu = 0;
+                for (size_t i = r0; i < std::min(R.size(), r0 + kChunk); ++i) {
+                    const int64_t g = R[i], nc = g / kChunk, lane = g % kChunk;
+                    int32_t nl = 0, nu = 0;
+                    for (int64_t q = off[nc]; q < off[nc + 1]; ++q) {
+                        const int64_t j = col[q * kChunk + lane];
+                        if (j == g) continue;
+                        if (colour[j] < k) ++nl;
+                        else ++nu;
+                    }
+                    ml = std::max(ml, nl);
+                    mu = std::max(mu, nu);
+                    G.nnzb_sub[s] += nl + nu;
+                }
+                nsl.push_back(ml);
+                nsu.push_back(mu);
+                offl.push_back(nslot);
+                offu.push_back(nslot + ml);
+                nslot += ml + mu;
+                G.slots_sub[s] += ml + mu;
+            }
+        }
+    }
+    const int64_t nch = (int64_t)csub.size();
+    cb[nsub] = nch;
+    rowidx.assign(nch * kChunk, 0);
+    const bool c16 = L.col16.p != nullptr;
+    std::vector<int32_t> gcol(c16 ? 0 : std::max<int64_t>(nslot * kChunk, 1), 0);
+    std::vector<int16_t> gcol16(c16 ? std::max<int64_t>(nslot * kChunk, 1) : 0, 0);
+    const int nv = vt == kValH16 ? 10 : 9;
+    std::vector<uint16_t> v16(vt == kValH16 ? std::max<int64_t>(nslot * nv * kChunk, 1) : 0, 0);
+    std::vector<float> v32(vt == kVal32 ? std::max<int64_t>(nslot * nv * kChunk, 1) : 0, 0.0f);
+    std::vector<double> v64(vt == kVal64 ? std::max<int64_t>(nslot * nv * kChunk, 1) : 0, 0.0);
+#pragma omp parallel for schedule(dynamic, 64)
+    for (int64_t c = 0; c < nch; ++c) {
+        const auto& R = rows[lists[c]];
+        const int k = (int)(lists[c] % K);
+        const int64_t r0 = base[c], nr = std::min<int64_t>(kChunk, (int64_t)R.size() - r0);
+        for (int64_t lane = 0; lane < kChunk; ++lane) {
+            const bool real = lane < nr;
+            const int64_t g = real ? R[r0 + lane] : R[r0];
+            rowidx[c * kChunk + lane] = real ? (int32_t)g : ~(int32_t)g;
+            // pad slots: the row itself (offset 0), zero blocks
+            for (int64_t q = offl[c]; q < offl[c] + nsl[c] + nsu[c]; ++q) {
+                if (c16) gcol16[q * kChunk + lane] = 0;
+                else gcol[q * kChunk + lane] = (int32_t)g;
+            }
+            if (!real) continue;
+            const int64_t nc = g / kChunk, nl = g % kChunk;
+            int64_t ql = offl[c], qu = offu[c];
+            for (int64_t q = off[nc]; q < off[nc + 1]; ++q) {
+                const int64_t j = col[q * kChunk + nl];
+                if (j == g) continue;
+                const int64_t t = colour[j] < k ? ql++ : qu++;
+                if (c16) gcol16[t * kChunk + lane] = (int16_t)(j - g);
+                else gcol[t * kChunk + lane] = (int32_t)j;
+                double blk[9];
+                for (int ij = 0; ij < 9; ++ij) blk[ij] = val[(q * 9 + ij) * kChunk + nl];
+                if (vt == kValH16) {
+                    uint16_t rec[10];
+                    to_h16_block(blk, rec);
+                    for (int e = 0; e < 10; ++e) v16[t * 10 * kChunk + 128 * (e / 2) + 2 * lane + e % 2] = rec[e];
+                } else if (vt == kVal32) {
+                    for (int ij = 0; ij < 9; ++ij) v32[t * 9 * kChunk + slot_elem<float>(ij, lane)] = (float)blk[ij];
+                } else {
+                    for (int ij = 0; ij < 9; ++ij) v64[t * 9 * kChunk + slot_elem<double>(ij, lane)] = blk[ij];
+                }
+            }
+        }
+    }
+    G.ncol = K;
+    G.nchunk = nch;
+    G.first.assign(K, 0);
+    G.count.assign(K, 0);
+    std::vector<int32_t> list;
+    for (int k = 0; k < K; ++k) {
+        G.first[k] = (int64_t)list.size();
+        G.count[k] = (int64_t)bycol[k].size();
+        list.insert(list.end(), bycol[k].begin(), bycol[k].end());
+    }
+    G.list.upload(list);
+    G.rowidx.upload(rowidx);
+    G.csub.upload(csub);
+    G.nsl.upload(nsl);
+    G.nsu.upload(nsu);
+    G.offl.upload(offl);
+    G.offu.upload(offu);
+    G.cb.upload(cb);
+    if (c16) G.col16.upload(gcol16);
+    else G.col.upload(gcol);
+    if (vt == kValH16) G.val16.upload(v16);
+    else if (vt == kVal32) G.val32.upload(v32);
+    else G.val64.upload(v64);
+    if (std::getenv("DDPCA_VERBOSE"))
+        std::fprintf(stderr, "[ddpca] fine level: multicolour Gauss-Seidel, %d colours, %lld chunks, %lld slots\n", K,
+                     (long long)nch, (long long)nslot);
+}
 }  // namespace
 
 MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const mgpis_options_t& o, bool gen,
@@ -1435,6 +1655,9 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
     DDPCA_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
     if (opt.nu < 1) opt.nu = 1;
     if (opt.iters_per_graph < 1) opt.iters_per_graph = 1;
+    if (opt.smoother < 0 || opt.smoother > 3) throw ApiError(DDPCA_EINVAL, "smoother must be 0..3");
+    // the multicolour sweeps' symmetric pairing needs K = K^T: nonsymmetric handles smooth with block Jacobi
+    if (opt.smoother == 3 && general) opt.smoother = 1;
     const bool bj = opt.smoother >= 1;
     // device numbering: perm[l][s][reference local node] = device local node.  Levels >= 1 with
     // coordinates: lexicographic, or -- table mode, when the level's distinct rows compress --
@@ -1630,6 +1853,11 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
                     m32[w * g + k] = bj && !general ? (float)(0.5 * (m[k] + m[3 * (k % 3) + k / 3])) : (float)m[k];
             }
             L.minv32.upload(m32);
+        }
+        if (l == nlev - 1 && nlev > 1 && opt.smoother == 3) {
+            // the V-cycle copy's storage type of this level (vc_type once the level is up)
+            const int vt = (!vc32 || L.tbl) ? kVal64 : L.val16.p ? kValH16 : kVal32;
+            build_gs(gs, L, nsub, off, col, val, vt);
         }
         L.mask.upload(mask);
         for (auto* v : {&L.x, &L.t, &L.b, &L.r, &L.d}) {
@@ -1901,6 +2129,7 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
     int64_t maxch = 0;
     for (auto& L : lev) maxch = std::max<int64_t>(maxch, L.nch);
     partial.alloc(2 * maxch);
+    if (gs_fine()) gs.partial.alloc(gs.nchunk);
     sc.alloc(nsub);
     DDPCA_HIP(hipHostMalloc(reinterpret_cast<void**>(&sc_host), nsub * sizeof(PcgScal)));
     std::memset(sc_host, 0, nsub * sizeof(PcgScal));
@@ -2220,6 +2449,60 @@ bool MgpisDevice::fuse_jac0() const {
     return on && !no_coarse && opt.smoother == 1 && Lf > clev && vc_type(Lf) != kVal64 && lev[Lf].minv32.p;
 }
 
+namespace {
+// one k_gs launch: phase ph over colour k's chunks (k < 0: every chunk)
+template <int PH, bool DOT, typename T>
+void launch_gs_t(const GsArgs& a, bool c16, hipStream_t st) {
+    const dim3 grid((unsigned)ceil_div(a.n, kBlock / kWave));
+    // slot loop (sell_rows): 1 non-temporal streaming, 2 with the columns prefetched a group
+    // ahead (DDPCA_GS_LOOP, read at graph capture)
+    const char* e = std::getenv("DDPCA_GS_LOOP");
+    const int v = e ? std::atoi(e) : 1;
+    if (c16) {
+        if (v == 2) hipLaunchKernelGGL((k_gs<PH, DOT, T, int16_t, 2>), grid, dim3(kBlock), 0, st, a);
+        else hipLaunchKernelGGL((k_gs<PH, DOT, T, int16_t, 1>), grid, dim3(kBlock), 0, st, a);
+    } else if (v == 2) hipLaunchKernelGGL((k_gs<PH, DOT, T, int32_t, 2>), grid, dim3(kBlock), 0, st, a);
+    else hipLaunchKernelGGL((k_gs<PH, DOT, T, int32_t, 1>), grid, dim3(kBlock), 0, st, a);
+}
+
+template <int PH, bool DOT>
+void launch_gs(const MgpisDevice& D, int k, double* x, const double* b, double* r, const PcgScal* scp, double* partial) {
+    const GsFine& G = D.gs;
+    const LevelDev& F = D.lev.back();
+    GsArgs a{};
+    a.list = k < 0 ? nullptr : G.list.p + G.first[k];
+    a.n = k < 0 ? G.nchunk : G.count[k];
+    if (a.n == 0) return;
+    a.rowidx = G.rowidx.p;
+    a.csub = G.csub.p;
+    a.nsl = G.nsl.p;
+    a.nsu = G.nsu.p;
+    a.offl = G.offl.p;
+    a.offu = G.offu.p;
+    a.col = G.col.p;
+    a.col16 = G.col16.p;
+    a.x = x;
+    a.b = b;
+    a.r = r;
+    a.sc = scp;
+    a.partial = partial;
+    const bool c16 = G.col16.p != nullptr;
+    if (G.val16.p) {
+        a.val = G.val16.p;
+        a.minv = F.minv32.p;
+        launch_gs_t<PH, DOT, uint16_t>(a, c16, D.stream);
+    } else if (G.val32.p) {
+        a.val = G.val32.p;
+        a.minv = F.minv32.p;
+        launch_gs_t<PH, DOT, float>(a, c16, D.stream);
+    } else {
+        a.val = G.val64.p;
+        a.minv = F.minv.p;
+        launch_gs_t<PH, DOT, double>(a, c16, D.stream);
+    }
+}
+}  // namespace
+
 void MgpisDevice::vcycle(const double* rin, double* zout, bool dot, bool first_done) {
     if (no_coarse) throw ApiError(DDPCA_ESTATE, "one-level handle without a coarse inverse: diagonal preconditioner only");
     const int nlev = (int)lev.size();
@@ -2271,8 +2554,15 @@ void MgpisDevice::vcycle(const double* rin, double* zout, bool dot, bool first_d
             std::swap(cur[l], oth[l]);
         }
     };
+    const bool gsf = gs_fine();
+    if (gsf) cur[Lf] = zout;  // the Gauss-Seidel sweeps run in place
     // ---- descend
-    if (first_done) {
+    if (gsf) {
+        if (first_done) throw ApiError(DDPCA_ESTATE, "fused first sweep with the multicolour smoother");
+        // forward sweep from zero, colour by colour, then r = -U x in one launch
+        for (int k = 0; k < gs.ncol; ++k) launch_gs<0, false>(*this, k, zout, rin, nullptr, scp, nullptr);
+        launch_gs<1, false>(*this, -1, zout, nullptr, lev[Lf].r.p, scp, nullptr);
+    } else if (first_done) {
         // k_axpy_jac0 wrote x0 = omega M rin into the fine level's first iterate buffer
         if (cur[Lf] != lev[Lf].t.p || !fuse_jac0()) throw ApiError(DDPCA_ESTATE, "fused first sweep");
     } else {
@@ -2288,8 +2578,8 @@ void MgpisDevice::vcycle(const double* rin, double* zout, bool dot, bool first_d
         else hipLaunchKernelGGL((k_jac0<false, false>), dim3(grid), dim3(kBlock), 0, stream, rin, F.minv.p, coef(Lf, 0), cur[Lf], nullptr, F.nn, F.csub.p, scp);
     }
     for (int l = Lf; l >= cl + 1; --l) {
-        smooth(l, 1, nu - 1, false);
-        {
+        if (!(gsf && l == Lf)) {
+            smooth(l, 1, nu - 1, false);
             SellArgs a = vc_level_args(*this, l);
             a.sc = scp;
             a.x = cur[l];
@@ -2350,6 +2640,14 @@ void MgpisDevice::vcycle(const double* rin, double* zout, bool dot, bool first_d
         else hipLaunchKernelGGL(k_prolong<false>, dim3(ceil_div(F.nn, kBlock)), dim3(kBlock), 0, stream, cur[l - 1], F.ppar.p, F.pw.p,
                            F.mask.p, cur[l], F.nn, F.csub.p, scp);
         rot_prolong(l, cur[l - 1], cur[l], scp);
+        if (gsf && l == Lf) {
+            // backward sweep; the dot product's partials per colour chunk (vc_cb)
+            for (int k = gs.ncol - 1; k >= 0; --k) {
+                if (dot) launch_gs<2, true>(*this, k, zout, rin, nullptr, scp, gs.partial.p);
+                else launch_gs<2, false>(*this, k, zout, rin, nullptr, scp, nullptr);
+            }
+            continue;
+        }
         // post-smoothing restarts the smoother (Chebyshev recurrence) from the prolongated iterate
         smooth(l, 0, nu, dot && l == Lf);
     }
@@ -2404,10 +2702,24 @@ void MgpisDevice::vcycle_bytes(int s, double out[2]) const {
         out[0] += coarse + 16.0 * n0;  // + the dot product's second read
         return;
     }
-    put(Lf, n(Lf) * (48.0 + minv(Lf) + (cheb ? 24.0 : 0.0)));  // k_jac0: b in, x out
+    const bool gsf = gs_fine();
+    // multicolour sweeps on the fine level: L + U = the off-diagonal blocks, read once by the
+    // forward sweep + residual pair and once by the backward sweep; per launch the x entries of
+    // the colours it reads (forward colour k: the k earlier ones, residual: the later ones,
+    // backward: all others), and per row b, M^-1, the row index and x (or r) written
+    const double K = gsf ? (double)gs.ncol : 0.0;
+    const double gsmat = gsf ? (vbytes(vc_type(Lf)) + (gs.col16.p ? 2.0 : 4.0)) * (double)gs.nnzb_sub[s] : 0.0;
+    if (gsf) {
+        put(Lf, gsmat + n(Lf) * (24.0 + minv(Lf) + 24.0 + 4.0 + 24.0 * (K - 1.0) / 2.0));  // forward
+        put(Lf, n(Lf) * (24.0 + 4.0 + 24.0 * (K - 1.0) / 2.0));                              // residual
+    } else {
+        put(Lf, n(Lf) * (48.0 + minv(Lf) + (cheb ? 24.0 : 0.0)));  // k_jac0: b in, x out
+    }
     for (int l = Lf; l >= cl + 1; --l) {
-        for (int k = 1; k < opt.nu; ++k) put(l, sweep(l));
-        put(l, mat(l) + 72.0 * n(l));  // residual: x gathered, b, r
+        if (!(gsf && l == Lf)) {
+            for (int k = 1; k < opt.nu; ++k) put(l, sweep(l));
+            put(l, mat(l) + 72.0 * n(l));  // residual: x gathered, b, r
+        }
         const LevelDev& F = lev[l];
         const int c = l - 1;
         const bool init = c != cl;
@@ -2428,6 +2740,10 @@ void MgpisDevice::vcycle_bytes(int s, double out[2]) const {
         else pb += (F.uw ? 4.0 : 12.0) * (double)F.tent_sub[s];
         pb += 4.0 * 8.0 * (double)F.tblk_sub[s];
         put(l, pb);
+        if (gsf && l == Lf) {
+            put(l, gsmat + n(l) * (24.0 + minv(l) + 24.0 + 4.0 + 24.0 * (K - 1.0)));  // backward
+            continue;
+        }
         for (int k = 0; k < opt.nu; ++k) put(l, sweep(l));
     }
 }
@@ -2450,9 +2766,12 @@ void MgpisDevice::setup_bytes(int s, double out[2]) const {
 
 int64_t MgpisDevice::iteration_launches() const {
     // k_sell<kPcg>, k_axpy, 3 x k_fin, and the V-cycle: jac0 + per descended level (nu - 1 sweeps,
-    // residual, restriction) + coarse + per ascended level (prolongation, nu sweeps)
+    // residual, restriction) + coarse + per ascended level (prolongation, nu sweeps); the
+    // multicolour fine level: one forward and one backward launch per colour + the residual in
+    // place of jac0, nu - 1 + 1 + nu sweep launches
     const int64_t nd = (int64_t)lev.size() - 1 - clev;
-    return 5 + (nd == 0 ? 2 : 1 + nd * (opt.nu + 1) + 1 + nd * (1 + opt.nu));
+    const int64_t base = 5 + (nd == 0 ? 2 : 1 + nd * (opt.nu + 1) + 1 + nd * (1 + opt.nu));
+    return gs_fine() && nd > 0 ? base - 1 - 2 * opt.nu + 2 * gs.ncol + 1 : base;
 }
 
 // k_fin over every member (1024 threads, or 256 with DDPCA_FIN_THREADS=256)
@@ -2493,7 +2812,8 @@ void MgpisDevice::enqueue_iteration(int prec, bool timed) {
     launch_fin(stream, (int)kFinRR, partial.p, nullptr, fin_cb.p, scp, mirror.dev);
     if (prec == 1) vcycle(rs.p, zs.p, true, fuse0);
     else hipLaunchKernelGGL(k_diag, dim3(nblk), dim3(kBlock), 0, stream, rs.p, L.dinv.p, zs.p, partial.p, L.nn, L.csub.p, scp);
-    launch_fin(stream, (int)kFinBeta, partial.p, nullptr, fin_cb.p, scp, mirror.dev);
+    launch_fin(stream, (int)kFinBeta, prec == 1 ? vc_partial() : partial.p, nullptr, prec == 1 ? vc_cb() : fin_cb.p, scp,
+               mirror.dev);
 }
 
 // graph_[prec]: iters_per_graph PCG iterations captured once and replayed.
@@ -2649,7 +2969,8 @@ void MgpisDevice::pcg_begin(int prec, double rtol, const std::vector<int64_t>& m
     }
     if (prec == 1) vcycle(rs.p, zs.p, true);
     else hipLaunchKernelGGL(k_diag, dim3(nblk), dim3(kBlock), 0, stream, rs.p, L.dinv.p, zs.p, partial.p, L.nn, L.csub.p, sc.p);
-    launch_fin(stream, (int)kFinBeta0, partial.p, nullptr, fin_cb.p, sc.p, mirror.dev);
+    launch_fin(stream, (int)kFinBeta0, prec == 1 ? vc_partial() : partial.p, nullptr, prec == 1 ? vc_cb() : fin_cb.p, sc.p,
+               mirror.dev);
     sample_pending_ = false;
     if (time_kernel) {
         // first iteration eagerly, with HIP events around its fine-level SpMV on this stream

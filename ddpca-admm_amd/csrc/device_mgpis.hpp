@@ -129,6 +129,35 @@ struct LevelDev {
     DevBuf<double> x, t, b, r, d;
 };
 
+// Multicolour node-block Gauss-Seidel on the fine level (opt.smoother = 3): the fine nodes of
+// each member are coloured greedily in device order (8 colours on a 27-point lattice), each
+// colour's rows packed into 64-row chunks of their own.  A chunk's off-diagonal blocks are split
+// by the column's colour into L (earlier colours) and U (later colours), both in the V-cycle
+// copy's storage type, columns as in the level's SELL (offsets from the row node or int32).
+// The pre-smoothing forward sweep from a zero guess reads only L (x_i = M_i (b_i - L_i x),
+// colour by colour); the residual after it is r_i = -U_i x exactly (the row's own equation is
+// met), so sweep + residual cost one operator pass; the backward post-smoothing sweep reads L
+// and U.  With the symmetrised M the V-cycle stays symmetric (pre = forward, post = backward).
+struct GsFine {
+    int ncol = 0;                        // colours
+    int64_t nchunk = 0;                  // colour chunks of the batch, member-major, colour-minor
+    std::vector<int64_t> first, count;   // per colour: its chunk ids in `list`
+    DevBuf<int32_t> list;                // chunk ids grouped by colour
+    DevBuf<int32_t> rowidx;              // per chunk lane: device row, ~first row of the chunk on pad lanes
+    DevBuf<int32_t> csub, nsl, nsu;      // per chunk: member, L slots, U slots
+    DevBuf<int64_t> offl, offu;          // per chunk: first L / U slot
+    DevBuf<int32_t> col;                 // per slot lane (when the level has no 16-bit offsets)
+    DevBuf<int16_t> col16;
+    DevBuf<uint16_t> val16;
+    DevBuf<float> val32;
+    DevBuf<double> val64;
+    DevBuf<int64_t> cb;                  // per member: first colour chunk (nsub + 1), the dot partials
+    DevBuf<double> partial;              // per colour chunk: the backward sweep's dot partials (their own
+                                         // buffer: a split batch's other half writes the Krylov partials meanwhile)
+    std::vector<int64_t> nnzb_sub;       // per member: stored off-diagonal blocks (byte model)
+    std::vector<int64_t> slots_sub;      // per member: L + U slots incl. padding
+};
+
 class MgpisDevice {
 public:
     // general: the operators may be nonsymmetric (LAGRANGE's condensed systems under Coulomb
@@ -145,6 +174,11 @@ public:
     hipStream_t stream = nullptr;
     mgpis_options_t opt{};
     std::vector<LevelDev> lev;
+    GsFine gs;                            // opt.smoother = 3: the fine level's colour structure
+    bool gs_fine() const { return gs.ncol > 0; }
+    // chunk partials the V-cycle's dot product leaves and their bounds (k_fin after vcycle(dot))
+    const int64_t* vc_cb() const { return gs_fine() ? gs.cb.p : fin_cb.p; }
+    double* vc_partial() const { return gs_fine() ? gs.partial.p : partial.p; }
     // exact coarse solve on level clev: per-subdomain dense inverses, packed
     int clev = 0;
     DevBuf<double> ainv;

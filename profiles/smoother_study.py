@@ -1,0 +1,210 @@
+"""Smoother study on the headline's subdomain hierarchy (CPU, scipy): PCG iterations to the
+reference's stop rule (||r|| <= 1e-14 ||b||, x0 = 0) with the V(1,1) preconditioners the device
+could run at equal fine-level operator passes:
+
+  bj     3x3 node-block Jacobi, damping 1.7 / lambda_max(D^-1 K) (the headline's smoother)
+  mcgs   multicolour node-block Gauss-Seidel: forward over the colours before the coarse
+         correction, backward after it (symmetric V-cycle); colours from a greedy colouring of
+         the node graph (8 on a 27-point lattice)
+  mcgs_fine  mcgs on the finest level only, bj below
+  mcgs_coarse  bj on the finest level, mcgs below
+  sgs    the reference's lexicographic point SGS (MGPIS.h:61-114) for comparison
+
+    python profiles/smoother_study.py [gl] [subdomain]
+"""
+from __future__ import annotations
+
+import importlib
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+import scipy.sparse as sp
+import scipy.sparse.linalg as spl
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+D = importlib.import_module("ddpca-admm_amd")
+
+
+def hierarchy(gl: int, tv: int):
+    P = D.headline_problem(gl=gl).ESTABLISH()
+    G = P.grid(tv)
+    L = G.maxiLeve
+    nn = [int(x) for x in P.array("leveCount", tv)]
+    flag = np.asarray(P.array("consFlag", tv))
+    K = [G.consStif(l).tocsr() for l in range(L + 1)]
+    Pr = [G.realProl(l).tocsr() for l in range(L)]
+    node = []
+    for l in range(L + 1):
+        dofs = np.nonzero(flag[:3 * nn[l]])[0]
+        assert len(dofs) == K[l].shape[0]
+        node.append(dofs // 3)
+    b = np.asarray(P.array("consForc", tv), dtype=np.float64)
+    if not np.any(b):
+        b = np.random.default_rng(0).standard_normal(K[L].shape[0])
+    return K, Pr, node, b
+
+
+class BlockDiag:
+    """node blocks of K (1-3 free dofs per node) and their inverses, padded to 3x3"""
+
+    def __init__(self, K, node):
+        n = K.shape[0]
+        un, first = np.unique(node, return_index=True)
+        self.nodes = un
+        self.loc = np.searchsorted(un, node)
+        self.slot = np.arange(n) - first[self.loc]
+        nb = len(un)
+        Bk = np.zeros((nb, 3, 3))
+        Kc = K.tocoo()
+        same = self.loc[Kc.row] == self.loc[Kc.col]
+        Bk[self.loc[Kc.row[same]], self.slot[Kc.row[same]], self.slot[Kc.col[same]]] = Kc.data[same]
+        for k in range(3):
+            pad = Bk[:, k, k] == 0
+            Bk[pad, k, k] = 1.0
+        self.inv = np.linalg.inv(Bk)
+        self.n = n
+
+    def apply(self, r, rows=None):
+        rows = np.arange(self.n) if rows is None else rows
+        v = np.zeros((self.inv.shape[0], 3))
+        v[self.loc[rows], self.slot[rows]] = r
+        w = np.einsum("nij,nj->ni", self.inv, v)
+        return w[self.loc[rows], self.slot[rows]]
+
+
+def colouring(K, node):
+    """greedy colouring of the node graph in node order"""
+    bd_loc = np.unique(node, return_inverse=True)[1]
+    nb = bd_loc.max() + 1
+    A = sp.csr_matrix((np.ones(K.nnz), K.indices, K.indptr), shape=K.shape)
+    R = sp.csr_matrix((np.ones(len(node)), (bd_loc, np.arange(len(node)))), shape=(nb, len(node)))
+    G = (R @ A @ R.T).tocsr()
+    col = -np.ones(nb, dtype=np.int64)
+    for v in range(nb):
+        nb_cols = col[G.indices[G.indptr[v]:G.indptr[v + 1]]]
+        used = set(nb_cols[nb_cols >= 0].tolist())
+        c = 0
+        while c in used:
+            c += 1
+        col[v] = c
+    return col[bd_loc]
+
+
+class VCycle:
+    def __init__(self, K, Pr, node, smoother: str, coarse: int = 0):
+        # "name" or "name:nu_fine:nu_coarse" (sweeps before and after the coarse correction)
+        smoother, *nus = smoother.split(":")
+        self.nu_fine, self.nu_coarse = (int(nus[0]), int(nus[1])) if nus else (1, 1)
+        self.nu_second = int(nus[2]) if len(nus) > 2 else self.nu_coarse  # level L-1
+        self.K, self.Pr, self.sm = K, Pr, smoother
+        self.L = len(K) - 1
+        self.coarse = coarse
+        self.lu = spl.splu(K[coarse].tocsc())
+        self.bd, self.omega, self.rows, self.Krows, self.tri = {}, {}, {}, {}, {}
+        for l in range(coarse + 1, self.L + 1):
+            bd = BlockDiag(K[l], node[l])
+            self.bd[l] = bd
+            if self.is_bj(l):
+                lam = spl.eigsh(spl.LinearOperator(K[l].shape, matvec=lambda x, l=l: bd.apply(K[l] @ x)), k=1,
+                                which="LM", return_eigenvectors=False, tol=1e-3)[0]
+                self.omega[l] = 1.7 / lam
+            elif smoother.startswith("mcgs"):
+                c = colouring(K[l], node[l])
+                self.rows[l] = [np.nonzero(c == k)[0] for k in range(c.max() + 1)]
+                self.Krows[l] = [K[l][r] for r in self.rows[l]]
+            elif smoother == "sgs":
+                self.tri[l] = (sp.tril(K[l], format="csr"), sp.triu(K[l], format="csr"))
+
+    def is_bj(self, l):
+        return self.sm == "bj" or (self.sm == "mcgs_fine" and l < self.L) or (self.sm == "mcgs_coarse" and l == self.L)
+
+    def smooth(self, l, x, b, forward: bool):
+        K = self.K[l]
+        if self.is_bj(l):
+            return x + self.omega[l] * self.bd[l].apply(b - K @ x)
+        if self.sm.startswith("mcgs"):
+            order = range(len(self.rows[l])) if forward else reversed(range(len(self.rows[l])))
+            x = x.copy()
+            for k in order:
+                r = self.rows[l][k]
+                x[r] += self.bd[l].apply(b[r] - self.Krows[l][k] @ x, r)
+            return x
+        lo, up = self.tri[l]
+        if forward:
+            return x + spl.spsolve_triangular(lo, b - K @ x, lower=True)
+        return x + spl.spsolve_triangular(up, b - K @ x, lower=False)
+
+    def apply(self, l, b):
+        if l == self.coarse:
+            return self.lu.solve(b)
+        nu = self.nu_fine if l == self.L else self.nu_second if l == self.L - 1 else self.nu_coarse
+        x = np.zeros_like(b)
+        for _ in range(nu):
+            x = self.smooth(l, x, b, True)
+        r = b - self.K[l] @ x
+        x = x + self.Pr[l - 1] @ self.apply(l - 1, self.Pr[l - 1].T @ r)
+        for _ in range(nu):
+            x = self.smooth(l, x, b, False)
+        return x
+
+
+def pcg(K, b, M, rtol=1e-14, maxit=500):
+    x = np.zeros_like(b)
+    r = b.copy()
+    z = M(r)
+    p = z.copy()
+    rz = r @ z
+    nb = np.linalg.norm(b)
+    for it in range(1, maxit + 1):
+        q = K @ p
+        a = rz / (p @ q)
+        x += a * p
+        r -= a * q
+        if np.linalg.norm(r) <= rtol * nb:
+            return it, x
+        z = M(r)
+        rz, rz0 = r @ z, rz
+        p = z + (rz / rz0) * p
+    return maxit, x
+
+
+def round_h16(K, node):
+    """K with every 3x3 node block stored as 2^e x nine fp16 values (the device's block-exponent
+    fp16 copy of the fine level, precond_fp32 = 2)"""
+    Kc = K.tocoo()
+    key = node[Kc.row].astype(np.int64) * (node.max() + 1) + node[Kc.col]
+    uk, inv = np.unique(key, return_inverse=True)
+    mx = np.zeros(len(uk))
+    np.maximum.at(mx, inv, np.abs(Kc.data))
+    _, e = np.frexp(mx)
+    sc = np.ldexp(1.0, e)[inv]
+    v = (Kc.data / sc).astype(np.float16).astype(np.float64) * sc
+    return sp.csr_matrix((v, (Kc.row, Kc.col)), shape=K.shape)
+
+
+def main():
+    gl = int(sys.argv[1]) if len(sys.argv) > 1 else 4
+    tv = int(sys.argv[2]) if len(sys.argv) > 2 else 0
+    K, Pr, node, b = hierarchy(gl, tv)
+    if "--h16" in sys.argv:
+        # the V-cycle's fine level on the fp16 copy (the Krylov operator stays fp64)
+        K16 = round_h16(K[-1], node[-1])
+        Kv = K[:-1] + [K16]
+        print("fine level rounded to block-exponent fp16: |K16 - K| / |K| =",
+              spl.norm(K16 - K[-1]) / spl.norm(K[-1]))
+    else:
+        Kv = K
+    print(f"gl {gl} subdomain {tv}: levels {len(K)}, fine rows {K[-1].shape[0]}")
+    for sm in sys.argv[3].split(",") if len(sys.argv) > 3 and not sys.argv[3].startswith("-") else ("bj", "mcgs", "mcgs_fine", "sgs"):
+        t = time.time()
+        V = VCycle(Kv, Pr, node, sm)
+        it, x = pcg(K[-1], b, lambda r: V.apply(V.L, r))
+        res = np.linalg.norm(b - K[-1] @ x) / np.linalg.norm(b)
+        ncol = max((len(v) for v in V.rows.values()), default=0)
+        print(f"{sm:5s} PCG iterations {it:3d}  true relres {res:.2e}  colours {ncol}  ({time.time() - t:.1f} s)")
+
+
+if __name__ == "__main__":
+    main()

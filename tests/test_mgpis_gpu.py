@@ -54,7 +54,7 @@ def test_table_mode_is_the_same_operator(ddpca, gpu, case):
     assert np.linalg.norm(xt - golden(case)["x_mg"]) <= 1e-8 * np.linalg.norm(golden(case)["x_mg"])
 
 
-@pytest.mark.parametrize("smoother,nu", [(0, 1), (1, 1), (1, 2), (2, 2)])
+@pytest.mark.parametrize("smoother,nu", [(0, 1), (1, 1), (1, 2), (2, 2), (3, 1), (3, 2)])
 @pytest.mark.parametrize("case", ["beam_s1", "beam_s2", "beam_gl1"])
 def test_cg_solution_matches_reference(ddpca, gpu, case, smoother, nu):
     g = golden(case)
@@ -111,12 +111,31 @@ def test_vcycle_is_symmetric_positive(ddpca, gpu):
     P = _problem(ddpca, "beam_s2")
     n = len(P.grid(0).consForc)
     rng = np.random.default_rng(20251017)
-    for smoother, nu, f32 in [(0, 1, 0), (1, 1, 0), (2, 2, 0), (2, 2, 1), (1, 1, 2), (2, 2, 2)]:
+    for smoother, nu, f32 in [(0, 1, 0), (1, 1, 0), (2, 2, 0), (2, 2, 1), (1, 1, 2), (2, 2, 2), (3, 1, 0), (3, 2, 1),
+                              (3, 2, 2)]:
         M = ddpca.MGPIS.from_problem(P, 0, smoother=smoother, nu=nu, precond_fp32=f32)
         u, v = rng.standard_normal(n), rng.standard_normal(n)
         Mu, Mv = M.MULT_VCYC(u), M.MULT_VCYC(v)
         assert abs(u @ Mv - v @ Mu) <= 1e-10 * abs(u @ Mv)
         assert v @ Mv > 0
+
+
+@pytest.mark.parametrize("f32", [0, 2])
+def test_multicolour_gauss_seidel_on_the_headline_subdomains(ddpca, gpu, f32):
+    """smoother = 3: multicolour block Gauss-Seidel on the fine level (forward before, backward
+    after the coarse correction; the forward sweep's residual r = -U x), block Jacobi with nu = 2
+    sweeps below.  On the headline's DEHW-synthetic subdomains (gl = 3) it must reach the same stop
+    rule with the same solution as block Jacobi V(1,1) in fewer PCG iterations (CPU study,
+    profiles/smoother_study.py at gl = 4: 23-24 -> 18)."""
+    P = ddpca.headline_problem(gl=3).ESTABLISH()
+    for tv in (0, 1):
+        b = P.grid(tv).consForc
+        xj, ij, _ = ddpca.MGPIS.from_problem(P, tv, smoother=1, nu=1, omega=-1.7, precond_fp32=f32).CG_SOLV(1, b)
+        xg, ig, rr = ddpca.MGPIS.from_problem(P, tv, smoother=3, nu=2, omega=-1.7, precond_fp32=f32).CG_SOLV(1, b)
+        print(tv, "block Jacobi", ij, "multicolour GS", ig)
+        assert rr <= 1e-14
+        assert ig <= 0.85 * ij, (ig, ij)
+        assert np.linalg.norm(xg - xj) <= 1e-10 * np.linalg.norm(xj)
 
 
 def test_csr_dropin_matches_native(ddpca, gpu):
