@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <cstring>
 #include <memory>
+#include <map>
 #include <set>
 #include <string>
 
@@ -60,7 +61,115 @@ ddpca_multigrid& open(ddpca_multigrid_t h, bool want_built) {
 
 }  // namespace
 
+// CURVEDS (CURVEDS.h:8-121): a curved surface as a grid of points indiPoin[i][j] with the reverse
+// map point -> (i, j) under the mesh's coordinate comparison.  REFINE_SEARCH: a corner set lies on
+// the surface when every corner is a grid point; its new node is the point at the corners'
+// averaged (integer) indices.
+struct ddpca_curveds {
+    int64_t ni = 0, nj = 0;
+    std::vector<std::array<double, 3>> pt;  // ni x nj
+    std::vector<uint8_t> present;
+    std::map<std::array<double, 3>, std::array<int64_t, 2>, MULTIGRID::CoorLess> index;
+    // the last plan (ddpca_curveds_plan)
+    std::vector<int64_t> plan_ptr, plan_node;
+    std::vector<double> plan_xyz;
+    void reindex() {  // CURVEDS::INSERT's poinIndi.emplace: the first point of equal coordinates wins
+        index.clear();
+        for (int64_t i = 0; i < ni; ++i)
+            for (int64_t j = 0; j < nj; ++j)
+                if (present[i * nj + j]) index.emplace(pt[i * nj + j], std::array<int64_t, 2>{i, j});
+    }
+    bool search(const std::vector<std::array<double, 3>>& c, std::array<double, 3>& out) const {
+        int64_t si = 0, sj = 0;
+        for (const auto& p : c) {
+            const auto it = index.find(p);
+            if (it == index.end()) return false;
+            si += it->second[0];
+            sj += it->second[1];
+        }
+        si /= (int64_t)c.size();
+        sj /= (int64_t)c.size();
+        out = pt[si * nj + sj];
+        return true;
+    }
+};
+
 extern "C" {
+
+int ddpca_curveds_create(int64_t ni, int64_t nj, const double* xyz, const uint8_t* present, ddpca_curveds_t* out) {
+    return guarded([&] {
+        if (ni < 1 || nj < 1 || !xyz || !out) throw ApiError(DDPCA_EINVAL, "null argument or empty surface grid");
+        auto c = std::make_unique<ddpca_curveds>();
+        c->ni = ni;
+        c->nj = nj;
+        c->pt.resize(ni * nj);
+        c->present.assign(ni * nj, 1);
+        for (int64_t k = 0; k < ni * nj; ++k) {
+            for (int a = 0; a < 3; ++a) c->pt[k][a] = xyz[3 * k + a];
+            if (present) c->present[k] = present[k] ? 1 : 0;
+        }
+        c->reindex();
+        *out = c.release();
+    });
+}
+
+int ddpca_curveds_rigid(ddpca_curveds_t c, const double* R, const double* t) {
+    return guarded([&] {
+        if (!c || !R || !t) throw ApiError(DDPCA_EINVAL, "null argument");
+        for (int64_t k = 0; k < c->ni * c->nj; ++k) {
+            if (!c->present[k]) continue;
+            const std::array<double, 3> p = c->pt[k];
+            for (int a = 0; a < 3; ++a) c->pt[k][a] = (R[3 * a] * p[0] + R[3 * a + 1] * p[1] + R[3 * a + 2] * p[2]) + t[a];
+        }
+        c->reindex();
+    });
+}
+
+int ddpca_curveds_plan(ddpca_curveds_t c, ddpca_multigrid_t h, int64_t n, const int64_t* elem, const int64_t** plan_ptr,
+                       const int64_t** plan_node, const double** plan_xyz, int64_t* nplan) {
+    return guarded([&] {
+        if (!c || !h || (n > 0 && !elem) || !plan_ptr || !plan_node || !plan_xyz || !nplan)
+            throw ApiError(DDPCA_EINVAL, "null argument");
+        if (h->built) throw ApiError(DDPCA_ESTATE, "the operators are already built");
+        const MULTIGRID& g = h->g;
+        // CURVEDS::REFINE (CURVEDS.h:58-101): every line and face of every split element
+        static const int line[12][2] = {{0, 1}, {1, 2}, {2, 3}, {3, 0}, {4, 5}, {5, 6}, {6, 7}, {7, 4}, {0, 4}, {1, 5}, {2, 6}, {3, 7}};
+        static const int face[6][4] = {{0, 3, 7, 4}, {1, 2, 6, 5}, {0, 4, 5, 1}, {3, 7, 6, 2}, {0, 1, 2, 3}, {4, 5, 6, 7}};
+        std::map<std::vector<int64_t>, std::array<double, 3>> plan;
+        auto try_key = [&](std::vector<int64_t> key) {
+            std::vector<std::array<double, 3>> xyz;
+            for (int64_t v : key) xyz.push_back(g.nodeCoor[v]);
+            std::array<double, 3> p;
+            if (!c->search(xyz, p)) return;
+            std::sort(key.begin(), key.end());
+            plan.emplace(key, p);  // planSurf.insert: an existing key keeps its point
+        };
+        for (int64_t k = 0; k < n; ++k) {
+            if (elem[k] < 0 || elem[k] >= (int64_t)g.elemVect.size()) throw ApiError(DDPCA_EINVAL, "element out of range");
+            const auto& cn = g.elemVect[elem[k]].cornNode;
+            for (const auto& l : line) try_key({cn[l[0]], cn[l[1]]});
+            for (const auto& f : face) try_key({cn[f[0]], cn[f[1]], cn[f[2]], cn[f[3]]});
+        }
+        c->plan_ptr.assign(1, 0);
+        c->plan_node.clear();
+        c->plan_xyz.clear();
+        for (const auto& kv : plan) {
+            c->plan_node.insert(c->plan_node.end(), kv.first.begin(), kv.first.end());
+            c->plan_ptr.push_back((int64_t)c->plan_node.size());
+            c->plan_xyz.insert(c->plan_xyz.end(), kv.second.begin(), kv.second.end());
+        }
+        *plan_ptr = c->plan_ptr.data();
+        *plan_node = c->plan_node.data();
+        *plan_xyz = c->plan_xyz.data();
+        *nplan = (int64_t)plan.size();
+    });
+}
+
+int ddpca_curveds_destroy(ddpca_curveds_t c) {
+    delete c;
+    return DDPCA_OK;
+}
+
 
 int ddpca_multigrid_create(int64_t nnode, const double* coords, int64_t nelem, const int64_t* corner,
                            const int64_t* parent, const int64_t* level, const int64_t* refiPatt,

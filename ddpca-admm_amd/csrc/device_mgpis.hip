@@ -11,6 +11,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <numeric>
+#include <tuple>
 #include <type_traits>
 #include <omp.h>
 #include <random>
@@ -468,7 +469,7 @@ struct GsArgs {
 template <int PH, bool DOT, typename T, typename CT, int V = 1>
 __global__ __launch_bounds__(kBlock) void k_gs(GsArgs a) {
     const int lane = threadIdx.x & 63;
-    const int64_t li = (int64_t)blockIdx.x * (kBlock / kWave) + (threadIdx.x >> 6);
+    const int64_t li = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     if (li >= a.n) return;
     const int64_t c = a.list ? (int64_t)a.list[li] : li;
     const int sub = a.csub[c];
@@ -1521,6 +1522,46 @@ void build_gs(GsFine& G, const LevelDev& L, int nsub, const std::vector<int64_t>
     std::vector<std::vector<int64_t>> rows((size_t)nsub * K);
     for (int s = 0; s < nsub; ++s)
         for (int64_t g = L.noff[s]; g < L.noff[s] + L.nloc[s]; ++g) rows[(size_t)s * K + colour[g]].push_back(g);
+    // a member that is a full nx x ny x nz box in lexicographic device order (the generators'
+    // meshes): its colour rows go to chunks tile by tile -- 16 x 16 nodes of one plane, i.e.
+    // 8 x 8 rows of a colour -- instead of along the x lines (a chunk of 64 rows of one colour
+    // spans 128 nodes of x, more than a line), so a chunk's neighbour gathers stay in ~18 x 18 x 3
+    // nodes
+    // (measured 1.8 % slower at the headline, profiles/r03i: opt-in DDPCA_GS_TILE=1)
+    static const bool tile = std::getenv("DDPCA_GS_TILE") && std::atoi(std::getenv("DDPCA_GS_TILE")) != 0;
+    int tiled = 0;
+    for (int s = 0; s < nsub && tile; ++s) {
+        // nx, nx*ny from the column offsets of an interior row (the first past the member's middle
+        // with 26 neighbours): positive offsets 1, nx - 1, nx, nx + 1, nx ny - nx - 1, ...
+        std::vector<int64_t> d;
+        for (int64_t g = L.noff[s] + L.nloc[s] / 2; g < L.noff[s] + L.nloc[s] && d.size() != 13; ++g) {
+            const int64_t c = g / kChunk, lane = g % kChunk;
+            d.clear();
+            int64_t nb = 0;
+            for (int64_t q = off[c]; q < off[c + 1]; ++q) {
+                const int64_t j = col[q * kChunk + lane];
+                nb += j != g;
+                if (j > g) d.push_back(j - g);
+            }
+            std::sort(d.begin(), d.end());
+            d.erase(std::unique(d.begin(), d.end()), d.end());
+            if (nb != 26) d.clear();
+        }
+        if (d.size() != 13 || d[0] != 1) continue;
+        const int64_t nx = d[1] + 1, nxy = d[4] + nx + 1;
+        if (d[2] != nx || d[3] != nx + 1 || nxy % nx || L.nloc[s] % nxy) continue;
+        const int64_t ny = nxy / nx;
+        for (int k = 0; k < K; ++k) {
+            auto& R = rows[(size_t)s * K + k];
+            std::stable_sort(R.begin(), R.end(), [&](int64_t u, int64_t v) {
+                const int64_t lu = u - L.noff[s], lv = v - L.noff[s];
+                const int64_t zu = lu / nxy, zv = lv / nxy, yu = lu % nxy / nx, yv = lv % nxy / nx, xu = lu % nx, xv = lv % nx;
+                return std::make_tuple(zu, yu / 16, xu / 16, yu, xu) < std::make_tuple(zv, yv / 16, xv / 16, yv, xv);
+            });
+        }
+        (void)ny;
+        ++tiled;
+    }
     std::vector<int32_t> rowidx, csub, nsl, nsu;
     std::vector<int64_t> offl, offu, cb(nsub + 1, 0);
     std::vector<std::vector<int32_t>> bycol(K);
@@ -1633,8 +1674,8 @@ void build_gs(GsFine& G, const LevelDev& L, int nsub, const std::vector<int64_t>
     else if (vt == kVal32) G.val32.upload(v32);
     else G.val64.upload(v64);
     if (std::getenv("DDPCA_VERBOSE"))
-        std::fprintf(stderr, "[ddpca] fine level: multicolour Gauss-Seidel, %d colours, %lld chunks, %lld slots\n", K,
-                     (long long)nch, (long long)nslot);
+        std::fprintf(stderr, "[ddpca] fine level: multicolour Gauss-Seidel, %d colours, %lld chunks, %lld slots, %d of %d members tiled\n",
+                     K, (long long)nch, (long long)nslot, tiled, nsub);
 }
 }  // namespace
 
@@ -2453,16 +2494,20 @@ namespace {
 // one k_gs launch: phase ph over colour k's chunks (k < 0: every chunk)
 template <int PH, bool DOT, typename T>
 void launch_gs_t(const GsArgs& a, bool c16, hipStream_t st) {
-    const dim3 grid((unsigned)ceil_div(a.n, kBlock / kWave));
+    // workgroup of one wave (DDPCA_GS_BLOCK=64) or four (256, default): a small batch's colour
+    // launches have a few hundred chunks, which one-wave groups spread over more CUs
+    const char* eb = std::getenv("DDPCA_GS_BLOCK");
+    const int bs = eb && std::atoi(eb) == 64 ? 64 : kBlock;
+    const dim3 grid((unsigned)ceil_div(a.n, bs / kWave));
     // slot loop (sell_rows): 1 non-temporal streaming, 2 with the columns prefetched a group
-    // ahead (DDPCA_GS_LOOP, read at graph capture)
+    // ahead (DDPCA_GS_LOOP, read at graph capture; measured equal, profiles/r03i)
     const char* e = std::getenv("DDPCA_GS_LOOP");
     const int v = e ? std::atoi(e) : 1;
     if (c16) {
-        if (v == 2) hipLaunchKernelGGL((k_gs<PH, DOT, T, int16_t, 2>), grid, dim3(kBlock), 0, st, a);
-        else hipLaunchKernelGGL((k_gs<PH, DOT, T, int16_t, 1>), grid, dim3(kBlock), 0, st, a);
-    } else if (v == 2) hipLaunchKernelGGL((k_gs<PH, DOT, T, int32_t, 2>), grid, dim3(kBlock), 0, st, a);
-    else hipLaunchKernelGGL((k_gs<PH, DOT, T, int32_t, 1>), grid, dim3(kBlock), 0, st, a);
+        if (v == 2) hipLaunchKernelGGL((k_gs<PH, DOT, T, int16_t, 2>), grid, dim3(bs), 0, st, a);
+        else hipLaunchKernelGGL((k_gs<PH, DOT, T, int16_t, 1>), grid, dim3(bs), 0, st, a);
+    } else if (v == 2) hipLaunchKernelGGL((k_gs<PH, DOT, T, int32_t, 2>), grid, dim3(bs), 0, st, a);
+    else hipLaunchKernelGGL((k_gs<PH, DOT, T, int32_t, 1>), grid, dim3(bs), 0, st, a);
 }
 
 template <int PH, bool DOT>

@@ -322,6 +322,20 @@ int ddpca_multigrid_set(ddpca_multigrid_t g, const char* what, int64_t n, const 
 int ddpca_multigrid_refine(ddpca_multigrid_t g, int64_t n, const int64_t* elem, const int64_t* patt, int64_t nplan,
                            const int64_t* plan_ptr, const int64_t* plan_node, const double* plan_xyz, int64_t nflag,
                            const int64_t* flag_elem, const int64_t* flag_child);
+/* CURVEDS (CURVEDS.h:8-121): a curved surface as an ni x nj grid of points (xyz row-major,
+ * present[i nj + j] = 0 for grid cells the reference leaves empty; NULL = all present).
+ * ddpca_curveds_plan = CURVEDS::REFINE (CURVEDS.h:58-101): for every line and face of the n
+ * elements of the (unbuilt) multigrid g whose corners are all grid points, the new node's position
+ * = the point at the corners' averaged indices -- the planSurf of ddpca_multigrid_refine (keys as
+ * CSR of sorted node ids); the arrays stay valid until the next plan call on c.  Several surfaces:
+ * concatenate their plans in the order the reference calls their REFINE (the first entry of a key
+ * wins, as planSurf.insert).  ddpca_curveds_rigid = RIGI_ROTR (p <- R p + t, R row-major). */
+typedef struct ddpca_curveds* ddpca_curveds_t;
+int ddpca_curveds_create(int64_t ni, int64_t nj, const double* xyz, const uint8_t* present, ddpca_curveds_t* out);
+int ddpca_curveds_rigid(ddpca_curveds_t c, const double* R, const double* t);
+int ddpca_curveds_plan(ddpca_curveds_t c, ddpca_multigrid_t g, int64_t n, const int64_t* elem, const int64_t** plan_ptr,
+                       const int64_t** plan_node, const double** plan_xyz, int64_t* nplan);
+int ddpca_curveds_destroy(ddpca_curveds_t c);
 /* The tree before build (int64 unless noted): "nodeCoor" (f64, 3 per node), "corner" (8 per element),
  * "parent", "level", "refiPatt", "child_ptr" (elements + 1), "child", "nextSplit". */
 int ddpca_multigrid_tree(ddpca_multigrid_t g, const char* what, const void** data, int64_t* count, int* dtype);

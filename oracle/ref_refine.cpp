@@ -5,7 +5,11 @@
 // CSEARCH::ADAPTIVE_REFINE (CSEARCH.h:839-956) on the first curved contact pair, at the finest
 // leaf level and the given distCrit; the leaf elements of that level that the reference then has
 // refined (they gained children) are compared with the elements libddpca_amd's
-// ddpca_refine_select flags on the same faces, coordinates and buckets.  CPU only.  One JSON line.
+// ddpca_refine_select flags on the same faces, coordinates and buckets.  Then the refinement
+// itself: each side's tree as it was before ADAPTIVE_REFINE goes through ddpca_curveds_plan (the
+// side's CURVEDS, exported from the reference's indiPoin grid) and ddpca_multigrid_refine with
+// the flagged elements, and the refined trees are compared with the reference's (node ids and
+// coordinates bitwise, corners, parents, levels, patterns, children).  CPU only.  One JSON line.
 //   ref_refine distCrit [locaLeve]
 #include <unistd.h>
 
@@ -50,6 +54,23 @@ int main(int argc, char** argv) {
         for (const auto& nc : g[s]->nodeCoor)
             for (int a = 0; a < 3; ++a) xyz[s][3 * nc.first + a] = nc.second[a];
     }
+    // the trees and surfaces before the reference refines them
+    ddpca_multigrid_t tree[2] = {ddpca_bind::tree_create(*g[0]), ddpca_bind::tree_create(*g[1])};
+    ddpca_curveds_t cds[2] = {nullptr, nullptr};
+    for (int s = 0; s < 2; ++s) {
+        const auto& ip = surf[s]->indiPoin;
+        size_t nj = 0;
+        for (const auto& row : ip) nj = std::max(nj, row.size());
+        std::vector<double> pts(3 * ip.size() * nj, 0.0);
+        std::vector<uint8_t> present(ip.size() * nj, 0);
+        for (size_t i = 0; i < ip.size(); ++i)
+            for (size_t j = 0; j < ip[i].size(); ++j) {
+                if (ip[i][j].size() != 3) continue;
+                present[i * nj + j] = 1;
+                for (int a = 0; a < 3; ++a) pts[3 * (i * nj + j) + a] = ip[i][j][a];
+            }
+        ddpca_bind::check(ddpca_curveds_create((int64_t)ip.size(), (int64_t)nj, pts.data(), present.data(), &cds[s]));
+    }
     CSEARCH cs = c.searCont[ts];
     cs.mastSegm.clear();
     cs.slavSegm.clear();
@@ -93,10 +114,55 @@ int main(int argc, char** argv) {
             nflag[s] += flag[s][i];
             equal = equal && refined == (flag[s][i] != 0);
         }
+    // the refinement of the flagged elements through the library, against the reference's trees
+    bool trees_equal = true;
+    long planned[2] = {0, 0}, nodes[2] = {0, 0}, elems[2] = {0, 0};
+    for (int s = 0; s < 2; ++s) {
+        std::vector<int64_t> el, pa;
+        for (size_t i = 0; i < cand[s].size(); ++i)
+            if (flag[s][i]) el.push_back(cand[s][i]), pa.push_back(0);
+        const int64_t *pp = nullptr, *pn = nullptr;
+        const double* px = nullptr;
+        int64_t np = 0;
+        ddpca_bind::check(ddpca_curveds_plan(cds[s], tree[s], (int64_t)el.size(), el.data(), &pp, &pn, &px, &np));
+        planned[s] = (long)np;
+        ddpca_bind::check(ddpca_multigrid_refine(tree[s], (int64_t)el.size(), el.data(), pa.data(), np, pp, pn, px, 0, nullptr,
+                                                 nullptr));
+        auto get = [&](const char* what, auto tag) {
+            const void* data = nullptr;
+            int64_t n = 0;
+            int dt = -1;
+            ddpca_bind::check(ddpca_multigrid_tree(tree[s], what, &data, &n, &dt));
+            using T = decltype(tag);
+            return std::vector<T>((const T*)data, (const T*)data + n);
+        };
+        const auto xyzs = get("nodeCoor", 0.0);
+        const auto corner_ = get("corner", int64_t{}), parent = get("parent", int64_t{}), level = get("level", int64_t{}),
+                   patt = get("refiPatt", int64_t{}), cptr = get("child_ptr", int64_t{}), child = get("child", int64_t{});
+        const MULTIGRID& G = *g[s];
+        nodes[s] = (long)G.nodeCoor.size();
+        elems[s] = (long)G.elemVect.size();
+        bool eq = (long)xyzs.size() == 3 * nodes[s] && (long)parent.size() == elems[s];
+        for (const auto& nc : G.nodeCoor)
+            for (int a = 0; eq && a < 3; ++a) eq = nc.first < nodes[s] && xyzs[3 * nc.first + a] == nc.second[a];
+        for (long e = 0; eq && e < elems[s]; ++e) {
+            const TREE_ELEM& t = G.elemVect[e];
+            for (int k = 0; k < 8; ++k) eq = eq && corner_[8 * e + k] == t.cornNode[k];
+            eq = eq && parent[e] == t.parent && level[e] == t.level && patt[e] == t.refiPatt;
+            const long nch = t.children.empty() ? 0 : t.refiPatt == 0 ? 8 : t.refiPatt <= 3 ? 4 : 2;
+            eq = eq && cptr[e + 1] - cptr[e] == nch;
+            for (long q = 0; eq && q < nch; ++q) eq = child[cptr[e] + q] == t.children[q];
+        }
+        trees_equal = trees_equal && eq;
+        ddpca_curveds_destroy(cds[s]);
+        ddpca_multigrid_destroy(tree[s]);
+    }
     std::fprintf(stderr,
                  "{\"equal\": %s, \"isnoRefi\": %s, \"level\": %ld, \"candidates\": [%zu, %zu], \"refined_ref\": [%ld, %ld], "
-                 "\"flagged\": [%ld, %ld], \"faces\": [%zu, %zu]}\n",
+                 "\"flagged\": [%ld, %ld], \"faces\": [%zu, %zu], \"trees_equal\": %s, \"planSurf\": [%ld, %ld], "
+                 "\"nodes\": [%ld, %ld], \"elements\": [%ld, %ld]}\n",
                  equal ? "true" : "false", isnoRefi ? "true" : "false", lev, cand[0].size(), cand[1].size(), nref[0], nref[1],
-                 nflag[0], nflag[1], cs.mastSegm.size(), cs.slavSegm.size());
-    return equal ? 0 : 1;
+                 nflag[0], nflag[1], cs.mastSegm.size(), cs.slavSegm.size(), trees_equal ? "true" : "false", planned[0],
+                 planned[1], nodes[0], nodes[1], elems[0], elems[1]);
+    return equal && trees_equal ? 0 : 1;
 }

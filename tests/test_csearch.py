@@ -57,7 +57,12 @@ def test_adaptive_refine_selection_matches_reference(tmp_path, dist):
     its CYLINDER example (oracle/ref_refine.cpp): of the 4096 finest leaf elements per side of the
     first curved contact pair, exactly the elements the reference refines (1024 per side, the band
     within distCrit = 1e-5 of the other surface; none at 0) are the ones ddpca_refine_select flags,
-    and isnoRefi agrees."""
+    and isnoRefi agrees.  Then the refinement itself through the library -- CURVEDS::REFINE
+    (ddpca_curveds_plan on the side's cylinder surface, exported from the reference's indiPoin
+    grid) and MULTIGRID::REFINE with GRLE_CHECK (ddpca_multigrid_refine) on the trees as they were
+    before -- must leave each side's tree exactly as the reference's ADAPTIVE_REFINE does: node ids
+    and coordinates bitwise (3332 nodes per side on the curved surface), corners, parents, levels,
+    patterns, children."""
     exe = Path(__file__).resolve().parents[1] / "oracle" / "_ref" / "ref_refine"
     if not exe.exists():
         pytest.skip("oracle/_ref/ref_refine is built where the reference is (oracle/Makefile)")
@@ -65,8 +70,8 @@ def test_adaptive_refine_selection_matches_reference(tmp_path, dist):
     assert out.returncode == 0, out.stderr[-2000:]
     res = json.loads(out.stderr.strip().splitlines()[-1])
     print(res)
-    assert res["equal"], res
+    assert res["equal"] and res["trees_equal"], res
     if dist != "0":
-        assert res["isnoRefi"] and min(res["refined_ref"]) > 0, res
+        assert res["isnoRefi"] and min(res["refined_ref"]) > 0 and min(res["planSurf"]) > 0, res
     else:
         assert not res["isnoRefi"], res
