@@ -2494,10 +2494,10 @@ namespace {
 // one k_gs launch: phase ph over colour k's chunks (k < 0: every chunk)
 template <int PH, bool DOT, typename T>
 void launch_gs_t(const GsArgs& a, bool c16, hipStream_t st) {
-    // workgroup of one wave (DDPCA_GS_BLOCK=64) or four (256, default): a small batch's colour
-    // launches have a few hundred chunks, which one-wave groups spread over more CUs
+    // workgroup of one wave (default) or four (DDPCA_GS_BLOCK=256): one-wave groups spread a
+    // colour's chunks over more CUs (+1 % at 8 subdomains, profiles/r03j)
     const char* eb = std::getenv("DDPCA_GS_BLOCK");
-    const int bs = eb && std::atoi(eb) == 64 ? 64 : kBlock;
+    const int bs = eb && std::atoi(eb) == 256 ? kBlock : 64;
     const dim3 grid((unsigned)ceil_div(a.n, bs / kWave));
     // slot loop (sell_rows): 1 non-temporal streaming, 2 with the columns prefetched a group
     // ahead (DDPCA_GS_LOOP, read at graph capture; measured equal, profiles/r03i)

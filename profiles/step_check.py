@@ -14,7 +14,8 @@ profiles/r01_pmc_calibration.txt).
 Every launch of an ADMM iteration (which ends with its MONITOR reductions, k_reduce_pairs) is put
 in one of bench.py's phases by name, grid and position:
   fine_level_pcg            k_sell<3> and the V-cycle's launches on the fine level (grid = fine
-                            nodes), k_axpy, the restriction out of the fine level
+                            nodes; the multicolour sweeps k_gs), k_axpy, the restriction out of
+                            the fine level
   coarse_levels_and_scalars every other launch of the PCG (coarser levels, k_coarse, k_fin)
   coarse_space              launches between k_outp and the interface's first launch
   mass_cg                   k_mcg_*, k_scal_*
@@ -32,7 +33,7 @@ import statistics
 
 PHASES = ["fine_level_pcg", "coarse_levels_and_scalars", "coarse_space", "mass_cg", "interface_rhs_monitor"]
 PCG = ("k_sell", "k_jac0", "k_restrict", "k_prolong", "k_axpy", "k_fin", "k_coarse", "k_dot", "k_pcg_init",
-       "k_split_sc", "k_merge_sc", "k_diag")
+       "k_split_sc", "k_merge_sc", "k_diag", "k_gs")
 IFACE_START = ("k_gamma_ip", "k_sell_w", "k_project", "k_pair_norms")
 
 
@@ -79,7 +80,7 @@ def classify(it):
             out.append("mass_cg")
         elif stage == "pcg" and n.startswith(PCG):
             fine = (n.startswith(("k_sell", "k_jac0", "k_prolong", "k_axpy", "k_pcg_init")) and r[1] >= 0.5 * fine_grid) or \
-                   (n.startswith("k_restrict") and r[1] == rgrid)
+                   (n.startswith("k_restrict") and r[1] == rgrid) or n.startswith("k_gs")
             out.append("fine_level_pcg" if fine else "coarse_levels_and_scalars")
         elif stage == "cs":
             out.append("coarse_space")

@@ -1,9 +1,9 @@
 """Parity of the exact option set the headline number is measured with.
 
 bench.py runs MCONTACT on the synthetic DEHW chain with ``HEADLINE_OPTIONS`` (ddpca-admm_amd/
-__init__.py: block-Jacobi V(1,1), damping 1.7/lambda_max, fp32 V-cycle levels with block-exponent
-fp16 on the two finest, streamed rows (table_mode 0), automatic exact-solve level, 4 PCG
-iterations per hipGraph replay) and ``HEADLINE_MUSC`` (interface-eliminated coarse space,
+__init__.py: multicolour block Gauss-Seidel on the fine level, block-Jacobi with two sweeps
+below, damping 1.7/lambda_max, fp32 V-cycle levels with block-exponent fp16 on the two finest,
+streamed rows (table_mode 0), automatic exact-solve level, 4 PCG iterations per hipGraph replay) and ``HEADLINE_MUSC`` (interface-eliminated coarse space,
 muscSett = 2, doleMcsc = 1).  These tests run that same set:
 
 * reduced chain: ``headline_problem(gl=3)`` -- the bench's workload (``HEADLINE_WORKLOAD``: 8-subdomain
@@ -159,12 +159,14 @@ def test_headline_fullsize_batched_solves_match_oracle(ddpca, oracle, gpu):
         assert err <= 1e-8, (tv, err)
 
 
-@pytest.mark.parametrize("env", [("DDPCA_STREAMS", "1"), ("DDPCA_FUSE_JAC0", "1")], ids=["one-stream", "fused-jac0"])
+@pytest.mark.parametrize("env", [("DDPCA_STREAMS", "1"), ("DDPCA_FUSE_JAC0", "1"), ("DDPCA_GS_BLOCK", "256")],
+                         ids=["one-stream", "fused-jac0", "gs-workgroup-256"])
 def test_schedule_variants_are_bit_identical(ddpca, gpu, monkeypatch, env):
     """Schedule-only variants of the headline path must not change a bit: the two-stream split of
     the body-balance batch and of the mass CG (MgpisDevice / MassBatch ::set_split, default on)
-    against one stream, and the V-cycle's first fine sweep fused into k_axpy (k_axpy_jac0, opt-in)
-    against the separate k_jac0 (default).  ADMM trajectory, displacements and PCG iteration counts equal
+    against one stream, the V-cycle's first fine sweep fused into k_axpy (k_axpy_jac0, opt-in,
+    block-Jacobi option sets only) against the separate k_jac0, and the multicolour sweeps in
+    four-wave workgroups against one-wave ones (default).  ADMM trajectory, displacements and PCG iteration counts equal
     bit for bit (8 ADMM iterations, reduced chain, headline option set)."""
     H, M = ddpca.HEADLINE_OPTIONS, ddpca.HEADLINE_MUSC
     out = {}
