@@ -42,8 +42,15 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("fetch_csv")
     ap.add_argument("write_csv")
-    for k, d in [("groups", 4), ("nx", 3), ("ny", 2), ("nz", 2), ("gl", 5), ("smoother", 1), ("nu", 1),
-                 ("precond-fp32", 2), ("table-mode", 0)]:
+    # defaults: bench.py's (the package's HEADLINE_WORKLOAD / HEADLINE_OPTIONS)
+    import importlib
+    import sys
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+    pkg = importlib.import_module("ddpca-admm_amd")
+    W, H = pkg.HEADLINE_WORKLOAD, pkg.HEADLINE_OPTIONS
+    for k, d in [("groups", W["groups"]), ("nx", W["nx"]), ("ny", W["ny"]), ("nz", W["nz"]), ("gl", W["gl"]),
+                 ("smoother", H["smoother"]), ("nu", H["nu"]), ("precond-fp32", H["precond_fp32"]),
+                 ("table-mode", H["table_mode"])]:
         ap.add_argument(f"--{k}", type=int, default=d)
     ap.add_argument("--value-layout", default="fp64-pairs, col16")
     ap.add_argument("--out", default=str(Path(__file__).resolve().parent / "traffic.json"))
