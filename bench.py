@@ -55,9 +55,10 @@ def parse():
                     help="contact faces integrated over 2^k x 2^k polygons (k = 2: M3's 0.8 ip per DOF with --ip-glued 1)")
     ap.add_argument("--ip-glued", type=int, default=W["ip_glued"], help="the same for the glued faces")
     # defaults: the fastest configuration of the round-1 sweep (profiles/r01_sweep.txt)
-    ap.add_argument("--smoother", type=int, default=H["smoother"], help="0 point Jacobi, 1 block Jacobi, 2 Chebyshev, "
-                    "3 multicolour block Gauss-Seidel on the fine level (block Jacobi below, --nu sweeps)")
-    ap.add_argument("--nu", type=int, default=H["nu"])
+    ap.add_argument("--smoother", type=int, default=None, help="0 point Jacobi, 1 block Jacobi, 2 Chebyshev, "
+                    "3 multicolour block Gauss-Seidel on the fine level (block Jacobi below, --nu sweeps); default: "
+                    "headline_options(subdomains per rank) -- 3 with nu 2 from 4 subdomains per rank, else 1 with nu 1")
+    ap.add_argument("--nu", type=int, default=None)
     ap.add_argument("--omega-scale", type=float, default=-H["omega"],
                     help="Jacobi damping = scale / lambda_max(M^-1 K) per level (profiles/r01_sweep_omega.txt)")
     ap.add_argument("--iters-per-graph", type=int, default=H["iters_per_graph"])
@@ -109,6 +110,12 @@ def main():
     nip = sum(len(P.array("ip_w", ts)) for ts in range(P.nint))
     nsub = P.nsub
     owner = part.block_owner(nsub, world)
+    # the option set of the rank with the most subdomains (all ranks run the same set)
+    Hs = D.headline_options(max(list(owner).count(r) for r in range(world)))
+    if a.smoother is None:
+        a.smoother = Hs["smoother"]
+    if a.nu is None:
+        a.nu = Hs["nu"]
     if a.musc:
         P.set_coarse(a.musc, [a.dole] * nsub)
     P.ESTABLISH(owner, rank)
