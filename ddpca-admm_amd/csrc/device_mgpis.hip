@@ -441,6 +441,14 @@ __global__ __launch_bounds__(kBlock) void k_sell_split(SellArgs a) {
     }
 }
 
+// Workgroup b is dispatched to XCD b % 8: the logical block that makes XCD x own the x-th
+// contiguous run of the grid (runs of q+1 blocks for the first r XCDs, q for the rest; G = 8q + r)
+__device__ __forceinline__ int64_t xcd_slab_block() {
+    const int64_t G = gridDim.x, b = blockIdx.x, q = G / 8, r = G % 8, x = b % 8, k = b / 8;
+    const int64_t start = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q;
+    return start + k;
+}
+
 // Multicolour block Gauss-Seidel on the fine level (GsFine): one wavefront per colour chunk,
 // lane = one row of that colour.  PH 0: forward sweep from zero over the L part, x_i = M_i (b_i -
 // L_i x); PH 1: the residual after the forward sweep, r_i = -U_i x (every chunk, one launch);
@@ -464,12 +472,15 @@ struct GsArgs {
     double* r;
     const PcgScal* sc;
     double* partial;
+    int xcd;  // 1: workgroups mapped so each XCD takes one contiguous run of the launch's chunks
+    const float* minvc;  // chunk-ordered fp32 inverses (GsFine::minvc) or null: minv by row
 };
 
 template <int PH, bool DOT, typename T, typename CT, int V = 1>
 __global__ __launch_bounds__(kBlock) void k_gs(GsArgs a) {
     const int lane = threadIdx.x & 63;
-    const int64_t li = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const int64_t blk = a.xcd ? xcd_slab_block() : (int64_t)blockIdx.x;
+    const int64_t li = blk * (blockDim.x >> 6) + (threadIdx.x >> 6);
     if (li >= a.n) return;
     const int64_t c = a.list ? (int64_t)a.list[li] : li;
     const int sub = a.csub[c];
@@ -502,7 +513,15 @@ __global__ __launch_bounds__(kBlock) void k_gs(GsArgs a) {
     } else {
         const double b0 = a.b[o], b1 = a.b[o + 1], b2 = a.b[o + 2];
         double m0, m1, m2;
-        apply_m<true>(static_cast<const SmoothInv<T>*>(a.minv), row, b0 - s0, b1 - s1, b2 - s2, m0, m1, m2);
+        if (a.minvc) {
+            const float* m = a.minvc + c * 9 * kChunk + lane;
+            const double r0 = b0 - s0, r1 = b1 - s1, r2 = b2 - s2;
+            m0 = (double)m[0] * r0 + (double)m[kChunk] * r1 + (double)m[2 * kChunk] * r2;
+            m1 = (double)m[3 * kChunk] * r0 + (double)m[4 * kChunk] * r1 + (double)m[5 * kChunk] * r2;
+            m2 = (double)m[6 * kChunk] * r0 + (double)m[7 * kChunk] * r1 + (double)m[8 * kChunk] * r2;
+        } else {
+            apply_m<true>(static_cast<const SmoothInv<T>*>(a.minv), row, b0 - s0, b1 - s1, b2 - s2, m0, m1, m2);
+        }
         if (real) {
             a.x[o] = m0;
             a.x[o + 1] = m1;
@@ -513,13 +532,6 @@ __global__ __launch_bounds__(kBlock) void k_gs(GsArgs a) {
     if (DOT) chunk_partial(dotv, a.partial, c);
 }
 
-// Workgroup b is dispatched to XCD b % 8: the logical block that makes XCD x own the x-th
-// contiguous run of the grid (runs of q+1 blocks for the first r XCDs, q for the rest; G = 8q + r)
-__device__ __forceinline__ int64_t xcd_slab_block() {
-    const int64_t G = gridDim.x, b = blockIdx.x, q = G / 8, r = G % 8, x = b % 8, k = b / 8;
-    const int64_t start = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q;
-    return start + k;
-}
 
 // Node-parallel kernels: thread = node, 256 nodes per workgroup; a wavefront is one chunk, so
 // the subdomain (and its stop flag) is uniform per wavefront.  nn is a multiple of 64.
@@ -1660,6 +1672,18 @@ void build_gs(GsFine& G, const LevelDev& L, int nsub, const std::vector<int64_t>
         G.count[k] = (int64_t)bycol[k].size();
         list.insert(list.end(), bycol[k].begin(), bycol[k].end());
     }
+    if (vt != kVal64 && L.minv32.p) {
+        const std::vector<float> m32 = L.minv32.download();
+        std::vector<float> mc((size_t)nch * 9 * kChunk, 0.0f);
+#pragma omp parallel for schedule(static)
+        for (int64_t c = 0; c < nch; ++c)
+            for (int64_t lane = 0; lane < kChunk; ++lane) {
+                const int32_t rr = rowidx[c * kChunk + lane];
+                const int64_t g = rr >= 0 ? rr : ~rr;  // pad lanes: the chunk's first row (their x is not stored)
+                for (int ij = 0; ij < 9; ++ij) mc[(c * 9 + ij) * kChunk + lane] = m32[9 * g + ij];
+            }
+        G.minvc.upload(mc);
+    }
     G.list.upload(list);
     G.rowidx.upload(rowidx);
     G.csub.upload(csub);
@@ -2531,6 +2555,12 @@ void launch_gs(const MgpisDevice& D, int k, double* x, const double* b, double* 
     a.r = r;
     a.sc = scp;
     a.partial = partial;
+    // DDPCA_GS_XCD=1: neighbouring chunks (which gather the same x lines) on one XCD's L2
+    const char* ex = std::getenv("DDPCA_GS_XCD");
+    a.xcd = ex && std::atoi(ex) == 1 ? 1 : 0;
+    // chunk-ordered inverses (DDPCA_GS_MINVC=0: by row)
+    const char* em = std::getenv("DDPCA_GS_MINVC");
+    a.minvc = (em && std::atoi(em) == 0) ? nullptr : G.minvc.p;
     const bool c16 = G.col16.p != nullptr;
     if (G.val16.p) {
         a.val = G.val16.p;

@@ -151,6 +151,8 @@ struct GsFine {
     DevBuf<uint16_t> val16;
     DevBuf<float> val32;
     DevBuf<double> val64;
+    DevBuf<float> minvc;                 // the rows' fp32 3x3 inverses in chunk order, [chunk][ij][lane]
+                                         // (coalesced; the natural array at stride 2 nodes wastes half of every line)
     DevBuf<int64_t> cb;                  // per member: first colour chunk (nsub + 1), the dot partials
     DevBuf<double> partial;              // per colour chunk: the backward sweep's dot partials (their own
                                          // buffer: a split batch's other half writes the Krylov partials meanwhile)

@@ -162,14 +162,16 @@ def test_headline_fullsize_batched_solves_match_oracle(ddpca, oracle, gpu):
         assert err <= 1e-8, (tv, err)
 
 
-@pytest.mark.parametrize("env", [("DDPCA_STREAMS", "1"), ("DDPCA_FUSE_JAC0", "1"), ("DDPCA_GS_BLOCK", "256")],
-                         ids=["one-stream", "fused-jac0", "gs-workgroup-256"])
+@pytest.mark.parametrize("env", [("DDPCA_STREAMS", "1"), ("DDPCA_FUSE_JAC0", "1"), ("DDPCA_GS_BLOCK", "256"),
+                                 ("DDPCA_GS_MINVC", "0"), ("DDPCA_GS_XCD", "1")],
+                         ids=["one-stream", "fused-jac0", "gs-workgroup-256", "gs-inverses-by-row", "gs-xcd-slabs"])
 def test_schedule_variants_are_bit_identical(ddpca, gpu, monkeypatch, env):
     """Schedule-only variants of the headline path must not change a bit: the two-stream split of
     the body-balance batch and of the mass CG (MgpisDevice / MassBatch ::set_split, default on)
     against one stream, the V-cycle's first fine sweep fused into k_axpy (k_axpy_jac0, opt-in,
     block-Jacobi option sets only) against the separate k_jac0, and the multicolour sweeps in
-    four-wave workgroups against one-wave ones (default).  ADMM trajectory, displacements and PCG iteration counts equal
+    four-wave workgroups, with the inverses read by row instead of in chunk order, and with
+    XCD-slab workgroup placement, against the defaults.  ADMM trajectory, displacements and PCG iteration counts equal
     bit for bit (8 ADMM iterations, reduced chain, headline option set)."""
     H, M = ddpca.HEADLINE_OPTIONS, ddpca.HEADLINE_MUSC
     out = {}
