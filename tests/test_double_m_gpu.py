@@ -20,16 +20,19 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
+@pytest.mark.parametrize("opts", ["default", "HEADLINE_OPTIONS"])
 @pytest.mark.parametrize("dole", [1, 2])
-def test_double_m_matches_oracle(ddpca, oracle, gpu, monkeypatch, dole):
+def test_double_m_matches_oracle(ddpca, oracle, gpu, monkeypatch, dole, opts):
     """dole 2 = the fine level (the coarse problem is the whole interface-eliminated problem,
-    a 3-level coarse hierarchy); dole 1: two levels."""
+    a 3-level coarse hierarchy); dole 1: two levels.  opts HEADLINE_OPTIONS: the coarse problem's
+    own MGPIS takes the multicolour smoother on its fine level too (no coordinates there)."""
+    O = {} if opts == "default" else dict(getattr(ddpca, opts))
     from test_mcontact_gpu import _oracle_coarse, _oracle_problem, _rows_close
     monkeypatch.setenv("DDPCA_COARSE_MG_MIN", "1")
     P = ddpca.Problem("dehw", 2, 2, 2, 1, 2, 0.3)
     P.set_coarse(2, [dole] * P.nsub)
     P.ESTABLISH()
-    mc = ddpca.MCONTACT(P)
+    mc = ddpca.MCONTACT(P, **O)
     k = 30
     assert mc.CONTACT_ANALYSIS(k, check=False) == k
     subs, ifaces = _oracle_problem(P)

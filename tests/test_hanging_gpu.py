@@ -76,8 +76,12 @@ def _graft(subs, ifaces, tv, rng, latin=None):
     return H
 
 
+@pytest.mark.parametrize("opts", ["default", "HEADLINE_OPTIONS"])
 @pytest.mark.parametrize("musc", [0, 1])
-def test_hanging_level_matches_oracle(ddpca, oracle, gpu, musc):
+def test_hanging_level_matches_oracle(ddpca, oracle, gpu, musc, opts):
+    """opts HEADLINE_OPTIONS: the multicolour Gauss-Seidel fine level on operators handed over
+    without coordinates (reference node order, colours of a general graph)."""
+    O = {} if opts == "default" else dict(getattr(ddpca, opts))
     from test_mcontact_gpu import _oracle_problem, _rows_close
     P = ddpca.Problem("dehw", 2, 2, 2, 1, 2, 0.3)
     if musc:
@@ -93,13 +97,13 @@ def test_hanging_level_matches_oracle(ddpca, oracle, gpu, musc):
                       globTran_D=[[P.csr("globTran_D", 2 * ts + s) for s in range(2)] for ts in range(P.nint)],
                       accuProl=[P.csr("accuProl", tv) for tv in range(P.nsub)])
     k = 30
-    base = ddpca.MCONTACT(ddpca.Problem.from_operators(subs, ifaces, coarse=coarse))
+    base = ddpca.MCONTACT(ddpca.Problem.from_operators(subs, ifaces, coarse=coarse), **O)
     assert base.CONTACT_ANALYSIS(k, check=False) == k
     u_base = [base.get("resuDisp", tv) for tv in range(P.nsub)]
     rng = np.random.default_rng(20251017)
     Hs = {tv: _graft(subs, ifaces, tv, rng, latin=coarse) for tv in (0, 3)}
     Q = ddpca.Problem.from_operators(subs, ifaces, coarse=coarse)
-    mc = ddpca.MCONTACT(Q)
+    mc = ddpca.MCONTACT(Q, **O)
     assert mc.CONTACT_ANALYSIS(k, check=False) == k
     osubs, oifaces = _oracle_problem(P)
     for tv, H in Hs.items():
