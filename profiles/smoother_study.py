@@ -96,6 +96,9 @@ class VCycle:
     def __init__(self, K, Pr, node, smoother: str, coarse: int = 0):
         # "name" or "name:nu_fine:nu_coarse" (sweeps before and after the coarse correction)
         smoother, *nus = smoother.split(":")
+        # "name@w": over-relaxed multicolour sweeps (SSOR-type: the same w forward and backward)
+        smoother, _, w = smoother.partition("@")
+        self.w = float(w) if w else 1.0
         self.nu_fine, self.nu_coarse = (int(nus[0]), int(nus[1])) if nus else (1, 1)
         self.nu_second = int(nus[2]) if len(nus) > 2 else self.nu_coarse  # level L-1
         self.K, self.Pr, self.sm = K, Pr, smoother
@@ -129,7 +132,7 @@ class VCycle:
             x = x.copy()
             for k in order:
                 r = self.rows[l][k]
-                x[r] += self.bd[l].apply(b[r] - self.Krows[l][k] @ x, r)
+                x[r] += self.w * self.bd[l].apply(b[r] - self.Krows[l][k] @ x, r)
             return x
         lo, up = self.tri[l]
         if forward:
