@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <climits>
 #include <cstdint>
 #include <string>
 #include <vector>
@@ -106,9 +107,13 @@ struct MirrorBuf {
 // Replay `graph` (k iterations each) on `stream` until every mirror reports done, keeping
 // about one replay queued ahead of the slowest unfinished solve.  `launched` = iterations
 // already enqueued (eager + pre-enqueued replays).  Returns the number of replays launched.
-int64_t pace_until_done(hipStream_t stream, hipGraphExec_t graph, const MirrorBuf& m, int64_t k, int64_t launched);
+// graph1 (one iteration) and horizon: once the queued iterations would pass `horizon` (the
+// solves' expected count), single iterations are queued two ahead of the slowest solve instead.
+int64_t pace_until_done(hipStream_t stream, hipGraphExec_t graph, const MirrorBuf& m, int64_t k, int64_t launched,
+                        hipGraphExec_t graph1 = nullptr, int64_t horizon = INT64_MAX);
 // the same for a batch split into two halves (half[s] = 0 or 1), each half's graph on its stream
+// (g1 / horizon: per half, or null)
 int64_t pace_halves(hipStream_t st[2], hipGraphExec_t g[2], const MirrorBuf& m, const std::vector<int>& half, int64_t k,
-                    int64_t launched0);
+                    int64_t launched0, hipGraphExec_t* g1 = nullptr, const int64_t* horizon = nullptr);
 
 }  // namespace ddpca

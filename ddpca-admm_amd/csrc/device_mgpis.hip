@@ -52,7 +52,21 @@ struct SellArgs {
     const double* tab;     // table mode: tstride doubles per table row, slot-major 3x3 blocks
     int64_t tstride;
     const int32_t* ctype;  // table mode: chunk -> its rows' common table row, -1 = mixed
+    // stencil-coded copy (LevelDev::coded): per chunk position mask / row-split sub-masks /
+    // first slot, per member strides, last node of the level (gathers clamp into the level)
+    const uint32_t* cm;
+    const uint32_t* cmq;
+    const int64_t* coff;
+    const int32_t* lstr;
+    int64_t nlast;
 };
+
+// column of stencil position q (0..26 = (dz+1) 9 + (dy+1) 3 + (dx+1)) for a row of a lattice
+// with strides nx, nxy, clamped into [0, hi] (a zero block's gather stays inside the level)
+__device__ __forceinline__ int64_t stencil_col(int64_t row, int q, int64_t nx, int64_t nxy, int64_t hi) {
+    const int64_t j = row + (int64_t)(q / 9 - 1) * nxy + (int64_t)((q / 3) % 3 - 1) * nx + (q % 3 - 1);
+    return j < 0 ? 0 : (j > hi ? hi : j);
+}
 
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
@@ -73,9 +87,9 @@ __device__ __forceinline__ void apply_m(const MT* minv, int64_t row, double r0, 
                                         double& m0, double& m1, double& m2) {
     if (BJ) {
         const MT* m = minv + 9 * row;
-        m0 = m[0] * r0 + m[1] * r1 + m[2] * r2;
-        m1 = m[3] * r0 + m[4] * r1 + m[5] * r2;
-        m2 = m[6] * r0 + m[7] * r1 + m[8] * r2;
+        m0 = __builtin_fma((double)m[2], r2, __builtin_fma((double)m[1], r1, (double)m[0] * r0));
+        m1 = __builtin_fma((double)m[5], r2, __builtin_fma((double)m[4], r1, (double)m[3] * r0));
+        m2 = __builtin_fma((double)m[8], r2, __builtin_fma((double)m[7], r1, (double)m[6] * r0));
     } else {
         const MT* m = minv + 3 * row;
         m0 = m[0] * r0;
@@ -141,26 +155,31 @@ __device__ __forceinline__ void block_fma_any(const T* v, const double* xj, doub
                                               int lane) {
     const double x0 = xj[0], x1 = xj[1], x2 = xj[2];
     auto ldv = [](const auto* p) { if constexpr (NT) return __builtin_nontemporal_load(p); else return *p; };
+    // row . x as fma(v2, x2, fma(v1, x1, v0 x0)), added to the accumulator: the contraction is
+    // spelled out so every kernel instantiating this rounds alike (left to fp-contract, the
+    // compiler fused different products in different kernels, e.g. the colour sweeps over
+    // column-indexed and stencil-coded slots)
+    auto dot3 = [x0, x1, x2](double v0, double v1, double v2) { return __builtin_fma(v2, x2, __builtin_fma(v1, x1, v0 * x0)); };
     if constexpr (sizeof(T) == 2) {
         // v = slot base + lane in halves; the lane's dword of pair p is at dword 64 p + lane
         const uint32_t* p = reinterpret_cast<const uint32_t*>(v - lane) + lane;
         const uint32_t a = ldv(p), b = ldv(p + 64), c = ldv(p + 128), d = ldv(p + 192), e = ldv(p + 256);
         const double sc = __builtin_amdgcn_ldexp(1.0, (int)(int16_t)(e >> 16));
-        s0 += sc * (h16_lo(a) * x0 + h16_hi(a) * x1 + h16_lo(b) * x2);
-        s1 += sc * (h16_hi(b) * x0 + h16_lo(c) * x1 + h16_hi(c) * x2);
-        s2 += sc * (h16_lo(d) * x0 + h16_hi(d) * x1 + h16_lo(e) * x2);
+        s0 = __builtin_fma(sc, dot3(h16_lo(a), h16_hi(a), h16_lo(b)), s0);
+        s1 = __builtin_fma(sc, dot3(h16_hi(b), h16_lo(c), h16_hi(c)), s1);
+        s2 = __builtin_fma(sc, dot3(h16_lo(d), h16_hi(d), h16_lo(e)), s2);
     } else if constexpr (paired_values<T>() && sizeof(T) == 8) {
         const dbl2_t* p = reinterpret_cast<const dbl2_t*>(v - lane) + lane;
         const dbl2_t a = ldv(p), b = ldv(p + 64), c = ldv(p + 128), d = ldv(p + 192);
         const double v8 = ldv(v + 512);
-        s0 += a.x * x0 + a.y * x1 + b.x * x2;
-        s1 += b.y * x0 + c.x * x1 + c.y * x2;
-        s2 += d.x * x0 + d.y * x1 + v8 * x2;
+        s0 = s0 + dot3(a.x, a.y, b.x);
+        s1 = s1 + dot3(b.y, c.x, c.y);
+        s2 = s2 + dot3(d.x, d.y, v8);
     } else {
         auto ld = [&](int i) { return (double)ldv(v + i * kChunk); };
-        s0 += ld(0) * x0 + ld(1) * x1 + ld(2) * x2;
-        s1 += ld(3) * x0 + ld(4) * x1 + ld(5) * x2;
-        s2 += ld(6) * x0 + ld(7) * x1 + ld(8) * x2;
+        s0 = s0 + dot3(ld(0), ld(1), ld(2));
+        s1 = s1 + dot3(ld(3), ld(4), ld(5));
+        s2 = s2 + dot3(ld(6), ld(7), ld(8));
     }
 }
 
@@ -232,6 +251,18 @@ __device__ __forceinline__ void sell_rows(const CT* colp, const T* valp, const d
         }
         for (; k < ns; ++k) block_fma(valp + (int64_t)k * SV, x + 3 * col_of(colp[(int64_t)k * kChunk], row), s0, s1, s2);
     }
+}
+
+// Stencil-coded rows (LevelDev::coded): slot k = the k-th set bit of the wave-uniform mask m, its
+// column arithmetic on scalar registers -- the x gathers depend on nothing loaded
+template <typename T>
+__device__ __forceinline__ void sell_rows_coded(uint32_t m, const T* valp, const double* x, int64_t row, int64_t nx,
+                                                int64_t nxy, int64_t hi, double& s0, double& s1, double& s2) {
+    constexpr int64_t SV = slot_vals<T>() * kChunk;
+    m = __builtin_amdgcn_readfirstlane(m);
+#pragma unroll 3
+    for (int k = 0; m; ++k, m &= m - 1)
+        block_fma(valp + (int64_t)k * SV, x + 3 * stencil_col(row, __builtin_ctz(m), nx, nxy, hi), s0, s1, s2);
 }
 
 // Table mode: the row's blocks are the 9-double records tv[9k .. 9k+8] of its table row (shared
@@ -333,6 +364,13 @@ __global__ __launch_bounds__(kBlock) void k_sell(SellArgs a, const double* __res
                                                 s0, s1, s2);
         else
             sell_rows_tbl(a.col + base * kChunk + lane, tab + (int64_t)a.rtype[row] * a.tstride, a.x, ns, s0, s1, s2);
+    } else if constexpr (std::is_same<CT, uint32_t>::value) {
+        // stencil-coded copy (CT = uint32_t tags it)
+        (void)ns;
+        (void)base;
+        const int64_t cb = a.coff[c];
+        sell_rows_coded<T>(a.cm[c], static_cast<const T*>(a.val) + cb * slot_vals<T>() * kChunk + lane, a.x, row,
+                           a.lstr[2 * sub], a.lstr[2 * sub + 1], a.nlast, s0, s1, s2);
     } else if constexpr (sizeof(CT) == 2)
         sell_rows<V, T, CT>(a.col16 + base * kChunk + lane, static_cast<const T*>(a.val) + base * slot_vals<T>() * kChunk + lane,
                             a.x, ns, row, s0, s1, s2);
@@ -350,35 +388,40 @@ __global__ __launch_bounds__(kBlock) void k_sell(SellArgs a, const double* __res
         a.y[o] = r0;
         a.y[o + 1] = r1;
         a.y[o + 2] = r2;
-        if (DOT) dotv = r0 * r0 + r1 * r1 + r2 * r2;
+        if (DOT) dotv = __builtin_fma(r2, r2, __builtin_fma(r1, r1, r0 * r0));
     } else if (MODE == kJac) {
         const double om = a.coef[2 * sub + 1];
         const double b0 = a.b[o], b1 = a.b[o + 1], b2 = a.b[o + 2];
         double m0, m1, m2;
         apply_m<BJ>(static_cast<const SmoothInv<T>*>(a.minv), row, b0 - s0, b1 - s1, b2 - s2, m0, m1, m2);
-        const double n0 = a.x[o] + om * m0, n1 = a.x[o + 1] + om * m1, n2 = a.x[o + 2] + om * m2;
+        // (explicit contraction throughout the epilogues: every instantiation rounds alike)
+        const double n0 = __builtin_fma(om, m0, a.x[o]), n1 = __builtin_fma(om, m1, a.x[o + 1]),
+                     n2 = __builtin_fma(om, m2, a.x[o + 2]);
         a.xo[o] = n0;
         a.xo[o + 1] = n1;
         a.xo[o + 2] = n2;
-        if (DOT) dotv = b0 * n0 + b1 * n1 + b2 * n2;
+        if (DOT) dotv = __builtin_fma(b2, n2, __builtin_fma(b1, n1, b0 * n0));
     } else if (MODE == kPcg) {
         // q = K z + beta q_old, p = z + beta p_old  (K p = K z + beta K p_old)
         const double be = a.sc[sub].beta;
-        const double q0 = s0 + be * a.y[o], q1 = s1 + be * a.y[o + 1], q2 = s2 + be * a.y[o + 2];
-        const double p0 = a.x[o] + be * a.p[o], p1 = a.x[o + 1] + be * a.p[o + 1], p2 = a.x[o + 2] + be * a.p[o + 2];
+        const double q0 = __builtin_fma(be, a.y[o], s0), q1 = __builtin_fma(be, a.y[o + 1], s1),
+                     q2 = __builtin_fma(be, a.y[o + 2], s2);
+        const double p0 = __builtin_fma(be, a.p[o], a.x[o]), p1 = __builtin_fma(be, a.p[o + 1], a.x[o + 1]),
+                     p2 = __builtin_fma(be, a.p[o + 2], a.x[o + 2]);
         a.y[o] = q0;
         a.y[o + 1] = q1;
         a.y[o + 2] = q2;
         a.p[o] = p0;
         a.p[o + 1] = p1;
         a.p[o + 2] = p2;
-        if (DOT) dotv = p0 * q0 + p1 * q1 + p2 * q2;
+        if (DOT) dotv = __builtin_fma(p2, q2, __builtin_fma(p1, q1, p0 * q0));
     } else if (MODE == kCheb) {
         const double c1 = a.coef[2 * sub], c2 = a.coef[2 * sub + 1];
         const double b0 = a.b[o], b1 = a.b[o + 1], b2 = a.b[o + 2];
         double m0, m1, m2;
         apply_m<BJ>(static_cast<const SmoothInv<T>*>(a.minv), row, b0 - s0, b1 - s1, b2 - s2, m0, m1, m2);
-        const double d0 = c1 * a.p[o] + c2 * m0, d1 = c1 * a.p[o + 1] + c2 * m1, d2 = c1 * a.p[o + 2] + c2 * m2;
+        const double d0 = __builtin_fma(c2, m0, c1 * a.p[o]), d1 = __builtin_fma(c2, m1, c1 * a.p[o + 1]),
+                     d2 = __builtin_fma(c2, m2, c1 * a.p[o + 2]);
         a.p[o] = d0;
         a.p[o + 1] = d1;
         a.p[o + 2] = d2;
@@ -386,7 +429,7 @@ __global__ __launch_bounds__(kBlock) void k_sell(SellArgs a, const double* __res
         a.xo[o] = n0;
         a.xo[o + 1] = n1;
         a.xo[o + 2] = n2;
-        if (DOT) dotv = b0 * n0 + b1 * n1 + b2 * n2;
+        if (DOT) dotv = __builtin_fma(b2, n2, __builtin_fma(b1, n1, b0 * n0));
     }
     if (DOT) chunk_partial(dotv, a.partial, c);
 }
@@ -407,14 +450,29 @@ __global__ __launch_bounds__(kBlock) void k_sell_split(SellArgs a) {
     const int ns = a.slots[c];
     const int64_t base = a.off[c];
     constexpr int64_t SV = slot_vals<T>() * kChunk;
-    const T* valp = static_cast<const T*>(a.val) + base * SV + rin;
-    const CT* colp;
-    if constexpr (sizeof(CT) == 2) colp = a.col16 + base * kChunk + rin;
-    else colp = a.col + base * kChunk + rin;
     double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+    if constexpr (std::is_same<CT, uint32_t>::value) {
+        // stencil-coded copy: lane group g takes the positions of its sub-mask (slots k = g mod 4)
+        (void)base;
+        (void)ns;
+        const T* valp = static_cast<const T*>(a.val) + a.coff[c] * SV + rin;
+        const uint32_t m = a.cm[c];
+        const int64_t nx = a.lstr[2 * sub], nxy = a.lstr[2 * sub + 1];
 #pragma unroll 2
-    for (int k = g; k < ns; k += 4)
-        block_fma_any<true>(valp + (int64_t)k * SV, a.x + 3 * col_of(colp[(int64_t)k * kChunk], row), s0, s1, s2, rin);
+        for (uint32_t mg = a.cmq[4 * c + g]; mg; mg &= mg - 1) {
+            const int q = __builtin_ctz(mg);
+            const int k = __popc(m & ((1u << q) - 1u));
+            block_fma_any<true>(valp + (int64_t)k * SV, a.x + 3 * stencil_col(row, q, nx, nxy, a.nlast), s0, s1, s2, rin);
+        }
+    } else {
+        const T* valp = static_cast<const T*>(a.val) + base * SV + rin;
+        const CT* colp;
+        if constexpr (sizeof(CT) == 2) colp = a.col16 + base * kChunk + rin;
+        else colp = a.col + base * kChunk + rin;
+#pragma unroll 2
+        for (int k = g; k < ns; k += 4)
+            block_fma_any<true>(valp + (int64_t)k * SV, a.x + 3 * col_of(colp[(int64_t)k * kChunk], row), s0, s1, s2, rin);
+    }
     s0 += __shfl_xor(s0, 16, 64);
     s1 += __shfl_xor(s1, 16, 64);
     s2 += __shfl_xor(s2, 16, 64);
@@ -474,6 +532,10 @@ struct GsArgs {
     double* partial;
     int xcd;  // 1: workgroups mapped so each XCD takes one contiguous run of the launch's chunks
     const float* minvc;  // chunk-ordered fp32 inverses (GsFine::minvc) or null: minv by row
+    const uint32_t* lm;  // stencil-coded chunks: L / U position masks, member strides, last node
+    const uint32_t* um;
+    const int32_t* lstr;
+    int64_t nlast;
 };
 
 template <int PH, bool DOT, typename T, typename CT, int V = 1>
@@ -490,17 +552,24 @@ __global__ __launch_bounds__(kBlock) void k_gs(GsArgs a) {
     const int64_t row = real ? rr : ~rr;  // pad lanes gather at a real row with zero blocks
     constexpr int64_t SV = slot_vals<T>() * kChunk;
     const T* val = static_cast<const T*>(a.val);
-    const CT* colp;
-    if constexpr (sizeof(CT) == 2) colp = a.col16;
-    else colp = a.col;
     double s0 = 0.0, s1 = 0.0, s2 = 0.0;
-    if (PH != 1) {
-        const int64_t o = a.offl[c];
-        sell_rows<V, T, CT>(colp + o * kChunk + lane, val + o * SV + lane, a.x, a.nsl[c], row, s0, s1, s2);
-    }
-    if (PH != 0) {
-        const int64_t o = a.offu[c];
-        sell_rows<V, T, CT>(colp + o * kChunk + lane, val + o * SV + lane, a.x, a.nsu[c], row, s0, s1, s2);
+    if constexpr (std::is_same<CT, uint32_t>::value) {
+        // stencil-coded colour chunks (GsFine::coded): the L and U position masks
+        const int64_t nx = a.lstr[2 * sub], nxy = a.lstr[2 * sub + 1];
+        if (PH != 1) sell_rows_coded<T>(a.lm[c], val + a.offl[c] * SV + lane, a.x, row, nx, nxy, a.nlast, s0, s1, s2);
+        if (PH != 0) sell_rows_coded<T>(a.um[c], val + a.offu[c] * SV + lane, a.x, row, nx, nxy, a.nlast, s0, s1, s2);
+    } else {
+        const CT* colp;
+        if constexpr (sizeof(CT) == 2) colp = a.col16;
+        else colp = a.col;
+        if (PH != 1) {
+            const int64_t o = a.offl[c];
+            sell_rows<V, T, CT>(colp + o * kChunk + lane, val + o * SV + lane, a.x, a.nsl[c], row, s0, s1, s2);
+        }
+        if (PH != 0) {
+            const int64_t o = a.offu[c];
+            sell_rows<V, T, CT>(colp + o * kChunk + lane, val + o * SV + lane, a.x, a.nsu[c], row, s0, s1, s2);
+        }
     }
     const int64_t o = 3 * row;
     double dotv = 0.0;
@@ -516,9 +585,10 @@ __global__ __launch_bounds__(kBlock) void k_gs(GsArgs a) {
         if (a.minvc) {
             const float* m = a.minvc + c * 9 * kChunk + lane;
             const double r0 = b0 - s0, r1 = b1 - s1, r2 = b2 - s2;
-            m0 = (double)m[0] * r0 + (double)m[kChunk] * r1 + (double)m[2 * kChunk] * r2;
-            m1 = (double)m[3 * kChunk] * r0 + (double)m[4 * kChunk] * r1 + (double)m[5 * kChunk] * r2;
-            m2 = (double)m[6 * kChunk] * r0 + (double)m[7 * kChunk] * r1 + (double)m[8 * kChunk] * r2;
+            // explicit contraction, as in block_fma_any (bit-identical across instantiations)
+            m0 = __builtin_fma((double)m[2 * kChunk], r2, __builtin_fma((double)m[kChunk], r1, (double)m[0] * r0));
+            m1 = __builtin_fma((double)m[5 * kChunk], r2, __builtin_fma((double)m[4 * kChunk], r1, (double)m[3 * kChunk] * r0));
+            m2 = __builtin_fma((double)m[8 * kChunk], r2, __builtin_fma((double)m[7 * kChunk], r1, (double)m[6 * kChunk] * r0));
         } else {
             apply_m<true>(static_cast<const SmoothInv<T>*>(a.minv), row, b0 - s0, b1 - s1, b2 - s2, m0, m1, m2);
         }
@@ -526,7 +596,7 @@ __global__ __launch_bounds__(kBlock) void k_gs(GsArgs a) {
             a.x[o] = m0;
             a.x[o + 1] = m1;
             a.x[o + 2] = m2;
-            if (DOT) dotv = b0 * m0 + b1 * m1 + b2 * m2;
+            if (DOT) dotv = __builtin_fma(b2, m2, __builtin_fma(b1, m1, b0 * m0));
         }
     }
     if (DOT) chunk_partial(dotv, a.partial, c);
@@ -1358,7 +1428,9 @@ MirrorBuf::~MirrorBuf() {
     if (host) (void)hipHostFree(host);
 }
 
-int64_t pace_until_done(hipStream_t stream, hipGraphExec_t graph, const MirrorBuf& m, int64_t k, int64_t launched) {
+int64_t pace_until_done(hipStream_t stream, hipGraphExec_t graph, const MirrorBuf& m, int64_t k, int64_t launched,
+                        hipGraphExec_t graph1, int64_t horizon) {
+    constexpr int64_t kRunway = 2;  // tail: single iterations kept this far ahead of the slowest member
     int64_t replays = 0;
     for (int64_t spin = 0;; ++spin) {
         bool all = true;
@@ -1369,10 +1441,12 @@ int64_t pace_until_done(hipStream_t stream, hipGraphExec_t graph, const MirrorBu
             slowest = std::min<int64_t>(slowest, __atomic_load_n(&m.host[s].iter, __ATOMIC_RELAXED));
         }
         if (all) return replays;
-        // keep one replay of runway: launch when the slowest solve has entered the last one
-        if (launched - slowest <= k) {
-            DDPCA_HIP(hipGraphLaunch(graph, stream));
-            launched += k;
+        // keep one replay of runway: launch when the slowest solve has entered the last one;
+        // past the expected iteration count, single iterations kRunway ahead
+        const bool tail = graph1 && launched + k > horizon;
+        if (tail ? launched - slowest <= kRunway : launched - slowest <= k) {
+            DDPCA_HIP(hipGraphLaunch(tail ? graph1 : graph, stream));
+            launched += tail ? 1 : k;
             ++replays;
             continue;
         }
@@ -1383,8 +1457,8 @@ int64_t pace_until_done(hipStream_t stream, hipGraphExec_t graph, const MirrorBu
                 bool done_now = true;
                 for (int s = 0; s < m.n; ++s) done_now &= __atomic_load_n(&m.host[s].done, __ATOMIC_ACQUIRE) != 0;
                 if (done_now) return replays;
-                DDPCA_HIP(hipGraphLaunch(graph, stream));
-                launched += k;
+                DDPCA_HIP(hipGraphLaunch(tail ? graph1 : graph, stream));
+                launched += tail ? 1 : k;
                 ++replays;
             } else if (q != hipErrorNotReady) {
                 DDPCA_HIP(q);
@@ -1502,10 +1576,82 @@ bool lattice_transfer(LevelDev& L, const LevelDev& C, const std::vector<int32_t>
     return true;
 }
 
+// Stencil position (0..26, (dz+1) 9 + (dy+1) 3 + (dx+1)) of the column offset d on a lattice
+// with strides nx >= 3, nxy >= 3 nx, or -1
+int stencil_code(int64_t d, int64_t nx, int64_t nxy) {
+    auto rdiv = [](int64_t a, int64_t b) { return a >= 0 ? (a + b / 2) / b : -((-a + b / 2) / b); };
+    const int64_t dz = rdiv(d, nxy), r = d - dz * nxy, dy = rdiv(r, nx), dx = r - dy * nx;
+    if (dz < -1 || dz > 1 || dy < -1 || dy > 1 || dx < -1 || dx > 1) return -1;
+    return (int)((dz + 1) * 9 + (dy + 1) * 3 + (dx + 1));
+}
+
+// DDPCA_CODED=1 (or 2) builds the stencil-coded V-cycle copies (read at create).  Opt-in: per
+// launch the coded colour sweeps and level sweeps ran 2-6 % shorter, yet the headline lost 2.5 %
+// (16.78 vs 17.22 ADMM it/s alternating in one call, profiles/r03r; 2: the level copies alone,
+// 17.05 vs 17.15, r03t)
+bool coded_wanted() {
+    const char* e = std::getenv("DDPCA_CODED");
+    return e && std::atoi(e) != 0;
+}
+
+// Box-lattice strides (nx, nx ny) of every member of a level from its device-ordered host SELL
+// arrays, or empty when the level is not a lattice: nx, nxy from a row with 26 neighbours (its
+// positive offsets 1, nx-1, nx, nx+1, nxy-nx-1, ...), then every block of every row must sit at
+// a stencil offset of its member, a position repeated within a row (the padding slots repeat the
+// row's own column) only with zero values.  The generators' boxes and their lexicographic device
+// numbering pass; general meshes keep the column-indexed copy.
+std::vector<int32_t> lattice_strides(const LevelDev& L, const std::vector<int32_t>& csub, const std::vector<int64_t>& off,
+                                     const std::vector<int32_t>& col, const std::vector<double>& val) {
+    const int ns = (int)L.noff.size();
+    std::vector<int32_t> st(2 * ns, 0);
+    for (int s = 0; s < ns; ++s) {
+        int64_t nx = 0, nxy = 0;
+        std::vector<int64_t> d;
+        for (int64_t g = L.noff[s]; g < L.noff[s] + L.nloc[s] && nx == 0; ++g) {
+            const int64_t c = g / kChunk, lane = g % kChunk;
+            d.clear();
+            for (int64_t q = off[c]; q < off[c + 1]; ++q) {
+                const int64_t j = col[q * kChunk + lane];
+                if (j > g) d.push_back(j - g);
+            }
+            std::sort(d.begin(), d.end());
+            d.erase(std::unique(d.begin(), d.end()), d.end());
+            if (d.size() != 13 || d[0] != 1) continue;
+            const int64_t ax = d[2], axy = d[4] + d[2] + 1;
+            if (d[1] == ax - 1 && d[3] == ax + 1 && d[5] == axy - ax && d[8] == axy && d[12] == axy + ax + 1) {
+                nx = ax;
+                nxy = axy;
+            }
+        }
+        if (nx < 3 || nxy < 3 * nx || nxy > INT32_MAX) return {};
+        st[2 * s] = (int32_t)nx;
+        st[2 * s + 1] = (int32_t)nxy;
+    }
+    int bad = 0;
+#pragma omp parallel for schedule(static) reduction(| : bad)
+    for (int64_t c = 0; c < L.nch; ++c) {
+        const int s = csub[c];
+        for (int64_t lane = 0; lane < kChunk; ++lane) {
+            const int64_t g = c * kChunk + lane;
+            uint32_t seen = 0;
+            for (int64_t q = off[c]; q < off[c + 1]; ++q) {
+                const int code = stencil_code((int64_t)col[q * kChunk + lane] - g, st[2 * s], st[2 * s + 1]);
+                if (code < 0) { bad = 1; break; }
+                if ((seen >> code) & 1u)
+                    for (int ij = 0; ij < 9; ++ij) bad |= val[(q * 9 + ij) * kChunk + lane] != 0.0;
+                seen |= 1u << code;
+            }
+        }
+    }
+    if (bad) return {};
+    return st;
+}
+
 // The fine level's colour structure (GsFine) from its host SELL arrays (col: batch device
-// columns, val: masked fp64 blocks val[(q * 9 + ij) * 64 + lane]); vt: the V-cycle copy's type.
+// columns, val: masked fp64 blocks val[(q * 9 + ij) * 64 + lane]); vt: the V-cycle copy's type;
+// lstr: the level's lattice strides (empty: not a lattice -- column-indexed colour chunks).
 void build_gs(GsFine& G, const LevelDev& L, int nsub, const std::vector<int64_t>& off, const std::vector<int32_t>& col,
-              const std::vector<double>& val, int vt) {
+              const std::vector<double>& val, int vt, const std::vector<int32_t>& lstr) {
     // greedy colouring in device order, per member
     std::vector<int8_t> colour(L.nn, -1);
     std::vector<int> ncol_sub(nsub, 0);
@@ -1576,12 +1722,13 @@ void build_gs(GsFine& G, const LevelDev& L, int nsub, const std::vector<int64_t>
     }
     std::vector<int32_t> rowidx, csub, nsl, nsu;
     std::vector<int64_t> offl, offu, cb(nsub + 1, 0);
+    std::vector<uint32_t> lmk, umk;  // stencil positions of each chunk's L and U blocks (lattice levels)
     std::vector<std::vector<int32_t>> bycol(K);
     std::vector<int64_t> base;  // first row of each chunk in its (s, k) list
     std::vector<size_t> lists;
     G.nnzb_sub.assign(nsub, 0);
     G.slots_sub.assign(nsub, 0);
-    int64_t nslot = 0;
+    bool coded = !lstr.empty();
     for (int s = 0; s < nsub; ++s) {
         cb[s] = (int64_t)csub.size();
         for (int k = 0; k < K; ++k) {
@@ -1593,33 +1740,50 @@ void build_gs(GsFine& G, const LevelDev& L, int nsub, const std::vector<int64_t>
                 base.push_back((int64_t)r0);
                 lists.push_back((size_t)s * K + k);
                 int32_t ml = 0, mu = 0;
+                uint32_t lmask = 0, umask = 0;
                 for (size_t i = r0; i < std::min(R.size(), r0 + kChunk); ++i) {
                     const int64_t g = R[i], nc = g / kChunk, lane = g % kChunk;
                     int32_t nl = 0, nu = 0;
                     for (int64_t q = off[nc]; q < off[nc + 1]; ++q) {
                         const int64_t j = col[q * kChunk + lane];
                         if (j == g) continue;
-                        if (colour[j] < k) ++nl;
+                        const bool lower = colour[j] < k;
+                        if (lower) ++nl;
                         else ++nu;
+                        if (coded) {
+                            const int code = stencil_code(j - g, lstr[2 * s], lstr[2 * s + 1]);
+                            (lower ? lmask : umask) |= 1u << code;
+                        }
                     }
                     ml = std::max(ml, nl);
                     mu = std::max(mu, nu);
                     G.nnzb_sub[s] += nl + nu;
                 }
+                coded = coded && (lmask & umask) == 0;
                 nsl.push_back(ml);
                 nsu.push_back(mu);
-                offl.push_back(nslot);
-                offu.push_back(nslot + ml);
-                nslot += ml + mu;
-                G.slots_sub[s] += ml + mu;
+                lmk.push_back(lmask);
+                umk.push_back(umask);
             }
         }
     }
     const int64_t nch = (int64_t)csub.size();
     cb[nsub] = nch;
+    // slots per chunk: the longest row's L and U counts, or (coded) one per stencil position
+    int64_t nslot = 0;
+    for (int64_t c = 0; c < nch; ++c) {
+        if (coded) {
+            nsl[c] = __builtin_popcount(lmk[c]);
+            nsu[c] = __builtin_popcount(umk[c]);
+        }
+        offl.push_back(nslot);
+        offu.push_back(nslot + nsl[c]);
+        nslot += nsl[c] + nsu[c];
+        G.slots_sub[csub[c]] += nsl[c] + nsu[c];
+    }
     rowidx.assign(nch * kChunk, 0);
-    const bool c16 = L.col16.p != nullptr;
-    std::vector<int32_t> gcol(c16 ? 0 : std::max<int64_t>(nslot * kChunk, 1), 0);
+    const bool c16 = !coded && L.col16.p != nullptr;
+    std::vector<int32_t> gcol(c16 || coded ? 0 : std::max<int64_t>(nslot * kChunk, 1), 0);
     std::vector<int16_t> gcol16(c16 ? std::max<int64_t>(nslot * kChunk, 1) : 0, 0);
     const int nv = vt == kValH16 ? 10 : 9;
     std::vector<uint16_t> v16(vt == kValH16 ? std::max<int64_t>(nslot * nv * kChunk, 1) : 0, 0);
@@ -1635,19 +1799,28 @@ void build_gs(GsFine& G, const LevelDev& L, int nsub, const std::vector<int64_t>
             const int64_t g = real ? R[r0 + lane] : R[r0];
             rowidx[c * kChunk + lane] = real ? (int32_t)g : ~(int32_t)g;
             // pad slots: the row itself (offset 0), zero blocks
-            for (int64_t q = offl[c]; q < offl[c] + nsl[c] + nsu[c]; ++q) {
+            for (int64_t q = offl[c]; q < offl[c] + nsl[c] + nsu[c] && !coded; ++q) {
                 if (c16) gcol16[q * kChunk + lane] = 0;
                 else gcol[q * kChunk + lane] = (int32_t)g;
             }
             if (!real) continue;
             const int64_t nc = g / kChunk, nl = g % kChunk;
+            const int s = csub[c];
             int64_t ql = offl[c], qu = offu[c];
             for (int64_t q = off[nc]; q < off[nc + 1]; ++q) {
                 const int64_t j = col[q * kChunk + nl];
                 if (j == g) continue;
-                const int64_t t = colour[j] < k ? ql++ : qu++;
+                const bool lower = colour[j] < k;
+                int64_t t;
+                if (coded) {
+                    // the rank of the block's stencil position among the chunk's L (U) positions
+                    const uint32_t below = (1u << stencil_code(j - g, lstr[2 * s], lstr[2 * s + 1])) - 1u;
+                    t = lower ? offl[c] + __builtin_popcount(lmk[c] & below) : offu[c] + __builtin_popcount(umk[c] & below);
+                } else {
+                    t = lower ? ql++ : qu++;
+                }
                 if (c16) gcol16[t * kChunk + lane] = (int16_t)(j - g);
-                else gcol[t * kChunk + lane] = (int32_t)j;
+                else if (!coded) gcol[t * kChunk + lane] = (int32_t)j;
                 double blk[9];
                 for (int ij = 0; ij < 9; ++ij) blk[ij] = val[(q * 9 + ij) * kChunk + nl];
                 if (vt == kValH16) {
@@ -1692,14 +1865,18 @@ void build_gs(GsFine& G, const LevelDev& L, int nsub, const std::vector<int64_t>
     G.offl.upload(offl);
     G.offu.upload(offu);
     G.cb.upload(cb);
-    if (c16) G.col16.upload(gcol16);
+    G.coded = coded;
+    if (coded) {
+        G.lm.upload(lmk);
+        G.um.upload(umk);
+    } else if (c16) G.col16.upload(gcol16);
     else G.col.upload(gcol);
     if (vt == kValH16) G.val16.upload(v16);
     else if (vt == kVal32) G.val32.upload(v32);
     else G.val64.upload(v64);
     if (std::getenv("DDPCA_VERBOSE"))
-        std::fprintf(stderr, "[ddpca] fine level: multicolour Gauss-Seidel, %d colours, %lld chunks, %lld slots, %d of %d members tiled\n",
-                     K, (long long)nch, (long long)nslot, tiled, nsub);
+        std::fprintf(stderr, "[ddpca] fine level: multicolour Gauss-Seidel, %d colours, %lld chunks, %lld slots, %d of %d members tiled, stencil-coded %d\n",
+                     K, (long long)nch, (long long)nslot, tiled, nsub, (int)coded);
 }
 }  // namespace
 
@@ -1870,6 +2047,58 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
         // dense inverse).  Table-mode levels need neither.
         const bool vc32 = opt.precond_fp32 != 0 && nlev > 1;
         const int64_t nslot = L.nslots;
+        // stencil-coded V-cycle copy on box-lattice levels (its own val16 / val32 array)
+        std::vector<int32_t> lstr_h;
+        if (!L.tbl && vc32 && l >= 1 && coded_wanted()) lstr_h = lattice_strides(L, csub, off, col, val);
+        std::vector<int64_t> coff_h;
+        std::vector<uint32_t> cm_h;
+        if (!lstr_h.empty()) {
+            cm_h.assign(L.nch, 0u);
+            coff_h.assign(L.nch + 1, 0);
+            std::vector<uint32_t> cmq_h(4 * L.nch, 0u);
+#pragma omp parallel for schedule(static)
+            for (int64_t c = 0; c < L.nch; ++c) {
+                const int s = csub[c];
+                uint32_t m = 0;
+                for (int64_t lane = 0; lane < kChunk; ++lane)
+                    for (int64_t q = off[c]; q < off[c + 1]; ++q)
+                        m |= 1u << stencil_code((int64_t)col[q * kChunk + lane] - (c * kChunk + lane), lstr_h[2 * s],
+                                                lstr_h[2 * s + 1]);
+                cm_h[c] = m;
+                int k = 0;
+                for (uint32_t r = m; r; r &= r - 1, ++k) cmq_h[4 * c + (k & 3)] |= r & (~r + 1u);
+            }
+            for (int64_t c = 0; c < L.nch; ++c) coff_h[c + 1] = coff_h[c] + __builtin_popcount(cm_h[c]);
+            L.coded = true;
+            L.ncslots = coff_h[L.nch];
+            L.lstr.upload(lstr_h);
+            L.cm.upload(cm_h);
+            L.cmq.upload(cmq_h);
+            L.coff.upload(coff_h);
+        }
+        // destination slot of every (sorted slot, lane) in the V-cycle copy: itself, or (coded) the
+        // rank of its stencil position in the chunk's mask, -1 for a repeated position (padding)
+        auto for_vc_slots = [&](auto&& put) {
+#pragma omp parallel for schedule(static)
+            for (int64_t c = 0; c < L.nch; ++c) {
+                const int s = csub[c];
+                for (int64_t lane = 0; lane < kChunk; ++lane) {
+                    uint32_t seen = 0;
+                    for (int64_t q = off[c]; q < off[c + 1]; ++q) {
+                        int64_t dst = q;
+                        if (L.coded) {
+                            const int code = stencil_code((int64_t)col[q * kChunk + lane] - (c * kChunk + lane),
+                                                          lstr_h[2 * s], lstr_h[2 * s + 1]);
+                            if ((seen >> code) & 1u) continue;
+                            seen |= 1u << code;
+                            dst = coff_h[c] + __builtin_popcount(cm_h[c] & ((1u << code) - 1u));
+                        }
+                        put(q, dst, lane);
+                    }
+                }
+            }
+        };
+        const int64_t vc_nslot = L.coded ? L.ncslots : nslot;
         if (!L.tbl && (l == nlev - 1 || !vc32)) {
             std::vector<double> v64(val.size());
 #pragma omp parallel for schedule(static)
@@ -1884,24 +2113,21 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
         if (!L.tbl && vc32 && l >= 1 && l >= nlev - h16_levels && opt.precond_fp32 == 2) {
             // block-exponent fp16 copy of the fine level for the smoother and the V-cycle
             // residual (symmetric: a block and its transpose round alike); coarser levels fp32
-            std::vector<uint16_t> v16((size_t)nslot * 10 * kChunk);
-#pragma omp parallel for schedule(static)
-            for (int64_t q = 0; q < nslot; ++q)
-                for (int64_t lane = 0; lane < kChunk; ++lane) {
-                    double blk[9];
-                    uint16_t rec[10];
-                    for (int ij = 0; ij < 9; ++ij) blk[ij] = val[(q * 9 + ij) * kChunk + lane];
-                    to_h16_block(blk, rec);
-                    for (int k = 0; k < 10; ++k) v16[q * 10 * kChunk + 128 * (k / 2) + 2 * lane + k % 2] = rec[k];
-                }
+            std::vector<uint16_t> v16((size_t)vc_nslot * 10 * kChunk, 0);  // zero blocks: e = 0, values 0
+            for_vc_slots([&](int64_t q, int64_t dst, int64_t lane) {
+                double blk[9];
+                uint16_t rec[10];
+                for (int ij = 0; ij < 9; ++ij) blk[ij] = val[(q * 9 + ij) * kChunk + lane];
+                to_h16_block(blk, rec);
+                for (int k = 0; k < 10; ++k) v16[dst * 10 * kChunk + 128 * (k / 2) + 2 * lane + k % 2] = rec[k];
+            });
             L.val16.upload(v16);
         } else if (!L.tbl && vc32 && l >= 1) {
-            std::vector<float> v32(val.size());
-#pragma omp parallel for schedule(static)
-            for (int64_t q = 0; q < nslot; ++q)
+            std::vector<float> v32((size_t)vc_nslot * 9 * kChunk, 0.0f);
+            for_vc_slots([&](int64_t q, int64_t dst, int64_t lane) {
                 for (int ij = 0; ij < 9; ++ij)
-                    for (int64_t lane = 0; lane < kChunk; ++lane)
-                        v32[q * 9 * kChunk + slot_elem<float>(ij, lane)] = (float)val[(q * 9 + ij) * kChunk + lane];
+                    v32[dst * 9 * kChunk + slot_elem<float>(ij, lane)] = (float)val[(q * 9 + ij) * kChunk + lane];
+            });
             L.val32.upload(v32);
         }
         L.dinv.upload(dinv);
@@ -1922,7 +2148,9 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
         if (l == nlev - 1 && nlev > 1 && opt.smoother == 3) {
             // the V-cycle copy's storage type of this level (vc_type once the level is up)
             const int vt = (!vc32 || L.tbl) ? kVal64 : L.val16.p ? kValH16 : kVal32;
-            build_gs(gs, L, nsub, off, col, val, vt);
+            // (DDPCA_CODED=2: coded level copies, column-indexed colour chunks -- diagnostics)
+            const char* ec = std::getenv("DDPCA_CODED");
+            build_gs(gs, L, nsub, off, col, val, vt, ec && std::atoi(ec) == 2 ? std::vector<int32_t>{} : lstr_h);
         }
         L.mask.upload(mask);
         for (auto* v : {&L.x, &L.t, &L.b, &L.r, &L.d}) {
@@ -2223,11 +2451,13 @@ MgpisDevice::~MgpisDevice() {
     (void)hipSetDevice(device);
     if (stream) (void)hipStreamSynchronize(stream);
     if (stream2_) (void)hipStreamSynchronize(stream2_);
-    for (auto& g : graph_)
-        if (g) (void)hipGraphExecDestroy(g);
-    for (auto& gp : graph_h_)
-        for (auto& g : gp)
-            if (g) (void)hipGraphExecDestroy(g);
+    for (auto* ga : {graph_, graph1_})
+        for (int p = 0; p < 2; ++p)
+            if (ga[p]) (void)hipGraphExecDestroy(ga[p]);
+    for (auto* gh : {graph_h_, graph1_h_})
+        for (int p = 0; p < 2; ++p)
+            for (int h = 0; h < 2; ++h)
+                if (gh[p][h]) (void)hipGraphExecDestroy(gh[p][h]);
     if (ev_fork_) (void)hipEventDestroy(ev_fork_);
     if (ev_join_) (void)hipEventDestroy(ev_join_);
     if (stream2_) (void)hipStreamDestroy(stream2_);
@@ -2316,13 +2546,19 @@ void launch_sell(int vt, const SellArgs& a, hipStream_t s) {
     const int grid = ceil_div(a.nch, 4);
     constexpr int V = default_variant(MODE);
     using I16 = int16_t;
+    using U32 = uint32_t;  // column type tag of the stencil-coded copy
     // small levels: the row-split kernel (DDPCA_SPLIT_CHUNKS = the largest level it takes, in chunks)
-    static const int64_t split_max = std::getenv("DDPCA_SPLIT_CHUNKS") ? std::atoll(std::getenv("DDPCA_SPLIT_CHUNKS")) : 2048;
+    // (read per launch: launches are captured into graphs once per handle, and tests switch it)
+    const char* esp = std::getenv("DDPCA_SPLIT_CHUNKS");
+    const int64_t split_max = esp ? std::atoll(esp) : 2048;
     // (V-cycle modes only: y = Kx keeps the slot order the table mode reproduces bit for bit)
     if constexpr (!DOT && (MODE == kResid || MODE == kJac)) {
         if (!a.tab && a.nch <= split_max) {
             const dim3 gs((unsigned)a.nch);
-            if (a.col16) {
+            if (a.cm) {
+                if (vt == kValH16) hipLaunchKernelGGL((k_sell_split<MODE, BJ, uint16_t, U32>), gs, dim3(kBlock), 0, s, a);
+                else hipLaunchKernelGGL((k_sell_split<MODE, BJ, float, U32>), gs, dim3(kBlock), 0, s, a);
+            } else if (a.col16) {
                 if (vt == kValH16) hipLaunchKernelGGL((k_sell_split<MODE, BJ, uint16_t, I16>), gs, dim3(kBlock), 0, s, a);
                 else if (vt == kVal32) hipLaunchKernelGGL((k_sell_split<MODE, BJ, float, I16>), gs, dim3(kBlock), 0, s, a);
                 else hipLaunchKernelGGL((k_sell_split<MODE, BJ, double, I16>), gs, dim3(kBlock), 0, s, a);
@@ -2333,7 +2569,10 @@ void launch_sell(int vt, const SellArgs& a, hipStream_t s) {
         }
     }
     if (a.tab) hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, double, V, true>), dim3(grid), dim3(kBlock), 0, s, a, a.tab);
-    else if (a.col16) {
+    else if (a.cm) {
+        if (vt == kValH16) hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, uint16_t, V, false, U32>), dim3(grid), dim3(kBlock), 0, s, a, a.tab);
+        else hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, float, V, false, U32>), dim3(grid), dim3(kBlock), 0, s, a, a.tab);
+    } else if (a.col16) {
         if (vt == kValH16) hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, uint16_t, V, false, I16>), dim3(grid), dim3(kBlock), 0, s, a, a.tab);
         else if (vt == kVal32) hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, float, V, false, I16>), dim3(grid), dim3(kBlock), 0, s, a, a.tab);
         else hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, double, V, false, I16>), dim3(grid), dim3(kBlock), 0, s, a, a.tab);
@@ -2376,9 +2615,17 @@ namespace {
 SellArgs vc_level_args(const MgpisDevice& D, int level) {
     SellArgs a = level_args(D.lev[level]);
     const int vt = D.vc_type(level);
-    if (vt == kValH16) a.val = D.lev[level].val16.p;
-    else if (vt == kVal32) a.val = D.lev[level].val32.p;
-    if (vt != kVal64) a.minv = D.lev[level].minv32.p;
+    const LevelDev& L = D.lev[level];
+    if (vt == kValH16) a.val = L.val16.p;
+    else if (vt == kVal32) a.val = L.val32.p;
+    if (vt != kVal64) a.minv = L.minv32.p;
+    if (vt != kVal64 && L.coded) {
+        a.cm = L.cm.p;
+        a.cmq = L.cmq.p;
+        a.coff = L.coff.p;
+        a.lstr = L.lstr.p;
+        a.nlast = L.nn - 1;
+    }
     return a;
 }
 }  // namespace
@@ -2517,7 +2764,7 @@ bool MgpisDevice::fuse_jac0() const {
 namespace {
 // one k_gs launch: phase ph over colour k's chunks (k < 0: every chunk)
 template <int PH, bool DOT, typename T>
-void launch_gs_t(const GsArgs& a, bool c16, hipStream_t st) {
+void launch_gs_t(const GsArgs& a, int ct, hipStream_t st) {  // ct: 0 int32 columns, 1 16-bit offsets, 2 stencil-coded
     // workgroup of one wave (default) or four (DDPCA_GS_BLOCK=256): one-wave groups spread a
     // colour's chunks over more CUs (+1 % at 8 subdomains, profiles/r03j)
     const char* eb = std::getenv("DDPCA_GS_BLOCK");
@@ -2527,7 +2774,8 @@ void launch_gs_t(const GsArgs& a, bool c16, hipStream_t st) {
     // ahead (DDPCA_GS_LOOP, read at graph capture; measured equal, profiles/r03i)
     const char* e = std::getenv("DDPCA_GS_LOOP");
     const int v = e ? std::atoi(e) : 1;
-    if (c16) {
+    if (ct == 2) hipLaunchKernelGGL((k_gs<PH, DOT, T, uint32_t, 1>), grid, dim3(bs), 0, st, a);
+    else if (ct == 1) {
         if (v == 2) hipLaunchKernelGGL((k_gs<PH, DOT, T, int16_t, 2>), grid, dim3(bs), 0, st, a);
         else hipLaunchKernelGGL((k_gs<PH, DOT, T, int16_t, 1>), grid, dim3(bs), 0, st, a);
     } else if (v == 2) hipLaunchKernelGGL((k_gs<PH, DOT, T, int32_t, 2>), grid, dim3(bs), 0, st, a);
@@ -2561,19 +2809,25 @@ void launch_gs(const MgpisDevice& D, int k, double* x, const double* b, double* 
     // chunk-ordered inverses (DDPCA_GS_MINVC=0: by row)
     const char* em = std::getenv("DDPCA_GS_MINVC");
     a.minvc = (em && std::atoi(em) == 0) ? nullptr : G.minvc.p;
-    const bool c16 = G.col16.p != nullptr;
+    const int ct = G.coded ? 2 : G.col16.p != nullptr ? 1 : 0;
+    if (G.coded) {
+        a.lm = G.lm.p;
+        a.um = G.um.p;
+        a.lstr = F.lstr.p;
+        a.nlast = F.nn - 1;
+    }
     if (G.val16.p) {
         a.val = G.val16.p;
         a.minv = F.minv32.p;
-        launch_gs_t<PH, DOT, uint16_t>(a, c16, D.stream);
+        launch_gs_t<PH, DOT, uint16_t>(a, ct, D.stream);
     } else if (G.val32.p) {
         a.val = G.val32.p;
         a.minv = F.minv32.p;
-        launch_gs_t<PH, DOT, float>(a, c16, D.stream);
+        launch_gs_t<PH, DOT, float>(a, ct, D.stream);
     } else {
         a.val = G.val64.p;
         a.minv = F.minv.p;
-        launch_gs_t<PH, DOT, double>(a, c16, D.stream);
+        launch_gs_t<PH, DOT, double>(a, ct, D.stream);
     }
 }
 }  // namespace
@@ -2765,7 +3019,9 @@ void MgpisDevice::vcycle_bytes(int s, double out[2]) const {
     auto mat = [&](int l) {  // one pass over the V-cycle's copy of level l
         const LevelDev& L = lev[l];
         if (L.tbl) return 4.0 * (double)L.nnzb_sub[s] + 4.0 * n(l);
-        return (vbytes(vc_type(l)) + (L.col16.p ? 2.0 : 4.0)) * (double)L.nnzb_sub[s];
+        // stencil-coded copies read no column indices (their zero blocks are not counted)
+        const double cb = (L.coded && vc_type(l) != kVal64) ? 0.0 : L.col16.p ? 2.0 : 4.0;
+        return (vbytes(vc_type(l)) + cb) * (double)L.nnzb_sub[s];
     };
     auto minv = [&](int l) { return (bj ? 9.0 : 3.0) * (vc_type(l) != kVal64 ? 4.0 : 8.0); };
     auto put = [&](int l, double b) { out[l == Lf ? 0 : 1] += b; };
@@ -2783,7 +3039,7 @@ void MgpisDevice::vcycle_bytes(int s, double out[2]) const {
     // the colours it reads (forward colour k: the k earlier ones, residual: the later ones,
     // backward: all others), and per row b, M^-1, the row index and x (or r) written
     const double K = gsf ? (double)gs.ncol : 0.0;
-    const double gsmat = gsf ? (vbytes(vc_type(Lf)) + (gs.col16.p ? 2.0 : 4.0)) * (double)gs.nnzb_sub[s] : 0.0;
+    const double gsmat = gsf ? (vbytes(vc_type(Lf)) + (gs.coded ? 0.0 : gs.col16.p ? 2.0 : 4.0)) * (double)gs.nnzb_sub[s] : 0.0;
     if (gsf) {
         put(Lf, gsmat + n(Lf) * (24.0 + minv(Lf) + 24.0 + 4.0 + 24.0 * (K - 1.0) / 2.0));  // forward
         put(Lf, n(Lf) * (24.0 + 4.0 + 24.0 * (K - 1.0) / 2.0));                              // residual
@@ -2891,7 +3147,20 @@ void MgpisDevice::enqueue_iteration(int prec, bool timed) {
                mirror.dev);
 }
 
-// graph_[prec]: iters_per_graph PCG iterations captured once and replayed.
+// graph_[prec]: iters_per_graph PCG iterations captured once and replayed; graph1_[prec]: one.
+hipGraphExec_t MgpisDevice::capture_iterations(int prec, int count, PcgScal* scp) {
+    sc_cur_ = scp;
+    hipGraph_t g;
+    hipGraphExec_t ge = nullptr;
+    DDPCA_HIP(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
+    for (int k = 0; k < count; ++k) enqueue_iteration(prec, false);
+    DDPCA_HIP(hipStreamEndCapture(stream, &g));
+    sc_cur_ = nullptr;
+    DDPCA_HIP(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+    DDPCA_HIP(hipGraphDestroy(g));
+    return ge;
+}
+
 void MgpisDevice::build_graph(int prec) {
     if (split_) {
         build_half_graph(prec, 0);
@@ -2899,26 +3168,29 @@ void MgpisDevice::build_graph(int prec) {
         return;
     }
     if (graph_[prec]) return;
-    hipGraph_t g;
-    DDPCA_HIP(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
-    for (int k = 0; k < opt.iters_per_graph; ++k) enqueue_iteration(prec, false);
-    DDPCA_HIP(hipStreamEndCapture(stream, &g));
-    DDPCA_HIP(hipGraphInstantiate(&graph_[prec], g, nullptr, nullptr, 0));
-    DDPCA_HIP(hipGraphDestroy(g));
+    graph_[prec] = capture_iterations(prec, opt.iters_per_graph, nullptr);
+    if (opt.iters_per_graph > 1) graph1_[prec] = capture_iterations(prec, 1, nullptr);
 }
 
 // the same iterations bound to half h's copy of the scalars (captured on `stream`, replayed on
 // the half's own stream)
 void MgpisDevice::build_half_graph(int prec, int h) {
     if (graph_h_[prec][h]) return;
-    sc_cur_ = sc_half_.p + (int64_t)h * nsub;
-    hipGraph_t g;
-    DDPCA_HIP(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
-    for (int k = 0; k < opt.iters_per_graph; ++k) enqueue_iteration(prec, false);
-    DDPCA_HIP(hipStreamEndCapture(stream, &g));
-    sc_cur_ = nullptr;
-    DDPCA_HIP(hipGraphInstantiate(&graph_h_[prec][h], g, nullptr, nullptr, 0));
-    DDPCA_HIP(hipGraphDestroy(g));
+    graph_h_[prec][h] = capture_iterations(prec, opt.iters_per_graph, sc_half_.p + (int64_t)h * nsub);
+    if (opt.iters_per_graph > 1) graph1_h_[prec][h] = capture_iterations(prec, 1, sc_half_.p + (int64_t)h * nsub);
+}
+
+int64_t MgpisDevice::horizon(int prec, int half) const {
+    // DDPCA_TAIL_PACING=0: whole replays to the end (A/B)
+    const char* e = std::getenv("DDPCA_TAIL_PACING");
+    if ((e && std::atoi(e) == 0) || (int)expect_[prec].size() != nsub) return INT64_MAX;
+    int64_t h = 0;
+    for (int s = 0; s < nsub; ++s) {
+        if (half >= 0 && half_host_[s] != half) continue;
+        if (expect_[prec][s] <= 0) return INT64_MAX;
+        h = std::max(h, expect_[prec][s]);
+    }
+    return h;
 }
 
 // scs[h][s] = sc[s], with done forced on the members of the other half
@@ -2967,7 +3239,8 @@ void MgpisDevice::set_split(bool on) {
 // Host pacing of the two halves' replays (pace_until_done per half, one loop): a half gets its
 // next replay when its slowest member has entered the last one enqueued for it.
 int64_t pace_halves(hipStream_t st[2], hipGraphExec_t g[2], const MirrorBuf& m, const std::vector<int>& half, int64_t k,
-                    int64_t launched0) {
+                    int64_t launched0, hipGraphExec_t* g1, const int64_t* horizon) {
+    constexpr int64_t kRunway = 2;
     int64_t launched[2] = {launched0, launched0}, replays = 0;
     for (int64_t spin = 0;; ++spin) {
         bool all = true;
@@ -2981,13 +3254,16 @@ int64_t pace_halves(hipStream_t st[2], hipGraphExec_t g[2], const MirrorBuf& m, 
         }
         if (all) return replays;
         bool launched_now = false;
-        for (int h = 0; h < 2; ++h)
-            if (busy[h] && launched[h] - slowest[h] <= k) {
-                DDPCA_HIP(hipGraphLaunch(g[h], st[h]));
-                launched[h] += k;
+        bool tail[2];
+        for (int h = 0; h < 2; ++h) {
+            tail[h] = g1 && horizon && g1[h] && launched[h] + k > horizon[h];
+            if (busy[h] && (tail[h] ? launched[h] - slowest[h] <= kRunway : launched[h] - slowest[h] <= k)) {
+                DDPCA_HIP(hipGraphLaunch(tail[h] ? g1[h] : g[h], st[h]));
+                launched[h] += tail[h] ? 1 : k;
                 ++replays;
                 launched_now = true;
             }
+        }
         if (launched_now) continue;
         if ((spin & 255) == 255) {
             for (int h = 0; h < 2; ++h) {
@@ -2999,8 +3275,8 @@ int64_t pace_halves(hipStream_t st[2], hipGraphExec_t g[2], const MirrorBuf& m, 
                     for (int s = 0; s < m.n; ++s)
                         if (half[s] == h) done_now &= __atomic_load_n(&m.host[s].done, __ATOMIC_ACQUIRE) != 0;
                     if (!done_now) {
-                        DDPCA_HIP(hipGraphLaunch(g[h], st[h]));
-                        launched[h] += k;
+                        DDPCA_HIP(hipGraphLaunch(tail[h] ? g1[h] : g[h], st[h]));
+                        launched[h] += tail[h] ? 1 : k;
                         ++replays;
                     }
                 } else if (q != hipErrorNotReady) {
@@ -3014,6 +3290,7 @@ int64_t pace_halves(hipStream_t st[2], hipGraphExec_t g[2], const MirrorBuf& m, 
 
 void MgpisDevice::pcg_begin(int prec, double rtol, const std::vector<int64_t>& maxit, bool warm) {
     select_device(device);
+    last_prec_ = prec;
     solve_accounted_ = prec != 1 || warm;  // the byte model covers the V-cycle PCG from x0 = 0
     if ((int)maxit.size() != nsub) throw ApiError(DDPCA_EINVAL, "maxit per subdomain");
     build_graph(prec);
@@ -3077,14 +3354,16 @@ void MgpisDevice::pcg_wait(int prec, int64_t pre_enqueued) {
     if (split_) {
         hipStream_t st[2] = {stream, stream2_};
         hipGraphExec_t g[2] = {graph_h_[prec][0], graph_h_[prec][1]};
-        graphs_launched += pace_halves(st, g, mirror, half_host_, k, launched);
+        hipGraphExec_t g1[2] = {graph1_h_[prec][0], graph1_h_[prec][1]};
+        const int64_t hz[2] = {horizon(prec, 0), horizon(prec, 1)};
+        graphs_launched += pace_halves(st, g, mirror, half_host_, k, launched, g1, hz);
         // join: `stream` continues after the second half's replays; the scalars merge back
         DDPCA_HIP(hipEventRecord(ev_join_, stream2_));
         DDPCA_HIP(hipStreamWaitEvent(stream, ev_join_, 0));
         hipLaunchKernelGGL(k_merge_sc, dim3(ceil_div(nsub, 64)), dim3(64), 0, stream, sc.p, sc_half_.p, half_.p, nsub);
         return;
     }
-    graphs_launched += pace_until_done(stream, graph_[prec], mirror, k, launched);
+    graphs_launched += pace_until_done(stream, graph_[prec], mirror, k, launched, graph1_[prec], horizon(prec, -1));
 }
 
 void MgpisDevice::pcg_fetch() {
@@ -3114,6 +3393,12 @@ void MgpisDevice::pcg_check() {
     }
     for (int s = 0; s < nsub; ++s)
         if (sc_host[s].fail) throw ApiError(DDPCA_ENUMERIC, "PCG breakdown (non-finite or non-positive curvature) in batch member " + std::to_string(s));
+    // this solve's iteration counts pace the next one's tail (pcg_wait)
+    if (last_prec_ >= 0) {
+        expect_[last_prec_].resize(nsub);
+        for (int s = 0; s < nsub; ++s) expect_[last_prec_][s] = sc_host[s].iter;
+        last_prec_ = -1;
+    }
     if (!no_coarse && !solve_accounted_) {
         // algorithmic bytes of the solve that just finished: members done at initialisation moved
         // only k_pcg_init's share; the others ran iter SpMVs and iter V-cycles (the setup's

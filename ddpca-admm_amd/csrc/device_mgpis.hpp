@@ -79,6 +79,18 @@ struct LevelDev {
                            // V-cycle runs on fp64 operators
     DevBuf<float> val32;   // V-cycle operator rounded once to fp32 (opt.precond_fp32), levels >= 1
     DevBuf<uint16_t> val16;  // fine level's V-cycle copy in block-exponent fp16 (opt.precond_fp32 = 2)
+    // stencil-coded V-cycle copy (val16 / val32 of a box-lattice level; opt-in DDPCA_CODED=1): the
+    // slots of chunk c are the 27-point stencil positions its rows use, in stencil order -- slot
+    // k = the k-th set bit q of cm[c], column = row + (q/9-1) nxy + ((q/3)%3-1) nx + (q%3-1) with
+    // the member's strides (lstr) -- so the column is wave-uniform arithmetic instead of a per-lane
+    // 2-B load in front of every x gather; a row without that neighbour holds a zero block there
+    // (the slot order is the sorted one, sums are bit-identical to the column-indexed copy)
+    bool coded = false;
+    DevBuf<uint32_t> cm;    // per chunk: stencil positions present
+    DevBuf<uint32_t> cmq;   // per chunk: 4 sub-masks, slots k = g (mod 4) (row-split kernel, lane group g)
+    DevBuf<int64_t> coff;   // per chunk + 1: first coded slot
+    DevBuf<int32_t> lstr;   // per member: nx, nx * ny of its lattice
+    int64_t ncslots = 0;
     // table mode: rows whose block values (in device slot order, masks applied) are bit-identical
     // share one table row; the kernel streams only column indices and a row type, the values
     // come from the cache-resident table (structured meshes: ~30x fewer distinct rows than rows)
@@ -148,6 +160,11 @@ struct GsFine {
     DevBuf<int64_t> offl, offu;          // per chunk: first L / U slot
     DevBuf<int32_t> col;                 // per slot lane (when the level has no 16-bit offsets)
     DevBuf<int16_t> col16;
+    // stencil-coded form (the fine level is a coded lattice and every chunk's L and U stencil
+    // positions are disjoint -- the parity colouring of a box): per chunk the L and U position
+    // masks; its L / U slots are their set bits in stencil order (no column arrays)
+    bool coded = false;
+    DevBuf<uint32_t> lm, um;
     DevBuf<uint16_t> val16;
     DevBuf<float> val32;
     DevBuf<double> val64;
@@ -283,6 +300,16 @@ public:
 private:
     hipGraphExec_t graph_[2] = {nullptr, nullptr};
     hipGraphExec_t graph_h_[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};  // [prec][half]
+    // one-iteration graphs for the tail of a solve: once the queued iterations reach the members'
+    // expected count (their previous solve's, expect_[prec]), the host queues single iterations
+    // two ahead of the slowest member instead of whole replays, so at most two iterations of
+    // launches run after the last member converged (a replay of iters_per_graph left up to
+    // ~1.5 k over, every launch of it dispatching its full grid to exit at once)
+    hipGraphExec_t graph1_[2] = {nullptr, nullptr};
+    hipGraphExec_t graph1_h_[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
+    std::vector<int64_t> expect_[2];
+    int last_prec_ = -1;
+    int64_t horizon(int prec, int half) const;  // max expected iterations (half -1: all members), INT64_MAX unknown
     bool split_ = false;
     hipStream_t stream2_ = nullptr;
     hipEvent_t ev_fork_ = nullptr, ev_join_ = nullptr;
@@ -291,6 +318,7 @@ private:
     std::vector<int> half_host_;
     PcgScal* sc_cur_ = nullptr; // the scalars enqueue_iteration / vcycle bind (sc, or a half's copy)
     void build_half_graph(int prec, int h);
+    hipGraphExec_t capture_iterations(int prec, int count, PcgScal* scp);
     int fin_threads() const;
     void launch_fin(hipStream_t st, int what, const double* part, const double* part2, const int64_t* cb, PcgScal* scp,
                     PcgMirror* mir);

@@ -162,18 +162,33 @@ def test_headline_fullsize_batched_solves_match_oracle(ddpca, oracle, gpu):
         assert err <= 1e-8, (tv, err)
 
 
-@pytest.mark.parametrize("env", [("DDPCA_STREAMS", "1"), ("DDPCA_FUSE_JAC0", "1"), ("DDPCA_GS_BLOCK", "256"),
-                                 ("DDPCA_GS_MINVC", "0"), ("DDPCA_GS_XCD", "1")],
-                         ids=["one-stream", "fused-jac0", "gs-workgroup-256", "gs-inverses-by-row", "gs-xcd-slabs"])
-def test_schedule_variants_are_bit_identical(ddpca, gpu, monkeypatch, env):
+@pytest.mark.parametrize("env,opts", [(("DDPCA_STREAMS", "1"), "HEADLINE_OPTIONS"),
+                                      (("DDPCA_FUSE_JAC0", "1"), "HEADLINE_OPTIONS"),
+                                      (("DDPCA_GS_BLOCK", "256"), "HEADLINE_OPTIONS"),
+                                      (("DDPCA_GS_MINVC", "0"), "HEADLINE_OPTIONS"),
+                                      (("DDPCA_GS_XCD", "1"), "HEADLINE_OPTIONS"),
+                                      (("DDPCA_CODED", "1"), "HEADLINE_OPTIONS"),
+                                      (("DDPCA_CODED", "1"), "HEADLINE_OPTIONS_SMALL"),
+                                      (("DDPCA_TAIL_PACING", "0"), "HEADLINE_OPTIONS")],
+                         ids=["one-stream", "fused-jac0", "gs-workgroup-256", "gs-inverses-by-row", "gs-xcd-slabs",
+                              "stencil-coded-vcycle", "stencil-coded-vcycle-small", "whole-replay-pacing"])
+def test_schedule_variants_are_bit_identical(ddpca, gpu, monkeypatch, env, opts):
     """Schedule-only variants of the headline path must not change a bit: the two-stream split of
     the body-balance batch and of the mass CG (MgpisDevice / MassBatch ::set_split, default on)
     against one stream, the V-cycle's first fine sweep fused into k_axpy (k_axpy_jac0, opt-in,
     block-Jacobi option sets only) against the separate k_jac0, and the multicolour sweeps in
     four-wave workgroups, with the inverses read by row instead of in chunk order, and with
-    XCD-slab workgroup placement, against the defaults.  ADMM trajectory, displacements and PCG iteration counts equal
-    bit for bit (8 ADMM iterations, reduced chain, headline option set)."""
-    H, M = ddpca.HEADLINE_OPTIONS, ddpca.HEADLINE_MUSC
+    XCD-slab workgroup placement, against the defaults; the V-cycle's stencil-coded copies (opt-in:
+    columns from the 27-point stencil position, zero blocks where a row lacks a neighbour) against
+    the column-indexed ones, on both option sets (the small one smooths the fine level with block
+    Jacobi); and whole-replay pacing to the end of every solve against the one-iteration tail
+    graphs.  ADMM trajectory,
+    displacements and PCG iteration counts equal bit for bit (8 ADMM iterations, reduced chain)."""
+    H, M = getattr(ddpca, opts), ddpca.HEADLINE_MUSC
+    if env[0] == "DDPCA_CODED":
+        # the row-split kernel of the small levels sums a row's slots in four groups by slot rank,
+        # and the coded copy's zero blocks shift those ranks: compare with it off on both sides
+        monkeypatch.setenv("DDPCA_SPLIT_CHUNKS", "0")
     out = {}
     for variant in ("default", "alt"):
         if variant == "alt":
