@@ -319,6 +319,33 @@ __global__ __launch_bounds__(256) void k_mcg_init(const double* b, const double*
     }
 }
 
+// warm start (MassBatch::solve from the previous solution x): r = b - A x, z = D^-1 r, p = q = 0;
+// partials (r.z, b.b) per chunk and r.r per chunk in prr; x is kept
+__global__ __launch_bounds__(256) void k_mcg_init_warm(EllArgs e, const double* b, const double* x, double* r, double* z,
+                                                       double* p, double* q, double* partial, double* prr) {
+    const int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (c >= e.nch) return;
+    const int lane = threadIdx.x & 63;
+    const int64_t row = c * 64 + lane;
+    const int ns = e.slots[c];
+    const int32_t* cp = e.col + e.off[c] * 64 + lane;
+    const double* vp = e.val + e.off[c] * 64 + lane;
+    double s = 0.0;
+#pragma unroll 4
+    for (int k = 0; k < ns; ++k) s += vp[(int64_t)k * 64] * x[cp[(int64_t)k * 64]];
+    const double bi = b[row], ri = bi - s, zi = e.dinv[row] * ri;
+    r[row] = ri;
+    z[row] = zi;
+    p[row] = 0.0;
+    q[row] = 0.0;
+    const double a = wsum(ri * zi), bb = wsum(bi * bi), rr = wsum(ri * ri);
+    if (lane == 0) {
+        partial[2 * c] = a;
+        partial[2 * c + 1] = bb;
+        prr[c] = rr;
+    }
+}
+
 // q = A z + beta q, p = z + beta p; partial p.q per chunk
 __global__ __launch_bounds__(256) void k_mcg_spmv(EllArgs e, const PcgScal* sc, const double* z, double* q, double* p,
                                                   double* partial) {
@@ -366,7 +393,7 @@ enum McgWhat { kMcgInit = 0, kMcgAlpha = 1, kMcgBeta = 2 };
 
 // per-system scalars: one workgroup per system, fixed order over its chunks
 __global__ __launch_bounds__(256) void k_mcg_fin(int what, const double* partial, const int64_t* cb, PcgScal* scv,
-                                                 PcgMirror* mirror) {
+                                                 PcgMirror* mirror, const double* prr = nullptr) {
     const int sys = blockIdx.x;
     PcgScal* sc = scv + sys;
     if (what != kMcgInit && sc->done) return;
@@ -395,14 +422,20 @@ __global__ __launch_bounds__(256) void k_mcg_fin(int what, const double* partial
     a = (r0[0] + r0[1]) + (r0[2] + r0[3]);
     b = (r1[0] + r1[1]) + (r1[2] + r1[3]);
     if (what == kMcgInit) {
+        // ||r0||^2: b.b from zero, the warm start's own r.r otherwise (one thread, chunk order)
+        double rr = b;
+        if (prr) {
+            rr = 0.0;
+            for (int64_t k = cb[sys]; k < k1; ++k) rr += prr[k];
+        }
         sc->delta = a;
         sc->bb = b;
-        sc->rr = b;
+        sc->rr = rr;
         sc->tol2 = sc->tol2 * b;
         sc->beta = 0.0;
         sc->iter = 0;
         sc->fail = 0;
-        sc->done = (b <= sc->tol2 || sc->maxit <= 0) ? 1 : 0;
+        sc->done = (rr <= sc->tol2 || sc->maxit <= 0) ? 1 : 0;
         mirror_store(mirror + sys, 0, sc->done, 0);
     } else if (what == kMcgAlpha) {
         sc->pq = a;
@@ -716,26 +749,27 @@ public:
         // per CG iteration -- k_mcg_spmv: stored entries (12 B), z gathered once, z, q, p read
         // and q, p written; k_mcg_axpy: x, r read + written, z written, p, q, D^-1 read (112 B per row)
         init_bytes_.assign(nsys, 0.0);
+        init_warm_bytes_.clear();
         it_bytes_.assign(nsys, 0.0);
         for (int s = 0; s < nsys; ++s) {
             const double rows = (double)A[s]->nrow, ent = (double)A[s]->nnz();
             init_bytes_[s] = 56.0 * rows;
+            // warm: + the stored entries and x gathered once (r = b - A x)
+            init_warm_bytes_.push_back(56.0 * rows + 12.0 * ent + 8.0 * rows);
             it_bytes_[s] = 12.0 * ent + 8.0 * rows + 40.0 * rows + 64.0 * rows;
         }
         for (auto* v : {&b, &x, &r, &z, &p, &q}) {
             v->alloc(std::max<int64_t>(nrow, 2));
             v->zero();
         }
-        partial.alloc(2 * std::max<int64_t>(nch, 1));
+        partial.alloc(3 * std::max<int64_t>(nch, 1));  // (a, b) pairs + the warm start's r.r
         sc.alloc(std::max(nsys, 1));
         DDPCA_HIP(hipHostMalloc(reinterpret_cast<void**>(&sc_host), std::max(nsys, 1) * sizeof(PcgScal)));
         mirror.alloc(nsys);
     }
     ~MassBatch() {
         if (s2_) (void)hipStreamSynchronize(s2_);
-        if (graph_ && !split_) (void)hipGraphExecDestroy(graph_);
-        for (auto& g : graph_h_)
-            if (g) (void)hipGraphExecDestroy(g);
+        drop_graphs();
         if (ev_fork_) (void)hipEventDestroy(ev_fork_);
         if (ev_join_) (void)hipEventDestroy(ev_join_);
         if (s2_) (void)hipStreamDestroy(s2_);
@@ -747,15 +781,9 @@ public:
         if (nsys == 0) return;
         solved_ = true;
         if (x_out != x_target_) {
-            if (split_) {
-                for (auto& g : graph_h_)
-                    if (g) (void)hipGraphExecDestroy(g);
-                graph_h_[0] = graph_h_[1] = nullptr;
-            } else if (graph_) {
-                (void)hipGraphExecDestroy(graph_);
-            }
-            graph_ = nullptr;
+            drop_graphs();
             x_target_ = x_out;
+            warm_ready_ = false;
         }
         if (!graph_) capture(s);
         mirror.reset();  // the previous solve on `s` was paced to completion before this point
@@ -765,22 +793,37 @@ public:
             sc_host[i].maxit = maxit;
         }
         DDPCA_HIP(hipMemcpyAsync(sc.p, sc_host, nsys * sizeof(PcgScal), hipMemcpyHostToDevice, s));
-        hipLaunchKernelGGL(k_mcg_init, dim3(nb256(nrow)), dim3(256), 0, s, b.p, dinv.p, x_out, r.p, z.p, p.p, q.p,
-                           partial.p, nrow);
-        hipLaunchKernelGGL(k_mcg_fin, dim3(nsys), dim3(256), 0, s, (int)kMcgInit, partial.p, cb.p, sc.p, mirror.dev);
+        // opt-in warm start from the previous solution in x_out (DDPCA_MASS_WARM=1; the first
+        // solve into a buffer starts from zero): 39.3 -> 37.1 mass-CG iterations per ADMM
+        // iteration at the headline, no measurable gain (profiles/r03v), so off by default
+        const char* ew = std::getenv("DDPCA_MASS_WARM");
+        const bool warm = warm_ready_ && ew && std::atoi(ew) != 0;
+        if (warm) {
+            EllArgs e{slots.p, off.p, col.p, val.p, csys.p, dinv.p, nch};
+            hipLaunchKernelGGL(k_mcg_init_warm, dim3(ceil_div(nch, 4)), dim3(256), 0, s, e, b.p, x_out, r.p, z.p, p.p,
+                               q.p, partial.p, partial.p + 2 * nch);
+        } else {
+            hipLaunchKernelGGL(k_mcg_init, dim3(nb256(nrow)), dim3(256), 0, s, b.p, dinv.p, x_out, r.p, z.p, p.p, q.p,
+                               partial.p, nrow);
+        }
+        hipLaunchKernelGGL(k_mcg_fin, dim3(nsys), dim3(256), 0, s, (int)kMcgInit, partial.p, cb.p, sc.p, mirror.dev,
+                           warm ? partial.p + 2 * nch : nullptr);
+        warm_started_ = warm;
+        warm_ready_ = true;  // x_out holds this solve's result for the next one
         if (split_) {
             // fork into the two halves' streams, pace both, join and merge the scalars back
             hipLaunchKernelGGL(k_scal_split, dim3(ceil_div(nsys, 64)), dim3(64), 0, s, sc.p, sc_half_.p, half_.p, nsys);
             DDPCA_HIP(hipEventRecord(ev_fork_, s));
             DDPCA_HIP(hipStreamWaitEvent(s2_, ev_fork_, 0));
             hipStream_t st[2] = {s, s2_};
-            pace_halves(st, graph_h_, mirror, half_host_, k, 0);
+            const int64_t hz[2] = {horizon(0), horizon(1)};
+            pace_halves(st, graph_h_, mirror, half_host_, k, 0, graph1_h_, hz);
             DDPCA_HIP(hipEventRecord(ev_join_, s2_));
             DDPCA_HIP(hipStreamWaitEvent(s, ev_join_, 0));
             hipLaunchKernelGGL(k_scal_merge, dim3(ceil_div(nsys, 64)), dim3(64), 0, s, sc.p, sc_half_.p, half_.p, nsys);
             return;
         }
-        pace_until_done(s, graph_, mirror, k, 0);
+        pace_until_done(s, graph_, mirror, k, 0, graph1_, horizon(-1));
     }
 
     // Two-stream split of the systems (as MgpisDevice::set_split): two halves of equal rows, each
@@ -809,23 +852,19 @@ public:
             }
             half_.upload(half_host_);
         }
-        if (on != split_) {
-            for (auto& g : graph_h_)
-                if (g) (void)hipGraphExecDestroy(g);
-            graph_h_[0] = graph_h_[1] = nullptr;
-            if (graph_ && !split_) (void)hipGraphExecDestroy(graph_);
-            graph_ = nullptr;
-        }
+        if (on != split_) drop_graphs();
         split_ = on;
     }
 
     // after the stream synchronised: iterations of the last solve, breakdown check
     void check() {
         last_iters = 0;
+        expect_.resize(nsys);
         for (int i = 0; i < nsys; ++i) {
             if (mirror.host[i].fail) throw ApiError(DDPCA_ENUMERIC, "surface mass CG breakdown");
+            expect_[i] = mirror.host[i].iter;  // paces the next solve's tail
             last_iters = std::max<int64_t>(last_iters, mirror.host[i].iter);
-            if (solved_) alg_bytes += init_bytes_[i] + (double)mirror.host[i].iter * it_bytes_[i];
+            if (solved_) alg_bytes += (warm_started_ ? init_warm_bytes_[i] : init_bytes_[i]) + (double)mirror.host[i].iter * it_bytes_[i];
         }
         solved_ = false;
     }
@@ -833,6 +872,30 @@ public:
 private:
     hipGraphExec_t graph_ = nullptr;
     hipGraphExec_t graph_h_[2] = {nullptr, nullptr};
+    // one-iteration graphs for the tail (MgpisDevice::graph1_): past the systems' previous
+    // iteration counts the host queues single iterations two ahead of the slowest system
+    hipGraphExec_t graph1_ = nullptr;
+    hipGraphExec_t graph1_h_[2] = {nullptr, nullptr};
+    std::vector<int64_t> expect_;
+    int64_t horizon(int half) const {
+        const char* e = std::getenv("DDPCA_TAIL_PACING");
+        if ((e && std::atoi(e) == 0) || (int)expect_.size() != nsys) return INT64_MAX;
+        int64_t h = 0;
+        for (int i = 0; i < nsys; ++i) {
+            if (half >= 0 && half_host_[i] != half) continue;
+            if (expect_[i] <= 0) return INT64_MAX;
+            h = std::max(h, expect_[i]);
+        }
+        return h;
+    }
+    void drop_graphs() {
+        for (hipGraphExec_t* g : {&graph_h_[0], &graph_h_[1], &graph1_h_[0], &graph1_h_[1], &graph1_}) {
+            if (*g) (void)hipGraphExecDestroy(*g);
+            *g = nullptr;
+        }
+        if (graph_ && !split_) (void)hipGraphExecDestroy(graph_);  // (split: graph_ aliases graph_h_[0])
+        graph_ = nullptr;
+    }
     double* x_target_ = nullptr;
     bool split_ = false;
     hipStream_t s2_ = nullptr;
@@ -841,27 +904,34 @@ private:
     DevBuf<int32_t> half_;
     std::vector<int> half_host_;
     std::vector<int64_t> cb_host_;
-    std::vector<double> init_bytes_, it_bytes_;
+    std::vector<double> init_bytes_, init_warm_bytes_, it_bytes_;
     bool solved_ = false;
+    bool warm_ready_ = false;    // x_target_ holds a previous solution (finite) to start from
+    bool warm_started_ = false;  // the last solve started from it
     void capture(hipStream_t s) {
         if (split_) {
-            capture_one(s, sc_half_.p, &graph_h_[0]);
-            capture_one(s, sc_half_.p + nsys, &graph_h_[1]);
+            capture_one(s, sc_half_.p, &graph_h_[0], k);
+            capture_one(s, sc_half_.p + nsys, &graph_h_[1], k);
+            if (k > 1) {
+                capture_one(s, sc_half_.p, &graph1_h_[0], 1);
+                capture_one(s, sc_half_.p + nsys, &graph1_h_[1], 1);
+            }
             graph_ = graph_h_[0];  // marks the capture done (destroyed through graph_h_)
             return;
         }
-        capture_one(s, sc.p, &graph_);
+        capture_one(s, sc.p, &graph_, k);
+        if (k > 1) capture_one(s, sc.p, &graph1_, 1);
     }
-    void capture_one(hipStream_t s, PcgScal* scp, hipGraphExec_t* out) {
+    void capture_one(hipStream_t s, PcgScal* scp, hipGraphExec_t* out, int64_t iters) {
         EllArgs e{slots.p, off.p, col.p, val.p, csys.p, dinv.p, nch};
         hipGraph_t g;
         DDPCA_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
-        for (int64_t it = 0; it < k; ++it) {
+        for (int64_t it = 0; it < iters; ++it) {
             hipLaunchKernelGGL(k_mcg_spmv, dim3(ceil_div(nch, 4)), dim3(256), 0, s, e, scp, z.p, q.p, p.p, partial.p);
-            hipLaunchKernelGGL(k_mcg_fin, dim3(nsys), dim3(256), 0, s, (int)kMcgAlpha, partial.p, cb.p, scp, mirror.dev);
+            hipLaunchKernelGGL(k_mcg_fin, dim3(nsys), dim3(256), 0, s, (int)kMcgAlpha, partial.p, cb.p, scp, mirror.dev, nullptr);
             hipLaunchKernelGGL(k_mcg_axpy, dim3(nb256(nrow)), dim3(256), 0, s, e, scp, x_target_, r.p, z.p, p.p, q.p,
                                partial.p);
-            hipLaunchKernelGGL(k_mcg_fin, dim3(nsys), dim3(256), 0, s, (int)kMcgBeta, partial.p, cb.p, scp, mirror.dev);
+            hipLaunchKernelGGL(k_mcg_fin, dim3(nsys), dim3(256), 0, s, (int)kMcgBeta, partial.p, cb.p, scp, mirror.dev, nullptr);
         }
         DDPCA_HIP(hipStreamEndCapture(s, &g));
         DDPCA_HIP(hipGraphInstantiate(out, g, nullptr, nullptr, 0));

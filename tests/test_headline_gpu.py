@@ -209,6 +209,34 @@ def test_schedule_variants_are_bit_identical(ddpca, gpu, monkeypatch, env, opts)
     assert np.array_equal(out["default"][2], out["alt"][2])
 
 
+def test_mass_solves_warm_started(ddpca, gpu, monkeypatch):
+    """Opt-in (DDPCA_MASS_WARM=1): the batched surface-mass CG (the reference's LDLT solves,
+    MCONTACT.h:2671-2704) starts from the previous ADMM iteration's solution (MassBatch::solve,
+    k_mcg_init_warm: r0 = b - M x_prev) and stops at the same ||r|| <= 1e-14 ||b||.  Against
+    starting from zero (the default):
+    resuMoni rows within 1e-8 relative and displacements within 1e-9 after 10 ADMM iterations,
+    and fewer mass-CG iterations."""
+    H, M = ddpca.HEADLINE_OPTIONS, ddpca.HEADLINE_MUSC
+    out = {}
+    for v in ("0", "1"):
+        monkeypatch.setenv("DDPCA_MASS_WARM", v)
+        P = ddpca.headline_problem(gl=3)
+        P.set_coarse(M["muscSett"], [M["doleMcsc"]] * P.nsub)
+        P.ESTABLISH()
+        mc = ddpca.MCONTACT(P, **H)
+        assert mc.CONTACT_ANALYSIS(10, check=False) == 10
+        out[v] = (mc.monitor().copy(), [mc.get("resuDisp", tv).copy() for tv in range(P.nsub)],
+                  int(mc.get("mass_iters")[0]))
+        del mc
+    ok, worst = _rows_close(out["0"][0], out["1"][0], k=10, rtol=1e-8)
+    du = max(np.linalg.norm(a - b) / np.linalg.norm(b) for a, b in zip(out["0"][1], out["1"][1]) if np.any(b))
+    it0, it1 = (out[v][2] for v in ("0", "1"))
+    print(f"warm vs cold mass solves: worst resuMoni rel {worst:.2e}, displacements {du:.2e}, mass-CG iterations {it0} -> {it1}")
+    assert ok, worst
+    assert du <= 1e-9, du
+    assert it1 < it0
+
+
 def test_coarse_correction_kx_from_recursive_residual(ddpca, gpu, monkeypatch):
     """The coarse-space correction takes consStif[L] x as b - r from PCG's recursive residual
     (device_mcontact.hip coarse_correct) instead of the reference's explicit product
