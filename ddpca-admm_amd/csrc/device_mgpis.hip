@@ -276,11 +276,11 @@ __device__ __forceinline__ void sell_rows_tbl(const int32_t* colp, const double*
         c1 = __builtin_nontemporal_load(colp + kChunk);
         c2 = __builtin_nontemporal_load(colp + 2 * kChunk);
     }
-    auto blk = [&](const double* v, const double* xj) {
+    auto blk = [&](const double* v, const double* xj) {  // block_fma_any's contraction (bit-identical sums)
         const double x0 = xj[0], x1 = xj[1], x2 = xj[2];
-        s0 += v[0] * x0 + v[1] * x1 + v[2] * x2;
-        s1 += v[3] * x0 + v[4] * x1 + v[5] * x2;
-        s2 += v[6] * x0 + v[7] * x1 + v[8] * x2;
+        s0 = s0 + __builtin_fma(v[2], x2, __builtin_fma(v[1], x1, v[0] * x0));
+        s1 = s1 + __builtin_fma(v[5], x2, __builtin_fma(v[4], x1, v[3] * x0));
+        s2 = s2 + __builtin_fma(v[8], x2, __builtin_fma(v[7], x1, v[6] * x0));
     };
     for (; k + 3 <= ns; k += 3) {
         const int64_t j0 = c0, j1 = c1, j2 = c2;
@@ -329,9 +329,9 @@ __device__ __forceinline__ void sell_rows_uniform(const int32_t* colp, const dou
             x2 = x[3 * j + 2];
         }
         const double* v = tv + 9 * k;
-        s0 += v[0] * x0 + v[1] * x1 + v[2] * x2;
-        s1 += v[3] * x0 + v[4] * x1 + v[5] * x2;
-        s2 += v[6] * x0 + v[7] * x1 + v[8] * x2;
+        s0 = s0 + __builtin_fma(v[2], x2, __builtin_fma(v[1], x1, v[0] * x0));
+        s1 = s1 + __builtin_fma(v[5], x2, __builtin_fma(v[4], x1, v[3] * x0));
+        s2 = s2 + __builtin_fma(v[8], x2, __builtin_fma(v[7], x1, v[6] * x0));
     }
 }
 
