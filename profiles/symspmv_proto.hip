@@ -104,6 +104,32 @@ __global__ __launch_bounds__(64 * WPB) void k_spmv(Args a) {
     if (lane == 0) a.partial[c] = d;
 }
 
+// the full layout with a chosen slot unroll and a waves-per-EU floor (register budget)
+template <int U, int WPE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void k_full_occ(Args a) {
+    const int lane = threadIdx.x & 63;
+    const int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (c >= a.nch) return;
+    const int64_t row = c * C + lane;
+    double s0 = 0, s1 = 0, s2 = 0;
+    const int ns = a.ns[c];
+    const int64_t base = a.off[c];
+#pragma unroll U
+    for (int k = 0; k < ns; ++k) {
+        const int64_t j = row + __builtin_nontemporal_load(a.c16 + (base + k) * C + lane);
+        bfma<true, false>(a.val + (base + k) * 576, lane, a.z + 3 * j, s0, s1, s2);
+    }
+    const int64_t o = 3 * row;
+    const double be = a.beta;
+    const double q0 = s0 + be * a.q[o], q1 = s1 + be * a.q[o + 1], q2 = s2 + be * a.q[o + 2];
+    const double p0 = a.z[o] + be * a.p[o], p1 = a.z[o + 1] + be * a.p[o + 1], p2 = a.z[o + 2] + be * a.p[o + 2];
+    a.q[o] = q0; a.q[o + 1] = q1; a.q[o + 2] = q2;
+    a.p[o] = p0; a.p[o + 1] = p1; a.p[o + 2] = p2;
+    double d = p0 * q0 + p1 * q1 + p2 * q2;
+    for (int s = 32; s > 0; s >>= 1) d += __shfl_xor(d, s, 64);
+    if (lane == 0) a.partial[c] = d;
+}
+
 static uint64_t mix(uint64_t x) {
     x ^= x >> 33; x *= 0xff51afd7ed558ccdULL; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ULL; x ^= x >> 33;
     return x;
@@ -299,6 +325,19 @@ int main(int argc, char** argv) {
     std::vector<int32_t> pB4 = band_perm(4), pB8 = band_perm(8), pB16 = band_perm(16), pB65 = band_perm(65);
     auto upperm = [&](std::vector<int32_t>& v) { int32_t* d = nullptr; CK(hipMalloc(&d, v.size() * 4)); CK(hipMemcpy(d, v.data(), v.size() * 4, hipMemcpyHostToDevice)); return d; };
     int32_t *dB4 = upperm(pB4), *dB8 = upperm(pB8), *dB16 = upperm(pB16), *dB65 = upperm(pB65);
+    if (argc > 3) {  // occupancy / unroll sweep of the full layout only
+        for (int rep = 0; rep < 2; ++rep) {
+            run("full (NT values)", k_spmv<false, true, true>, F, bF, &qF);
+            run("full U3 wpe1", k_full_occ<3, 1>, F, bF, nullptr);
+            run("full U3 wpe6", k_full_occ<3, 6>, F, bF, nullptr);
+            run("full U3 wpe8", k_full_occ<3, 8>, F, bF, nullptr);
+            run("full U2 wpe8", k_full_occ<2, 8>, F, bF, nullptr);
+            run("full U4 wpe1", k_full_occ<4, 1>, F, bF, nullptr);
+            run("full U6 wpe1", k_full_occ<6, 1>, F, bF, nullptr);
+            run("full U1 wpe8", k_full_occ<1, 8>, F, bF, nullptr);
+        }
+        return 0;
+    }
     for (int rep = 0; rep < 2; ++rep) {
         run("full (NT values)", k_spmv<false, true, true>, F, bF, &qF);
         run("full 1-wave WGs", k_spmv<false, true, true, 1>, F, bF, nullptr, (int)nch, 64);
