@@ -538,6 +538,42 @@ struct GsArgs {
     int64_t nlast;
 };
 
+// the colour sweep's per-row tail: PH 1 stores r = -s; PH 0 / 2 store x = M (b - s) and return
+// its share of b.x (DOT); ln = the row's position in its colour chunk
+template <int PH, bool DOT, typename T>
+__device__ __forceinline__ double gs_epilogue(const GsArgs& a, int64_t c, int ln, int64_t row, bool real, double s0,
+                                              double s1, double s2) {
+    const int64_t o = 3 * row;
+    double dotv = 0.0;
+    if (PH == 1) {
+        if (real) {
+            a.r[o] = -s0;
+            a.r[o + 1] = -s1;
+            a.r[o + 2] = -s2;
+        }
+    } else {
+        const double b0 = a.b[o], b1 = a.b[o + 1], b2 = a.b[o + 2];
+        double m0, m1, m2;
+        if (a.minvc) {
+            const float* m = a.minvc + c * 9 * kChunk + ln;
+            const double r0 = b0 - s0, r1 = b1 - s1, r2 = b2 - s2;
+            // explicit contraction, as in block_fma_any (bit-identical across instantiations)
+            m0 = __builtin_fma((double)m[2 * kChunk], r2, __builtin_fma((double)m[kChunk], r1, (double)m[0] * r0));
+            m1 = __builtin_fma((double)m[5 * kChunk], r2, __builtin_fma((double)m[4 * kChunk], r1, (double)m[3 * kChunk] * r0));
+            m2 = __builtin_fma((double)m[8 * kChunk], r2, __builtin_fma((double)m[7 * kChunk], r1, (double)m[6 * kChunk] * r0));
+        } else {
+            apply_m<true>(static_cast<const SmoothInv<T>*>(a.minv), row, b0 - s0, b1 - s1, b2 - s2, m0, m1, m2);
+        }
+        if (real) {
+            a.x[o] = m0;
+            a.x[o + 1] = m1;
+            a.x[o + 2] = m2;
+            if (DOT) dotv = __builtin_fma(b2, m2, __builtin_fma(b1, m1, b0 * m0));
+        }
+    }
+    return dotv;
+}
+
 template <int PH, bool DOT, typename T, typename CT, int V = 1>
 __global__ __launch_bounds__(kBlock) void k_gs(GsArgs a) {
     const int lane = threadIdx.x & 63;
@@ -571,35 +607,62 @@ __global__ __launch_bounds__(kBlock) void k_gs(GsArgs a) {
             sell_rows<V, T, CT>(colp + o * kChunk + lane, val + o * SV + lane, a.x, a.nsu[c], row, s0, s1, s2);
         }
     }
-    const int64_t o = 3 * row;
-    double dotv = 0.0;
-    if (PH == 1) {
-        if (real) {
-            a.r[o] = -s0;
-            a.r[o + 1] = -s1;
-            a.r[o + 2] = -s2;
-        }
-    } else {
-        const double b0 = a.b[o], b1 = a.b[o + 1], b2 = a.b[o + 2];
-        double m0, m1, m2;
-        if (a.minvc) {
-            const float* m = a.minvc + c * 9 * kChunk + lane;
-            const double r0 = b0 - s0, r1 = b1 - s1, r2 = b2 - s2;
-            // explicit contraction, as in block_fma_any (bit-identical across instantiations)
-            m0 = __builtin_fma((double)m[2 * kChunk], r2, __builtin_fma((double)m[kChunk], r1, (double)m[0] * r0));
-            m1 = __builtin_fma((double)m[5 * kChunk], r2, __builtin_fma((double)m[4 * kChunk], r1, (double)m[3 * kChunk] * r0));
-            m2 = __builtin_fma((double)m[8 * kChunk], r2, __builtin_fma((double)m[7 * kChunk], r1, (double)m[6 * kChunk] * r0));
-        } else {
-            apply_m<true>(static_cast<const SmoothInv<T>*>(a.minv), row, b0 - s0, b1 - s1, b2 - s2, m0, m1, m2);
-        }
-        if (real) {
-            a.x[o] = m0;
-            a.x[o + 1] = m1;
-            a.x[o + 2] = m2;
-            if (DOT) dotv = __builtin_fma(b2, m2, __builtin_fma(b1, m1, b0 * m0));
-        }
-    }
+    const double dotv = gs_epilogue<PH, DOT, T>(a, c, lane, row, real, s0, s1, s2);
     if (DOT) chunk_partial(dotv, a.partial, c);
+}
+
+// Row-split colour sweep for small launches (opt-in: up to DDPCA_GS_SPLIT_CHUNKS chunks, measured
+// no faster at 2 or 4 subdomains per GPU): one workgroup per colour chunk, each of
+// its four waves 16 of the chunk's rows, each lane a quarter of its row's L / U slots (k = g,
+// g + 4, ...), the quarters summed by lane shuffles -- four times the waves in flight and a
+// quarter of the dependent column -> x chain per lane (as k_sell_split for the block-Jacobi
+// levels).  The dot partial of the chunk: per wave, then the four waves in order through LDS.
+template <int PH, bool DOT, typename T, typename CT>
+__global__ __launch_bounds__(kBlock) void k_gs_split(GsArgs a) {
+    const int64_t li = blockIdx.x;
+    const int64_t c = a.list ? (int64_t)a.list[li] : li;
+    const int sub = a.csub[c];
+    if (stopped(a.sc, sub)) return;  // uniform over the workgroup
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int rin = w * 16 + (lane & 15), g = lane >> 4;
+    const int32_t rr = a.rowidx[c * kChunk + rin];
+    const bool real = rr >= 0;
+    const int64_t row = real ? rr : ~rr;
+    constexpr int64_t SV = slot_vals<T>() * kChunk;
+    const T* val = static_cast<const T*>(a.val);
+    const CT* colp;
+    if constexpr (sizeof(CT) == 2) colp = a.col16;
+    else colp = a.col;
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+    if (PH != 1) {
+        const int64_t o = a.offl[c];
+        const int ns = a.nsl[c];
+#pragma unroll 2
+        for (int k = g; k < ns; k += 4)
+            block_fma_any<true>(val + (o + k) * SV + rin, a.x + 3 * col_of(colp[(o + k) * kChunk + rin], row), s0, s1, s2, rin);
+    }
+    if (PH != 0) {
+        const int64_t o = a.offu[c];
+        const int ns = a.nsu[c];
+#pragma unroll 2
+        for (int k = g; k < ns; k += 4)
+            block_fma_any<true>(val + (o + k) * SV + rin, a.x + 3 * col_of(colp[(o + k) * kChunk + rin], row), s0, s1, s2, rin);
+    }
+    s0 += __shfl_xor(s0, 16, 64);
+    s1 += __shfl_xor(s1, 16, 64);
+    s2 += __shfl_xor(s2, 16, 64);
+    s0 += __shfl_xor(s0, 32, 64);
+    s1 += __shfl_xor(s1, 32, 64);
+    s2 += __shfl_xor(s2, 32, 64);
+    double dotv = 0.0;
+    if (g == 0) dotv = gs_epilogue<PH, DOT, T>(a, c, rin, row, real, s0, s1, s2);
+    if (DOT) {
+        __shared__ double wp[kBlock / kWave];
+        dotv = wave_sum(dotv);
+        if (lane == 0) wp[w] = dotv;
+        __syncthreads();
+        if (threadIdx.x == 0) a.partial[c] = (wp[0] + wp[1]) + (wp[2] + wp[3]);
+    }
 }
 
 
@@ -2774,6 +2837,16 @@ void launch_gs_t(const GsArgs& a, int ct, hipStream_t st) {  // ct: 0 int32 colu
     // ahead (DDPCA_GS_LOOP, read at graph capture; measured equal, profiles/r03i)
     const char* e = std::getenv("DDPCA_GS_LOOP");
     const int v = e ? std::atoi(e) : 1;
+    // small launches: the row-split sweep, opt-in (DDPCA_GS_SPLIT_CHUNKS = the largest launch it
+    // takes; read at graph capture): at 2 subdomains per GPU 58.2 vs 58.9-60.5 ADMM it/s without
+    // it, at 4 no better either (profiles/r03aa) -- the colour launches are not short of waves
+    const char* es = std::getenv("DDPCA_GS_SPLIT_CHUNKS");
+    const int64_t split_max = es ? std::atoll(es) : 0;
+    if (ct != 2 && a.n <= split_max && !a.xcd) {
+        if (ct == 1) hipLaunchKernelGGL((k_gs_split<PH, DOT, T, int16_t>), dim3((unsigned)a.n), dim3(kBlock), 0, st, a);
+        else hipLaunchKernelGGL((k_gs_split<PH, DOT, T, int32_t>), dim3((unsigned)a.n), dim3(kBlock), 0, st, a);
+        return;
+    }
     if (ct == 2) hipLaunchKernelGGL((k_gs<PH, DOT, T, uint32_t, 1>), grid, dim3(bs), 0, st, a);
     else if (ct == 1) {
         if (v == 2) hipLaunchKernelGGL((k_gs<PH, DOT, T, int16_t, 2>), grid, dim3(bs), 0, st, a);
