@@ -479,6 +479,64 @@ __global__ void k_pair_norms(const double* a, const double* o, int64_t n, double
     }
 }
 
+// All MONITOR pair norms of an iteration in two launches (instead of two per vector pair): block b
+// of k_pair_norms_all is block b - blk0[g] of segment g = bseg[b], exactly the block k_pair_norms
+// would run for that segment, and k_reduce_pairs_all reduces segment g's blocks as k_reduce_pairs
+// does -- the same sums bit for bit
+struct NormSeg {
+    const double* a;
+    const double* o;
+    int64_t n;
+    int64_t blk0;  // first block of the segment in the batched grid
+    int64_t nb;    // its blocks
+    int64_t slot;  // moni slot (2 doubles)
+};
+
+__global__ void k_pair_norms_all(const NormSeg* seg, const int32_t* bseg, double* partial) {
+    __shared__ double r1[4], r2[4];
+    const NormSeg& S = seg[bseg[blockIdx.x]];
+    const int64_t i = (int64_t)(blockIdx.x - S.blk0) * blockDim.x + threadIdx.x;
+    double d = 0.0, s = 0.0;
+    if (i < S.n) {
+        const double ai = S.a[i], di = ai - S.o[i];
+        d = di * di;
+        s = ai * ai;
+    }
+    d = wsum(d);
+    s = wsum(s);
+    if ((threadIdx.x & 63) == 0) {
+        r1[threadIdx.x >> 6] = d;
+        r2[threadIdx.x >> 6] = s;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        partial[2 * blockIdx.x] = (r1[0] + r1[1]) + (r1[2] + r1[3]);
+        partial[2 * blockIdx.x + 1] = (r2[0] + r2[1]) + (r2[2] + r2[3]);
+    }
+}
+
+__global__ void k_reduce_pairs_all(const NormSeg* seg, const double* partial, double* moni) {
+    __shared__ double r1[4], r2[4];
+    const NormSeg& S = seg[blockIdx.x];
+    const double* pp = partial + 2 * S.blk0;
+    double d = 0.0, s = 0.0;
+    for (int64_t k = threadIdx.x; k < S.nb; k += blockDim.x) {
+        d += pp[2 * k];
+        s += pp[2 * k + 1];
+    }
+    d = wsum(d);
+    s = wsum(s);
+    if ((threadIdx.x & 63) == 0) {
+        r1[threadIdx.x >> 6] = d;
+        r2[threadIdx.x >> 6] = s;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        moni[S.slot] = (r1[0] + r1[1]) + (r1[2] + r1[3]);
+        moni[S.slot + 1] = (r2[0] + r2[1]) + (r2[2] + r2[3]);
+    }
+}
+
 __global__ void k_reduce_pairs(const double* partial, int64_t nb, double* out2) {
     __shared__ double r1[4], r2[4];
     double d = 0.0, s = 0.0;
@@ -1146,6 +1204,11 @@ struct ddpca_mcontact {
     double* state = nullptr;
     double* gamma = nullptr;
     DevBuf<double> uo, state_old, gcst, partial, moni;
+    // the MONITOR pair norms as one batch (k_pair_norms_all): segments, block -> segment
+    std::vector<NormSeg> norm_seg_host;
+    DevBuf<NormSeg> norm_seg;
+    DevBuf<int32_t> norm_bseg;
+    DevBuf<double> norm_partial;
     SellOp op_gamma, op_aux, op_lam;     // gamma (my halves), aux RHS, lambda RHS
     // interfaces whose per-ip operators are applied in factored form (Interface::factored)
     struct FactItf {
@@ -2239,15 +2302,45 @@ bool iterate_once(ddpca_mcontact& H, bool check) {
     }
     // ---- MONITOR norms (owned entries; others zero) and their reduction across ranks
     DDPCA_HIP(hipMemsetAsync(H.moni.p, 0, H.moni.n * sizeof(double), st));
-    for (auto& S : H.subs) {
-        pair_norm(H, H.u + S.dof0, H.uo.p + S.dof0, 3 * S.nn, 2 * S.tv);
-        if (S.nh)
-            pair_norm(H, H.u + H.oH + S.hoff, H.uo.p + H.oH + S.hoff, S.nh, 2 * H.nsub + 8 * H.nint + 2 * S.tv);
-    }
-    for (auto& sd : H.sides) {
-        const int64_t base = 2 * H.nsub + 8 * sd.ts + 4 * sd.s;
-        pair_norm(H, H.state + sd.roff, H.state_old.p + sd.roff, sd.m, base);
-        pair_norm(H, H.state + H.R + sd.roff, H.state_old.p + H.R + sd.roff, sd.m, base + 2);
+    {
+        std::vector<NormSeg> seg;
+        int64_t nblk = 0;
+        auto add = [&](const double* a, const double* o, int64_t n, int64_t slot) {
+            const int64_t nb = nb256(n);
+            seg.push_back({a, o, n, nblk, nb, slot});
+            nblk += nb;
+        };
+        for (auto& S : H.subs) {
+            add(H.u + S.dof0, H.uo.p + S.dof0, 3 * S.nn, 2 * S.tv);
+            if (S.nh) add(H.u + H.oH + S.hoff, H.uo.p + H.oH + S.hoff, S.nh, 2 * H.nsub + 8 * H.nint + 2 * S.tv);
+        }
+        for (auto& sd : H.sides) {
+            const int64_t base = 2 * H.nsub + 8 * sd.ts + 4 * sd.s;
+            add(H.state + sd.roff, H.state_old.p + sd.roff, sd.m, base);
+            add(H.state + H.R + sd.roff, H.state_old.p + H.R + sd.roff, sd.m, base + 2);
+        }
+        const char* eb = std::getenv("DDPCA_NORMS_BATCHED");  // 0: two launches per pair (A/B)
+        if (eb && std::atoi(eb) == 0) {
+            for (const NormSeg& g : seg) pair_norm(H, g.a, g.o, g.n, g.slot);
+        } else if (!seg.empty()) {
+            // the segments are the same every iteration: upload once (and again if they change)
+            const bool same = seg.size() == H.norm_seg_host.size() &&
+                              std::memcmp(seg.data(), H.norm_seg_host.data(), seg.size() * sizeof(NormSeg)) == 0;
+            if (!same) {
+                std::vector<int32_t> bseg(nblk);
+                for (size_t g = 0; g < seg.size(); ++g)
+                    for (int64_t k = 0; k < seg[g].nb; ++k) bseg[seg[g].blk0 + k] = (int32_t)g;
+                DDPCA_HIP(hipStreamSynchronize(st));  // the previous iteration's launches read the old table
+                H.norm_seg.upload(seg);
+                H.norm_bseg.upload(bseg);
+                H.norm_partial.alloc(2 * nblk);
+                H.norm_seg_host = seg;
+            }
+            hipLaunchKernelGGL(k_pair_norms_all, dim3((unsigned)nblk), dim3(256), 0, st, H.norm_seg.p, H.norm_bseg.p,
+                               H.norm_partial.p);
+            hipLaunchKernelGGL(k_reduce_pairs_all, dim3((unsigned)seg.size()), dim3(256), 0, st, H.norm_seg.p,
+                               H.norm_partial.p, H.moni.p);
+        }
     }
     if (H.nranks > 1) H.comm->allreduce_sum(H.moni.p, H.moni.n, st);
     DDPCA_HIP(hipEventRecord(H.ev[3], st));

@@ -169,9 +169,11 @@ def test_headline_fullsize_batched_solves_match_oracle(ddpca, oracle, gpu):
                                       (("DDPCA_GS_XCD", "1"), "HEADLINE_OPTIONS"),
                                       (("DDPCA_CODED", "1"), "HEADLINE_OPTIONS"),
                                       (("DDPCA_CODED", "1"), "HEADLINE_OPTIONS_SMALL"),
-                                      (("DDPCA_TAIL_PACING", "0"), "HEADLINE_OPTIONS")],
+                                      (("DDPCA_TAIL_PACING", "0"), "HEADLINE_OPTIONS"),
+                                      (("DDPCA_NORMS_BATCHED", "0"), "HEADLINE_OPTIONS")],
                          ids=["one-stream", "fused-jac0", "gs-workgroup-256", "gs-inverses-by-row", "gs-xcd-slabs",
-                              "stencil-coded-vcycle", "stencil-coded-vcycle-small", "whole-replay-pacing"])
+                              "stencil-coded-vcycle", "stencil-coded-vcycle-small", "whole-replay-pacing",
+                              "monitor-norms-per-pair"])
 def test_schedule_variants_are_bit_identical(ddpca, gpu, monkeypatch, env, opts):
     """Schedule-only variants of the headline path must not change a bit: the two-stream split of
     the body-balance batch and of the mass CG (MgpisDevice / MassBatch ::set_split, default on)
@@ -182,7 +184,7 @@ def test_schedule_variants_are_bit_identical(ddpca, gpu, monkeypatch, env, opts)
     columns from the 27-point stencil position, zero blocks where a row lacks a neighbour) against
     the column-indexed ones, on both option sets (the small one smooths the fine level with block
     Jacobi); and whole-replay pacing to the end of every solve against the one-iteration tail
-    graphs.  ADMM trajectory,
+    graphs; and the MONITOR pair norms two launches per vector pair against one batch.  ADMM trajectory,
     displacements and PCG iteration counts equal bit for bit (8 ADMM iterations, reduced chain)."""
     H, M = getattr(ddpca, opts), ddpca.HEADLINE_MUSC
     if env[0] == "DDPCA_CODED":
