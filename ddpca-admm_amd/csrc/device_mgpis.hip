@@ -1033,6 +1033,44 @@ __global__ __launch_bounds__(kBlock) void k_axpy_jac0(double* x, double* r, cons
     x0[3 * i + 2] = om * m2;
 }
 
+// k_axpy fused with the colour sweep's first launch (GsFine, forward from zero): colour 0 has no
+// earlier colour, so its rows' sweep is z_i = M_i r_i -- computed here from the new residual (via
+// LDS, as k_axpy_jac0) for the rows flagged in is0, the same operations on the same values as
+// k_gs<0> on colour 0 (bit for bit), one launch per PCG iteration fewer
+__global__ __launch_bounds__(kBlock) void k_axpy_gs0(double* x, double* r, const double* p, const double* q,
+                                                     const PcgScal* sc, double* partial, int64_t nn, const int32_t* csub,
+                                                     const float* minv, const uint8_t* is0, double* z) {
+    __shared__ double rl[kBlock / kWave][3 * kChunk];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t c = (int64_t)blockIdx.x * (kBlock / kWave) + w;
+    const int sub = c * kChunk < nn ? csub[c] : 0;
+    const bool live = c * kChunk < nn && !stopped(sc, sub);  // wave-uniform
+    if (live) {
+        const double al = sc[sub].alpha;
+        const int64_t base = c * 3 * kChunk + lane;
+        double s = 0.0;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const int64_t k = base + j * kChunk;
+            x[k] += al * p[k];
+            const double v = r[k] - al * q[k];
+            r[k] = v;
+            s += v * v;
+            rl[w][lane + j * kChunk] = v;
+        }
+        chunk_partial(s, partial, c);
+    }
+    __syncthreads();
+    if (!live) return;
+    const int64_t i = c * kChunk + lane;
+    if (!is0[i]) return;
+    double m0, m1, m2;
+    apply_m<true>(minv, i, rl[w][3 * lane], rl[w][3 * lane + 1], rl[w][3 * lane + 2], m0, m1, m2);
+    z[3 * i] = m0;
+    z[3 * i + 1] = m1;
+    z[3 * i + 2] = m2;
+}
+
 // z = D^-1 r (diagonal preconditioner, DIAG_PREC), partial r^T z
 __global__ __launch_bounds__(kBlock) void k_diag(const double* r, const double* dinv, double* z, double* partial,
                                                  int64_t nn, const int32_t* csub, const PcgScal* sc) {
@@ -1928,6 +1966,11 @@ void build_gs(GsFine& G, const LevelDev& L, int nsub, const std::vector<int64_t>
     G.offl.upload(offl);
     G.offu.upload(offu);
     G.cb.upload(cb);
+    {
+        std::vector<uint8_t> is0(L.nn, 0);  // rows of colour 0 (k_axpy_gs0)
+        for (int64_t g = 0; g < L.nn; ++g) is0[g] = colour[g] == 0 ? 1 : 0;
+        G.is0.upload(is0);
+    }
     G.coded = coded;
     if (coded) {
         G.lm.upload(lmk);
@@ -2815,6 +2858,16 @@ double MgpisDevice::bench_spmv(int variant, int reps) {
 
 // the first fine sweep can ride on k_axpy (k_axpy_jac0): block Jacobi from the fp32 inverses on
 // a level with a coarser one
+// the colour sweep's colour-0 launch rides on k_axpy (k_axpy_gs0): multicolour fine level with fp32
+// inverses; opt-in DDPCA_FUSE_GS0=1 (read at graph capture): bit-identical, measured neutral --
+// 17.39 vs 17.42 ADMM it/s at 8 subdomains, 31.97 vs 31.88 at 4 (profiles/r03ac)
+bool MgpisDevice::fuse_gs0() const {
+    const char* e = std::getenv("DDPCA_FUSE_GS0");
+    const bool on = e && e[0] == '1';
+    const int Lf = (int)lev.size() - 1;
+    return on && gs_fine() && gs.is0.p && !no_coarse && Lf > clev && vc_type(Lf) != kVal64 && lev[Lf].minv32.p;
+}
+
 bool MgpisDevice::fuse_jac0() const {
     // opt-in (DDPCA_FUSE_JAC0=1): measured 0.4 % slower at 8 subdomains per GPU, as in round 1
     // (profiles/r02u_ab.json, r01_sweep_fuse_axpy.txt) -- the wider k_axpy costs what k_jac0 did
@@ -2960,9 +3013,10 @@ void MgpisDevice::vcycle(const double* rin, double* zout, bool dot, bool first_d
     if (gsf) cur[Lf] = zout;  // the Gauss-Seidel sweeps run in place
     // ---- descend
     if (gsf) {
-        if (first_done) throw ApiError(DDPCA_ESTATE, "fused first sweep with the multicolour smoother");
-        // forward sweep from zero, colour by colour, then r = -U x in one launch
-        for (int k = 0; k < gs.ncol; ++k) launch_gs<0, false>(*this, k, zout, rin, nullptr, scp, nullptr);
+        if (first_done && !fuse_gs0()) throw ApiError(DDPCA_ESTATE, "fused first sweep with the multicolour smoother");
+        // forward sweep from zero, colour by colour (colour 0 already done by k_axpy_gs0 when
+        // first_done), then r = -U x in one launch
+        for (int k = first_done ? 1 : 0; k < gs.ncol; ++k) launch_gs<0, false>(*this, k, zout, rin, nullptr, scp, nullptr);
         launch_gs<1, false>(*this, -1, zout, nullptr, lev[Lf].r.p, scp, nullptr);
     } else if (first_done) {
         // k_axpy_jac0 wrote x0 = omega M rin into the fine level's first iterate buffer
@@ -3175,7 +3229,7 @@ int64_t MgpisDevice::iteration_launches() const {
     // place of jac0, nu - 1 + 1 + nu sweep launches
     const int64_t nd = (int64_t)lev.size() - 1 - clev;
     const int64_t base = 5 + (nd == 0 ? 2 : 1 + nd * (opt.nu + 1) + 1 + nd * (1 + opt.nu));
-    return gs_fine() && nd > 0 ? base - 1 - 2 * opt.nu + 2 * gs.ncol + 1 : base;
+    return gs_fine() && nd > 0 ? base - 1 - 2 * opt.nu + 2 * gs.ncol + 1 - (fuse_gs0() ? 1 : 0) : base;
 }
 
 // k_fin over every member (1024 threads, or 256 with DDPCA_FIN_THREADS=256)
@@ -3208,13 +3262,17 @@ void MgpisDevice::enqueue_iteration(int prec, bool timed) {
     if (timed) DDPCA_HIP(hipEventRecord(ev_k1, stream));
     launch_fin(stream, (int)kFinAlpha, partial.p, nullptr, fin_cb.p, scp, mirror.dev);
     const bool fuse0 = prec == 1 && fuse_jac0();
+    const bool fusegs = prec == 1 && !fuse0 && fuse_gs0();
     if (fuse0)
         hipLaunchKernelGGL(k_axpy_jac0, dim3(nblk), dim3(kBlock), 0, stream, xs.p, rs.p, ps.p, qs.p, scp, partial.p, L.nn,
                            L.csub.p, L.minv32.p, L.coef.p, L.t.p);
+    else if (fusegs)
+        hipLaunchKernelGGL(k_axpy_gs0, dim3(nblk), dim3(kBlock), 0, stream, xs.p, rs.p, ps.p, qs.p, scp, partial.p, L.nn,
+                           L.csub.p, L.minv32.p, gs.is0.p, zs.p);
     else
         hipLaunchKernelGGL(k_axpy, dim3(nblk), dim3(kBlock), 0, stream, xs.p, rs.p, ps.p, qs.p, scp, partial.p, L.nn, L.csub.p);
     launch_fin(stream, (int)kFinRR, partial.p, nullptr, fin_cb.p, scp, mirror.dev);
-    if (prec == 1) vcycle(rs.p, zs.p, true, fuse0);
+    if (prec == 1) vcycle(rs.p, zs.p, true, fuse0 || fusegs);
     else hipLaunchKernelGGL(k_diag, dim3(nblk), dim3(kBlock), 0, stream, rs.p, L.dinv.p, zs.p, partial.p, L.nn, L.csub.p, scp);
     launch_fin(stream, (int)kFinBeta, prec == 1 ? vc_partial() : partial.p, nullptr, prec == 1 ? vc_cb() : fin_cb.p, scp,
                mirror.dev);

@@ -165,6 +165,7 @@ struct GsFine {
     // masks; its L / U slots are their set bits in stencil order (no column arrays)
     bool coded = false;
     DevBuf<uint32_t> lm, um;
+    DevBuf<uint8_t> is0;                 // per fine node: 1 = colour 0 (swept inside k_axpy_gs0)
     DevBuf<uint16_t> val16;
     DevBuf<float> val32;
     DevBuf<double> val64;
@@ -243,6 +244,7 @@ public:
     // (k_axpy_jac0, only when fuse_jac0())
     void vcycle(const double* r, double* z, bool dot, bool first_done = false);
     bool fuse_jac0() const;
+    bool fuse_gs0() const;  // the colour sweep's first launch rides on k_axpy (k_axpy_gs0)
     // b_{l-1} = realProl[l-1]^T r_l on every member (masked), batch nodal layouts of levels l, l-1
     void restrict_level(int l, const double* rf, double* bc);
     // block (rotated-node) parts of the transfer from level l-1 to l: b_c += B^T r_f, x_f += B e_c

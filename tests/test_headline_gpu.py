@@ -170,10 +170,11 @@ def test_headline_fullsize_batched_solves_match_oracle(ddpca, oracle, gpu):
                                       (("DDPCA_CODED", "1"), "HEADLINE_OPTIONS"),
                                       (("DDPCA_CODED", "1"), "HEADLINE_OPTIONS_SMALL"),
                                       (("DDPCA_TAIL_PACING", "0"), "HEADLINE_OPTIONS"),
-                                      (("DDPCA_NORMS_BATCHED", "0"), "HEADLINE_OPTIONS")],
+                                      (("DDPCA_NORMS_BATCHED", "0"), "HEADLINE_OPTIONS"),
+                                      (("DDPCA_FUSE_GS0", "1"), "HEADLINE_OPTIONS")],
                          ids=["one-stream", "fused-jac0", "gs-workgroup-256", "gs-inverses-by-row", "gs-xcd-slabs",
                               "stencil-coded-vcycle", "stencil-coded-vcycle-small", "whole-replay-pacing",
-                              "monitor-norms-per-pair"])
+                              "monitor-norms-per-pair", "fused-colour-0-sweep"])
 def test_schedule_variants_are_bit_identical(ddpca, gpu, monkeypatch, env, opts):
     """Schedule-only variants of the headline path must not change a bit: the two-stream split of
     the body-balance batch and of the mass CG (MgpisDevice / MassBatch ::set_split, default on)
@@ -184,7 +185,8 @@ def test_schedule_variants_are_bit_identical(ddpca, gpu, monkeypatch, env, opts)
     columns from the 27-point stencil position, zero blocks where a row lacks a neighbour) against
     the column-indexed ones, on both option sets (the small one smooths the fine level with block
     Jacobi); and whole-replay pacing to the end of every solve against the one-iteration tail
-    graphs; and the MONITOR pair norms two launches per vector pair against one batch.  ADMM trajectory,
+    graphs; the MONITOR pair norms two launches per vector pair against one batch; and the colour
+    sweep's colour-0 launch fused into k_axpy (opt-in) against its own launch.  ADMM trajectory,
     displacements and PCG iteration counts equal bit for bit (8 ADMM iterations, reduced chain)."""
     H, M = getattr(ddpca, opts), ddpca.HEADLINE_MUSC
     if env[0] == "DDPCA_CODED":
