@@ -348,7 +348,7 @@ __global__ __launch_bounds__(256) void k_mcg_init_warm(EllArgs e, const double* 
 
 // q = A z + beta q, p = z + beta p; partial p.q per chunk
 __global__ __launch_bounds__(256) void k_mcg_spmv(EllArgs e, const PcgScal* sc, const double* z, double* q, double* p,
-                                                  double* partial) {
+                                                  double* partial, int ostride = 2) {
     const int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (c >= e.nch) return;
     const int sys = e.csys[c];
@@ -366,7 +366,44 @@ __global__ __launch_bounds__(256) void k_mcg_spmv(EllArgs e, const PcgScal* sc, 
     q[row] = qi;
     p[row] = pi;
     const double d = wsum(pi * qi);
-    if (lane == 0) partial[2 * c] = d;
+    if (lane == 0) partial[ostride * c] = d;
+}
+
+// k_mcg_axpy with alpha computed in place of a k_mcg_fin(kMcgAlpha) launch: every wave sums its
+// system's p.q chunk partials (ppq, written by k_mcg_spmv with stride 1 -- not the (r.r, r.z)
+// pairs this kernel writes) in one fixed order, so all waves hold the same alpha; the system's
+// first chunk stores alpha / p.q and the breakdown flag as k_mcg_fin did
+__global__ __launch_bounds__(256) void k_mcg_axpy_fa(EllArgs e, PcgScal* sc, double* x, double* r, double* z,
+                                                     const double* p, const double* q, double* partial,
+                                                     const double* ppq, const int64_t* cb, PcgMirror* mirror) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t c = i >> 6;
+    if (c >= e.nch) return;
+    const int sys = e.csys[c];
+    if (sc[sys].done) return;
+    const int lane = threadIdx.x & 63;
+    double pq = 0.0;
+    for (int64_t k = cb[sys] + lane; k < cb[sys + 1]; k += 64) pq += ppq[k];
+    pq = wsum(pq);
+    const double al = sc[sys].delta / pq;
+    if (c == cb[sys] && lane == 0) {
+        sc[sys].pq = pq;
+        sc[sys].alpha = al;
+        if (!(pq > 0.0) || !isfinite(pq)) {
+            sc[sys].fail = 1;
+            sc[sys].done = 1;
+            mirror_store(mirror + sys, sc[sys].iter, 1, 1);
+        }
+    }
+    x[i] += al * p[i];
+    const double ri = r[i] - al * q[i], zi = e.dinv[i] * ri;
+    r[i] = ri;
+    z[i] = zi;
+    const double a = wsum(ri * ri), b = wsum(ri * zi);
+    if (lane == 0) {
+        partial[2 * c] = a;
+        partial[2 * c + 1] = b;
+    }
 }
 
 // x += alpha p, r -= alpha q, z = D^-1 r; partials (r.r, r.z) per chunk
@@ -984,11 +1021,21 @@ private:
         EllArgs e{slots.p, off.p, col.p, val.p, csys.p, dinv.p, nch};
         hipGraph_t g;
         DDPCA_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+        // alpha inside k_mcg_axpy_fa (DDPCA_MCG_FUSE_ALPHA=0: its own k_mcg_fin launch; read at capture)
+        const char* ef = std::getenv("DDPCA_MCG_FUSE_ALPHA");
+        const bool fa = !(ef && std::atoi(ef) == 0);
+        double* ppq = partial.p + 2 * nch;  // p.q per chunk (the warm start's r.r slice, free by now)
         for (int64_t it = 0; it < iters; ++it) {
-            hipLaunchKernelGGL(k_mcg_spmv, dim3(ceil_div(nch, 4)), dim3(256), 0, s, e, scp, z.p, q.p, p.p, partial.p);
-            hipLaunchKernelGGL(k_mcg_fin, dim3(nsys), dim3(256), 0, s, (int)kMcgAlpha, partial.p, cb.p, scp, mirror.dev, nullptr);
-            hipLaunchKernelGGL(k_mcg_axpy, dim3(nb256(nrow)), dim3(256), 0, s, e, scp, x_target_, r.p, z.p, p.p, q.p,
-                               partial.p);
+            if (fa) {
+                hipLaunchKernelGGL(k_mcg_spmv, dim3(ceil_div(nch, 4)), dim3(256), 0, s, e, scp, z.p, q.p, p.p, ppq, 1);
+                hipLaunchKernelGGL(k_mcg_axpy_fa, dim3(nb256(nrow)), dim3(256), 0, s, e, scp, x_target_, r.p, z.p, p.p,
+                                   q.p, partial.p, (const double*)ppq, cb.p, mirror.dev);
+            } else {
+                hipLaunchKernelGGL(k_mcg_spmv, dim3(ceil_div(nch, 4)), dim3(256), 0, s, e, scp, z.p, q.p, p.p, partial.p, 2);
+                hipLaunchKernelGGL(k_mcg_fin, dim3(nsys), dim3(256), 0, s, (int)kMcgAlpha, partial.p, cb.p, scp, mirror.dev, nullptr);
+                hipLaunchKernelGGL(k_mcg_axpy, dim3(nb256(nrow)), dim3(256), 0, s, e, scp, x_target_, r.p, z.p, p.p, q.p,
+                                   partial.p);
+            }
             hipLaunchKernelGGL(k_mcg_fin, dim3(nsys), dim3(256), 0, s, (int)kMcgBeta, partial.p, cb.p, scp, mirror.dev, nullptr);
         }
         DDPCA_HIP(hipStreamEndCapture(s, &g));
