@@ -76,6 +76,7 @@ def parse():
     ap.add_argument("--coarse-level", type=int, default=H["coarse_level"],
                     help="V-cycle level of the exact dense coarse solve (-1: auto, 0: the reference's)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-stream-ceiling", action="store_true", help="skip the same-process STREAM ceiling")
     ap.add_argument("--traffic-json", default=os.environ.get("DDPCA_TRAFFIC_JSON", str(ROOT / "profiles" / "traffic.json")),
                     help="PMC-derived HBM bytes per launch of the roofline kernel (profiles/make_traffic.py)")
     return ap.parse_args()
@@ -176,11 +177,22 @@ def main():
         achieved = kbytes / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else None
         # PMC-measured HBM bytes per launch of the same kernel on the same configuration
         # (profiles/make_traffic.py); ignored when it was measured on another configuration
-        traffic = None
+        traffic, traffic_src = None, None
         if a.traffic_json and Path(a.traffic_json).exists():
             tj = json.loads(Path(a.traffic_json).read_text())
             if tj.get("config") == traffic_key(a):
                 traffic = tj.get("hbm_bytes_per_launch")
+                # PMC counters cannot be read inside this process (rocprofv3 --pmc is its own run):
+                # the figure is the committed measurement of this kernel on this configuration
+                traffic_src = f"replayed: {Path(a.traffic_json).relative_to(ROOT) if Path(a.traffic_json).is_relative_to(ROOT) else a.traffic_json}" \
+                              f" ({tj.get('source', 'rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE')})"
+        # this box's own STREAM ceiling, measured in this process after the timed region (SURVEY §8
+        # d3): boxes of this pool stream at different rates, so frac_of_stream is the figure that
+        # carries from one box to another; frac stays against the 8 TB/s spec peak
+        ceiling = None
+        if not a.no_stream_ceiling:
+            ceiling = D.stream_ceiling(local)
+            log(rank, f"STREAM ceiling: copy {ceiling['copy_gbs']:.0f} GB/s, read {ceiling['read_gbs']:.0f} GB/s")
         result = {
             "metric": "ADMM iters/sec",
             "value": n / elapsed,
@@ -229,11 +241,20 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS if achieved else None,
                 "traffic": traffic,
+                "traffic_source": traffic_src,
                 "algorithmic_bytes_per_launch": kbytes,
                 "avg_launch_ms": kern_ms,
                 "samples": int(tm["spmv_samples"]),
             },
         }
+        if ceiling is not None:
+            best = max(ceiling["copy_gbs"], ceiling["read_gbs"])
+            result["roofline"].update({
+                "stream_ceiling_gbs": {"copy": ceiling["copy_gbs"], "read": ceiling["read_gbs"],
+                                       "bytes_per_buffer": ceiling["bytes_per_buffer"]},
+                # against the higher of the two (the kernel's bytes are ~94 % reads)
+                "frac_of_stream": achieved / best if achieved else None,
+            })
         # whole-step roofline: the algorithmic bytes of EVERY kernel
         # of an ADMM iteration (byte model per kernel, DESIGN.md §3, summed over the members'
         # actual iteration counts) / the measured time per ADMM iteration / the HBM peak
@@ -249,6 +270,8 @@ def main():
             "step_split_bytes": {k: v / max(n, 1) for k, v in split.items()},
             "pcg_launches_per_admm_iter": by["pcg_launches"] / max(n, 1),
         })
+        if ceiling is not None:
+            result["roofline"]["step_frac_of_stream"] = step_bytes / step_s / 1e9 / max(ceiling["copy_gbs"], ceiling["read_gbs"])
         if world == 1 and not a.no_cpu_baseline:
             result["cpu_baseline"] = cpu_baseline(P, mc)
     # release device state before the process group

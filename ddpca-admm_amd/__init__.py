@@ -100,6 +100,7 @@ class _CsrArg(C.Structure):  # ddpca_csr_t
 def _declare(L: C.CDLL) -> None:
     L.ddpca_last_error.restype = C.c_char_p
     L.ddpca_gpu_available.restype = C.c_int
+    L.ddpca_stream_ceiling.argtypes = [C.c_int, C.c_int64, C.c_int, _DP]
     L.mgpis_default_options.argtypes = [C.POINTER(MgpisOptions)]
     L.mgpis_default_options.restype = None
     L.ddpca_problem_create.argtypes = [C.c_char_p, _DP, C.c_int, C.POINTER(_P)]
@@ -178,6 +179,9 @@ def _declare(L: C.CDLL) -> None:
         L.mcontact_gpu_bytes.argtypes = [_P, _DP, C.c_int64]
         L.mcontact_gpu_bytes.restype = C.c_int64
         L.mcontact_gpu_destroy.argtypes = [_P]
+        L.mcontact_gpu_comm_check.argtypes = [_P, C.c_int64]
+        L.ddpca_mass_solve.argtypes = [C.c_int, C.c_int64, C.POINTER(_CsrArg), _P, _P, C.c_double, C.c_int64, C.c_int,
+                                       _P]
 
 
 def _check(rc: int) -> int:
@@ -188,6 +192,13 @@ def _check(rc: int) -> int:
 
 def gpu_available() -> bool:
     return bool(lib().ddpca_gpu_available())
+
+
+def stream_ceiling(device: int = 0, nbytes: int = 2 << 30, reps: int = 10) -> dict:
+    """This box's STREAM copy / read bandwidth (ddpca_stream_ceiling), in GB/s."""
+    out = (C.c_double * 4)()
+    _check(lib().ddpca_stream_ceiling(device, int(nbytes), int(reps), out))
+    return dict(copy_gbs=out[0], read_gbs=out[1], copy_ms=out[2], read_ms=out[3], bytes_per_buffer=int(nbytes))
 
 
 def default_options(**kw) -> MgpisOptions:
@@ -725,6 +736,30 @@ def write_resuMoni(path: str, rows: np.ndarray) -> None:
     _check(lib().ddpca_write_resuMoni(str(path).encode(), _ptr(r), r.shape[0], r.shape[1]))
 
 
+def mass_solve(systems: Sequence, b: np.ndarray, rtol: float = 1e-14, maxit: int = 2000, fuse_alpha: int = -1,
+               device: int = 0):
+    """The ADMM loop's batched surface-mass Jacobi-PCG on its own (ddpca_mass_solve): systems = square
+    scipy CSR matrices, b their right-hand sides concatenated.  Returns (x, iterations per system);
+    a breakdown raises DdpcaError(DDPCA_ENUMERIC) with the last good iterate in the .x attribute."""
+    keep = []
+    arr = (_CsrArg * len(systems))()
+    for k, m in enumerate(systems):
+        m = m.tocsr()
+        ptr, col, val = (np.ascontiguousarray(m.indptr, np.int64), np.ascontiguousarray(m.indices, np.int32),
+                         np.ascontiguousarray(m.data, np.float64))
+        keep += [ptr, col, val]
+        arr[k] = _CsrArg(m.shape[0], m.shape[1], ptr.ctypes.data, col.ctypes.data, val.ctypes.data)
+    b = np.ascontiguousarray(b, dtype=np.float64)
+    x = np.zeros_like(b)
+    its = np.zeros(len(systems), np.int64)
+    rc = lib().ddpca_mass_solve(device, len(systems), arr, _ptr(b), _ptr(x), rtol, maxit, fuse_alpha, _ptr(its))
+    if rc < 0:
+        e = DdpcaError(rc, lib().ddpca_last_error().decode())
+        e.x, e.iters = x, its
+        raise e
+    return x, its
+
+
 class MCONTACT:
     """Device ADMM loop of MCONTACT::CONTACT_ANALYSIS (MCONTACT.h:2493-2845) for one rank."""
 
@@ -762,6 +797,11 @@ class MCONTACT:
         transport (mcontact_gpu_comm_local); run each rank's CONTACT_ANALYSIS on its own thread."""
         arr = (C.c_void_p * len(ranks))(*[m._h.value for m in ranks])
         _check(lib().mcontact_gpu_comm_local(arr, len(ranks)))
+
+    def comm_check(self, n: int = 1000) -> None:
+        """Collective transport check (mcontact_gpu_comm_check): tagged messages to every rank and an
+        all-reduce, every element exact; raises DdpcaError(DDPCA_ECOMM) otherwise."""
+        _check(lib().mcontact_gpu_comm_check(self._h, int(n)))
 
     def CONTACT_ANALYSIS(self, maxit: int = 3000, check: bool = True) -> int:
         return _check(lib().mcontact_gpu_iterate(self._h, maxit, 1 if check else 0))
@@ -818,7 +858,7 @@ class MCONTACT:
 
 
 __all__ = ["Problem", "MULTIGRID", "MGPIS", "MCONTACT", "DdpcaError", "lib", "gpu_available", "default_options",
-           "contact_search",
+           "contact_search", "mass_solve", "stream_ceiling",
            "LIBPATH", "HEADLINE_OPTIONS", "HEADLINE_OPTIONS_SMALL", "headline_options", "HEADLINE_MUSC",
            "HEADLINE_WORKLOAD",
            "headline_problem"]

@@ -34,6 +34,7 @@
 #include <condition_variable>
 #include <cstdio>
 #include <cstring>
+#include <deque>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -319,33 +320,6 @@ __global__ __launch_bounds__(256) void k_mcg_init(const double* b, const double*
     }
 }
 
-// warm start (MassBatch::solve from the previous solution x): r = b - A x, z = D^-1 r, p = q = 0;
-// partials (r.z, b.b) per chunk and r.r per chunk in prr; x is kept
-__global__ __launch_bounds__(256) void k_mcg_init_warm(EllArgs e, const double* b, const double* x, double* r, double* z,
-                                                       double* p, double* q, double* partial, double* prr) {
-    const int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (c >= e.nch) return;
-    const int lane = threadIdx.x & 63;
-    const int64_t row = c * 64 + lane;
-    const int ns = e.slots[c];
-    const int32_t* cp = e.col + e.off[c] * 64 + lane;
-    const double* vp = e.val + e.off[c] * 64 + lane;
-    double s = 0.0;
-#pragma unroll 4
-    for (int k = 0; k < ns; ++k) s += vp[(int64_t)k * 64] * x[cp[(int64_t)k * 64]];
-    const double bi = b[row], ri = bi - s, zi = e.dinv[row] * ri;
-    r[row] = ri;
-    z[row] = zi;
-    p[row] = 0.0;
-    q[row] = 0.0;
-    const double a = wsum(ri * zi), bb = wsum(bi * bi), rr = wsum(ri * ri);
-    if (lane == 0) {
-        partial[2 * c] = a;
-        partial[2 * c + 1] = bb;
-        prr[c] = rr;
-    }
-}
-
 // q = A z + beta q, p = z + beta p; partial p.q per chunk
 __global__ __launch_bounds__(256) void k_mcg_spmv(EllArgs e, const PcgScal* sc, const double* z, double* q, double* p,
                                                   double* partial, int ostride = 2) {
@@ -372,7 +346,12 @@ __global__ __launch_bounds__(256) void k_mcg_spmv(EllArgs e, const PcgScal* sc, 
 // k_mcg_axpy with alpha computed in place of a k_mcg_fin(kMcgAlpha) launch: every wave sums its
 // system's p.q chunk partials (ppq, written by k_mcg_spmv with stride 1 -- not the (r.r, r.z)
 // pairs this kernel writes) in one fixed order, so all waves hold the same alpha; the system's
-// first chunk stores alpha / p.q and the breakdown flag as k_mcg_fin did
+// first chunk stores alpha / p.q and the breakdown flag as k_mcg_fin did.  On a breakdown (p.q
+// not positive or not finite) every wave sees the same p.q and leaves x, r, z untouched, so x
+// keeps the last good iterate as with the separate k_mcg_fin launch.  Every wave re-reads its
+// system's partials (chunks^2 L2 reads per system), so MassBatch takes this form only up to
+// kMcgFuseMaxChunks chunks (65,536 rows) per system; the headline's sides have up to ~300.
+constexpr int64_t kMcgFuseMaxChunks = 1024;
 __global__ __launch_bounds__(256) void k_mcg_axpy_fa(EllArgs e, PcgScal* sc, double* x, double* r, double* z,
                                                      const double* p, const double* q, double* partial,
                                                      const double* ppq, const int64_t* cb, PcgMirror* mirror) {
@@ -386,15 +365,17 @@ __global__ __launch_bounds__(256) void k_mcg_axpy_fa(EllArgs e, PcgScal* sc, dou
     for (int64_t k = cb[sys] + lane; k < cb[sys + 1]; k += 64) pq += ppq[k];
     pq = wsum(pq);
     const double al = sc[sys].delta / pq;
+    const bool bad = !(pq > 0.0) || !isfinite(pq);  // the same in every wave of the system
     if (c == cb[sys] && lane == 0) {
         sc[sys].pq = pq;
         sc[sys].alpha = al;
-        if (!(pq > 0.0) || !isfinite(pq)) {
+        if (bad) {
             sc[sys].fail = 1;
             sc[sys].done = 1;
             mirror_store(mirror + sys, sc[sys].iter, 1, 1);
         }
     }
+    if (bad) return;
     x[i] += al * p[i];
     const double ri = r[i] - al * q[i], zi = e.dinv[i] * ri;
     r[i] = ri;
@@ -430,7 +411,7 @@ enum McgWhat { kMcgInit = 0, kMcgAlpha = 1, kMcgBeta = 2 };
 
 // per-system scalars: one workgroup per system, fixed order over its chunks
 __global__ __launch_bounds__(256) void k_mcg_fin(int what, const double* partial, const int64_t* cb, PcgScal* scv,
-                                                 PcgMirror* mirror, const double* prr = nullptr) {
+                                                 PcgMirror* mirror) {
     const int sys = blockIdx.x;
     PcgScal* sc = scv + sys;
     if (what != kMcgInit && sc->done) return;
@@ -459,20 +440,15 @@ __global__ __launch_bounds__(256) void k_mcg_fin(int what, const double* partial
     a = (r0[0] + r0[1]) + (r0[2] + r0[3]);
     b = (r1[0] + r1[1]) + (r1[2] + r1[3]);
     if (what == kMcgInit) {
-        // ||r0||^2: b.b from zero, the warm start's own r.r otherwise (one thread, chunk order)
-        double rr = b;
-        if (prr) {
-            rr = 0.0;
-            for (int64_t k = cb[sys]; k < k1; ++k) rr += prr[k];
-        }
+        // x0 = 0: ||r0||^2 = b.b
         sc->delta = a;
         sc->bb = b;
-        sc->rr = rr;
+        sc->rr = b;
         sc->tol2 = sc->tol2 * b;
         sc->beta = 0.0;
         sc->iter = 0;
         sc->fail = 0;
-        sc->done = (rr <= sc->tol2 || sc->maxit <= 0) ? 1 : 0;
+        sc->done = (b <= sc->tol2 || sc->maxit <= 0) ? 1 : 0;
         mirror_store(mirror + sys, 0, sc->done, 0);
     } else if (what == kMcgAlpha) {
         sc->pq = a;
@@ -493,33 +469,10 @@ __global__ __launch_bounds__(256) void k_mcg_fin(int what, const double* partial
     }
 }
 
-// partial[2b], partial[2b+1] = sum (a-o)^2, sum a^2 over block b of one vector pair
-__global__ void k_pair_norms(const double* a, const double* o, int64_t n, double* partial) {
-    __shared__ double r1[4], r2[4];
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    double d = 0.0, s = 0.0;
-    if (i < n) {
-        const double ai = a[i], di = ai - o[i];
-        d = di * di;
-        s = ai * ai;
-    }
-    d = wsum(d);
-    s = wsum(s);
-    if ((threadIdx.x & 63) == 0) {
-        r1[threadIdx.x >> 6] = d;
-        r2[threadIdx.x >> 6] = s;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        partial[2 * blockIdx.x] = (r1[0] + r1[1]) + (r1[2] + r1[3]);
-        partial[2 * blockIdx.x + 1] = (r2[0] + r2[1]) + (r2[2] + r2[3]);
-    }
-}
-
-// All MONITOR pair norms of an iteration in two launches (instead of two per vector pair): block b
-// of k_pair_norms_all is block b - blk0[g] of segment g = bseg[b], exactly the block k_pair_norms
-// would run for that segment, and k_reduce_pairs_all reduces segment g's blocks as k_reduce_pairs
-// does -- the same sums bit for bit
+// All MONITOR pair norms of an iteration in two launches (instead of two per vector pair, 3.63 ->
+// 3.40 ms interface step at the headline, profiles/r03ab): block b of k_pair_norms_all is block
+// b - blk0[g] of segment g = bseg[b] (256 elements, the pair's squared difference and square), and
+// k_reduce_pairs_all reduces segment g's blocks in one workgroup, a fixed order
 struct NormSeg {
     const double* a;
     const double* o;
@@ -571,26 +524,6 @@ __global__ void k_reduce_pairs_all(const NormSeg* seg, const double* partial, do
     if (threadIdx.x == 0) {
         moni[S.slot] = (r1[0] + r1[1]) + (r1[2] + r1[3]);
         moni[S.slot + 1] = (r2[0] + r2[1]) + (r2[2] + r2[3]);
-    }
-}
-
-__global__ void k_reduce_pairs(const double* partial, int64_t nb, double* out2) {
-    __shared__ double r1[4], r2[4];
-    double d = 0.0, s = 0.0;
-    for (int64_t k = threadIdx.x; k < nb; k += blockDim.x) {
-        d += partial[2 * k];
-        s += partial[2 * k + 1];
-    }
-    d = wsum(d);
-    s = wsum(s);
-    if ((threadIdx.x & 63) == 0) {
-        r1[threadIdx.x >> 6] = d;
-        r2[threadIdx.x >> 6] = s;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        out2[0] = (r1[0] + r1[1]) + (r1[2] + r1[3]);
-        out2[1] = (r2[0] + r2[1]) + (r2[2] + r2[3]);
     }
 }
 
@@ -844,20 +777,18 @@ public:
         // per CG iteration -- k_mcg_spmv: stored entries (12 B), z gathered once, z, q, p read
         // and q, p written; k_mcg_axpy: x, r read + written, z written, p, q, D^-1 read (112 B per row)
         init_bytes_.assign(nsys, 0.0);
-        init_warm_bytes_.clear();
         it_bytes_.assign(nsys, 0.0);
         for (int s = 0; s < nsys; ++s) {
             const double rows = (double)A[s]->nrow, ent = (double)A[s]->nnz();
             init_bytes_[s] = 56.0 * rows;
-            // warm: + the stored entries and x gathered once (r = b - A x)
-            init_warm_bytes_.push_back(56.0 * rows + 12.0 * ent + 8.0 * rows);
-            it_bytes_[s] = 12.0 * ent + 8.0 * rows + 40.0 * rows + 64.0 * rows;
+            // (+ the p.q and (r.r, r.z) chunk partials written once and read once: 24 B each way per chunk)
+            it_bytes_[s] = 12.0 * ent + 8.0 * rows + 40.0 * rows + 64.0 * rows + 48.0 * (double)(pad64(A[s]->nrow) / 64);
         }
         for (auto* v : {&b, &x, &r, &z, &p, &q}) {
             v->alloc(std::max<int64_t>(nrow, 2));
             v->zero();
         }
-        partial.alloc(3 * std::max<int64_t>(nch, 1));  // (a, b) pairs + the warm start's r.r
+        partial.alloc(3 * std::max<int64_t>(nch, 1));  // (a, b) pairs + the fused form's p.q
         sc.alloc(std::max(nsys, 1));
         DDPCA_HIP(hipHostMalloc(reinterpret_cast<void**>(&sc_host), std::max(nsys, 1) * sizeof(PcgScal)));
         mirror.alloc(nsys);
@@ -878,7 +809,6 @@ public:
         if (x_out != x_target_) {
             drop_graphs();
             x_target_ = x_out;
-            warm_ready_ = false;
         }
         if (!graph_) capture(s);
         mirror.reset();  // the previous solve on `s` was paced to completion before this point
@@ -888,23 +818,11 @@ public:
             sc_host[i].maxit = maxit;
         }
         DDPCA_HIP(hipMemcpyAsync(sc.p, sc_host, nsys * sizeof(PcgScal), hipMemcpyHostToDevice, s));
-        // opt-in warm start from the previous solution in x_out (DDPCA_MASS_WARM=1; the first
-        // solve into a buffer starts from zero): 39.3 -> 37.1 mass-CG iterations per ADMM
-        // iteration at the headline, no measurable gain (profiles/r03v), so off by default
-        const char* ew = std::getenv("DDPCA_MASS_WARM");
-        const bool warm = warm_ready_ && ew && std::atoi(ew) != 0;
-        if (warm) {
-            EllArgs e{slots.p, off.p, col.p, val.p, csys.p, dinv.p, nch};
-            hipLaunchKernelGGL(k_mcg_init_warm, dim3(ceil_div(nch, 4)), dim3(256), 0, s, e, b.p, x_out, r.p, z.p, p.p,
-                               q.p, partial.p, partial.p + 2 * nch);
-        } else {
-            hipLaunchKernelGGL(k_mcg_init, dim3(nb256(nrow)), dim3(256), 0, s, b.p, dinv.p, x_out, r.p, z.p, p.p, q.p,
-                               partial.p, nrow);
-        }
-        hipLaunchKernelGGL(k_mcg_fin, dim3(nsys), dim3(256), 0, s, (int)kMcgInit, partial.p, cb.p, sc.p, mirror.dev,
-                           warm ? partial.p + 2 * nch : nullptr);
-        warm_started_ = warm;
-        warm_ready_ = true;  // x_out holds this solve's result for the next one
+        // x0 = 0 (warm starts from the previous ADMM iteration's solution: 39.3 -> 37.1 mass-CG
+        // iterations at the headline, no measurable gain, profiles/r03v)
+        hipLaunchKernelGGL(k_mcg_init, dim3(nb256(nrow)), dim3(256), 0, s, b.p, dinv.p, x_out, r.p, z.p, p.p, q.p,
+                           partial.p, nrow);
+        hipLaunchKernelGGL(k_mcg_fin, dim3(nsys), dim3(256), 0, s, (int)kMcgInit, partial.p, cb.p, sc.p, mirror.dev);
         if (split_) {
             // fork into the two halves' streams, pace both, join and merge the scalars back
             hipLaunchKernelGGL(k_scal_split, dim3(ceil_div(nsys, 64)), dim3(64), 0, s, sc.p, sc_half_.p, half_.p, nsys);
@@ -951,15 +869,32 @@ public:
         split_ = on;
     }
 
+    // alpha inside k_mcg_axpy_fa: default while every system has at most kMcgFuseMaxChunks chunks
+    // (each wave re-reads its system's p.q partials); DDPCA_MCG_FUSE_ALPHA=0 forces the separate
+    // k_mcg_fin launch, =1 the fused form at any size (read at graph capture)
+    int fuse_override = -1;  // ddpca_mass_solve: 0 / 1 forces the form (tests), -1 the rule below
+    bool fuse_alpha() const {
+        if (fuse_override >= 0) return fuse_override != 0;
+        const char* ef = std::getenv("DDPCA_MCG_FUSE_ALPHA");
+        if (ef && std::atoi(ef) == 0) return false;
+        if (ef && std::atoi(ef) == 1) return true;
+        for (int s = 0; s < nsys; ++s)
+            if (cb_host_[s + 1] - cb_host_[s] > kMcgFuseMaxChunks) return false;
+        return true;
+    }
+
     // after the stream synchronised: iterations of the last solve, breakdown check
     void check() {
         last_iters = 0;
         expect_.resize(nsys);
         for (int i = 0; i < nsys; ++i) {
-            if (mirror.host[i].fail) throw ApiError(DDPCA_ENUMERIC, "surface mass CG breakdown");
+            if (mirror.host[i].fail) {
+                solved_ = false;
+                throw ApiError(DDPCA_ENUMERIC, "surface mass CG breakdown in system " + std::to_string(i));
+            }
             expect_[i] = mirror.host[i].iter;  // paces the next solve's tail
             last_iters = std::max<int64_t>(last_iters, mirror.host[i].iter);
-            if (solved_) alg_bytes += (warm_started_ ? init_warm_bytes_[i] : init_bytes_[i]) + (double)mirror.host[i].iter * it_bytes_[i];
+            if (solved_) alg_bytes += init_bytes_[i] + (double)mirror.host[i].iter * it_bytes_[i];
         }
         solved_ = false;
     }
@@ -999,10 +934,8 @@ private:
     DevBuf<int32_t> half_;
     std::vector<int> half_host_;
     std::vector<int64_t> cb_host_;
-    std::vector<double> init_bytes_, init_warm_bytes_, it_bytes_;
+    std::vector<double> init_bytes_, it_bytes_;
     bool solved_ = false;
-    bool warm_ready_ = false;    // x_target_ holds a previous solution (finite) to start from
-    bool warm_started_ = false;  // the last solve started from it
     void capture(hipStream_t s) {
         if (split_) {
             capture_one(s, sc_half_.p, &graph_h_[0], k);
@@ -1021,10 +954,8 @@ private:
         EllArgs e{slots.p, off.p, col.p, val.p, csys.p, dinv.p, nch};
         hipGraph_t g;
         DDPCA_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
-        // alpha inside k_mcg_axpy_fa (DDPCA_MCG_FUSE_ALPHA=0: its own k_mcg_fin launch; read at capture)
-        const char* ef = std::getenv("DDPCA_MCG_FUSE_ALPHA");
-        const bool fa = !(ef && std::atoi(ef) == 0);
-        double* ppq = partial.p + 2 * nch;  // p.q per chunk (the warm start's r.r slice, free by now)
+        const bool fa = fuse_alpha();
+        double* ppq = partial.p + 2 * nch;  // p.q per chunk
         for (int64_t it = 0; it < iters; ++it) {
             if (fa) {
                 hipLaunchKernelGGL(k_mcg_spmv, dim3(ceil_div(nch, 4)), dim3(256), 0, s, e, scp, z.p, q.p, p.p, ppq, 1);
@@ -1032,11 +963,11 @@ private:
                                    q.p, partial.p, (const double*)ppq, cb.p, mirror.dev);
             } else {
                 hipLaunchKernelGGL(k_mcg_spmv, dim3(ceil_div(nch, 4)), dim3(256), 0, s, e, scp, z.p, q.p, p.p, partial.p, 2);
-                hipLaunchKernelGGL(k_mcg_fin, dim3(nsys), dim3(256), 0, s, (int)kMcgAlpha, partial.p, cb.p, scp, mirror.dev, nullptr);
+                hipLaunchKernelGGL(k_mcg_fin, dim3(nsys), dim3(256), 0, s, (int)kMcgAlpha, partial.p, cb.p, scp, mirror.dev);
                 hipLaunchKernelGGL(k_mcg_axpy, dim3(nb256(nrow)), dim3(256), 0, s, e, scp, x_target_, r.p, z.p, p.p, q.p,
                                    partial.p);
             }
-            hipLaunchKernelGGL(k_mcg_fin, dim3(nsys), dim3(256), 0, s, (int)kMcgBeta, partial.p, cb.p, scp, mirror.dev, nullptr);
+            hipLaunchKernelGGL(k_mcg_fin, dim3(nsys), dim3(256), 0, s, (int)kMcgBeta, partial.p, cb.p, scp, mirror.dev);
         }
         DDPCA_HIP(hipStreamEndCapture(s, &g));
         DDPCA_HIP(hipGraphInstantiate(out, g, nullptr, nullptr, 0));
@@ -1144,8 +1075,16 @@ struct LocalHub {
     int arrived = 0;
     int64_t generation = 0;
     bool broken = false;
-    std::vector<std::vector<double>> slot;                       // allreduce staging per rank
-    std::map<std::tuple<int, int, int64_t>, const double*> post;  // (src, dst, tag) -> device send buffer
+    std::vector<std::vector<double>> slot;  // allreduce staging per rank
+    // posted sends per (src, dst) in issue order -- matched against the receiver's receives from
+    // src in ITS issue order, as RCCL matches grouped ncclSend / ncclRecv pairs per peer (tags and
+    // sizes are only checked, never used for matching: an ordering bug fails here as on the wire)
+    struct Posted {
+        int64_t tag;
+        const double* buf;
+        int64_t n;
+    };
+    std::map<std::pair<int, int>, std::deque<Posted>> post;
     void barrier() {
         std::unique_lock<std::mutex> lk(mu);
         if (broken) throw ApiError(DDPCA_ECOMM, "local transport: a peer failed");
@@ -1182,23 +1121,44 @@ struct LocalTransport : Transport {
         DDPCA_HIP(hipStreamSynchronize(st));
         {
             std::lock_guard<std::mutex> lk(hub->mu);
-            for (const Msg& m : msgs) hub->post[{rank, m.peer, m.tag}] = m.send;
+            for (const Msg& m : msgs) hub->post[{rank, m.peer}].push_back({m.tag, m.send, m.n});
         }
         hub->barrier();
+        std::string err;
         for (const Msg& m : msgs) {
-            const double* src = nullptr;
+            LocalHub::Posted p{};
             {
                 std::lock_guard<std::mutex> lk(hub->mu);
-                auto it = hub->post.find({m.peer, rank, m.tag});
-                if (it == hub->post.end()) throw ApiError(DDPCA_ECOMM, "local transport: unmatched receive");
-                src = it->second;
+                auto& q = hub->post[{m.peer, rank}];
+                if (q.empty()) {
+                    err = "local transport: receive from rank " + std::to_string(m.peer) + " has no matching send";
+                    break;
+                }
+                p = q.front();
+                q.pop_front();
             }
-            DDPCA_HIP(hipMemcpyAsync(m.recv, src, m.n * sizeof(double), hipMemcpyDeviceToDevice, st));
+            if (p.tag != m.tag || p.n != m.n) {
+                err = "local transport: message order differs between ranks " + std::to_string(m.peer) + " and " +
+                      std::to_string(rank) + " (tag " + std::to_string(p.tag) + " sent, " + std::to_string(m.tag) +
+                      " expected)";
+                break;
+            }
+            DDPCA_HIP(hipMemcpyAsync(m.recv, p.buf, m.n * sizeof(double), hipMemcpyDeviceToDevice, st));
         }
         DDPCA_HIP(hipStreamSynchronize(st));
+        if (!err.empty()) {
+            std::lock_guard<std::mutex> lk(hub->mu);
+            hub->broken = true;
+            hub->cv.notify_all();
+            throw ApiError(DDPCA_ECOMM, err);
+        }
         hub->barrier();  // the peers' send buffers stay untouched until every copy has landed
         std::lock_guard<std::mutex> lk(hub->mu);
-        for (const Msg& m : msgs) hub->post.erase({rank, m.peer, m.tag});
+        for (const Msg& m : msgs)
+            if (!hub->post[{rank, m.peer}].empty()) {
+                hub->broken = true;
+                throw ApiError(DDPCA_ECOMM, "local transport: a send to rank " + std::to_string(m.peer) + " was not received");
+            }
     }
 };
 
@@ -1250,7 +1210,7 @@ struct ddpca_mcontact {
     double* u = nullptr;
     double* state = nullptr;
     double* gamma = nullptr;
-    DevBuf<double> uo, state_old, gcst, partial, moni;
+    DevBuf<double> uo, state_old, gcst, moni;
     // the MONITOR pair norms as one batch (k_pair_norms_all): segments, block -> segment
     std::vector<NormSeg> norm_seg_host;
     DevBuf<NormSeg> norm_seg;
@@ -1281,7 +1241,7 @@ struct ddpca_mcontact {
     CoarseDev cs;
     std::vector<double> moni_host;
     hipStream_t main = nullptr;          // == mg->stream
-    std::unique_ptr<Transport> comm;     // nranks > 1: RCCL, or the in-process test transport
+    std::unique_ptr<Transport> comm;     // RCCL (any rank count, 1 included), or the in-process test transport
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     // reference MONITOR state (MCONTACT.h:2494-2498, 2725-2845)
     int64_t tc = 0;
@@ -1710,10 +1670,6 @@ void build(ddpca_mcontact& H, Problem& P) {
         // MONITOR: snapshots of u and [aux, lambda] (read + written), the pair norms (16 B per entry)
         H.bytes_moni = 16.0 * (nu + 2.0 * rows) + 16.0 * (nu + 2.0 * rows);
     }
-    int64_t maxn = 1;
-    for (auto& S : H.subs) maxn = std::max(maxn, std::max(3 * S.nn, S.nh));
-    for (auto& sd : H.sides) maxn = std::max(maxn, sd.m);
-    H.partial.alloc(2 * nb256(maxn));
     // monitor norms [2 nsub u | 8 nint aux, lambda | 2 nsub hanging-level parts of u]
     const int64_t nmon = 4 * H.nsub + 8 * H.nint;
     H.moni.alloc(nmon);
@@ -2096,10 +2052,8 @@ void coarse_invert(ddpca_mcontact& H) {
     A.upload(C.dense);
     std::vector<double>().swap(C.dense);
     hipStream_t st = H.main;
-    if (H.nranks > 1) {
-        if (!H.comm) throw ApiError(DDPCA_ESTATE, "the coarse space of a multi-rank run needs mcontact_gpu_comm_init");
-        H.comm->allreduce_sum(A.p, n * n, st);
-    }
+    if (H.nranks > 1 && !H.comm) throw ApiError(DDPCA_ESTATE, "the coarse space of a multi-rank run needs mcontact_gpu_comm_init");
+    if (H.comm) H.comm->allreduce_sum(A.p, n * n, st);
     rocblas_handle rh = nullptr;
     if (rocblas_create_handle(&rh) != rocblas_status_success) throw ApiError(DDPCA_EHIP, "rocblas_create_handle");
     DevBuf<rocblas_int> info(2);
@@ -2171,7 +2125,7 @@ void coarse_correct(ddpca_mcontact& H) {
                                (int64_t)G.rows.n);
         }
     }
-    if (H.nranks > 1) H.comm->allreduce_sum(C.g.p, n, st);
+    if (H.comm) H.comm->allreduce_sum(C.g.p, n, st);
     if (!C.nown) return;
     if (C.mg) {  // mgpi_1.CG_SOLV(1, globForc, globSolu) (MCONTACT.h:2594), on the coarse solver's stream
         MgpisDevice& M = *C.cmg;
@@ -2197,12 +2151,6 @@ void coarse_correct(ddpca_mcontact& H) {
     hipLaunchKernelGGL(k_cs_scatter, dim3(nb256(C.nxn)), dim3(256), 0, st, C.xsrc.p, C.xc.p, C.xn.p, C.nxn);
     hipLaunchKernelGGL(k_cs_prolong, dim3(nb256(C.qnn)), dim3(256), 0, st, C.qcol.p, C.qw.p, C.qnn, C.xn.p, C.flag.p,
                        H.presc.p, H.u);
-}
-
-void pair_norm(ddpca_mcontact& H, const double* a, const double* o, int64_t n, int64_t slot) {
-    const int nb = nb256(n);
-    hipLaunchKernelGGL(k_pair_norms, dim3(nb), dim3(256), 0, H.main, a, o, n, H.partial.p);
-    hipLaunchKernelGGL(k_reduce_pairs, dim3(1), dim3(256), 0, H.main, H.partial.p, (int64_t)nb, H.moni.p + slot);
 }
 
 // Reference MONITOR (MCONTACT.h:2725-2845) on the reduced norms; true = converged.
@@ -2366,10 +2314,7 @@ bool iterate_once(ddpca_mcontact& H, bool check) {
             add(H.state + sd.roff, H.state_old.p + sd.roff, sd.m, base);
             add(H.state + H.R + sd.roff, H.state_old.p + H.R + sd.roff, sd.m, base + 2);
         }
-        const char* eb = std::getenv("DDPCA_NORMS_BATCHED");  // 0: two launches per pair (A/B)
-        if (eb && std::atoi(eb) == 0) {
-            for (const NormSeg& g : seg) pair_norm(H, g.a, g.o, g.n, g.slot);
-        } else if (!seg.empty()) {
+        if (!seg.empty()) {
             // the segments are the same every iteration: upload once (and again if they change)
             const bool same = seg.size() == H.norm_seg_host.size() &&
                               std::memcmp(seg.data(), H.norm_seg_host.data(), seg.size() * sizeof(NormSeg)) == 0;
@@ -2389,7 +2334,7 @@ bool iterate_once(ddpca_mcontact& H, bool check) {
                                H.norm_partial.p, H.moni.p);
         }
     }
-    if (H.nranks > 1) H.comm->allreduce_sum(H.moni.p, H.moni.n, st);
+    if (H.comm) H.comm->allreduce_sum(H.moni.p, H.moni.n, st);
     DDPCA_HIP(hipEventRecord(H.ev[3], st));
     DDPCA_HIP(hipMemcpyAsync(H.moni_host.data(), H.moni.p, H.moni.n * sizeof(double), hipMemcpyDeviceToHost, st));
     if (H.mg) H.mg->pcg_fetch();
@@ -2485,8 +2430,11 @@ int mcontact_gpu_unique_id(void* out128) {
 
 int mcontact_gpu_comm_init(mcontact_t h, const void* uid) {
     return guarded([&] {
+        if (!h || !uid) throw ApiError(DDPCA_EINVAL, "handle / unique id");
         select_device(h->device);
-        if (h->nranks == 1) return;
+        if (h->comm) throw ApiError(DDPCA_ESTATE, "handle already has a communicator");
+        // nranks == 1 builds a one-rank communicator too: the MONITOR and coarse-RHS all-reduces then
+        // run through RCCL on the solve stream (bit-identical to the run without one)
         ncclUniqueId id;
         std::memcpy(&id, uid, sizeof(id));
         auto t = std::make_unique<RcclTransport>();
@@ -2531,6 +2479,47 @@ int mcontact_gpu_comm_local(mcontact_t* handles, int n) {
     });
 }
 
+int mcontact_gpu_comm_check(mcontact_t h, int64_t n) {
+    return guarded([&] {
+        if (!h || n < 1) throw ApiError(DDPCA_EINVAL, "handle / n");
+        select_device(h->device);
+        if (!h->comm) throw ApiError(DDPCA_ESTATE, "no communicator (mcontact_gpu_comm_init / _comm_local)");
+        const int R = h->nranks, me = h->rank;
+        hipStream_t st = h->main;
+        // exchange: to every rank q (me included) two messages in the order q, then 2 q + 1 tags;
+        // message (me -> q, k) carries v = 1e6 me + 1e3 q + k + i 2^-20 (exact in fp64)
+        auto val = [](int src, int dst, int k, int64_t i) { return 1.0e6 * src + 1.0e3 * dst + k + std::ldexp((double)i, -20); };
+        std::vector<double> hs((size_t)R * 2 * n);
+        for (int q = 0; q < R; ++q)
+            for (int k = 0; k < 2; ++k)
+                for (int64_t i = 0; i < n; ++i) hs[((size_t)q * 2 + k) * n + i] = val(me, q, k, i);
+        DevBuf<double> sbuf, rbuf((size_t)R * 2 * n), ar(n);
+        sbuf.upload(hs);
+        std::vector<Transport::Msg> msgs;
+        for (int q = 0; q < R; ++q)
+            for (int k = 0; k < 2; ++k)
+                msgs.push_back({q, 2 * (int64_t)q + k, sbuf.p + ((size_t)q * 2 + k) * n, rbuf.p + ((size_t)q * 2 + k) * n, n});
+        h->comm->exchange(msgs, st);
+        // all-reduce: rank r contributes (r + 1) (i + 1); the sum is R (R + 1) / 2 (i + 1)
+        std::vector<double> ha(n);
+        for (int64_t i = 0; i < n; ++i) ha[i] = (double)(me + 1) * (double)(i + 1);
+        DDPCA_HIP(hipMemcpyAsync(ar.p, ha.data(), n * sizeof(double), hipMemcpyHostToDevice, st));
+        h->comm->allreduce_sum(ar.p, n, st);
+        DDPCA_HIP(hipStreamSynchronize(st));
+        const auto hr = rbuf.download();
+        const auto hsum = ar.download();
+        for (int q = 0; q < R; ++q)
+            for (int k = 0; k < 2; ++k)
+                for (int64_t i = 0; i < n; ++i)
+                    if (hr[((size_t)q * 2 + k) * n + i] != val(q, me, k, i))
+                        throw ApiError(DDPCA_ECOMM, "comm check: message " + std::to_string(k) + " from rank " + std::to_string(q) +
+                                                        " arrived wrong at element " + std::to_string(i));
+        for (int64_t i = 0; i < n; ++i)
+            if (hsum[i] != 0.5 * R * (R + 1) * (double)(i + 1))
+                throw ApiError(DDPCA_ECOMM, "comm check: all-reduce element " + std::to_string(i) + " wrong");
+    });
+}
+
 int64_t mcontact_gpu_iterate(mcontact_t h, int64_t maxit, int check) {
     int64_t n = 0;
     const int rc = guarded([&] {
@@ -2539,6 +2528,7 @@ int64_t mcontact_gpu_iterate(mcontact_t h, int64_t maxit, int check) {
         for (double& b : h->bytes) b = 0.0;
         h->mass_iters = 0.0;
         if (h->mg) h->mg->time_kernel = true;
+        if (h->nranks > 1 && !h->comm) throw ApiError(DDPCA_ESTATE, "a multi-rank run needs mcontact_gpu_comm_init");
         for (; n < maxit;) {
             const bool conv = iterate_once(*h, check != 0);
             ++n;
@@ -2641,6 +2631,76 @@ int64_t mcontact_gpu_bytes(mcontact_t h, double* out, int64_t cap) {
     if (out)
         for (int64_t i = 0; i < std::min(n, cap); ++i) out[i] = h->bytes[i];
     return n;
+}
+
+int ddpca_mass_solve(int device, int64_t nsys, const ddpca_csr_t* A, const double* b, double* x, double rtol,
+                     int64_t maxit, int fuse_alpha, int64_t* iters) {
+    int64_t nrow = 0;
+    std::vector<int64_t> roff;
+    std::vector<Csr> sys;
+    DevBuf<double> xd;
+    MassBatch mb;
+    hipStream_t st = nullptr;
+    auto copy_out = [&]() {  // the systems' rows of the padded batch vector, in order
+        std::vector<double> h(std::max<int64_t>(nrow, 1));
+        DDPCA_HIP(hipMemcpy(h.data(), xd.p, nrow * sizeof(double), hipMemcpyDeviceToHost));
+        int64_t o = 0;
+        for (int64_t s = 0; s < nsys; ++s) {
+            std::memcpy(x + o, h.data() + roff[s], sys[s].nrow * sizeof(double));
+            o += sys[s].nrow;
+        }
+    };
+    const int rc = guarded([&] {
+        if (nsys < 1 || !A || !b || !x || !(rtol > 0.0) || maxit < 1) throw ApiError(DDPCA_EINVAL, "ddpca_mass_solve: arguments");
+        select_device(device);
+        for (int64_t s = 0; s < nsys; ++s) {
+            const ddpca_csr_t& a = A[s];
+            if (a.nrow < 1 || a.ncol != a.nrow || !a.ptr || (a.ptr[a.nrow] > 0 && (!a.col || !a.val)))
+                throw ApiError(DDPCA_EINVAL, "ddpca_mass_solve: system " + std::to_string(s) + " is not a square CSR");
+            Csr c;
+            c.nrow = c.ncol = a.nrow;
+            c.ptr.assign(a.ptr, a.ptr + a.nrow + 1);
+            if (c.ptr[0] != 0) throw ApiError(DDPCA_EINVAL, "ddpca_mass_solve: ptr[0] != 0");
+            for (int64_t r = 0; r < a.nrow; ++r)
+                if (c.ptr[r + 1] < c.ptr[r]) throw ApiError(DDPCA_EINVAL, "ddpca_mass_solve: row pointer decreases");
+            c.col.assign(a.col, a.col + c.ptr[a.nrow]);
+            c.val.assign(a.val, a.val + c.ptr[a.nrow]);
+            bool diag = false;
+            for (int64_t r = 0; r < a.nrow; ++r)
+                for (int64_t k = c.ptr[r]; k < c.ptr[r + 1]; ++k) {
+                    if (c.col[k] < 0 || c.col[k] >= a.nrow) throw ApiError(DDPCA_EINVAL, "ddpca_mass_solve: column out of range");
+                    diag |= c.col[k] == r;
+                }
+            if (!diag) throw ApiError(DDPCA_EINVAL, "ddpca_mass_solve: a system without diagonal entries");
+            roff.push_back(nrow);
+            nrow += pad64(a.nrow);
+            sys.push_back(std::move(c));
+        }
+        std::vector<const Csr*> ptrs;
+        for (const Csr& c : sys) ptrs.push_back(&c);
+        mb.build(ptrs, roff, nrow);
+        mb.fuse_override = fuse_alpha;
+        std::vector<double> hb(nrow, 0.0);
+        int64_t o = 0;
+        for (int64_t s = 0; s < nsys; ++s) {
+            std::memcpy(hb.data() + roff[s], b + o, sys[s].nrow * sizeof(double));
+            o += sys[s].nrow;
+        }
+        DDPCA_HIP(hipMemcpy(mb.b.p, hb.data(), nrow * sizeof(double), hipMemcpyHostToDevice));
+        xd.alloc(nrow);
+        DDPCA_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+        mb.solve(st, xd.p, rtol, maxit);
+        DDPCA_HIP(hipStreamSynchronize(st));
+        if (iters)
+            for (int64_t s = 0; s < nsys; ++s) iters[s] = mb.mirror.host[s].iter;
+        copy_out();
+        mb.check();  // DDPCA_ENUMERIC on a breakdown (x already copied: the last good iterate)
+    });
+    if (st) {
+        (void)hipStreamSynchronize(st);
+        (void)hipStreamDestroy(st);
+    }
+    return rc;
 }
 
 int mcontact_gpu_destroy(mcontact_t h) {

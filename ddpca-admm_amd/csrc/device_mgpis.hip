@@ -52,21 +52,7 @@ struct SellArgs {
     const double* tab;     // table mode: tstride doubles per table row, slot-major 3x3 blocks
     int64_t tstride;
     const int32_t* ctype;  // table mode: chunk -> its rows' common table row, -1 = mixed
-    // stencil-coded copy (LevelDev::coded): per chunk position mask / row-split sub-masks /
-    // first slot, per member strides, last node of the level (gathers clamp into the level)
-    const uint32_t* cm;
-    const uint32_t* cmq;
-    const int64_t* coff;
-    const int32_t* lstr;
-    int64_t nlast;
 };
-
-// column of stencil position q (0..26 = (dz+1) 9 + (dy+1) 3 + (dx+1)) for a row of a lattice
-// with strides nx, nxy, clamped into [0, hi] (a zero block's gather stays inside the level)
-__device__ __forceinline__ int64_t stencil_col(int64_t row, int q, int64_t nx, int64_t nxy, int64_t hi) {
-    const int64_t j = row + (int64_t)(q / 9 - 1) * nxy + (int64_t)((q / 3) % 3 - 1) * nx + (q % 3 - 1);
-    return j < 0 ? 0 : (j > hi ? hi : j);
-}
 
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
@@ -253,18 +239,6 @@ __device__ __forceinline__ void sell_rows(const CT* colp, const T* valp, const d
     }
 }
 
-// Stencil-coded rows (LevelDev::coded): slot k = the k-th set bit of the wave-uniform mask m, its
-// column arithmetic on scalar registers -- the x gathers depend on nothing loaded
-template <typename T>
-__device__ __forceinline__ void sell_rows_coded(uint32_t m, const T* valp, const double* x, int64_t row, int64_t nx,
-                                                int64_t nxy, int64_t hi, double& s0, double& s1, double& s2) {
-    constexpr int64_t SV = slot_vals<T>() * kChunk;
-    m = __builtin_amdgcn_readfirstlane(m);
-#pragma unroll 3
-    for (int k = 0; m; ++k, m &= m - 1)
-        block_fma(valp + (int64_t)k * SV, x + 3 * stencil_col(row, __builtin_ctz(m), nx, nxy, hi), s0, s1, s2);
-}
-
 // Table mode: the row's blocks are the 9-double records tv[9k .. 9k+8] of its table row (shared
 // with every row of the same type, so they come from L1/L2), columns prefetched one group ahead.
 __device__ __forceinline__ void sell_rows_tbl(const int32_t* colp, const double* tv, const double* x, int ns,
@@ -364,13 +338,6 @@ __global__ __launch_bounds__(kBlock) void k_sell(SellArgs a, const double* __res
                                                 s0, s1, s2);
         else
             sell_rows_tbl(a.col + base * kChunk + lane, tab + (int64_t)a.rtype[row] * a.tstride, a.x, ns, s0, s1, s2);
-    } else if constexpr (std::is_same<CT, uint32_t>::value) {
-        // stencil-coded copy (CT = uint32_t tags it)
-        (void)ns;
-        (void)base;
-        const int64_t cb = a.coff[c];
-        sell_rows_coded<T>(a.cm[c], static_cast<const T*>(a.val) + cb * slot_vals<T>() * kChunk + lane, a.x, row,
-                           a.lstr[2 * sub], a.lstr[2 * sub + 1], a.nlast, s0, s1, s2);
     } else if constexpr (sizeof(CT) == 2)
         sell_rows<V, T, CT>(a.col16 + base * kChunk + lane, static_cast<const T*>(a.val) + base * slot_vals<T>() * kChunk + lane,
                             a.x, ns, row, s0, s1, s2);
@@ -451,20 +418,7 @@ __global__ __launch_bounds__(kBlock) void k_sell_split(SellArgs a) {
     const int64_t base = a.off[c];
     constexpr int64_t SV = slot_vals<T>() * kChunk;
     double s0 = 0.0, s1 = 0.0, s2 = 0.0;
-    if constexpr (std::is_same<CT, uint32_t>::value) {
-        // stencil-coded copy: lane group g takes the positions of its sub-mask (slots k = g mod 4)
-        (void)base;
-        (void)ns;
-        const T* valp = static_cast<const T*>(a.val) + a.coff[c] * SV + rin;
-        const uint32_t m = a.cm[c];
-        const int64_t nx = a.lstr[2 * sub], nxy = a.lstr[2 * sub + 1];
-#pragma unroll 2
-        for (uint32_t mg = a.cmq[4 * c + g]; mg; mg &= mg - 1) {
-            const int q = __builtin_ctz(mg);
-            const int k = __popc(m & ((1u << q) - 1u));
-            block_fma_any<true>(valp + (int64_t)k * SV, a.x + 3 * stencil_col(row, q, nx, nxy, a.nlast), s0, s1, s2, rin);
-        }
-    } else {
+    {
         const T* valp = static_cast<const T*>(a.val) + base * SV + rin;
         const CT* colp;
         if constexpr (sizeof(CT) == 2) colp = a.col16 + base * kChunk + rin;
@@ -499,14 +453,6 @@ __global__ __launch_bounds__(kBlock) void k_sell_split(SellArgs a) {
     }
 }
 
-// Workgroup b is dispatched to XCD b % 8: the logical block that makes XCD x own the x-th
-// contiguous run of the grid (runs of q+1 blocks for the first r XCDs, q for the rest; G = 8q + r)
-__device__ __forceinline__ int64_t xcd_slab_block() {
-    const int64_t G = gridDim.x, b = blockIdx.x, q = G / 8, r = G % 8, x = b % 8, k = b / 8;
-    const int64_t start = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q;
-    return start + k;
-}
-
 // Multicolour block Gauss-Seidel on the fine level (GsFine): one wavefront per colour chunk,
 // lane = one row of that colour.  PH 0: forward sweep from zero over the L part, x_i = M_i (b_i -
 // L_i x); PH 1: the residual after the forward sweep, r_i = -U_i x (every chunk, one launch);
@@ -530,12 +476,7 @@ struct GsArgs {
     double* r;
     const PcgScal* sc;
     double* partial;
-    int xcd;  // 1: workgroups mapped so each XCD takes one contiguous run of the launch's chunks
-    const float* minvc;  // chunk-ordered fp32 inverses (GsFine::minvc) or null: minv by row
-    const uint32_t* lm;  // stencil-coded chunks: L / U position masks, member strides, last node
-    const uint32_t* um;
-    const int32_t* lstr;
-    int64_t nlast;
+    const float* minvc;  // chunk-ordered fp32 inverses (GsFine::minvc), or null (fp64 copy): minv by row
 };
 
 // the colour sweep's per-row tail: PH 1 stores r = -s; PH 0 / 2 store x = M (b - s) and return
@@ -574,11 +515,12 @@ __device__ __forceinline__ double gs_epilogue(const GsArgs& a, int64_t c, int ln
     return dotv;
 }
 
-template <int PH, bool DOT, typename T, typename CT, int V = 1>
-__global__ __launch_bounds__(kBlock) void k_gs(GsArgs a) {
-    const int lane = threadIdx.x & 63;
-    const int64_t blk = a.xcd ? xcd_slab_block() : (int64_t)blockIdx.x;
-    const int64_t li = blk * (blockDim.x >> 6) + (threadIdx.x >> 6);
+// One wave per workgroup: a colour's chunks spread over more CUs than four-wave groups (+1 % at 8
+// subdomains per GPU, profiles/r03j)
+template <int PH, bool DOT, typename T, typename CT>
+__global__ __launch_bounds__(kWave) void k_gs(GsArgs a) {
+    const int lane = threadIdx.x;
+    const int64_t li = blockIdx.x;
     if (li >= a.n) return;
     const int64_t c = a.list ? (int64_t)a.list[li] : li;
     const int sub = a.csub[c];
@@ -589,82 +531,20 @@ __global__ __launch_bounds__(kBlock) void k_gs(GsArgs a) {
     constexpr int64_t SV = slot_vals<T>() * kChunk;
     const T* val = static_cast<const T*>(a.val);
     double s0 = 0.0, s1 = 0.0, s2 = 0.0;
-    if constexpr (std::is_same<CT, uint32_t>::value) {
-        // stencil-coded colour chunks (GsFine::coded): the L and U position masks
-        const int64_t nx = a.lstr[2 * sub], nxy = a.lstr[2 * sub + 1];
-        if (PH != 1) sell_rows_coded<T>(a.lm[c], val + a.offl[c] * SV + lane, a.x, row, nx, nxy, a.nlast, s0, s1, s2);
-        if (PH != 0) sell_rows_coded<T>(a.um[c], val + a.offu[c] * SV + lane, a.x, row, nx, nxy, a.nlast, s0, s1, s2);
-    } else {
-        const CT* colp;
-        if constexpr (sizeof(CT) == 2) colp = a.col16;
-        else colp = a.col;
-        if (PH != 1) {
-            const int64_t o = a.offl[c];
-            sell_rows<V, T, CT>(colp + o * kChunk + lane, val + o * SV + lane, a.x, a.nsl[c], row, s0, s1, s2);
-        }
-        if (PH != 0) {
-            const int64_t o = a.offu[c];
-            sell_rows<V, T, CT>(colp + o * kChunk + lane, val + o * SV + lane, a.x, a.nsu[c], row, s0, s1, s2);
-        }
+    const CT* colp;
+    if constexpr (sizeof(CT) == 2) colp = a.col16;
+    else colp = a.col;
+    if (PH != 1) {
+        const int64_t o = a.offl[c];
+        sell_rows<1, T, CT>(colp + o * kChunk + lane, val + o * SV + lane, a.x, a.nsl[c], row, s0, s1, s2);
+    }
+    if (PH != 0) {
+        const int64_t o = a.offu[c];
+        sell_rows<1, T, CT>(colp + o * kChunk + lane, val + o * SV + lane, a.x, a.nsu[c], row, s0, s1, s2);
     }
     const double dotv = gs_epilogue<PH, DOT, T>(a, c, lane, row, real, s0, s1, s2);
     if (DOT) chunk_partial(dotv, a.partial, c);
 }
-
-// Row-split colour sweep for small launches (opt-in: up to DDPCA_GS_SPLIT_CHUNKS chunks, measured
-// no faster at 2 or 4 subdomains per GPU): one workgroup per colour chunk, each of
-// its four waves 16 of the chunk's rows, each lane a quarter of its row's L / U slots (k = g,
-// g + 4, ...), the quarters summed by lane shuffles -- four times the waves in flight and a
-// quarter of the dependent column -> x chain per lane (as k_sell_split for the block-Jacobi
-// levels).  The dot partial of the chunk: per wave, then the four waves in order through LDS.
-template <int PH, bool DOT, typename T, typename CT>
-__global__ __launch_bounds__(kBlock) void k_gs_split(GsArgs a) {
-    const int64_t li = blockIdx.x;
-    const int64_t c = a.list ? (int64_t)a.list[li] : li;
-    const int sub = a.csub[c];
-    if (stopped(a.sc, sub)) return;  // uniform over the workgroup
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int rin = w * 16 + (lane & 15), g = lane >> 4;
-    const int32_t rr = a.rowidx[c * kChunk + rin];
-    const bool real = rr >= 0;
-    const int64_t row = real ? rr : ~rr;
-    constexpr int64_t SV = slot_vals<T>() * kChunk;
-    const T* val = static_cast<const T*>(a.val);
-    const CT* colp;
-    if constexpr (sizeof(CT) == 2) colp = a.col16;
-    else colp = a.col;
-    double s0 = 0.0, s1 = 0.0, s2 = 0.0;
-    if (PH != 1) {
-        const int64_t o = a.offl[c];
-        const int ns = a.nsl[c];
-#pragma unroll 2
-        for (int k = g; k < ns; k += 4)
-            block_fma_any<true>(val + (o + k) * SV + rin, a.x + 3 * col_of(colp[(o + k) * kChunk + rin], row), s0, s1, s2, rin);
-    }
-    if (PH != 0) {
-        const int64_t o = a.offu[c];
-        const int ns = a.nsu[c];
-#pragma unroll 2
-        for (int k = g; k < ns; k += 4)
-            block_fma_any<true>(val + (o + k) * SV + rin, a.x + 3 * col_of(colp[(o + k) * kChunk + rin], row), s0, s1, s2, rin);
-    }
-    s0 += __shfl_xor(s0, 16, 64);
-    s1 += __shfl_xor(s1, 16, 64);
-    s2 += __shfl_xor(s2, 16, 64);
-    s0 += __shfl_xor(s0, 32, 64);
-    s1 += __shfl_xor(s1, 32, 64);
-    s2 += __shfl_xor(s2, 32, 64);
-    double dotv = 0.0;
-    if (g == 0) dotv = gs_epilogue<PH, DOT, T>(a, c, rin, row, real, s0, s1, s2);
-    if (DOT) {
-        __shared__ double wp[kBlock / kWave];
-        dotv = wave_sum(dotv);
-        if (lane == 0) wp[w] = dotv;
-        __syncthreads();
-        if (threadIdx.x == 0) a.partial[c] = (wp[0] + wp[1]) + (wp[2] + wp[3]);
-    }
-}
-
 
 // Node-parallel kernels: thread = node, 256 nodes per workgroup; a wavefront is one chunk, so
 // the subdomain (and its stop flag) is uniform per wavefront.  nn is a multiple of 64.
@@ -755,11 +635,8 @@ template <bool INIT, bool BJ, bool SETD, typename MT = double>
 __global__ __launch_bounds__(kBlock) void k_restrict_lat(const double* rf, const uint32_t* rmsk, const int32_t* rf0,
                                                          const int32_t* rstr, const uint8_t* cmask, double* bc,
                                                          double* xc, double* dc, const MT* minv, const double* coef,
-                                                         int64_t nc, const int32_t* csub, const PcgScal* sc, int xcd) {
-    // xcd: each XCD takes one contiguous eighth of the coarse nodes (workgroup b runs on XCD
-    // b % 8), so the fine planes two neighbouring coarse planes share are fetched into one L2
-    const int64_t blk = xcd ? xcd_slab_block() : (int64_t)blockIdx.x;
-    const int64_t i = blk * kBlock + threadIdx.x;
+                                                         int64_t nc, const int32_t* csub, const PcgScal* sc) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= nc) return;
     const int sub = csub[i >> 6];
     if (stopped(sc, sub)) return;
@@ -993,84 +870,6 @@ __global__ __launch_bounds__(kBlock) void k_axpy(double* x, double* r, const dou
     chunk_partial(s, partial, c);
 }
 
-// k_axpy fused with the V-cycle's first fine-level sweep x0 = omega M r_new (k_jac0 from a zero
-// guess, block Jacobi with the fp32 3x3 inverses): the new residual goes through LDS from the
-// chunk-flat layout to one node per lane, so r is not read again.  Same arithmetic on the same
-// values as k_axpy + k_jac0, bit for bit.  (Members that converge in this iteration compute an
-// x0 nobody reads: the V-cycle's launches skip them.)
-__global__ __launch_bounds__(kBlock) void k_axpy_jac0(double* x, double* r, const double* p, const double* q,
-                                                      const PcgScal* sc, double* partial, int64_t nn,
-                                                      const int32_t* csub, const float* minv, const double* coef,
-                                                      double* x0) {
-    __shared__ double rl[kBlock / kWave][3 * kChunk];
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int64_t c = (int64_t)blockIdx.x * (kBlock / kWave) + w;
-    const int sub = c * kChunk < nn ? csub[c] : 0;
-    const bool live = c * kChunk < nn && !stopped(sc, sub);  // wave-uniform
-    if (live) {
-        const double al = sc[sub].alpha;
-        const int64_t base = c * 3 * kChunk + lane;
-        double s = 0.0;
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-            const int64_t k = base + j * kChunk;
-            x[k] += al * p[k];
-            const double v = r[k] - al * q[k];
-            r[k] = v;
-            s += v * v;
-            rl[w][lane + j * kChunk] = v;
-        }
-        chunk_partial(s, partial, c);
-    }
-    __syncthreads();
-    if (!live) return;
-    const int64_t i = c * kChunk + lane;
-    const double om = coef[2 * sub + 1];
-    double m0, m1, m2;
-    apply_m<true>(minv, i, rl[w][3 * lane], rl[w][3 * lane + 1], rl[w][3 * lane + 2], m0, m1, m2);
-    x0[3 * i] = om * m0;
-    x0[3 * i + 1] = om * m1;
-    x0[3 * i + 2] = om * m2;
-}
-
-// k_axpy fused with the colour sweep's first launch (GsFine, forward from zero): colour 0 has no
-// earlier colour, so its rows' sweep is z_i = M_i r_i -- computed here from the new residual (via
-// LDS, as k_axpy_jac0) for the rows flagged in is0, the same operations on the same values as
-// k_gs<0> on colour 0 (bit for bit), one launch per PCG iteration fewer
-__global__ __launch_bounds__(kBlock) void k_axpy_gs0(double* x, double* r, const double* p, const double* q,
-                                                     const PcgScal* sc, double* partial, int64_t nn, const int32_t* csub,
-                                                     const float* minv, const uint8_t* is0, double* z) {
-    __shared__ double rl[kBlock / kWave][3 * kChunk];
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int64_t c = (int64_t)blockIdx.x * (kBlock / kWave) + w;
-    const int sub = c * kChunk < nn ? csub[c] : 0;
-    const bool live = c * kChunk < nn && !stopped(sc, sub);  // wave-uniform
-    if (live) {
-        const double al = sc[sub].alpha;
-        const int64_t base = c * 3 * kChunk + lane;
-        double s = 0.0;
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-            const int64_t k = base + j * kChunk;
-            x[k] += al * p[k];
-            const double v = r[k] - al * q[k];
-            r[k] = v;
-            s += v * v;
-            rl[w][lane + j * kChunk] = v;
-        }
-        chunk_partial(s, partial, c);
-    }
-    __syncthreads();
-    if (!live) return;
-    const int64_t i = c * kChunk + lane;
-    if (!is0[i]) return;
-    double m0, m1, m2;
-    apply_m<true>(minv, i, rl[w][3 * lane], rl[w][3 * lane + 1], rl[w][3 * lane + 2], m0, m1, m2);
-    z[3 * i] = m0;
-    z[3 * i + 1] = m1;
-    z[3 * i + 2] = m2;
-}
-
 // z = D^-1 r (diagonal preconditioner, DIAG_PREC), partial r^T z
 __global__ __launch_bounds__(kBlock) void k_diag(const double* r, const double* dinv, double* z, double* partial,
                                                  int64_t nn, const int32_t* csub, const PcgScal* sc) {
@@ -1095,10 +894,9 @@ __global__ __launch_bounds__(kBlock) void k_dot(const double* x, const double* y
 
 // Scalar updates of the PCG recurrence: one workgroup per subdomain, fixed summation order
 // over that subdomain's chunk partials.  Stop-state changes are mirrored to host memory.
-// kFinT threads: 1024 (default) reads a subdomain's ~6400 fine chunk partials in ~2 loads each;
-// 256 needs only four free wave slots on one CU (placed sooner while the other half of a split
-// batch streams) -- measured 0.2-0.6 % slower overall, kept for A/B (DDPCA_FIN_THREADS=256)
-template <int kFinT>
+// kFinT = 1024 threads read a subdomain's ~6400 fine chunk partials in ~2 loads each (256: 0.2-0.6 %
+// slower overall, profiles/r02u_ab.json)
+constexpr int kFinT = 1024;
 __global__ __launch_bounds__(kFinT) void k_fin(int what, const double* partial, const double* partial2,
                                                const int64_t* cb, PcgScal* scv, PcgMirror* mirror) {
     const int sub = blockIdx.x;
@@ -1677,82 +1475,12 @@ bool lattice_transfer(LevelDev& L, const LevelDev& C, const std::vector<int32_t>
     return true;
 }
 
-// Stencil position (0..26, (dz+1) 9 + (dy+1) 3 + (dx+1)) of the column offset d on a lattice
-// with strides nx >= 3, nxy >= 3 nx, or -1
-int stencil_code(int64_t d, int64_t nx, int64_t nxy) {
-    auto rdiv = [](int64_t a, int64_t b) { return a >= 0 ? (a + b / 2) / b : -((-a + b / 2) / b); };
-    const int64_t dz = rdiv(d, nxy), r = d - dz * nxy, dy = rdiv(r, nx), dx = r - dy * nx;
-    if (dz < -1 || dz > 1 || dy < -1 || dy > 1 || dx < -1 || dx > 1) return -1;
-    return (int)((dz + 1) * 9 + (dy + 1) * 3 + (dx + 1));
-}
-
-// DDPCA_CODED=1 (or 2) builds the stencil-coded V-cycle copies (read at create).  Opt-in: per
-// launch the coded colour sweeps and level sweeps ran 2-6 % shorter, yet the headline lost 2.5 %
-// (16.78 vs 17.22 ADMM it/s alternating in one call, profiles/r03r; 2: the level copies alone,
-// 17.05 vs 17.15, r03t)
-bool coded_wanted() {
-    const char* e = std::getenv("DDPCA_CODED");
-    return e && std::atoi(e) != 0;
-}
-
-// Box-lattice strides (nx, nx ny) of every member of a level from its device-ordered host SELL
-// arrays, or empty when the level is not a lattice: nx, nxy from a row with 26 neighbours (its
-// positive offsets 1, nx-1, nx, nx+1, nxy-nx-1, ...), then every block of every row must sit at
-// a stencil offset of its member, a position repeated within a row (the padding slots repeat the
-// row's own column) only with zero values.  The generators' boxes and their lexicographic device
-// numbering pass; general meshes keep the column-indexed copy.
-std::vector<int32_t> lattice_strides(const LevelDev& L, const std::vector<int32_t>& csub, const std::vector<int64_t>& off,
-                                     const std::vector<int32_t>& col, const std::vector<double>& val) {
-    const int ns = (int)L.noff.size();
-    std::vector<int32_t> st(2 * ns, 0);
-    for (int s = 0; s < ns; ++s) {
-        int64_t nx = 0, nxy = 0;
-        std::vector<int64_t> d;
-        for (int64_t g = L.noff[s]; g < L.noff[s] + L.nloc[s] && nx == 0; ++g) {
-            const int64_t c = g / kChunk, lane = g % kChunk;
-            d.clear();
-            for (int64_t q = off[c]; q < off[c + 1]; ++q) {
-                const int64_t j = col[q * kChunk + lane];
-                if (j > g) d.push_back(j - g);
-            }
-            std::sort(d.begin(), d.end());
-            d.erase(std::unique(d.begin(), d.end()), d.end());
-            if (d.size() != 13 || d[0] != 1) continue;
-            const int64_t ax = d[2], axy = d[4] + d[2] + 1;
-            if (d[1] == ax - 1 && d[3] == ax + 1 && d[5] == axy - ax && d[8] == axy && d[12] == axy + ax + 1) {
-                nx = ax;
-                nxy = axy;
-            }
-        }
-        if (nx < 3 || nxy < 3 * nx || nxy > INT32_MAX) return {};
-        st[2 * s] = (int32_t)nx;
-        st[2 * s + 1] = (int32_t)nxy;
-    }
-    int bad = 0;
-#pragma omp parallel for schedule(static) reduction(| : bad)
-    for (int64_t c = 0; c < L.nch; ++c) {
-        const int s = csub[c];
-        for (int64_t lane = 0; lane < kChunk; ++lane) {
-            const int64_t g = c * kChunk + lane;
-            uint32_t seen = 0;
-            for (int64_t q = off[c]; q < off[c + 1]; ++q) {
-                const int code = stencil_code((int64_t)col[q * kChunk + lane] - g, st[2 * s], st[2 * s + 1]);
-                if (code < 0) { bad = 1; break; }
-                if ((seen >> code) & 1u)
-                    for (int ij = 0; ij < 9; ++ij) bad |= val[(q * 9 + ij) * kChunk + lane] != 0.0;
-                seen |= 1u << code;
-            }
-        }
-    }
-    if (bad) return {};
-    return st;
-}
-
 // The fine level's colour structure (GsFine) from its host SELL arrays (col: batch device
-// columns, val: masked fp64 blocks val[(q * 9 + ij) * 64 + lane]); vt: the V-cycle copy's type;
-// lstr: the level's lattice strides (empty: not a lattice -- column-indexed colour chunks).
+// columns, val: masked fp64 blocks val[(q * 9 + ij) * 64 + lane]); vt: the V-cycle copy's type.
+// A colour's rows go to chunks in device order, i.e. along the x lines of a box (16 x 16-node
+// tiles of one plane measured 1.8 % slower at the headline, profiles/r03i).
 void build_gs(GsFine& G, const LevelDev& L, int nsub, const std::vector<int64_t>& off, const std::vector<int32_t>& col,
-              const std::vector<double>& val, int vt, const std::vector<int32_t>& lstr) {
+              const std::vector<double>& val, int vt) {
     // greedy colouring in device order, per member
     std::vector<int8_t> colour(L.nn, -1);
     std::vector<int> ncol_sub(nsub, 0);
@@ -1781,55 +1509,13 @@ void build_gs(GsFine& G, const LevelDev& L, int nsub, const std::vector<int64_t>
     std::vector<std::vector<int64_t>> rows((size_t)nsub * K);
     for (int s = 0; s < nsub; ++s)
         for (int64_t g = L.noff[s]; g < L.noff[s] + L.nloc[s]; ++g) rows[(size_t)s * K + colour[g]].push_back(g);
-    // a member that is a full nx x ny x nz box in lexicographic device order (the generators'
-    // meshes): its colour rows go to chunks tile by tile -- 16 x 16 nodes of one plane, i.e.
-    // 8 x 8 rows of a colour -- instead of along the x lines (a chunk of 64 rows of one colour
-    // spans 128 nodes of x, more than a line), so a chunk's neighbour gathers stay in ~18 x 18 x 3
-    // nodes
-    // (measured 1.8 % slower at the headline, profiles/r03i: opt-in DDPCA_GS_TILE=1)
-    static const bool tile = std::getenv("DDPCA_GS_TILE") && std::atoi(std::getenv("DDPCA_GS_TILE")) != 0;
-    int tiled = 0;
-    for (int s = 0; s < nsub && tile; ++s) {
-        // nx, nx*ny from the column offsets of an interior row (the first past the member's middle
-        // with 26 neighbours): positive offsets 1, nx - 1, nx, nx + 1, nx ny - nx - 1, ...
-        std::vector<int64_t> d;
-        for (int64_t g = L.noff[s] + L.nloc[s] / 2; g < L.noff[s] + L.nloc[s] && d.size() != 13; ++g) {
-            const int64_t c = g / kChunk, lane = g % kChunk;
-            d.clear();
-            int64_t nb = 0;
-            for (int64_t q = off[c]; q < off[c + 1]; ++q) {
-                const int64_t j = col[q * kChunk + lane];
-                nb += j != g;
-                if (j > g) d.push_back(j - g);
-            }
-            std::sort(d.begin(), d.end());
-            d.erase(std::unique(d.begin(), d.end()), d.end());
-            if (nb != 26) d.clear();
-        }
-        if (d.size() != 13 || d[0] != 1) continue;
-        const int64_t nx = d[1] + 1, nxy = d[4] + nx + 1;
-        if (d[2] != nx || d[3] != nx + 1 || nxy % nx || L.nloc[s] % nxy) continue;
-        const int64_t ny = nxy / nx;
-        for (int k = 0; k < K; ++k) {
-            auto& R = rows[(size_t)s * K + k];
-            std::stable_sort(R.begin(), R.end(), [&](int64_t u, int64_t v) {
-                const int64_t lu = u - L.noff[s], lv = v - L.noff[s];
-                const int64_t zu = lu / nxy, zv = lv / nxy, yu = lu % nxy / nx, yv = lv % nxy / nx, xu = lu % nx, xv = lv % nx;
-                return std::make_tuple(zu, yu / 16, xu / 16, yu, xu) < std::make_tuple(zv, yv / 16, xv / 16, yv, xv);
-            });
-        }
-        (void)ny;
-        ++tiled;
-    }
     std::vector<int32_t> rowidx, csub, nsl, nsu;
     std::vector<int64_t> offl, offu, cb(nsub + 1, 0);
-    std::vector<uint32_t> lmk, umk;  // stencil positions of each chunk's L and U blocks (lattice levels)
     std::vector<std::vector<int32_t>> bycol(K);
     std::vector<int64_t> base;  // first row of each chunk in its (s, k) list
     std::vector<size_t> lists;
     G.nnzb_sub.assign(nsub, 0);
     G.slots_sub.assign(nsub, 0);
-    bool coded = !lstr.empty();
     for (int s = 0; s < nsub; ++s) {
         cb[s] = (int64_t)csub.size();
         for (int k = 0; k < K; ++k) {
@@ -1841,50 +1527,37 @@ void build_gs(GsFine& G, const LevelDev& L, int nsub, const std::vector<int64_t>
                 base.push_back((int64_t)r0);
                 lists.push_back((size_t)s * K + k);
                 int32_t ml = 0, mu = 0;
-                uint32_t lmask = 0, umask = 0;
                 for (size_t i = r0; i < std::min(R.size(), r0 + kChunk); ++i) {
                     const int64_t g = R[i], nc = g / kChunk, lane = g % kChunk;
                     int32_t nl = 0, nu = 0;
                     for (int64_t q = off[nc]; q < off[nc + 1]; ++q) {
                         const int64_t j = col[q * kChunk + lane];
                         if (j == g) continue;
-                        const bool lower = colour[j] < k;
-                        if (lower) ++nl;
+                        if (colour[j] < k) ++nl;
                         else ++nu;
-                        if (coded) {
-                            const int code = stencil_code(j - g, lstr[2 * s], lstr[2 * s + 1]);
-                            (lower ? lmask : umask) |= 1u << code;
-                        }
                     }
                     ml = std::max(ml, nl);
                     mu = std::max(mu, nu);
                     G.nnzb_sub[s] += nl + nu;
                 }
-                coded = coded && (lmask & umask) == 0;
                 nsl.push_back(ml);
                 nsu.push_back(mu);
-                lmk.push_back(lmask);
-                umk.push_back(umask);
             }
         }
     }
     const int64_t nch = (int64_t)csub.size();
     cb[nsub] = nch;
-    // slots per chunk: the longest row's L and U counts, or (coded) one per stencil position
+    // slots per chunk: the longest row's L and U counts
     int64_t nslot = 0;
     for (int64_t c = 0; c < nch; ++c) {
-        if (coded) {
-            nsl[c] = __builtin_popcount(lmk[c]);
-            nsu[c] = __builtin_popcount(umk[c]);
-        }
         offl.push_back(nslot);
         offu.push_back(nslot + nsl[c]);
         nslot += nsl[c] + nsu[c];
         G.slots_sub[csub[c]] += nsl[c] + nsu[c];
     }
     rowidx.assign(nch * kChunk, 0);
-    const bool c16 = !coded && L.col16.p != nullptr;
-    std::vector<int32_t> gcol(c16 || coded ? 0 : std::max<int64_t>(nslot * kChunk, 1), 0);
+    const bool c16 = L.col16.p != nullptr;
+    std::vector<int32_t> gcol(c16 ? 0 : std::max<int64_t>(nslot * kChunk, 1), 0);
     std::vector<int16_t> gcol16(c16 ? std::max<int64_t>(nslot * kChunk, 1) : 0, 0);
     const int nv = vt == kValH16 ? 10 : 9;
     std::vector<uint16_t> v16(vt == kValH16 ? std::max<int64_t>(nslot * nv * kChunk, 1) : 0, 0);
@@ -1900,28 +1573,19 @@ void build_gs(GsFine& G, const LevelDev& L, int nsub, const std::vector<int64_t>
             const int64_t g = real ? R[r0 + lane] : R[r0];
             rowidx[c * kChunk + lane] = real ? (int32_t)g : ~(int32_t)g;
             // pad slots: the row itself (offset 0), zero blocks
-            for (int64_t q = offl[c]; q < offl[c] + nsl[c] + nsu[c] && !coded; ++q) {
+            for (int64_t q = offl[c]; q < offl[c] + nsl[c] + nsu[c]; ++q) {
                 if (c16) gcol16[q * kChunk + lane] = 0;
                 else gcol[q * kChunk + lane] = (int32_t)g;
             }
             if (!real) continue;
             const int64_t nc = g / kChunk, nl = g % kChunk;
-            const int s = csub[c];
             int64_t ql = offl[c], qu = offu[c];
             for (int64_t q = off[nc]; q < off[nc + 1]; ++q) {
                 const int64_t j = col[q * kChunk + nl];
                 if (j == g) continue;
-                const bool lower = colour[j] < k;
-                int64_t t;
-                if (coded) {
-                    // the rank of the block's stencil position among the chunk's L (U) positions
-                    const uint32_t below = (1u << stencil_code(j - g, lstr[2 * s], lstr[2 * s + 1])) - 1u;
-                    t = lower ? offl[c] + __builtin_popcount(lmk[c] & below) : offu[c] + __builtin_popcount(umk[c] & below);
-                } else {
-                    t = lower ? ql++ : qu++;
-                }
+                const int64_t t = colour[j] < k ? ql++ : qu++;
                 if (c16) gcol16[t * kChunk + lane] = (int16_t)(j - g);
-                else if (!coded) gcol[t * kChunk + lane] = (int32_t)j;
+                else gcol[t * kChunk + lane] = (int32_t)j;
                 double blk[9];
                 for (int ij = 0; ij < 9; ++ij) blk[ij] = val[(q * 9 + ij) * kChunk + nl];
                 if (vt == kValH16) {
@@ -1966,23 +1630,14 @@ void build_gs(GsFine& G, const LevelDev& L, int nsub, const std::vector<int64_t>
     G.offl.upload(offl);
     G.offu.upload(offu);
     G.cb.upload(cb);
-    {
-        std::vector<uint8_t> is0(L.nn, 0);  // rows of colour 0 (k_axpy_gs0)
-        for (int64_t g = 0; g < L.nn; ++g) is0[g] = colour[g] == 0 ? 1 : 0;
-        G.is0.upload(is0);
-    }
-    G.coded = coded;
-    if (coded) {
-        G.lm.upload(lmk);
-        G.um.upload(umk);
-    } else if (c16) G.col16.upload(gcol16);
+    if (c16) G.col16.upload(gcol16);
     else G.col.upload(gcol);
     if (vt == kValH16) G.val16.upload(v16);
     else if (vt == kVal32) G.val32.upload(v32);
     else G.val64.upload(v64);
     if (std::getenv("DDPCA_VERBOSE"))
-        std::fprintf(stderr, "[ddpca] fine level: multicolour Gauss-Seidel, %d colours, %lld chunks, %lld slots, %d of %d members tiled, stencil-coded %d\n",
-                     K, (long long)nch, (long long)nslot, tiled, nsub, (int)coded);
+        std::fprintf(stderr, "[ddpca] fine level: multicolour Gauss-Seidel, %d colours, %lld chunks, %lld slots\n", K,
+                     (long long)nch, (long long)nslot);
 }
 }  // namespace
 
@@ -2153,58 +1808,13 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
         // dense inverse).  Table-mode levels need neither.
         const bool vc32 = opt.precond_fp32 != 0 && nlev > 1;
         const int64_t nslot = L.nslots;
-        // stencil-coded V-cycle copy on box-lattice levels (its own val16 / val32 array)
-        std::vector<int32_t> lstr_h;
-        if (!L.tbl && vc32 && l >= 1 && coded_wanted()) lstr_h = lattice_strides(L, csub, off, col, val);
-        std::vector<int64_t> coff_h;
-        std::vector<uint32_t> cm_h;
-        if (!lstr_h.empty()) {
-            cm_h.assign(L.nch, 0u);
-            coff_h.assign(L.nch + 1, 0);
-            std::vector<uint32_t> cmq_h(4 * L.nch, 0u);
-#pragma omp parallel for schedule(static)
-            for (int64_t c = 0; c < L.nch; ++c) {
-                const int s = csub[c];
-                uint32_t m = 0;
-                for (int64_t lane = 0; lane < kChunk; ++lane)
-                    for (int64_t q = off[c]; q < off[c + 1]; ++q)
-                        m |= 1u << stencil_code((int64_t)col[q * kChunk + lane] - (c * kChunk + lane), lstr_h[2 * s],
-                                                lstr_h[2 * s + 1]);
-                cm_h[c] = m;
-                int k = 0;
-                for (uint32_t r = m; r; r &= r - 1, ++k) cmq_h[4 * c + (k & 3)] |= r & (~r + 1u);
-            }
-            for (int64_t c = 0; c < L.nch; ++c) coff_h[c + 1] = coff_h[c] + __builtin_popcount(cm_h[c]);
-            L.coded = true;
-            L.ncslots = coff_h[L.nch];
-            L.lstr.upload(lstr_h);
-            L.cm.upload(cm_h);
-            L.cmq.upload(cmq_h);
-            L.coff.upload(coff_h);
-        }
-        // destination slot of every (sorted slot, lane) in the V-cycle copy: itself, or (coded) the
-        // rank of its stencil position in the chunk's mask, -1 for a repeated position (padding)
+        // every (slot, lane) of the V-cycle copy, in the Krylov operator's slot order
         auto for_vc_slots = [&](auto&& put) {
 #pragma omp parallel for schedule(static)
-            for (int64_t c = 0; c < L.nch; ++c) {
-                const int s = csub[c];
-                for (int64_t lane = 0; lane < kChunk; ++lane) {
-                    uint32_t seen = 0;
-                    for (int64_t q = off[c]; q < off[c + 1]; ++q) {
-                        int64_t dst = q;
-                        if (L.coded) {
-                            const int code = stencil_code((int64_t)col[q * kChunk + lane] - (c * kChunk + lane),
-                                                          lstr_h[2 * s], lstr_h[2 * s + 1]);
-                            if ((seen >> code) & 1u) continue;
-                            seen |= 1u << code;
-                            dst = coff_h[c] + __builtin_popcount(cm_h[c] & ((1u << code) - 1u));
-                        }
-                        put(q, dst, lane);
-                    }
-                }
-            }
+            for (int64_t q = 0; q < nslot; ++q)
+                for (int64_t lane = 0; lane < kChunk; ++lane) put(q, q, lane);
         };
-        const int64_t vc_nslot = L.coded ? L.ncslots : nslot;
+        const int64_t vc_nslot = nslot;
         if (!L.tbl && (l == nlev - 1 || !vc32)) {
             std::vector<double> v64(val.size());
 #pragma omp parallel for schedule(static)
@@ -2254,9 +1864,7 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
         if (l == nlev - 1 && nlev > 1 && opt.smoother == 3) {
             // the V-cycle copy's storage type of this level (vc_type once the level is up)
             const int vt = (!vc32 || L.tbl) ? kVal64 : L.val16.p ? kValH16 : kVal32;
-            // (DDPCA_CODED=2: coded level copies, column-indexed colour chunks -- diagnostics)
-            const char* ec = std::getenv("DDPCA_CODED");
-            build_gs(gs, L, nsub, off, col, val, vt, ec && std::atoi(ec) == 2 ? std::vector<int32_t>{} : lstr_h);
+            build_gs(gs, L, nsub, off, col, val, vt);
         }
         L.mask.upload(mask);
         for (auto* v : {&L.x, &L.t, &L.b, &L.r, &L.d}) {
@@ -2652,7 +2260,6 @@ void launch_sell(int vt, const SellArgs& a, hipStream_t s) {
     const int grid = ceil_div(a.nch, 4);
     constexpr int V = default_variant(MODE);
     using I16 = int16_t;
-    using U32 = uint32_t;  // column type tag of the stencil-coded copy
     // small levels: the row-split kernel (DDPCA_SPLIT_CHUNKS = the largest level it takes, in chunks)
     // (read per launch: launches are captured into graphs once per handle, and tests switch it)
     const char* esp = std::getenv("DDPCA_SPLIT_CHUNKS");
@@ -2661,10 +2268,7 @@ void launch_sell(int vt, const SellArgs& a, hipStream_t s) {
     if constexpr (!DOT && (MODE == kResid || MODE == kJac)) {
         if (!a.tab && a.nch <= split_max) {
             const dim3 gs((unsigned)a.nch);
-            if (a.cm) {
-                if (vt == kValH16) hipLaunchKernelGGL((k_sell_split<MODE, BJ, uint16_t, U32>), gs, dim3(kBlock), 0, s, a);
-                else hipLaunchKernelGGL((k_sell_split<MODE, BJ, float, U32>), gs, dim3(kBlock), 0, s, a);
-            } else if (a.col16) {
+            if (a.col16) {
                 if (vt == kValH16) hipLaunchKernelGGL((k_sell_split<MODE, BJ, uint16_t, I16>), gs, dim3(kBlock), 0, s, a);
                 else if (vt == kVal32) hipLaunchKernelGGL((k_sell_split<MODE, BJ, float, I16>), gs, dim3(kBlock), 0, s, a);
                 else hipLaunchKernelGGL((k_sell_split<MODE, BJ, double, I16>), gs, dim3(kBlock), 0, s, a);
@@ -2675,10 +2279,7 @@ void launch_sell(int vt, const SellArgs& a, hipStream_t s) {
         }
     }
     if (a.tab) hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, double, V, true>), dim3(grid), dim3(kBlock), 0, s, a, a.tab);
-    else if (a.cm) {
-        if (vt == kValH16) hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, uint16_t, V, false, U32>), dim3(grid), dim3(kBlock), 0, s, a, a.tab);
-        else hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, float, V, false, U32>), dim3(grid), dim3(kBlock), 0, s, a, a.tab);
-    } else if (a.col16) {
+    else if (a.col16) {
         if (vt == kValH16) hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, uint16_t, V, false, I16>), dim3(grid), dim3(kBlock), 0, s, a, a.tab);
         else if (vt == kVal32) hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, float, V, false, I16>), dim3(grid), dim3(kBlock), 0, s, a, a.tab);
         else hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, double, V, false, I16>), dim3(grid), dim3(kBlock), 0, s, a, a.tab);
@@ -2725,13 +2326,6 @@ SellArgs vc_level_args(const MgpisDevice& D, int level) {
     if (vt == kValH16) a.val = L.val16.p;
     else if (vt == kVal32) a.val = L.val32.p;
     if (vt != kVal64) a.minv = L.minv32.p;
-    if (vt != kVal64 && L.coded) {
-        a.cm = L.cm.p;
-        a.cmq = L.cmq.p;
-        a.coff = L.coff.p;
-        a.lstr = L.lstr.p;
-        a.nlast = L.nn - 1;
-    }
     return a;
 }
 }  // namespace
@@ -2745,9 +2339,8 @@ void launch_restrict(const LevelDev& F, int grid, hipStream_t st, const double* 
     // stored weights: deriving them from a gathered parent count (as k_prolong<true> does)
     // measured 58 -> 102 us on the fine level (profiles/r01_transfer_weights.txt)
     if (F.lat) {
-        static const int xcd = std::getenv("DDPCA_XCD_RESTRICT") ? std::atoi(std::getenv("DDPCA_XCD_RESTRICT")) : 0;
         hipLaunchKernelGGL((k_restrict_lat<INIT, BJ, SETD, MT>), dim3(grid), dim3(kBlock), 0, st, rf, F.rmsk.p, F.rf0.p,
-                           F.rstr.p, cmask, bc, xc, dc, minv, coef, nc, csub, sc, xcd);
+                           F.rstr.p, cmask, bc, xc, dc, minv, coef, nc, csub, sc);
         return;
     }
     hipLaunchKernelGGL((k_restrict<INIT, BJ, SETD, MT>), dim3(grid), dim3(kBlock), 0, st, rf, F.rslots.p, F.roff.p,
@@ -2856,56 +2449,12 @@ double MgpisDevice::bench_spmv(int variant, int reps) {
     return (double)ms / std::max(reps, 1);
 }
 
-// the first fine sweep can ride on k_axpy (k_axpy_jac0): block Jacobi from the fp32 inverses on
-// a level with a coarser one
-// the colour sweep's colour-0 launch rides on k_axpy (k_axpy_gs0): multicolour fine level with fp32
-// inverses; opt-in DDPCA_FUSE_GS0=1 (read at graph capture): bit-identical, measured neutral --
-// 17.39 vs 17.42 ADMM it/s at 8 subdomains, 31.97 vs 31.88 at 4 (profiles/r03ac)
-bool MgpisDevice::fuse_gs0() const {
-    const char* e = std::getenv("DDPCA_FUSE_GS0");
-    const bool on = e && e[0] == '1';
-    const int Lf = (int)lev.size() - 1;
-    return on && gs_fine() && gs.is0.p && !no_coarse && Lf > clev && vc_type(Lf) != kVal64 && lev[Lf].minv32.p;
-}
-
-bool MgpisDevice::fuse_jac0() const {
-    // opt-in (DDPCA_FUSE_JAC0=1): measured 0.4 % slower at 8 subdomains per GPU, as in round 1
-    // (profiles/r02u_ab.json, r01_sweep_fuse_axpy.txt) -- the wider k_axpy costs what k_jac0 did
-    const char* e = std::getenv("DDPCA_FUSE_JAC0");  // read at graph capture, per handle
-    const bool on = e && e[0] == '1';
-    const int Lf = (int)lev.size() - 1;
-    return on && !no_coarse && opt.smoother == 1 && Lf > clev && vc_type(Lf) != kVal64 && lev[Lf].minv32.p;
-}
-
 namespace {
 // one k_gs launch: phase ph over colour k's chunks (k < 0: every chunk)
 template <int PH, bool DOT, typename T>
-void launch_gs_t(const GsArgs& a, int ct, hipStream_t st) {  // ct: 0 int32 columns, 1 16-bit offsets, 2 stencil-coded
-    // workgroup of one wave (default) or four (DDPCA_GS_BLOCK=256): one-wave groups spread a
-    // colour's chunks over more CUs (+1 % at 8 subdomains, profiles/r03j)
-    const char* eb = std::getenv("DDPCA_GS_BLOCK");
-    const int bs = eb && std::atoi(eb) == 256 ? kBlock : 64;
-    const dim3 grid((unsigned)ceil_div(a.n, bs / kWave));
-    // slot loop (sell_rows): 1 non-temporal streaming, 2 with the columns prefetched a group
-    // ahead (DDPCA_GS_LOOP, read at graph capture; measured equal, profiles/r03i)
-    const char* e = std::getenv("DDPCA_GS_LOOP");
-    const int v = e ? std::atoi(e) : 1;
-    // small launches: the row-split sweep, opt-in (DDPCA_GS_SPLIT_CHUNKS = the largest launch it
-    // takes; read at graph capture): at 2 subdomains per GPU 58.2 vs 58.9-60.5 ADMM it/s without
-    // it, at 4 no better either (profiles/r03aa) -- the colour launches are not short of waves
-    const char* es = std::getenv("DDPCA_GS_SPLIT_CHUNKS");
-    const int64_t split_max = es ? std::atoll(es) : 0;
-    if (ct != 2 && a.n <= split_max && !a.xcd) {
-        if (ct == 1) hipLaunchKernelGGL((k_gs_split<PH, DOT, T, int16_t>), dim3((unsigned)a.n), dim3(kBlock), 0, st, a);
-        else hipLaunchKernelGGL((k_gs_split<PH, DOT, T, int32_t>), dim3((unsigned)a.n), dim3(kBlock), 0, st, a);
-        return;
-    }
-    if (ct == 2) hipLaunchKernelGGL((k_gs<PH, DOT, T, uint32_t, 1>), grid, dim3(bs), 0, st, a);
-    else if (ct == 1) {
-        if (v == 2) hipLaunchKernelGGL((k_gs<PH, DOT, T, int16_t, 2>), grid, dim3(bs), 0, st, a);
-        else hipLaunchKernelGGL((k_gs<PH, DOT, T, int16_t, 1>), grid, dim3(bs), 0, st, a);
-    } else if (v == 2) hipLaunchKernelGGL((k_gs<PH, DOT, T, int32_t, 2>), grid, dim3(bs), 0, st, a);
-    else hipLaunchKernelGGL((k_gs<PH, DOT, T, int32_t, 1>), grid, dim3(bs), 0, st, a);
+void launch_gs_t(const GsArgs& a, bool c16, hipStream_t st) {  // c16: 16-bit column offsets, else int32 columns
+    if (c16) hipLaunchKernelGGL((k_gs<PH, DOT, T, int16_t>), dim3((unsigned)a.n), dim3(kWave), 0, st, a);
+    else hipLaunchKernelGGL((k_gs<PH, DOT, T, int32_t>), dim3((unsigned)a.n), dim3(kWave), 0, st, a);
 }
 
 template <int PH, bool DOT>
@@ -2929,36 +2478,27 @@ void launch_gs(const MgpisDevice& D, int k, double* x, const double* b, double* 
     a.r = r;
     a.sc = scp;
     a.partial = partial;
-    // DDPCA_GS_XCD=1: neighbouring chunks (which gather the same x lines) on one XCD's L2
-    const char* ex = std::getenv("DDPCA_GS_XCD");
-    a.xcd = ex && std::atoi(ex) == 1 ? 1 : 0;
-    // chunk-ordered inverses (DDPCA_GS_MINVC=0: by row)
-    const char* em = std::getenv("DDPCA_GS_MINVC");
-    a.minvc = (em && std::atoi(em) == 0) ? nullptr : G.minvc.p;
-    const int ct = G.coded ? 2 : G.col16.p != nullptr ? 1 : 0;
-    if (G.coded) {
-        a.lm = G.lm.p;
-        a.um = G.um.p;
-        a.lstr = F.lstr.p;
-        a.nlast = F.nn - 1;
-    }
+    // the rows' fp32 inverses in chunk order (coalesced: read by row at stride 2 nodes they pulled
+    // whole lines for half the data, +1.1 %, profiles/r03o); the fp64 copy reads minv by row
+    a.minvc = G.minvc.p;
+    const bool c16 = G.col16.p != nullptr;
     if (G.val16.p) {
         a.val = G.val16.p;
         a.minv = F.minv32.p;
-        launch_gs_t<PH, DOT, uint16_t>(a, ct, D.stream);
+        launch_gs_t<PH, DOT, uint16_t>(a, c16, D.stream);
     } else if (G.val32.p) {
         a.val = G.val32.p;
         a.minv = F.minv32.p;
-        launch_gs_t<PH, DOT, float>(a, ct, D.stream);
+        launch_gs_t<PH, DOT, float>(a, c16, D.stream);
     } else {
         a.val = G.val64.p;
         a.minv = F.minv.p;
-        launch_gs_t<PH, DOT, double>(a, ct, D.stream);
+        launch_gs_t<PH, DOT, double>(a, c16, D.stream);
     }
 }
 }  // namespace
 
-void MgpisDevice::vcycle(const double* rin, double* zout, bool dot, bool first_done) {
+void MgpisDevice::vcycle(const double* rin, double* zout, bool dot) {
     if (no_coarse) throw ApiError(DDPCA_ESTATE, "one-level handle without a coarse inverse: diagonal preconditioner only");
     const int nlev = (int)lev.size();
     const int Lf = nlev - 1;
@@ -3013,14 +2553,9 @@ void MgpisDevice::vcycle(const double* rin, double* zout, bool dot, bool first_d
     if (gsf) cur[Lf] = zout;  // the Gauss-Seidel sweeps run in place
     // ---- descend
     if (gsf) {
-        if (first_done && !fuse_gs0()) throw ApiError(DDPCA_ESTATE, "fused first sweep with the multicolour smoother");
-        // forward sweep from zero, colour by colour (colour 0 already done by k_axpy_gs0 when
-        // first_done), then r = -U x in one launch
-        for (int k = first_done ? 1 : 0; k < gs.ncol; ++k) launch_gs<0, false>(*this, k, zout, rin, nullptr, scp, nullptr);
+        // forward sweep from zero, colour by colour, then r = -U x in one launch
+        for (int k = 0; k < gs.ncol; ++k) launch_gs<0, false>(*this, k, zout, rin, nullptr, scp, nullptr);
         launch_gs<1, false>(*this, -1, zout, nullptr, lev[Lf].r.p, scp, nullptr);
-    } else if (first_done) {
-        // k_axpy_jac0 wrote x0 = omega M rin into the fine level's first iterate buffer
-        if (cur[Lf] != lev[Lf].t.p || !fuse_jac0()) throw ApiError(DDPCA_ESTATE, "fused first sweep");
     } else {
         const LevelDev& F = lev[Lf];
         const int grid = ceil_div(F.nn, kBlock);
@@ -3146,8 +2681,7 @@ void MgpisDevice::vcycle_bytes(int s, double out[2]) const {
     auto mat = [&](int l) {  // one pass over the V-cycle's copy of level l
         const LevelDev& L = lev[l];
         if (L.tbl) return 4.0 * (double)L.nnzb_sub[s] + 4.0 * n(l);
-        // stencil-coded copies read no column indices (their zero blocks are not counted)
-        const double cb = (L.coded && vc_type(l) != kVal64) ? 0.0 : L.col16.p ? 2.0 : 4.0;
+        const double cb = L.col16.p ? 2.0 : 4.0;
         return (vbytes(vc_type(l)) + cb) * (double)L.nnzb_sub[s];
     };
     auto minv = [&](int l) { return (bj ? 9.0 : 3.0) * (vc_type(l) != kVal64 ? 4.0 : 8.0); };
@@ -3166,7 +2700,7 @@ void MgpisDevice::vcycle_bytes(int s, double out[2]) const {
     // the colours it reads (forward colour k: the k earlier ones, residual: the later ones,
     // backward: all others), and per row b, M^-1, the row index and x (or r) written
     const double K = gsf ? (double)gs.ncol : 0.0;
-    const double gsmat = gsf ? (vbytes(vc_type(Lf)) + (gs.coded ? 0.0 : gs.col16.p ? 2.0 : 4.0)) * (double)gs.nnzb_sub[s] : 0.0;
+    const double gsmat = gsf ? (vbytes(vc_type(Lf)) + (gs.col16.p ? 2.0 : 4.0)) * (double)gs.nnzb_sub[s] : 0.0;
     if (gsf) {
         put(Lf, gsmat + n(Lf) * (24.0 + minv(Lf) + 24.0 + 4.0 + 24.0 * (K - 1.0) / 2.0));  // forward
         put(Lf, n(Lf) * (24.0 + 4.0 + 24.0 * (K - 1.0) / 2.0));                              // residual
@@ -3229,22 +2763,13 @@ int64_t MgpisDevice::iteration_launches() const {
     // place of jac0, nu - 1 + 1 + nu sweep launches
     const int64_t nd = (int64_t)lev.size() - 1 - clev;
     const int64_t base = 5 + (nd == 0 ? 2 : 1 + nd * (opt.nu + 1) + 1 + nd * (1 + opt.nu));
-    return gs_fine() && nd > 0 ? base - 1 - 2 * opt.nu + 2 * gs.ncol + 1 - (fuse_gs0() ? 1 : 0) : base;
+    return gs_fine() && nd > 0 ? base - 1 - 2 * opt.nu + 2 * gs.ncol + 1 : base;
 }
 
-// k_fin over every member (1024 threads, or 256 with DDPCA_FIN_THREADS=256)
+// k_fin over every member
 void MgpisDevice::launch_fin(hipStream_t st, int what, const double* part, const double* part2, const int64_t* cb,
                              PcgScal* scp, PcgMirror* mir) {
-    if (fin_threads() == 256)
-        hipLaunchKernelGGL(k_fin<256>, dim3(nsub), dim3(256), 0, st, what, part, part2, cb, scp, mir);
-    else
-        hipLaunchKernelGGL(k_fin<1024>, dim3(nsub), dim3(1024), 0, st, what, part, part2, cb, scp, mir);
-}
-
-int MgpisDevice::fin_threads() const {
-    const char* e = std::getenv("DDPCA_FIN_THREADS");
-    // measured (profiles/r02u_ab.json): 1024 is 0.2-0.6 % faster with and without the split
-    return (e && std::atoi(e) == 256) ? 256 : 1024;
+    hipLaunchKernelGGL(k_fin, dim3(nsub), dim3(kFinT), 0, st, what, part, part2, cb, scp, mir);
 }
 
 void MgpisDevice::enqueue_iteration(int prec, bool timed) {
@@ -3261,18 +2786,9 @@ void MgpisDevice::enqueue_iteration(int prec, bool timed) {
     launch_sell<kPcg, false, true>(kVal64, a, stream);
     if (timed) DDPCA_HIP(hipEventRecord(ev_k1, stream));
     launch_fin(stream, (int)kFinAlpha, partial.p, nullptr, fin_cb.p, scp, mirror.dev);
-    const bool fuse0 = prec == 1 && fuse_jac0();
-    const bool fusegs = prec == 1 && !fuse0 && fuse_gs0();
-    if (fuse0)
-        hipLaunchKernelGGL(k_axpy_jac0, dim3(nblk), dim3(kBlock), 0, stream, xs.p, rs.p, ps.p, qs.p, scp, partial.p, L.nn,
-                           L.csub.p, L.minv32.p, L.coef.p, L.t.p);
-    else if (fusegs)
-        hipLaunchKernelGGL(k_axpy_gs0, dim3(nblk), dim3(kBlock), 0, stream, xs.p, rs.p, ps.p, qs.p, scp, partial.p, L.nn,
-                           L.csub.p, L.minv32.p, gs.is0.p, zs.p);
-    else
-        hipLaunchKernelGGL(k_axpy, dim3(nblk), dim3(kBlock), 0, stream, xs.p, rs.p, ps.p, qs.p, scp, partial.p, L.nn, L.csub.p);
+    hipLaunchKernelGGL(k_axpy, dim3(nblk), dim3(kBlock), 0, stream, xs.p, rs.p, ps.p, qs.p, scp, partial.p, L.nn, L.csub.p);
     launch_fin(stream, (int)kFinRR, partial.p, nullptr, fin_cb.p, scp, mirror.dev);
-    if (prec == 1) vcycle(rs.p, zs.p, true, fuse0 || fusegs);
+    if (prec == 1) vcycle(rs.p, zs.p, true);
     else hipLaunchKernelGGL(k_diag, dim3(nblk), dim3(kBlock), 0, stream, rs.p, L.dinv.p, zs.p, partial.p, L.nn, L.csub.p, scp);
     launch_fin(stream, (int)kFinBeta, prec == 1 ? vc_partial() : partial.p, nullptr, prec == 1 ? vc_cb() : fin_cb.p, scp,
                mirror.dev);

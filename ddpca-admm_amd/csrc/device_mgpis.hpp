@@ -79,18 +79,6 @@ struct LevelDev {
                            // V-cycle runs on fp64 operators
     DevBuf<float> val32;   // V-cycle operator rounded once to fp32 (opt.precond_fp32), levels >= 1
     DevBuf<uint16_t> val16;  // fine level's V-cycle copy in block-exponent fp16 (opt.precond_fp32 = 2)
-    // stencil-coded V-cycle copy (val16 / val32 of a box-lattice level; opt-in DDPCA_CODED=1): the
-    // slots of chunk c are the 27-point stencil positions its rows use, in stencil order -- slot
-    // k = the k-th set bit q of cm[c], column = row + (q/9-1) nxy + ((q/3)%3-1) nx + (q%3-1) with
-    // the member's strides (lstr) -- so the column is wave-uniform arithmetic instead of a per-lane
-    // 2-B load in front of every x gather; a row without that neighbour holds a zero block there
-    // (the slot order is the sorted one, sums are bit-identical to the column-indexed copy)
-    bool coded = false;
-    DevBuf<uint32_t> cm;    // per chunk: stencil positions present
-    DevBuf<uint32_t> cmq;   // per chunk: 4 sub-masks, slots k = g (mod 4) (row-split kernel, lane group g)
-    DevBuf<int64_t> coff;   // per chunk + 1: first coded slot
-    DevBuf<int32_t> lstr;   // per member: nx, nx * ny of its lattice
-    int64_t ncslots = 0;
     // table mode: rows whose block values (in device slot order, masks applied) are bit-identical
     // share one table row; the kernel streams only column indices and a row type, the values
     // come from the cache-resident table (structured meshes: ~30x fewer distinct rows than rows)
@@ -160,12 +148,6 @@ struct GsFine {
     DevBuf<int64_t> offl, offu;          // per chunk: first L / U slot
     DevBuf<int32_t> col;                 // per slot lane (when the level has no 16-bit offsets)
     DevBuf<int16_t> col16;
-    // stencil-coded form (the fine level is a coded lattice and every chunk's L and U stencil
-    // positions are disjoint -- the parity colouring of a box): per chunk the L and U position
-    // masks; its L / U slots are their set bits in stencil order (no column arrays)
-    bool coded = false;
-    DevBuf<uint32_t> lm, um;
-    DevBuf<uint8_t> is0;                 // per fine node: 1 = colour 0 (swept inside k_axpy_gs0)
     DevBuf<uint16_t> val16;
     DevBuf<float> val32;
     DevBuf<double> val64;
@@ -240,11 +222,8 @@ public:
         if (!vc32() || lev[l].tbl) return kVal64;
         return lev[l].val16.p ? kValH16 : kVal32;
     }
-    // z = M^-1 r (fine level); first_done: the first fine sweep is already in lev.back().t
-    // (k_axpy_jac0, only when fuse_jac0())
-    void vcycle(const double* r, double* z, bool dot, bool first_done = false);
-    bool fuse_jac0() const;
-    bool fuse_gs0() const;  // the colour sweep's first launch rides on k_axpy (k_axpy_gs0)
+    // z = M^-1 r (fine level); dot: leave the partials of r.z (vc_partial)
+    void vcycle(const double* r, double* z, bool dot);
     // b_{l-1} = realProl[l-1]^T r_l on every member (masked), batch nodal layouts of levels l, l-1
     void restrict_level(int l, const double* rf, double* bc);
     // block (rotated-node) parts of the transfer from level l-1 to l: b_c += B^T r_f, x_f += B e_c
@@ -321,7 +300,6 @@ private:
     PcgScal* sc_cur_ = nullptr; // the scalars enqueue_iteration / vcycle bind (sc, or a half's copy)
     void build_half_graph(int prec, int h);
     hipGraphExec_t capture_iterations(int prec, int count, PcgScal* scp);
-    int fin_threads() const;
     void launch_fin(hipStream_t st, int what, const double* part, const double* part2, const int64_t* cb, PcgScal* scp,
                     PcgMirror* mir);
     bool sample_pending_ = false;

@@ -1,0 +1,112 @@
+// Same-process HBM ceiling for the roofline line ("also report a measured
+// STREAM-copy ceiling"): a STREAM copy and a STREAM read over buffers far larger than the 256 MiB
+// Infinity Cache, timed with HIP events on a stream of their own.  bench.py divides the roofline
+// kernel's achieved GB/s by these to report the fraction of what THIS box streams, next to the
+// fraction of the 8 TB/s spec peak.  No reference counterpart (measurement only).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "../../include/ddpca_amd.h"
+#include "device_common.hpp"
+
+using namespace ddpca;
+
+namespace {
+
+typedef double dbl2_t __attribute__((ext_vector_type(2)));
+
+// y = x, 16 B per lane, grid-stride, four loads in flight per lane; non-temporal both ways
+__global__ __launch_bounds__(256) void k_stream_copy(const dbl2_t* __restrict__ x, dbl2_t* __restrict__ y, int64_t n) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (; i + 3 * stride < n; i += 4 * stride) {
+        const dbl2_t a = __builtin_nontemporal_load(x + i), b = __builtin_nontemporal_load(x + i + stride),
+                     c = __builtin_nontemporal_load(x + i + 2 * stride), d = __builtin_nontemporal_load(x + i + 3 * stride);
+        __builtin_nontemporal_store(a, y + i);
+        __builtin_nontemporal_store(b, y + i + stride);
+        __builtin_nontemporal_store(c, y + i + 2 * stride);
+        __builtin_nontemporal_store(d, y + i + 3 * stride);
+    }
+    for (; i < n; i += stride) __builtin_nontemporal_store(__builtin_nontemporal_load(x + i), y + i);
+}
+
+// partial[block] = sum of x over the block's share: 16 B per lane, four loads in flight per lane
+__global__ __launch_bounds__(256) void k_stream_read(const dbl2_t* __restrict__ x, int64_t n, double* partial) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    double s0 = 0.0, s1 = 0.0;
+    for (; i + 3 * stride < n; i += 4 * stride) {
+        const dbl2_t a = __builtin_nontemporal_load(x + i), b = __builtin_nontemporal_load(x + i + stride),
+                     c = __builtin_nontemporal_load(x + i + 2 * stride), d = __builtin_nontemporal_load(x + i + 3 * stride);
+        s0 += (a.x + a.y) + (b.x + b.y);
+        s1 += (c.x + c.y) + (d.x + d.y);
+    }
+    for (; i < n; i += stride) {
+        const dbl2_t a = __builtin_nontemporal_load(x + i);
+        s0 += a.x + a.y;
+    }
+    double s = s0 + s1;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    __shared__ double w[4];
+    if ((threadIdx.x & 63) == 0) w[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) partial[blockIdx.x] = (w[0] + w[1]) + (w[2] + w[3]);
+}
+
+__global__ void k_fill(dbl2_t* x, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) x[i] = dbl2_t{1.0, 2.0};
+}
+
+}  // namespace
+
+extern "C" int ddpca_stream_ceiling(int device, int64_t bytes, int reps, double* out4) {
+    return guarded([&] {
+        if (!out4 || bytes < (int64_t)(64 << 20) || reps < 1) throw ApiError(DDPCA_EINVAL, "ddpca_stream_ceiling: arguments");
+        select_device(device);
+        const int64_t n = bytes / 16;  // 16-B elements per buffer
+        int cus = 256;
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0) cus = prop.multiProcessorCount;
+        const int grid = cus * 8;  // 8 workgroups (32 waves) per CU
+        DevBuf<double> a((size_t)2 * n), b((size_t)2 * n), part(grid);
+        hipStream_t st;
+        DDPCA_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+        hipEvent_t e0, e1;
+        DDPCA_HIP(hipEventCreate(&e0));
+        DDPCA_HIP(hipEventCreate(&e1));
+        auto* x = reinterpret_cast<dbl2_t*>(a.p);
+        auto* y = reinterpret_cast<dbl2_t*>(b.p);
+        hipLaunchKernelGGL(k_fill, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, x, n);
+        hipLaunchKernelGGL(k_fill, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, y, n);
+        // best of three timed batches of `reps` back-to-back launches, after one warm-up launch
+        auto timed = [&](auto launch) {
+            launch();
+            double best = 1e300;
+            for (int t = 0; t < 3; ++t) {
+                DDPCA_HIP(hipEventRecord(e0, st));
+                for (int r = 0; r < reps; ++r) launch();
+                DDPCA_HIP(hipEventRecord(e1, st));
+                DDPCA_HIP(hipEventSynchronize(e1));
+                float ms = 0.f;
+                DDPCA_HIP(hipEventElapsedTime(&ms, e0, e1));
+                best = std::min(best, (double)ms / reps);
+            }
+            return best;
+        };
+        const double ms_copy = timed([&] { hipLaunchKernelGGL(k_stream_copy, dim3(grid), dim3(256), 0, st, x, y, n); });
+        const double ms_read = timed([&] { hipLaunchKernelGGL(k_stream_read, dim3(grid), dim3(256), 0, st, x, n, part.p); });
+        DDPCA_HIP(hipStreamSynchronize(st));
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+        (void)hipStreamDestroy(st);
+        const double B = 16.0 * (double)n;
+        out4[0] = 2.0 * B / (ms_copy * 1e-3) / 1e9;  // copy: bytes read + bytes written
+        out4[1] = B / (ms_read * 1e-3) / 1e9;
+        out4[2] = ms_copy;
+        out4[3] = ms_read;
+    });
+}

@@ -33,6 +33,11 @@ extern "C" {
 const char* ddpca_last_error(void);
 /* 1 if a gfx950 device is visible, 0 otherwise (no HIP context is created otherwise) */
 int ddpca_gpu_available(void);
+/* Measurement only (no reference counterpart; SURVEY §8 d3's measured STREAM ceiling): a STREAM copy
+ * and a STREAM read of `bytes` per buffer (>= 64 MiB; use >> the 256 MiB Infinity Cache), 16 B per
+ * lane, non-temporal, best of three batches of `reps` launches on a stream of its own.
+ * out4 = [copy GB/s (bytes read + written), read GB/s, copy ms, read ms]. */
+int ddpca_stream_ceiling(int device, int64_t bytes, int reps, double* out4);
 
 /* ========================================================================================
  * MGPIS -- multigrid-preconditioned CG on one subdomain (MGPIS.h:8-225)
@@ -398,8 +403,16 @@ typedef struct ddpca_mcontact* mcontact_t;
 int mcontact_gpu_create(ddpca_problem_t p, int device, int rank, int nranks,
                         const int32_t* owner, const mgpis_options_t* opt, mcontact_t* out);
 /* RCCL communicator from an ncclUniqueId (128 bytes) produced by rank 0 and broadcast by the
- * caller (e.g. through torch.distributed); not needed when nranks == 1. */
+ * caller (e.g. through torch.distributed); required when nranks > 1.  With nranks == 1 it is
+ * optional: the per-iteration all-reduces (MONITOR norms, coarse right-hand side) then run through
+ * a one-rank RCCL communicator, bit-identical to the run without one. */
 int mcontact_gpu_comm_init(mcontact_t h, const void* nccl_unique_id);
+/* Transport check (no reference counterpart): every rank sends two tagged messages of n doubles to
+ * every rank (itself included) in one grouped exchange -- the path the gamma halves take
+ * (MCONTACT.h:2632-2636 shares them in memory) -- and all-reduces n doubles (the MONITOR / coarse
+ * right-hand-side path); DDPCA_ECOMM unless every element arrives exact.  Collective: all ranks call
+ * it (in-process ranks from their own threads). */
+int mcontact_gpu_comm_check(mcontact_t h, int64_t n);
 /* 128-byte ncclUniqueId for rank 0 to broadcast. */
 int mcontact_gpu_unique_id(void* out128);
 /* Test transport (no reference counterpart): connects the n handles of ONE process, handles[r] =
@@ -436,6 +449,15 @@ int mcontact_gpu_timing(mcontact_t h, double* out10);
  * copies min(8, cap) when out != NULL.  No equivalent in the reference (measurement only). */
 int64_t mcontact_gpu_bytes(mcontact_t h, double* out, int64_t cap);
 int mcontact_gpu_destroy(mcontact_t h);
+/* The batched surface-mass solver of the ADMM loop on its own (replaces the interface mass solves
+ * of MCONTACT.h:2671-2704: SimplicialLDLT below 120000 rows, MCONTACT.h:838-847, Eigen CG above,
+ * 2680-2682): nsys square CSR systems A[s], right-hand sides b and solutions x concatenated in
+ * system order; Jacobi-PCG per system from x0 = 0 to ||r|| <= rtol ||b|| or maxit.  fuse_alpha:
+ * -1 the production rule (alpha inside the update kernel up to 1024 chunks per system), 0 / 1
+ * force the separate / fused alpha launch.  iters[nsys] (may be NULL).  On a breakdown (p.q <= 0
+ * or not finite) the system's x is its last good iterate and the call returns DDPCA_ENUMERIC. */
+int ddpca_mass_solve(int device, int64_t nsys, const ddpca_csr_t* A, const double* b, double* x, double rtol,
+                     int64_t maxit, int fuse_alpha, int64_t* iters);
 
 /* ========================================================================================
  * LAGRANGE path: MCONTACT::LAGRANGE (MCONTACT.h:2847-3701) -- dual mortar basis (2894-2947),

@@ -28,6 +28,7 @@
 
 #include "examples/CYLINDER_1.h"
 #include "ref_bind.hpp"
+#include "ref_ranks.hpp"
 
 namespace {
 
@@ -160,7 +161,9 @@ int main(int argc, char** argv) {
         itf += buf;
     }
     itf += "]";
-    // ---- the same problem on two ranks (in-process transport)
+    // ---- the same problem on two ranks (in-process transport), against a single-rank run with the
+    // same options; the V-cycle's exact-solve level is pinned (the reference's level 0): its
+    // automatic choice depends on how many subdomains a rank batches (oracle/ref_ranks.hpp)
     std::string ranks2 = "null";
     if (argc > 6) {
         const std::string own = argv[6];
@@ -169,57 +172,14 @@ int main(int argc, char** argv) {
             return 2;
         }
         std::vector<int32_t> ow(own.size());
-        for (size_t tv = 0; tv < own.size(); ++tv) ow[tv] = own[tv] - '0';
-        mcontact_t hr[2] = {nullptr, nullptr};
-        for (int r = 0; r < 2; ++r) ddpca_bind::check(mcontact_gpu_create(p, 0, r, 2, ow.data(), nullptr, &hr[r]));
-        ddpca_bind::check(mcontact_gpu_comm_local(hr, 2));
-        int64_t nr[2] = {0, 0};
-        std::thread th[2];
-        for (int r = 0; r < 2; ++r) th[r] = std::thread([&, r] { nr[r] = mcontact_gpu_iterate(hr[r], 3000, 1); });
-        for (auto& t : th) t.join();
-        for (int r = 0; r < 2; ++r) ddpca_bind::check((int)std::min<int64_t>(nr[r], 0));
-        double dm = 0.0, du2 = 0.0, dg = 0.0;
-        int64_t cross = 0;
-        for (int r = 0; r < 2; ++r) {
-            const int64_t rows = mcontact_gpu_monitor(hr[r], nullptr, 0);
-            std::vector<double> m(rows * ncol);
-            mcontact_gpu_monitor(hr[r], m.data(), rows);
-            if (rows != nrows) dm = 1e300;
-            for (int64_t j = 0; j < ncol && rows == nrows; ++j) {
-                double scale = 0.0;
-                for (int64_t k = 0; k < rows; ++k) scale = std::max(scale, std::abs(moni[k * ncol + j]));
-                for (int64_t k = 0; k < rows; ++k) {
-                    const double a = m[k * ncol + j], b = moni[k * ncol + j];
-                    dm = std::max(dm, std::abs(a - b) / (std::abs(b) + 1e-12 * scale + 1e-300));
-                }
-            }
-        }
-        for (size_t tv = 0; tv < c.multGrid.size(); ++tv) {
-            const int64_t n = mcontact_gpu_get(h, "resuDisp", tv, nullptr, 0);
-            std::vector<double> a(n), b(n);
-            mcontact_gpu_get(h, "resuDisp", tv, b.data(), n);
-            ddpca_bind::check((int)std::min<int64_t>(mcontact_gpu_get(hr[ow[tv]], "resuDisp", tv, a.data(), n), 0));
-            double d = 0.0, s = 0.0;
-            for (int64_t i = 0; i < n; ++i) d += (a[i] - b[i]) * (a[i] - b[i]), s += b[i] * b[i];
-            du2 = std::max(du2, std::sqrt(d / s));
-        }
-        for (size_t ts = 0; ts < c.searCont.size(); ++ts) {
-            const int r = ow[c.contBody[ts][0]];
-            cross += ow[c.contBody[ts][0]] != ow[c.contBody[ts][1]];
-            const int64_t n = mcontact_gpu_get(h, "inpoGamm", ts, nullptr, 0);
-            std::vector<double> a(n), b(n);
-            mcontact_gpu_get(h, "inpoGamm", ts, b.data(), n);
-            ddpca_bind::check((int)std::min<int64_t>(mcontact_gpu_get(hr[r], "inpoGamm", ts, a.data(), n), 0));
-            double gm = 0.0, d = 0.0;
-            for (int64_t i = 0; i < n; ++i) gm = std::max(gm, std::abs(b[i])), d = std::max(d, std::abs(a[i] - b[i]));
-            dg = std::max(dg, gm > 0 ? d / gm : d);
-        }
-        for (auto& x : hr) mcontact_gpu_destroy(x);
-        char buf[300];
-        std::snprintf(buf, sizeof(buf), "{\"owners\": \"%s\", \"cross_interfaces\": %ld, \"iters\": [%ld, %ld], \"moni_rel\": %.3g, "
-                      "\"resuDisp_rel\": %.3g, \"gamma_rel\": %.3g}",
-                      own.c_str(), (long)cross, (long)nr[0], (long)nr[1], dm, du2, dg);
-        ranks2 = buf;
+        int nr = 1;
+        for (size_t tv = 0; tv < own.size(); ++tv) nr = std::max(nr, (ow[tv] = own[tv] - '0') + 1);
+        std::vector<std::array<long, 2>> body;
+        for (size_t ts = 0; ts < c.searCont.size(); ++ts) body.push_back({(long)c.contBody[ts][0], (long)c.contBody[ts][1]});
+        mgpis_options_t o;
+        mgpis_default_options(&o);
+        o.coarse_level = 0;
+        ranks2 = ddpca_ranks::compare(p, ow, nr, (int64_t)c.multGrid.size(), (int64_t)c.searCont.size(), body, &o);
     }
     mcontact_gpu_destroy(h);
     ddpca_problem_destroy(p);

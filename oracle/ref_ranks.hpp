@@ -1,0 +1,110 @@
+// ORACLE TEST INFRASTRUCTURE -- NOT PART OF THE PRODUCT.
+//
+// Multi-rank check of an established device problem on ONE GPU: the same problem on `owners`'
+// ranks, each rank a device handle of this process connected to the others by the in-process
+// transport (mcontact_gpu_comm_local: RCCL's matching rules -- grouped sends and receives paired per
+// peer in issue order -- on host-staged copies), every rank's ADMM loop on its own host thread.
+// Compared with a single-rank device run of the same problem and options: iteration counts,
+// resuMoni rows (relative, floor 1e-12 of the column's largest value), resuDisp of every subdomain
+// (its owner's copy) and the projected gamma of every interface (the first side owner's copy).
+// The reference keeps all subdomains in one process (MCONTACT.h:2511-2537, 2629-2704); the device
+// distributes them, so this is what stands between the one-GPU tests and an 8-GPU run.
+#pragma once
+#include <algorithm>
+#include <array>
+#include <cmath>
+#include <cstdio>
+#include <stdexcept>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "ddpca_amd.h"
+
+namespace ddpca_ranks {
+
+inline void check(int rc) {
+    if (rc < 0) throw std::runtime_error(std::string("libddpca_amd: ") + ddpca_last_error());
+}
+
+// body[ts] = {contBody[ts][0], contBody[ts][1]}; returns one JSON object
+inline std::string compare(ddpca_problem_t p, const std::vector<int32_t>& owners, int nranks, int64_t nsub, int64_t nint,
+                           const std::vector<std::array<long, 2>>& body, const mgpis_options_t* opt, int64_t maxit = 3000) {
+    const int64_t ncol = 2 * nsub + 8 * nint + 2;
+    std::vector<int32_t> zero(nsub, 0);
+    mcontact_t h1 = nullptr;
+    check(mcontact_gpu_create(p, 0, 0, 1, zero.data(), opt, &h1));
+    const int64_t n1 = mcontact_gpu_iterate(h1, maxit, 1);
+    check((int)std::min<int64_t>(n1, 0));
+    const int64_t rows1 = mcontact_gpu_monitor(h1, nullptr, 0);
+    std::vector<double> moni1(rows1 * ncol);
+    mcontact_gpu_monitor(h1, moni1.data(), rows1);
+
+    std::vector<mcontact_t> hr(nranks, nullptr);
+    for (int r = 0; r < nranks; ++r) check(mcontact_gpu_create(p, 0, r, nranks, owners.data(), opt, &hr[r]));
+    check(mcontact_gpu_comm_local(hr.data(), nranks));
+    std::vector<int64_t> nr(nranks, 0);
+    std::vector<int> ck(nranks, 0);
+    {
+        std::vector<std::thread> th;
+        for (int r = 0; r < nranks; ++r)
+            th.emplace_back([&, r] {
+                ck[r] = mcontact_gpu_comm_check(hr[r], 4096);  // the transport itself first
+                nr[r] = ck[r] < 0 ? ck[r] : mcontact_gpu_iterate(hr[r], maxit, 1);
+            });
+        for (auto& t : th) t.join();
+    }
+    for (int r = 0; r < nranks; ++r) {
+        check(ck[r]);
+        check((int)std::min<int64_t>(nr[r], 0));
+    }
+    double dm = 0.0, du = 0.0, dg = 0.0;
+    for (int r = 0; r < nranks; ++r) {
+        const int64_t rows = mcontact_gpu_monitor(hr[r], nullptr, 0);
+        std::vector<double> m(rows * ncol);
+        mcontact_gpu_monitor(hr[r], m.data(), rows);
+        if (rows != rows1) dm = 1e300;
+        for (int64_t j = 0; j < ncol && rows == rows1; ++j) {
+            double scale = 0.0;
+            for (int64_t k = 0; k < rows; ++k) scale = std::max(scale, std::abs(moni1[k * ncol + j]));
+            for (int64_t k = 0; k < rows; ++k) {
+                const double a = m[k * ncol + j], b = moni1[k * ncol + j];
+                dm = std::max(dm, std::abs(a - b) / (std::abs(b) + 1e-12 * scale + 1e-300));
+            }
+        }
+    }
+    for (int64_t tv = 0; tv < nsub; ++tv) {
+        const int64_t n = mcontact_gpu_get(h1, "resuDisp", tv, nullptr, 0);
+        std::vector<double> a(n), b(n);
+        mcontact_gpu_get(h1, "resuDisp", tv, b.data(), n);
+        check((int)std::min<int64_t>(mcontact_gpu_get(hr[owners[tv]], "resuDisp", tv, a.data(), n), 0));
+        double d = 0.0, s = 0.0;
+        for (int64_t i = 0; i < n; ++i) d += (a[i] - b[i]) * (a[i] - b[i]), s += b[i] * b[i];
+        du = std::max(du, std::sqrt(d / std::max(s, 1e-300)));
+    }
+    int64_t cross = 0;
+    for (int64_t ts = 0; ts < nint; ++ts) {
+        const int r = owners[body[ts][0]];
+        cross += owners[body[ts][0]] != owners[body[ts][1]];
+        const int64_t n = mcontact_gpu_get(h1, "inpoGamm", ts, nullptr, 0);
+        std::vector<double> a(n), b(n);
+        mcontact_gpu_get(h1, "inpoGamm", ts, b.data(), n);
+        check((int)std::min<int64_t>(mcontact_gpu_get(hr[r], "inpoGamm", ts, a.data(), n), 0));
+        double gm = 0.0, d = 0.0;
+        for (int64_t i = 0; i < n; ++i) gm = std::max(gm, std::abs(b[i])), d = std::max(d, std::abs(a[i] - b[i]));
+        dg = std::max(dg, gm > 0 ? d / gm : d);
+    }
+    for (auto& x : hr) mcontact_gpu_destroy(x);
+    mcontact_gpu_destroy(h1);
+    std::string own, its;
+    for (size_t tv = 0; tv < owners.size(); ++tv) own += (tv ? ", " : "") + std::to_string(owners[tv]);
+    for (int r = 0; r < nranks; ++r) its += std::to_string(nr[r]) + (r + 1 < nranks ? ", " : "");
+    char buf[512];
+    std::snprintf(buf, sizeof(buf),
+                  "{\"nranks\": %d, \"owners\": [%s], \"cross_interfaces\": %ld, \"iters_1rank\": %ld, \"iters\": [%s], "
+                  "\"moni_rel\": %.3g, \"resuDisp_rel\": %.3g, \"gamma_rel\": %.3g}",
+                  nranks, own.c_str(), (long)cross, (long)n1, its.c_str(), dm, du, dg);
+    return buf;
+}
+
+}  // namespace ddpca_ranks

@@ -11,7 +11,10 @@
 // (126,750 rows at globHomo 2 >= DIRE_MAXI) and the reference solves it with its DOUBLE_M_1 MGPIS
 // (MCONTACT.h:1857-1865, 2303-2341, 2593-2594) -- as the device does above that size.
 // musc = 1: the LATIN coarse space instead (globCoup, DOUBLE_M past the same row count).
-//   ref_torsion globHomo [dole] [musc]
+// ranks = N > 1: the same problem on N device ranks of one process (subdomain tv on rank tv % N,
+// in-process transport) against a single-rank run of the same options (oracle/ref_ranks.hpp):
+// BASELINE config 4's 4 subdomains on 4 ranks.
+//   ref_torsion globHomo [dole] [musc] [ranks]
 #include <unistd.h>
 
 #include <cmath>
@@ -19,11 +22,13 @@
 
 #include "examples/TORSION.h"
 #include "ref_bind.hpp"
+#include "ref_ranks.hpp"
 
 int main(int argc, char** argv) {
     const long gh = argc > 1 ? std::atol(argv[1]) : 2;
     const long dole = argc > 2 ? std::atol(argv[2]) : 1;
     const long musc = argc > 3 ? std::atol(argv[3]) : 2;
+    const int nranks = argc > 4 ? std::atoi(argv[4]) : 1;
     const int saved = dup(1);
     if (!std::freopen("/dev/null", "w", stdout)) return 2;  // the reference's progress output
     TORSION t(1);
@@ -56,11 +61,23 @@ int main(int argc, char** argv) {
         }
     }
     mcontact_gpu_destroy(h);
+    std::string ranks = "null";
+    if (nranks > 1) {
+        std::vector<int32_t> ow(t.multGrid.size());
+        for (size_t tv = 0; tv < ow.size(); ++tv) ow[tv] = (int32_t)(tv % nranks);
+        std::vector<std::array<long, 2>> body;
+        for (size_t ts = 0; ts < t.searCont.size(); ++ts) body.push_back({(long)t.contBody[ts][0], (long)t.contBody[ts][1]});
+        mgpis_options_t o;
+        mgpis_default_options(&o);
+        o.coarse_level = 0;  // pinned: the automatic level depends on the subdomains per rank
+        ranks = ddpca_ranks::compare(p, ow, nranks, (int64_t)t.multGrid.size(), (int64_t)t.searCont.size(), body, &o);
+    }
     ddpca_problem_destroy(p);
     std::fprintf(stderr,
-                 "{\"iters_gpu\": %ld, \"iters_ref\": %ld, \"umax_gpu\": %.12g, \"umax_ref\": %.12g, "
-                 "\"analytic\": 1.159111630361142e-06, \"resuDisp_rel\": %.3g, \"coarse_rows\": %ld, \"dofs\": %ld}\n",
-                 (long)n_gpu, (long)t.iterNumbReco, umax_gpu, umax_ref, du, (long)(musc == 1 ? t.globCoup.rows() : t.globCoup_1.rows()),
-                 (long)[&] { long n = 0; for (auto& g : t.multGrid) n += g.mgpi.consStif[g.mgpi.maxiLeve].rows(); return n; }());
+                 "{\"ranks\": %s, \"iters_gpu\": %ld, \"iters_ref\": %ld, \"umax_gpu\": %.12g, \"umax_ref\": %.12g, "
+                 "\"analytic\": 1.159111630361142e-06, \"resuDisp_rel\": %.3g, \"coarse_rows\": %ld, \"dofs\": %ld, \"interfaces\": %ld}\n",
+                 ranks.c_str(), (long)n_gpu, (long)t.iterNumbReco, umax_gpu, umax_ref, du, (long)(musc == 1 ? t.globCoup.rows() : t.globCoup_1.rows()),
+                 (long)[&] { long n = 0; for (auto& g : t.multGrid) n += g.mgpi.consStif[g.mgpi.maxiLeve].rows(); return n; }(),
+                 (long)t.searCont.size());
     return 0;
 }

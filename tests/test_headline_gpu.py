@@ -163,40 +163,18 @@ def test_headline_fullsize_batched_solves_match_oracle(ddpca, oracle, gpu):
 
 
 @pytest.mark.parametrize("env,opts", [(("DDPCA_STREAMS", "1"), "HEADLINE_OPTIONS"),
-                                      (("DDPCA_FUSE_JAC0", "1"), "HEADLINE_OPTIONS"),
-                                      (("DDPCA_GS_BLOCK", "256"), "HEADLINE_OPTIONS"),
-                                      (("DDPCA_GS_MINVC", "0"), "HEADLINE_OPTIONS"),
-                                      (("DDPCA_GS_XCD", "1"), "HEADLINE_OPTIONS"),
-                                      (("DDPCA_CODED", "1"), "HEADLINE_OPTIONS"),
-                                      (("DDPCA_CODED", "1"), "HEADLINE_OPTIONS_SMALL"),
-                                      (("DDPCA_TAIL_PACING", "0"), "HEADLINE_OPTIONS"),
-                                      (("DDPCA_NORMS_BATCHED", "0"), "HEADLINE_OPTIONS"),
-                                      (("DDPCA_FUSE_GS0", "1"), "HEADLINE_OPTIONS")],
-                         ids=["one-stream", "fused-jac0", "gs-workgroup-256", "gs-inverses-by-row", "gs-xcd-slabs",
-                              "stencil-coded-vcycle", "stencil-coded-vcycle-small", "whole-replay-pacing",
-                              "monitor-norms-per-pair", "fused-colour-0-sweep"])
+                                      (("DDPCA_STREAMS", "1"), "HEADLINE_OPTIONS_SMALL"),
+                                      (("DDPCA_TAIL_PACING", "0"), "HEADLINE_OPTIONS")],
+                         ids=["one-stream", "one-stream-small", "whole-replay-pacing"])
 def test_schedule_variants_are_bit_identical(ddpca, gpu, monkeypatch, env, opts):
     """Schedule-only variants of the headline path must not change a bit: the two-stream split of
     the body-balance batch and of the mass CG (MgpisDevice / MassBatch ::set_split, default on)
-    against one stream, the V-cycle's first fine sweep fused into k_axpy (k_axpy_jac0, opt-in,
-    block-Jacobi option sets only) against the separate k_jac0, and the multicolour sweeps in
-    four-wave workgroups, with the inverses read by row instead of in chunk order, and with
-    XCD-slab workgroup placement, against the defaults; the V-cycle's stencil-coded copies (opt-in:
-    columns from the 27-point stencil position, zero blocks where a row lacks a neighbour) against
-    the column-indexed ones, on both option sets (the small one smooths the fine level with block
-    Jacobi); and whole-replay pacing to the end of every solve against the one-iteration tail
-    graphs; the MONITOR pair norms two launches per vector pair against one batch; and the colour
-    sweep's colour-0 launch fused into k_axpy (opt-in) against its own launch.  ADMM trajectory,
-    displacements and PCG iteration counts equal bit for bit (8 ADMM iterations, reduced chain)."""
+    against one stream, on both option sets; and whole-replay pacing to the end of every solve
+    against the one-iteration tail graphs.  ADMM trajectory, displacements and PCG iteration
+    counts equal bit for bit (8 ADMM iterations, reduced chain).  (The variants measured slower
+    and kept opt-in in round 3 -- stencil-coded copies, XCD-slab placement, four-wave colour
+    workgroups, inverses by row, fused first sweeps -- were deleted in round 4)"""
     H, M = getattr(ddpca, opts), ddpca.HEADLINE_MUSC
-    if env[0] == "DDPCA_CODED":
-        # the row-split kernel of the small levels sums a row's slots in four groups by slot rank,
-        # and the coded copy's zero blocks shift those ranks: compare with it off on both sides
-        monkeypatch.setenv("DDPCA_SPLIT_CHUNKS", "0")
-    if env[0].startswith("DDPCA_GS_") or env[0] == "DDPCA_CODED":
-        # the layout variants of the streamed colour sweep: keep the reduced chain's small colour
-        # launches on it (the row-split sweep sums in four groups, k_gs_split)
-        monkeypatch.setenv("DDPCA_GS_SPLIT_CHUNKS", "0")
     out = {}
     for variant in ("default", "alt"):
         if variant == "alt":
@@ -215,34 +193,6 @@ def test_schedule_variants_are_bit_identical(ddpca, gpu, monkeypatch, env, opts)
     for a, b in zip(out["default"][1], out["alt"][1]):
         assert np.array_equal(a, b)
     assert np.array_equal(out["default"][2], out["alt"][2])
-
-
-def test_mass_solves_warm_started(ddpca, gpu, monkeypatch):
-    """Opt-in (DDPCA_MASS_WARM=1): the batched surface-mass CG (the reference's LDLT solves,
-    MCONTACT.h:2671-2704) starts from the previous ADMM iteration's solution (MassBatch::solve,
-    k_mcg_init_warm: r0 = b - M x_prev) and stops at the same ||r|| <= 1e-14 ||b||.  Against
-    starting from zero (the default):
-    resuMoni rows within 1e-8 relative and displacements within 1e-9 after 10 ADMM iterations,
-    and fewer mass-CG iterations."""
-    H, M = ddpca.HEADLINE_OPTIONS, ddpca.HEADLINE_MUSC
-    out = {}
-    for v in ("0", "1"):
-        monkeypatch.setenv("DDPCA_MASS_WARM", v)
-        P = ddpca.headline_problem(gl=3)
-        P.set_coarse(M["muscSett"], [M["doleMcsc"]] * P.nsub)
-        P.ESTABLISH()
-        mc = ddpca.MCONTACT(P, **H)
-        assert mc.CONTACT_ANALYSIS(10, check=False) == 10
-        out[v] = (mc.monitor().copy(), [mc.get("resuDisp", tv).copy() for tv in range(P.nsub)],
-                  int(mc.get("mass_iters")[0]))
-        del mc
-    ok, worst = _rows_close(out["0"][0], out["1"][0], k=10, rtol=1e-8)
-    du = max(np.linalg.norm(a - b) / np.linalg.norm(b) for a, b in zip(out["0"][1], out["1"][1]) if np.any(b))
-    it0, it1 = (out[v][2] for v in ("0", "1"))
-    print(f"warm vs cold mass solves: worst resuMoni rel {worst:.2e}, displacements {du:.2e}, mass-CG iterations {it0} -> {it1}")
-    assert ok, worst
-    assert du <= 1e-9, du
-    assert it1 < it0
 
 
 def test_coarse_correction_kx_from_recursive_residual(ddpca, gpu, monkeypatch):
