@@ -490,6 +490,11 @@ int ddpca_problem_view(ddpca_problem_t h, const char* cname, int64_t index, int6
         } else if (name.rfind("K:", 0) == 0 || name.rfind("P:", 0) == 0) {
             const bool isK = name[0] == 'K';
             if (level < 0 || level > g.maxiLeve - (isK ? 0 : 1)) throw ApiError(DDPCA_EINVAL, "level");
+            // a rank-local build (establish_owned) leaves other ranks' subdomains without operators
+            const bool built = (int64_t)g.freeCount.size() > level + (isK ? 0 : 1) &&
+                               (isK ? (int64_t)g.levelStif.size() > level
+                                    : (int64_t)std::max(g.prolOper.size(), g.scalProl.size()) > level);
+            if (!built) throw ApiError(DDPCA_ESTATE, "operators of subdomain " + std::to_string(index) + " were not built here");
             const std::string ck = std::string(isK ? "K" : "P") + "#" + std::to_string(index) + "#" + std::to_string(level);
             auto it = P.cache_csr.find(ck);
             if (it == P.cache_csr.end()) it = P.cache_csr.emplace(ck, isK ? g.consStif(level) : g.realProl(level)).first;

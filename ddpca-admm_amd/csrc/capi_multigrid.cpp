@@ -226,17 +226,19 @@ int ddpca_multigrid_set(ddpca_multigrid_t h, const char* what, int64_t n, const 
             if (v < 0 || v >= M.nnode) throw ApiError(DDPCA_EINVAL, w + ": node out of range");
             return v;
         };
+        auto dof = [&](int64_t d) {  // not node(d / 3): division truncates -1 and -2 to node 0
+            if (d < 0 || d >= 3 * M.nnode) throw ApiError(DDPCA_EINVAL, w + ": dof out of range");
+            return d;
+        };
         if (w == "consDofv") {  // MULTIGRID::consDofv.emplace (first value of a dof wins)
             need(true, true);
             for (int64_t k = 0; k < n; ++k) {
-                node(idx[k] / 3);
-                g.consDofv.emplace(idx[k], val[k]);
+                g.consDofv.emplace(dof(idx[k]), val[k]);
             }
         } else if (w == "exteForc") {  // LOAD_ACCU in the given order (MULTIGRID.h:1084-1100)
             need(true, true);
             for (int64_t k = 0; k < n; ++k) {
-                node(idx[k] / 3);
-                g.LOAD_ACCU(idx[k], val[k]);
+                g.LOAD_ACCU(dof(idx[k]), val[k]);
             }
         } else if (w == "nodeRota") {
             need(true, true);
@@ -272,16 +274,22 @@ int ddpca_multigrid_refine(ddpca_multigrid_t h, int64_t n, const int64_t* elem, 
         if (n < 0 || (n > 0 && (!elem || !patt)) || nplan < 0 || (nplan > 0 && (!plan_ptr || !plan_node || !plan_xyz)) ||
             nflag < 0 || (nflag > 0 && (!flag_elem || !flag_child)))
             throw ApiError(DDPCA_EINVAL, "null argument");
+        // every argument is checked before the tree changes; REFINE's own checks (GRLE_CHECK's
+        // level balance, spliFlag children against the pattern) run on a copy that replaces the
+        // tree only when the whole refinement succeeded
         const int64_t ne = (int64_t)g.elemVect.size();
         std::set<int64_t> split;
         for (int64_t k = 0; k < n; ++k) {
             if (elem[k] < 0 || elem[k] >= ne || !g.elemVect[elem[k]].leaf()) throw ApiError(DDPCA_EINVAL, "refine: not a leaf element");
             if (patt[k] < 0 || patt[k] > 6) throw ApiError(DDPCA_EINVAL, "refine: pattern must be 0..6");
-            g.elemVect[elem[k]].refiPatt = (int)patt[k];
             split.insert(elem[k]);
         }
         std::map<std::vector<int64_t>, std::array<double, 3>> plan;
         if (nplan > 0 && plan_ptr[0] != 0) throw ApiError(DDPCA_EINVAL, "plan_ptr[0] must be 0");
+        for (int64_t q = 0; q < nplan; ++q)
+            if (plan_ptr[q + 1] < plan_ptr[q]) throw ApiError(DDPCA_EINVAL, "refine: plan_ptr must be non-decreasing");
+        for (int64_t k = 0; k < (nplan > 0 ? plan_ptr[nplan] : 0); ++k)
+            if (plan_node[k] < 0 || plan_node[k] >= M.nnode) throw ApiError(DDPCA_EINVAL, "refine: planSurf node out of range");
         for (int64_t q = 0; q < nplan; ++q) {
             std::vector<int64_t> key(plan_node + plan_ptr[q], plan_node + plan_ptr[q + 1]);
             if (key.size() < 2) throw ApiError(DDPCA_EINVAL, "refine: planSurf key of fewer than 2 nodes");
@@ -289,12 +297,19 @@ int ddpca_multigrid_refine(ddpca_multigrid_t h, int64_t n, const int64_t* elem, 
             plan.emplace(key, std::array<double, 3>{plan_xyz[3 * q], plan_xyz[3 * q + 1], plan_xyz[3 * q + 2]});
         }
         std::map<int64_t, std::set<int>> flag;
-        for (int64_t k = 0; k < nflag; ++k) flag[flag_elem[k]].insert((int)flag_child[k]);
+        for (int64_t k = 0; k < nflag; ++k) {
+            if (flag_elem[k] < 0 || flag_elem[k] >= ne) throw ApiError(DDPCA_EINVAL, "refine: spliFlag element out of range");
+            if (flag_child[k] < 0 || flag_child[k] > 7) throw ApiError(DDPCA_EINVAL, "refine: spliFlag child must be 0..7");
+            flag[flag_elem[k]].insert((int)flag_child[k]);
+        }
+        MULTIGRID t = g;
+        for (int64_t k = 0; k < n; ++k) t.elemVect[elem[k]].refiPatt = (int)patt[k];
         try {
-            g.REFINE(split, flag, plan);
+            t.REFINE(split, flag, plan);
         } catch (const std::invalid_argument& e) {
             throw ApiError(DDPCA_EINVAL, e.what());
         }
+        g = std::move(t);
         M.next_split.assign(split.begin(), split.end());
         M.nnode = g.numNodes();
         g.nodeLevel.assign(M.nnode, 0);

@@ -2053,7 +2053,23 @@ void coarse_invert(ddpca_mcontact& H) {
     std::vector<double>().swap(C.dense);
     hipStream_t st = H.main;
     if (H.nranks > 1 && !H.comm) throw ApiError(DDPCA_ESTATE, "the coarse space of a multi-rank run needs mcontact_gpu_comm_init");
+    const bool verbose = std::getenv("DDPCA_VERBOSE") != nullptr;
+    auto checksum = [n](const std::vector<double>& v) {
+        double a = 0.0, b = 0.0;
+        for (int64_t i = 0; i < n * n; ++i) a += std::abs(v[i]), b += v[i] * (double)(i % 9973);
+        return std::make_pair(a, b);
+    };
+    if (verbose) {
+        const auto c = checksum(A.download());
+        std::fprintf(stderr, "[ddpca] rank %d coarse rows %ld owned %ld: own part |.| %.17g w %.17g\n", H.rank, (long)n,
+                     (long)C.nown, c.first, c.second);
+    }
     if (H.comm) H.comm->allreduce_sum(A.p, n * n, st);
+    if (verbose) {
+        DDPCA_HIP(hipStreamSynchronize(st));
+        const auto c = checksum(A.download());
+        std::fprintf(stderr, "[ddpca] rank %d coarse matrix |.| %.17g w %.17g\n", H.rank, c.first, c.second);
+    }
     rocblas_handle rh = nullptr;
     if (rocblas_create_handle(&rh) != rocblas_status_success) throw ApiError(DDPCA_EHIP, "rocblas_create_handle");
     DevBuf<rocblas_int> info(2);
@@ -2486,7 +2502,8 @@ int mcontact_gpu_comm_check(mcontact_t h, int64_t n) {
         if (!h->comm) throw ApiError(DDPCA_ESTATE, "no communicator (mcontact_gpu_comm_init / _comm_local)");
         const int R = h->nranks, me = h->rank;
         hipStream_t st = h->main;
-        // exchange: to every rank q (me included) two messages in the order q, then 2 q + 1 tags;
+        // exchange: to every rank q (me included) two messages, tagged by the unordered pair {me, q}
+        // and k as the interfaces' gamma halves are (both ends name the same tag);
         // message (me -> q, k) carries v = 1e6 me + 1e3 q + k + i 2^-20 (exact in fp64)
         auto val = [](int src, int dst, int k, int64_t i) { return 1.0e6 * src + 1.0e3 * dst + k + std::ldexp((double)i, -20); };
         std::vector<double> hs((size_t)R * 2 * n);
@@ -2498,7 +2515,7 @@ int mcontact_gpu_comm_check(mcontact_t h, int64_t n) {
         std::vector<Transport::Msg> msgs;
         for (int q = 0; q < R; ++q)
             for (int k = 0; k < 2; ++k)
-                msgs.push_back({q, 2 * (int64_t)q + k, sbuf.p + ((size_t)q * 2 + k) * n, rbuf.p + ((size_t)q * 2 + k) * n, n});
+                msgs.push_back({q, 2 * ((int64_t)std::min(me, q) * R + std::max(me, q)) + k, sbuf.p + ((size_t)q * 2 + k) * n, rbuf.p + ((size_t)q * 2 + k) * n, n});
         h->comm->exchange(msgs, st);
         // all-reduce: rank r contributes (r + 1) (i + 1); the sum is R (R + 1) / 2 (i + 1)
         std::vector<double> ha(n);

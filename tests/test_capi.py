@@ -74,3 +74,63 @@ def test_reference_binding_hands_over_operators_exactly(fric):
     assert out.returncode == 0, out.stdout + out.stderr
     res = json.loads(out.stdout.splitlines()[0])
     assert res["ok"] and res["K_rel"] == 0 and res["iface_ops"] == 0
+
+
+def _one_hex(L):
+    """A one-element tree (the unit cube, corners in MULTIGRID's order) through ddpca_multigrid_create."""
+    c = ctypes
+    xyz = np.array([[0, 0, 0], [1, 0, 0], [1, 1, 0], [0, 1, 0], [0, 0, 1], [1, 0, 1], [1, 1, 1], [0, 1, 1]], np.float64)
+    keep = [xyz, np.arange(8, dtype=np.int64), np.array([-1], np.int64), np.zeros(1, np.int64),
+            np.array([-1], np.int64), np.zeros(2, np.int64)]
+    h = c.c_void_p()
+    rc = L.ddpca_multigrid_create(c.c_int64(8), keep[0].ctypes.data_as(c.c_void_p), c.c_int64(1),
+                                  *[k.ctypes.data_as(c.c_void_p) for k in keep[1:]], c.c_void_p(0), c.byref(h))
+    assert rc == 0
+    return h
+
+
+def _nelem(L, h):
+    c = ctypes
+    data, count, dt = c.c_void_p(), c.c_int64(), c.c_int()
+    assert L.ddpca_multigrid_tree(h, b"parent", c.byref(data), c.byref(count), c.byref(dt)) == 0
+    return count.value
+
+
+def test_multigrid_inputs_are_checked_before_the_tree_changes(ddpca):
+    """ADVICE r03: negative dofs of consDofv / exteForc are refused (not truncated to node 0);
+    ddpca_multigrid_refine checks plan_ptr (monotone, nodes in range) and spliFlag (element, child
+    0..7) and runs REFINE on a copy, so a refused call leaves the tree and its refinement patterns
+    as they were, and a valid call afterwards refines normally."""
+    c = ctypes
+    L = ddpca.lib()
+    h = _one_hex(L)
+    try:
+        p = lambda a: np.ascontiguousarray(a).ctypes.data_as(c.c_void_p)  # noqa: E731
+        for what in (b"consDofv", b"exteForc"):
+            for bad in (-1, -2, 24):
+                idx, val = np.array([bad], np.int64), np.array([1.0])
+                assert L.ddpca_multigrid_set(h, what, c.c_int64(1), p(idx), p(val)) == -1, (what, bad)
+        elem, patt = np.array([0], np.int64), np.array([1], np.int64)
+        # reversed plan_ptr, node out of range, spliFlag child beyond pattern 1's four children
+        cases = [dict(pp=[0, 2, 1], pn=[0, 1, 2], fe=[], fc=[]),
+                 dict(pp=[0, 2], pn=[0, 99], fe=[], fc=[]),
+                 dict(pp=[0], pn=[0], fe=[0], fc=[9]),
+                 dict(pp=[0], pn=[0], fe=[0], fc=[6])]
+        for cs in cases:
+            npl = len(cs["pp"]) - 1
+            pp, pn = np.array(cs["pp"], np.int64), np.array(cs["pn"], np.int64)
+            px = np.zeros(3 * max(npl, 1))
+            fe, fc = np.array(cs["fe"] or [0], np.int64), np.array(cs["fc"] or [0], np.int64)
+            rc = L.ddpca_multigrid_refine(h, c.c_int64(1), p(elem), p(patt), c.c_int64(npl), p(pp), p(pn), p(px),
+                                          c.c_int64(len(cs["fe"])), p(fe), p(fc))
+            assert rc == -1, cs
+            assert _nelem(L, h) == 1, cs
+            data, count, dt = c.c_void_p(), c.c_int64(), c.c_int()
+            assert L.ddpca_multigrid_tree(h, b"refiPatt", c.byref(data), c.byref(count), c.byref(dt)) == 0
+            assert c.cast(data, c.POINTER(c.c_int64))[0] == -1, cs  # the pattern was not written
+        z = np.zeros(3)
+        rc = L.ddpca_multigrid_refine(h, c.c_int64(1), p(elem), p(np.array([0], np.int64)), c.c_int64(0), p(z), p(z),
+                                      p(z), c.c_int64(0), p(z), p(z))
+        assert rc == 0 and _nelem(L, h) == 9
+    finally:
+        L.ddpca_multigrid_destroy(h)
