@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <climits>
+#include <mutex>
 #include <cstdint>
 #include <string>
 #include <vector>
@@ -115,5 +116,15 @@ int64_t pace_until_done(hipStream_t stream, hipGraphExec_t graph, const MirrorBu
 // (g1 / horizon: per half, or null)
 int64_t pace_halves(hipStream_t st[2], hipGraphExec_t g[2], const MirrorBuf& m, const std::vector<int>& half, int64_t k,
                     int64_t launched0, hipGraphExec_t* g1 = nullptr, const int64_t* horizon = nullptr);
+
+// rocSOLVER / rocBLAS from several host threads of one process (the in-process ranks of the
+// multi-rank tests) gave non-deterministic potrf failures on the very same matrix (TORSION on 4
+// ranks, n = 3468: info 2229, then 1479, while every rank held the 1-rank matrix bit for bit,
+// profiles/r04b): the dense factorisations of one process take this lock.  A production rank is one
+// process with one factorisation at a time, so it serialises nothing there.
+inline std::mutex& solver_mutex() {
+    static std::mutex m;
+    return m;
+}
 
 }  // namespace ddpca

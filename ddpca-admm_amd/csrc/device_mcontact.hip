@@ -991,6 +991,7 @@ private:
 struct CoarseDev {
     bool on = false, inverted = false;
     int64_t n = 0, nown = 0, nxn = 0, qnn = 0;
+    double dense_bytes = 0.0;  // n^2 8 B: what the dense inverse would hold per rank
     DevBuf<double> g, f0, xc, xn, ainv;
     DevBuf<int64_t> rptr;
     DevBuf<int32_t> rcol;
@@ -1896,10 +1897,18 @@ void build_coarse(ddpca_mcontact& H, Problem& P) {
     C.g.alloc(std::max<int64_t>(n, 1));
     C.xc.alloc(std::max<int64_t>(C.nown, 1));
     // the reference solves globCoup_1 directly below DIRE_MAXI = 120000 rows and with its DOUBLE_M_1
-    // MGPIS above (PREP.h:69, MCONTACT.h:1857-1865); DDPCA_COARSE_MG_MIN moves the switch (tests)
+    // MGPIS above (PREP.h:69, MCONTACT.h:1857-1865); DDPCA_COARSE_MG_MIN moves the switch (tests).
+    // The direct solve here is a dense explicit inverse, n^2 8 B on every rank and streamed by the
+    // GEMV every ADMM iteration, so it is also bounded by memory: above DDPCA_COARSE_DENSE_MB
+    // (default 1024 MiB, n ~ 11,600 rows) the multigrid solve takes over below DIRE_MAXI too --
+    // where the inverse would cost ~0.2 ms of HBM streaming per iteration and grow as n^2
     const char* mg_env = std::getenv("DDPCA_COARSE_MG_MIN");
+    const char* dense_env = std::getenv("DDPCA_COARSE_DENSE_MB");
+    const double dense_max = (dense_env ? std::atof(dense_env) : 1024.0) * 1048576.0;
+    C.dense_bytes = 8.0 * (double)n * (double)n;
     // LATIN: DOUBLE_M (MCONTACT.h:1236) with the host MULTISCALE's coarse contact nodes, one rank
-    C.mg = n >= (mg_env ? std::atoll(mg_env) : 120000) && (!cs.latin || (!cs.rank_local && !cs.coarNode.empty()));
+    const bool mg_ok = !cs.latin || (!cs.rank_local && !cs.coarNode.empty());
+    C.mg = (n >= (mg_env ? std::atoll(mg_env) : 120000) || C.dense_bytes > dense_max) && mg_ok;
     C.latin = cs.latin;
     // coarse solve: the owned rows of the dense inverse against g, or (DOUBLE_M) g scattered into
     // the coarse MGPIS and its owned rows gathered back (its PCG is counted by its own model)
@@ -2070,6 +2079,7 @@ void coarse_invert(ddpca_mcontact& H) {
         const auto c = checksum(A.download());
         std::fprintf(stderr, "[ddpca] rank %d coarse matrix |.| %.17g w %.17g\n", H.rank, c.first, c.second);
     }
+    std::lock_guard<std::mutex> solver_lock(solver_mutex());
     rocblas_handle rh = nullptr;
     if (rocblas_create_handle(&rh) != rocblas_status_success) throw ApiError(DDPCA_EHIP, "rocblas_create_handle");
     DevBuf<rocblas_int> info(2);
@@ -2621,6 +2631,16 @@ int64_t mcontact_gpu_get(mcontact_t h, const char* what, int64_t index, void* ou
             n = (int64_t)h->subs.size();
             if (out)
                 for (int64_t i = 0; i < std::min(n, cap); ++i) static_cast<int64_t*>(out)[i] = h->subs[i].tv;
+            return;
+        }
+        if (w == "coarse_solve") {  // [rows, 1 = multigrid (DOUBLE_M / DOUBLE_M_1) else 0, dense inverse bytes]
+            n = 3;
+            if (out && cap >= 3) {
+                auto* o = static_cast<int64_t*>(out);
+                o[0] = h->cs.on ? h->cs.n : 0;
+                o[1] = h->cs.on && h->cs.mg ? 1 : 0;
+                o[2] = h->cs.on && !h->cs.mg ? (int64_t)h->cs.dense_bytes : 0;
+            }
             return;
         }
         if (w == "mass_iters") {

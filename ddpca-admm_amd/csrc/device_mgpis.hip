@@ -1019,6 +1019,7 @@ void invert_spd_device(std::vector<double>& A, int64_t n, hipStream_t st) {
     d.upload(A);
     DevBuf<rocblas_int> info(2);
     info.zero(st);
+    std::lock_guard<std::mutex> solver_lock(solver_mutex());
     rocblas_handle h = nullptr;
     if (rocblas_create_handle(&h) != rocblas_status_success) throw ApiError(DDPCA_EHIP, "rocblas_create_handle");
     rocblas_set_stream(h, st);
@@ -1052,6 +1053,7 @@ void pinv_general_device(std::vector<double>& A, int64_t n, hipStream_t st, int6
     d.upload(A);
     DevBuf<rocblas_int> info(1);
     info.zero(st);
+    std::lock_guard<std::mutex> solver_lock(solver_mutex());
     rocblas_handle h = nullptr;
     if (rocblas_create_handle(&h) != rocblas_status_success) throw ApiError(DDPCA_EHIP, "rocblas_create_handle");
     rocblas_set_stream(h, st);

@@ -13,6 +13,7 @@
 
 #include "examples/BLOCK.h"
 #include "ref_bind.hpp"
+#include "ref_ranks.hpp"
 
 int main(int argc, char** argv) {
     const long gl = argc > 1 ? std::atol(argv[1]) : 1;
@@ -63,9 +64,10 @@ int main(int argc, char** argv) {
         itf += buf;
     }
     itf += "]";
+    const std::string alt = ddpca_ranks::coarse_alt(p, (int64_t)b.multGrid.size(), h, n_gpu);
     mcontact_gpu_destroy(h);
     ddpca_problem_destroy(p);
-    std::fprintf(stderr, "{\"iters_gpu\": %ld, \"iters_ref\": %ld, \"resuDisp_rel\": %.3g, \"interfaces\": %s}\n",
-                 (long)n_gpu, (long)b.iterNumbReco, du, itf.c_str());
+    std::fprintf(stderr, "{\"coarse_alt\": %s, \"iters_gpu\": %ld, \"iters_ref\": %ld, \"resuDisp_rel\": %.3g, \"interfaces\": %s}\n",
+                 alt.c_str(), (long)n_gpu, (long)b.iterNumbReco, du, itf.c_str());
     return 0;
 }

@@ -14,6 +14,7 @@
 #include <array>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 #include <thread>
@@ -104,6 +105,47 @@ inline std::string compare(ddpca_problem_t p, const std::vector<int32_t>& owners
                   "{\"nranks\": %d, \"owners\": [%s], \"cross_interfaces\": %ld, \"iters_1rank\": %ld, \"iters\": [%s], "
                   "\"moni_rel\": %.3g, \"resuDisp_rel\": %.3g, \"gamma_rel\": %.3g}",
                   nranks, own.c_str(), (long)cross, (long)n1, its.c_str(), dm, du, dg);
+    return buf;
+}
+
+// The same problem solved with the coarse space's other solve (the dense inverse <-> the
+// multigrid solve of DOUBLE_M / DOUBLE_M_1, switched by the dense-inverse memory budget
+// DDPCA_COARSE_DENSE_MB): iterations and resuDisp (position order) against the first run's.
+// Returns a JSON object; "null" when the first run had no coarse space or its multigrid solve was
+// forced by the row count (DIRE_MAXI), where the dense inverse is not available.
+inline std::string coarse_alt(ddpca_problem_t p, int64_t nsub, mcontact_t h0, int64_t n0, int64_t maxit = 3000) {
+    int64_t cs0[3] = {0, 0, 0};
+    check((int)std::min<int64_t>(mcontact_gpu_get(h0, "coarse_solve", 0, cs0, 3), 0));
+    if (cs0[0] == 0 || (cs0[1] == 1 && cs0[0] >= 120000)) return "null";
+    const char* old = std::getenv("DDPCA_COARSE_DENSE_MB");
+    const std::string keep = old ? old : "";
+    setenv("DDPCA_COARSE_DENSE_MB", cs0[1] ? "1e9" : "0", 1);
+    std::vector<int32_t> zero(nsub, 0);
+    mcontact_t h = nullptr;
+    const int rc = mcontact_gpu_create(p, 0, 0, 1, zero.data(), nullptr, &h);
+    if (old) setenv("DDPCA_COARSE_DENSE_MB", keep.c_str(), 1);
+    else unsetenv("DDPCA_COARSE_DENSE_MB");
+    check(rc);
+    int64_t cs1[3] = {0, 0, 0};
+    check((int)std::min<int64_t>(mcontact_gpu_get(h, "coarse_solve", 0, cs1, 3), 0));
+    const int64_t n1 = mcontact_gpu_iterate(h, maxit, 1);
+    check((int)std::min<int64_t>(n1, 0));
+    double du = 0.0;
+    for (int64_t tv = 0; tv < nsub; ++tv) {
+        const int64_t n = mcontact_gpu_get(h0, "resuDisp", tv, nullptr, 0);
+        std::vector<double> a(n), b(n);
+        check((int)std::min<int64_t>(mcontact_gpu_get(h0, "resuDisp", tv, b.data(), n), 0));
+        check((int)std::min<int64_t>(mcontact_gpu_get(h, "resuDisp", tv, a.data(), n), 0));
+        double d = 0.0, s = 0.0;
+        for (int64_t i = 0; i < n; ++i) d += (a[i] - b[i]) * (a[i] - b[i]), s += b[i] * b[i];
+        du = std::max(du, std::sqrt(d / std::max(s, 1e-300)));
+    }
+    mcontact_gpu_destroy(h);
+    char buf[320];
+    std::snprintf(buf, sizeof(buf),
+                  "{\"rows\": %ld, \"first_mg\": %ld, \"first_dense_bytes\": %ld, \"alt_mg\": %ld, \"iters_first\": %ld, "
+                  "\"iters_alt\": %ld, \"resuDisp_rel\": %.3g}",
+                  (long)cs0[0], (long)cs0[1], (long)cs0[2], (long)cs1[1], (long)n0, (long)n1, du);
     return buf;
 }
 

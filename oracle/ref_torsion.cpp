@@ -60,6 +60,7 @@ int main(int argc, char** argv) {
             umax_ref = std::max(umax_ref, t.resuDisp[tv].segment<3>(3 * i).norm());
         }
     }
+    const std::string alt = ddpca_ranks::coarse_alt(p, (int64_t)t.multGrid.size(), h, n_gpu);
     mcontact_gpu_destroy(h);
     std::string ranks = "null";
     if (nranks > 1) {
@@ -74,9 +75,9 @@ int main(int argc, char** argv) {
     }
     ddpca_problem_destroy(p);
     std::fprintf(stderr,
-                 "{\"ranks\": %s, \"iters_gpu\": %ld, \"iters_ref\": %ld, \"umax_gpu\": %.12g, \"umax_ref\": %.12g, "
+                 "{\"coarse_alt\": %s, \"ranks\": %s, \"iters_gpu\": %ld, \"iters_ref\": %ld, \"umax_gpu\": %.12g, \"umax_ref\": %.12g, "
                  "\"analytic\": 1.159111630361142e-06, \"resuDisp_rel\": %.3g, \"coarse_rows\": %ld, \"dofs\": %ld, \"interfaces\": %ld}\n",
-                 ranks.c_str(), (long)n_gpu, (long)t.iterNumbReco, umax_gpu, umax_ref, du, (long)(musc == 1 ? t.globCoup.rows() : t.globCoup_1.rows()),
+                 alt.c_str(), ranks.c_str(), (long)n_gpu, (long)t.iterNumbReco, umax_gpu, umax_ref, du, (long)(musc == 1 ? t.globCoup.rows() : t.globCoup_1.rows()),
                  (long)[&] { long n = 0; for (auto& g : t.multGrid) n += g.mgpi.consStif[g.mgpi.maxiLeve].rows(); return n; }(),
                  (long)t.searCont.size());
     return 0;

@@ -327,6 +327,7 @@ def test_torsion_known_answer(gpu, tmp_path):
     assert out.returncode == 0, out.stderr[-2000:]
     res = json.loads(out.stderr.strip().splitlines()[-1])
     print(res["ranks"])
+    _check_coarse_alt(res)
     rk = res["ranks"]
     assert rk["nranks"] == 4 and rk["cross_interfaces"] == res["interfaces"], rk
     assert rk["iters"] == [rk["iters_1rank"]] * 4, rk
@@ -335,6 +336,20 @@ def test_torsion_known_answer(gpu, tmp_path):
     assert res["resuDisp_rel"] <= 1e-6, res
     assert abs(res["umax_gpu"] - res["umax_ref"]) <= 1e-6 * res["umax_ref"], res
     assert abs(res["umax_gpu"] - res["analytic"]) <= 1e-3 * res["analytic"], res
+
+
+def _check_coarse_alt(res):
+    """The coarse space's other solve on the same problem (oracle/ref_ranks.hpp coarse_alt): the
+    dense inverse while n^2 8 B fits DDPCA_COARSE_DENSE_MB (default 1 GiB), the multigrid solve of
+    DOUBLE_M / DOUBLE_M_1 above it (MCONTACT.h:1857-1866 switch it at DIRE_MAXI rows only; the
+    dense inverse is this library's, so its memory bounds it too).  With the budget forced to the
+    other side the ADMM run must take the same iterations (+-1) and resuDisp within 1e-8."""
+    alt = res["coarse_alt"]
+    print("coarse_alt", alt)
+    assert alt is not None and alt["rows"] > 0, res
+    assert alt["alt_mg"] != alt["first_mg"], alt
+    assert alt["first_dense_bytes"] == (0 if alt["first_mg"] else 8 * alt["rows"] ** 2), alt
+    assert abs(alt["iters_alt"] - alt["iters_first"]) <= 1 and alt["resuDisp_rel"] <= 1e-8, alt
 
 
 @pytest.mark.parametrize("musc", ["1", "2"])
@@ -357,6 +372,7 @@ def test_block_patch_pressure_known_answer(gpu, tmp_path, musc):
     res = json.loads(out.stderr.strip().splitlines()[-1])
     assert abs(res["iters_gpu"] - res["iters_ref"]) <= 1, res
     assert res["resuDisp_rel"] <= 1e-6, res
+    _check_coarse_alt(res)
     assert len(res["interfaces"]) == 8
     for itf in res["interfaces"]:
         assert itf["nip"] > 0
