@@ -75,6 +75,11 @@ def parse():
     ap.add_argument("--dole", type=int, default=M["doleMcsc"], help="doleMcsc: coarse-space level of every subdomain (DEHW.h:2239)")
     ap.add_argument("--coarse-level", type=int, default=H["coarse_level"],
                     help="V-cycle level of the exact dense coarse solve (-1: auto, 0: the reference's)")
+    ap.add_argument("--mesh", choices=["headline", "general"], default="headline",
+                    help="general: DEHW's general-mesh features on the same chain (the contact band refined once "
+                         "more -> hanging level, rotated support nodes, explicit transfer lists, no coarse space)")
+    ap.add_argument("--no-general", action="store_true",
+                    help="skip the general-mesh line the N = 1 headline run adds (a child process, before the headline)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-stream-ceiling", action="store_true", help="skip the same-process STREAM ceiling")
     ap.add_argument("--traffic-json", default=os.environ.get("DDPCA_TRAFFIC_JSON", str(ROOT / "profiles" / "traffic.json")),
@@ -93,6 +98,11 @@ def main():
     import torch
     import torch.distributed as dist
 
+    # the general-mesh line: its own process, before the headline allocates anything
+    # on the host (each setup peaks at tens of GB), its JSON object attached to this line
+    general_line = None
+    if a.mesh == "headline" and world == 1 and not a.no_general:
+        general_line = run_general_child(a)
     torch.cuda.set_device(local)  # the timing syncs below must hit this rank's GPU, not device 0
     if world > 1:
         # one node: RCCL's bootstrap over loopback (its data path is xGMI peer-to-peer either way);
@@ -106,8 +116,12 @@ def main():
     part = import_module("ddpca-admm_amd.partition")
 
     t_setup = time.perf_counter()
+    general = a.mesh == "general"
+    feat = dict(D.GENERAL_FEATURES) if general else {}
+    if general:
+        a.musc = 0  # MULTISCALE_1 is restated for uniform hierarchies (multiscale.cpp)
     P = D.headline_problem(groups=a.groups, nx=a.nx, ny=a.ny, nz=a.nz, gl=a.gl, fric=a.fric,
-                           ip_contact=a.ip_contact, ip_glued=a.ip_glued)
+                           ip_contact=a.ip_contact, ip_glued=a.ip_glued, **feat)
     nip = sum(len(P.array("ip_w", ts)) for ts in range(P.nint))
     nsub = P.nsub
     owner = part.block_owner(nsub, world)
@@ -207,22 +221,27 @@ def main():
             "dtype": "f64",
             "data": "synthetic",
             "config": {
-                "workload": f"dehw-synthetic: {nsub} subdomains x {total_dofs // nsub} DOF = {total_dofs} DOF, "
-                            f"{a.groups} frictional contacts (mu={a.fric}) + {2 * (a.groups - 1)} glued interfaces, "
-                            f"{nip} integration points ({nip / total_dofs:.2f} per DOF), "
-                            f"{a.gl + 1} MG levels, MGPIS-PCG rtol 1e-14",
+                "workload": (f"dehw-synthetic{' general-mesh' if general else ''}: {nsub} subdomains x "
+                             f"{total_dofs // nsub} DOF = {total_dofs} DOF, "
+                             f"{a.groups} frictional contacts (mu={a.fric}) + {2 * (a.groups - 1)} glued interfaces, "
+                             f"{nip} integration points ({nip / total_dofs:.2f} per DOF), "
+                             f"{a.gl + 1 + (1 if general else 0)} MG levels, MGPIS-PCG rtol 1e-14"
+                             + (", contact band refined once more (hanging level past the MGPIS hierarchy), "
+                                "rotated support nodes, explicit transfer lists (DDPCA_LATTICE=0)" if general else "")),
                 "subdomains": nsub,
                 "dof": total_dofs,
                 "interfaces": P.nint,
                 "integration_points": nip,
                 "ip_per_dof": nip / total_dofs,
-                "mg_levels": a.gl + 1,
+                "mg_levels": a.gl + 1 + (1 if general else 0),
                 "smoother": {0: "jacobi", 1: "block-jacobi", 2: "chebyshev"}[a.smoother] + f"({a.nu})" if a.smoother != 3
                 else f"fine: multicolour block Gauss-Seidel (1 forward, 1 backward); below: block-jacobi({a.nu})",
                 "pcg_x0": "previous solution" if a.warm_start else "zero",
                 "vcycle_operator_storage": {0: "fp64", 1: "fp32", 2: "fp32, fine level block-exponent fp16"}[a.precond_fp32],
                 "operator_rows": "deduplicated table" if a.table_mode else "streamed",
                 "coarse_space": f"interface-eliminated (muscSett={a.musc}, doleMcsc={a.dole})" if a.musc else "none",
+                **({"hanging_dofs": int(sum(P.grid(tv).hangRows().shape[0] for tv in range(nsub) if owner[tv] == rank)),
+                    "lattice_transfers": os.environ.get("DDPCA_LATTICE", "1") != "0"} if general else {}),
                 "parallelism": f"dd{world}",
             },
             "mgpis_dof_iter_per_s": dof_its / elapsed,
@@ -274,6 +293,8 @@ def main():
             result["roofline"]["step_frac_of_stream"] = step_bytes / step_s / 1e9 / max(ceiling["copy_gbs"], ceiling["read_gbs"])
         if world == 1 and not a.no_cpu_baseline:
             result["cpu_baseline"] = cpu_baseline(P, mc)
+        if general_line is not None:
+            result["general_mesh"] = general_line
     # release device state before the process group
     del mc
     if world > 1:
@@ -281,6 +302,31 @@ def main():
         dist.destroy_process_group()
     if result is not None:
         print(json.dumps(result), flush=True)
+
+
+def run_general_child(a) -> dict:
+    """The general-mesh line: bench.py --mesh general in a child process (DDPCA_LATTICE=0), same
+    workload size, steps and warmup; its JSON object, or the failure."""
+    import subprocess
+    cmd = [sys.executable, str(Path(__file__).resolve()), "--mesh", "general", "--no-general", "--no-cpu-baseline",
+           "--no-stream-ceiling", "--steps", str(a.steps), "--warmup", str(a.warmup), "--groups", str(a.groups),
+           "--nx", str(a.nx), "--ny", str(a.ny), "--nz", str(a.nz), "--gl", str(a.gl), "--fric", str(a.fric),
+           "--ip-contact", str(a.ip_contact), "--ip-glued", str(a.ip_glued)]
+    env = dict(os.environ, DDPCA_LATTICE="0")
+    t0 = time.perf_counter()
+    log(0, "general-mesh line (child process) ...")
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=1500, env=env)
+    except subprocess.TimeoutExpired:
+        return {"error": "timeout"}
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    if r.returncode != 0 or not lines:
+        return {"error": f"rc={r.returncode}", "stderr_tail": r.stderr[-1500:]}
+    j = json.loads(lines[-1])
+    log(0, f"general-mesh line: {j.get('value', 0):.3f} ADMM it/s ({time.perf_counter() - t0:.0f} s incl. setup)")
+    for k in ("n_gpus", "steps", "warmup", "higher_is_better", "scaling", "vs_baseline", "data"):
+        j.pop(k, None)
+    return j
 
 
 def log(rank: int, msg: str) -> None:
@@ -291,8 +337,11 @@ def log(rank: int, msg: str) -> None:
 
 def traffic_key(a) -> dict:
     # the roofline launch does not depend on musc / omega / coarse level; it does on the value layout
-    return dict(groups=a.groups, nx=a.nx, ny=a.ny, nz=a.nz, gl=a.gl, smoother=a.smoother, nu=a.nu,
-                precond_fp32=a.precond_fp32, table_mode=a.table_mode, value_layout=VALUE_LAYOUT)
+    k = dict(groups=a.groups, nx=a.nx, ny=a.ny, nz=a.nz, gl=a.gl, smoother=a.smoother, nu=a.nu,
+             precond_fp32=a.precond_fp32, table_mode=a.table_mode, value_layout=VALUE_LAYOUT)
+    if a.mesh != "headline":
+        k["mesh"] = a.mesh
+    return k
 
 
 def cpu_baseline(P, mc, budget_s=20.0):

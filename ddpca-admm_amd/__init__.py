@@ -75,7 +75,12 @@ HEADLINE_MUSC = dict(muscSett=2, doleMcsc=1)
 # density -- contact faces integrated over 2^2 x 2^2 polygons, glued faces over 2^1 x 2^1
 # (0.80 integration points per DOF at gl = 5).  bench.py's defaults and the headline parity tests
 # (tests/test_headline_gpu.py, at gl = 3 for the oracle trajectory) both take it from here.
-HEADLINE_WORKLOAD = dict(groups=4, nx=3, ny=2, nz=2, gl=5, fric=0.2, ip_contact=2, ip_glued=1)
+HEADLINE_WORKLOAD = dict(groups=4, nx=3, ny=2, nz=2, gl=5, fric=0.2, ip_contact=2, ip_glued=1, band=0, rot=0)
+# DEHW's general-mesh features on the same chain (bench.py --mesh general): the contact band refined
+# once more (a general tree: hanging level past the MGPIS hierarchy, explicit transfer lists) and
+# rotated support nodes (prolongation blocks off w I); no coarse space (MULTISCALE_1 is restated for
+# uniform hierarchies only, multiscale.cpp)
+GENERAL_FEATURES = dict(band=1, rot=1)
 
 
 def headline_problem(gl: int | None = None, **override) -> "Problem":
@@ -85,7 +90,7 @@ def headline_problem(gl: int | None = None, **override) -> "Problem":
     if gl is not None:
         w["gl"] = gl
     return Problem("dehw", w["groups"], w["nx"], w["ny"], w["nz"], w["gl"], w["fric"], w["ip_contact"],
-                   w["ip_glued"])
+                   w["ip_glued"], w["band"], w["rot"])
 
 _P = C.c_void_p
 _I64P = C.POINTER(C.c_int64)
@@ -563,6 +568,11 @@ class MULTIGRID:
 
     def realProl(self, level: int):
         return self.problem.csr("P", self.tv, level)
+
+    def hangRows(self):
+        """Rows of prolOper[maxiLeve] past the MGPIS fine level (the hanging level's values over the
+        level-maxiLeve nodal vector, OUTP_SUB1, MULTIGRID.h:1279); 0 rows without a hanging level."""
+        return self.problem.csr("H", self.tv, 0)
 
     def OUTP_SUB1(self, x: np.ndarray) -> np.ndarray:
         """Condensed solution -> nodal displacement (MULTIGRID.h:1263-1281; no rotations)."""

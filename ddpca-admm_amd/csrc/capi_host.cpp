@@ -3,6 +3,7 @@
 #include <cmath>
 #include <cstring>
 #include <map>
+#include <set>
 #include <memory>
 #include <stdexcept>
 #include <string>
@@ -51,6 +52,43 @@ void conforming_interface(const MULTIGRID& gm, const MULTIGRID& gs, int axis, in
     std::map<std::array<std::array<int64_t, 3>, 4>, std::array<int64_t, 4>> mast;
     for (const auto& f : plane_faces(gm, axis, value)) mast.emplace(key(gm, f), f);
     for (const auto& f : plane_faces(gs, axis, value)) {
+        auto it = mast.find(key(gs, f));
+        if (it == mast.end()) continue;
+        conforming_face_ips(gm, it->second.data(), gs, f.data(), ips, sub);
+    }
+}
+
+// The same on a general tree (local refinement: the new nodes carry no lattice coordinates):
+// leaf faces on the coordinate plane x[axis] == value, matched by their corners' coordinates.
+std::vector<std::array<int64_t, 4>> plane_faces_xyz(const MULTIGRID& g, int axis, double value) {
+    std::vector<std::array<int64_t, 4>> out;
+    for (const auto& el : g.elemVect) {
+        if (!el.leaf()) continue;
+        for (const auto& f : kHexFace) {
+            bool on = true;
+            std::array<int64_t, 4> nodes;
+            for (int k = 0; k < 4; ++k) {
+                nodes[k] = el.cornNode[f[k]];
+                on &= std::abs(g.nodeCoor[nodes[k]][axis] - value) <= 1e-12;
+            }
+            if (on) out.push_back(nodes);
+        }
+    }
+    return out;
+}
+
+void conforming_interface_xyz(const MULTIGRID& gm, const MULTIGRID& gs, int axis, double value,
+                              std::vector<IntegralPoint>& ips, int sub) {
+    auto key = [](const MULTIGRID& g, const std::array<int64_t, 4>& f) {
+        std::array<std::array<int64_t, 3>, 4> k;
+        for (int i = 0; i < 4; ++i)
+            for (int a = 0; a < 3; ++a) k[i][a] = std::llround(g.nodeCoor[f[i]][a] * 1.0e9);
+        std::sort(k.begin(), k.end());
+        return k;
+    };
+    std::map<std::array<std::array<int64_t, 3>, 4>, std::array<int64_t, 4>> mast;
+    for (const auto& f : plane_faces_xyz(gm, axis, value)) mast.emplace(key(gm, f), f);
+    for (const auto& f : plane_faces_xyz(gs, axis, value)) {
         auto it = mast.find(key(gs, f));
         if (it == mast.end()) continue;
         conforming_face_ips(gm, it->second.data(), gs, f.data(), ips, sub);
@@ -178,6 +216,17 @@ void make_dehw(Problem& P, const double* q, int nq) {
     const int64_t gl = (int64_t)q[4];
     const double fric = q[5];
     const int kc = nq > 6 ? (int)q[6] : 0, kg = nq > 7 ? (int)q[7] : 0;
+    // DEHW's general-mesh features (q[8], q[9], default off):
+    //   band: the contact band refined once more (DEHW.h:1562, 2079: adaptively refined contact
+    //         zones): the layer of elements on either side of each worm/wheel contact plane is cut
+    //         with pattern 0 (MULTIGRID::REFINE + GRLE_CHECK) -- a general tree, renumbered by
+    //         TRANSFER, whose band/bulk faces leave hanging nodes on the level past the MGPIS
+    //         hierarchy; the contact faces (and the glued faces in the band) are the refined ones
+    //   rot:  nodal frames on the worms' supported faces (DEHW.h:197, 272, 352: the hub's rotated
+    //         nodes): each node of a worm's bottom face off the glued planes is rotated about x by
+    //         an angle varying with y and supported along its local z (a curved roller bed) --
+    //         prolongation blocks off w I, R^T K R, CONSTRAINT with nodeRota (MULTIGRID.h:1102-1255)
+    const bool band = nq > 8 && q[8] != 0.0, rot = nq > 9 && q[9] != 0.0;
     if (G < 1) throw std::invalid_argument("dehw: ngroups >= 1");
     if (kc < 0 || kc > 4 || kg < 0 || kg > 4) throw std::invalid_argument("dehw: integration refinement in [0, 4]");
     const double h = 0.01;  // cubic coarse elements
@@ -191,15 +240,38 @@ void make_dehw(Problem& P, const double* q, int nq) {
         MULTIGRID& m = P.mc.multGrid[s];
         if (wheel) m.mateElas = 110.0e9;
         build_box(m, lo, hi, n, gl, off);
+        if (wheel) {  // (on the lattice, before any local refinement)
+            const double t[3] = {0.5 * fric * p, 0.0, -p};
+            face_traction(m, 2, 2 * n[2] * (int64_t(1) << gl), t);
+        }
+        if (band) {
+            // the element layer touching the contact plane (lattice z = n[2] 2^gl)
+            const int64_t zc = n[2] * (int64_t(1) << gl);
+            std::set<int64_t> split;
+            for (int64_t e = 0; e < (int64_t)m.elemVect.size(); ++e) {
+                if (!m.elemVect[e].leaf()) continue;
+                int on = 0;
+                for (int64_t c : m.elemVect[e].cornNode) on += m.nodeLatt[c][2] == zc;
+                if (on == 4) {
+                    m.elemVect[e].refiPatt = 0;
+                    split.insert(e);
+                }
+            }
+            m.REFINE(split, {}, {});
+        }
         for (int64_t i = 0; i < m.numNodes(); ++i) {
             const auto& c = m.nodeCoor[i];
             if (g == 0 && c[0] <= 1e-12)
                 for (int a = 0; a < 3; ++a) m.consDofv.emplace(3 * i + a, 0.0);
-            if (!wheel && c[2] <= 1e-12) m.consDofv.emplace(3 * i + 2, 0.0);
-        }
-        if (wheel) {
-            const double t[3] = {0.5 * fric * p, 0.0, -p};
-            face_traction(m, 2, 2 * n[2] * (int64_t(1) << gl), t);
+            if (!wheel && c[2] <= 1e-12) {
+                m.consDofv.emplace(3 * i + 2, 0.0);
+                // (not on the glued x planes: a rotated node's dofs are in its own frame, as the
+                // reference's, which the interface operators would mix with the mate's)
+                if (rot && c[0] > lo[0] + 1e-12 && c[0] < hi[0] - 1e-12) {
+                    const double th = 0.3 * (c[1] / Ly - 0.5), cs = std::cos(th), sn = std::sin(th);
+                    m.nodeRota.emplace(i, std::array<double, 9>{1.0, 0.0, 0.0, 0.0, cs, -sn, 0.0, sn, cs});
+                }
+            }
         }
     }
     const int64_t scale = int64_t(1) << gl;
@@ -224,8 +296,17 @@ void make_dehw(Problem& P, const double* q, int nq) {
     for (int64_t ts = 0; ts < nint; ++ts) {
         Interface& itf = P.mc.searCont[ts];
         const int k = ts < G ? kc : kg;
-        conforming_interface(P.mc.multGrid[itf.body[0]], P.mc.multGrid[itf.body[1]], (int)plane[ts][0], plane[ts][1], itf.ip,
-                             1 << k);
+        if (band) {
+            // refined contact faces are half as wide: one subdivision level less keeps the
+            // integration points per unit area
+            const int ke = ts < G ? std::max(k - 1, 0) : k;
+            const double v = (double)plane[ts][1] / (double)scale * (plane[ts][0] == 2 ? H / n[2] : Lx / n[0]);
+            conforming_interface_xyz(P.mc.multGrid[itf.body[0]], P.mc.multGrid[itf.body[1]], (int)plane[ts][0], v, itf.ip,
+                                     1 << ke);
+        } else {
+            conforming_interface(P.mc.multGrid[itf.body[0]], P.mc.multGrid[itf.body[1]], (int)plane[ts][0], plane[ts][1],
+                                 itf.ip, 1 << k);
+        }
     }
     set_penalty(P);
 }
@@ -498,6 +579,21 @@ int ddpca_problem_view(ddpca_problem_t h, const char* cname, int64_t index, int6
             const std::string ck = std::string(isK ? "K" : "P") + "#" + std::to_string(index) + "#" + std::to_string(level);
             auto it = P.cache_csr.find(ck);
             if (it == P.cache_csr.end()) it = P.cache_csr.emplace(ck, isK ? g.consStif(level) : g.realProl(level)).first;
+            const Csr& m = it->second;
+            const std::string part = name.substr(2);
+            if (part == "ptr") put(m.ptr, data, count, dtype);
+            else if (part == "col") put(m.col, data, count, dtype);
+            else if (part == "val") put(m.val, data, count, dtype);
+            else if (part == "shape") { auto& v = P.cache_i64[key]; v = {m.nrow, m.ncol}; put(v, data, count, dtype); }
+            else throw ApiError(DDPCA_EINVAL, "csr part");
+        } else if (name.rfind("H:", 0) == 0) {
+            // the hanging level's rows of prolOper[maxiLeve] (3 (nodeAll - NL) x 3 NL; empty without one)
+            const std::string ck = "H#" + std::to_string(index);
+            auto it = P.cache_csr.find(ck);
+            if (it == P.cache_csr.end()) {
+                if (g.leveCount.empty()) throw ApiError(DDPCA_ESTATE, "subdomain " + std::to_string(index) + " was not built here");
+                it = P.cache_csr.emplace(ck, g.hangRows()).first;
+            }
             const Csr& m = it->second;
             const std::string part = name.substr(2);
             if (part == "ptr") put(m.ptr, data, count, dtype);

@@ -992,6 +992,7 @@ struct CoarseDev {
     bool on = false, inverted = false;
     int64_t n = 0, nown = 0, nxn = 0, qnn = 0;
     double dense_bytes = 0.0;  // n^2 8 B: what the dense inverse would hold per rank
+    bool mg_fallback = false;  // the memory budget asked for DOUBLE_M, its hierarchy was not buildable
     DevBuf<double> g, f0, xc, xn, ainv;
     DevBuf<int64_t> rptr;
     DevBuf<int32_t> rcol;
@@ -1277,7 +1278,10 @@ void build(ddpca_mcontact& H, Problem& P) {
         SubdomainOps o;
         o.nnodes.assign(g.leveCount.begin(), g.leveCount.end());
         for (const auto& b : g.levelStif) o.K.push_back(&b);
-        for (const auto& s : g.scalProl) o.S.push_back(&s);
+        // prolOper: scalProl with the nodal rotations' 3x3 blocks as block entries (MULTIGRID.h:
+        // 1141-1181; == scalProl without nodeRota); an operator-level subdomain has scalProl only
+        // (its block entries already in it)
+        for (const auto& s : g.prolOper.empty() ? g.scalProl : g.prolOper) o.S.push_back(&s);
         o.dof_free = g.consFlag.data();
         o.coords = g.nodeCoor.empty() ? nullptr : g.nodeCoor[0].data();
         ops.push_back(o);
@@ -1908,15 +1912,28 @@ void build_coarse(ddpca_mcontact& H, Problem& P) {
     C.dense_bytes = 8.0 * (double)n * (double)n;
     // LATIN: DOUBLE_M (MCONTACT.h:1236) with the host MULTISCALE's coarse contact nodes, one rank
     const bool mg_ok = !cs.latin || (!cs.rank_local && !cs.coarNode.empty());
-    C.mg = (n >= (mg_env ? std::atoll(mg_env) : 120000) || C.dense_bytes > dense_max) && mg_ok;
+    const bool by_rows = n >= (mg_env ? std::atoll(mg_env) : 120000);
+    C.mg = (by_rows || C.dense_bytes > dense_max) && mg_ok;
     C.latin = cs.latin;
+    if (C.mg && H.mg && C.nown) {
+        try {
+            build_coarse_mg(H, mc, C);
+        } catch (const ApiError& e) {
+            // LATIN's DOUBLE_M hierarchy needs the coarse contact nodes nested level by level; where
+            // they are not (BLOCK's stacked bodies), a one-rank handle that chose the multigrid
+            // solve for memory alone keeps the dense inverse (the reference: LDLT below DIRE_MAXI)
+            if (by_rows || !cs.latin || H.nranks > 1 || n > 46000) throw;
+            C.cmg.reset();
+            C.mg = false;
+            C.mg_fallback = true;
+            if (std::getenv("DDPCA_VERBOSE")) std::fprintf(stderr, "[ddpca] DOUBLE_M not built (%s): dense coarse inverse\n", e.what());
+        }
+    }
     // coarse solve: the owned rows of the dense inverse against g, or (DOUBLE_M) g scattered into
     // the coarse MGPIS and its owned rows gathered back (its PCG is counted by its own model)
     C.bytes_iter += C.mg ? 20.0 * (double)n + 24.0 * (double)C.nown
                          : 8.0 * (double)C.nown * (double)n + 8.0 * (double)n + 8.0 * (double)C.nown;
-    if (C.mg) {
-        if (H.mg && C.nown) build_coarse_mg(H, mc, C);
-    } else {
+    if (!C.mg) {
         // dense rows of globCoup_1 (inverted once every rank holds all rows)
         C.dense.assign((size_t)n * n, 0.0);
         std::vector<int64_t> fill_rows = C.own_rows;
@@ -2633,13 +2650,16 @@ int64_t mcontact_gpu_get(mcontact_t h, const char* what, int64_t index, void* ou
                 for (int64_t i = 0; i < std::min(n, cap); ++i) static_cast<int64_t*>(out)[i] = h->subs[i].tv;
             return;
         }
-        if (w == "coarse_solve") {  // [rows, 1 = multigrid (DOUBLE_M / DOUBLE_M_1) else 0, dense inverse bytes]
-            n = 3;
-            if (out && cap >= 3) {
+        if (w == "coarse_solve") {
+            // [rows, 1 = multigrid (DOUBLE_M / DOUBLE_M_1) else 0, dense inverse bytes,
+            //  1 = the budget asked for DOUBLE_M but its hierarchy was not buildable (dense kept)]
+            n = 4;
+            if (out && cap >= 4) {
                 auto* o = static_cast<int64_t*>(out);
                 o[0] = h->cs.on ? h->cs.n : 0;
                 o[1] = h->cs.on && h->cs.mg ? 1 : 0;
                 o[2] = h->cs.on && !h->cs.mg ? (int64_t)h->cs.dense_bytes : 0;
+                o[3] = h->cs.mg_fallback ? 1 : 0;
             }
             return;
         }

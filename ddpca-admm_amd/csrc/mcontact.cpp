@@ -236,19 +236,48 @@ void Interface::BUILD(const MULTIGRID& g0, const MULTIGRID& g1) {
 
 void MCONTACT::ESTABLISH(const std::vector<uint8_t>* owned) {
     auto mine = [&](int64_t tv) { return !owned || (*owned)[tv] != 0; };
+    const int64_t nsub = (int64_t)multGrid.size(), nint = (int64_t)searCont.size();
+    // ---- TRANSFER first: a general tree (local refinement -> hanging level, coupled nodes) is
+    // renumbered to the reference's positions (MULTIGRID.h:884-910, earlTran), and the integration
+    // points of its interfaces follow the numbering before the mortar operators are built; on a
+    // uniform tree node ids already are positions.  Transferred: the owned subdomains, the mates of
+    // their interfaces, and with a coarse space every subdomain (MULTISCALE reads all of them).
+    std::vector<uint8_t> need(nsub, 0);
+    for (int64_t tv = 0; tv < nsub; ++tv) need[tv] = mine(tv) || (muscSett & 3) ? 1 : 0;
+    for (const auto& itf : searCont)
+        if (mine(itf.body[0]) || mine(itf.body[1])) need[itf.body[0]] = need[itf.body[1]] = 1;
+    std::vector<uint8_t> renumbered(nsub, 0);
+    std::vector<double> t_transfer(nsub, 0.0);
 #pragma omp parallel for schedule(dynamic, 1)
-    for (int64_t ts = 0; ts < (int64_t)searCont.size(); ++ts) {
+    for (int64_t tv = 0; tv < nsub; ++tv) {
+        MULTIGRID& g = multGrid[tv];
+        if (!need[tv] || !g.scalProl.empty()) continue;
+        const auto t0 = std::chrono::steady_clock::now();
+        g.TRANSFER();
+        t_transfer[tv] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        renumbered[tv] = g.general ? 1 : 0;
+    }
+    for (int64_t ts = 0; ts < nint; ++ts)
+        for (int s = 0; s < 2; ++s) {
+            const int64_t b = searCont[ts].body[s];
+            if (!renumbered[b]) continue;
+            const MULTIGRID& g = multGrid[b];
+            std::vector<int64_t> pos(g.posiNode.size());
+            for (int64_t p = 0; p < (int64_t)g.posiNode.size(); ++p) pos[g.posiNode[p]] = p;
+            for (auto& ip : searCont[ts].ip)
+                for (int k = 0; k < 4; ++k) ip.node[s][k] = pos.at(ip.node[s][k]);
+        }
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int64_t ts = 0; ts < nint; ++ts) {
         Interface& itf = searCont[ts];
         if (mine(itf.body[0]) || mine(itf.body[1])) itf.BUILD(multGrid[itf.body[0]], multGrid[itf.body[1]]);
     }
 #pragma omp parallel for schedule(dynamic, 1)
-    for (int64_t tv = 0; tv < (int64_t)multGrid.size(); ++tv) {
+    for (int64_t tv = 0; tv < nsub; ++tv) {
         if (!mine(tv)) continue;
         MULTIGRID& g = multGrid[tv];
         const bool verbose = std::getenv("DDPCA_VERBOSE") != nullptr;
         auto now = [] { return std::chrono::steady_clock::now(); };
-        auto t0 = now();
-        g.TRANSFER();
         auto t1 = now();
         g.STIF_MATR();
         auto t2 = now();
@@ -257,11 +286,14 @@ void MCONTACT::ESTABLISH(const std::vector<uint8_t>* owned) {
                 if (itf.body[s] == tv) g.ADD_NODAL(itf.systMass[s]);
         auto t3 = now();
         g.CONSTRAINT();
+        // the hanging level's rows of prolOper[maxiLeve] (OUTP_SUB1, MULTIGRID.h:1279), read by the
+        // device (op_hang) as for an operator-level subdomain (ddpca_problem_set_hanging)
+        if (g.nodeAll) g.hangProl = g.hangRows();
         auto t4 = now();
         if (verbose) {
             auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
             std::fprintf(stderr, "[ddpca] establish sd %ld: transfer %.0f ms, stif %.0f ms, systMass %.0f ms, constraint %.0f ms\n",
-                         (long)tv, ms(t0, t1), ms(t1, t2), ms(t2, t3), ms(t3, t4));
+                         (long)tv, t_transfer[tv], ms(t1, t2), ms(t2, t3), ms(t3, t4));
         }
     }
     // ---- coarse space (MCONTACT.h:858-863)

@@ -114,8 +114,8 @@ inline std::string compare(ddpca_problem_t p, const std::vector<int32_t>& owners
 // Returns a JSON object; "null" when the first run had no coarse space or its multigrid solve was
 // forced by the row count (DIRE_MAXI), where the dense inverse is not available.
 inline std::string coarse_alt(ddpca_problem_t p, int64_t nsub, mcontact_t h0, int64_t n0, int64_t maxit = 3000) {
-    int64_t cs0[3] = {0, 0, 0};
-    check((int)std::min<int64_t>(mcontact_gpu_get(h0, "coarse_solve", 0, cs0, 3), 0));
+    int64_t cs0[4] = {0, 0, 0, 0};
+    check((int)std::min<int64_t>(mcontact_gpu_get(h0, "coarse_solve", 0, cs0, 4), 0));
     if (cs0[0] == 0 || (cs0[1] == 1 && cs0[0] >= 120000)) return "null";
     const char* old = std::getenv("DDPCA_COARSE_DENSE_MB");
     const std::string keep = old ? old : "";
@@ -126,8 +126,8 @@ inline std::string coarse_alt(ddpca_problem_t p, int64_t nsub, mcontact_t h0, in
     if (old) setenv("DDPCA_COARSE_DENSE_MB", keep.c_str(), 1);
     else unsetenv("DDPCA_COARSE_DENSE_MB");
     check(rc);
-    int64_t cs1[3] = {0, 0, 0};
-    check((int)std::min<int64_t>(mcontact_gpu_get(h, "coarse_solve", 0, cs1, 3), 0));
+    int64_t cs1[4] = {0, 0, 0, 0};
+    check((int)std::min<int64_t>(mcontact_gpu_get(h, "coarse_solve", 0, cs1, 4), 0));
     const int64_t n1 = mcontact_gpu_iterate(h, maxit, 1);
     check((int)std::min<int64_t>(n1, 0));
     double du = 0.0;
@@ -143,9 +143,9 @@ inline std::string coarse_alt(ddpca_problem_t p, int64_t nsub, mcontact_t h0, in
     mcontact_gpu_destroy(h);
     char buf[320];
     std::snprintf(buf, sizeof(buf),
-                  "{\"rows\": %ld, \"first_mg\": %ld, \"first_dense_bytes\": %ld, \"alt_mg\": %ld, \"iters_first\": %ld, "
+                  "{\"rows\": %ld, \"first_mg\": %ld, \"first_dense_bytes\": %ld, \"alt_mg\": %ld, \"alt_fallback\": %ld, \"iters_first\": %ld, "
                   "\"iters_alt\": %ld, \"resuDisp_rel\": %.3g}",
-                  (long)cs0[0], (long)cs0[1], (long)cs0[2], (long)cs1[1], (long)n0, (long)n1, du);
+                  (long)cs0[0], (long)cs0[1], (long)cs0[2], (long)cs1[1], (long)cs1[3], (long)n0, (long)n1, du);
     return buf;
 }
 

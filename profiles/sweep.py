@@ -14,7 +14,7 @@ import time
 
 def main():
     out = sys.argv[1]
-    base = ["python3", "bench.py", "--steps", "4", "--warmup", "1", "--no-cpu-baseline"]
+    base = ["python3", "bench.py", "--steps", "4", "--warmup", "1", "--no-cpu-baseline", "--no-general"]
     for cfg in sys.argv[2:]:
         t0 = time.time()
         toks = cfg.split()

@@ -164,13 +164,18 @@ def test_headline_fullsize_batched_solves_match_oracle(ddpca, oracle, gpu):
 
 @pytest.mark.parametrize("env,opts", [(("DDPCA_STREAMS", "1"), "HEADLINE_OPTIONS"),
                                       (("DDPCA_STREAMS", "1"), "HEADLINE_OPTIONS_SMALL"),
-                                      (("DDPCA_TAIL_PACING", "0"), "HEADLINE_OPTIONS")],
-                         ids=["one-stream", "one-stream-small", "whole-replay-pacing"])
+                                      (("DDPCA_TAIL_PACING", "0"), "HEADLINE_OPTIONS"),
+                                      (("DDPCA_FUSED_FIN", "0"), "HEADLINE_OPTIONS"),
+                                      (("DDPCA_FUSED_FIN", "0"), "HEADLINE_OPTIONS_SMALL")],
+                         ids=["one-stream", "one-stream-small", "whole-replay-pacing", "k_fin-launches",
+                              "k_fin-launches-small"])
 def test_schedule_variants_are_bit_identical(ddpca, gpu, monkeypatch, env, opts):
     """Schedule-only variants of the headline path must not change a bit: the two-stream split of
     the body-balance batch and of the mass CG (MgpisDevice / MassBatch ::set_split, default on)
-    against one stream, on both option sets; and whole-replay pacing to the end of every solve
-    against the one-iteration tail graphs.  ADMM trajectory, displacements and PCG iteration
+    against one stream, on both option sets; whole-replay pacing to the end of every solve
+    against the one-iteration tail graphs; and the PCG scalar updates as separate k_fin launches
+    against their fused form (the last-arriving workgroup of the SpMV, k_axpy and the V-cycle's last
+    fine-level launch reduces the subdomain's partials in k_fin's order), on both option sets.  ADMM trajectory, displacements and PCG iteration
     counts equal bit for bit (8 ADMM iterations, reduced chain).  (The variants measured slower
     and kept opt-in in round 3 -- stencil-coded copies, XCD-slab placement, four-wave colour
     workgroups, inverses by row, fused first sweeps -- were deleted in round 4)"""
@@ -217,3 +222,67 @@ def test_coarse_correction_kx_from_recursive_residual(ddpca, gpu, monkeypatch):
     print(f"b - r vs explicit K x: worst resuMoni rel {worst:.2e}, displacements {du:.2e}")
     assert ok, worst
     assert du <= 1e-9, du
+
+
+def _oracle_problem_no_coarse(P, oracle):
+    """_oracle_problem without a coarse space, plus each subdomain's hanging rows (oracle.admm's
+    `hang`: OUTP_SUB1's prolOper[maxiLeve] rows, MULTIGRID.h:1279, and their fold into the body
+    balance, 1257-1261)."""
+    subs = []
+    for tv in range(P.nsub):
+        G = P.grid(tv)
+        L = G.maxiLeve
+        M = oracle.MgpisOracle([G.consStif(l) for l in range(L + 1)], [G.realProl(l) for l in range(L)])
+        n3 = 3 * int(P.array("leveCount", tv)[-1])  # the MGPIS fine level (consFlag also covers the hanging level)
+        s = dict(consForc=G.consForc, solve=(lambda b, M=M: M.CG_SOLV(1, b)[0]), consFlag=G.consFlag[:n3],
+                 presc=np.zeros(n3))
+        H = G.hangRows()
+        if H.shape[0]:
+            s["hang"] = H
+        subs.append(s)
+    names = ["systTran", "systTran_pena", "inteMass", "inteMass_pena", "inpoLagr", "pemaInpo_r", "inteInpo"]
+    ifaces = []
+    for ts in range(P.nint):
+        fric, pn, pf = P.array("iface_param", ts)
+        ifaces.append(dict(body=tuple(int(b) for b in P.array("iface_body", ts)), fric=float(fric),
+                           comp=1 if fric == 0.0 else 3, pemaDiag=P.array("pemaDiag", ts),
+                           inpoNgap=P.array("inpoNgap", ts),
+                           ops=[{n: P.csr(n, 2 * ts + s) for n in names} for s in range(2)]))
+    return subs, ifaces
+
+
+@pytest.mark.parametrize("opts", ["HEADLINE_OPTIONS"])
+def test_general_mesh_trajectory_matches_oracle(ddpca, oracle, gpu, monkeypatch, opts):
+    """bench.py's general-mesh line at reduced size: the DEHW chain with its contact band refined
+    once more (DEHW.h:1562 -- a general tree: TRANSFER renumbers it, hanging nodes on the level past
+    the MGPIS hierarchy, contact and glued faces in the band refined) and rotated support nodes
+    (DEHW.h:197 -- prolongation blocks off w I, R^T K R), no coarse space, the lattice transfers
+    switched off (DDPCA_LATTICE=0: explicit index lists), the bench's option set at 8 subdomains per
+    GPU.  A fixed-k trajectory (8 ADMM iterations) against the CPU oracle on the same host operators, with the hanging rows:
+    resuMoni rows 1e-6 relative, displacements (incl. the hanging level) 1e-7, contact tractions
+    1e-6 -- the headline trajectory test's tolerances."""
+    monkeypatch.setenv("DDPCA_LATTICE", "0")
+    H = getattr(ddpca, opts)
+    P = ddpca.headline_problem(gl=3, **ddpca.GENERAL_FEATURES).ESTABLISH()
+    Pu = ddpca.headline_problem(gl=3, band=1, rot=0).ESTABLISH()
+    G, Gu = P.grid(0), Pu.grid(0)
+    L = G.maxiLeve
+    assert L == 4 and G.hangRows().shape[0] > 0  # gl 3 + the band level, hanging nodes past it
+    # the rotated support nodes change the transfer blocks below the band level (a new node above
+    # the bottom face takes w R_par from its rotated parents; same positions, same sparsity)
+    assert abs(G.realProl(L - 2) - Gu.realProl(L - 2)).max() > 1e-3
+    mc = ddpca.MCONTACT(P, **H)
+    k = 8
+    assert mc.CONTACT_ANALYSIS(k, check=False) == k
+    subs, ifaces = _oracle_problem_no_coarse(P, oracle)
+    res = oracle.admm(subs, ifaces, maxit=k, check=False)
+    ok, worst = _rows_close(mc.monitor(), res["rows"], k=k, rtol=1e-6)
+    print(f"general mesh ({opts}): last PCG iterations {list(mc.get('pcg_iters'))}, worst resuMoni rel {worst:.2e}")
+    assert ok, worst
+    for tv in range(P.nsub):
+        u, ur = mc.get("resuDisp", tv), res["u"][tv]
+        assert len(u) == len(ur) == 3 * len(P.grid(tv).nodeCoor), tv
+        assert np.linalg.norm(u - ur) <= 1e-7 * np.linalg.norm(ur), tv
+    for ts in range(P.nint):
+        g, gr = mc.get("inpoGamm", ts), res["gamma"][ts]
+        assert np.linalg.norm(g - gr) <= 1e-6 * max(np.linalg.norm(gr), 1e-300), ts

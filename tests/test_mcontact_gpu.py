@@ -347,7 +347,9 @@ def _check_coarse_alt(res):
     alt = res["coarse_alt"]
     print("coarse_alt", alt)
     assert alt is not None and alt["rows"] > 0, res
-    assert alt["alt_mg"] != alt["first_mg"], alt
+    # LATIN's DOUBLE_M needs coarse contact nodes nested level by level; where they are not (BLOCK's
+    # stacked bodies) the one-rank handle keeps the dense inverse and says so
+    assert alt["alt_mg"] != alt["first_mg"] or alt["alt_fallback"] == 1, alt
     assert alt["first_dense_bytes"] == (0 if alt["first_mg"] else 8 * alt["rows"] ** 2), alt
     assert abs(alt["iters_alt"] - alt["iters_first"]) <= 1 and alt["resuDisp_rel"] <= 1e-8, alt
 
