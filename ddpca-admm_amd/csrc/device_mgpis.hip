@@ -29,17 +29,7 @@ namespace ddpca {
 namespace {
 
 enum SellMode { kSpmv = 0, kResid = 1, kJac = 2, kPcg = 3, kCheb = 4 };
-enum FinWhat { kFinInit = 0, kFinBeta0 = 1, kFinAlpha = 2, kFinRR = 3, kFinBeta = 4, kFinInitWarm = 5 };  // fin_apply's codes
-
-struct FinFuse {
-    unsigned int* tick;    // per subdomain arrivals in this launch (zero between launches)
-    const int32_t* need;   // per subdomain: waves arriving in this launch (null: cb[s+1] - cb[s])
-    const int64_t* cb;     // per subdomain chunk-partial bounds
-    const double* partial;
-    PcgScal* sc;           // the scalars the launch reads (this half's copy under the split)
-    PcgMirror* mirror;
-    int what = -1;         // FinWhat; < 0: no fused update
-};
+enum FinWhat { kFinInit = 0, kFinBeta0 = 1, kFinAlpha = 2, kFinRR = 3, kFinBeta = 4, kFinInitWarm = 5 };
 
 struct SellArgs {
     const int32_t* slots;
@@ -62,7 +52,6 @@ struct SellArgs {
     const double* tab;     // table mode: tstride doubles per table row, slot-major 3x3 blocks
     int64_t tstride;
     const int32_t* ctype;  // table mode: chunk -> its rows' common table row, -1 = mixed
-    FinFuse fin;           // DOT launches: the fused scalar update (fin.what < 0: none, k_fin follows)
 };
 
 __device__ __forceinline__ double wave_sum(double v) {
@@ -71,145 +60,13 @@ __device__ __forceinline__ double wave_sum(double v) {
     return v;
 }
 
-typedef __attribute__((address_space(1))) unsigned long long gu64;
-typedef __attribute__((address_space(1))) unsigned int gu32;
-
-// write-through (sc1) store / load of one chunk partial: the fused finish hands partials from the
-// waves of one launch to its last arriving workgroup across the eight per-XCD L2s without fences
-// (MI355X_MICROARCH.md, inter-workgroup visibility: every handed-off word stored sc1 and drained
-// before the ticket, every load of it sc1)
-__device__ __forceinline__ void store_wt(double* p, double v) {
-    __hip_atomic_store((gu64*)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ double load_wt(const double* p) {
-    return __longlong_as_double((long long)__hip_atomic_load((gu64*)const_cast<double*>(p), __ATOMIC_RELAXED,
-                                                               __HIP_MEMORY_SCOPE_AGENT));
-}
-
 // Chunk partial of a dot product: one wavefront = one 64-node chunk, fixed shuffle order.
 __device__ __forceinline__ void chunk_partial(double v, double* partial, int64_t chunk) {
     v = wave_sum(v);
-    if ((threadIdx.x & 63) == 0) store_wt(partial + chunk, v);  // sc1: a fused finish may read it in-launch
+    if ((threadIdx.x & 63) == 0) partial[chunk] = v;
 }
 
 __device__ __forceinline__ bool stopped(const PcgScal* sc, int sub) { return sc && sc[sub].done; }
-
-// ---- PCG scalar updates (k_fin's per-subdomain reductions), standalone or fused into the kernel
-// that produces the chunk partials.
-// k_fin's update of one subdomain's scalars from its reduced sum(s); FinWhat below
-__device__ __forceinline__ void fin_apply(int what, double s, double s2, PcgScal* sc, PcgMirror* mirror) {
-    const int was_done = sc->done;
-    if (what == 0 || what == 5) {  // kFinInit / kFinInitWarm
-        const double bb = what == 0 ? s : s2;
-        sc->rr = s;
-        sc->bb = bb;
-        sc->tol2 = sc->tol2 * bb;  // tol2 holds rtol^2 on entry
-        sc->iter = 0;
-        sc->fail = 0;
-        sc->beta = 0.0;
-        sc->done = (s <= sc->tol2 || sc->maxit <= 0) ? 1 : 0;
-        mirror_store(mirror, 0, sc->done, 0);
-        return;
-    } else if (what == 1) {  // kFinBeta0
-        sc->delta = s;
-        sc->beta = 0.0;
-    } else if (what == 2) {  // kFinAlpha
-        sc->pq = s;
-        if (!(s > 0.0) || !isfinite(s)) {
-            sc->fail = 1;
-            sc->done = 1;
-        }
-        sc->alpha = sc->delta / s;
-    } else if (what == 3) {  // kFinRR
-        sc->rr = s;
-        sc->iter += 1;
-        if (!isfinite(s)) {
-            sc->fail = 1;
-            sc->done = 1;
-        }
-        if (s <= sc->tol2 || sc->iter >= sc->maxit) sc->done = 1;
-        mirror_store(mirror, sc->iter, sc->done, sc->fail);
-        return;
-    } else {  // kFinBeta
-        if (!isfinite(s)) {
-            sc->fail = 1;
-            sc->done = 1;
-        }
-        sc->beta = s / sc->delta;
-        sc->delta = s;
-    }
-    if (sc->done != was_done) mirror_store(mirror, sc->iter, sc->done, sc->fail);
-}
-
-// The last-arriving workgroup of a subdomain reduces its chunk partials in k_fin's exact order
-// (1024 virtual threads, four accumulators each, 16 wave sums combined in fours), so the fused
-// and the separate update produce the same bits.
-
-
-constexpr int kFinVT = 1024;  // k_fin's threads (the summation order)
-
-// Every wave of the block calls this once with its subdomain (-1: no partial from this wave);
-// its partial store (store_wt) must precede the call.
-template <int NW>
-__device__ __forceinline__ void fused_finish(const FinFuse& f, int sub) {
-    __shared__ int s_sub[NW];
-    __shared__ int s_last[NW];
-    __shared__ double red[kFinVT / kWave];
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's partial has landed (sc1)
-    if (lane == 0) s_sub[w] = sub;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        for (int v = 0; v < NW;) {
-            const int sv = s_sub[v];
-            int e = v + 1;
-            while (e < NW && s_sub[e] == sv) ++e;
-            s_last[v] = 0;
-            for (int q = v + 1; q < e; ++q) s_last[q] = 0;
-            if (sv >= 0) {
-                const unsigned n = (unsigned)(e - v);
-                const unsigned need = f.need ? (unsigned)f.need[sv] : (unsigned)(f.cb[sv + 1] - f.cb[sv]);
-                const unsigned old = __hip_atomic_fetch_add((gu32*)(f.tick + sv), n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (old + n == need) s_last[v] = 1;
-            }
-            v = e;
-        }
-    }
-    __syncthreads();
-    for (int v = 0; v < NW; ++v) {
-        if (!s_last[v]) continue;  // block-uniform
-        const int sv = s_sub[v];
-        const int64_t k0 = f.cb[sv], k1 = f.cb[sv + 1];
-        // real wave w holds k_fin's virtual waves vw = w, w + NW, ... (virtual thread t = 64 vw + lane),
-        // one at a time (the finish must not raise the streaming kernel's register count), each
-        // with two of k_fin's rounds of four loads in flight together, added in k_fin's order
-        for (int vw = w; vw < kFinVT / kWave; vw += NW) {
-            const int64_t t = (int64_t)vw * kWave + lane;
-            double a[4] = {0.0, 0.0, 0.0, 0.0};
-            for (int64_t k = k0 + t; k < k1; k += 8 * kFinVT) {
-                double l[8];
-#pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    const int64_t q = k + (int64_t)u * kFinVT;
-                    l[u] = q < k1 ? load_wt(f.partial + q) : 0.0;
-                }
-#pragma unroll
-                for (int u = 0; u < 8; ++u)
-                    if (k + (int64_t)u * kFinVT < k1) a[u & 3] += l[u];
-            }
-            const double sw = wave_sum((a[0] + a[1]) + (a[2] + a[3]));
-            if (lane == 0) red[vw] = sw;
-        }
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            double st = 0.0;
-            for (int q = 0; q < kFinVT / kWave; q += 4) st += (red[q] + red[q + 1]) + (red[q + 2] + red[q + 3]);
-            fin_apply(f.what, st, 0.0, f.sc + sv, f.mirror + sv);
-            __hip_atomic_store((gu32*)(f.tick + sv), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        __syncthreads();
-    }
-}
 
 template <bool BJ, typename MT = double>
 __device__ __forceinline__ void apply_m(const MT* minv, int64_t row, double r0, double r1, double r2,
@@ -460,22 +317,14 @@ constexpr int default_variant(int mode) { return (mode == 0 || mode == 1) ? 2 : 
 
 // One wavefront per 64-node chunk, one lane per node row, three accumulators per lane; T is the
 // storage type of streamed operator values (all arithmetic fp64); TBL: values from the table.
-// FIN: the dot product's scalar update (a.fin) fused in: every wave reaches the tail, the
-// subdomain's last-arriving workgroup reduces its partials (fused_finish)
 template <int MODE, bool BJ, bool DOT, typename T = double, int V = default_variant(MODE), bool TBL = false,
-          typename CT = int32_t, bool FIN = false>
+          typename CT = int32_t>
 __global__ __launch_bounds__(kBlock) void k_sell(SellArgs a, const double* __restrict__ tab) {
     const int lane = threadIdx.x & 63;
     const int64_t c = (int64_t)blockIdx.x * (kBlock / kWave) + (threadIdx.x >> 6);
-    int sub = -1;
-    if (c < a.nch) {
-        sub = a.csub[c];
-        if (stopped(a.sc, sub)) sub = -1;
-    }
-    if (sub < 0) {
-        if constexpr (FIN) fused_finish<kBlock / kWave>(a.fin, -1);
-        return;
-    }
+    if (c >= a.nch) return;
+    const int sub = a.csub[c];
+    if (stopped(a.sc, sub)) return;
     const int64_t row = c * kChunk + lane;
     const int ns = a.slots[c];
     const int64_t base = a.off[c];
@@ -550,7 +399,6 @@ __global__ __launch_bounds__(kBlock) void k_sell(SellArgs a, const double* __res
         if (DOT) dotv = __builtin_fma(b2, n2, __builtin_fma(b1, n1, b0 * n0));
     }
     if (DOT) chunk_partial(dotv, a.partial, c);
-    if constexpr (FIN) fused_finish<kBlock / kWave>(a.fin, sub);
 }
 
 // Small levels (fewer chunks than the chip has SIMDs): one workgroup per chunk, each of its four
@@ -629,7 +477,6 @@ struct GsArgs {
     const PcgScal* sc;
     double* partial;
     const float* minvc;  // chunk-ordered fp32 inverses (GsFine::minvc), or null (fp64 copy): minv by row
-    FinFuse fin;         // the backward sweep's last launch: the fused beta update
 };
 
 // the colour sweep's per-row tail: PH 1 stores r = -s; PH 0 / 2 store x = M (b - s) and return
@@ -670,29 +517,14 @@ __device__ __forceinline__ double gs_epilogue(const GsArgs& a, int64_t c, int ln
 
 // One wave per workgroup: a colour's chunks spread over more CUs than four-wave groups (+1 % at 8
 // subdomains per GPU, profiles/r03j)
-// Occupancy: at 82 VGPRs the block-exponent fp16 backward sweep ran 5 waves per SIMD, so a colour
-// launch of the headline (6.3k one-wave groups) needed 1.24 rounds of the chip's 5120 wave slots;
-// capped at 64 VGPRs (8 waves per SIMD, 8192 slots) every colour launch is resident at once
-#ifndef DDPCA_GS_WAVES_PER_EU
-#define DDPCA_GS_WAVES_PER_EU 8
-#endif
-// FIN (the backward sweep's last launch with the fused beta update): four-wave workgroups, so the
-// last-arriving one reduces the member's partials with 256 threads
-template <int PH, bool DOT, typename T, typename CT, bool FIN = false>
-__global__ __launch_bounds__(FIN ? kBlock : kWave) __attribute__((amdgpu_waves_per_eu(DDPCA_GS_WAVES_PER_EU))) void k_gs(GsArgs a) {
-    const int lane = threadIdx.x & 63;
-    const int64_t li = FIN ? (int64_t)blockIdx.x * (kBlock / kWave) + (threadIdx.x >> 6) : (int64_t)blockIdx.x;
-    int sub = -1;
-    int64_t c = 0;
-    if (li < a.n) {
-        c = a.list ? (int64_t)a.list[li] : li;
-        sub = a.csub[c];
-        if (stopped(a.sc, sub)) sub = -1;
-    }
-    if (sub < 0) {
-        if constexpr (FIN) fused_finish<kBlock / kWave>(a.fin, -1);
-        return;
-    }
+template <int PH, bool DOT, typename T, typename CT>
+__global__ __launch_bounds__(kWave) void k_gs(GsArgs a) {
+    const int lane = threadIdx.x;
+    const int64_t li = blockIdx.x;
+    if (li >= a.n) return;
+    const int64_t c = a.list ? (int64_t)a.list[li] : li;
+    const int sub = a.csub[c];
+    if (stopped(a.sc, sub)) return;
     const int32_t rr = a.rowidx[c * kChunk + lane];
     const bool real = rr >= 0;
     const int64_t row = real ? rr : ~rr;  // pad lanes gather at a real row with zero blocks
@@ -712,7 +544,6 @@ __global__ __launch_bounds__(FIN ? kBlock : kWave) __attribute__((amdgpu_waves_p
     }
     const double dotv = gs_epilogue<PH, DOT, T>(a, c, lane, row, real, s0, s1, s2);
     if (DOT) chunk_partial(dotv, a.partial, c);
-    if constexpr (FIN) fused_finish<kBlock / kWave>(a.fin, sub);
 }
 
 // Node-parallel kernels: thread = node, 256 nodes per workgroup; a wavefront is one chunk, so
@@ -1019,20 +850,12 @@ __global__ __launch_bounds__(kBlock) void k_pcg_init_warm(const double* b, doubl
 // x += alpha p, r -= alpha q, partial ||r||^2.  One wavefront per 64-node chunk walks the chunk's
 // 192 doubles flat (lane, lane + 64, lane + 128): every load is a contiguous 512-B wave access
 // instead of three 24-B-strided ones.
-template <bool FIN = false>
 __global__ __launch_bounds__(kBlock) void k_axpy(double* x, double* r, const double* p, const double* q,
-                                                 const PcgScal* sc, double* partial, int64_t nn, const int32_t* csub,
-                                                 FinFuse fin) {
+                                                 const PcgScal* sc, double* partial, int64_t nn, const int32_t* csub) {
     const int64_t c = (int64_t)blockIdx.x * (kBlock / kWave) + (threadIdx.x >> 6);
-    int sub = -1;
-    if (c * kChunk < nn) {
-        sub = csub[c];
-        if (stopped(sc, sub)) sub = -1;
-    }
-    if (sub < 0) {
-        if constexpr (FIN) fused_finish<kBlock / kWave>(fin, -1);
-        return;
-    }
+    if (c * kChunk >= nn) return;
+    const int sub = csub[c];
+    if (stopped(sc, sub)) return;
     const double al = sc[sub].alpha;
     const int64_t base = c * 3 * kChunk + (threadIdx.x & 63);
     double s = 0.0;
@@ -1045,7 +868,6 @@ __global__ __launch_bounds__(kBlock) void k_axpy(double* x, double* r, const dou
         s += v * v;
     }
     chunk_partial(s, partial, c);
-    if constexpr (FIN) fused_finish<kBlock / kWave>(fin, sub);
 }
 
 // z = D^-1 r (diagonal preconditioner, DIAG_PREC), partial r^T z
@@ -1075,7 +897,6 @@ __global__ __launch_bounds__(kBlock) void k_dot(const double* x, const double* y
 // kFinT = 1024 threads read a subdomain's ~6400 fine chunk partials in ~2 loads each (256: 0.2-0.6 %
 // slower overall, profiles/r02u_ab.json)
 constexpr int kFinT = 1024;
-static_assert(kFinT == kFinVT, "the fused finish reproduces k_fin's order");
 __global__ __launch_bounds__(kFinT) void k_fin(int what, const double* partial, const double* partial2,
                                                const int64_t* cb, PcgScal* scv, PcgMirror* mirror) {
     const int sub = blockIdx.x;
@@ -1109,7 +930,47 @@ __global__ __launch_bounds__(kFinT) void k_fin(int what, const double* partial, 
         s += (red[w] + red[w + 1]) + (red[w + 2] + red[w + 3]);
         s2 += (red2[w] + red2[w + 1]) + (red2[w + 2] + red2[w + 3]);
     }
-    fin_apply(what, s, s2, sc, mirror + sub);
+    const int was_done = sc->done;
+    if (what == kFinInit || what == kFinInitWarm) {
+        const double bb = what == kFinInit ? s : s2;
+        sc->rr = s;
+        sc->bb = bb;
+        sc->tol2 = sc->tol2 * bb;  // tol2 holds rtol^2 on entry
+        sc->iter = 0;
+        sc->fail = 0;
+        sc->beta = 0.0;
+        sc->done = (s <= sc->tol2 || sc->maxit <= 0) ? 1 : 0;
+        mirror_store(mirror + sub, 0, sc->done, 0);
+        return;
+    } else if (what == kFinBeta0) {
+        sc->delta = s;
+        sc->beta = 0.0;
+    } else if (what == kFinAlpha) {
+        sc->pq = s;
+        if (!(s > 0.0) || !isfinite(s)) {
+            sc->fail = 1;
+            sc->done = 1;
+        }
+        sc->alpha = sc->delta / s;
+    } else if (what == kFinRR) {
+        sc->rr = s;
+        sc->iter += 1;
+        if (!isfinite(s)) {
+            sc->fail = 1;
+            sc->done = 1;
+        }
+        if (s <= sc->tol2 || sc->iter >= sc->maxit) sc->done = 1;
+        mirror_store(mirror + sub, sc->iter, sc->done, sc->fail);
+        return;
+    } else {
+        if (!isfinite(s)) {
+            sc->fail = 1;
+            sc->done = 1;
+        }
+        sc->beta = s / sc->delta;
+        sc->delta = s;
+    }
+    if (sc->done != was_done) mirror_store(mirror + sub, sc->iter, sc->done, sc->fail);
 }
 
 // full[free_dof[i]] = cond[i] (full zero-filled first) / cond[i] = full[free_dof[i]]
@@ -1771,11 +1632,6 @@ void build_gs(GsFine& G, const LevelDev& L, int nsub, const std::vector<int64_t>
     G.offl.upload(offl);
     G.offu.upload(offu);
     G.cb.upload(cb);
-    {
-        std::vector<int32_t> need0(nsub, 0);
-        for (int64_t i = 0; i < G.count[0]; ++i) need0[csub[list[G.first[0] + i]]]++;
-        G.need0.upload(need0);
-    }
     if (c16) G.col16.upload(gcol16);
     else G.col.upload(gcol);
     if (vt == kValH16) G.val16.upload(v16);
@@ -2288,12 +2144,6 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
     DDPCA_HIP(hipHostMalloc(reinterpret_cast<void**>(&sc_host), nsub * sizeof(PcgScal)));
     std::memset(sc_host, 0, nsub * sizeof(PcgScal));
     mirror.alloc(nsub);
-    fin_tick.alloc(3 * nsub);
-    fin_tick.zero(stream);
-    {
-        const char* e = std::getenv("DDPCA_FUSED_FIN");
-        fused_fin_ = !(e && e[0] == '0');
-    }
     DDPCA_HIP(hipEventCreate(&ev_k0));
     DDPCA_HIP(hipEventCreate(&ev_k1));
     // smoother coefficients from the spectrum of M K on each smoothed level and subdomain
@@ -2428,20 +2278,6 @@ void launch_sell(int vt, const SellArgs& a, hipStream_t s) {
             } else if (vt == kValH16) hipLaunchKernelGGL((k_sell_split<MODE, BJ, uint16_t, int32_t>), gs, dim3(kBlock), 0, s, a);
             else if (vt == kVal32) hipLaunchKernelGGL((k_sell_split<MODE, BJ, float, int32_t>), gs, dim3(kBlock), 0, s, a);
             else hipLaunchKernelGGL((k_sell_split<MODE, BJ, double, int32_t>), gs, dim3(kBlock), 0, s, a);
-            return;
-        }
-    }
-    // the dot product's scalar update fused into the launch (fused_finish): the PCG SpMV (alpha) and
-    // the V-cycle's last fine-level Jacobi sweep (beta)
-    if constexpr (DOT && (MODE == kPcg || MODE == kJac)) {
-        if (a.fin.what >= 0 && !a.tab) {
-            if (a.col16) {
-                if (vt == kValH16) hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, uint16_t, V, false, I16, true>), dim3(grid), dim3(kBlock), 0, s, a, a.tab);
-                else if (vt == kVal32) hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, float, V, false, I16, true>), dim3(grid), dim3(kBlock), 0, s, a, a.tab);
-                else hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, double, V, false, I16, true>), dim3(grid), dim3(kBlock), 0, s, a, a.tab);
-            } else if (vt == kValH16) hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, uint16_t, V, false, int32_t, true>), dim3(grid), dim3(kBlock), 0, s, a, a.tab);
-            else if (vt == kVal32) hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, float, V, false, int32_t, true>), dim3(grid), dim3(kBlock), 0, s, a, a.tab);
-            else hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, double, V, false, int32_t, true>), dim3(grid), dim3(kBlock), 0, s, a, a.tab);
             return;
         }
     }
@@ -2620,21 +2456,12 @@ namespace {
 // one k_gs launch: phase ph over colour k's chunks (k < 0: every chunk)
 template <int PH, bool DOT, typename T>
 void launch_gs_t(const GsArgs& a, bool c16, hipStream_t st) {  // c16: 16-bit column offsets, else int32 columns
-    if constexpr (PH == 2 && DOT) {
-        if (a.fin.what >= 0) {  // the backward sweep's last launch with the fused beta update
-            const dim3 g((unsigned)ceil_div(a.n, (int64_t)(kBlock / kWave)));
-            if (c16) hipLaunchKernelGGL((k_gs<PH, DOT, T, int16_t, true>), g, dim3(kBlock), 0, st, a);
-            else hipLaunchKernelGGL((k_gs<PH, DOT, T, int32_t, true>), g, dim3(kBlock), 0, st, a);
-            return;
-        }
-    }
     if (c16) hipLaunchKernelGGL((k_gs<PH, DOT, T, int16_t>), dim3((unsigned)a.n), dim3(kWave), 0, st, a);
     else hipLaunchKernelGGL((k_gs<PH, DOT, T, int32_t>), dim3((unsigned)a.n), dim3(kWave), 0, st, a);
 }
 
 template <int PH, bool DOT>
-void launch_gs(const MgpisDevice& D, int k, double* x, const double* b, double* r, const PcgScal* scp, double* partial,
-               const FinFuse* fin = nullptr) {
+void launch_gs(const MgpisDevice& D, int k, double* x, const double* b, double* r, const PcgScal* scp, double* partial) {
     const GsFine& G = D.gs;
     const LevelDev& F = D.lev.back();
     GsArgs a{};
@@ -2657,7 +2484,6 @@ void launch_gs(const MgpisDevice& D, int k, double* x, const double* b, double* 
     // the rows' fp32 inverses in chunk order (coalesced: read by row at stride 2 nodes they pulled
     // whole lines for half the data, +1.1 %, profiles/r03o); the fp64 copy reads minv by row
     a.minvc = G.minvc.p;
-    if (fin) a.fin = *fin;
     const bool c16 = G.col16.p != nullptr;
     if (G.val16.p) {
         a.val = G.val16.p;
@@ -2712,8 +2538,6 @@ void MgpisDevice::vcycle(const double* rin, double* zout, bool dot) {
             a.xo = oth[l];
             a.coef = coef(l, s);
             const bool d = last_dot && s == first + count - 1;
-            if (d && vc_fin_) a.fin = FinFuse{fin_tick.p + 2 * nsub, nullptr, fin_cb.p, partial.p, const_cast<PcgScal*>(scp),
-                                              mirror.dev, (int)kFinBeta};
             if (cheb) {
                 a.p = lev[l].d.p;
                 if (d) launch_sell<kCheb, true, true>(f32, a, stream);
@@ -2812,11 +2636,8 @@ void MgpisDevice::vcycle(const double* rin, double* zout, bool dot) {
         rot_prolong(l, cur[l - 1], cur[l], scp);
         if (gsf && l == Lf) {
             // backward sweep; the dot product's partials per colour chunk (vc_cb)
-            // (the last launch, colour 0, with the fused beta update when enqueue_iteration asks)
-            const FinFuse fb{fin_tick.p + 2 * nsub, gs.need0.p, gs.cb.p, gs.partial.p, const_cast<PcgScal*>(scp), mirror.dev,
-                             (int)kFinBeta};
             for (int k = gs.ncol - 1; k >= 0; --k) {
-                if (dot) launch_gs<2, true>(*this, k, zout, rin, nullptr, scp, gs.partial.p, k == 0 && vc_fin_ ? &fb : nullptr);
+                if (dot) launch_gs<2, true>(*this, k, zout, rin, nullptr, scp, gs.partial.p);
                 else launch_gs<2, false>(*this, k, zout, rin, nullptr, scp, nullptr);
             }
             continue;
@@ -2964,44 +2785,16 @@ void MgpisDevice::enqueue_iteration(int prec, bool timed) {
     a.sc = scp;
     a.partial = partial.p;
     const int nblk = ceil_div(L.nn, kBlock);
-    // the three scalar updates fused into the kernels that leave their partials (fused_finish:
-    // alpha in the SpMV, ||r||^2 and the stop test in k_axpy, beta in the V-cycle's last fine-level
-    // launch), bit-identical to the k_fin launches they replace; DDPCA_FUSED_FIN=0 keeps k_fin
-    const bool ff = fused_fin_ && !L.tbl;  // (the table-mode SpMV keeps k_fin)
-    const bool fb = ff && prec == 1 && vcycle_fuses_dot();
-    if (ff) a.fin = FinFuse{fin_tick.p, nullptr, fin_cb.p, partial.p, scp, mirror.dev, (int)kFinAlpha};
     if (timed) DDPCA_HIP(hipEventRecord(ev_k0, stream));
     launch_sell<kPcg, false, true>(kVal64, a, stream);
     if (timed) DDPCA_HIP(hipEventRecord(ev_k1, stream));
-    if (ff) {
-        const FinFuse fr{fin_tick.p + nsub, nullptr, fin_cb.p, partial.p, scp, mirror.dev, (int)kFinRR};
-        hipLaunchKernelGGL(k_axpy<true>, dim3(nblk), dim3(kBlock), 0, stream, xs.p, rs.p, ps.p, qs.p, scp, partial.p, L.nn,
-                           L.csub.p, fr);
-    } else {
-        launch_fin(stream, (int)kFinAlpha, partial.p, nullptr, fin_cb.p, scp, mirror.dev);
-        hipLaunchKernelGGL(k_axpy<false>, dim3(nblk), dim3(kBlock), 0, stream, xs.p, rs.p, ps.p, qs.p, scp, partial.p, L.nn,
-                           L.csub.p, FinFuse{});
-        launch_fin(stream, (int)kFinRR, partial.p, nullptr, fin_cb.p, scp, mirror.dev);
-    }
-    if (prec == 1) {
-        vc_fin_ = fb;
-        vcycle(rs.p, zs.p, true);
-        vc_fin_ = false;
-    } else {
-        hipLaunchKernelGGL(k_diag, dim3(nblk), dim3(kBlock), 0, stream, rs.p, L.dinv.p, zs.p, partial.p, L.nn, L.csub.p, scp);
-    }
-    if (!fb)
-        launch_fin(stream, (int)kFinBeta, prec == 1 ? vc_partial() : partial.p, nullptr, prec == 1 ? vc_cb() : fin_cb.p, scp,
-                   mirror.dev);
-}
-
-// the V-cycle's dot product comes from a fine-level launch that can carry the fused beta update:
-// the multicolour backward sweep, or a (block-)Jacobi sweep (not Chebyshev, not a one-level cycle)
-bool MgpisDevice::vcycle_fuses_dot() const {
-    const int Lf = (int)lev.size() - 1;
-    if (no_coarse || Lf == clev) return false;
-    if (gs_fine()) return gs.need0.p != nullptr;
-    return opt.smoother != 2 && opt.nu >= 1 && !lev[Lf].tbl;
+    launch_fin(stream, (int)kFinAlpha, partial.p, nullptr, fin_cb.p, scp, mirror.dev);
+    hipLaunchKernelGGL(k_axpy, dim3(nblk), dim3(kBlock), 0, stream, xs.p, rs.p, ps.p, qs.p, scp, partial.p, L.nn, L.csub.p);
+    launch_fin(stream, (int)kFinRR, partial.p, nullptr, fin_cb.p, scp, mirror.dev);
+    if (prec == 1) vcycle(rs.p, zs.p, true);
+    else hipLaunchKernelGGL(k_diag, dim3(nblk), dim3(kBlock), 0, stream, rs.p, L.dinv.p, zs.p, partial.p, L.nn, L.csub.p, scp);
+    launch_fin(stream, (int)kFinBeta, prec == 1 ? vc_partial() : partial.p, nullptr, prec == 1 ? vc_cb() : fin_cb.p, scp,
+               mirror.dev);
 }
 
 // graph_[prec]: iters_per_graph PCG iterations captured once and replayed; graph1_[prec]: one.

@@ -154,7 +154,6 @@ struct GsFine {
     DevBuf<float> minvc;                 // the rows' fp32 3x3 inverses in chunk order, [chunk][ij][lane]
                                          // (coalesced; the natural array at stride 2 nodes wastes half of every line)
     DevBuf<int64_t> cb;                  // per member: first colour chunk (nsub + 1), the dot partials
-    DevBuf<int32_t> need0;               // per member: its colour-0 chunks (the fused beta update's arrivals)
     DevBuf<double> partial;              // per colour chunk: the backward sweep's dot partials (their own
                                          // buffer: a split batch's other half writes the Krylov partials meanwhile)
     std::vector<int64_t> nnzb_sub;       // per member: stored off-diagonal blocks (byte model)
@@ -210,12 +209,6 @@ public:
     PcgScal* sc_host = nullptr;      // pinned, filled by pcg_finish()
     MirrorBuf mirror;                // per-subdomain stop state, host-mapped
     DevBuf<int64_t> fin_cb;          // per-subdomain first chunk of the fine level (nsub + 1)
-    // the PCG scalar updates fused into the kernels that leave their partials (fused_finish):
-    // per update site and subdomain the arrivals of the current launch (zero between launches)
-    DevBuf<unsigned int> fin_tick;   // 3 x nsub: alpha, rr, beta
-    bool fused_fin_ = true;          // DDPCA_FUSED_FIN=0: the separate k_fin launches
-    bool vc_fin_ = false;            // set by enqueue_iteration around its vcycle(dot)
-    bool vcycle_fuses_dot() const;
 
     int64_t fine_dof_offset(int s) const { return 3 * lev.back().noff[s]; }
     int64_t fine_nodes(int s) const { return lev.back().nloc[s]; }
