@@ -1913,7 +1913,11 @@ void build_coarse(ddpca_mcontact& H, Problem& P) {
     // LATIN: DOUBLE_M (MCONTACT.h:1236) with the host MULTISCALE's coarse contact nodes, one rank
     const bool mg_ok = !cs.latin || (!cs.rank_local && !cs.coarNode.empty());
     const bool by_rows = n >= (mg_env ? std::atoll(mg_env) : 120000);
-    C.mg = (by_rows || C.dense_bytes > dense_max) && mg_ok;
+    // the budget alone switches LATIN's DOUBLE_M on one rank only: its hierarchy may not be
+    // buildable (below), and the fallback to the dense solve must be the same on every rank (the
+    // dense matrix is summed by a collective), which a rank without owned rows cannot decide
+    const bool by_budget = C.dense_bytes > dense_max && (!cs.latin || H.nranks == 1 || n > 46000);
+    C.mg = (by_rows || by_budget) && mg_ok;
     C.latin = cs.latin;
     if (C.mg && H.mg && C.nown) {
         try {

@@ -17,7 +17,7 @@
 // curved contacts exchanged, the LATIN coarse space's operator rows filled by rank 0 and summed,
 // the MONITOR all-reduce -- compared with the single-rank device run (iterations equal, resuMoni
 // 1e-8, displacements 1e-8, contact tractions 1e-7 of the largest).
-//   ref_cylinder copyNumb locaLeve globInho bandWidt [native|ref] [owners]
+//   ref_cylinder copyNumb locaLeve globInho bandWidt [native|ref] [owners] [noref]
 #include <unistd.h>
 
 #include <cstdio>
@@ -60,7 +60,11 @@ int main(int argc, char** argv) {
     c.locaLeve = locaLeve;
     c.globInho = globInho;
     c.bandWidt = bandWidt;
-    c.SOLVE(1);  // MESH, contact search, ESTABLISH and the reference's CONTACT_ANALYSIS
+    // noref (after the owners): the two-rank comparison alone -- the reference builds the problem
+    // (MESH, contact search, ESTABLISH) but does not run its CONTACT_ANALYSIS, whose answers
+    // test_cylinder_known_answer checks
+    const bool noref = argc > 7 && std::string(argv[7]) == "noref";
+    c.SOLVE(noref ? 0 : 1);  // MESH, contact search, ESTABLISH (and the reference's CONTACT_ANALYSIS)
     std::fflush(stdout);
     dup2(saved, 1);
     long nhang = 0, nnodes = 0;
@@ -107,11 +111,11 @@ int main(int argc, char** argv) {
     std::vector<int32_t> owner(c.multGrid.size(), 0);
     mcontact_t h = nullptr;
     ddpca_bind::check(mcontact_gpu_create(p, 0, 0, 1, owner.data(), nullptr, &h));
-    const int64_t n_gpu = mcontact_gpu_iterate(h, 3000, 1);
+    const int64_t n_gpu = noref ? 0 : mcontact_gpu_iterate(h, 3000, 1);
     ddpca_bind::check((int)std::min<int64_t>(n_gpu, 0));
     // displacements: position order (hanging level last) -> node-id order
     double du = 0.0;
-    for (size_t tv = 0; tv < c.multGrid.size(); ++tv) {
+    for (size_t tv = 0; tv < c.multGrid.size() && !noref; ++tv) {
         const MULTIGRID& g = c.multGrid[tv];
         Eigen::VectorXd u_pos(g.earlTran.cols());
         const int64_t n = mcontact_gpu_get(h, "resuDisp", tv, u_pos.data(), u_pos.size());
@@ -124,7 +128,7 @@ int main(int argc, char** argv) {
         du = std::max(du, (u - c.resuDisp[tv]).norm() / c.resuDisp[tv].norm());
     }
     // resuMoni rows (the reference's file, scientific 20 digits) vs the device's monitor rows
-    const auto ref_moni = read_rows(DIRECTORY("resuMoni.txt"));
+    const auto ref_moni = noref ? std::vector<std::vector<double>>() : read_rows(DIRECTORY("resuMoni.txt"));
     const int64_t ncol = 2 * (int64_t)c.multGrid.size() + 8 * (int64_t)c.searCont.size() + 2;
     const int64_t nrows = mcontact_gpu_monitor(h, nullptr, 0);
     std::vector<double> moni(nrows * ncol);
@@ -140,7 +144,7 @@ int main(int argc, char** argv) {
     std::string itf = "[";
     std::vector<double> gam(1 << 22);
     double dp_all = 0.0;
-    for (size_t ts = 0; ts < c.searCont.size(); ++ts) {
+    for (size_t ts = 0; ts < c.searCont.size() && !noref; ++ts) {
         const int64_t n = mcontact_gpu_get(h, "inpoGamm", ts, gam.data(), (int64_t)gam.size());
         ddpca_bind::check((int)std::min<int64_t>(n, 0));
         const auto ref = read_rows(DIRECTORY("resuCont_" + std::to_string(ts) + ".txt"));

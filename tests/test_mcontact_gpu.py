@@ -431,7 +431,8 @@ def test_cylinder_two_ranks_in_one_process(gpu, tmp_path, owners):
     level pinned: its automatic choice depends on the subdomains per rank, which moved the rows by
     1.1e-7 in r03c): the same iteration count on both ranks, resuMoni rows within SURVEY §8 c4's
     1e-7 (relative, floor 1e-12 of the column), displacements 1e-8, contact tractions 1e-7 of the
-    largest -- and the default single-rank run the reference (as test_cylinder_known_answer)."""
+    largest.  The reference builds the problem but skips its own CONTACT_ANALYSIS ("noref": the
+    single-rank answers against the reference are test_cylinder_known_answer's)."""
     import json
     import os
     import subprocess
@@ -439,15 +440,13 @@ def test_cylinder_two_ranks_in_one_process(gpu, tmp_path, owners):
     exe = Path(__file__).resolve().parents[1] / "oracle" / "_ref" / "ref_cylinder"
     if not exe.exists():
         pytest.skip("oracle/_ref/ref_cylinder is built only where the reference is (travels with the snapshot)")
-    out = subprocess.run([str(exe), "1", "4", "2", "2e-4", "ref", owners], capture_output=True, text=True, timeout=240,
-                         env=dict(os.environ), cwd=tmp_path)
+    out = subprocess.run([str(exe), "1", "4", "2", "2e-4", "ref", owners, "noref"], capture_output=True, text=True,
+                         timeout=240, env=dict(os.environ), cwd=tmp_path)
     assert out.returncode == 0, out.stderr[-2000:]
     res = json.loads(out.stderr.strip().splitlines()[-1])
-    print(res["ranks2"], res["iters_gpu"], res["iters_ref"])
+    print(res["ranks2"])
     r2 = res["ranks2"]
     assert r2["cross_interfaces"] == (1 if owners == "0011" else 3), r2
-    assert r2["iters"] == [r2["iters_1rank"], r2["iters_1rank"]], r2
-    assert abs(r2["iters_1rank"] - res["iters_gpu"]) <= 1, (r2, res["iters_gpu"])
+    assert r2["iters"] == [r2["iters_1rank"], r2["iters_1rank"]] and r2["iters_1rank"] > 1, r2
     assert r2["moni_rel"] <= 1e-7 and r2["resuDisp_rel"] <= 1e-8 and r2["gamma_rel"] <= 1e-7, r2
-    assert abs(res["iters_gpu"] - res["iters_ref"]) <= 1 and res["resuDisp_rel"] <= 1e-6, res
 
