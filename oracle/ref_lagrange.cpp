@@ -9,6 +9,13 @@
 // count, the final active set and multipliers (the reference's resuLagr_<ts>.txt), and the
 // displacements (reference resuDisp vs OUTP_SUB1 of the device's condensed solution).  One JSON
 // line on stderr.
+// Record / replay of the reference's answers (so the GPU box need not re-run the reference's
+// single-threaded Newton loop each time): DDPCA_REF_RECORD=<dir> writes the reference's progress
+// log, its resuLagr_<ts>.txt and resuDisp (raw fp64 per subdomain) there after its LAGRANGE;
+// DDPCA_REF_REPLAY=<dir> (when <dir>/log.txt exists) builds the same problem -- MESH, the contact
+// searches, then exactly LAGRANGE's own setup (TRANSFER, STIF_MATR, CONSTRAINT(precType == 1 ? 1
+// : -1), MCONTACT.h:2847-2860) -- and compares against the recorded answers instead
+// (tests/golden/lagrange/*, made by tests/golden/make_lagrange_golden.sh).
 //   ref_lagrange globLeve precType fric tangential_load
 #include <execinfo.h>
 #include <unistd.h>
@@ -74,9 +81,23 @@ int main(int argc, char** argv) {
     if (cyl) cy = std::make_unique<CYLINDER_1>();  // creates ./Cylinder/
     else blk = std::make_unique<BLOCK>();           // creates ./Block/
     MCONTACT& b = cyl ? static_cast<MCONTACT&>(*cy) : static_cast<MCONTACT&>(*blk);
-    const std::string log = std::string(cyl ? "Cylinder" : "Block") + "/ref_lagrange_stdout.txt";
+    const std::string outdir = cyl ? "Cylinder" : "Block";
+    std::string log = outdir + "/ref_lagrange_stdout.txt";
+    const char* rec = std::getenv("DDPCA_REF_RECORD");
+    const char* rep = std::getenv("DDPCA_REF_REPLAY");
+    const bool replay = rep && std::ifstream(std::string(rep) + "/log.txt").good();
     const int saved = dup(1);
-    if (!std::freopen(log.c_str(), "w", stdout)) return 2;  // the reference's progress output, parsed below
+    if (!std::freopen(replay ? "/dev/null" : log.c_str(), "w", stdout)) return 2;  // the reference's progress output, parsed below
+    // replay: LAGRANGE's own setup instead of the reference's Newton loop (MCONTACT.h:2847-2860)
+    auto lagrange_setup = [&] {
+        for (auto& g : b.multGrid) g.leveNode.clear();  // (TRANSFER appends to leveNode)
+#pragma omp parallel for
+        for (long tv = 0; tv < (long)b.multGrid.size(); ++tv) {
+            b.multGrid[tv].TRANSFER();
+            b.multGrid[tv].STIF_MATR();
+            b.multGrid[tv].CONSTRAINT(prec == 1 ? 1 : -1);
+        }
+    };
     if (cyl) {
         // CYLINDER_1 (locally refined: hanging non-mortar nodes are dropped, MCONTACT.h:2870-2893),
         // reduced locaLeve as in ref_cylinder; frictionless as the example sets it
@@ -84,7 +105,12 @@ int main(int argc, char** argv) {
         cy->locaLeve = 3 + gl;
         cy->globInho = 2;
         cy->bandWidt = 2.0e-4;
-        cy->SOLVE(1 + prec);
+        if (replay) {
+            cy->SOLVE(0);  // MESH, contact searches, ESTABLISH
+            lagrange_setup();
+        } else {
+            cy->SOLVE(1 + prec);
+        }
     } else {
         blk->domaNumb = {1, 1, 1};
         blk->globLeve = gl;
@@ -92,7 +118,7 @@ int main(int argc, char** argv) {
         blk->doleMcsc.assign(3 * 1 + 6, 1);
         blk->loadPres << tang, 0.0, -1.0E7;
         blk->ESTA_SURF();
-        if (fric == 0.0 && tang == 0.0) {
+        if (fric == 0.0 && tang == 0.0 && !replay) {
             blk->SOLVE(1 + prec);  // MESH, contact searches, the reference's LAGRANGE(prec)
         } else {
             blk->SOLVE(0);  // MESH, contact searches, ESTABLISH
@@ -100,12 +126,41 @@ int main(int argc, char** argv) {
                 if (b.fricCoef[ts] == 0.0) b.fricCoef[ts] = fric;  // the contact (not glued) interfaces
             // LAGRANGE re-runs TRANSFER, which appends to leveNode (MULTIGRID.h:884-900): start it
             // from the state MESH left, as SOLVE(2) does
-            for (auto& g : b.multGrid) g.leveNode.clear();
-            b.LAGRANGE(prec);
+            if (replay) {
+                lagrange_setup();
+            } else {
+                for (auto& g : b.multGrid) g.leveNode.clear();
+                b.LAGRANGE(prec);
+            }
         }
     }
     std::fflush(stdout);
     dup2(saved, 1);
+    auto lagr_file = [&](int64_t ts) {
+        return replay ? std::string(rep) + "/resuLagr_" + std::to_string(ts) + ".txt"
+                      : DIRECTORY("resuLagr_" + std::to_string(ts) + ".txt");
+    };
+    if (replay) {
+        log = std::string(rep) + "/log.txt";
+        b.resuDisp.resize(b.multGrid.size());
+        for (size_t tv = 0; tv < b.multGrid.size(); ++tv) {
+            std::ifstream f(std::string(rep) + "/resuDisp_" + std::to_string(tv) + ".bin", std::ios::binary);
+            f.seekg(0, std::ios::end);
+            const std::streamoff n = f.tellg() / (std::streamoff)sizeof(double);
+            f.seekg(0);
+            b.resuDisp[tv].resize(n);
+            f.read(reinterpret_cast<char*>(b.resuDisp[tv].data()), n * sizeof(double));
+        }
+    } else if (rec) {
+        const std::string d(rec);
+        std::ofstream(d + "/log.txt") << std::ifstream(log).rdbuf();
+        for (size_t ts = 0; ts < b.searCont.size(); ++ts)
+            std::ofstream(d + "/resuLagr_" + std::to_string(ts) + ".txt") << std::ifstream(lagr_file((int64_t)ts)).rdbuf();
+        for (size_t tv = 0; tv < b.resuDisp.size(); ++tv)
+            std::ofstream(d + "/resuDisp_" + std::to_string(tv) + ".bin", std::ios::binary)
+                .write(reinterpret_cast<const char*>(b.resuDisp[tv].data()), b.resuDisp[tv].size() * sizeof(double));
+        std::fprintf(stderr, "recorded the reference's answers in %s\n", rec);
+    }
     // the reference's Newton count and BiCGSTAB iterations from its progress output
     long tc_ref = -1;
     std::vector<long> its_ref;
@@ -206,7 +261,7 @@ int main(int argc, char** argv) {
     bool nodes_equal = true, stat_equal = true;
     double dl = 0.0;
     for (int64_t ts = 0; ts < nint; ++ts) {
-        const RefLagr r = read_lagr(DIRECTORY("resuLagr_" + std::to_string(ts) + ".txt"));
+        const RefLagr r = read_lagr(lagr_file(ts));
         const int64_t m = ddpca_lagrange_get(h, "node", ts, nullptr, 0);
         std::vector<double> nd(m), st(m), lam(3 * m);
         ddpca_lagrange_get(h, "node", ts, nd.data(), m);
@@ -252,8 +307,8 @@ int main(int argc, char** argv) {
     std::fprintf(stderr,
                  "{\"newton\": %ld, \"newton_ref\": %ld, \"bicgstab_iters\": %s, \"bicgstab_iters_ref\": %s, "
                  "\"bicgstab_relres\": %s, \"bicgstab_breakdown\": %s, \"resuDisp_rel\": %.3g, "
-                 "\"lambda_rel\": %.3g, \"nodes_equal\": %s, \"status_equal\": %s, \"interfaces\": %s}\n",
+                 "\"lambda_rel\": %.3g, \"nodes_equal\": %s, \"status_equal\": %s, \"replayed\": %s, \"interfaces\": %s}\n",
                  (long)tc, tc_ref, sit.c_str(), rit.c_str(), srel.c_str(), sbrk.c_str(), du, dl, nodes_equal ? "true" : "false", stat_equal ? "true" : "false",
-                 itf.c_str());
+                 replay ? "true" : "false", itf.c_str());
     return 0;
 }

@@ -25,7 +25,7 @@ EXE = Path(__file__).resolve().parents[1] / "oracle" / "_ref" / "ref_lagrange"
 @pytest.mark.parametrize("example,prec,fric,tang", [("block", "1", "0", "0"), ("block", "1", "0.2", "2e6"),
                                                     ("block", "2", "0", "0"), ("cylinder", "1", "0", "0")],
                          ids=["mgpis-frictionless", "mgpis-coulomb-slip", "diagonal-frictionless", "cylinder-hanging"])
-def test_lagrange_matches_reference(gpu, tmp_path, example, prec, fric, tang):
+def test_lagrange_matches_reference(gpu, tmp_path, request, example, prec, fric, tang):
     """block: BLOCK as above.  cylinder: the reference's CYLINDER_1 (copyNumb 1, locaLeve 4: four
     cylinders, locally refined contact bands, 35 % hanging nodes -- integration points whose
     non-mortar face holds a hanging node are dropped, MCONTACT.h:2870-2893; curved contact search);
@@ -33,11 +33,17 @@ def test_lagrange_matches_reference(gpu, tmp_path, example, prec, fric, tang):
     if not EXE.exists():
         pytest.skip("oracle/_ref/ref_lagrange is built where the reference is (travels with the snapshot)")
     args = ([example] if example != "block" else []) + ["1", prec, fric, tang]
-    out = subprocess.run([str(EXE), *args], capture_output=True, text=True, timeout=840, cwd=tmp_path,
-                         env=dict(os.environ))
+    # the reference's own answers recorded by tests/golden/make_lagrange_golden.sh (the harness then
+    # builds the same problem with LAGRANGE's own setup and skips the reference's Newton loop)
+    env = dict(os.environ)
+    golden = Path(__file__).resolve().parent / "golden" / "lagrange" / request.node.callspec.id
+    if (golden / "log.txt").exists():
+        env["DDPCA_REF_REPLAY"] = str(golden)
+    out = subprocess.run([str(EXE), *args], capture_output=True, text=True, timeout=840, cwd=tmp_path, env=env)
     assert out.returncode == 0, out.stderr[-2000:]
     res = json.loads(out.stderr.strip().splitlines()[-1])
     print(res)
+    assert res["replayed"] == ("DDPCA_REF_REPLAY" in env), res
     assert res["newton"] == res["newton_ref"], res
     assert res["nodes_equal"] and res["status_equal"], res
     assert res["lambda_rel"] <= 1e-6, res
