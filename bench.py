@@ -316,7 +316,7 @@ def run_general_child(a) -> dict:
     t0 = time.perf_counter()
     log(0, "general-mesh line (child process) ...")
     try:
-        r = subprocess.run(cmd, capture_output=True, text=True, timeout=1500, env=env)
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env)
     except subprocess.TimeoutExpired:
         return {"error": "timeout"}
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
