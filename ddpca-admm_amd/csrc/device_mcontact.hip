@@ -343,6 +343,51 @@ __global__ __launch_bounds__(256) void k_mcg_spmv(EllArgs e, const PcgScal* sc, 
     if (lane == 0) partial[ostride * c] = d;
 }
 
+// k_mcg_spmv over a batch whose second half repeats the first half's matrices R rows further on
+// (the fused w|v interface update: both sides' v systems carry the w systems' inteMass): a wave
+// takes chunk c and its twin c + nch2, reads the stored entries once and gathers z at j and j + R.
+// Each row's sum runs over the same slots in the same order as in k_mcg_spmv, so q, p and the
+// partials are bit for bit those of the unpaired launch; the matrix stream is halved.
+__global__ __launch_bounds__(256) void k_mcg_spmv2(EllArgs e, const PcgScal* sc, const double* z, double* q, double* p,
+                                                   double* partial, int ostride, int64_t R, int64_t nch2) {
+    const int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (c >= nch2) return;
+    const int sw = e.csys[c], sv = e.csys[c + nch2];
+    const bool dw = sc[sw].done != 0, dv = sc[sv].done != 0;
+    if (dw && dv) return;
+    const int lane = threadIdx.x & 63;
+    const int64_t row = c * 64 + lane;
+    const int ns = e.slots[c];
+    const int32_t* cp = e.col + e.off[c] * 64 + lane;
+    const double* vp = e.val + e.off[c] * 64 + lane;
+    const double* zv = z + R;
+    double s0 = 0.0, s1 = 0.0;
+#pragma unroll 4
+    for (int k = 0; k < ns; ++k) {
+        const double v = vp[(int64_t)k * 64];
+        const int32_t j = cp[(int64_t)k * 64];
+        s0 += v * z[j];
+        s1 += v * zv[j];
+    }
+    if (!dw) {
+        const double be = sc[sw].beta;
+        const double qi = s0 + be * q[row], pi = z[row] + be * p[row];
+        q[row] = qi;
+        p[row] = pi;
+        const double d = wsum(pi * qi);
+        if (lane == 0) partial[ostride * c] = d;
+    }
+    if (!dv) {
+        const double be = sc[sv].beta;
+        const int64_t rv = row + R;
+        const double qi = s1 + be * q[rv], pi = z[rv] + be * p[rv];
+        q[rv] = qi;
+        p[rv] = pi;
+        const double d = wsum(pi * qi);
+        if (lane == 0) partial[ostride * (c + nch2)] = d;
+    }
+}
+
 // k_mcg_axpy with alpha computed in place of a k_mcg_fin(kMcgAlpha) launch: every wave sums its
 // system's p.q chunk partials (ppq, written by k_mcg_spmv with stride 1 -- not the (r.r, r.z)
 // pairs this kernel writes) in one fixed order, so all waves hold the same alpha; the system's
@@ -765,6 +810,10 @@ public:
                 }
             }
         }
+        // paired batch: systems i and i + nsys/2 share one matrix, R = nrow/2 rows apart
+        paired_ = nsys >= 2 && nsys % 2 == 0 && nrow % 128 == 0;
+        for (int s = 0; paired_ && s < nsys / 2; ++s)
+            paired_ = A[s] == A[s + nsys / 2] && roff[s + nsys / 2] == roff[s] + nrow / 2;
         slots.upload(sl);
         csys.upload(cs);
         off.upload(of);
@@ -778,11 +827,13 @@ public:
         // and q, p written; k_mcg_axpy: x, r read + written, z written, p, q, D^-1 read (112 B per row)
         init_bytes_.assign(nsys, 0.0);
         it_bytes_.assign(nsys, 0.0);
+        mat_bytes_.assign(nsys, 0.0);
         for (int s = 0; s < nsys; ++s) {
             const double rows = (double)A[s]->nrow, ent = (double)A[s]->nnz();
             init_bytes_[s] = 56.0 * rows;
             // (+ the p.q and (r.r, r.z) chunk partials written once and read once: 24 B each way per chunk)
-            it_bytes_[s] = 12.0 * ent + 8.0 * rows + 40.0 * rows + 64.0 * rows + 48.0 * (double)(pad64(A[s]->nrow) / 64);
+            it_bytes_[s] = 8.0 * rows + 40.0 * rows + 64.0 * rows + 48.0 * (double)(pad64(A[s]->nrow) / 64);
+            mat_bytes_[s] = 12.0 * ent;  // (k_mcg_spmv2: once per pair, for the pair's longer solve)
         }
         for (auto* v : {&b, &x, &r, &z, &p, &q}) {
             v->alloc(std::max<int64_t>(nrow, 2));
@@ -849,18 +900,18 @@ public:
             DDPCA_HIP(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
             DDPCA_HIP(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
             sc_half_.alloc(2 * nsys);
-            std::vector<int64_t> rows(nsys);
-            std::vector<int> ord(nsys);
-            for (int i = 0; i < nsys; ++i) {
-                rows[i] = cb_host_[i + 1] - cb_host_[i];
-                ord[i] = i;
-            }
+            // a paired batch splits by pairs, so that a pair's shared matrix is read by one half
+            const int nu = paired_ ? nsys / 2 : nsys;
+            std::vector<int64_t> rows(nu, 0);
+            std::vector<int> ord(nu);
+            for (int i = 0; i < nsys; ++i) rows[i % nu] += cb_host_[i + 1] - cb_host_[i];
+            for (int i = 0; i < nu; ++i) ord[i] = i;
             std::stable_sort(ord.begin(), ord.end(), [&](int a, int c) { return rows[a] > rows[c]; });
             half_host_.assign(nsys, 0);
             int64_t w[2] = {0, 0};
             for (int i : ord) {
                 const int h = w[1] < w[0] ? 1 : 0;
-                half_host_[i] = h;
+                for (int j = i; j < nsys; j += nu) half_host_[j] = h;
                 w[h] += rows[i];
             }
             half_.upload(half_host_);
@@ -894,7 +945,11 @@ public:
             }
             expect_[i] = mirror.host[i].iter;  // paces the next solve's tail
             last_iters = std::max<int64_t>(last_iters, mirror.host[i].iter);
-            if (solved_) alg_bytes += init_bytes_[i] + (double)mirror.host[i].iter * it_bytes_[i];
+            if (solved_) {
+                int64_t mit = mirror.host[i].iter;
+                if (pair_used_) mit = i < nsys / 2 ? std::max(mit, mirror.host[i + nsys / 2].iter) : 0;
+                alg_bytes += init_bytes_[i] + (double)mirror.host[i].iter * it_bytes_[i] + (double)mit * mat_bytes_[i];
+            }
         }
         solved_ = false;
     }
@@ -934,8 +989,9 @@ private:
     DevBuf<int32_t> half_;
     std::vector<int> half_host_;
     std::vector<int64_t> cb_host_;
-    std::vector<double> init_bytes_, it_bytes_;
+    std::vector<double> init_bytes_, it_bytes_, mat_bytes_;
     bool solved_ = false;
+    bool paired_ = false, pair_used_ = false;
     void capture(hipStream_t s) {
         if (split_) {
             capture_one(s, sc_half_.p, &graph_h_[0], k);
@@ -955,14 +1011,25 @@ private:
         hipGraph_t g;
         DDPCA_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
         const bool fa = fuse_alpha();
+        // DDPCA_MCG_PAIR=0: the unpaired k_mcg_spmv on a paired batch (bit-identical, A/B and tests)
+        const char* ep = std::getenv("DDPCA_MCG_PAIR");
+        const bool pair = paired_ && !(ep && std::atoi(ep) == 0);
+        pair_used_ = pair;
         double* ppq = partial.p + 2 * nch;  // p.q per chunk
+        auto spmv = [&](double* part, int stride) {
+            if (pair)
+                hipLaunchKernelGGL(k_mcg_spmv2, dim3(ceil_div(nch / 2, 4)), dim3(256), 0, s, e, scp, z.p, q.p, p.p, part,
+                                   stride, nrow / 2, nch / 2);
+            else
+                hipLaunchKernelGGL(k_mcg_spmv, dim3(ceil_div(nch, 4)), dim3(256), 0, s, e, scp, z.p, q.p, p.p, part, stride);
+        };
         for (int64_t it = 0; it < iters; ++it) {
             if (fa) {
-                hipLaunchKernelGGL(k_mcg_spmv, dim3(ceil_div(nch, 4)), dim3(256), 0, s, e, scp, z.p, q.p, p.p, ppq, 1);
+                spmv(ppq, 1);
                 hipLaunchKernelGGL(k_mcg_axpy_fa, dim3(nb256(nrow)), dim3(256), 0, s, e, scp, x_target_, r.p, z.p, p.p,
                                    q.p, partial.p, (const double*)ppq, cb.p, mirror.dev);
             } else {
-                hipLaunchKernelGGL(k_mcg_spmv, dim3(ceil_div(nch, 4)), dim3(256), 0, s, e, scp, z.p, q.p, p.p, partial.p, 2);
+                spmv(partial.p, 2);
                 hipLaunchKernelGGL(k_mcg_fin, dim3(nsys), dim3(256), 0, s, (int)kMcgAlpha, partial.p, cb.p, scp, mirror.dev);
                 hipLaunchKernelGGL(k_mcg_axpy, dim3(nb256(nrow)), dim3(256), 0, s, e, scp, x_target_, r.p, z.p, p.p, q.p,
                                    partial.p);

@@ -164,13 +164,15 @@ def test_headline_fullsize_batched_solves_match_oracle(ddpca, oracle, gpu):
 
 @pytest.mark.parametrize("env,opts", [(("DDPCA_STREAMS", "1"), "HEADLINE_OPTIONS"),
                                       (("DDPCA_STREAMS", "1"), "HEADLINE_OPTIONS_SMALL"),
-                                      (("DDPCA_TAIL_PACING", "0"), "HEADLINE_OPTIONS")],
-                         ids=["one-stream", "one-stream-small", "whole-replay-pacing"])
+                                      (("DDPCA_TAIL_PACING", "0"), "HEADLINE_OPTIONS"),
+                                      (("DDPCA_MCG_PAIR", "0"), "HEADLINE_OPTIONS")],
+                         ids=["one-stream", "one-stream-small", "whole-replay-pacing", "unpaired-mass-spmv"])
 def test_schedule_variants_are_bit_identical(ddpca, gpu, monkeypatch, env, opts):
     """Schedule-only variants of the headline path must not change a bit: the two-stream split of
     the body-balance batch and of the mass CG (MgpisDevice / MassBatch ::set_split, default on)
-    against one stream, on both option sets; and whole-replay pacing to the end of every solve
-    against the one-iteration tail graphs.  ADMM trajectory, displacements and PCG iteration
+    against one stream, on both option sets; whole-replay pacing to the end of every solve
+    against the one-iteration tail graphs; and the fused interface update's mass SpMV reading each
+    shared inteMass once for both its systems (k_mcg_spmv2) against one read per system.  ADMM trajectory, displacements and PCG iteration
     counts equal bit for bit (8 ADMM iterations, reduced chain).  (The variants measured slower
     and kept opt-in in round 3 -- stencil-coded copies, XCD-slab placement, four-wave colour
     workgroups, inverses by row, fused first sweeps -- were deleted in round 4)"""
