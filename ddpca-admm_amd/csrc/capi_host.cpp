@@ -2,6 +2,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <exception>
 #include <map>
 #include <set>
 #include <memory>
@@ -472,6 +473,29 @@ int ddpca_problem_view(ddpca_problem_t h, const char* cname, int64_t index, int6
                 if (index < 0 || index >= nsub || !cs.built[index]) throw ApiError(DDPCA_EINVAL, "subdomain index");
                 const std::string ck = b + std::to_string(index);
                 auto it = P.cache_csr.find(ck);
+                if (it == P.cache_csr.end() && !cs.assembled && b[0] == 'g') {
+                    // the first globTran_D_1 view assembles every built subdomain's at once, in
+                    // parallel (Rc consStif[L] products: ~35 s per 1.2M-dof subdomain on one core);
+                    // MCONTACT::globTran_D_1 only reads the established hierarchy
+                    std::vector<int64_t> todo;
+                    for (int64_t t = 0; t < nsub; ++t)
+                        if (cs.built[t] && !P.cache_csr.count(b + std::to_string(t))) todo.push_back(t);
+                    std::vector<Csr> out(todo.size());
+                    std::vector<std::exception_ptr> err(todo.size());
+#pragma omp parallel for schedule(dynamic, 1)
+                    for (int64_t k = 0; k < (int64_t)todo.size(); ++k) {
+                        try {
+                            out[k] = P.mc.globTran_D_1(todo[k]);
+                        } catch (...) {
+                            err[k] = std::current_exception();
+                        }
+                    }
+                    for (auto& e : err)
+                        if (e) std::rethrow_exception(e);
+                    for (size_t k = 0; k < todo.size(); ++k)
+                        P.cache_csr.emplace(b + std::to_string(todo[k]), std::move(out[k]));
+                    it = P.cache_csr.find(ck);
+                }
                 if (it == P.cache_csr.end()) {
                     Csr m = cs.assembled ? (b[0] == 'g' ? cs.globTran_D_full[index] : cs.accuProl_full[index])
                                          : (b[0] == 'g' ? P.mc.globTran_D_1(index) : P.mc.accuProl(index));
