@@ -106,6 +106,7 @@ def _declare(L: C.CDLL) -> None:
     L.ddpca_last_error.restype = C.c_char_p
     L.ddpca_gpu_available.restype = C.c_int
     L.ddpca_stream_ceiling.argtypes = [C.c_int, C.c_int64, C.c_int, _DP]
+    L.ddpca_probe_grid_barrier.argtypes = [C.c_int, C.c_int64, C.c_int, C.c_int, _DP]
     L.mgpis_default_options.argtypes = [C.POINTER(MgpisOptions)]
     L.mgpis_default_options.restype = None
     L.ddpca_problem_create.argtypes = [C.c_char_p, _DP, C.c_int, C.POINTER(_P)]
@@ -204,6 +205,14 @@ def stream_ceiling(device: int = 0, nbytes: int = 2 << 30, reps: int = 10) -> di
     out = (C.c_double * 4)()
     _check(lib().ddpca_stream_ceiling(device, int(nbytes), int(reps), out))
     return dict(copy_gbs=out[0], read_gbs=out[1], copy_ms=out[2], read_ms=out[3], bytes_per_buffer=int(nbytes))
+
+
+def probe_grid_barrier(n: int, phases: int = 64, blocks: int = 256, device: int = 0) -> dict:
+    """Graph kernel boundary vs persistent grid barrier per dependent pass over n doubles
+    (ddpca_probe_grid_barrier; measurement only)."""
+    out = (C.c_double * 4)()
+    _check(lib().ddpca_probe_grid_barrier(device, int(n), int(phases), int(blocks), out))
+    return dict(graph_us=out[0], persistent_us=out[1], max_diff=out[2], timed_out=int(out[3]))
 
 
 def default_options(**kw) -> MgpisOptions:
@@ -868,7 +877,7 @@ class MCONTACT:
 
 
 __all__ = ["Problem", "MULTIGRID", "MGPIS", "MCONTACT", "DdpcaError", "lib", "gpu_available", "default_options",
-           "contact_search", "mass_solve", "stream_ceiling",
+           "contact_search", "mass_solve", "stream_ceiling", "probe_grid_barrier",
            "LIBPATH", "HEADLINE_OPTIONS", "HEADLINE_OPTIONS_SMALL", "headline_options", "HEADLINE_MUSC",
            "HEADLINE_WORKLOAD",
            "headline_problem"]

@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <vector>
 
 #include "../../include/ddpca_amd.h"
@@ -61,7 +62,133 @@ __global__ void k_fill(dbl2_t* x, int64_t n) {
     if (i < n) x[i] = dbl2_t{1.0, 2.0};
 }
 
+// ---- grid barrier against a graph kernel boundary (the persistent below-fine V-cycle question,
+// DESIGN §8): `phases` dependent passes y = (x[i] + x[i + n/2 + 977]) / 2 over n doubles (every
+// pass reads what other workgroups, on other XCDs, wrote in the previous one), either as one
+// graph of `phases` launches or as one persistent launch with a grid barrier between passes.
+__device__ __forceinline__ double phase_value(const double* x, int64_t i, int64_t n) {
+    int64_t j = i + n / 2 + 977;
+    if (j >= n) j -= n;
+    if (j >= n) j -= n;
+    return 0.5 * (x[i] + x[j]);
+}
+
+__global__ __launch_bounds__(256) void k_phase(const double* x, double* y, int64_t n) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) y[i] = phase_value(x, i, n);
+}
+
+// every workgroup of the launch is resident (the caller launches at most one per CU); the wait is
+// bounded, so a grid that is not all resident ends with err = 1 instead of hanging
+__global__ __launch_bounds__(256) void k_phase_persistent(double* x, double* y, int64_t n, int phases, unsigned* count,
+                                                          unsigned* gen, int* err) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    __shared__ int bad;
+    if (threadIdx.x == 0) bad = 0;
+    for (int p = 0; p < phases; ++p) {
+        const double* src = (p & 1) ? y : x;
+        double* dst = (p & 1) ? x : y;
+        for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) dst[i] = phase_value(src, i, n);
+        if (p + 1 == phases) break;
+        // grid barrier: agent-scope release of this workgroup's writes, arrival ticket, the last
+        // arrival bumps the generation; acquire before the next pass reads other workgroups' data
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const unsigned g = __hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned a = __hip_atomic_fetch_add(count, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+            if (a + 1 == gridDim.x) {
+                __hip_atomic_store(count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(gen, g + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+                int64_t spin = 0;
+                while (__hip_atomic_load(gen, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == g) {
+                    if (++spin > (int64_t)1 << 24) {
+                        bad = 1;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(2);
+                }
+            }
+        }
+        __syncthreads();
+        if (bad) {
+            if (threadIdx.x == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return;
+        }
+    }
+}
+
 }  // namespace
+
+extern "C" int ddpca_probe_grid_barrier(int device, int64_t n, int phases, int blocks, double* out4) {
+    return guarded([&] {
+        if (!out4 || n < 1024 || n > ((int64_t)1 << 28) || phases < 2 || phases > 4096 || blocks < 1)
+            throw ApiError(DDPCA_EINVAL, "ddpca_probe_grid_barrier: arguments");
+        select_device(device);
+        int cus = 256;
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0) cus = prop.multiProcessorCount;
+        if (blocks > cus) throw ApiError(DDPCA_EINVAL, "ddpca_probe_grid_barrier: at most one workgroup per CU");
+        std::vector<double> h(n);
+        for (int64_t i = 0; i < n; ++i) h[i] = (double)((i * 2654435761ll) % 1000003);
+        DevBuf<double> xg, yg, xp, yp;
+        DevBuf<unsigned> sync(2);
+        DevBuf<int> err(1);
+        sync.zero();
+        err.zero();
+        hipStream_t st;
+        DDPCA_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+        hipEvent_t e0, e1;
+        DDPCA_HIP(hipEventCreate(&e0));
+        DDPCA_HIP(hipEventCreate(&e1));
+        auto elapsed = [&] {
+            DDPCA_HIP(hipEventSynchronize(e1));
+            float ms = 0.f;
+            DDPCA_HIP(hipEventElapsedTime(&ms, e0, e1));
+            return (double)ms;
+        };
+        // graph of `phases` launches (blocks workgroups each, as the persistent form)
+        hipGraph_t g;
+        hipGraphExec_t ge;
+        xg.upload(h);
+        yg.alloc(n);
+        DDPCA_HIP(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+        for (int p = 0; p < phases; ++p)
+            hipLaunchKernelGGL(k_phase, dim3(blocks), dim3(256), 0, st, (p & 1) ? yg.p : xg.p, (p & 1) ? xg.p : yg.p, n);
+        DDPCA_HIP(hipStreamEndCapture(st, &g));
+        DDPCA_HIP(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+        DDPCA_HIP(hipGraphLaunch(ge, st));  // warm-up
+        DDPCA_HIP(hipMemcpyAsync(xg.p, h.data(), n * sizeof(double), hipMemcpyHostToDevice, st));
+        DDPCA_HIP(hipEventRecord(e0, st));
+        DDPCA_HIP(hipGraphLaunch(ge, st));
+        DDPCA_HIP(hipEventRecord(e1, st));
+        const double ms_graph = elapsed();
+        // persistent launch
+        xp.upload(h);
+        yp.alloc(n);
+        hipLaunchKernelGGL(k_phase_persistent, dim3(blocks), dim3(256), 0, st, xp.p, yp.p, n, 2, sync.p, sync.p + 1, err.p);
+        DDPCA_HIP(hipMemcpyAsync(xp.p, h.data(), n * sizeof(double), hipMemcpyHostToDevice, st));
+        DDPCA_HIP(hipEventRecord(e0, st));
+        hipLaunchKernelGGL(k_phase_persistent, dim3(blocks), dim3(256), 0, st, xp.p, yp.p, n, phases, sync.p, sync.p + 1,
+                           err.p);
+        DDPCA_HIP(hipEventRecord(e1, st));
+        const double ms_pers = elapsed();
+        DDPCA_HIP(hipStreamSynchronize(st));
+        const std::vector<double> rg = ((phases & 1) ? yg : xg).download(), rp = ((phases & 1) ? yp : xp).download();
+        double diff = 0.0;
+        for (int64_t i = 0; i < n; ++i) diff = std::max(diff, std::abs(rg[i] - rp[i]));
+        const int bad = err.download()[0];
+        (void)hipGraphExecDestroy(ge);
+        (void)hipGraphDestroy(g);
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+        (void)hipStreamDestroy(st);
+        out4[0] = 1e3 * ms_graph / phases;  // us per pass
+        out4[1] = 1e3 * ms_pers / phases;
+        out4[2] = diff;                     // 0: the barrier made every pass's writes visible
+        out4[3] = bad;                      // 1: a workgroup timed out waiting (not all resident)
+    });
+}
 
 extern "C" int ddpca_stream_ceiling(int device, int64_t bytes, int reps, double* out4) {
     return guarded([&] {

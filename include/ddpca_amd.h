@@ -38,6 +38,12 @@ int ddpca_gpu_available(void);
  * lane, non-temporal, best of three batches of `reps` launches on a stream of its own.
  * out4 = [copy GB/s (bytes read + written), read GB/s, copy ms, read ms]. */
 int ddpca_stream_ceiling(int device, int64_t bytes, int reps, double* out4);
+/* Measurement only (the persistent below-fine V-cycle): `phases` dependent passes over n
+ * doubles, each reading what other workgroups wrote in the previous pass, run as one hipGraph of
+ * `phases` launches and as one persistent launch with an agent-scope grid barrier between passes,
+ * `blocks` (<= CUs) workgroups of 256 each way.  out4 = [graph us per pass, persistent us per pass,
+ * max |difference| of the two results, 1 if a persistent workgroup timed out waiting]. */
+int ddpca_probe_grid_barrier(int device, int64_t n, int phases, int blocks, double* out4);
 
 /* ========================================================================================
  * MGPIS -- multigrid-preconditioned CG on one subdomain (MGPIS.h:8-225)
