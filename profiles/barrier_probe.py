@@ -9,7 +9,9 @@ workgroups (one per CU at most).
 import importlib
 import json
 import sys
+from pathlib import Path
 
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 D = importlib.import_module("ddpca-admm_amd")
 
 
