@@ -237,7 +237,9 @@ def main():
                 "smoother": {0: "jacobi", 1: "block-jacobi", 2: "chebyshev"}[a.smoother] + f"({a.nu})" if a.smoother != 3
                 else f"fine: multicolour block Gauss-Seidel (1 forward, 1 backward); below: block-jacobi({a.nu})",
                 "pcg_x0": "previous solution" if a.warm_start else "zero",
-                "vcycle_operator_storage": {0: "fp64", 1: "fp32", 2: "fp32, fine level block-exponent fp16"}[a.precond_fp32],
+                "vcycle_operator_storage": {0: "fp64", 1: "fp32",
+                                            2: f"fp32, the {os.environ.get('DDPCA_H16_LEVELS', '3')} finest levels "
+                                               "block-exponent fp16"}[a.precond_fp32],
                 "operator_rows": "deduplicated table" if a.table_mode else "streamed",
                 "coarse_space": f"interface-eliminated (muscSett={a.musc}, doleMcsc={a.dole})" if a.musc else "none",
                 **({"hanging_dofs": int(sum(P.grid(tv).hangRows().shape[0] for tv in range(nsub) if owner[tv] == rank)),

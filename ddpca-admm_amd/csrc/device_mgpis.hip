@@ -1826,8 +1826,10 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
                         v64[q * 9 * kChunk + slot_elem<double>(ij, lane)] = val[(q * 9 + ij) * kChunk + lane];
             L.val.upload(v64);
         }
-        // levels in block-exponent fp16: the finest h16_levels (DDPCA_H16_LEVELS, default 2: +2 % over 1, profiles/r01_sweep_h16.txt)
-        static const int h16_levels = std::getenv("DDPCA_H16_LEVELS") ? std::atoi(std::getenv("DDPCA_H16_LEVELS")) : 2;
+        // levels in block-exponent fp16: the finest h16_levels (DDPCA_H16_LEVELS, default 3: +2 % over 1 under block
+        // Jacobi, profiles/r01_sweep_h16.txt; with the multicolour fine level 3 over 2 +1.1 % at 8 subdomains,
+        // +0.4 % at 2, 1 over 2 -4 %, the same 18.0 PCG iterations, profiles/r04j/ab_h16.txt)
+        static const int h16_levels = std::getenv("DDPCA_H16_LEVELS") ? std::atoi(std::getenv("DDPCA_H16_LEVELS")) : 3;
         if (!L.tbl && vc32 && l >= 1 && l >= nlev - h16_levels && opt.precond_fp32 == 2) {
             // block-exponent fp16 copy of the fine level for the smoother and the V-cycle
             // residual (symmetric: a block and its transpose round alike); coarser levels fp32

@@ -2,7 +2,7 @@
 of the synthetic DEHW chain, 1,216,800 free dof, 6 MG levels; measured: 24 device PCG
 iterations vs 16 SGS, solutions 5e-14 apart, true residual 1.9e-13) -- the size the headline number
 is measured on, with the bench's preconditioner storage (precond_fp32 = 2: fp32 levels,
-block-exponent fp16 on the two finest, 16-bit column offsets).
+block-exponent fp16 on the three finest, 16-bit column offsets).
 
 * MGPIS CG_SOLV(1) on the device vs the SGS-faithful oracle's CG_SOLV(1) (oracle.cpp, pinned to
   the reference by test_oracle.py) on the same operators and right-hand side: solutions to 1e-8

@@ -2,7 +2,7 @@
 
 bench.py runs MCONTACT on the synthetic DEHW chain with ``HEADLINE_OPTIONS`` (ddpca-admm_amd/
 __init__.py: multicolour block Gauss-Seidel on the fine level, block-Jacobi with two sweeps
-below, damping 1.7/lambda_max, fp32 V-cycle levels with block-exponent fp16 on the two finest,
+below, damping 1.7/lambda_max, fp32 V-cycle levels with block-exponent fp16 on the three finest,
 streamed rows (table_mode 0), automatic exact-solve level, 4 PCG iterations per hipGraph replay) and ``HEADLINE_MUSC`` (interface-eliminated coarse space,
 muscSett = 2, doleMcsc = 1).  These tests run that same set:
 
