@@ -58,15 +58,18 @@ class MgpisOptions(C.Structure):
 # profiles/r03j.)
 HEADLINE_OPTIONS = dict(smoother=3, nu=2, omega=-1.7, iters_per_graph=4, warm_start=0, precond_fp32=2,
                         table_mode=0, coarse_level=-1)
-# ... for a rank that owns fewer than 4 subdomains (the 4- and 8-GPU runs of the same chain): the
-# colour sweeps' 17 fine-level launches per V-cycle are latency-bound there (equal time at 2
-# subdomains per GPU, profiles/r03j), so the block-Jacobi V(1,1) set, pinned by the same tests.
+# ... for a rank that owns one subdomain (the 8-GPU run of the same chain): a colour launch then
+# holds ~400 chunks, the 17 fine-level launches per V-cycle are latency-bound, so the block-Jacobi
+# V(1,1) set, pinned by the same tests.  (Round 3 measured the two equal at 2 subdomains per GPU,
+# profiles/r03j; with the round-4 library the multicolour set is ahead there, 59.4-59.6 vs
+# 57.0-57.2 ADMM it/s, and at 4, 33.2 vs 30.1: profiles/r04l/ab_small_batch.txt.  One subdomain
+# per GPU is not measurable on one GPU and stays on this set.)
 HEADLINE_OPTIONS_SMALL = dict(HEADLINE_OPTIONS, smoother=1, nu=1)
 
 
 def headline_options(n_owned: int) -> dict:
     """The measured-best headline option set for a rank owning n_owned subdomains."""
-    return dict(HEADLINE_OPTIONS if n_owned >= 4 else HEADLINE_OPTIONS_SMALL)
+    return dict(HEADLINE_OPTIONS if n_owned >= 2 else HEADLINE_OPTIONS_SMALL)
 # and the ADMM setting it runs: interface-eliminated coarse space (muscSett = 2) on level 1 of
 # every subdomain (DEHW.h:2222, 2239)
 HEADLINE_MUSC = dict(muscSett=2, doleMcsc=1)
