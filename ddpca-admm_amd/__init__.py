@@ -51,11 +51,11 @@ class MgpisOptions(C.Structure):
 # The option set bench.py measures the headline on (its defaults; tests/test_headline_gpu.py pins
 # this exact set against the oracle): multicolour block Gauss-Seidel on the fine level (one
 # forward sweep before, one backward after the coarse correction), 3x3 block-Jacobi with two
-# sweeps (damping 1.7 / lambda_max) on the levels below, V-cycle levels stored fp32 with the two
+# sweeps (damping 1.7 / lambda_max) on the levels below, V-cycle levels stored fp32 with the three
 # finest as block-exponent fp16, streamed operator rows, automatic exact-solve level, 4 PCG
 # iterations per hipGraph replay, x0 = 0.  (18.0 instead of block-Jacobi V(1,1)'s 23.6 PCG
 # iterations per solve, +8-10 % ADMM it/s at 8 subdomains per GPU, +5 % at 4, equal at 2:
-# profiles/r03j.)
+# profiles/r03j; round 4: +10 % at 4, +4 % at 2, profiles/r04l/ab_small_batch.txt.)
 HEADLINE_OPTIONS = dict(smoother=3, nu=2, omega=-1.7, iters_per_graph=4, warm_start=0, precond_fp32=2,
                         table_mode=0, coarse_level=-1)
 # ... for a rank that owns one subdomain (the 8-GPU run of the same chain): a colour launch then
@@ -63,7 +63,7 @@ HEADLINE_OPTIONS = dict(smoother=3, nu=2, omega=-1.7, iters_per_graph=4, warm_st
 # V(1,1) set, pinned by the same tests.  (Round 3 measured the two equal at 2 subdomains per GPU,
 # profiles/r03j; with the round-4 library the multicolour set is ahead there, 59.4-59.6 vs
 # 57.0-57.2 ADMM it/s, and at 4, 33.2 vs 30.1: profiles/r04l/ab_small_batch.txt.  One subdomain
-# per GPU is not measurable on one GPU and stays on this set.)
+# per GPU: profiles/one_sub_probe.py times the subdomain solve alone.)
 HEADLINE_OPTIONS_SMALL = dict(HEADLINE_OPTIONS, smoother=1, nu=1)
 
 
