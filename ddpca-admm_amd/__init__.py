@@ -63,7 +63,8 @@ HEADLINE_OPTIONS = dict(smoother=3, nu=2, omega=-1.7, iters_per_graph=4, warm_st
 # V(1,1) set, pinned by the same tests.  (Round 3 measured the two equal at 2 subdomains per GPU,
 # profiles/r03j; with the round-4 library the multicolour set is ahead there, 59.4-59.6 vs
 # 57.0-57.2 ADMM it/s, and at 4, 33.2 vs 30.1: profiles/r04l/ab_small_batch.txt.  One subdomain
-# per GPU: profiles/one_sub_probe.py times the subdomain solve alone.)
+# per GPU, the subdomain solve alone: block Jacobi 10.1 ms (23 PCG iterations) vs multicolour
+# 10.9 ms (18), profiles/r04l/one_sub_probe.json.)
 HEADLINE_OPTIONS_SMALL = dict(HEADLINE_OPTIONS, smoother=1, nu=1)
 
 
