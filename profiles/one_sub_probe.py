@@ -4,7 +4,7 @@ the block-Jacobi small-batch set, alternating, best of 5 timed solves each (host
 included, the same for both).  The worm's consForc is zero at iteration 0, so both take a fixed
 pseudo-random right-hand side.
 
-    python profiles/one_sub_probe.py OUT.json
+    python profiles/one_sub_probe.py OUT.json [--variants]
 """
 import importlib
 import json
@@ -21,11 +21,17 @@ D = importlib.import_module("ddpca-admm_amd")
 def main():
     P = D.Problem("dehw", 1, 3, 2, 2, 5, 0.2).ESTABLISH()
     rows = []
-    for tv in (0, 1):
+    sets = [("multicolour", D.HEADLINE_OPTIONS), ("block-jacobi", D.HEADLINE_OPTIONS_SMALL)]
+    if "--variants" in sys.argv:  # exact solve one level higher, Chebyshev smoothing
+        sets += [("block-jacobi, exact level 2", dict(D.HEADLINE_OPTIONS_SMALL, coarse_level=2)),
+                 ("multicolour, exact level 2", dict(D.HEADLINE_OPTIONS, coarse_level=2)),
+                 ("chebyshev nu 2", dict(D.HEADLINE_OPTIONS_SMALL, smoother=2, nu=2)),
+                 ("block-jacobi nu 2", dict(D.HEADLINE_OPTIONS_SMALL, nu=2))]
+    for tv in ((1,) if "--variants" in sys.argv else (0, 1)):
         n = len(P.grid(tv).consForc)
         b = ((np.arange(n) * 7919 + 13) % 2003) / 2003.0 - 0.5
         for rep in range(2):
-            for name, opts in (("multicolour", D.HEADLINE_OPTIONS), ("block-jacobi", D.HEADLINE_OPTIONS_SMALL)):
+            for name, opts in sets:
                 M = D.MGPIS.from_problem(P, tv, **opts)
                 M.CG_SOLV(1, b)  # warm-up (graph capture)
                 best, its = 1e300, 0

@@ -4,4 +4,4 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 500 python -u profiles/one_sub_probe.py gpurun_out/r04n_one_sub.json || { echo "probe failed rc=$?"; exit 1; }
+timeout -k 10 500 python -u profiles/one_sub_probe.py gpurun_out/r04n_one_sub.json ${VARIANTS:-} || { echo "probe failed rc=$?"; exit 1; }
