@@ -6,6 +6,7 @@
 // the reference's to its BiCGSTAB accuracy.  Runs without a GPU (tests/test_lagrange.py); the
 // device path is checked by oracle/ref_lagrange.cpp (tests/test_lagrange_gpu.py).
 //   ref_lagrange_host [cylinder] globLeve fric tangential_load
+#include <chrono>
 #include <unistd.h>
 
 #include <Eigen/SparseLU>
@@ -136,7 +137,15 @@ int main(int argc, char** argv) {
             itfs[ts].ips.push_back(q);
         }
     }
-    const ddpca::LagrangeResult r = ddpca::run_lagrange(subs, itfs, 50, [](const ddpca::LagrangeSystem& sys, std::vector<double>& x) {
+    double t_solve = 0.0;
+    const auto t_run = std::chrono::steady_clock::now();
+    const ddpca::LagrangeResult r = ddpca::run_lagrange(subs, itfs, 50, [&](const ddpca::LagrangeSystem& sys, std::vector<double>& x) {
+        const auto t0 = std::chrono::steady_clock::now();
+        struct Acc {
+            double& t;
+            std::chrono::steady_clock::time_point s;
+            ~Acc() { t += std::chrono::duration<double>(std::chrono::steady_clock::now() - s).count(); }
+        } acc{t_solve, t0};
         Eigen::SparseMatrix<double> K = from_csr(sys.K.back());
         Eigen::SparseLU<Eigen::SparseMatrix<double>> lu(K);
         Eigen::Map<const Eigen::VectorXd> F(sys.F.data(), (Eigen::Index)sys.F.size());
@@ -144,6 +153,8 @@ int main(int argc, char** argv) {
         x.assign(u.data(), u.data() + u.size());
         return (int64_t)0;
     });
+    const double t_all = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_run).count();
+    std::fprintf(stderr, "[timing] run_lagrange %.2f s, of which the Eigen LU solves %.2f s\n", t_all, t_solve);
     double du = 0.0;
     for (size_t tv = 0; tv < subs.size(); ++tv) {
         MULTIGRID& g = b.multGrid[tv];
