@@ -2096,13 +2096,26 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
             const auto& p = perm[clev][s];
             const int64_t nc = subs[s].nnodes[clev], n0 = 3 * nc;
             std::vector<double> D(n0 * n0, 0.0);
+            // a constrained dof's decoupled row and column (zeroed again after the inverse) carry 1,
+            // or in the general path the largest free diagonal entry, so that its pivot does not
+            // read as near-singular against stiffness-scaled ones (inv_general_lu_device's test)
+            double cdiag = 1.0;
+            if (general) {
+                cdiag = 0.0;
+                for (int64_t r = 0; r < nc; ++r)
+                    for (int64_t k = A.ptr[r]; k < A.ptr[r + 1]; ++k)
+                        if (A.col[k] == r)
+                            for (int a = 0; a < 3; ++a)
+                                if (fr[3 * r + a]) cdiag = std::max(cdiag, std::abs(A.val[9 * k + 4 * a]));
+                if (!(cdiag > 0.0)) cdiag = 1.0;
+            }
             for (int64_t r = 0; r < nc; ++r)
                 for (int64_t k = A.ptr[r]; k < A.ptr[r + 1]; ++k) {
                     const int64_t j = A.col[k];
                     for (int a = 0; a < 3; ++a)
                         for (int b = 0; b < 3; ++b) {
                             double v = A.val[9 * k + 3 * a + b];
-                            if (!fr[3 * r + a] || !fr[3 * j + b]) v = (j == r && a == b) ? 1.0 : 0.0;
+                            if (!fr[3 * r + a] || !fr[3 * j + b]) v = (j == r && a == b) ? cdiag : 0.0;
                             D[(3 * p[r] + a) * n0 + 3 * p[j] + b] = v;
                         }
                 }
