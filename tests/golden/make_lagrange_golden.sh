@@ -17,6 +17,7 @@ run() {  # id args...
     rm -rf "$tmp"
     echo "$id: $(ls "$out" | wc -l) files"
 }
+run mgpis-frictionless 1 1 0 0
 run mgpis-coulomb-slip 1 1 0.2 2e6
 run diagonal-frictionless 1 2 0 0
 run cylinder-hanging cylinder 1 1 0 0

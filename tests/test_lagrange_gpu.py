@@ -22,11 +22,9 @@ EXE = Path(__file__).resolve().parents[1] / "oracle" / "_ref" / "ref_lagrange"
 
 
 @pytest.mark.timeout(900)
-# (round 4 dropped BLOCK frictionless under MGPIS, 34 s of the GPU suite: the Coulomb case runs the
-# same MGPIS-preconditioned BiCGSTAB over three Newton steps, the diagonal one the patch test)
-@pytest.mark.parametrize("example,prec,fric,tang", [("block", "1", "0.2", "2e6"), ("block", "2", "0", "0"),
-                                                    ("cylinder", "1", "0", "0")],
-                         ids=["mgpis-coulomb-slip", "diagonal-frictionless", "cylinder-hanging"])
+@pytest.mark.parametrize("example,prec,fric,tang", [("block", "1", "0", "0"), ("block", "1", "0.2", "2e6"),
+                                                    ("block", "2", "0", "0"), ("cylinder", "1", "0", "0")],
+                         ids=["mgpis-frictionless", "mgpis-coulomb-slip", "diagonal-frictionless", "cylinder-hanging"])
 def test_lagrange_matches_reference(gpu, tmp_path, request, example, prec, fric, tang):
     """block: BLOCK as above.  cylinder: the reference's CYLINDER_1 (copyNumb 1, locaLeve 4: four
     cylinders, locally refined contact bands, 35 % hanging nodes -- integration points whose
