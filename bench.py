@@ -77,7 +77,8 @@ def parse():
                     help="V-cycle level of the exact dense coarse solve (-1: auto, 0: the reference's)")
     ap.add_argument("--mesh", choices=["headline", "general"], default="headline",
                     help="general: DEHW's general-mesh features on the same chain (the contact band refined once "
-                         "more -> hanging level, rotated support nodes, explicit transfer lists, no coarse space)")
+                         "more -> hanging level, rotated support nodes, explicit transfer lists) with the same "
+                         "coarse space (MULTISCALE_1 on the general tree)")
     ap.add_argument("--no-general", action="store_true",
                     help="skip the general-mesh line the N = 1 headline run adds (a child process, before the headline)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -118,8 +119,6 @@ def main():
     t_setup = time.perf_counter()
     general = a.mesh == "general"
     feat = dict(D.GENERAL_FEATURES) if general else {}
-    if general:
-        a.musc = 0  # MULTISCALE_1 is restated for uniform hierarchies (multiscale.cpp)
     P = D.headline_problem(groups=a.groups, nx=a.nx, ny=a.ny, nz=a.nz, gl=a.gl, fric=a.fric,
                            ip_contact=a.ip_contact, ip_glued=a.ip_glued, **feat)
     nip = sum(len(P.array("ip_w", ts)) for ts in range(P.nint))

@@ -82,8 +82,8 @@ HEADLINE_MUSC = dict(muscSett=2, doleMcsc=1)
 HEADLINE_WORKLOAD = dict(groups=4, nx=3, ny=2, nz=2, gl=5, fric=0.2, ip_contact=2, ip_glued=1, band=0, rot=0)
 # DEHW's general-mesh features on the same chain (bench.py --mesh general): the contact band refined
 # once more (a general tree: hanging level past the MGPIS hierarchy, explicit transfer lists) and
-# rotated support nodes (prolongation blocks off w I); no coarse space (MULTISCALE_1 is restated for
-# uniform hierarchies only, multiscale.cpp)
+# rotated support nodes (prolongation blocks off w I); the same coarse space as the headline
+# (HEADLINE_MUSC: MULTISCALE_1 on the general tree, multiscale.cpp)
 GENERAL_FEATURES = dict(band=1, rot=1)
 
 

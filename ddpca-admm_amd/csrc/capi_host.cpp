@@ -592,6 +592,54 @@ int ddpca_problem_view(ddpca_problem_t h, const char* cname, int64_t index, int6
             v.clear();
             for (const auto& kv : g.consDofv) v.push_back(kv.first);
             put(v, data, count, dtype);
+        } else if (name == "consDofv_val") {
+            auto& v = P.cache_f64[key];
+            v.clear();
+            for (const auto& kv : g.consDofv) v.push_back(kv.second);
+            put(v, data, count, dtype);
+        } else if (name == "nodeRota") {  // rotated nodes (MULTIGRID::nodeRota keys)
+            auto& v = P.cache_i64[key];
+            v.clear();
+            for (const auto& kv : g.nodeRota) v.push_back(kv.first);
+            put(v, data, count, dtype);
+        } else if (name == "nodeRota_val") {  // their 3x3 matrices, row-major, 9 per node
+            auto& v = P.cache_f64[key];
+            v.clear();
+            for (const auto& kv : g.nodeRota) v.insert(v.end(), kv.second.begin(), kv.second.end());
+            put(v, data, count, dtype);
+        } else if (name == "material") {
+            auto& v = P.cache_f64[key];
+            v = {g.mateElas, g.matePois};
+            put(v, data, count, dtype);
+        } else if (name.rfind("tree:", 0) == 0) {
+            // the element tree as the generator left it (node ids; before establish's TRANSFER renumbers
+            // a general tree): corner (8 per element), parent, level, refiPatt, child_ptr, child
+            if (P.established && g.general) throw ApiError(DDPCA_ESTATE, "tree views before establish (a general tree is renumbered)");
+            const std::string w = name.substr(5);
+            auto& v = P.cache_i64[key];
+            v.clear();
+            if (w == "corner") {
+                for (const auto& e : g.elemVect) v.insert(v.end(), e.cornNode.begin(), e.cornNode.end());
+            } else if (w == "parent") {
+                for (const auto& e : g.elemVect) v.push_back(e.parent);
+            } else if (w == "level") {
+                for (const auto& e : g.elemVect) v.push_back(e.level);
+            } else if (w == "refiPatt") {
+                for (const auto& e : g.elemVect) v.push_back(e.leaf() ? 7 : e.refiPatt);
+            } else if (w == "child_ptr") {
+                v.push_back(0);
+                for (const auto& e : g.elemVect)
+                    v.push_back(v.back() + (int64_t)(e.children.empty() && e.firstChild >= 0 ? 8 : e.children.size()));
+            } else if (w == "child") {
+                for (const auto& e : g.elemVect) {
+                    if (e.children.empty() && e.firstChild >= 0)
+                        for (int c = 0; c < 8; ++c) v.push_back(e.firstChild + c);
+                    else v.insert(v.end(), e.children.begin(), e.children.end());
+                }
+            } else {
+                throw ApiError(DDPCA_EINVAL, "unknown tree array " + w);
+            }
+            put(v, data, count, dtype);
         } else if (name.rfind("K:", 0) == 0 || name.rfind("P:", 0) == 0) {
             const bool isK = name[0] == 'K';
             if (level < 0 || level > g.maxiLeve - (isK ? 0 : 1)) throw ApiError(DDPCA_EINVAL, "level");

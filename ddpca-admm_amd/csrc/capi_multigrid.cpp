@@ -486,6 +486,35 @@ int ddpca_problem_set_subdomain_multigrid(ddpca_problem_t p, int64_t tv, ddpca_m
     });
 }
 
+int ddpca_problem_set_subdomain_tree(ddpca_problem_t p, int64_t tv, ddpca_multigrid_t h) {
+    return guarded([&] {
+        if (!p) throw ApiError(DDPCA_EINVAL, "null problem");
+        Problem& P = *reinterpret_cast<Problem*>(p);
+        if (P.established) throw ApiError(DDPCA_ESTATE, "problem already established");
+        if (tv < 0 || tv >= (int64_t)P.mc.multGrid.size()) throw ApiError(DDPCA_EINVAL, "subdomain index");
+        ddpca_multigrid& M = open(h, false);
+        if (!M.g.coupNode.empty() && M.g.coupReps < 0) throw ApiError(DDPCA_EINVAL, "coupled nodes need coupReps");
+        MULTIGRID g = M.g;
+        g.force_general = true;  // TRANSFER's general algorithm: node ids become positions
+        P.mc.multGrid[tv] = std::move(g);
+        P.owned[tv] = 0;         // established by ddpca_problem_establish(_owned)
+    });
+}
+
+int ddpca_problem_set_contact(ddpca_problem_t p, int64_t ts, int64_t body0, int64_t body1) {
+    return guarded([&] {
+        if (!p) throw ApiError(DDPCA_EINVAL, "null problem");
+        Problem& P = *reinterpret_cast<Problem*>(p);
+        if (P.established) throw ApiError(DDPCA_ESTATE, "problem already established");
+        const int64_t nsub = (int64_t)P.mc.multGrid.size();
+        if (ts < 0 || ts >= (int64_t)P.mc.searCont.size()) throw ApiError(DDPCA_EINVAL, "interface index");
+        if (body0 < 0 || body0 >= nsub || body1 < 0 || body1 >= nsub || body0 == body1)
+            throw ApiError(DDPCA_EINVAL, "interface bodies");
+        P.mc.searCont[ts].body[0] = body0;
+        P.mc.searCont[ts].body[1] = body1;
+    });
+}
+
 int ddpca_multigrid_destroy(ddpca_multigrid_t h) {
     delete h;
     return DDPCA_OK;

@@ -1074,7 +1074,10 @@ struct CoarseDev {
     DevBuf<int32_t> xsrc, qcol;
     DevBuf<double> qw;
     DevBuf<uint8_t> flag;
-    // assembled variant (cs.assembled): accuProl as CSR rows over the owned fine free dofs
+    // assembled variant (cs.assembled): the caller's globTran_D_1 in the right-hand side CSR and
+    // accuProl as CSR rows over the owned fine free dofs; factored: the scalar stencil (<= 8
+    // parents) for every node it can hold, CSR rows (same arrays) for the rest -- nodes whose chain
+    // meets a nodal rotation's 3x3 block (general trees)
     bool assembled = false, latin = false;
     int64_t npr = 0, ncd = 0;
     DevBuf<int64_t> pptr;
@@ -2017,8 +2020,8 @@ void build_coarse(ddpca_mcontact& H, Problem& P) {
                 C.dense[(size_t)r * n + cs.globCoup_1.col[k]] = cs.globCoup_1.val[k];
     }
     if (!H.mg) return;
+    C.assembled = cs.assembled;
     if (cs.assembled) {
-        C.assembled = true;
         std::vector<int64_t> ptr{0};
         std::vector<int32_t> col, tgt, cd;
         std::vector<double> val;
@@ -2089,6 +2092,9 @@ void build_coarse(ddpca_mcontact& H, Problem& P) {
     std::vector<int32_t> qcol(8 * C.qnn, -1);
     std::vector<double> qw(8 * C.qnn, 0.0);
     std::vector<uint8_t> flag(H.NU, 0);
+    std::vector<int64_t> hptr{0};
+    std::vector<int32_t> hcol, htgt;
+    std::vector<double> hval;
     for (size_t i = 0; i < H.subs.size(); ++i) {
         const int64_t tv = H.subs[i].tv;
         const MULTIGRID& g = mc.multGrid[tv];
@@ -2099,15 +2105,49 @@ void build_coarse(ddpca_mcontact& H, Problem& P) {
         }
         const Stencil& Q = cs.accuQ[tv];
         const int64_t b0 = H.subs[i].dof0 / 3;
+        std::vector<int64_t> bo(Q.col.size(), -1);
+        for (size_t q = 0; q < Q.bent.size(); ++q) bo[Q.bent[q]] = (int64_t)q;
         for (int64_t nd = 0; nd < Q.nf; ++nd) {
             const int64_t len = Q.ptr[nd + 1] - Q.ptr[nd];
-            if (len > 8) throw ApiError(DDPCA_EINVAL, "accumulated prolongation with more than 8 parents");
-            for (int64_t k = 0; k < len; ++k) {
-                qcol[k * C.qnn + b0 + nd] = (int32_t)(xnoff[i] + 3 * Q.col[Q.ptr[nd] + k]);
-                qw[k * C.qnn + b0 + nd] = Q.w[Q.ptr[nd] + k];
+            bool scalar = len <= 8;
+            for (int64_t k = Q.ptr[nd]; k < Q.ptr[nd + 1] && scalar; ++k) scalar = bo[k] < 0;
+            if (scalar) {
+                for (int64_t k = 0; k < len; ++k) {
+                    qcol[k * C.qnn + b0 + nd] = (int32_t)(xnoff[i] + 3 * Q.col[Q.ptr[nd] + k]);
+                    qw[k * C.qnn + b0 + nd] = Q.w[Q.ptr[nd] + k];
+                }
+                continue;
+            }
+            // a CSR row per free dof over x_c (the scalar kernel adds 0 there and the prescribed
+            // values of the node's constrained dofs)
+            for (int a = 0; a < 3; ++a) {
+                const int64_t dof = 3 * nd + a;
+                if (!g.consFlag[dof]) continue;
+                for (int64_t k = Q.ptr[nd]; k < Q.ptr[nd + 1]; ++k) {
+                    const int64_t c = Q.col[k];
+                    for (int b = 0; b < 3; ++b) {
+                        if (bo[k] < 0 && b != a) continue;
+                        const int32_t f = g.freeIndex[3 * c + b];
+                        const double w = bo[k] < 0 ? Q.w[k] : Q.bval[9 * bo[k] + 3 * a + b];
+                        if (f < 0 || w == 0.0) continue;
+                        hcol.push_back((int32_t)(xoff[i] + f));
+                        hval.push_back(w);
+                    }
+                }
+                hptr.push_back((int64_t)hcol.size());
+                htgt.push_back((int32_t)(H.subs[i].dof0 + dof));
             }
         }
         for (int64_t dof = 0; dof < 3 * g.numNodes(); ++dof) flag[H.subs[i].dof0 + dof] = g.consFlag[dof];
+    }
+    C.npr = (int64_t)htgt.size();
+    C.ncd = 0;
+    if (C.npr) {
+        C.pptr.upload(hptr);
+        C.pcol.upload(hcol.empty() ? std::vector<int32_t>{0} : hcol);
+        C.pval.upload(hval.empty() ? std::vector<double>{0.0} : hval);
+        C.ptgt.upload(htgt);
+        C.bytes_iter += 12.0 * (double)hcol.size() + 20.0 * (double)C.npr;
     }
     C.xsrc.upload(xsrc);
     C.xn.alloc(std::max<int64_t>(nxn, 1));
@@ -2265,6 +2305,9 @@ void coarse_correct(ddpca_mcontact& H) {
     hipLaunchKernelGGL(k_cs_scatter, dim3(nb256(C.nxn)), dim3(256), 0, st, C.xsrc.p, C.xc.p, C.xn.p, C.nxn);
     hipLaunchKernelGGL(k_cs_prolong, dim3(nb256(C.qnn)), dim3(256), 0, st, C.qcol.p, C.qw.p, C.qnn, C.xn.p, C.flag.p,
                        H.presc.p, H.u);
+    if (C.npr)  // the nodes the scalar stencil cannot hold (rotation blocks)
+        hipLaunchKernelGGL(k_cs_prolong_csr, dim3(nb256(C.npr)), dim3(256), 0, st, C.pptr.p, C.pcol.p, C.pval.p, C.ptgt.p,
+                           C.xc.p, H.u, C.npr);
 }
 
 // Reference MONITOR (MCONTACT.h:2725-2845) on the reduced norms; true = converged.
@@ -2737,6 +2780,13 @@ int64_t mcontact_gpu_get(mcontact_t h, const char* what, int64_t index, void* ou
         if (w == "mass_iters") {
             n = 1;
             if (out && cap >= 1) static_cast<int64_t*>(out)[0] = (int64_t)h->mass_iters;
+            return;
+        }
+        if (w == "gs_launch_bytes") {  // the colour sweeps' per-launch byte model (GsFine::launch_bytes), doubles
+            const auto& v = h->mg->gs.launch_bytes;
+            n = (int64_t)v.size();
+            if (out)
+                for (int64_t i = 0; i < std::min(n, cap); ++i) static_cast<double*>(out)[i] = v[i];
             return;
         }
         throw ApiError(DDPCA_EINVAL, "unknown quantity " + w);

@@ -1641,6 +1641,43 @@ void build_gs(GsFine& G, const LevelDev& L, int nsub, const std::vector<int64_t>
             }
         }
     }
+    // per-launch byte model: a block's stored value record + its column entry, per real row b, the
+    // fp32 inverse, x or r written and the row index, and every distinct x entry the launch
+    // gathers (forward colour k: rows of earlier colours; residual: later ones; backward: all
+    // other colours) once
+    {
+        const double vb = (vt == kValH16 ? 20.0 : vt == kVal32 ? 36.0 : 72.0) + (c16 ? 2.0 : 4.0);
+        const double rowf = 24.0 + (vt == kVal64 ? 72.0 : 36.0) + 24.0 + 4.0;
+        std::vector<double> nl_k(K, 0.0), nu_k(K, 0.0), rows_k(K, 0.0), gx_f(K, 0.0), gx_b(K, 0.0);
+        double gx_r = 0.0;
+        std::vector<int32_t> seen_f(L.nn, -1), seen_b(L.nn, -1), seen_r(L.nn, 0);
+        for (int k = 0; k < K; ++k)
+            for (int s = 0; s < nsub; ++s)
+                for (int64_t g : rows[(size_t)s * K + k]) {
+                    rows_k[k] += 1.0;
+                    const int64_t nc = g / kChunk, lane = g % kChunk;
+                    for (int64_t q = off[nc]; q < off[nc + 1]; ++q) {
+                        const int64_t j = col[q * kChunk + lane];
+                        if (j == g) continue;
+                        if (colour[j] < k) {
+                            nl_k[k] += 1.0;
+                            if (seen_f[j] != k) seen_f[j] = k, gx_f[k] += 1.0;
+                        } else {
+                            nu_k[k] += 1.0;
+                            if (!seen_r[j]) seen_r[j] = 1, gx_r += 1.0;
+                        }
+                        if (seen_b[j] != k) seen_b[j] = k, gx_b[k] += 1.0;
+                    }
+                }
+        G.launch_bytes.clear();
+        double res = 0.0;
+        for (int k = 0; k < K; ++k) {
+            G.launch_bytes.push_back(vb * nl_k[k] + rowf * rows_k[k] + 24.0 * gx_f[k]);
+            res += vb * nu_k[k] + 28.0 * rows_k[k];
+        }
+        G.launch_bytes.push_back(res + 24.0 * gx_r);
+        for (int k = K - 1; k >= 0; --k) G.launch_bytes.push_back(vb * (nl_k[k] + nu_k[k]) + rowf * rows_k[k] + 24.0 * gx_b[k]);
+    }
     G.ncol = K;
     G.nchunk = nch;
     G.first.assign(K, 0);

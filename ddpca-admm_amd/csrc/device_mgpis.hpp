@@ -158,6 +158,10 @@ struct GsFine {
                                          // buffer: a split batch's other half writes the Krylov partials meanwhile)
     std::vector<int64_t> nnzb_sub;       // per member: stored off-diagonal blocks (byte model)
     std::vector<int64_t> slots_sub;      // per member: L + U slots incl. padding
+    // algorithmic bytes of each launch over the whole batch, in launch order: forward colours
+    // 0..K-1, the residual, backward colours K-1..0 (stored blocks, per-row vectors, every distinct
+    // x entry gathered once; profiles/gs_table.py sets the rocprof / PMC figures beside them)
+    std::vector<double> launch_bytes;
 };
 
 class MgpisDevice {

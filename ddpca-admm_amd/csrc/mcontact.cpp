@@ -220,13 +220,47 @@ void Interface::BUILD(const MULTIGRID& g0, const MULTIGRID& g1) {
                 }
         }
     }
+    // CONT_ROTA (MCONTACT.h:157-179) on the operators that map to or from a body's nodal vectors in
+    // its rotated frames: R^T on the rows of systTran(_pena) (349-350, 392-393, 415), R on the
+    // columns of inpoDisp (656-660, 693-697); systMass stays global (CONSTRAINT rotates it with the
+    // stiffness, MULTIGRID.h:1105-1124).  A side with rotated contact nodes leaves the factored
+    // per-ip form (its rows are no longer outer products of the shape values and the basis).
+    factored = true;
+    for (int s = 0; s < 2; ++s) {
+        const auto& rot = g[s]->nodeRota;
+        if (rot.empty()) continue;
+        bool any = false;
+        for (int64_t n : nodeCont[s]) any = any || rot.count(n);
+        if (!any) continue;
+        factored = false;
+        for (Csr* M : {&systTran[s], &systTran_pena[s]})
+            for (int64_t n : nodeCont[s]) {
+                const auto it = rot.find(n);
+                if (it == rot.end()) continue;
+                const double* R = it->second.data();
+                const int64_t len = M->ptr[3 * n + 1] - M->ptr[3 * n];
+                double* v[3] = {&M->val[M->ptr[3 * n]], &M->val[M->ptr[3 * n + 1]], &M->val[M->ptr[3 * n + 2]]};
+                for (int64_t k = 0; k < len; ++k) {
+                    const double o[3] = {v[0][k], v[1][k], v[2][k]};
+                    for (int a = 0; a < 3; ++a) v[a][k] = R[a] * o[0] + R[3 + a] * o[1] + R[6 + a] * o[2];
+                }
+            }
+        Csr& Dd = inpoDisp[s];
+        for (int64_t r = 0; r < Dd.nrow; ++r)
+            for (int64_t k = Dd.ptr[r]; k < Dd.ptr[r + 1]; k += 3) {  // one node's three columns, 3 n + 0..2
+                const auto it = rot.find(Dd.col[k] / 3);
+                if (it == rot.end()) continue;
+                const double* R = it->second.data();
+                const double o[3] = {Dd.val[k], Dd.val[k + 1], Dd.val[k + 2]};
+                for (int b = 0; b < 3; ++b) Dd.val[k + b] = o[0] * R[b] + o[1] * R[3 + b] + o[2] * R[6 + b];
+            }
+    }
     inpoNgap.assign(C * nip, 0.0);
     pemaDiag.assign(C * nip, 0.0);
     for (int64_t q = 0; q < nip; ++q) {
         inpoNgap[C * q] = ip[q].gap;
         for (int m = 0; m < C; ++m) pemaDiag[C * q + m] = pen[m];
     }
-    factored = true;
     for (int s = 0; s < 2; ++s) {
         pemaInpo_r[s] = inpoDisp[s];
         for (int64_t r = 0; r < pemaInpo_r[s].nrow; ++r)
@@ -307,6 +341,7 @@ void MCONTACT::ESTABLISH(const std::vector<uint8_t>* owned) {
             MULTIGRID& g = multGrid[tv];
             if (g.scalProl.empty()) g.TRANSFER();
             g.FLAGS();
+            g.PROL_OPER();
         }
         MULTISCALE(owned);
     }
@@ -318,6 +353,7 @@ void MCONTACT::ESTABLISH(const std::vector<uint8_t>* owned) {
             MULTIGRID& g = multGrid[tv];
             if (g.scalProl.empty()) g.TRANSFER();
             g.FLAGS();
+            g.PROL_OPER();
         }
         MULTISCALE_1(owned);
     }

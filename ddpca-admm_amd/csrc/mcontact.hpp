@@ -55,7 +55,8 @@ struct CoarseSpace {
     std::vector<Csr> globTran_S;              // [tv] n x 3N_tv: interface part of globTran_D_1
                                               // (the stiffness part Rc consStif[L] C_L is applied
                                               // in factored form)
-    std::vector<Stencil> accuQ;               // [tv] fine node -> level-d node prolongation chain
+    std::vector<Stencil> accuQ;               // [tv] fine node -> level-d node prolongation chain (3x3
+                                              // block entries where a nodal rotation enters)
     // assembled variant (operator-level builder: the caller's own MULTISCALE_1 output): the full
     // globTran_D_1[tv] (n x 3N_tv) and accuProl[tv] (nfree_L x nfree_d) replace the factored
     // stiffness part / globTran_S and accuQ

@@ -843,6 +843,12 @@ void stencil_apply_t(const Stencil& S, const double* x, double* y) {
 }
 }  // namespace
 
+void MULTIGRID::PROL_OPER() {
+    if (!prolOper.empty() || scalProl.size() != (size_t)maxiLeve) return;
+    for (int64_t l = 0; l < maxiLeve; ++l) prolOper.push_back(rotate_stencil(scalProl[l], nodeRota, coupNode, coupReps));
+    prolHang = nodeAll ? rotate_stencil(hangStencil, nodeRota, coupNode, coupReps) : Stencil();
+}
+
 void MULTIGRID::CONSTRAINT() {
     const int64_t N = numNodes();
     const int64_t L = maxiLeve;
@@ -874,8 +880,7 @@ void MULTIGRID::CONSTRAINT() {
         }
     }
     prolOper.clear();
-    for (int64_t l = 0; l < L; ++l) prolOper.push_back(rotate_stencil(scalProl[l], nodeRota, coupNode, coupReps));
-    prolHang = nodeAll ? rotate_stencil(hangStencil, nodeRota, coupNode, coupReps) : Stencil();
+    PROL_OPER();
     // the hanging level's Galerkin step, then the hierarchy (MULTIGRID.h:1182-1184)
     levelStif.assign(L + 1, Bsr3());
     levelStif[L] = nodeAll ? galerkin_rap(K, prolHang) : std::move(K);

@@ -133,6 +133,8 @@ public:
     std::vector<double> consForc;         // condensed load (MULTIGRID::consForc)
     std::vector<double> dispForc;         // prescribed values of constrained dofs, dof order
     void FLAGS();       // the dof bookkeeping of CONSTRAINT only (consFlag/freeIndex/freeCount)
+    void PROL_OPER();   // prolOper / prolHang from the stencils and nodeRota (CONSTRAINT's first step;
+                        // the coarse spaces read it on subdomains this rank does not build)
     void CONSTRAINT();  // FLAGS + Galerkin hierarchy + condensed load
 
     // ---------------------------------------------------------------- per-iteration adapters

@@ -1,14 +1,24 @@
-// Host restatement of the interface-eliminated coarse space, MCONTACT::MULTISCALE_1
-// (MCONTACT.h:1672-2301), and of accuProl (MCONTACT.h:864-872), for the uniformly refined
-// hexahedral hierarchies of multigrid.cpp (earlTran, prolOper[maxiLeve] and CONT_ROTA are
-// identities there).  Setup only: the per-iteration correction runs on the GPU
-// (device_mcontact.hip, MCONTACT.h:2578-2612).
+// Host restatement of the two coarse spaces of the reference's ADMM loop on any octree -- the
+// interface-eliminated one, MCONTACT::MULTISCALE_1 (MCONTACT.h:1672-2301), and the LATIN-type one,
+// MCONTACT::MULTISCALE (898-1536) -- and of accuProl (864-872).  Setup only: the per-iteration
+// correction runs on the GPU (device_mcontact.hip, MCONTACT.h:2539-2624).
 //
-// Notation for body b: L = maxiLeve, d = doleMcsc[b], C_l = consOper[l] (free-dof selection),
-// Q = the nodal prolongation prolOper[L-1] ... prolOper[d] as one scalar stencil (fine node ->
-// level-d nodes, <= 8 parents for nested trilinear refinement), Rc = realProl[d]^T ...
-// realProl[L-1]^T (the condensed chain, masked at every level).  The reference uses Q inside
-// globCoup_1 and accuProl, and Rc for every right-hand-side operator; both are kept.
+// Numbering: positions (MULTIGRID.h:884-910); the library renumbers a general tree at TRANSFER, so
+// the reference's earlTran is the identity here and the nodal interface operators already act on
+// positions (incl. the hanging level past maxiLeve).  Notation for body b: L = maxiLeve,
+// d = doleMcsc[b], C_l = consOper[l] (free-dof selection), R = the nodal rotations (CONT_ROTA,
+// MCONTACT.h:157-179: nodeRota's 3x3 block on a rotated node, I elsewhere),
+//   P_l  = prolOper[l] (MULTIGRID.h:1141-1181: scalar stencil entries, w R_off^T / w R_par blocks
+//          where exactly one end is rotated), P_L = prolOper[maxiLeve] (the hanging level: identity
+//          on the level-L positions, the hanging nodes' parents below),
+//   Q    = P_L P_{L-1} ... P_d   (positions incl. the hanging level <- level-d nodes; one composite
+//          stencil with 3x3 block entries where a rotation enters),
+//   H    = P_L C_L^T             (positions <- free fine dofs: the hanging fold),
+//   Rc   = realProl[d]^T ... realProl[L-1]^T, realProl[l] = C_{l+1} P_l C_l^T (the condensed
+//          chain, masked at every level; MULTIGRID.h:1246-1249).
+// The reference uses Q inside globCoup_1 / globCoup and accuProl, H and Rc for every right-hand-side
+// operator (MCONTACT.h:1808-1819, 2010-2019, 2113-2118, 2266-2271).  On a uniformly refined tree
+// without rotations H = C_L^T and Q is one scalar stencil with <= 8 parents per node.
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
@@ -41,7 +51,7 @@ Csr from_triplets(int64_t nrow, int64_t ncol, std::vector<Trip>& t) {
         double v = 0.0;
         while (e < t.size() && t[e].r == t[k].r && t[e].c == t[k].c) v += t[e++].v;
         if (t[k].r < 0 || t[k].r >= nrow || t[k].c < 0 || t[k].c >= ncol)
-            throw std::logic_error("MULTISCALE_1: triplet out of range");
+            throw std::logic_error("MULTISCALE: triplet out of range");
         m.col.push_back((int32_t)t[k].c);
         m.val.push_back(v);
         m.ptr[t[k].r + 1]++;
@@ -66,7 +76,7 @@ Csr transpose_csr(const Csr& A) {
 
 // A * B, both CSR
 Csr spgemm(const Csr& A, const Csr& B) {
-    if (A.ncol != B.nrow) throw std::logic_error("MULTISCALE_1: spgemm shape");
+    if (A.ncol != B.nrow) throw std::logic_error("MULTISCALE: spgemm shape");
     std::vector<Trip> t;
     for (int64_t r = 0; r < A.nrow; ++r)
         for (int64_t k = A.ptr[r]; k < A.ptr[r + 1]; ++k) {
@@ -80,65 +90,254 @@ Csr spgemm(const Csr& A, const Csr& B) {
 // prefix of the fine level's)
 std::vector<int64_t> free_to_dof(const MULTIGRID& g) {
     std::vector<int64_t> f(g.freeCount.back());
-    for (int64_t d = 0; d < (int64_t)g.consFlag.size(); ++d)
+    for (int64_t d = 0; d < (int64_t)g.freeIndex.size(); ++d)
         if (g.freeIndex[d] >= 0) f[g.freeIndex[d]] = d;
     return f;
 }
 
-// C_L A: nodal rows -> free rows of the fine level
-Csr rows_to_free(const MULTIGRID& g, const Csr& A) {
-    std::vector<Trip> t;
-    for (int64_t r = 0; r < A.nrow; ++r) {
-        const int32_t fr = g.freeIndex[r];
-        if (fr < 0) continue;
-        for (int64_t k = A.ptr[r]; k < A.ptr[r + 1]; ++k) t.push_back({fr, A.col[k], A.val[k]});
-    }
-    return from_triplets(g.freeCount.back(), A.ncol, t);
+std::vector<int64_t> block_of(const Stencil& S) {
+    std::vector<int64_t> b(S.col.size(), -1);
+    for (size_t q = 0; q < S.bent.size(); ++q) b[S.bent[q]] = (int64_t)q;
+    return b;
 }
 
-// A C_L^T C_L: zero the columns of constrained nodal dofs
-Csr drop_constrained_cols(const MULTIGRID& g, const Csr& A) {
-    Csr m = A;
-    for (int64_t k = 0; k < m.nnz(); ++k)
-        if (!g.consFlag[m.col[k]]) m.val[k] = 0.0;
-    return m;
+// The composite prolongation Q from level d to the positions [0, nrow), nrow = leveCount[L] or,
+// with `hanging`, every position (the hanging level's rows of P_L).  `rotated`: the prolOper chain
+// (block entries of the nodal rotations), else the scalar chain scalProl (MULTISCALE's ficoCotr,
+// MCONTACT.h:910-914).  Rows are built in position order: a node's parents sit at lower positions.
+Stencil composite(const MULTIGRID& g, int64_t d, bool hanging, bool rotated) {
+    const int64_t L = g.maxiLeve, NL = g.leveCount.at(L), nd = g.leveCount.at(d);
+    const bool hang = hanging && g.nodeAll > NL;
+    const int64_t nrow = hang ? g.nodeAll : NL;
+    const std::vector<Stencil>& P = rotated && !g.prolOper.empty() ? g.prolOper : g.scalProl;
+    const Stencil& Hs = rotated && g.prolHang.nf ? g.prolHang : g.hangStencil;
+    if ((int64_t)P.size() < L) throw std::logic_error("MULTISCALE: transfer stencils missing (TRANSFER)");
+    if ((int64_t)g.nodeLevel.size() < NL) throw std::logic_error("MULTISCALE: node levels missing (TRANSFER)");
+    std::vector<std::vector<int64_t>> bof(L);
+    for (int64_t l = d; l < L; ++l) bof[l] = block_of(P[l]);
+    const std::vector<int64_t> hof = hang ? block_of(Hs) : std::vector<int64_t>();
+    Stencil Q;
+    Q.nf = nrow;
+    Q.nc = nd;
+    Q.ptr.assign(1, 0);
+    std::vector<int64_t> qb;  // per entry: its block in Q.bval, or -1
+    struct Acc {
+        int32_t c;
+        bool blk;
+        double v[9];
+    };
+    std::vector<Acc> acc;
+    auto add = [&](int32_t c, bool blk, const double* m, double s) {
+        Acc* a = nullptr;
+        for (auto& e : acc)
+            if (e.c == c) a = &e;
+        if (!a) {
+            acc.push_back(Acc{c, false, {0, 0, 0, 0, 0, 0, 0, 0, 0}});
+            a = &acc.back();
+        }
+        if (blk && !a->blk) {  // scalar so far -> s I
+            const double s0 = a->v[0];
+            for (int q = 0; q < 9; ++q) a->v[q] = q % 4 == 0 ? s0 : 0.0;
+            a->blk = true;
+        }
+        if (a->blk) {
+            for (int q = 0; q < 9; ++q) a->v[q] += blk ? m[q] : (q % 4 == 0 ? s : 0.0);
+        } else {
+            a->v[0] += s;
+        }
+    };
+    for (int64_t n = 0; n < nrow; ++n) {
+        if (n < nd) {
+            Q.col.push_back((int32_t)n);
+            Q.w.push_back(1.0);
+            qb.push_back(-1);
+            Q.ptr.push_back((int64_t)Q.col.size());
+            continue;
+        }
+        const Stencil* S;
+        const std::vector<int64_t>* bo;
+        if (n < NL) {
+            const int lv = g.nodeLevel[n];  // created on level lv: parents on level lv - 1
+            if (lv < 1 || lv - 1 < d || lv > L) throw std::logic_error("MULTISCALE: node level inconsistent with leveCount");
+            S = &P[lv - 1];
+            bo = &bof[lv - 1];
+        } else {
+            S = &Hs;
+            bo = &hof;
+        }
+        acc.clear();
+        for (int64_t k = S->ptr[n]; k < S->ptr[n + 1]; ++k) {
+            const int64_t c = S->col[k];
+            const double* E = (*bo)[k] >= 0 ? &S->bval[9 * (*bo)[k]] : nullptr;
+            const double w = S->w[k];
+            for (int64_t q = Q.ptr[c]; q < Q.ptr[c + 1]; ++q) {
+                const double* F = qb[q] >= 0 ? &Q.bval[9 * qb[q]] : nullptr;
+                if (!E && !F) {
+                    add(Q.col[q], false, nullptr, w * Q.w[q]);
+                    continue;
+                }
+                double A[9], B[9], M[9];
+                for (int t = 0; t < 9; ++t) {
+                    A[t] = E ? E[t] : (t % 4 == 0 ? w : 0.0);
+                    B[t] = F ? F[t] : (t % 4 == 0 ? Q.w[q] : 0.0);
+                }
+                for (int i = 0; i < 3; ++i)
+                    for (int j = 0; j < 3; ++j) M[3 * i + j] = A[3 * i] * B[j] + A[3 * i + 1] * B[3 + j] + A[3 * i + 2] * B[6 + j];
+                add(Q.col[q], true, M, 0.0);
+            }
+        }
+        std::sort(acc.begin(), acc.end(), [](const Acc& a, const Acc& b) { return a.c < b.c; });
+        for (const auto& e : acc) {
+            Q.col.push_back(e.c);
+            if (e.blk) {
+                Q.w.push_back(0.0);
+                qb.push_back((int64_t)Q.bval.size() / 9);
+                Q.bval.insert(Q.bval.end(), e.v, e.v + 9);
+            } else {
+                Q.w.push_back(e.v[0]);
+                qb.push_back(-1);
+            }
+        }
+        Q.ptr.push_back((int64_t)Q.col.size());
+    }
+    for (int64_t k = 0; k < (int64_t)qb.size(); ++k)
+        if (qb[k] >= 0) Q.bent.push_back(k);
+    return Q;
+}
+
+// Q (x) I3 (block entries as they are) C_d^T as nodal rows 3 n + a of the nodes n < nrow selected
+// by sel (others empty); columns = free dofs of level d (MCONTACT.h:1812-1819, 866-871)
+Csr nodal_prolong(const MULTIGRID& g, const Stencil& Q, int64_t d, const std::vector<uint8_t>* sel, int64_t nrow = -1) {
+    if (nrow < 0) nrow = Q.nf;
+    const std::vector<int64_t> bo = block_of(Q);
+    std::vector<Trip> t;
+    for (int64_t n = 0; n < nrow; ++n) {
+        if (sel && !(*sel)[n]) continue;
+        for (int a = 0; a < 3; ++a)
+            for (int64_t k = Q.ptr[n]; k < Q.ptr[n + 1]; ++k) {
+                const int64_t c = Q.col[k];
+                if (bo[k] >= 0) {
+                    for (int b = 0; b < 3; ++b) {
+                        const int32_t f = g.freeIndex[3 * c + b];
+                        if (f >= 0) t.push_back({3 * n + a, f, Q.bval[9 * bo[k] + 3 * a + b]});
+                    }
+                } else {
+                    const int32_t f = g.freeIndex[3 * c + a];
+                    if (f >= 0) t.push_back({3 * n + a, f, Q.w[k]});
+                }
+            }
+    }
+    return from_triplets(3 * nrow, g.freeCount[d], t);
+}
+
+// CONT_ROTA (MCONTACT.h:157-179) on assembled nodal operators: R^T A (rows) and A R (columns);
+// R's block on node n is nodeRota[n] (positions), I elsewhere
+const double* rota(const MULTIGRID& g, int64_t node) {
+    const auto it = g.nodeRota.find(node);
+    return it == g.nodeRota.end() ? nullptr : it->second.data();
+}
+
+Csr rot_rows(const MULTIGRID& g, const Csr& A) {
+    if (g.nodeRota.empty()) return A;
+    std::vector<Trip> t;
+    for (int64_t r = 0; r < A.nrow; ++r) {
+        const double* R = rota(g, r / 3);
+        const int b = (int)(r % 3);
+        for (int64_t k = A.ptr[r]; k < A.ptr[r + 1]; ++k) {
+            if (!R) {
+                t.push_back({r, A.col[k], A.val[k]});
+                continue;
+            }
+            for (int a = 0; a < 3; ++a) t.push_back({r - b + a, A.col[k], R[3 * b + a] * A.val[k]});  // (R^T)_ab = R_ba
+        }
+    }
+    return from_triplets(A.nrow, A.ncol, t);
+}
+
+Csr rot_cols(const MULTIGRID& g, const Csr& A) {
+    if (g.nodeRota.empty()) return A;
+    std::vector<Trip> t;
+    for (int64_t r = 0; r < A.nrow; ++r)
+        for (int64_t k = A.ptr[r]; k < A.ptr[r + 1]; ++k) {
+            const int64_t c = A.col[k];
+            const double* R = rota(g, c / 3);
+            const int a = (int)(c % 3);
+            if (!R) {
+                t.push_back({r, c, A.val[k]});
+                continue;
+            }
+            for (int b = 0; b < 3; ++b) t.push_back({r, c - a + b, A.val[k] * R[3 * a + b]});
+        }
+    return from_triplets(A.nrow, A.ncol, t);
+}
+
+void rot_vec(const MULTIGRID& g, std::vector<double>& v) {
+    for (const auto& kv : g.nodeRota) {
+        const int64_t n = kv.first;
+        if (3 * n + 2 >= (int64_t)v.size()) continue;
+        const double* R = kv.second.data();
+        double o[3];
+        for (int a = 0; a < 3; ++a) o[a] = R[a] * v[3 * n] + R[3 + a] * v[3 * n + 1] + R[6 + a] * v[3 * n + 2];
+        for (int a = 0; a < 3; ++a) v[3 * n + a] = o[a];
+    }
+}
+
+// H^T A: nodal rows (positions incl. the hanging level) -> free rows of the fine level
+Csr fold_rows(const Csr& H, int64_t nfree, const Csr& A) {
+    std::vector<Trip> t;
+    for (int64_t r = 0; r < A.nrow && r < H.nrow; ++r) {
+        if (A.ptr[r] == A.ptr[r + 1]) continue;
+        for (int64_t h = H.ptr[r]; h < H.ptr[r + 1]; ++h)
+            for (int64_t k = A.ptr[r]; k < A.ptr[r + 1]; ++k) t.push_back({H.col[h], A.col[k], H.val[h] * A.val[k]});
+    }
+    return from_triplets(nfree, A.ncol, t);
+}
+
+// A H with the free fine columns moved back to their nodal dofs (neceTran, MCONTACT.h:1874-1880:
+// the level-L positions' free dofs; a hanging column folds into its parents)
+Csr fold_cols(const Csr& H, const std::vector<int64_t>& f2d, const Csr& A) {
+    std::vector<Trip> t;
+    for (int64_t r = 0; r < A.nrow; ++r)
+        for (int64_t k = A.ptr[r]; k < A.ptr[r + 1]; ++k) {
+            const int64_t c = A.col[k];
+            if (c >= H.nrow) continue;
+            for (int64_t h = H.ptr[c]; h < H.ptr[c + 1]; ++h) t.push_back({r, f2d[H.col[h]], A.val[k] * H.val[h]});
+        }
+    return from_triplets(A.nrow, A.ncol, t);
 }
 
 // Rc A = realProl[d]^T ... realProl[L-1]^T A for A with rows = free dofs of level L
-// (MCONTACT.h:1885-1887, 2113-2115, 2142-2144, 2286-2288): scatter form, touching only A's
-// nonempty rows (surface operators).
+// (MCONTACT.h:1883-1885, 2017-2019, 2116-2118, 2269-2271): scatter form, touching only A's
+// nonempty rows (surface operators); prolOper's block entries as 3x3 blocks
 Csr restrict_chain(const MULTIGRID& g, int64_t d, const std::vector<int64_t>& f2d, Csr A) {
+    const std::vector<Stencil>& P = !g.prolOper.empty() ? g.prolOper : g.scalProl;
     for (int64_t l = g.maxiLeve - 1; l >= d; --l) {
-        const Stencil& S = g.scalProl[l];
+        const Stencil& S = P[l];
+        const std::vector<int64_t> bo = block_of(S);
         std::vector<Trip> t;
         for (int64_t r = 0; r < A.nrow; ++r) {
             if (A.ptr[r] == A.ptr[r + 1]) continue;
             const int64_t dof = f2d[r];  // free row r of level l+1 -> nodal dof
             const int64_t n = dof / 3, a = dof % 3;
             for (int64_t s = S.ptr[n]; s < S.ptr[n + 1]; ++s) {
-                const int32_t c = g.freeIndex[3 * (int64_t)S.col[s] + a];
-                if (c < 0) continue;  // realProl keeps free coarse columns only
-                for (int64_t k = A.ptr[r]; k < A.ptr[r + 1]; ++k) t.push_back({c, A.col[k], S.w[s] * A.val[k]});
+                const int64_t cn = S.col[s];
+                if (bo[s] >= 0) {
+                    for (int b = 0; b < 3; ++b) {
+                        const int32_t c = g.freeIndex[3 * cn + b];
+                        const double w = S.bval[9 * bo[s] + 3 * a + b];
+                        if (c < 0 || w == 0.0) continue;
+                        for (int64_t k = A.ptr[r]; k < A.ptr[r + 1]; ++k) t.push_back({c, A.col[k], w * A.val[k]});
+                    }
+                } else {
+                    const int32_t c = g.freeIndex[3 * cn + a];
+                    if (c < 0) continue;  // realProl keeps free coarse columns only
+                    for (int64_t k = A.ptr[r]; k < A.ptr[r + 1]; ++k) t.push_back({c, A.col[k], S.w[s] * A.val[k]});
+                }
             }
         }
         A = from_triplets(g.freeCount[l], A.ncol, t);
     }
     return A;
-}
-
-// Q (x) I3 C_d^T as rows 3*node + a for the selected fine nodes (others empty): nodal rows,
-// columns = free dofs of level d (MCONTACT.h:1794-1800, 1825-1827, 866-871)
-Csr nodal_prolong(const MULTIGRID& g, const Stencil& Q, int64_t d, const std::vector<uint8_t>* sel) {
-    std::vector<Trip> t;
-    for (int64_t n = 0; n < Q.nf; ++n) {
-        if (sel && !(*sel)[n]) continue;
-        for (int a = 0; a < 3; ++a)
-            for (int64_t k = Q.ptr[n]; k < Q.ptr[n + 1]; ++k) {
-                const int32_t c = g.freeIndex[3 * (int64_t)Q.col[k] + a];
-                if (c >= 0) t.push_back({3 * n + a, c, Q.w[k]});
-            }
-    }
-    return from_triplets(3 * Q.nf, g.freeCount[d], t);
 }
 
 Csr dense_vector_csr(const std::vector<double>& v) {
@@ -156,42 +355,43 @@ Csr dense_vector_csr(const std::vector<double>& v) {
     return m;
 }
 
+// rows of the fine level's free dofs of a nodal-row operator whose rows lie on the level-L
+// positions (C_L A)
+Csr rows_to_free(const MULTIGRID& g, const Csr& A) {
+    std::vector<Trip> t;
+    for (int64_t r = 0; r < A.nrow; ++r) {
+        const int32_t fr = r < (int64_t)g.freeIndex.size() ? g.freeIndex[r] : -1;
+        if (fr < 0) continue;
+        for (int64_t k = A.ptr[r]; k < A.ptr[r + 1]; ++k) t.push_back({fr, A.col[k], A.val[k]});
+    }
+    return from_triplets(g.freeCount.back(), A.ncol, t);
+}
+
+// the first `rows` rows of a stencil (the level-L positions of a composite with hanging rows)
+Stencil stencil_prefix(const Stencil& Q, int64_t rows) {
+    Stencil P;
+    P.nf = rows;
+    P.nc = Q.nc;
+    P.ptr.assign(Q.ptr.begin(), Q.ptr.begin() + rows + 1);
+    P.col.assign(Q.col.begin(), Q.col.begin() + P.ptr.back());
+    P.w.assign(Q.w.begin(), Q.w.begin() + P.ptr.back());
+    for (size_t q = 0; q < Q.bent.size(); ++q)
+        if (Q.bent[q] < P.ptr.back()) {
+            P.bent.push_back(Q.bent[q]);
+            P.bval.insert(P.bval.end(), Q.bval.begin() + 9 * q, Q.bval.begin() + 9 * q + 9);
+        }
+    return P;
+}
+
+// accuProl[tv] = C_L P_{L-1} ... P_d C_d^T (MCONTACT.h:864-872), free_L x free_d
+Csr accu_prol(const MULTIGRID& g, const Stencil& Qfine, int64_t d) {
+    return rows_to_free(g, nodal_prolong(g, Qfine, d, nullptr));
+}
+
 }  // namespace
 
-// Composite nodal prolongation from level d to the fine level (prolOper chain, no masks).
-Stencil accumulated_stencil(const MULTIGRID& g, int64_t d) {
-    const int64_t N = g.numNodes(), nd = g.leveCount.at(d);
-    Stencil Q;
-    Q.nf = N;
-    Q.nc = nd;
-    std::vector<std::vector<std::pair<int32_t, double>>> row(N);
-    for (int64_t n = 0; n < N; ++n) {
-        if (n < nd) {
-            row[n] = {{(int32_t)n, 1.0}};
-            continue;
-        }
-        const int lv = g.nodeLevel[n];  // created on level lv: parents on level lv - 1
-        const Stencil& S = g.scalProl[lv - 1];
-        std::vector<std::pair<int32_t, double>> acc;
-        for (int64_t k = S.ptr[n]; k < S.ptr[n + 1]; ++k)
-            for (const auto& e : row[S.col[k]]) acc.push_back({e.first, S.w[k] * e.second});
-        std::sort(acc.begin(), acc.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
-        auto& out = row[n];
-        for (const auto& e : acc) {
-            if (!out.empty() && out.back().first == e.first) out.back().second += e.second;
-            else out.push_back(e);
-        }
-    }
-    Q.ptr.assign(N + 1, 0);
-    for (int64_t n = 0; n < N; ++n) {
-        for (const auto& e : row[n]) {
-            Q.col.push_back(e.first);
-            Q.w.push_back(e.second);
-        }
-        Q.ptr[n + 1] = (int64_t)Q.col.size();
-    }
-    return Q;
-}
+// Composite nodal prolongation from level d to the fine level (scalar chain, no masks).
+Stencil accumulated_stencil(const MULTIGRID& g, int64_t d) { return composite(g, d, false, false); }
 
 void MCONTACT::MULTISCALE_1(const std::vector<uint8_t>* owned) {
     const int64_t nsub = (int64_t)multGrid.size(), nint = (int64_t)searCont.size();
@@ -231,21 +431,27 @@ void MCONTACT::MULTISCALE_1(const std::vector<uint8_t>* owned) {
     }
     C.n = C.baseReco[nsub];
     std::vector<std::vector<int64_t>> f2d(nsub);
+    std::vector<Stencil> Qall(nsub);  // Q with the hanging level's rows
+    std::vector<Csr> Hf(nsub);        // H = P_L C_L^T
     C.accuQ.assign(nsub, Stencil());
 #pragma omp parallel for schedule(dynamic, 1)
     for (int64_t tv = 0; tv < nsub; ++tv) {
         if (!need[tv]) continue;
-        f2d[tv] = free_to_dof(multGrid[tv]);
-        C.accuQ[tv] = accumulated_stencil(multGrid[tv], doleMcsc[tv]);
+        const MULTIGRID& g = multGrid[tv];
+        f2d[tv] = free_to_dof(g);
+        Qall[tv] = composite(g, doleMcsc[tv], true, true);
+        Hf[tv] = nodal_prolong(g, composite(g, g.maxiLeve, true, true), g.maxiLeve, nullptr);
+        if (mine(tv)) C.accuQ[tv] = stencil_prefix(Qall[tv], g.leveCount[g.maxiLeve]);
     }
     for (int64_t tv = 0; tv < nsub; ++tv) C.built[tv] = mine(tv);
     lap("accumulated stencils");
     auto Rc = [&](int64_t tv, const Csr& A_free) { return restrict_chain(multGrid[tv], doleMcsc[tv], f2d[tv], A_free); };
     auto QI = [&](int64_t tv, const std::vector<uint8_t>& sel) {
-        return nodal_prolong(multGrid[tv], C.accuQ[tv], doleMcsc[tv], &sel);
+        return nodal_prolong(multGrid[tv], Qall[tv], doleMcsc[tv], &sel);
     };
+    auto HT = [&](int64_t tv, const Csr& A) { return fold_rows(Hf[tv], multGrid[tv].freeCount.back(), A); };
     // ---- per interface side: nodal surface operators from the integration points
-    //      (MCONTACT.h:1699-1786, 1906-1990, 2007-2040, 2150-2246)
+    //      (MCONTACT.h:1699-1841, 1906-2047, 2078-2119, 2130-2297)
     std::vector<Trip> coup;                       // globCoup_1 (owned rows)
     std::vector<std::vector<Trip>> tranS(nsub);   // globTran_S[tv]
     std::vector<double> forc(C.n, 0.0);
@@ -267,111 +473,111 @@ void MCONTACT::MULTISCALE_1(const std::vector<uint8_t>* owned) {
         std::vector<Trip>& coup_t = outs[task].coup;
         std::vector<Trip>& tran_t = outs[task].tran;
         auto& forc_t = outs[task].forc;
-        {
         const Interface& itf = searCont[ts];
         const int Cc = itf.comp();
         const double pen[3] = {itf.penN, itf.penF, itf.penF};
-        {
-            const int64_t e = itf.body[s], m = itf.body[1 - s];
-            const MULTIGRID& ge = multGrid[e];
-            const MULTIGRID& gm = multGrid[m];
-            const int64_t Ne = ge.numNodes(), Nm = gm.numNodes();
-            // self operators are the interface mass / transfer of ESTABLISH up to -1/2:
-            //   sum_ip -1/2 w N_e^T T^T P T N_e = -1/2 systMass[s]           (MCONTACT.h:1734-1762)
-            //   sum_ip -1/2 w N_e^T T^T [T] M_e  = -1/2 systTran[s]           (MCONTACT.h:2188-2245)
-            Csr S = itf.systMass[s], Ts = itf.systTran[s];
-            for (auto& v : S.val) v *= -0.5;
-            for (auto& v : Ts.val) v *= -0.5;
-            // cross (self node a, mate node b) blocks: sum_ip w Me_a Mm_b {T^T P T, T^T T, n}
-            std::vector<int64_t> cidx(Ne, -1), midx(Nm, -1);
-            for (size_t k = 0; k < itf.nodeCont[s].size(); ++k) cidx[itf.nodeCont[s][k]] = (int64_t)k;
-            for (size_t k = 0; k < itf.nodeCont[1 - s].size(); ++k) midx[itf.nodeCont[1 - s][k]] = (int64_t)k;
-            const int64_t nce = (int64_t)itf.nodeCont[s].size();
-            std::vector<std::vector<int64_t>> part(nce);     // mate contact nodes per self contact node
-            std::vector<std::vector<double>> blk(nce);       // 9 GP + 9 G + 3 n per partner
-            std::vector<double> gap(3 * Ne, 0.0);
-            std::vector<uint8_t> sel_e(Ne, 0), sel_m(Nm, 0);
-            for (const auto& p : itf.ip) {
-                double G[9], GP[9];
-                for (int i = 0; i < 3; ++i)
-                    for (int j = 0; j < 3; ++j) {
-                        double x = 0, y = 0;
-                        for (int c = 0; c < Cc; ++c) {
-                            x += p.basis[c][i] * p.basis[c][j];
-                            y += p.basis[c][i] * pen[c] * p.basis[c][j];
-                        }
-                        G[3 * i + j] = x;
-                        GP[3 * i + j] = y;
+        const int64_t e = itf.body[s], m = itf.body[1 - s];
+        const MULTIGRID& ge = multGrid[e];
+        const MULTIGRID& gm = multGrid[m];
+        const int64_t Ne = ge.nodalCount(), Nm = gm.nodalCount();
+        // self operators are the interface mass / transfer of ESTABLISH up to -1/2 and CONT_ROTA:
+        //   sum_ip -1/2 w R^T N_e^T T^T P T N_e R = -1/2 R^T systMass[s] R   (MCONTACT.h:1734-1749)
+        //   sum_ip -1/2 w R^T N_e^T T^T [T] M_e  = -1/2 systTran[s]          (MCONTACT.h:2170-2212; BUILD rotates systTran)
+        Csr S = rot_rows(ge, rot_cols(ge, itf.systMass[s])), Ts = itf.systTran[s];
+        for (auto& v : S.val) v *= -0.5;
+        for (auto& v : Ts.val) v *= -0.5;
+        // cross (self node a, mate node b) blocks: sum_ip w Me_a Mm_b {T^T P T, T^T T, n}
+        std::vector<int64_t> cidx(Ne, -1), midx(Nm, -1);
+        for (size_t k = 0; k < itf.nodeCont[s].size(); ++k) cidx[itf.nodeCont[s][k]] = (int64_t)k;
+        for (size_t k = 0; k < itf.nodeCont[1 - s].size(); ++k) midx[itf.nodeCont[1 - s][k]] = (int64_t)k;
+        const int64_t nce = (int64_t)itf.nodeCont[s].size();
+        std::vector<std::vector<int64_t>> part(nce);     // mate contact nodes per self contact node
+        std::vector<std::vector<double>> blk(nce);       // 9 GP + 9 G + 3 n per partner
+        std::vector<double> gap(3 * Ne, 0.0);
+        std::vector<uint8_t> sel_e(Ne, 0), sel_m(Nm, 0);
+        for (const auto& p : itf.ip) {
+            double G[9], GP[9];
+            for (int i = 0; i < 3; ++i)
+                for (int j = 0; j < 3; ++j) {
+                    double x = 0, y = 0;
+                    for (int c = 0; c < Cc; ++c) {
+                        x += p.basis[c][i] * p.basis[c][j];
+                        y += p.basis[c][i] * pen[c] * p.basis[c][j];
                     }
-                const double* Me = p.shap[s];
-                const double* Mm = p.shap[1 - s];
-                for (int a = 0; a < 4; ++a) {
-                    const int64_t na = p.node[s][a], ca = cidx[na];
-                    sel_e[na] = 1;
-                    sel_m[p.node[1 - s][a]] = 1;
-                    for (int b = 0; b < 4; ++b) {
-                        const int64_t cb = midx[p.node[1 - s][b]];
-                        auto& pl = part[ca];
-                        size_t k = std::find(pl.begin(), pl.end(), cb) - pl.begin();
-                        if (k == pl.size()) {
-                            pl.push_back(cb);
-                            blk[ca].resize(21 * pl.size(), 0.0);
-                        }
-                        double* q = &blk[ca][21 * k];
-                        const double ww = p.w * Me[a] * Mm[b];
-                        for (int t = 0; t < 9; ++t) {
-                            q[t] += ww * GP[t];
-                            q[9 + t] += ww * G[t];
-                        }
-                        for (int t = 0; t < 3; ++t) q[18 + t] += ww * p.basis[0][t];
-                    }
-                    // initial-gap force, normal only (MCONTACT.h:2061-2098), side 1 negated
-                    const double gsc = (s == 1 ? -0.5 : 0.5) * p.w * itf.penN * p.gap * Me[a];
-                    for (int i = 0; i < 3; ++i) gap[3 * na + i] += gsc * p.basis[0][i];
+                    G[3 * i + j] = x;
+                    GP[3 * i + j] = y;
                 }
-            }
-            std::vector<Trip> tM, tTm;
-            for (int64_t ca = 0; ca < nce; ++ca) {
-                const int64_t na = itf.nodeCont[s][ca];
-                for (size_t k = 0; k < part[ca].size(); ++k) {
-                    const int64_t mb = itf.nodeCont[1 - s][part[ca][k]];
-                    const double* q = &blk[ca][21 * k];
-                    for (int i = 0; i < 3; ++i) {
-                        for (int j = 0; j < 3; ++j) tM.push_back({3 * na + i, 3 * mb + j, -0.5 * q[3 * i + j]});
-                        // globTran_1 mate: +1/2 w N_m^T T^T [T] N_e, row = mate dof, col = self contact dof
-                        if (Cc == 1) tTm.push_back({3 * mb + i, ca, 0.5 * q[18 + i]});
-                        else
-                            for (int j = 0; j < 3; ++j) tTm.push_back({3 * mb + i, 3 * ca + j, 0.5 * q[9 + 3 * j + i]});
+            const double* Me = p.shap[s];
+            const double* Mm = p.shap[1 - s];
+            for (int a = 0; a < 4; ++a) {
+                const int64_t na = p.node[s][a], ca = cidx[na];
+                sel_e[na] = 1;
+                sel_m[p.node[1 - s][a]] = 1;
+                for (int b = 0; b < 4; ++b) {
+                    const int64_t cb = midx[p.node[1 - s][b]];
+                    auto& pl = part[ca];
+                    size_t k = std::find(pl.begin(), pl.end(), cb) - pl.begin();
+                    if (k == pl.size()) {
+                        pl.push_back(cb);
+                        blk[ca].resize(21 * pl.size(), 0.0);
                     }
+                    double* q = &blk[ca][21 * k];
+                    const double ww = p.w * Me[a] * Mm[b];
+                    for (int t = 0; t < 9; ++t) {
+                        q[t] += ww * GP[t];
+                        q[9 + t] += ww * G[t];
+                    }
+                    for (int t = 0; t < 3; ++t) q[18 + t] += ww * p.basis[0][t];
                 }
-            }
-            const Csr Mx = from_triplets(3 * Ne, 3 * Nm, tM);   // -1/2 w N_e^T T^T P T N_m
-            const Csr MT = transpose_csr(Mx);                     // -1/2 w N_m^T T^T P T N_e
-            const Csr Tm = from_triplets(3 * Nm, itf.mside(s), tTm);
-            // globCoup_1 += inteCoup[ts][s] (MCONTACT.h:1787-1841): Q-based Galerkin blocks
-            {
-                const Csr Qe = QI(e, sel_e), Qm = QI(m, sel_m);
-                const Csr QeT = transpose_csr(Qe);
-                append(coup_t, spgemm(QeT, spgemm(S, Qe)), C.baseReco[e], C.baseReco[e]);
-                append(coup_t, spgemm(QeT, spgemm(Mx, Qm)), C.baseReco[e], C.baseReco[m]);
-            }
-            // globTran_D_1 interface part (MCONTACT.h:1993-2048): rows e and rows m, columns = u_e
-            append(tran_t, Rc(e, rows_to_free(ge, drop_constrained_cols(ge, S))), C.baseReco[e], 0);
-            append(tran_t, Rc(m, rows_to_free(gm, drop_constrained_cols(ge, MT))), C.baseReco[m], 0);
-            // globForc_1 gap part (MCONTACT.h:2099-2109)
-            {
-                const Csr gc = Rc(e, rows_to_free(ge, dense_vector_csr(gap)));
-                for (int64_t r = 0; r < gc.nrow; ++r)
-                    for (int64_t k = gc.ptr[r]; k < gc.ptr[r + 1]; ++k) forc_t.push_back({C.baseReco[e] + r, gc.val[k]});
-            }
-            // globTran_1[ts][s] (MCONTACT.h:2248-2297)
-            {
-                std::vector<Trip> t;
-                append(t, Rc(e, rows_to_free(ge, Ts)), C.baseReco[e], 0);
-                append(t, Rc(m, rows_to_free(gm, Tm)), C.baseReco[m], 0);
-                C.globTran_1[ts][s] = from_triplets(C.n, itf.mside(s), t);
+                // initial-gap force, normal only (MCONTACT.h:2081-2108), side 1 negated
+                const double gsc = (s == 1 ? -0.5 : 0.5) * p.w * itf.penN * p.gap * Me[a];
+                for (int i = 0; i < 3; ++i) gap[3 * na + i] += gsc * p.basis[0][i];
             }
         }
+        std::vector<Trip> tM, tTm;
+        for (int64_t ca = 0; ca < nce; ++ca) {
+            const int64_t na = itf.nodeCont[s][ca];
+            for (size_t k = 0; k < part[ca].size(); ++k) {
+                const int64_t mb = itf.nodeCont[1 - s][part[ca][k]];
+                const double* q = &blk[ca][21 * k];
+                for (int i = 0; i < 3; ++i) {
+                    for (int j = 0; j < 3; ++j) tM.push_back({3 * na + i, 3 * mb + j, -0.5 * q[3 * i + j]});
+                    // globTran_1 mate: +1/2 w N_m^T T^T [T] N_e, row = mate dof, col = self contact dof
+                    if (Cc == 1) tTm.push_back({3 * mb + i, ca, 0.5 * q[18 + i]});
+                    else
+                        for (int j = 0; j < 3; ++j) tTm.push_back({3 * mb + i, 3 * ca + j, 0.5 * q[9 + 3 * j + i]});
+                }
+            }
+        }
+        // -1/2 w R_e^T N_e^T T^T P T N_m R_m (MCONTACT.h:1765-1780), and its transpose, the mate
+        // rows of globTran_D_1 (1967-1982)
+        const Csr Mx = rot_rows(ge, rot_cols(gm, from_triplets(3 * Ne, 3 * Nm, tM)));
+        const Csr MT = transpose_csr(Mx);
+        const Csr Tm = rot_rows(gm, from_triplets(3 * Nm, itf.mside(s), tTm));  // (MCONTACT.h:2177-2179, 2213-2215)
+        rot_vec(ge, gap);                                                           // (2096-2098)
+        // globCoup_1 += inteCoup[ts][s] (MCONTACT.h:1797-1841): Q-based Galerkin blocks
+        {
+            const Csr Qe = QI(e, sel_e), Qm = QI(m, sel_m);
+            const Csr QeT = transpose_csr(Qe);
+            append(coup_t, spgemm(QeT, spgemm(S, Qe)), C.baseReco[e], C.baseReco[e]);
+            append(coup_t, spgemm(QeT, spgemm(Mx, Qm)), C.baseReco[e], C.baseReco[m]);
+        }
+        // globTran_D_1 interface part (MCONTACT.h:1999-2052): rows e and rows m (H^T, Rc),
+        // columns = u_e through H (the level-L free dofs)
+        append(tran_t, Rc(e, HT(e, fold_cols(Hf[e], f2d[e], S))), C.baseReco[e], 0);
+        append(tran_t, Rc(m, HT(m, fold_cols(Hf[e], f2d[e], MT))), C.baseReco[m], 0);
+        // globForc_1 gap part (MCONTACT.h:2110-2119)
+        {
+            const Csr gc = Rc(e, HT(e, dense_vector_csr(gap)));
+            for (int64_t r = 0; r < gc.nrow; ++r)
+                for (int64_t k = gc.ptr[r]; k < gc.ptr[r + 1]; ++k) forc_t.push_back({C.baseReco[e] + r, gc.val[k]});
+        }
+        // globTran_1[ts][s] (MCONTACT.h:2246-2297)
+        {
+            std::vector<Trip> t;
+            append(t, Rc(e, HT(e, Ts)), C.baseReco[e], 0);
+            append(t, Rc(m, HT(m, Tm)), C.baseReco[m], 0);
+            C.globTran_1[ts][s] = from_triplets(C.n, itf.mside(s), t);
         }
     }
     for (size_t task = 0; task < tasks.size(); ++task) {
@@ -382,7 +588,7 @@ void MCONTACT::MULTISCALE_1(const std::vector<uint8_t>* owned) {
         outs[task] = SideOut();
     }
     lap("interface operators");
-    // ---- subdomain blocks: consStif[d] (MCONTACT.h:1675-1693) and Rc consForc (2052-2059)
+    // ---- subdomain blocks: consStif[d] (MCONTACT.h:1675-1693) and Rc consForc (2058-2067)
     for (int64_t tv = 0; tv < nsub; ++tv) {
         if (!mine(tv)) continue;
         const MULTIGRID& g = multGrid[tv];
@@ -395,30 +601,32 @@ void MCONTACT::MULTISCALE_1(const std::vector<uint8_t>* owned) {
     C.globForc_1 = std::move(forc);
     C.globTran_S.assign(nsub, Csr());
     for (int64_t tv = 0; tv < nsub; ++tv)
-        if (mine(tv)) C.globTran_S[tv] = from_triplets(C.n, 3 * multGrid[tv].numNodes(), tranS[tv]);
+        if (mine(tv)) C.globTran_S[tv] = from_triplets(C.n, 3 * multGrid[tv].nodalCount(), tranS[tv]);
     lap("subdomain blocks");
     C.ready = true;
 }
 
-// Full globTran_D_1[tv] = Rc consStif[L] C_L + interface part (tests; the device applies the
-// stiffness part as an SpMV followed by the restriction chain instead)
+// Full globTran_D_1[tv] = Rc consStif[L] neceTran + interface part (tests; the device applies the
+// stiffness part as an SpMV followed by the restriction chain instead); columns = nodal dofs
+// (positions), the level-L positions' free dofs only (MCONTACT.h:1868-1895)
 Csr MCONTACT::globTran_D_1(int64_t tv) const {
     const MULTIGRID& g = multGrid.at(tv);
     const std::vector<int64_t> f2d = free_to_dof(g);
     Csr K = g.consStif(g.maxiLeve);
     for (auto& c : K.col) c = (int32_t)f2d[c];
-    K.ncol = 3 * g.numNodes();
+    K.ncol = 3 * g.nodalCount();
     Csr R = restrict_chain(g, doleMcsc.at(tv), f2d, K);
     std::vector<Trip> t;
     append(t, R, coarse.baseReco[tv], 0);
     append(t, coarse.globTran_S.at(tv), 0, 0);
-    return from_triplets(coarse.n, 3 * g.numNodes(), t);
+    return from_triplets(coarse.n, 3 * g.nodalCount(), t);
 }
 
-// accuProl[tv] = C_L (Q (x) I3) C_d^T (MCONTACT.h:864-872), free_L x free_d
+// accuProl[tv] = C_L P_{L-1} ... P_d C_d^T (MCONTACT.h:864-872), free_L x free_d
 Csr MCONTACT::accuProl(int64_t tv) const {
+    if (coarse.assembled) return coarse.accuProl_full.at(tv);
     const MULTIGRID& g = multGrid.at(tv);
-    return rows_to_free(g, nodal_prolong(g, coarse.accuQ.at(tv), doleMcsc.at(tv), nullptr));
+    return accu_prol(g, coarse.accuQ.at(tv), doleMcsc.at(tv));
 }
 
 }  // namespace ddpca
@@ -426,12 +634,12 @@ Csr MCONTACT::accuProl(int64_t tv) const {
 namespace ddpca {
 
 // Host restatement of the LATIN-type coarse space, MCONTACT::MULTISCALE (MCONTACT.h:898-1536,
-// muscSett bit 0, CYLINDER.h:42), for this library's uniformly refined hierarchies (earlTran,
-// prolOper[maxiLeve] and CONT_ROTA identities; prolOper[L-1..d] = Q (x) I3).  Side 0 of every
-// interface carries the coarse contact unknowns: ficoCotr = the columns of Q restricted to
-// side 0's contact nodes that touch any of them (MCONTACT.h:900-959), one unknown per such
-// level-d node (x3 with friction).  Output in the assembled LATIN form the device consumes
-// (CoarseSpace::latin; the same fields ddpca_problem_set_coarse_latin fills from a caller).
+// muscSett bit 0, CYLINDER.h:42) on any octree.  Side 0 of every interface carries the coarse
+// contact unknowns: ficoCotr = the scalar chain scalProl[L..d] (hanging level included, no
+// rotations: MCONTACT.h:910-914) restricted to side 0's contact nodes, one unknown per level-d node
+// it touches (x3 with friction).  dispUnba takes R^T on its rows and Q^T (MCONTACT.h:1033-1035,
+// 1069-1074), globTran_D R on its columns (1430-1432).  Output in the assembled LATIN form the device
+// consumes (CoarseSpace::latin; the same fields ddpca_problem_set_coarse_latin fills from a caller).
 void MCONTACT::MULTISCALE(const std::vector<uint8_t>* owned) {
     const int64_t nsub = (int64_t)multGrid.size(), nint = (int64_t)searCont.size();
     auto mine = [&](int64_t tv) { return !owned || (*owned)[tv] != 0; };
@@ -451,15 +659,17 @@ void MCONTACT::MULTISCALE(const std::vector<uint8_t>* owned) {
     C.baseReco.assign(nsub + 1, 0);
     for (int64_t tv = 0; tv < nsub; ++tv) C.baseReco[tv + 1] = C.baseReco[tv] + multGrid[tv].freeCount[doleMcsc[tv]];
     const int64_t N = C.baseReco[nsub];
-    // prolongation chains: owned bodies and side 0 of every interface (its coarse contact
-    // unknowns number every rank's columns, so each rank derives all of them)
-    std::vector<uint8_t> needQ(nsub, 0);
-    for (int64_t tv = 0; tv < nsub; ++tv) needQ[tv] = mine(tv);
-    for (const auto& itf : searCont) needQ[itf.body[0]] = 1;
-    C.accuQ.assign(nsub, Stencil());
+    // prolongation chains: the scalar one (hanging level included) of side 0 of every interface (its
+    // coarse contact unknowns number every rank's columns, so each rank derives all of them), the
+    // rotated one of the owned bodies
+    std::vector<uint8_t> need0(nsub, 0);
+    for (const auto& itf : searCont) need0[itf.body[0]] = 1;
+    std::vector<Stencil> Qs(nsub), Qr(nsub);
 #pragma omp parallel for schedule(dynamic, 1)
-    for (int64_t tv = 0; tv < nsub; ++tv)
-        if (needQ[tv]) C.accuQ[tv] = accumulated_stencil(multGrid[tv], doleMcsc[tv]);
+    for (int64_t tv = 0; tv < nsub; ++tv) {
+        if (need0[tv]) Qs[tv] = composite(multGrid[tv], doleMcsc[tv], true, false);
+        if (mine(tv)) Qr[tv] = composite(multGrid[tv], doleMcsc[tv], true, true);
+    }
     // side-0 contact nodes of interfaces this rank did not build (Interface::BUILD's order)
     std::vector<std::vector<int64_t>> nc0(nint);
     for (int64_t ts = 0; ts < nint; ++ts) {
@@ -479,7 +689,7 @@ void MCONTACT::MULTISCALE(const std::vector<uint8_t>* owned) {
     C.coarNode.assign(nint, {});
     for (int64_t ts = 0; ts < nint; ++ts) {
         const Interface& itf = searCont[ts];
-        const Stencil& Q0 = C.accuQ[itf.body[0]];
+        const Stencil& Q0 = Qs[itf.body[0]];
         const auto& nc0t = nc0[ts];
         std::vector<int64_t> newc(Q0.nc, -1);
         for (int64_t k = 0; k < (int64_t)nc0t.size(); ++k)
@@ -515,9 +725,9 @@ void MCONTACT::MULTISCALE(const std::vector<uint8_t>* owned) {
         if (!mine(b)) continue;  // the side's owner assembles it (the device sums the ranks)
         const MULTIGRID& g = multGrid[b];
         const int comp = itf.comp();
-        const int64_t N3 = 3 * g.numNodes();
+        const int64_t N3 = 3 * g.nodalCount();
         const int64_t m0 = itf.mside(0), mv = itf.mside(tv);
-        std::vector<int64_t> c0(multGrid[itf.body[0]].numNodes(), -1), cv(g.numNodes(), -1);
+        std::vector<int64_t> c0(multGrid[itf.body[0]].nodalCount(), -1), cv(g.nodalCount(), -1);
         for (size_t k = 0; k < itf.nodeCont[0].size(); ++k) c0[itf.nodeCont[0][k]] = (int64_t)k;
         for (size_t k = 0; k < itf.nodeCont[tv].size(); ++k) cv[itf.nodeCont[tv][k]] = (int64_t)k;
         std::vector<Trip> disp, unba, tran, tranp, tranD;
@@ -565,9 +775,9 @@ void MCONTACT::MULTISCALE(const std::vector<uint8_t>* owned) {
         }
         const Csr& F = fico[ts];
         const Csr FT = transpose_csr(F);
-        // dispUnba -> level-d free rows: C_d (Q (x) I3)^T (MCONTACT.h:1045-1054)
-        const Csr QI = nodal_prolong(g, C.accuQ[b], doleMcsc[b], nullptr);
-        const Csr D = spgemm(transpose_csr(QI), spgemm(from_triplets(N3, m0, disp), F));
+        // dispUnba -> level-d free rows: C_d Q^T R^T (MCONTACT.h:1033-1035, 1068-1074)
+        const Csr QI = nodal_prolong(g, Qr[b], doleMcsc[b], nullptr);
+        const Csr D = spgemm(transpose_csr(QI), spgemm(rot_rows(g, from_triplets(N3, m0, disp)), F));
         std::vector<Trip>& out = coup_side[task];
         const int64_t cr = N + contReco[ts];
         for (int64_t r = 0; r < D.nrow; ++r)
@@ -588,15 +798,14 @@ void MCONTACT::MULTISCALE(const std::vector<uint8_t>* owned) {
             for (auto& v : C.globTran_pena_L[ts][tv].val) v *= itf.penN;
         } else
             C.globTran_pena_L[ts][tv] = place(from_triplets(m0, mv, tranp), mv);
-        C.globTran_D_L[ts][tv] = place(from_triplets(m0, N3, tranD), N3);
+        C.globTran_D_L[ts][tv] = place(rot_cols(g, from_triplets(m0, N3, tranD)), N3);
     }
     for (auto& t : coup_side) coup.insert(coup.end(), t.begin(), t.end());
     C.globCoup_1 = from_triplets(n, n, coup);
     C.globForc_1.assign(n, 0.0);
-    // accuProl[tv] = C_L (Q (x) I3) C_d^T (MCONTACT.h:864-872)
+    // accuProl[tv] = C_L P_{L-1} ... P_d C_d^T (MCONTACT.h:864-872)
     for (int64_t tv = 0; tv < nsub; ++tv)
-        C.accuProl_full.push_back(mine(tv) ? rows_to_free(multGrid[tv], nodal_prolong(multGrid[tv], C.accuQ[tv], doleMcsc[tv], nullptr))
-                                           : Csr());
+        C.accuProl_full.push_back(mine(tv) ? accu_prol(multGrid[tv], Qr[tv], doleMcsc[tv]) : Csr());
     C.ready = true;
     coarse = std::move(C);
 }

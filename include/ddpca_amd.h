@@ -354,6 +354,16 @@ int ddpca_multigrid_build(ddpca_multigrid_t g, const ddpca_csr_t* extra);
 int ddpca_multigrid_view(ddpca_multigrid_t g, const char* what, int64_t level, const void** data, int64_t* count,
                          int* dtype);
 int ddpca_problem_set_subdomain_multigrid(ddpca_problem_t p, int64_t tv, ddpca_multigrid_t g);
+/* The whole MCONTACT::ESTABLISH (MCONTACT.h:181-896) from element trees: subdomain tv of an empty
+ * problem (ddpca_problem_empty) takes a copy of the UNBUILT multigrid g (its tree and the inputs
+ * set with ddpca_multigrid_set: constraints, loads, rotations, coupled nodes, material);
+ * ddpca_problem_set_contact gives interface ts its bodies (contBody) and ddpca_problem_set_ips its
+ * integration points in node ids; ddpca_problem_set_coarse, then ddpca_problem_establish run the
+ * library's own pipeline: TRANSFER + PATCH (positions), the mortar operators with CONT_ROTA, STIF_MATR
+ * + systMass, CONSTRAINT(1), and MULTISCALE / MULTISCALE_1 on these general trees (the hanging level,
+ * prolOper's rotation blocks).  Afterwards the problem's arrays are in the position numbering. */
+int ddpca_problem_set_subdomain_tree(ddpca_problem_t p, int64_t tv, ddpca_multigrid_t g);
+int ddpca_problem_set_contact(ddpca_problem_t p, int64_t ts, int64_t body0, int64_t body1);
 int ddpca_multigrid_destroy(ddpca_multigrid_t g);
 /* Interface ts between contBody {body0, body1} with fricCoef fric (< 0 glued, 0 frictionless,
  * > 0 Coulomb; comp = 1 if fric == 0 else 3), nip integration points, nnc_s contact nodes per

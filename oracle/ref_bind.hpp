@@ -171,8 +171,9 @@ inline ddpca_multigrid_t tree_create(const MULTIGRID& g) {
     return h;
 }
 
-// the MULTIGRID's constraints, loads, rotations, coupled nodes and material onto an unbuilt handle, then build
-inline void tree_inputs(ddpca_multigrid_t h, const MULTIGRID& g, const SpMat* extra = nullptr) {
+// the MULTIGRID's constraints, loads, rotations, coupled nodes and material onto an unbuilt handle, then
+// build (build = false: leave it unbuilt for ddpca_problem_set_subdomain_tree)
+inline void tree_inputs(ddpca_multigrid_t h, const MULTIGRID& g, const SpMat* extra = nullptr, bool build = true) {
     std::vector<int64_t> idx;
     std::vector<double> val;
     auto put = [&](const char* what) {
@@ -197,6 +198,7 @@ inline void tree_inputs(ddpca_multigrid_t h, const MULTIGRID& g, const SpMat* ex
     check(ddpca_multigrid_set(h, "coupReps", 1, &reps, nullptr));
     const double mat[2] = {g.mateElas, g.matePois};
     check(ddpca_multigrid_set(h, "material", 2, nullptr, mat));
+    if (!build) return;
     if (extra) {
         const Csr e(*extra);
         const ddpca_csr_t v = e.view();

@@ -6,6 +6,10 @@ Tolerance: 1e-12 of each operator's largest entry (the triple products are summe
 different order than Eigen's); accuProl exactly.  The oracle run on the host-built operators
 reproduces the reference's converged ADMM trajectory (iteration count identical).
 """
+import json
+import subprocess
+from pathlib import Path
+
 import numpy as np
 import pytest
 
@@ -176,3 +180,37 @@ def test_latin_rank_local_build_matches_global(ddpca):
                         B = full.csr(name, 2 * ts + s)
                         assert abs(P.csr(name, 2 * ts + s) - B).max() <= 1e-12 * abs(B).max()
     assert np.abs(total - A).max() <= 1e-12 * np.abs(A).max()
+
+
+@pytest.mark.parametrize("args", [("cylinder", "2", "4", "2"), ("dehw", "2", "2", "0"), ("dehw", "2", "2", "7"),
+                                  ("dehw", "1", "2", "0"), ("dehw", "1", "2", "7")],
+                         ids=["cylinder-musc2", "dehw-general-musc2", "dehw-rotated-musc2", "dehw-general-musc1",
+                              "dehw-rotated-musc1"])
+def test_general_tree_coarse_space_matches_reference(tmp_path, args):
+    """Both coarse spaces on general trees -- the hanging level past maxiLeve (prolOper[maxiLeve]),
+    the nodal rotations' prolongation blocks and CONT_ROTA on the interface operators -- built by the
+    library's own ESTABLISH from element trees and integration points (ddpca_problem_set_subdomain_tree,
+    multiscale.cpp) against the reference's own MULTISCALE_1 / MULTISCALE on the same input
+    (oracle/ref_multiscale.cpp): globCoup(_1), globForc_1, globTran_1 or globTran / globTran_pena /
+    globTran_D per side, globTran_D_1 and accuProl per subdomain, and the mortar operators carrying
+    CONT_ROTA (systTran, systTran_pena, pemaInpo_r), each within 1e-12 of its largest entry.
+    cylinder-musc2: the reference's CYLINDER example (CYLINDER_1.h, locaLeve 4, globInho 2) with
+    muscSett = 2 set, run by its own SOLVE (18,336 hanging nodes, 34,323 coarse rows); dehw-*: the
+    library's DEHW-synthetic general mesh (bench.py --mesh general at gl 2: contact band refined once
+    more, rotated support nodes) handed to a reference MCONTACT; "rotated" also rotates every 7th node
+    of every body (contact and hanging nodes among them) on both sides."""
+    exe = Path(__file__).resolve().parents[1] / "oracle" / "_ref" / "ref_multiscale"
+    if not exe.exists():
+        pytest.skip("oracle/_ref/ref_multiscale is built where the reference is (oracle/Makefile)")
+    out = subprocess.run([str(exe), *args], capture_output=True, text=True, timeout=900, cwd=tmp_path)
+    lines = [json.loads(l) for l in out.stdout.splitlines() if l.startswith("{")]
+    assert out.returncode == 0 and lines and lines[-1]["ok"], (out.stdout[-3000:], out.stderr[-2000:])
+    res = lines[-1]
+    assert res["hanging_nodes"] > 0 and res["coarse_rows"] > 0, res
+    assert all(v <= 1e-12 for v in res["operators"].values()), res["operators"]
+    names = res["operators"].keys()
+    want = ["globCoup_1", "globForc_1", "globTran_1[0,0]", "globTran_D_1[0]"] if args[1] == "2" else \
+        ["globCoup", "globTran[0,0]", "globTran_pena[0,0]", "globTran_D[0,0]"]
+    assert all(w in names for w in want + ["accuProl[0]", "systTran[0,0]", "pemaInpo_r[0,0]"]), names
+    if args[0] == "dehw":
+        assert res["rotated_nodes"] > 0
