@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <climits>
+#include <cstdlib>
 #include <mutex>
 #include <cstdint>
 #include <string>
@@ -120,11 +121,20 @@ int64_t pace_halves(hipStream_t st[2], hipGraphExec_t g[2], const MirrorBuf& m, 
 // rocSOLVER / rocBLAS from several host threads of one process (the in-process ranks of the
 // multi-rank tests) gave non-deterministic potrf failures on the very same matrix (TORSION on 4
 // ranks, n = 3468: info 2229, then 1479, while every rank held the 1-rank matrix bit for bit,
-// profiles/r04b): the dense factorisations of one process take this lock.  A production rank is one
-// process with one factorisation at a time, so it serialises nothing there.
+// profiles/r04b): the dense factorisations of one process take this lock (DESIGN.md §7 has the
+// audit of our side of those setup paths).  A production rank is one process with one factorisation
+// at a time, so it serialises nothing there.  DDPCA_SOLVER_LOCK=0 turns it off: the concurrency test
+// (tests/test_mgpis_gpu.py::test_concurrent_dense_factorisations_bit_identical) runs that way.
 inline std::mutex& solver_mutex() {
     static std::mutex m;
     return m;
+}
+inline std::unique_lock<std::mutex> solver_lock() {
+    static const bool on = [] {
+        const char* e = std::getenv("DDPCA_SOLVER_LOCK");
+        return !(e && e[0] == '0');
+    }();
+    return on ? std::unique_lock<std::mutex>(solver_mutex()) : std::unique_lock<std::mutex>();
 }
 
 }  // namespace ddpca

@@ -2030,7 +2030,7 @@ void build_coarse(ddpca_mcontact& H, Problem& P) {
             const MULTIGRID& g = mc.multGrid[tv];
             const Csr& A = cs.accuProl_full[tv];
             std::vector<int64_t> f2d(g.freeCount.back(), -1);
-            for (int64_t d = 0; d < (int64_t)g.consFlag.size(); ++d)
+            for (int64_t d = 0; d < 3 * g.leveCount.back(); ++d)  // the fine level (not the hanging one)
                 if (g.freeIndex[d] >= 0) f2d[g.freeIndex[d]] = d;
                 else cd.push_back((int32_t)(H.subs[i].dof0 + d));
             for (int64_t r = 0; r < A.nrow; ++r) {
@@ -2138,7 +2138,7 @@ void build_coarse(ddpca_mcontact& H, Problem& P) {
                 htgt.push_back((int32_t)(H.subs[i].dof0 + dof));
             }
         }
-        for (int64_t dof = 0; dof < 3 * g.numNodes(); ++dof) flag[H.subs[i].dof0 + dof] = g.consFlag[dof];
+        for (int64_t dof = 0; dof < 3 * g.leveCount.back(); ++dof) flag[H.subs[i].dof0 + dof] = g.consFlag[dof];
     }
     C.npr = (int64_t)htgt.size();
     C.ncd = 0;
@@ -2207,7 +2207,7 @@ void coarse_invert(ddpca_mcontact& H) {
         const auto c = checksum(A.download());
         std::fprintf(stderr, "[ddpca] rank %d coarse matrix |.| %.17g w %.17g\n", H.rank, c.first, c.second);
     }
-    std::lock_guard<std::mutex> solver_lock(solver_mutex());
+    auto solver_guard = solver_lock();
     rocblas_handle rh = nullptr;
     if (rocblas_create_handle(&rh) != rocblas_status_success) throw ApiError(DDPCA_EHIP, "rocblas_create_handle");
     DevBuf<rocblas_int> info(2);

@@ -1019,7 +1019,7 @@ void invert_spd_device(std::vector<double>& A, int64_t n, hipStream_t st) {
     d.upload(A);
     DevBuf<rocblas_int> info(2);
     info.zero(st);
-    std::lock_guard<std::mutex> solver_lock(solver_mutex());
+    auto solver_guard = solver_lock();
     rocblas_handle h = nullptr;
     if (rocblas_create_handle(&h) != rocblas_status_success) throw ApiError(DDPCA_EHIP, "rocblas_create_handle");
     rocblas_set_stream(h, st);
@@ -1056,7 +1056,7 @@ bool inv_general_lu_device(std::vector<double>& A, int64_t n, hipStream_t st) {
     d.upload(A);
     DevBuf<rocblas_int> ipiv(std::max<int64_t>(n, 1)), info(2);
     info.zero(st);
-    std::lock_guard<std::mutex> solver_lock(solver_mutex());
+    auto solver_guard = solver_lock();
     rocblas_handle h = nullptr;
     if (rocblas_create_handle(&h) != rocblas_status_success) throw ApiError(DDPCA_EHIP, "rocblas_create_handle");
     rocblas_set_stream(h, st);
@@ -1092,7 +1092,7 @@ void pinv_general_device(std::vector<double>& A, int64_t n, hipStream_t st, int6
     d.upload(A);
     DevBuf<rocblas_int> info(1);
     info.zero(st);
-    std::lock_guard<std::mutex> solver_lock(solver_mutex());
+    auto solver_guard = solver_lock();
     rocblas_handle h = nullptr;
     if (rocblas_create_handle(&h) != rocblas_status_success) throw ApiError(DDPCA_EHIP, "rocblas_create_handle");
     rocblas_set_stream(h, st);

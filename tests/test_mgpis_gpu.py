@@ -162,3 +162,58 @@ def test_csr_dropin_matches_native(ddpca, gpu):
     assert abs(i1 - i2) <= 2
     assert np.linalg.norm(x1 - x2) <= 1e-10 * np.linalg.norm(x2)
     assert np.linalg.norm(x1 - g["x_mg"]) <= 1e-8 * np.linalg.norm(g["x_mg"])
+
+
+_CONCURRENT = r'''
+import importlib, json, sys, threading
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+D = importlib.import_module("ddpca-admm_amd")
+# one problem per thread (no host state shared), the whole fine level as the V-cycle's exact level:
+# a dense SPD inverse of 4,455 - 165 rows by rocSOLVER potrf + potri (device_mgpis.hip
+# invert_spd_device), the size class of the r04b failures (n = 3468)
+probs = [D.Problem("beam", 16, 4, 2, 1, 1, 1, 1).ESTABLISH() for _ in range(5)]
+n = len(probs[0].grid(0).consForc)
+r = np.random.default_rng(20251017).standard_normal(n)
+rounds = []
+for rnd in range(2):  # the first round starts cold (rocBLAS / Tensile kernels not loaded yet)
+    out, err = [None] * 4, [None] * 4
+    def work(i):
+        try:
+            M = D.MGPIS.from_problem(probs[i], 0, coarse_level=1)
+            out[i] = M.MULT_VCYC(r)
+        except Exception as e:
+            err[i] = repr(e)
+    ts = [threading.Thread(target=work, args=(i,)) for i in range(4)]
+    for t in ts: t.start()
+    for t in ts: t.join()
+    rounds.append((out, err))
+serial = D.MGPIS.from_problem(probs[4], 0, coarse_level=1).MULT_VCYC(r)
+res = {"n": n, "errors": [e for _, err in rounds for e in err if e],
+       "bit_identical": [[bool(o is not None and np.array_equal(o, serial)) for o in out] for out, _ in rounds],
+       "max_abs_diff": [[float(np.abs(o - serial).max()) if o is not None else None for o in out] for out, _ in rounds]}
+print(json.dumps(res))
+'''
+
+
+def test_concurrent_dense_factorisations_bit_identical(ddpca, gpu, tmp_path):
+    """Four host threads of one fresh process factorise the same dense SPD matrix at once -- each its
+    own MGPIS handle whose exact level is the whole fine level (potrf + potri by rocSOLVER on its own
+    stream and rocBLAS handle, invert_spd_device), with the process-wide solver lock OFF
+    (DDPCA_SOLVER_LOCK=0) -- twice (the first round with rocBLAS cold).  Every thread's A^-1 r (the
+    V-cycle of that handle) must equal a serial handle's bit for bit: the r04b failures were potrf
+    info 1479 / 2229 on bit-identical input under 4 in-process ranks (DESIGN.md §7)."""
+    import json
+    import os
+    import subprocess
+    import sys
+    from pathlib import Path
+    root = str(Path(__file__).resolve().parents[1])
+    env = dict(os.environ, DDPCA_SOLVER_LOCK="0")
+    p = subprocess.run([sys.executable, "-c", _CONCURRENT, root], capture_output=True, text=True, timeout=300, env=env)
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert p.returncode == 0 and lines, (p.stdout[-2000:], p.stderr[-3000:])
+    res = json.loads(lines[-1])
+    print(f"concurrent potrf/potri, n = {res['n']}: {res}")
+    assert not res["errors"], res
+    assert all(all(r) for r in res["bit_identical"]), res
