@@ -26,6 +26,7 @@ import argparse
 import importlib
 import json
 import os
+import subprocess
 import sys
 import time
 from pathlib import Path
@@ -352,9 +353,17 @@ def cpu_baseline(P, mc, budget_s=20.0):
     measured ratio of the reference's own CG_SOLV (oracle/_ref/ref_harness_portable, compiled from
     /root/reference's headers) to the port on the same BEAM mesh (profiles/cpu_calibration.py),
     timed ON THE GPU HOST at its 16 threads (profiles/r03_cpu_calibration_host.json); the
-    container's 8-thread ratio is the fallback."""
+    container's 8-thread ratio is the fallback.  `reference_measured` is the reference's own
+    CG_SOLV(1) (MGPIS.h:163-225) timed on this host on a wheel's and a worm's operators at the same
+    state (oracle/_ref/ref_harness_portable time_cg_ops), the rest of the iteration by the port."""
     from oracle import cpu_admm
-    res = cpu_admm.price_iteration(P, mc, budget_s)
+    exe = ROOT / "oracle" / "_ref" / "ref_harness_portable"
+    try:
+        res = cpu_admm.price_iteration(P, mc, budget_s, ref_exe=exe if exe.exists() else None)
+    except (RuntimeError, OSError, ValueError, subprocess.TimeoutExpired) as e:  # the reference leg only
+        print(f"[cpu_baseline] reference CG_SOLV leg failed: {e}", file=sys.stderr, flush=True)
+        res = cpu_admm.price_iteration(P, mc, budget_s)
+        res["reference_measured"] = {"error": str(e)[-300:]}
     cal = ROOT / "profiles" / "r03_cpu_calibration_host.json"
     if not cal.exists():
         cal = ROOT / "profiles" / "r02_cpu_calibration.json"

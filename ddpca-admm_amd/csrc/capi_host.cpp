@@ -40,6 +40,15 @@ std::vector<std::array<int64_t, 4>> plane_faces(const MULTIGRID& g, int axis, in
     return out;
 }
 
+// A conforming interface pairs every face of one side with a face of the other: the same count on
+// both sides of the plane, and (checked per face below) a mate for every slave face -- otherwise
+// the interface would silently lose integration points.
+void check_face_match(size_t nm, size_t ns, int axis) {
+    if (nm == 0 || nm != ns)
+        throw std::invalid_argument("conforming interface on axis " + std::to_string(axis) + ": " + std::to_string(nm) +
+                                    " master faces vs " + std::to_string(ns) + " slave faces");
+}
+
 // Conforming interface on a shared lattice plane: master faces of body m, slave faces of body
 // s; integration points in CONTACT_SEARCH order (slave segments, CSEARCH.h:777-817).
 void conforming_interface(const MULTIGRID& gm, const MULTIGRID& gs, int axis, int64_t value,
@@ -51,10 +60,12 @@ void conforming_interface(const MULTIGRID& gm, const MULTIGRID& gs, int axis, in
         return k;
     };
     std::map<std::array<std::array<int64_t, 3>, 4>, std::array<int64_t, 4>> mast;
-    for (const auto& f : plane_faces(gm, axis, value)) mast.emplace(key(gm, f), f);
-    for (const auto& f : plane_faces(gs, axis, value)) {
+    const auto mf = plane_faces(gm, axis, value), sf = plane_faces(gs, axis, value);
+    for (const auto& f : mf) mast.emplace(key(gm, f), f);
+    check_face_match(mf.size(), sf.size(), axis);
+    for (const auto& f : sf) {
         auto it = mast.find(key(gs, f));
-        if (it == mast.end()) continue;
+        if (it == mast.end()) throw std::invalid_argument("conforming interface: a slave face without its master face");
         conforming_face_ips(gm, it->second.data(), gs, f.data(), ips, sub);
     }
 }
@@ -88,10 +99,12 @@ void conforming_interface_xyz(const MULTIGRID& gm, const MULTIGRID& gs, int axis
         return k;
     };
     std::map<std::array<std::array<int64_t, 3>, 4>, std::array<int64_t, 4>> mast;
-    for (const auto& f : plane_faces_xyz(gm, axis, value)) mast.emplace(key(gm, f), f);
-    for (const auto& f : plane_faces_xyz(gs, axis, value)) {
+    const auto mf = plane_faces_xyz(gm, axis, value), sf = plane_faces_xyz(gs, axis, value);
+    for (const auto& f : mf) mast.emplace(key(gm, f), f);
+    check_face_match(mf.size(), sf.size(), axis);
+    for (const auto& f : sf) {
         auto it = mast.find(key(gs, f));
-        if (it == mast.end()) continue;
+        if (it == mast.end()) throw std::invalid_argument("conforming interface: a slave face without its master face");
         conforming_face_ips(gm, it->second.data(), gs, f.data(), ips, sub);
     }
 }
@@ -162,12 +175,19 @@ void make_beam(Problem& P, const double* q) {
                     plane[ts] = {2, (t2 + 1) * real[2] * scale, 0};
                 }
             }
+    std::vector<std::exception_ptr> err(P.mc.searCont.size());
 #pragma omp parallel for schedule(dynamic, 1)
     for (int64_t ts = 0; ts < (int64_t)P.mc.searCont.size(); ++ts) {
         Interface& itf = P.mc.searCont[ts];
         itf.fric = -1.0;
-        conforming_interface(P.mc.multGrid[itf.body[0]], P.mc.multGrid[itf.body[1]], (int)plane[ts][0], plane[ts][1], itf.ip);
+        try {
+            conforming_interface(P.mc.multGrid[itf.body[0]], P.mc.multGrid[itf.body[1]], (int)plane[ts][0], plane[ts][1], itf.ip);
+        } catch (...) {
+            err[ts] = std::current_exception();
+        }
     }
+    for (auto& e : err)
+        if (e) std::rethrow_exception(e);
     set_penalty(P);
 }
 
@@ -293,8 +313,10 @@ void make_dehw(Problem& P, const double* q, int nq) {
             P.mc.searCont[ts].fric = -1.0;
             plane[ts] = {0, (g + 1) * n[0] * scale};
         }
+    std::vector<std::exception_ptr> err(nint);
 #pragma omp parallel for schedule(dynamic, 1)
     for (int64_t ts = 0; ts < nint; ++ts) {
+      try {
         Interface& itf = P.mc.searCont[ts];
         const int k = ts < G ? kc : kg;
         if (band) {
@@ -308,7 +330,12 @@ void make_dehw(Problem& P, const double* q, int nq) {
             conforming_interface(P.mc.multGrid[itf.body[0]], P.mc.multGrid[itf.body[1]], (int)plane[ts][0], plane[ts][1],
                                  itf.ip, 1 << k);
         }
+      } catch (...) {
+        err[ts] = std::current_exception();
+      }
     }
+    for (auto& e : err)
+        if (e) std::rethrow_exception(e);
     set_penalty(P);
 }
 

@@ -32,6 +32,7 @@ struct ddpca_lagrange {
     LagrangeResult res;
     std::vector<double> solver_relres;   // per Newton step: BiCGSTAB's ||r|| / ||b|| at exit
     std::vector<double> solver_brk;      // per Newton step: 0, 1 (rho = 0), 2 (attainable-accuracy stop)
+    std::vector<double> coarse_inv;      // per Newton step: coarse inverse kind (1 LU, 2 SVD), LU residual, dropped
     bool solved = false;
 };
 
@@ -64,7 +65,8 @@ Csr csr_in(const ddpca_csr_t& m, const char* what) {
 // BiCGSTAB on the device for one Newton step's system (levels lo..L of the hierarchy)
 // relres / brk: the solve's ||r|| / ||b|| and breakdown code (1 rho = 0, 2 attainable-accuracy stop)
 int64_t device_solve(int device, int prec_type, const mgpis_options_t& o, const std::vector<LagrangeSub>& subs,
-                     const LagrangeSystem& sys, std::vector<double>& x, double& relres, int& brk) {
+                     const LagrangeSystem& sys, std::vector<double>& x, double& relres, int& brk,
+                     std::vector<double>& coarse_inv) {
     const int L = (int)sys.K.size() - 1;
     const int lo = prec_type == 1 ? 0 : L;
     const int nl = L - lo + 1;
@@ -116,6 +118,8 @@ int64_t device_solve(int device, int prec_type, const mgpis_options_t& o, const 
     oo.warm_start = 0;
     // precType 2 runs the diagonal preconditioner only: no dense coarse pseudo-inverse
     MgpisDevice D(device, std::vector<SubdomainOps>{ops}, oo, true, prec_type != 1);
+    for (const auto& c : D.coarse_inverse) coarse_inv.insert(coarse_inv.end(), {(double)c.kind, c.resid, (double)c.dropped});
+    if (D.coarse_inverse.empty()) coarse_inv.insert(coarse_inv.end(), {-1.0, 0.0, 0.0});  // diagonal preconditioner
     // the device's condensed order is increasing nodal dof; the hierarchy's is subdomain-major
     const int64_t n = (int64_t)fd[L].size();
     if (D.nfree[0] != n) throw ApiError(DDPCA_ESTATE, "LAGRANGE: device dof count");
@@ -261,11 +265,12 @@ int64_t ddpca_lagrange_solve(ddpca_lagrange_t h, int device, int prec_type, cons
         std::vector<LagrangeItf> itfs = h->itfs;
         h->solver_relres.clear();
         h->solver_brk.clear();
+        h->coarse_inv.clear();
         try {
             h->res = run_lagrange(subs, itfs, max_newton, [&](const LagrangeSystem& sys, std::vector<double>& x) {
                 double relres = 0.0;
                 int brk = 0;
-                const int64_t it = device_solve(device, prec_type, o, subs, sys, x, relres, brk);
+                const int64_t it = device_solve(device, prec_type, o, subs, sys, x, relres, brk, h->coarse_inv);
                 h->solver_relres.push_back(relres);
                 h->solver_brk.push_back((double)brk);
                 // a Newton step must not continue from a solve that did not converge: the
@@ -312,6 +317,7 @@ int64_t ddpca_lagrange_get(ddpca_lagrange_t h, const char* what, int64_t index, 
         else if (w == "changes") n = copy_out(r.changes, out, cap);
         else if (w == "solver_relres") n = copy_out(h->solver_relres, out, cap);
         else if (w == "solver_breakdown") n = copy_out(h->solver_brk, out, cap);
+        else if (w == "coarse_inverse") n = copy_out(h->coarse_inv, out, cap);
         else throw ApiError(DDPCA_EINVAL, "unknown quantity: " + w);
     });
     return rc != 0 ? rc : n;

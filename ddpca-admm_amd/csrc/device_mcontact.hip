@@ -1059,7 +1059,7 @@ struct CoarseDev {
     bool on = false, inverted = false;
     int64_t n = 0, nown = 0, nxn = 0, qnn = 0;
     double dense_bytes = 0.0;  // n^2 8 B: what the dense inverse would hold per rank
-    bool mg_fallback = false;  // the memory budget asked for DOUBLE_M, its hierarchy was not buildable
+    bool mg_fallback = false;  // (kept for the "coarse_solve" getter: DOUBLE_M is always buildable now)
     DevBuf<double> g, f0, xc, xn, ainv;
     DevBuf<int64_t> rptr;
     DevBuf<int32_t> rcol;
@@ -1090,6 +1090,18 @@ struct CoarseDev {
     // 1857-1865): the coarse problem solved by its own MGPIS-PCG, redundantly on every rank, on a
     // hierarchy whose transfers are every subdomain's realProl below doleMcsc, block-diagonal
     bool mg = false;
+    bool mg_gather = false;  // a rank-local build: the whole operator is gathered at coarse_invert
+    // the coarse MGPIS's structure (plan_coarse_mg, at setup): nodes per level, transfers, the
+    // coarse rows' dofs, per-level dof flags; kept until the operator is there (finish_coarse_mg)
+    struct MgPlan {
+        std::vector<int64_t> nglob;
+        std::vector<Stencil> S;
+        std::vector<int32_t> fdg;
+        std::vector<std::vector<uint8_t>> flev;
+        bool latin = false;
+        void swap_into(MgPlan& o) { std::swap(*this, o); }
+    } plan;
+    Csr gathered_rows;  // this rank's rows of a rank-local operator (sent once at coarse_invert)
     std::unique_ptr<MgpisDevice> cmg;
     DevBuf<int32_t> cperm;  // coarse row -> dof of cmg's fine level (device layout)
     DevBuf<int32_t> cown;   // xc index -> coarse row
@@ -1759,20 +1771,20 @@ void build(ddpca_mcontact& H, Problem& P) {
 // level 0), and the level operators are Galerkin products.  Nodes are numbered so that every level
 // is a prefix of the next (the layout MgpisDevice takes): level l = level l-1's nodes, then the new
 // nodes of every subdomain in order.  Needs every subdomain's coarse rows on this rank.
-void build_coarse_mg(ddpca_mcontact& H, const MCONTACT& mc, CoarseDev& C) {
+void plan_coarse_mg(const MCONTACT& mc, CoarseDev& C) {
     const CoarseSpace& cs = mc.coarse;
     const int64_t nsub = (int64_t)mc.multGrid.size(), n = C.n;
-    for (int64_t tv = 0; tv < nsub; ++tv)
-        if (!cs.built[tv])
-            throw ApiError(DDPCA_ESTATE, "DOUBLE_M coarse solve: every subdomain's rows of globCoup_1 are needed on each rank "
-                                         "(a single-rank run or the caller's full MULTISCALE_1 output)");
+    CoarseDev::MgPlan& PL = C.plan;
     const int64_t Lc = *std::max_element(mc.doleMcsc.begin(), mc.doleMcsc.end());
     auto lev = [&](int64_t tv, int64_t l) { return std::max<int64_t>(0, mc.doleMcsc[tv] - (Lc - l)); };
     std::vector<std::vector<std::vector<int64_t>>> gid(Lc + 1, std::vector<std::vector<int64_t>>(nsub));
     // LATIN (DOUBLE_M, MCONTACT.h:1538-1670): the coarse contact unknowns of every interface are a
     // group of their own -- at level Lc the level-doleMcsc nodes coarNode[ts] of contBody[ts][0],
     // one level down the columns its scalProl rows touch (ficoCotr), comp unknowns per node
-    // (the node's first dof for frictionless contact)
+    // (the node's first dof for frictionless contact).  The sets need not be nested: a node of
+    // level l - 1 that level l does not carry (stacked bodies: BLOCK) keeps the prefix layout as a
+    // masked copy on level l and above (per-level dof flags, SubdomainOps::dof_free_lev) -- the
+    // masked transfer C_l P C_{l-1}^T then is the reference's ficoCotr
     const int64_t nint = cs.latin ? (int64_t)mc.searCont.size() : 0;
     if (cs.latin && (int64_t)cs.coarNode.size() != nint)
         throw ApiError(DDPCA_EINVAL, "DOUBLE_M for the LATIN coarse space needs the coarse contact nodes (coarNode)");
@@ -1787,18 +1799,15 @@ void build_coarse_mg(ddpca_mcontact& H, const MCONTACT& mc, CoarseDev& C) {
                 cset[l - 1][ts] = cset[l][ts];
                 continue;
             }
-            const Stencil& Sp = g.scalProl[fl - 1];
-            if (!Sp.bent.empty()) throw ApiError(DDPCA_EINVAL, "DOUBLE_M coarse solve with rotated-node transfers");
+            const Stencil& Sp = g.scalProl[fl - 1];  // scalar, no rotations (MCONTACT.h:1553)
+            if (!Sp.bent.empty())
+                throw ApiError(DDPCA_EINVAL, "LATIN DOUBLE_M: ficoCotr needs the scalar scalProl (a caller's rotated realProl has none)");
             std::vector<int64_t> cols;
             for (int64_t f : cset[l][ts])
                 for (int64_t k = Sp.ptr[f]; k < Sp.ptr[f + 1]; ++k) cols.push_back(Sp.col[k]);
             std::sort(cols.begin(), cols.end());
             cols.erase(std::unique(cols.begin(), cols.end()), cols.end());
             cset[l - 1][ts] = cols;
-            // the hierarchy keeps each level's nodes on the next (MgpisDevice's prefix layout)
-            for (int64_t c : cols)
-                if (!std::binary_search(cset[l][ts].begin(), cset[l][ts].end(), c))
-                    throw ApiError(DDPCA_EINVAL, "DOUBLE_M: a coarse contact node is not a contact node of the finer level");
         }
     }
     std::vector<std::unordered_map<int64_t, int64_t>> cg(nint);  // (interface, node) -> global node
@@ -1824,13 +1833,25 @@ void build_coarse_mg(ddpca_mcontact& H, const MCONTACT& mc, CoarseDev& C) {
     for (int64_t l = 1; l <= Lc; ++l) {
         std::vector<std::vector<std::pair<int32_t, double>>> rows(nglob[l]);
         for (int64_t i = 0; i < nglob[l - 1]; ++i) rows[i].push_back({(int32_t)i, 1.0});
+        std::vector<std::vector<std::array<double, 9>>> rblk(nglob[l]);  // block entries, parallel to rows (NaN-free marker below)
         for (int64_t tv = 0; tv < nsub; ++tv) {
             if (lev(tv, l) == lev(tv, l - 1)) continue;  // identity (MCONTACT.h:2325-2331)
-            const Stencil& Sp = mc.multGrid[tv].scalProl[lev(tv, l - 1)];
-            if (!Sp.bent.empty()) throw ApiError(DDPCA_EINVAL, "DOUBLE_M coarse solve with rotated-node transfers");
+            // the subdomain's realProl at that level (MCONTACT.h:1632, 2316): prolOper's rotation
+            // blocks as block entries (a caller's operator-level stencil carries them in scalProl)
+            const MULTIGRID& g = mc.multGrid[tv];
+            const Stencil& Sp = g.prolOper.empty() ? g.scalProl[lev(tv, l - 1)] : g.prolOper[lev(tv, l - 1)];
+            std::vector<int64_t> bo(Sp.col.size(), -1);
+            for (size_t q = 0; q < Sp.bent.size(); ++q) bo[Sp.bent[q]] = (int64_t)q;
             for (int64_t j = (int64_t)gid[l - 1][tv].size(); j < (int64_t)gid[l][tv].size(); ++j)
-                for (int64_t k = Sp.ptr[j]; k < Sp.ptr[j + 1]; ++k)
-                    rows[gid[l][tv][j]].push_back({(int32_t)gid[l - 1][tv][Sp.col[k]], Sp.w[k]});
+                for (int64_t k = Sp.ptr[j]; k < Sp.ptr[j + 1]; ++k) {
+                    const int64_t r = gid[l][tv][j];
+                    rows[r].push_back({(int32_t)gid[l - 1][tv][Sp.col[k]], Sp.w[k]});
+                    std::array<double, 9> b;
+                    if (bo[k] >= 0) std::copy(&Sp.bval[9 * bo[k]], &Sp.bval[9 * bo[k]] + 9, b.begin());
+                    else b[0] = std::numeric_limits<double>::quiet_NaN();  // scalar entry
+                    rblk[r].resize(rows[r].size());
+                    rblk[r].back() = b;
+                }
         }
         for (int64_t ts = 0; ts < nint; ++ts) {  // ficoCotr rows of the nodes new on level l
             const int64_t b0 = mc.searCont[ts].body[0];
@@ -1847,10 +1868,15 @@ void build_coarse_mg(ddpca_mcontact& H, const MCONTACT& mc, CoarseDev& C) {
         T.nf = nglob[l];
         T.nc = nglob[l - 1];
         T.ptr.assign(1, 0);
-        for (const auto& r : rows) {
-            for (const auto& e : r) {
-                T.col.push_back(e.first);
-                T.w.push_back(e.second);
+        for (int64_t r = 0; r < nglob[l]; ++r) {
+            for (size_t q = 0; q < rows[r].size(); ++q) {
+                const bool blk = q < rblk[r].size() && !std::isnan(rblk[r][q][0]);
+                if (blk) {
+                    T.bent.push_back((int64_t)T.col.size());
+                    T.bval.insert(T.bval.end(), rblk[r][q].begin(), rblk[r][q].end());
+                }
+                T.col.push_back(rows[r][q].first);
+                T.w.push_back(blk ? 0.0 : rows[r][q].second);
             }
             T.ptr.push_back((int64_t)T.col.size());
         }
@@ -1874,26 +1900,59 @@ void build_coarse_mg(ddpca_mcontact& H, const MCONTACT& mc, CoarseDev& C) {
         }
         if (r != n) throw ApiError(DDPCA_EINVAL, "DOUBLE_M: coarse contact unknowns do not match the coarse rows");
     }
+    // per-level dof flags: a subdomain node's dofs as its consOper (the prefix of its flags), a
+    // contact unknown's comp dofs free on the levels that carry it, its masked copies none
+    std::vector<std::vector<uint8_t>> flev(Lc + 1);
+    for (int64_t l = 0; l <= Lc; ++l) {
+        auto& f = flev[l];
+        f.assign(3 * nglob[l], 0);
+        for (int64_t tv = 0; tv < nsub; ++tv) {
+            const MULTIGRID& g = mc.multGrid[tv];
+            for (size_t j = 0; j < gid[l][tv].size(); ++j)
+                for (int a = 0; a < 3; ++a) f[3 * gid[l][tv][j] + a] = g.consFlag[3 * j + a];
+        }
+        for (int64_t ts = 0; ts < nint; ++ts) {
+            const int comp = mc.searCont[ts].comp();
+            for (int64_t node : cset[l][ts])
+                for (int j = 0; j < comp; ++j) f[3 * cg[ts].at(node) + j] = 1;
+        }
+    }
+    for (int32_t d : fdg)
+        if (!flev[Lc][d]) throw ApiError(DDPCA_EINVAL, "DOUBLE_M: a coarse row on a constrained dof");
+    PL.nglob = std::move(nglob);
+    PL.S = std::move(S);
+    PL.fdg = std::move(fdg);
+    PL.flev = std::move(flev);
+    PL.latin = cs.latin;
+}
+
+// The coarse MGPIS from the plan and the whole coarse operator A (globCoup_1 / globCoup):
+// K[Lc] = A on the hierarchy's fine level, the levels below Galerkin products (MCONTACT.h:
+// 1664-1665, 2337-2338)
+void finish_coarse_mg(ddpca_mcontact& H, CoarseDev& C, const Csr& A) {
+    CoarseDev::MgPlan& PL = C.plan;
+    const int64_t n = C.n, Lc = (int64_t)PL.nglob.size() - 1;
+    if (A.nrow != n || A.ncol != n) throw ApiError(DDPCA_EINVAL, "DOUBLE_M coarse solve: the whole coarse operator is needed");
     std::vector<Bsr3> K(Lc + 1);
-    K[Lc] = condensed_to_bsr3(nglob[Lc], n, fdg.data(), cs.globCoup_1.ptr.data(), cs.globCoup_1.col.data(),
-                              cs.globCoup_1.val.data());
-    for (int64_t l = Lc - 1; l >= 0; --l) K[l] = galerkin_rap(K[l + 1], S[l]);  // MCONTACT.h:2337-2338, 1664-1665
-    std::vector<uint8_t> flag(3 * nglob[Lc], 0);
-    for (int32_t d : fdg) flag[d] = 1;
+    K[Lc] = condensed_to_bsr3(PL.nglob[Lc], n, PL.fdg.data(), A.ptr.data(), A.col.data(), A.val.data());
+    for (int64_t l = Lc - 1; l >= 0; --l) K[l] = galerkin_rap(K[l + 1], PL.S[l]);
     SubdomainOps o;
-    o.nnodes = nglob;
+    o.nnodes = PL.nglob;
     for (const auto& k : K) o.K.push_back(&k);
-    for (const auto& s : S) o.S.push_back(&s);
-    o.dof_free = flag.data();
+    for (const auto& s : PL.S) o.S.push_back(&s);
+    o.dof_free = PL.flev[Lc].data();
+    for (const auto& f : PL.flev) o.dof_free_lev.push_back(f.data());
     C.cmg = std::make_unique<MgpisDevice>(H.device, std::vector<SubdomainOps>{o}, H.opt);
     std::vector<int32_t> perm(n), own(C.own_rows.begin(), C.own_rows.end());
-    for (int64_t r = 0; r < n; ++r) perm[r] = (int32_t)C.cmg->fine_dof(0, fdg[r]);
+    for (int64_t r = 0; r < n; ++r) perm[r] = (int32_t)C.cmg->fine_dof(0, PL.fdg[r]);
     C.cperm.upload(perm);
     C.cown.upload(own.empty() ? std::vector<int32_t>{0} : own);
     DDPCA_HIP(hipEventCreateWithFlags(&C.ev_in, hipEventDisableTiming));
     DDPCA_HIP(hipEventCreateWithFlags(&C.ev_out, hipEventDisableTiming));
     if (std::getenv("DDPCA_VERBOSE"))
-        std::fprintf(stderr, "[ddpca] DOUBLE_M%s coarse solve: %ld rows, %ld levels\n", cs.latin ? "" : "_1", (long)n, (long)(Lc + 1));
+        std::fprintf(stderr, "[ddpca] DOUBLE_M%s coarse solve: %ld rows, %ld levels%s\n", PL.latin ? "" : "_1", (long)n,
+                     (long)(Lc + 1), C.mg_gather ? " (operator gathered from every rank)" : "");
+    CoarseDev::MgPlan().swap_into(PL);
 }
 
 // ---- coarse space: device operands from the host MULTISCALE_1 output
@@ -1980,28 +2039,27 @@ void build_coarse(ddpca_mcontact& H, Problem& P) {
     const char* dense_env = std::getenv("DDPCA_COARSE_DENSE_MB");
     const double dense_max = (dense_env ? std::atof(dense_env) : 1024.0) * 1048576.0;
     C.dense_bytes = 8.0 * (double)n * (double)n;
-    // LATIN: DOUBLE_M (MCONTACT.h:1236) with the host MULTISCALE's coarse contact nodes, one rank
-    const bool mg_ok = !cs.latin || (!cs.rank_local && !cs.coarNode.empty());
+    // LATIN: DOUBLE_M (MCONTACT.h:1236) on the coarse contact nodes (the host MULTISCALE's, or the
+    // caller's through ddpca_problem_set_coarse_nodes)
+    if (cs.latin && cs.coarNode.empty() && (n >= (mg_env ? std::atoll(mg_env) : 120000) || C.dense_bytes > dense_max))
+        throw ApiError(DDPCA_EINVAL, "LATIN coarse space past the dense solve's limits needs its coarse contact nodes "
+                                     "(ddpca_problem_set_coarse_nodes) for DOUBLE_M");
     const bool by_rows = n >= (mg_env ? std::atoll(mg_env) : 120000);
-    // the budget alone switches LATIN's DOUBLE_M on one rank only: its hierarchy may not be
-    // buildable (below), and the fallback to the dense solve must be the same on every rank (the
-    // dense matrix is summed by a collective), which a rank without owned rows cannot decide
-    const bool by_budget = C.dense_bytes > dense_max && (!cs.latin || H.nranks == 1 || n > 46000);
-    C.mg = (by_rows || by_budget) && mg_ok;
+    const bool by_budget = C.dense_bytes > dense_max;  // the same decision on every rank: n is global
+    C.mg = by_rows || by_budget;
     C.latin = cs.latin;
-    if (C.mg && H.mg && C.nown) {
-        try {
-            build_coarse_mg(H, mc, C);
-        } catch (const ApiError& e) {
-            // LATIN's DOUBLE_M hierarchy needs the coarse contact nodes nested level by level; where
-            // they are not (BLOCK's stacked bodies), a one-rank handle that chose the multigrid
-            // solve for memory alone keeps the dense inverse (the reference: LDLT below DIRE_MAXI)
-            if (by_rows || !cs.latin || H.nranks > 1 || n > 46000) throw;
-            C.cmg.reset();
-            C.mg = false;
-            C.mg_fallback = true;
-            if (std::getenv("DDPCA_VERBOSE")) std::fprintf(stderr, "[ddpca] DOUBLE_M not built (%s): dense coarse inverse\n", e.what());
-        }
+    // the multigrid hierarchy needs the whole coarse operator: a caller's full operator or a
+    // single-rank build has it; a rank-local build gathers it from every rank once the transport
+    // exists (coarse_invert)
+    bool full = !cs.rank_local;
+    for (int64_t tv = 0; tv < (int64_t)cs.built.size(); ++tv) full = full && cs.built[tv];
+    if (C.mg && !full && H.nranks == 1)
+        throw ApiError(DDPCA_ESTATE, "DOUBLE_M coarse solve: a single rank without every subdomain's coarse rows");
+    C.mg_gather = C.mg && !full;
+    if (C.mg && H.mg) {
+        plan_coarse_mg(mc, C);
+        if (!C.mg_gather) finish_coarse_mg(H, C, cs.globCoup_1);
+        else C.gathered_rows = cs.globCoup_1;  // this rank's rows (its share of the contact rows)
     }
     // coarse solve: the owned rows of the dense inverse against g, or (DOUBLE_M) g scattered into
     // the coarse MGPIS and its owned rows gathered back (its PCG is counted by its own model)
@@ -2180,6 +2238,53 @@ void coarse_invert(ddpca_mcontact& H) {
     CoarseDev& C = H.cs;
     if (!C.on || C.inverted) return;
     if (C.mg) {  // DOUBLE_M: nothing to factorise (the same decision on every rank: n is global)
+        if (C.mg_gather) {
+            // a rank-local build: every rank's rows (the LATIN contact rows as per-rank shares) as
+            // (row, col, value) triplets, all-gathered by two all-reduces (the counts, then each
+            // rank's triplets in its own slot); duplicates summed
+            if (!H.comm) throw ApiError(DDPCA_ESTATE, "the DOUBLE_M coarse solve of a multi-rank run needs mcontact_gpu_comm_init");
+            const Csr& M = C.gathered_rows;
+            std::vector<double> cnt(H.nranks, 0.0);
+            cnt[H.rank] = (double)M.nnz();
+            DevBuf<double> dc;
+            dc.upload(cnt);
+            H.comm->allreduce_sum(dc.p, H.nranks, H.main);
+            DDPCA_HIP(hipStreamSynchronize(H.main));
+            cnt = dc.download();
+            std::vector<int64_t> off(H.nranks + 1, 0);
+            for (int r = 0; r < H.nranks; ++r) off[r + 1] = off[r] + (int64_t)cnt[r];
+            std::vector<double> trip(3 * off[H.nranks], 0.0);
+            for (int64_t r = 0, q = off[H.rank]; r < M.nrow; ++r)
+                for (int64_t k = M.ptr[r]; k < M.ptr[r + 1]; ++k, ++q) {
+                    trip[3 * q] = (double)r;
+                    trip[3 * q + 1] = (double)M.col[k];
+                    trip[3 * q + 2] = M.val[k];
+                }
+            DevBuf<double> dt;
+            dt.upload(trip);
+            H.comm->allreduce_sum(dt.p, (int64_t)trip.size(), H.main);
+            DDPCA_HIP(hipStreamSynchronize(H.main));
+            trip = dt.download();
+            std::vector<std::vector<std::pair<int32_t, double>>> rows(C.n);
+            for (int64_t q = 0; q < off[H.nranks]; ++q) rows[(int64_t)trip[3 * q]].push_back({(int32_t)trip[3 * q + 1], trip[3 * q + 2]});
+            Csr A;
+            A.nrow = A.ncol = C.n;
+            A.ptr.assign(1, 0);
+            for (auto& row : rows) {
+                std::stable_sort(row.begin(), row.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
+                for (size_t k = 0; k < row.size();) {
+                    size_t e = k;
+                    double v = 0.0;
+                    for (; e < row.size() && row[e].first == row[k].first; ++e) v += row[e].second;
+                    A.col.push_back(row[k].first);
+                    A.val.push_back(v);
+                    k = e;
+                }
+                A.ptr.push_back((int64_t)A.col.size());
+            }
+            C.gathered_rows = Csr();
+            if (!C.plan.nglob.empty()) finish_coarse_mg(H, C, A);
+        }
         C.inverted = true;
         return;
     }

@@ -1047,13 +1047,27 @@ __global__ void k_diag(const double* A, int64_t n, double* d) {
     if (i < n) d[i] = A[i * n + i];
 }
 
+// row sums of |M - I| (M column-major n x n): the residual of an inverse read as M = A^-1 A
+__global__ void k_resid_rows(const double* M, int64_t n, double* r) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    double s = 0.0;
+    for (int64_t i = 0; i < n; ++i) s += std::abs(M[i * n + j] - (i == j ? 1.0 : 0.0));
+    r[j] = s;
+}
+
 // In-place inverse of a dense general matrix by rocSOLVER getrf + getri when its LU is clearly
-// regular (every |U_ii| above 1e-10 of the largest); returns false, A untouched, otherwise.  The
+// regular (every |U_ii| above 1e-10 of the largest) and the inverse checks out (||A^-1 A - I||_inf
+// <= kLuMaxResid by a rocBLAS gemm against the kept copy of A); returns false, A untouched,
+// otherwise, and *resid the residual it measured (INFINITY when the pivot test failed).  The
 // column-major view of the row-major buffer is A^T, whose inverse read back row-major is A^-1.
 // (LAGRANGE's condensed coarse operators, 4851 rows at BLOCK: ~20 s per Newton step by gesvd.)
-bool inv_general_lu_device(std::vector<double>& A, int64_t n, hipStream_t st) {
-    DevBuf<double> d, diag(std::max<int64_t>(n, 1));
+constexpr double kLuMaxResid = 1e-6;
+bool inv_general_lu_device(std::vector<double>& A, int64_t n, hipStream_t st, double* resid) {
+    *resid = INFINITY;
+    DevBuf<double> d, a0, diag(std::max<int64_t>(n, 1));
     d.upload(A);
+    a0.upload(A);
     DevBuf<rocblas_int> ipiv(std::max<int64_t>(n, 1)), info(2);
     info.zero(st);
     auto solver_guard = solver_lock();
@@ -1074,9 +1088,21 @@ bool inv_general_lu_device(std::vector<double>& A, int64_t n, hipStream_t st) {
         return false;
     }
     const rocblas_status s2 = rocsolver_dgetri(h, (rocblas_int)n, d.p, (rocblas_int)n, ipiv.p, info.p + 1);
+    // column-major: d = (A^T)^-1 and a0 = A^T, so M = d a0 = (A A^-1)^T; ||M - I|| by column sums
+    // of M (= row sums of A A^-1 - I)
+    DevBuf<double> M(std::max<int64_t>(n * n, 1)), rs(std::max<int64_t>(n, 1));
+    const double one = 1.0, zero = 0.0;
+    const rocblas_status s3 = rocblas_dgemm(h, rocblas_operation_none, rocblas_operation_none, (rocblas_int)n, (rocblas_int)n,
+                                            (rocblas_int)n, &one, d.p, (rocblas_int)n, a0.p, (rocblas_int)n, &zero, M.p,
+                                            (rocblas_int)n);
+    hipLaunchKernelGGL(k_resid_rows, dim3(std::max<int64_t>(1, (n + 255) / 256)), dim3(256), 0, st, M.p, n, rs.p);
     DDPCA_HIP(hipStreamSynchronize(st));
     rocblas_destroy_handle(h);
-    if (s2 != rocblas_status_success || info.download()[1] != 0) return false;
+    if (s2 != rocblas_status_success || s3 != rocblas_status_success || info.download()[1] != 0) return false;
+    double r = 0.0;
+    for (double x : rs.download()) r = std::max(r, x);
+    *resid = r;
+    if (!(r <= kLuMaxResid)) return false;
     DDPCA_HIP(hipMemcpy(A.data(), d.p, A.size() * sizeof(double), hipMemcpyDeviceToHost));
     return true;
 }
@@ -1763,7 +1789,7 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
             int64_t nt = 0, tmax = 0;
             for (int64_t r = 0; r < A.nb; ++r) tmax = std::max<int64_t>(tmax, A.ptr[r + 1] - A.ptr[r]);
             if (tmax > kMaxRowBlocks) continue;  // long rows: no table for this subdomain
-            types[s] = row_types(A, subs[s].dof_free, keys[l][s], nt);
+            types[s] = row_types(A, subs[s].free_flags(l), keys[l][s], nt);
             tab_blocks += (double)nt * (double)tmax;
             blocks += (double)A.nnzb();
         }
@@ -1806,7 +1832,7 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
         std::vector<uint8_t> mask(L.nn, 0);
         for (int s = 0; s < nsub; ++s) {
             const Bsr3& A = *subs[s].K[l];
-            const uint8_t* fr = subs[s].dof_free;  // reference order: level-l nodes are a prefix
+            const uint8_t* fr = subs[s].free_flags(l);  // reference order: level-l nodes are a prefix
             const auto& p = perm[l][s];
             const int64_t base = L.noff[s];
             // padded rows of the subdomain: self column, zero values
@@ -2129,7 +2155,7 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
         std::vector<int64_t> ao(nsub), no(nsub), nz(nsub), ldv(nsub);
         for (int s = 0; s < nsub; ++s) {
             const Bsr3& A = *subs[s].K[clev];
-            const uint8_t* fr = subs[s].dof_free;
+            const uint8_t* fr = subs[s].free_flags(clev);
             const auto& p = perm[clev][s];
             const int64_t nc = subs[s].nnodes[clev], n0 = 3 * nc;
             std::vector<double> D(n0 * n0, 0.0);
@@ -2158,15 +2184,17 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
                 }
             if (general) {
                 // LU inverse when the LU is clearly regular, else the SVD pseudo-inverse
-                const bool lu = inv_general_lu_device(D, n0, stream);
+                double resid = INFINITY;
+                const bool lu = inv_general_lu_device(D, n0, stream, &resid);
                 int64_t dropped = 0;
                 if (!lu) pinv_general_device(D, n0, stream, &dropped);
+                coarse_inverse.push_back({lu ? 1 : 2, resid, dropped});
                 if (std::getenv("DDPCA_VERBOSE"))
-                    std::fprintf(stderr, lu ? "[ddpca] coarse inverse: LU, %ld rows\n"
-                                            : "[ddpca] coarse pseudo-inverse: %ld of %ld singular values dropped\n",
-                                 lu ? (long)n0 : (long)dropped, (long)n0);
+                    std::fprintf(stderr, "[ddpca] coarse inverse: %s, %ld rows, LU residual %.3g, %ld singular values dropped\n",
+                                 lu ? "LU" : "SVD pseudo-inverse", (long)n0, resid, (long)dropped);
             } else {
                 invert_spd_device(D, n0, stream);
+                coarse_inverse.push_back({0, 0.0, 0});
             }
             for (int64_t r = 0; r < nc; ++r)
                 for (int a = 0; a < 3; ++a) {

@@ -64,6 +64,11 @@ struct SubdomainOps {
     std::vector<int64_t> nnodes;           // nodes of level <= l
     std::vector<const Bsr3*> K;            // unconstrained Galerkin operator per level
     const uint8_t* dof_free = nullptr;     // 3 * nnodes.back() flags (consFlag)
+    // optional per-level flags (3 * nnodes[l] each) where a dof's status differs between levels
+    // (LATIN's DOUBLE_M: a coarse contact node its finer level does not carry is a masked copy
+    // there); empty = the fine flags' prefix on every level (consOper, MULTIGRID.h:1186-1243)
+    std::vector<const uint8_t*> dof_free_lev;
+    const uint8_t* free_flags(int l) const { return dof_free_lev.empty() ? dof_free : dof_free_lev[l]; }
     std::vector<const Stencil*> S;         // scalar prolongation stencils, nlev - 1
     const double* coords = nullptr;        // optional 3 * nnodes.back() node coordinates: when
                                            // given, levels >= 1 are renumbered on the device
@@ -173,6 +178,15 @@ public:
                 bool diag_only = false);
     bool general = false;
     bool no_coarse = false;  // one-level handle without the dense inverse (diagonal drivers only)
+    // per subdomain's dense coarse inverse: kind 0 SPD potri, 1 LU (getri, residual checked),
+    // 2 SVD pseudo-inverse; the LU's ||A^-1 A - I||_inf (INFINITY when its pivots failed); the
+    // singular values the pseudo-inverse dropped
+    struct CoarseInverse {
+        int kind;
+        double resid;
+        int64_t dropped;
+    };
+    std::vector<CoarseInverse> coarse_inverse;
     ~MgpisDevice();
 
     int device = 0;

@@ -516,7 +516,10 @@ int64_t ddpca_lagrange_solve(ddpca_lagrange_t h, int device, int prec_type, cons
  * "solver_relres" (per Newton step: BiCGSTAB's recursive ||r|| / ||b|| at exit) and
  * "solver_breakdown" (0 converged to 1e-14, 1 rho = 0, 2 stopped at the attainable accuracy:
  * ||r|| <= 1e-12 ||b|| and flat over five iterations -- the singular frictionless systems).  A step
- * whose solve ends above 1e-10 makes ddpca_lagrange_solve return DDPCA_ENUMERIC.
+ * whose solve ends above 1e-10 makes ddpca_lagrange_solve return DDPCA_ENUMERIC.  "coarse_inverse"
+ * (3 per Newton step: the dense coarse inverse taken -- 1 LU, kept only when ||A^-1 A - I||_inf
+ * <= 1e-6, 2 SVD pseudo-inverse, -1 none (diagonal preconditioner) -- the LU residual measured
+ * (inf when its pivot test failed) and the singular values the pseudo-inverse dropped).
  * Returns the count (copies min(count, cap) when out != NULL). */
 int64_t ddpca_lagrange_get(ddpca_lagrange_t h, const char* what, int64_t index, double* out, int64_t cap);
 int ddpca_lagrange_destroy(ddpca_lagrange_t h);

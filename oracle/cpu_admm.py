@@ -17,10 +17,21 @@ right-hand side, not iteration 0's.  Bounded sample:
     interface    (2629-2704)  gamma, projection, aux and lambda with the factorised surface mass
                               matrices (the reference's LDLT below 120000 rows), every interface
 Text output (OUTP_SUB2 / OUTPUT_PRTR every iteration in the reference) is left out.
+
+`reference_cg_solv` times the reference's OWN MGPIS::CG_SOLV(1) (MGPIS.h:163-225, compiled from
+/root/reference into oracle/_ref/ref_harness_portable, `time_cg_ops`) on a worm's and a wheel's
+consStif[l] / realProl[l] and the same right-hand side, handed over as raw files; bench.py reports
+it as `reference_measured`, the body balance priced by those solves and the rest of the
+iteration by the port.
 """
 from __future__ import annotations
 
+import json
+import os
+import shutil
+import subprocess
 import sys
+import tempfile
 import time
 
 import numpy as np
@@ -34,13 +45,73 @@ def _log(msg: str) -> None:
     print(f"[cpu_baseline] {msg}", file=sys.stderr, flush=True)
 
 
-def price_iteration(P, mc, budget_s: float = 20.0) -> dict:
+def _state(P, mc):
     nsub, nint = P.nsub, P.nint
     body = [tuple(int(b) for b in P.array("iface_body", ts)) for ts in range(nint)]
-    fric = [float(P.array("iface_param", ts)[0]) for ts in range(nint)]
-    u = [mc.get("resuDisp", tv) for tv in range(nsub)]
     aux = [[mc.get("inteAuxi", 2 * ts + s) for s in range(2)] for ts in range(nint)]
     lam = [[mc.get("inteLagr", 2 * ts + s) for s in range(2)] for ts in range(nint)]
+    return nsub, nint, body, aux, lam
+
+
+def _rhs(P, G, tv, body, aux, lam):
+    """consForc + consOper (systTran_pena aux - systTran lambda) of subdomain tv: the body
+    balance's right-hand side (ADDITIONAL_FORCE, MCONTACT.h:2520-2524), condensed."""
+    flag = G.consFlag == 1
+    f = np.zeros(len(flag))
+    for ts in range(len(body)):
+        for s in range(2):
+            if body[ts][s] == tv:
+                O.csr_matvec(O.csr64(P.csr("systTran_pena", 2 * ts + s)), aux[ts][s], f)
+                f -= O.csr_matvec(O.csr64(P.csr("systTran", 2 * ts + s)), lam[ts][s])
+    return G.consForc + f[flag]
+
+
+def reference_cg_solv(P, mc, exe, subdomains=(1, 0), threads: int | None = None, timeout_s: float = 300.0) -> dict:
+    """Wall time of the reference's own MGPIS::CG_SOLV(1) on the given subdomains (default: a
+    wheel, then a worm) at the device run's final state: each hierarchy is written to a scratch
+    directory as raw CSR files and `exe time_cg_ops` reads it into the reference's MGPIS
+    (consStif / realProl members, MGPIS::ESTABLISH untimed) and times CG_SOLV(1) once."""
+    nsub, nint, body, aux, lam = _state(P, mc)
+    env = dict(os.environ)
+    if threads:
+        env["OMP_NUM_THREADS"] = str(threads)
+    out = []
+    for tv in subdomains:
+        G = P.grid(tv)
+        L = G.maxiLeve
+        d = tempfile.mkdtemp(prefix="ddpca_refcg_")
+        try:
+            meta = [str(L + 1)]
+            for kind, n in (("K", L + 1), ("P", L)):
+                for l in range(n):
+                    base = "K" if kind == "K" else "P"
+                    shape = P.array(f"{base}:shape", tv, l)
+                    ptr = P.array(f"{base}:ptr", tv, l)
+                    meta.append(f"{int(shape[0])} {int(shape[1])} {int(ptr[-1])}")
+                    np.ascontiguousarray(ptr, dtype=np.int64).tofile(f"{d}/{kind}{l}.ptr")
+                    np.ascontiguousarray(P.array(f"{base}:col", tv, l), dtype=np.int32).tofile(f"{d}/{kind}{l}.col")
+                    np.ascontiguousarray(P.array(f"{base}:val", tv, l), dtype=np.float64).tofile(f"{d}/{kind}{l}.val")
+            b = _rhs(P, G, tv, body, aux, lam)
+            np.ascontiguousarray(b, dtype=np.float64).tofile(f"{d}/b.f64")
+            with open(f"{d}/meta.txt", "w") as f:
+                f.write("\n".join(meta) + "\n")
+            r = subprocess.run([str(exe), "time_cg_ops", d, "1"], capture_output=True, text=True, timeout=timeout_s, env=env)
+            if r.returncode != 0:
+                raise RuntimeError(f"{exe} time_cg_ops: exit {r.returncode}: {r.stderr[-500:]}")
+            rec = json.loads(r.stdout.strip().splitlines()[-1])
+            rec["subdomain"] = tv
+            out.append(rec)
+            _log(f"reference CG_SOLV(1) subdomain {tv}: {rec['iters']} iterations, {rec['cg_s']:.2f} s "
+                 f"({rec['threads']} threads, true relres {rec['true_relres']:.1e})")
+        finally:
+            shutil.rmtree(d, ignore_errors=True)
+    return {"solves": out, "threads": out[0]["threads"] if out else None}
+
+
+def price_iteration(P, mc, budget_s: float = 20.0, ref_exe=None, ref_threads: int | None = None) -> dict:
+    nsub, nint, body, aux, lam = _state(P, mc)
+    fric = [float(P.array("iface_param", ts)[0]) for ts in range(nint)]
+    u = [mc.get("resuDisp", tv) for tv in range(nsub)]
     try:
         has_coarse = P.csr("globCoup_1").shape[0] > 0
     except Exception:  # noqa: BLE001 -- no coarse space in this problem
@@ -54,14 +125,7 @@ def price_iteration(P, mc, budget_s: float = 20.0) -> dict:
         G = P.grid(tv)
         L = G.maxiLeve
         M = O.MgpisOracle([G.consStif(l) for l in range(L + 1)], [G.realProl(l) for l in range(L)])
-        flag = G.consFlag == 1
-        f = np.zeros(len(flag))
-        for ts in range(nint):
-            for s in range(2):
-                if body[ts][s] == tv:  # ADDITIONAL_FORCE, MCONTACT.h:2520-2524
-                    O.csr_matvec(O.csr64(P.csr("systTran_pena", 2 * ts + s)), aux[ts][s], f)
-                    f -= O.csr_matvec(O.csr64(P.csr("systTran", 2 * ts + s)), lam[ts][s])
-        b = G.consForc + f[flag]
+        b = _rhs(P, G, tv, body, aux, lam)
         t = time.perf_counter()
         x, it, _ = M.CG_SOLV(1, b)
         solve_s.append(time.perf_counter() - t)
@@ -117,6 +181,22 @@ def price_iteration(P, mc, budget_s: float = 20.0) -> dict:
     t_iface = time.perf_counter() - t
     _log(f"interface step {t_iface:.2f} s ({nip} integration points)")
     total = t_body + t_coarse + t_iface
+    ref = None
+    if ref_exe is not None:
+        # the reference's own CG_SOLV(1) on a wheel and a worm: the body balance priced by its
+        # solves (x nsub / 2), the coarse space and the interface step by the port as above
+        rc = reference_cg_solv(P, mc, ref_exe, (1, 0), ref_threads)
+        solves = rc["solves"]
+        t_body_ref = nsub / len(solves) * sum(x["cg_s"] for x in solves)
+        ref = {"value": 1.0 / (t_body_ref + t_coarse + t_iface), "unit": "ADMM it/s", "cores": rc["threads"],
+               "kind": "reference",
+               "sample": f"the reference's own MGPIS::CG_SOLV(1) (oracle/_ref/ref_harness_portable time_cg_ops) on "
+                         f"subdomains {[x['subdomain'] for x in solves]} ({solves[0]['n']} DOF each, "
+                         f"{[x['iters'] for x in solves]} iterations, {[round(x['cg_s'], 2) for x in solves]} s) "
+                         f"priced x{nsub / len(solves):g} = {t_body_ref:.1f} s; coarse space {t_coarse:.2f} s and "
+                         f"interface step {t_iface:.2f} s by the port",
+               "body_s": t_body_ref, "solves": solves,
+               "port_over_reference_cg": sum(solve_s[:2]) / max(sum(x["cg_s"] for x in solves), 1e-30)}
     return {
         "value": 1.0 / total,
         "unit": "ADMM it/s",
@@ -131,4 +211,5 @@ def price_iteration(P, mc, budget_s: float = 20.0) -> dict:
         "coarse_s": t_coarse,
         "iface_s": t_iface,
         "dof_iter_per_s": ndof * sum(iters) / sum(solve_s),
+        "reference_measured": ref,
     }

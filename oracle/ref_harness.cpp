@@ -26,6 +26,11 @@
 //       the same BEAM -> MULT_SOLV, BiCGSTAB_SOLV(0/1), GMRES_SOLV(0/1) solutions.
 //   time_cg d0 d1 d2 globLeve reps
 //       wall time of MGPIS::CG_SOLV(1) on the BEAM mesh (CPU baseline calibration).
+//   time_cg_ops dir reps
+//       wall time of MGPIS::CG_SOLV(1) on a hierarchy handed over as raw files (bench.py's
+//       cpu_baseline: a headline subdomain's consStif[l] / realProl[l] and its right-hand side):
+//       dir/meta.txt = "nlev" then "rows cols nnz" per K level and per P level; dir/K<l>.ptr (int64),
+//       .col (int32), .val (float64), the same for P<l>, dir/b.f64.
 #include "examples/BEAM.h"
 
 #include <chrono>
@@ -577,6 +582,58 @@ int time_cg(long d0, long d1, long d2, long gl, long reps) {
     return 0;
 }
 
+template <typename T>
+std::vector<T> read_raw(const std::string& path, size_t n) {
+    std::vector<T> v(n);
+    FILE* f = std::fopen(path.c_str(), "rb");
+    if (!f || std::fread(v.data(), sizeof(T), n, f) != n) throw std::runtime_error("cannot read " + path);
+    std::fclose(f);
+    return v;
+}
+
+Eigen::SparseMatrix<double, Eigen::RowMajor> read_csr(const std::string& pre, long rows, long cols, long nnz) {
+    const auto p64 = read_raw<int64_t>(pre + ".ptr", rows + 1);
+    auto col = read_raw<int32_t>(pre + ".col", nnz);
+    auto val = read_raw<double>(pre + ".val", nnz);
+    if (p64[0] != 0 || p64[rows] != nnz) throw std::runtime_error(pre + ": row pointer");
+    std::vector<int> ptr(p64.begin(), p64.end());
+    Eigen::Map<const Eigen::SparseMatrix<double, Eigen::RowMajor>> m(rows, cols, nnz, ptr.data(), col.data(), val.data());
+    return Eigen::SparseMatrix<double, Eigen::RowMajor>(m);
+}
+
+int time_cg_ops(const std::string& dir, long reps) {
+    std::ifstream meta(dir + "/meta.txt");
+    long nlev = 0;
+    if (!(meta >> nlev) || nlev < 1) throw std::runtime_error("meta.txt");
+    MGPIS mg;
+    mg.maxiLeve = nlev - 1;
+    for (long l = 0; l < nlev; ++l) {
+        long r, c, z;
+        meta >> r >> c >> z;
+        mg.consStif.push_back(read_csr(dir + "/K" + std::to_string(l), r, c, z));
+    }
+    for (long l = 0; l + 1 < nlev; ++l) {
+        long r, c, z;
+        meta >> r >> c >> z;
+        mg.realProl.push_back(read_csr(dir + "/P" + std::to_string(l), r, c, z));
+    }
+    const long n = mg.consStif.back().rows();
+    const auto bv = read_raw<double>(dir + "/b.f64", n);
+    const Eigen::VectorXd b = Eigen::Map<const Eigen::VectorXd>(bv.data(), n);
+    quiet([&] { mg.ESTABLISH(); });  // consLowe / consDiag / consUppe (MGPIS.h:36-49), setup
+    for (long r = 0; r < reps; ++r) {
+        Eigen::VectorXd x;
+        const double t1 = now_s();
+        const long it = capture_iters([&] { mg.CG_SOLV(1, b, x); });
+        const double t = now_s() - t1;
+        const double bn = b.norm(), rel = bn > 0 ? (b - mg.consStif.back() * x).norm() / bn : 0.0;
+        std::printf("{\"n\": %ld, \"levels\": %ld, \"iters\": %ld, \"cg_s\": %.6f, \"true_relres\": %.3e, \"threads\": %d}\n",
+                    n, nlev, it, t, rel, omp_get_max_threads());
+        std::fflush(stdout);
+    }
+    return 0;
+}
+
 }  // namespace harness
 
 #ifndef HARNESS_NO_MAIN
@@ -598,6 +655,7 @@ int main(int argc, char** argv) {
         return twoblock(std::stod(argv[2]), L(3), argc >= 6 ? L(5) : 0);
     }
     if (mode == "time_cg" && argc >= 7) return time_cg(L(2), L(3), L(4), L(5), L(6));
+    if (mode == "time_cg_ops" && argc >= 4) return time_cg_ops(argv[2], L(3));
     if (mode == "beam_solv" && argc >= 7) {
         g_out = argv[6];
         return beam_solv(L(2), L(3), L(4), L(5));

@@ -20,6 +20,7 @@
 #include <execinfo.h>
 #include <unistd.h>
 
+#include <cmath>
 #include <csignal>
 #include <cstdio>
 #include <fstream>
@@ -144,12 +145,29 @@ int main(int argc, char** argv) {
         log = std::string(rep) + "/log.txt";
         b.resuDisp.resize(b.multGrid.size());
         for (size_t tv = 0; tv < b.multGrid.size(); ++tv) {
-            std::ifstream f(std::string(rep) + "/resuDisp_" + std::to_string(tv) + ".bin", std::ios::binary);
+            // the recorded answer must exist and fit this subdomain's mesh (3 per node), else the
+            // comparison below would subtract vectors of different sizes
+            const std::string path = std::string(rep) + "/resuDisp_" + std::to_string(tv) + ".bin";
+            std::ifstream f(path, std::ios::binary);
+            if (!f) {
+                std::fprintf(stderr, "replay: cannot open %s\n", path.c_str());
+                return 2;
+            }
             f.seekg(0, std::ios::end);
-            const std::streamoff n = f.tellg() / (std::streamoff)sizeof(double);
+            const std::streamoff bytes = f.tellg();
+            const std::streamoff n = bytes / (std::streamoff)sizeof(double);
+            const std::streamoff want = 3 * (std::streamoff)b.multGrid[tv].nodeCoor.size();
+            if (bytes < 0 || n != want || n * (std::streamoff)sizeof(double) != bytes) {
+                std::fprintf(stderr, "replay: %s holds %ld doubles, subdomain %zu has %ld dofs\n", path.c_str(), (long)n, tv,
+                             (long)want);
+                return 2;
+            }
             f.seekg(0);
             b.resuDisp[tv].resize(n);
-            f.read(reinterpret_cast<char*>(b.resuDisp[tv].data()), n * sizeof(double));
+            if (!f.read(reinterpret_cast<char*>(b.resuDisp[tv].data()), n * sizeof(double))) {
+                std::fprintf(stderr, "replay: short read of %s\n", path.c_str());
+                return 2;
+            }
         }
     } else if (rec) {
         const std::string d(rec);
@@ -246,6 +264,8 @@ int main(int argc, char** argv) {
     std::vector<double> rel(64), brk(64);
     ddpca_lagrange_get(h, "solver_relres", 0, rel.data(), (int64_t)rel.size());
     ddpca_lagrange_get(h, "solver_breakdown", 0, brk.data(), (int64_t)brk.size());
+    std::vector<double> cinv(3 * nst);
+    ddpca_lagrange_get(h, "coarse_inverse", 0, cinv.data(), (int64_t)cinv.size());
     // displacements: OUTP_SUB1 of the device's condensed solution vs the reference's resuDisp
     double du = 0.0;
     for (int64_t tv = 0; tv < nsub; ++tv) {
@@ -290,9 +310,12 @@ int main(int argc, char** argv) {
         itf += buf;
     }
     itf += "]";
-    std::string sit = "[", rit = "[", srel = "[", sbrk = "[";
+    std::string sit = "[", rit = "[", srel = "[", sbrk = "[", scin = "[";
     for (int64_t k = 0; k < nst; ++k) {
-        char nb[32];
+        char nb[32], cb[96];
+        std::snprintf(cb, sizeof(cb), "%s[%d, %.3e, %ld]", k ? ", " : "", (int)cinv[3 * k],
+                      std::isfinite(cinv[3 * k + 1]) ? cinv[3 * k + 1] : -1.0, (long)cinv[3 * k + 2]);
+        scin += cb;
         std::snprintf(nb, sizeof(nb), "%.3e", rel[k]);
         sit += (k ? ", " : "") + std::to_string((long)its[k]);
         srel += (k ? ", " : "") + std::string(nb);
@@ -300,15 +323,16 @@ int main(int argc, char** argv) {
     }
     srel += "]";
     sbrk += "]";
+    scin += "]";
     for (size_t k = 0; k < its_ref.size(); ++k) rit += (k ? ", " : "") + std::to_string(its_ref[k]);
     sit += "]";
     rit += "]";
     ddpca_lagrange_destroy(h);
     std::fprintf(stderr,
                  "{\"newton\": %ld, \"newton_ref\": %ld, \"bicgstab_iters\": %s, \"bicgstab_iters_ref\": %s, "
-                 "\"bicgstab_relres\": %s, \"bicgstab_breakdown\": %s, \"resuDisp_rel\": %.3g, "
+                 "\"bicgstab_relres\": %s, \"bicgstab_breakdown\": %s, \"coarse_inverse\": %s, \"resuDisp_rel\": %.3g, "
                  "\"lambda_rel\": %.3g, \"nodes_equal\": %s, \"status_equal\": %s, \"replayed\": %s, \"interfaces\": %s}\n",
-                 (long)tc, tc_ref, sit.c_str(), rit.c_str(), srel.c_str(), sbrk.c_str(), du, dl, nodes_equal ? "true" : "false", stat_equal ? "true" : "false",
+                 (long)tc, tc_ref, sit.c_str(), rit.c_str(), srel.c_str(), sbrk.c_str(), scin.c_str(), du, dl, nodes_equal ? "true" : "false", stat_equal ? "true" : "false",
                  replay ? "true" : "false", itf.c_str());
     return 0;
 }

@@ -46,19 +46,19 @@ inline std::string compare(ddpca_problem_t p, const std::vector<int32_t>& owners
     check(mcontact_gpu_comm_local(hr.data(), nranks));
     std::vector<int64_t> nr(nranks, 0);
     std::vector<int> ck(nranks, 0);
+    std::vector<std::string> msg(nranks);  // the library's last error is per thread
     {
         std::vector<std::thread> th;
         for (int r = 0; r < nranks; ++r)
             th.emplace_back([&, r] {
                 ck[r] = mcontact_gpu_comm_check(hr[r], 4096);  // the transport itself first
                 nr[r] = ck[r] < 0 ? ck[r] : mcontact_gpu_iterate(hr[r], maxit, 1);
+                if (nr[r] < 0) msg[r] = std::string(ck[r] < 0 ? "comm_check: " : "iterate: ") + ddpca_last_error();
             });
         for (auto& t : th) t.join();
     }
-    for (int r = 0; r < nranks; ++r) {
-        check(ck[r]);
-        check((int)std::min<int64_t>(nr[r], 0));
-    }
+    for (int r = 0; r < nranks; ++r)
+        if (nr[r] < 0) throw std::runtime_error("libddpca_amd: rank " + std::to_string(r) + " " + msg[r]);
     double dm = 0.0, du = 0.0, dg = 0.0;
     for (int r = 0; r < nranks; ++r) {
         const int64_t rows = mcontact_gpu_monitor(hr[r], nullptr, 0);

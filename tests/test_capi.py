@@ -134,3 +134,24 @@ def test_multigrid_inputs_are_checked_before_the_tree_changes(ddpca):
         assert rc == 0 and _nelem(L, h) == 9
     finally:
         L.ddpca_multigrid_destroy(h)
+
+
+@pytest.mark.parametrize("band", [0, 1], ids=["uniform", "band-refined"])
+def test_dehw_interfaces_cover_their_planes(ddpca, band):
+    """The synthetic DEHW chain's conforming interfaces (capi_host.cpp conforming_interface(_xyz)):
+    every face of the plane on both sides paired (a missing mate is an error, not a skipped face), so
+    each interface's integration weights sum to its plane's area, and a contact plane carries
+    faces x 16 points x 4^k (the band splits each contact face in four and integrates it one level
+    coarser: the same points per area)."""
+    import numpy as np
+    G, nx, ny, nz, gl, kc, kg = 2, 3, 2, 2, 2, 2, 1
+    P = ddpca.Problem("dehw", G, nx, ny, nz, gl, 0.2, kc, kg, band, 0)
+    h = 0.01
+    for ts in range(P.nint):
+        w = P.array("ip_w", ts)
+        area = (nx * h) * (ny * h) if ts < G else (ny * h) * (nz * h)
+        assert abs(w.sum() - area) <= 1e-12 * area, (ts, w.sum(), area)
+        if ts < G:
+            faces = nx * ny * 4 ** (gl + band)
+            ke = max(kc - 1, 0) if band else kc
+            assert len(w) == faces * 16 * 4 ** ke, (ts, len(w))

@@ -59,6 +59,14 @@ def test_lagrange_matches_reference(gpu, tmp_path, request, example, prec, fric,
     assert len(res["bicgstab_relres"]) == len(res["bicgstab_iters"])
     for rel, brk in zip(res["bicgstab_relres"], res["bicgstab_breakdown"]):
         assert brk in (0, 2) and rel <= (1e-14 if brk == 0 else 1e-12) * 1.0001, res
+    # the dense coarse inverse each step took: an LU only with ||A^-1 A - I|| <= 1e-6, else the
+    # SVD pseudo-inverse (none under the diagonal preconditioner)
+    assert len(res["coarse_inverse"]) == res["newton"] + 1
+    for kind, resid, dropped in res["coarse_inverse"]:
+        if prec == "2":
+            assert kind == -1, res["coarse_inverse"]
+        else:
+            assert kind in (1, 2) and (kind == 2 or 0 <= resid <= 1e-6) and (kind == 1 or dropped >= 0), res["coarse_inverse"]
     if example == "block" and fric == "0":  # the patch test: every active node carries the 1e7 load pressure
         for itf in res["interfaces"]:
             if itf["fric"] == 0.0 and itf["nodes"]:
