@@ -109,8 +109,6 @@ class _CsrArg(C.Structure):  # ddpca_csr_t
 def _declare(L: C.CDLL) -> None:
     L.ddpca_last_error.restype = C.c_char_p
     L.ddpca_gpu_available.restype = C.c_int
-    L.ddpca_stream_ceiling.argtypes = [C.c_int, C.c_int64, C.c_int, _DP]
-    L.ddpca_probe_grid_barrier.argtypes = [C.c_int, C.c_int64, C.c_int, C.c_int, _DP]
     L.mgpis_default_options.argtypes = [C.POINTER(MgpisOptions)]
     L.mgpis_default_options.restype = None
     L.ddpca_problem_create.argtypes = [C.c_char_p, _DP, C.c_int, C.POINTER(_P)]
@@ -178,6 +176,7 @@ def _declare(L: C.CDLL) -> None:
                                           C.POINTER(_P)]
         L.mcontact_gpu_comm_init.argtypes = [_P, _P]
         L.mcontact_gpu_comm_local.argtypes = [_P, C.c_int]
+        L.mcontact_gpu_comm_loopback.argtypes = [_P, _P]
         L.mcontact_gpu_unique_id.argtypes = [_P]
         L.mcontact_gpu_iterate.argtypes = [_P, C.c_int64, C.c_int]
         L.mcontact_gpu_iterate.restype = C.c_int64
@@ -204,18 +203,36 @@ def gpu_available() -> bool:
     return bool(lib().ddpca_gpu_available())
 
 
+_probe_lib = None
+
+
+def probe_lib() -> C.CDLL:
+    """libddpca_probe.so (include/ddpca_probe.h): the measurement probes beside the product."""
+    global _probe_lib
+    if _probe_lib is None:
+        lib()  # the probe library resolves its error plumbing from the product library
+        path = Path(LIBPATH).with_name("libddpca_probe.so")
+        if not path.exists():
+            raise ImportError(f"{path} is missing: run ddpca-admm_amd/build.py")
+        L = C.CDLL(str(path))
+        L.ddpca_stream_ceiling.argtypes = [C.c_int, C.c_int64, C.c_int, _DP]
+        L.ddpca_probe_grid_barrier.argtypes = [C.c_int, C.c_int64, C.c_int, C.c_int, C.c_int, _DP]
+        _probe_lib = L
+    return _probe_lib
+
+
 def stream_ceiling(device: int = 0, nbytes: int = 2 << 30, reps: int = 10) -> dict:
     """This box's STREAM copy / read bandwidth (ddpca_stream_ceiling), in GB/s."""
     out = (C.c_double * 4)()
-    _check(lib().ddpca_stream_ceiling(device, int(nbytes), int(reps), out))
+    _check(probe_lib().ddpca_stream_ceiling(device, int(nbytes), int(reps), out))
     return dict(copy_gbs=out[0], read_gbs=out[1], copy_ms=out[2], read_ms=out[3], bytes_per_buffer=int(nbytes))
 
 
-def probe_grid_barrier(n: int, phases: int = 64, blocks: int = 256, device: int = 0) -> dict:
+def probe_grid_barrier(n: int, phases: int = 64, blocks: int = 256, pin: bool = False, device: int = 0) -> dict:
     """Graph kernel boundary vs persistent grid barrier per dependent pass over n doubles
-    (ddpca_probe_grid_barrier; measurement only)."""
+    (ddpca_probe_grid_barrier; measurement only); pin: the persistent workgroups on one XCD."""
     out = (C.c_double * 4)()
-    _check(lib().ddpca_probe_grid_barrier(device, int(n), int(phases), int(blocks), out))
+    _check(probe_lib().ddpca_probe_grid_barrier(device, int(n), int(phases), int(blocks), int(bool(pin)), out))
     return dict(graph_us=out[0], persistent_us=out[1], max_diff=out[2], timed_out=int(out[3]))
 
 
@@ -820,6 +837,11 @@ class MCONTACT:
         transport (mcontact_gpu_comm_local); run each rank's CONTACT_ANALYSIS on its own thread."""
         arr = (C.c_void_p * len(ranks))(*[m._h.value for m in ranks])
         _check(lib().mcontact_gpu_comm_local(arr, len(ranks)))
+
+    def comm_loopback(self) -> None:
+        """Timing only (mcontact_gpu_comm_loopback): this rank alone on its GPU, every exchange
+        returned to itself, all-reduces the identity; its problem must be established in full."""
+        _check(lib().mcontact_gpu_comm_loopback(self._h, self.problem.handle))
 
     def comm_check(self, n: int = 1000) -> None:
         """Collective transport check (mcontact_gpu_comm_check): tagged messages to every rank and an

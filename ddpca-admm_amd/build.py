@@ -20,6 +20,8 @@ OBJ = HERE / "build" / "obj"
 # experiment builds (A/B of a kernel change): DDPCA_BUILD_DEFINES="-DFOO=1" DDPCA_BUILD_OUT=libx.so
 # produce a second library next to this file; load it with DDPCA_AMD_LIB=<path>
 LIB = HERE / os.environ.get("DDPCA_BUILD_OUT", "libddpca_amd.so")
+PROBE = HERE / "probe"
+PROBE_LIB = HERE / "libddpca_probe.so"
 ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
 HIPCC = str(ROCM / "bin" / "hipcc")
 ARCH = "gfx950"
@@ -62,25 +64,35 @@ def _compile(src: Path) -> Path:
     return obj
 
 
-def build(verbose: bool = False) -> Path:
-    OBJ.mkdir(parents=True, exist_ok=True)
-    srcs = _sources()
-    jobs = min(len(srcs), int(os.environ.get("MAX_JOBS", os.cpu_count() or 4)), 16)
-    with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
-        objs = list(ex.map(_compile, srcs))
+def _link(objs: list[Path], out: Path, link: list[str], verbose: bool) -> Path:
     stamp = hashlib.sha1("".join(o.name for o in objs).encode()).hexdigest()[:16]
-    stamp_file = OBJ / f"link.{LIB.name}.stamp"
-    if LIB.exists() and stamp_file.exists() and stamp_file.read_text() == stamp:
-        return LIB
-    tmp = LIB.with_suffix(f".so.{os.getpid()}.tmp")
-    cmd = [HIPCC, *[str(o) for o in objs], *LINK, "-o", str(tmp)]
+    stamp_file = OBJ / f"link.{out.name}.stamp"
+    if out.exists() and stamp_file.exists() and stamp_file.read_text() == stamp:
+        return out
+    tmp = out.with_suffix(f".so.{os.getpid()}.tmp")
+    cmd = [HIPCC, *[str(o) for o in objs], *link, "-o", str(tmp)]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
-    os.replace(tmp, LIB)
+    os.replace(tmp, out)
     stamp_file.write_text(stamp)
     if verbose:
-        print(f"built {LIB}", file=sys.stderr)
+        print(f"built {out}", file=sys.stderr)
+    return out
+
+
+def build(verbose: bool = False) -> Path:
+    OBJ.mkdir(parents=True, exist_ok=True)
+    srcs = _sources()
+    probe = sorted(PROBE.glob("*.hip"))
+    jobs = min(len(srcs) + len(probe), int(os.environ.get("MAX_JOBS", os.cpu_count() or 4)), 16)
+    with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+        objs = list(ex.map(_compile, srcs + probe))
+    _link(objs[:len(srcs)], LIB, LINK, verbose)
+    # the measurement probes (STREAM ceiling, grid barrier): a library of their own beside the
+    # product, linked against it for the error plumbing
+    if LIB.name == "libddpca_amd.so":
+        _link(objs[len(srcs):], PROBE_LIB, LINK + [f"-L{HERE}", "-lddpca_amd", "-Wl,-rpath,$ORIGIN"], verbose)
     return LIB
 
 

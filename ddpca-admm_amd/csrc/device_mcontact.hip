@@ -1151,6 +1151,17 @@ struct RcclTransport : Transport {
     }
 };
 
+// Timing-only transport (mcontact_gpu_comm_loopback): every receive from peer p gets what this
+// rank sent p, as an on-device copy on the solve stream; all-reduces keep this rank's own values.
+// One rank of an N-rank layout then runs its own share of the work on a single GPU.
+struct LoopbackTransport : Transport {
+    void allreduce_sum(double*, int64_t, hipStream_t) override {}
+    void exchange(const std::vector<Msg>& msgs, hipStream_t st) override {
+        for (const Msg& m : msgs)
+            if (m.n) DDPCA_HIP(hipMemcpyAsync(m.recv, m.send, (size_t)m.n * sizeof(double), hipMemcpyDeviceToDevice, st));
+    }
+};
+
 // Rendezvous of the ranks of one process (each rank's calls come from its own host thread).
 struct LocalHub {
     int n = 0;
@@ -2738,6 +2749,29 @@ int mcontact_gpu_comm_local(mcontact_t* handles, int n) {
         for (auto& t : th) t.join();
         for (int r = 0; r < n; ++r)
             if (rc[r] < 0) throw ApiError(rc[r], "rank " + std::to_string(r) + ": " + msg[r]);
+    });
+}
+
+int mcontact_gpu_comm_loopback(mcontact_t h, ddpca_problem_t p) {
+    return guarded([&] {
+        if (!h || !p) throw ApiError(DDPCA_EINVAL, "handle / problem");
+        select_device(h->device);
+        if (h->comm) throw ApiError(DDPCA_ESTATE, "handle already has a communicator");
+        h->comm = std::make_unique<LoopbackTransport>();
+        CoarseDev& C = h->cs;
+        if (C.on && !C.inverted && !C.mg) {
+            // the other ranks' rows of the dense coarse operator come from the problem itself (the
+            // setup all-reduce that would sum them is the identity here)
+            const CoarseSpace& cs = reinterpret_cast<Problem*>(p)->mc.coarse;
+            if (cs.rank_local || cs.n != C.n)
+                throw ApiError(DDPCA_ESTATE, "loopback: the problem must be the handle's, established in full");
+            const int64_t n = C.n;
+            C.dense.assign((size_t)n * n, 0.0);
+            for (int64_t r = 0; r < n; ++r)
+                for (int64_t k = cs.globCoup_1.ptr[r]; k < cs.globCoup_1.ptr[r + 1]; ++k)
+                    C.dense[(size_t)r * n + cs.globCoup_1.col[k]] = cs.globCoup_1.val[k];
+        }
+        coarse_invert(*h);
     });
 }
 

@@ -10,7 +10,8 @@
 #include <vector>
 
 #include "../../include/ddpca_amd.h"
-#include "device_common.hpp"
+#include "../../include/ddpca_probe.h"
+#include "../csrc/device_common.hpp"
 
 using namespace ddpca;
 
@@ -78,37 +79,42 @@ __global__ __launch_bounds__(256) void k_phase(const double* x, double* y, int64
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) y[i] = phase_value(x, i, n);
 }
 
-// every workgroup of the launch is resident (the caller launches at most one per CU); the wait is
-// bounded, so a grid that is not all resident ends with err = 1 instead of hanging
-__global__ __launch_bounds__(256) void k_phase_persistent(double* x, double* y, int64_t n, int phases, unsigned* count,
-                                                          unsigned* gen, int* err) {
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+// Every working workgroup of the launch is resident (the caller launches at most one per CU, or
+// with pin one per CU of one XCD); the wait is bounded, so a grid that is not all resident ends with
+// err = 1 instead of hanging.  pin: only the workgroups with id % 8 == 0 work (the round-robin
+// dispatch puts them on one XCD), the others exit at once.  Barrier: one monotonic counter (zeroed
+// by the caller) -- every storing wave drains its stores, the workgroup's lane 0 releases at agent
+// scope and adds, polls relaxed with s_sleep, then acquires at agent scope (the XCD's L2 is shared
+// by co-located workgroups, their L1s are not: the acquire is needed either way).
+__global__ __launch_bounds__(256) void k_phase_persistent(double* x, double* y, int64_t n, int phases, int active, int pin,
+                                                          unsigned* count, int* err) {
+    if (pin && (blockIdx.x & 7)) return;
+    const int64_t wid = pin ? blockIdx.x >> 3 : blockIdx.x;
+    const int64_t stride = (int64_t)active * blockDim.x;
     __shared__ int bad;
     if (threadIdx.x == 0) bad = 0;
     for (int p = 0; p < phases; ++p) {
         const double* src = (p & 1) ? y : x;
         double* dst = (p & 1) ? x : y;
-        for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) dst[i] = phase_value(src, i, n);
+        for (int64_t i = wid * blockDim.x + threadIdx.x; i < n; i += stride) dst[i] = phase_value(src, i, n);
         if (p + 1 == phases) break;
-        // grid barrier: agent-scope release of this workgroup's writes, arrival ticket, the last
-        // arrival bumps the generation; acquire before the next pass reads other workgroups' data
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (threadIdx.x == 0) {
-            const unsigned g = __hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const unsigned a = __hip_atomic_fetch_add(count, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-            if (a + 1 == gridDim.x) {
-                __hip_atomic_store(count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(gen, g + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-            } else {
-                int64_t spin = 0;
-                while (__hip_atomic_load(gen, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == g) {
-                    if (++spin > (int64_t)1 << 24) {
-                        bad = 1;
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(2);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_fetch_add(count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned target = (unsigned)(p + 1) * (unsigned)active;
+            int64_t spin = 0;
+            while (__hip_atomic_load(count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+                if (++spin > (int64_t)1 << 24) {
+                    bad = 1;
+                    break;
                 }
+                __builtin_amdgcn_s_sleep(1);
             }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         __syncthreads();
         if (bad) {
@@ -120,19 +126,20 @@ __global__ __launch_bounds__(256) void k_phase_persistent(double* x, double* y, 
 
 }  // namespace
 
-extern "C" int ddpca_probe_grid_barrier(int device, int64_t n, int phases, int blocks, double* out4) {
+extern "C" int ddpca_probe_grid_barrier(int device, int64_t n, int phases, int blocks, int pin, double* out4) {
     return guarded([&] {
-        if (!out4 || n < 1024 || n > ((int64_t)1 << 28) || phases < 2 || phases > 4096 || blocks < 1)
+        if (!out4 || n < 1024 || n > ((int64_t)1 << 28) || phases < 2 || phases > 4096 || blocks < 1 || (pin != 0 && pin != 1))
             throw ApiError(DDPCA_EINVAL, "ddpca_probe_grid_barrier: arguments");
         select_device(device);
         int cus = 256;
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0) cus = prop.multiProcessorCount;
-        if (blocks > cus) throw ApiError(DDPCA_EINVAL, "ddpca_probe_grid_barrier: at most one workgroup per CU");
+        if (blocks > (pin ? cus / 8 : cus)) throw ApiError(DDPCA_EINVAL, "ddpca_probe_grid_barrier: at most one workgroup per CU (of one XCD with pin)");
+        const int grid = pin ? 8 * blocks : blocks;
         std::vector<double> h(n);
         for (int64_t i = 0; i < n; ++i) h[i] = (double)((i * 2654435761ll) % 1000003);
         DevBuf<double> xg, yg, xp, yp;
-        DevBuf<unsigned> sync(2);
+        DevBuf<unsigned> sync(1);
         DevBuf<int> err(1);
         sync.zero();
         err.zero();
@@ -166,11 +173,11 @@ extern "C" int ddpca_probe_grid_barrier(int device, int64_t n, int phases, int b
         // persistent launch
         xp.upload(h);
         yp.alloc(n);
-        hipLaunchKernelGGL(k_phase_persistent, dim3(blocks), dim3(256), 0, st, xp.p, yp.p, n, 2, sync.p, sync.p + 1, err.p);
+        hipLaunchKernelGGL(k_phase_persistent, dim3(grid), dim3(256), 0, st, xp.p, yp.p, n, 2, blocks, pin, sync.p, err.p);
         DDPCA_HIP(hipMemcpyAsync(xp.p, h.data(), n * sizeof(double), hipMemcpyHostToDevice, st));
+        DDPCA_HIP(hipMemsetAsync(sync.p, 0, sizeof(unsigned), st));
         DDPCA_HIP(hipEventRecord(e0, st));
-        hipLaunchKernelGGL(k_phase_persistent, dim3(blocks), dim3(256), 0, st, xp.p, yp.p, n, phases, sync.p, sync.p + 1,
-                           err.p);
+        hipLaunchKernelGGL(k_phase_persistent, dim3(grid), dim3(256), 0, st, xp.p, yp.p, n, phases, blocks, pin, sync.p, err.p);
         DDPCA_HIP(hipEventRecord(e1, st));
         const double ms_pers = elapsed();
         DDPCA_HIP(hipStreamSynchronize(st));

@@ -33,17 +33,8 @@ extern "C" {
 const char* ddpca_last_error(void);
 /* 1 if a gfx950 device is visible, 0 otherwise (no HIP context is created otherwise) */
 int ddpca_gpu_available(void);
-/* Measurement only (no reference counterpart; SURVEY §8 d3's measured STREAM ceiling): a STREAM copy
- * and a STREAM read of `bytes` per buffer (>= 64 MiB; use >> the 256 MiB Infinity Cache), 16 B per
- * lane, non-temporal, best of three batches of `reps` launches on a stream of its own.
- * out4 = [copy GB/s (bytes read + written), read GB/s, copy ms, read ms]. */
-int ddpca_stream_ceiling(int device, int64_t bytes, int reps, double* out4);
-/* Measurement only (the persistent below-fine V-cycle): `phases` dependent passes over n
- * doubles, each reading what other workgroups wrote in the previous pass, run as one hipGraph of
- * `phases` launches and as one persistent launch with an agent-scope grid barrier between passes,
- * `blocks` (<= CUs) workgroups of 256 each way.  out4 = [graph us per pass, persistent us per pass,
- * max |difference| of the two results, 1 if a persistent workgroup timed out waiting]. */
-int ddpca_probe_grid_barrier(int device, int64_t n, int phases, int blocks, double* out4);
+/* (the measurement probes -- STREAM ceiling, grid barrier -- are in libddpca_probe.so,
+ * include/ddpca_probe.h) */
 
 /* ========================================================================================
  * MGPIS -- multigrid-preconditioned CG on one subdomain (MGPIS.h:8-225)
@@ -437,6 +428,14 @@ int mcontact_gpu_unique_id(void* out128);
  * matrix) with the same multi-rank bookkeeping, so a multi-rank run can be checked on one GPU.
  * Each handle's mcontact_gpu_iterate must then be called from its own host thread. */
 int mcontact_gpu_comm_local(mcontact_t* handles, int n);
+/* Timing transport (no reference counterpart; profiles/one_rank_probe.py): one rank of an
+ * nranks > 1 layout alone on a GPU.  Every receive from peer p gets what this rank sent p (an
+ * on-device copy on the solve stream) and the all-reduces keep this rank's own values, so the
+ * numbers are NOT the N-rank answer but the work is one rank's: its subdomains' solves, its
+ * interface sides, its rows of the coarse solve, with the communication left out.  p = the
+ * problem h was created from, established in full: it completes the dense coarse operator that the
+ * setup all-reduce would sum. */
+int mcontact_gpu_comm_loopback(mcontact_t h, ddpca_problem_t p);
 /* Run up to maxit ADMM iterations (reference maxiIter = 3000) from the current state;
  * stop on MONITOR convergence (MCONTACT.h:2725-2845) when check != 0.
  * Returns the number of iterations run (>= 0) or a negative error. */

@@ -191,7 +191,7 @@ def price_iteration(P, mc, budget_s: float = 20.0, ref_exe=None, ref_threads: in
         ref = {"value": 1.0 / (t_body_ref + t_coarse + t_iface), "unit": "ADMM it/s", "cores": rc["threads"],
                "kind": "reference",
                "sample": f"the reference's own MGPIS::CG_SOLV(1) (oracle/_ref/ref_harness_portable time_cg_ops) on "
-                         f"subdomains {[x['subdomain'] for x in solves]} ({solves[0]['n']} DOF each, "
+                         f"subdomains {[x['subdomain'] for x in solves]} ({[x['n'] for x in solves]} DOF, "
                          f"{[x['iters'] for x in solves]} iterations, {[round(x['cg_s'], 2) for x in solves]} s) "
                          f"priced x{nsub / len(solves):g} = {t_body_ref:.1f} s; coarse space {t_coarse:.2f} s and "
                          f"interface step {t_iface:.2f} s by the port",

@@ -8,10 +8,11 @@ import numpy as np
 import pytest
 
 HEADER = Path(__file__).resolve().parents[1] / "include" / "ddpca_amd.h"
+PROBE_HEADER = HEADER.with_name("ddpca_probe.h")
 
 
-def declared():
-    text = HEADER.read_text()
+def declared(header=HEADER):
+    text = header.read_text()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
     return sorted(set(re.findall(r"\b((?:ddpca|mgpis|mcontact)_\w+)\s*\(", text)))
 
@@ -22,6 +23,16 @@ def test_exports_every_declared_symbol(ddpca):
     assert len(names) >= 20
     missing = [n for n in names if not hasattr(L, n)]
     assert not missing, missing
+
+
+def test_probes_live_in_their_own_library(ddpca):
+    """The measurement probes (include/ddpca_probe.h) are exported by libddpca_probe.so, not by the
+    product library."""
+    names = declared(PROBE_HEADER)
+    assert names == ["ddpca_probe_grid_barrier", "ddpca_stream_ceiling"]
+    P = ddpca.probe_lib()
+    assert all(hasattr(P, n) for n in names)
+    assert not any(hasattr(ddpca.lib(), n) for n in names)
 
 
 def test_built_for_gfx950_only():

@@ -232,6 +232,36 @@ def test_admm_coarse_space_matches_oracle_on_generated_problem(ddpca, oracle, gp
         assert np.linalg.norm(u - ur) <= 1e-7 * np.linalg.norm(ur)
 
 
+def test_loopback_timing_transport(ddpca, gpu):
+    """mcontact_gpu_comm_loopback (profiles/one_rank_probe.py: one rank of the N = 8 layout timed on
+    one GPU): each rank of a four-rank layout of the coarse-space chain, alone on the GPU with its
+    exchanges handed back to itself, runs a fixed number of ADMM iterations with its own PCG solves
+    (a rank's share, not the answer); a rank-locally established problem cannot complete the dense
+    coarse operator and is refused."""
+    P = ddpca.Problem("dehw", 2, 2, 2, 1, 2, 0.3)
+    P.set_coarse(2, [1] * P.nsub)
+    P.ESTABLISH()
+    owner = [tv % 4 for tv in range(P.nsub)]
+    for r in range(4):
+        mc = ddpca.MCONTACT(P, rank=r, nranks=4, owner=owner)
+        with pytest.raises(ddpca.DdpcaError):
+            mc.CONTACT_ANALYSIS(1, check=False)  # no transport yet
+        mc.comm_loopback()
+        assert mc.CONTACT_ANALYSIS(5, check=False) == 5
+        tm = mc.timing()
+        assert tm["pcg_iterations"] > 0 and tm["owned_dofs"] > 0
+        for tv in range(P.nsub):
+            if owner[tv] == r:
+                assert np.all(np.isfinite(mc.get("resuDisp", tv)))
+        del mc
+    Q = ddpca.Problem("dehw", 2, 2, 2, 1, 2, 0.3)
+    Q.set_coarse(2, [1] * Q.nsub)
+    Q.ESTABLISH(owner, 1)
+    mc = ddpca.MCONTACT(Q, rank=1, nranks=4, owner=owner)
+    with pytest.raises(ddpca.DdpcaError):
+        mc.comm_loopback()
+
+
 def test_admm_latin_matches_oracle_on_generated_problem(ddpca, oracle, gpu):
     """The same chain with the LATIN-type coarse space built by the host MULTISCALE (muscSett =
     1): fixed-k trajectory against the CPU oracle applying the same operators (MCONTACT.h:
