@@ -313,7 +313,8 @@ def run_general_child(a) -> dict:
     cmd = [sys.executable, str(Path(__file__).resolve()), "--mesh", "general", "--no-general", "--no-cpu-baseline",
            "--no-stream-ceiling", "--steps", str(a.steps), "--warmup", str(a.warmup), "--groups", str(a.groups),
            "--nx", str(a.nx), "--ny", str(a.ny), "--nz", str(a.nz), "--gl", str(a.gl), "--fric", str(a.fric),
-           "--ip-contact", str(a.ip_contact), "--ip-glued", str(a.ip_glued)]
+           "--ip-contact", str(a.ip_contact), "--ip-glued", str(a.ip_glued),
+           "--traffic-json", str(ROOT / "profiles" / "traffic_general.json")]
     env = dict(os.environ, DDPCA_LATTICE="0")
     t0 = time.perf_counter()
     log(0, "general-mesh line (child process) ...")

@@ -53,6 +53,7 @@ def main():
                  ("table-mode", H["table_mode"])]:
         ap.add_argument(f"--{k}", type=int, default=d)
     ap.add_argument("--value-layout", default="fp64-pairs, col16")
+    ap.add_argument("--mesh", default="headline", help="general: bench.py --mesh general's line (profiles/traffic_general.json)")
     ap.add_argument("--out", default=str(Path(__file__).resolve().parent / "traffic.json"))
     a = ap.parse_args()
     fetch = full_launches(per_launch(a.fetch_csv, "FETCH_SIZE"))
@@ -61,7 +62,8 @@ def main():
     res = {
         "kernel": "k_sell<kPcg> fine level",
         "config": dict(groups=a.groups, nx=a.nx, ny=a.ny, nz=a.nz, gl=a.gl, smoother=a.smoother, nu=a.nu,
-                       precond_fp32=a.precond_fp32, table_mode=a.table_mode, value_layout=a.value_layout),
+                       precond_fp32=a.precond_fp32, table_mode=a.table_mode, value_layout=a.value_layout,
+                       **({} if a.mesh == "headline" else {"mesh": a.mesh})),
         "fetch_size_kb_median": fkb,
         "write_size_kb_median": wkb,
         "launches_used": [len(fetch), len(write)],

@@ -4,7 +4,10 @@ is connected to the timing transport mcontact_gpu_comm_loopback -- every gamma h
 back to itself, the all-reduces keep its own values -- and its ADMM iterations are timed as bench.py
 times them.  What is measured is one rank's whole share of the iteration (its subdomains' PCG
 solves with the coarse-space correction, its interface sides, the mass solves, MONITOR) without
-the RCCL traffic; the numbers themselves are not the N-rank answer.
+the RCCL traffic; the numbers themselves are not the N-rank answer.  A rank whose subdomains are
+all worms never sees the loaded wheels here: its right-hand sides stay zero and its PCG solves exit
+at once, so the wheel ranks (odd ranks at N = 8) are the ones that time the solves -- in the real
+run a worm's PCG takes the same iteration count as a wheel's (cpu_baseline: 15 and 15).
 
     python profiles/one_rank_probe.py OUT.json [--layouts 8:0,8:1,4:0,2:0] [--steps 10] [--warmup 2]
 

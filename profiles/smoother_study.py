@@ -9,6 +9,10 @@ could run at equal fine-level operator passes:
   mcgs_fine  mcgs on the finest level only, bj below
   mcgs_coarse  bj on the finest level, mcgs below
   sgs    the reference's lexicographic point SGS (MGPIS.h:61-114) for comparison
+  hgs_fine   hybrid (tile-local) multicolour GS on the finest level, bj below: the colours are swept
+         inside 3D tiles of nodes (--tile tx,ty,tz, default 16,16,8), couplings across tiles read the
+         values from before the sweep (block Jacobi over tiles, GS inside: what one launch per sweep
+         with x in LDS would compute; symmetric, as the backward sweep is the forward one's adjoint)
 
     python profiles/smoother_study.py [gl] [subdomain]
 """
@@ -27,8 +31,13 @@ sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 D = importlib.import_module("ddpca-admm_amd")
 
 
+TILE = (16, 16, 8)
+
+
 def hierarchy(gl: int, tv: int):
     P = D.headline_problem(gl=gl).ESTABLISH()
+    global COORD
+    COORD = np.asarray(P.array("coords", tv), dtype=np.float64).reshape(-1, 3)
     G = P.grid(tv)
     L = G.maxiLeve
     nn = [int(x) for x in P.array("leveCount", tv)]
@@ -113,20 +122,55 @@ class VCycle:
                 lam = spl.eigsh(spl.LinearOperator(K[l].shape, matvec=lambda x, l=l: bd.apply(K[l] @ x)), k=1,
                                 which="LM", return_eigenvectors=False, tol=1e-3)[0]
                 self.omega[l] = 1.7 / lam
-            elif smoother.startswith("mcgs"):
+            elif smoother.startswith("mcgs") or smoother.startswith("hgs"):
                 c = colouring(K[l], node[l])
                 self.rows[l] = [np.nonzero(c == k)[0] for k in range(c.max() + 1)]
                 self.Krows[l] = [K[l][r] for r in self.rows[l]]
+                if smoother.startswith("hgs"):
+                    # tile of every dof: 3D blocks of TILE nodes on the level's node lattice
+                    xyz = COORD[node[l]]
+                    tid = np.zeros(len(xyz), dtype=np.int64)
+                    for d in range(3):
+                        u = np.unique(np.round(COORD[np.unique(node[l])][:, d], 12))
+                        idx = np.searchsorted(u, np.round(xyz[:, d], 12))
+                        tid = tid * (len(u) // TILE[d] + 2) + idx // TILE[d]
+                    self.split = getattr(self, "split", {})
+                    sp_l = []
+                    for r, Kr in zip(self.rows[l], self.Krows[l]):
+                        Kc = Kr.tocoo()
+                        same = tid[r][Kc.row] == tid[Kc.col]
+                        Kin = sp.csr_matrix((Kc.data[same], (Kc.row[same], Kc.col[same])), shape=Kr.shape)
+                        Koff = sp.csr_matrix((Kc.data[~same], (Kc.row[~same], Kc.col[~same])), shape=Kr.shape)
+                        sp_l.append((Kin, Koff))
+                    self.split[l] = sp_l
+                    self.ntile = len(np.unique(tid))
+                    if "l1" in smoother:
+                        # l1 hybrid GS (Baker, Falgout, Kolev, Yang 2011): each row's diagonal gets the
+                        # absolute sum of its off-tile couplings, which makes the tile-Jacobi smoother
+                        # convergent whatever the coupling
+                        Kc = K[l].tocoo()
+                        off = tid[Kc.row] != tid[Kc.col]
+                        l1 = np.bincount(Kc.row[off], weights=np.abs(Kc.data[off]), minlength=K[l].shape[0])
+                        self.bd[l] = BlockDiag(K[l] + sp.diags(l1), node[l])
             elif smoother == "sgs":
                 self.tri[l] = (sp.tril(K[l], format="csr"), sp.triu(K[l], format="csr"))
 
     def is_bj(self, l):
-        return self.sm == "bj" or (self.sm == "mcgs_fine" and l < self.L) or (self.sm == "mcgs_coarse" and l == self.L)
+        return self.sm == "bj" or (self.sm in ("mcgs_fine", "hgs_fine", "hgs_l1_fine") and l < self.L) or \
+            (self.sm == "mcgs_coarse" and l == self.L)
 
     def smooth(self, l, x, b, forward: bool):
         K = self.K[l]
         if self.is_bj(l):
             return x + self.omega[l] * self.bd[l].apply(b - K @ x)
+        if self.sm.startswith("hgs"):
+            order = range(len(self.rows[l])) if forward else reversed(range(len(self.rows[l])))
+            x0, x = x, x.copy()
+            for k in order:
+                r = self.rows[l][k]
+                Kin, Koff = self.split[l][k]
+                x[r] += self.bd[l].apply(b[r] - Kin @ x - Koff @ x0, r)
+            return x
         if self.sm.startswith("mcgs"):
             order = range(len(self.rows[l])) if forward else reversed(range(len(self.rows[l])))
             x = x.copy()
@@ -188,6 +232,9 @@ def round_h16(K, node):
 
 
 def main():
+    global TILE
+    if "--tile" in sys.argv:
+        TILE = tuple(int(v) for v in sys.argv[sys.argv.index("--tile") + 1].split(","))
     gl = int(sys.argv[1]) if len(sys.argv) > 1 else 4
     tv = int(sys.argv[2]) if len(sys.argv) > 2 else 0
     K, Pr, node, b = hierarchy(gl, tv)
@@ -206,7 +253,8 @@ def main():
         it, x = pcg(K[-1], b, lambda r: V.apply(V.L, r))
         res = np.linalg.norm(b - K[-1] @ x) / np.linalg.norm(b)
         ncol = max((len(v) for v in V.rows.values()), default=0)
-        print(f"{sm:5s} PCG iterations {it:3d}  true relres {res:.2e}  colours {ncol}  ({time.time() - t:.1f} s)")
+        extra = f"  tiles {V.ntile} of {TILE}" if sm.startswith("hgs") else ""
+        print(f"{sm:5s} PCG iterations {it:3d}  true relres {res:.2e}  colours {ncol}{extra}  ({time.time() - t:.1f} s)")
 
 
 if __name__ == "__main__":
