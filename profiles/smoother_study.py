@@ -9,6 +9,9 @@ could run at equal fine-level operator passes:
   mcgs_fine  mcgs on the finest level only, bj below
   mcgs_coarse  bj on the finest level, mcgs below
   sgs    the reference's lexicographic point SGS (MGPIS.h:61-114) for comparison
+  mcgs_band  (--general: bench.py's general mesh, contact band refined once more) mcgs on the finest
+         level restricted to the band -- the rows of the nodes level L adds to level L-1 and their
+         K_L neighbours -- bj below (level L-1 already smooths the unrefined rows' identical stencils)
   hgs_fine   hybrid (tile-local) multicolour GS on the finest level, bj below: the colours are swept
          inside 3D tiles of nodes (--tile tx,ty,tz, default 16,16,8), couplings across tiles read the
          values from before the sweep (block Jacobi over tiles, GS inside: what one launch per sweep
@@ -34,13 +37,17 @@ D = importlib.import_module("ddpca-admm_amd")
 TILE = (16, 16, 8)
 
 
+GENERAL = False
+
+
 def hierarchy(gl: int, tv: int):
-    P = D.headline_problem(gl=gl).ESTABLISH()
-    global COORD
+    P = D.headline_problem(gl=gl, **(D.GENERAL_FEATURES if GENERAL else {})).ESTABLISH()
+    global COORD, NN
     COORD = np.asarray(P.array("coords", tv), dtype=np.float64).reshape(-1, 3)
     G = P.grid(tv)
     L = G.maxiLeve
     nn = [int(x) for x in P.array("leveCount", tv)]
+    NN = nn
     flag = np.asarray(P.array("consFlag", tv))
     K = [G.consStif(l).tocsr() for l in range(L + 1)]
     Pr = [G.realProl(l).tocsr() for l in range(L)]
@@ -125,6 +132,12 @@ class VCycle:
             elif smoother.startswith("mcgs") or smoother.startswith("hgs"):
                 c = colouring(K[l], node[l])
                 self.rows[l] = [np.nonzero(c == k)[0] for k in range(c.max() + 1)]
+                if smoother == "mcgs_band" and l == self.L:
+                    new = (node[l] >= NN[l - 1]).astype(np.float64)
+                    A = sp.csr_matrix((np.ones(K[l].nnz), K[l].indices, K[l].indptr), shape=K[l].shape)
+                    band = (new > 0) | ((A @ new) > 0)
+                    self.band_rows = int(band.sum())
+                    self.rows[l] = [r[band[r]] for r in self.rows[l]]
                 self.Krows[l] = [K[l][r] for r in self.rows[l]]
                 if smoother.startswith("hgs"):
                     # tile of every dof: 3D blocks of TILE nodes on the level's node lattice
@@ -156,7 +169,7 @@ class VCycle:
                 self.tri[l] = (sp.tril(K[l], format="csr"), sp.triu(K[l], format="csr"))
 
     def is_bj(self, l):
-        return self.sm == "bj" or (self.sm in ("mcgs_fine", "hgs_fine", "hgs_l1_fine") and l < self.L) or \
+        return self.sm == "bj" or (self.sm in ("mcgs_fine", "hgs_fine", "hgs_l1_fine", "mcgs_band") and l < self.L) or \
             (self.sm == "mcgs_coarse" and l == self.L)
 
     def smooth(self, l, x, b, forward: bool):
@@ -232,7 +245,8 @@ def round_h16(K, node):
 
 
 def main():
-    global TILE
+    global TILE, GENERAL
+    GENERAL = "--general" in sys.argv
     if "--tile" in sys.argv:
         TILE = tuple(int(v) for v in sys.argv[sys.argv.index("--tile") + 1].split(","))
     gl = int(sys.argv[1]) if len(sys.argv) > 1 else 4
@@ -253,7 +267,8 @@ def main():
         it, x = pcg(K[-1], b, lambda r: V.apply(V.L, r))
         res = np.linalg.norm(b - K[-1] @ x) / np.linalg.norm(b)
         ncol = max((len(v) for v in V.rows.values()), default=0)
-        extra = f"  tiles {V.ntile} of {TILE}" if sm.startswith("hgs") else ""
+        extra = f"  tiles {V.ntile} of {TILE}" if sm.startswith("hgs") else \
+            f"  band rows {V.band_rows} of {K[-1].shape[0]}" if sm == "mcgs_band" else ""
         print(f"{sm:5s} PCG iterations {it:3d}  true relres {res:.2e}  colours {ncol}{extra}  ({time.time() - t:.1f} s)")
 
 
