@@ -546,6 +546,50 @@ __global__ __launch_bounds__(kWave) void k_gs(GsArgs a) {
     if (DOT) chunk_partial(dotv, a.partial, c);
 }
 
+// Band mode's rows outside the colours (GsFine::band; one wave per chunk of the ring / far groups):
+// PH 5: x = 0, r = b before the forward sweep (the ring's r is recomputed by PH 3); PH 3: the
+// ring's residual r = b - K x over its stored band columns (x is zero elsewhere after the forward
+// sweep from zero); PH 4: the dot product's chunk partial b . x of rows the backward sweep leaves
+// as the prolongation wrote them
+template <int PH, typename T, typename CT>
+__global__ __launch_bounds__(kWave) void k_gs_aux(GsArgs a) {
+    const int lane = threadIdx.x;
+    const int64_t li = blockIdx.x;
+    if (li >= a.n) return;
+    const int64_t c = a.list[li];
+    const int sub = a.csub[c];
+    if (stopped(a.sc, sub)) return;
+    const int32_t rr = a.rowidx[c * kChunk + lane];
+    const bool real = rr >= 0;
+    const int64_t row = real ? rr : ~rr;
+    const int64_t o = 3 * row;
+    if (PH == 5) {
+        if (real)
+            for (int e = 0; e < 3; ++e) {
+                a.x[o + e] = 0.0;
+                a.r[o + e] = a.b[o + e];
+            }
+        return;
+    }
+    if (PH == 4) {
+        const double d = real ? __builtin_fma(a.b[o + 2], a.x[o + 2], __builtin_fma(a.b[o + 1], a.x[o + 1], a.b[o] * a.x[o])) : 0.0;
+        chunk_partial(d, a.partial, c);
+        return;
+    }
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+    const CT* colp;
+    if constexpr (sizeof(CT) == 2) colp = a.col16;
+    else colp = a.col;
+    constexpr int64_t SV = slot_vals<T>() * kChunk;
+    const int64_t q = a.offl[c];
+    sell_rows<1, T, CT>(colp + q * kChunk + lane, static_cast<const T*>(a.val) + q * SV + lane, a.x, a.nsl[c], row, s0, s1, s2);
+    if (real) {
+        a.r[o] = a.b[o] - s0;
+        a.r[o + 1] = a.b[o + 1] - s1;
+        a.r[o + 2] = a.b[o + 2] - s2;
+    }
+}
+
 // Node-parallel kernels: thread = node, 256 nodes per workgroup; a wavefront is one chunk, so
 // the subdomain (and its stop flag) is uniform per wavefront.  nn is a multiple of 64.
 #define NODE_PROLOGUE(nn, csub, sc)                         \
@@ -1546,8 +1590,10 @@ bool lattice_transfer(LevelDev& L, const LevelDev& C, const std::vector<int32_t>
 // columns, val: masked fp64 blocks val[(q * 9 + ij) * 64 + lane]); vt: the V-cycle copy's type.
 // A colour's rows go to chunks in device order, i.e. along the x lines of a box (16 x 16-node
 // tiles of one plane measured 1.8 % slower at the headline, profiles/r03i).
+// band (optional, per device node of the level): colour and sweep only the flagged rows; the others
+// go to the ring group (a flagged neighbour) or the far group (none) -- GsFine::band
 void build_gs(GsFine& G, const LevelDev& L, int nsub, const std::vector<int64_t>& off, const std::vector<int32_t>& col,
-              const std::vector<double>& val, int vt) {
+              const std::vector<double>& val, int vt, const std::vector<uint8_t>* band = nullptr) {
     // greedy colouring in device order, per member
     std::vector<int8_t> colour(L.nn, -1);
     std::vector<int> ncol_sub(nsub, 0);
@@ -1555,6 +1601,7 @@ void build_gs(GsFine& G, const LevelDev& L, int nsub, const std::vector<int64_t>
 #pragma omp parallel for schedule(dynamic, 1) reduction(max : too_many)
     for (int s = 0; s < nsub; ++s) {
         for (int64_t g = L.noff[s]; g < L.noff[s] + L.nloc[s]; ++g) {
+            if (band && !(*band)[g]) continue;
             const int64_t c = g / kChunk, lane = g % kChunk;
             uint64_t used = 0;
             for (int64_t q = off[c]; q < off[c + 1]; ++q) {
@@ -1572,27 +1619,54 @@ void build_gs(GsFine& G, const LevelDev& L, int nsub, const std::vector<int64_t>
     }
     if (too_many) throw ApiError(DDPCA_EINVAL, "multicolour smoother: a node graph needing more than 64 colours");
     const int K = *std::max_element(ncol_sub.begin(), ncol_sub.end());
+    // chunk groups per member: the colours, then (band mode) the ring and the far rows
+    const int KG = band ? K + 2 : K;
+    auto is_band = [&](int64_t j) { return colour[j] >= 0; };
     // colour chunks, member-major and colour-minor
-    std::vector<std::vector<int64_t>> rows((size_t)nsub * K);
+    std::vector<std::vector<int64_t>> rows((size_t)nsub * KG);
     for (int s = 0; s < nsub; ++s)
-        for (int64_t g = L.noff[s]; g < L.noff[s] + L.nloc[s]; ++g) rows[(size_t)s * K + colour[g]].push_back(g);
+        for (int64_t g = L.noff[s]; g < L.noff[s] + L.nloc[s]; ++g) {
+            int grp = colour[g];
+            if (grp < 0) {
+                grp = K + 1;  // far unless a neighbour is in the band
+                const int64_t nc = g / kChunk, lane = g % kChunk;
+                for (int64_t q = off[nc]; q < off[nc + 1] && grp == K + 1; ++q) {
+                    const int64_t j = col[q * kChunk + lane];
+                    if (j != g && is_band(j)) grp = K;
+                }
+            }
+            rows[(size_t)s * KG + grp].push_back(g);
+        }
+    // which neighbours a row of group k stores: colours L = earlier colours and every non-band
+    // column (x = 0 there in the forward sweep), U = the rest; ring rows: their band columns as L
+    auto store = [&](int k, int64_t j) -> int {  // 0 L, 1 U, -1 not stored
+        if (k < K) return colour[j] < k ? 0 : 1;
+        if (k == K) return is_band(j) ? 0 : -1;
+        return -1;
+    };
     std::vector<int32_t> rowidx, csub, nsl, nsu;
     std::vector<int64_t> offl, offu, cb(nsub + 1, 0);
-    std::vector<std::vector<int32_t>> bycol(K);
+    std::vector<std::vector<int32_t>> bycol(KG);
     std::vector<int64_t> base;  // first row of each chunk in its (s, k) list
     std::vector<size_t> lists;
     G.nnzb_sub.assign(nsub, 0);
     G.slots_sub.assign(nsub, 0);
+    G.band = band != nullptr;
+    G.band_rows_sub.assign(nsub, 0);
+    G.ring_rows_sub.assign(nsub, 0);
+    G.far_rows_sub.assign(nsub, 0);
+    G.ring_nnzb_sub.assign(nsub, 0);
     for (int s = 0; s < nsub; ++s) {
         cb[s] = (int64_t)csub.size();
-        for (int k = 0; k < K; ++k) {
-            const auto& R = rows[(size_t)s * K + k];
+        for (int k = 0; k < KG; ++k) {
+            const auto& R = rows[(size_t)s * KG + k];
+            (k < K ? G.band_rows_sub : k == K ? G.ring_rows_sub : G.far_rows_sub)[s] += (int64_t)R.size();
             for (size_t r0 = 0; r0 < R.size(); r0 += kChunk) {
                 const int64_t c = (int64_t)csub.size();
                 bycol[k].push_back((int32_t)c);
                 csub.push_back(s);
                 base.push_back((int64_t)r0);
-                lists.push_back((size_t)s * K + k);
+                lists.push_back((size_t)s * KG + k);
                 int32_t ml = 0, mu = 0;
                 for (size_t i = r0; i < std::min(R.size(), r0 + kChunk); ++i) {
                     const int64_t g = R[i], nc = g / kChunk, lane = g % kChunk;
@@ -1600,12 +1674,13 @@ void build_gs(GsFine& G, const LevelDev& L, int nsub, const std::vector<int64_t>
                     for (int64_t q = off[nc]; q < off[nc + 1]; ++q) {
                         const int64_t j = col[q * kChunk + lane];
                         if (j == g) continue;
-                        if (colour[j] < k) ++nl;
-                        else ++nu;
+                        const int t = store(k, j);
+                        if (t == 0) ++nl;
+                        else if (t == 1) ++nu;
                     }
                     ml = std::max(ml, nl);
                     mu = std::max(mu, nu);
-                    G.nnzb_sub[s] += nl + nu;
+                    (k < K ? G.nnzb_sub : G.ring_nnzb_sub)[s] += nl + nu;
                 }
                 nsl.push_back(ml);
                 nsu.push_back(mu);
@@ -1633,7 +1708,7 @@ void build_gs(GsFine& G, const LevelDev& L, int nsub, const std::vector<int64_t>
 #pragma omp parallel for schedule(dynamic, 64)
     for (int64_t c = 0; c < nch; ++c) {
         const auto& R = rows[lists[c]];
-        const int k = (int)(lists[c] % K);
+        const int k = (int)(lists[c] % KG);
         const int64_t r0 = base[c], nr = std::min<int64_t>(kChunk, (int64_t)R.size() - r0);
         for (int64_t lane = 0; lane < kChunk; ++lane) {
             const bool real = lane < nr;
@@ -1650,7 +1725,9 @@ void build_gs(GsFine& G, const LevelDev& L, int nsub, const std::vector<int64_t>
             for (int64_t q = off[nc]; q < off[nc + 1]; ++q) {
                 const int64_t j = col[q * kChunk + nl];
                 if (j == g) continue;
-                const int64_t t = colour[j] < k ? ql++ : qu++;
+                const int st = store(k, j);
+                if (st < 0) continue;
+                const int64_t t = st == 0 ? ql++ : qu++;
                 if (c16) gcol16[t * kChunk + lane] = (int16_t)(j - g);
                 else gcol[t * kChunk + lane] = (int32_t)j;
                 double blk[9];
@@ -1679,7 +1756,7 @@ void build_gs(GsFine& G, const LevelDev& L, int nsub, const std::vector<int64_t>
         std::vector<int32_t> seen_f(L.nn, -1), seen_b(L.nn, -1), seen_r(L.nn, 0);
         for (int k = 0; k < K; ++k)
             for (int s = 0; s < nsub; ++s)
-                for (int64_t g : rows[(size_t)s * K + k]) {
+                for (int64_t g : rows[(size_t)s * KG + k]) {
                     rows_k[k] += 1.0;
                     const int64_t nc = g / kChunk, lane = g % kChunk;
                     for (int64_t q = off[nc]; q < off[nc + 1]; ++q) {
@@ -1706,10 +1783,10 @@ void build_gs(GsFine& G, const LevelDev& L, int nsub, const std::vector<int64_t>
     }
     G.ncol = K;
     G.nchunk = nch;
-    G.first.assign(K, 0);
-    G.count.assign(K, 0);
+    G.first.assign(KG, 0);
+    G.count.assign(KG, 0);
     std::vector<int32_t> list;
-    for (int k = 0; k < K; ++k) {
+    for (int k = 0; k < KG; ++k) {
         G.first[k] = (int64_t)list.size();
         G.count[k] = (int64_t)bycol[k].size();
         list.insert(list.end(), bycol[k].begin(), bycol[k].end());
@@ -1739,9 +1816,13 @@ void build_gs(GsFine& G, const LevelDev& L, int nsub, const std::vector<int64_t>
     if (vt == kValH16) G.val16.upload(v16);
     else if (vt == kVal32) G.val32.upload(v32);
     else G.val64.upload(v64);
-    if (std::getenv("DDPCA_VERBOSE"))
-        std::fprintf(stderr, "[ddpca] fine level: multicolour Gauss-Seidel, %d colours, %lld chunks, %lld slots\n", K,
-                     (long long)nch, (long long)nslot);
+    if (std::getenv("DDPCA_VERBOSE")) {
+        int64_t nb = 0, nr = 0, nf = 0;
+        for (int s = 0; s < nsub; ++s) nb += G.band_rows_sub[s], nr += G.ring_rows_sub[s], nf += G.far_rows_sub[s];
+        std::fprintf(stderr, "[ddpca] fine level: multicolour Gauss-Seidel, %d colours, %lld chunks, %lld slots%s\n", K,
+                     (long long)nch, (long long)nslot,
+                     band ? (", band " + std::to_string(nb) + " / ring " + std::to_string(nr) + " / far " + std::to_string(nf) + " rows").c_str() : "");
+    }
 }
 }  // namespace
 
@@ -1970,7 +2051,34 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
         if (l == nlev - 1 && nlev > 1 && opt.smoother == 3) {
             // the V-cycle copy's storage type of this level (vc_type once the level is up)
             const int vt = (!vc32 || L.tbl) ? kVal64 : L.val16.p ? kValH16 : kVal32;
-            build_gs(gs, L, nsub, off, col, val, vt);
+            // band mode (locally refined fine level): sweep only the nodes this level
+            // adds to level l - 1 (reference positions past nnodes[l - 1]) and their neighbours --
+            // elsewhere the stencils are level l - 1's, which the V-cycle smooths next -- when that
+            // is at most 60 % of the rows; DDPCA_GS_BAND=0 sweeps every row
+            std::vector<uint8_t> bandv;
+            const char* be = std::getenv("DDPCA_GS_BAND");
+            if (!(be && be[0] == '0')) {
+                bandv.assign(L.nn, 0);
+                int64_t nreal = 0, nband = 0;
+                for (int s = 0; s < nsub; ++s) {
+                    nreal += L.nloc[s];
+                    for (int64_t ref = subs[s].nnodes[l - 1]; ref < subs[s].nnodes[l]; ++ref)
+                        bandv[L.noff[s] + perm[l][s][ref]] = 2;  // new node
+                }
+                for (int64_t g = 0; g < L.nn; ++g) {
+                    if (bandv[g] != 2) continue;
+                    const int64_t c = g / kChunk, lane = g % kChunk;
+                    for (int64_t q = off[c]; q < off[c + 1]; ++q) {
+                        bool nz = false;
+                        for (int ij = 0; ij < 9 && !nz; ++ij) nz = val[(q * 9 + ij) * kChunk + lane] != 0.0;
+                        const int64_t j = col[q * kChunk + lane];
+                        if (nz && bandv[j] == 0) bandv[j] = 1;
+                    }
+                }
+                for (uint8_t f : bandv) nband += f != 0;
+                if (nband == 0 || nband > (nreal * 3) / 5) bandv.clear();
+            }
+            build_gs(gs, L, nsub, off, col, val, vt, bandv.empty() ? nullptr : &bandv);
         }
         L.mask.upload(mask);
         for (auto* v : {&L.x, &L.t, &L.b, &L.r, &L.d}) {
@@ -2583,13 +2691,31 @@ void launch_gs_t(const GsArgs& a, bool c16, hipStream_t st) {  // c16: 16-bit co
     else hipLaunchKernelGGL((k_gs<PH, DOT, T, int32_t>), dim3((unsigned)a.n), dim3(kWave), 0, st, a);
 }
 
+template <int PH, typename T>
+void launch_gs_aux_t(const GsArgs& a, bool c16, hipStream_t st) {
+    if (c16) hipLaunchKernelGGL((k_gs_aux<PH, T, int16_t>), dim3((unsigned)a.n), dim3(kWave), 0, st, a);
+    else hipLaunchKernelGGL((k_gs_aux<PH, T, int32_t>), dim3((unsigned)a.n), dim3(kWave), 0, st, a);
+}
+
+// k >= 0: colour k; k = -1: every colour chunk (the residual); band mode: k = -2 the ring group,
+// k = -3 the ring and far groups (PH 3..5 run k_gs_aux)
 template <int PH, bool DOT>
 void launch_gs(const MgpisDevice& D, int k, double* x, const double* b, double* r, const PcgScal* scp, double* partial) {
     const GsFine& G = D.gs;
     const LevelDev& F = D.lev.back();
+    const int K = G.ncol;
     GsArgs a{};
-    a.list = k < 0 ? nullptr : G.list.p + G.first[k];
-    a.n = k < 0 ? G.nchunk : G.count[k];
+    if (k >= 0) {
+        a.list = G.list.p + G.first[k];
+        a.n = G.count[k];
+    } else if (k == -1) {
+        a.list = G.band ? G.list.p : nullptr;
+        a.n = G.band ? G.first[K] : G.nchunk;
+    } else {
+        if (!G.band) throw ApiError(DDPCA_ESTATE, "ring / far chunk groups without band mode");
+        a.list = G.list.p + G.first[K];
+        a.n = G.count[K] + (k == -3 ? G.count[K + 1] : 0);
+    }
     if (a.n == 0) return;
     a.rowidx = G.rowidx.p;
     a.csub = G.csub.p;
@@ -2611,15 +2737,18 @@ void launch_gs(const MgpisDevice& D, int k, double* x, const double* b, double* 
     if (G.val16.p) {
         a.val = G.val16.p;
         a.minv = F.minv32.p;
-        launch_gs_t<PH, DOT, uint16_t>(a, c16, D.stream);
+        if constexpr (PH >= 3) launch_gs_aux_t<PH, uint16_t>(a, c16, D.stream);
+        else launch_gs_t<PH, DOT, uint16_t>(a, c16, D.stream);
     } else if (G.val32.p) {
         a.val = G.val32.p;
         a.minv = F.minv32.p;
-        launch_gs_t<PH, DOT, float>(a, c16, D.stream);
+        if constexpr (PH >= 3) launch_gs_aux_t<PH, float>(a, c16, D.stream);
+        else launch_gs_t<PH, DOT, float>(a, c16, D.stream);
     } else {
         a.val = G.val64.p;
         a.minv = F.minv.p;
-        launch_gs_t<PH, DOT, double>(a, c16, D.stream);
+        if constexpr (PH >= 3) launch_gs_aux_t<PH, double>(a, c16, D.stream);
+        else launch_gs_t<PH, DOT, double>(a, c16, D.stream);
     }
 }
 }  // namespace
@@ -2679,9 +2808,12 @@ void MgpisDevice::vcycle(const double* rin, double* zout, bool dot) {
     if (gsf) cur[Lf] = zout;  // the Gauss-Seidel sweeps run in place
     // ---- descend
     if (gsf) {
-        // forward sweep from zero, colour by colour, then r = -U x in one launch
+        // forward sweep from zero, colour by colour, then r = -U x in one launch; band mode: the
+        // rows outside the colours start at x = 0, r = b, the ring's r = b - K x after the sweep
+        if (gs.band) launch_gs<5, false>(*this, -3, zout, rin, lev[Lf].r.p, scp, nullptr);
         for (int k = 0; k < gs.ncol; ++k) launch_gs<0, false>(*this, k, zout, rin, nullptr, scp, nullptr);
         launch_gs<1, false>(*this, -1, zout, nullptr, lev[Lf].r.p, scp, nullptr);
+        if (gs.band) launch_gs<3, false>(*this, -2, zout, rin, lev[Lf].r.p, scp, nullptr);
     } else {
         const LevelDev& F = lev[Lf];
         const int grid = ceil_div(F.nn, kBlock);
@@ -2763,6 +2895,8 @@ void MgpisDevice::vcycle(const double* rin, double* zout, bool dot) {
                 if (dot) launch_gs<2, true>(*this, k, zout, rin, nullptr, scp, gs.partial.p);
                 else launch_gs<2, false>(*this, k, zout, rin, nullptr, scp, nullptr);
             }
+            // band mode: the dot product's partials of the rows outside the colours
+            if (dot && gs.band) launch_gs<4, false>(*this, -3, zout, rin, nullptr, scp, gs.partial.p);
             continue;
         }
         // post-smoothing restarts the smoother (Chebyshev recurrence) from the prolongated iterate
@@ -2826,10 +2960,18 @@ void MgpisDevice::vcycle_bytes(int s, double out[2]) const {
     // the colours it reads (forward colour k: the k earlier ones, residual: the later ones,
     // backward: all others), and per row b, M^-1, the row index and x (or r) written
     const double K = gsf ? (double)gs.ncol : 0.0;
-    const double gsmat = gsf ? (vbytes(vc_type(Lf)) + (gs.col16.p ? 2.0 : 4.0)) * (double)gs.nnzb_sub[s] : 0.0;
+    const double gsvb = gsf ? vbytes(vc_type(Lf)) + (gs.col16.p ? 2.0 : 4.0) : 0.0;
+    const double gsmat = gsvb * (gsf ? (double)gs.nnzb_sub[s] : 0.0);
+    // rows the colours sweep (all of them unless band mode), and band mode's ring and far rows
+    const double nsw = gsf && gs.band ? (double)gs.band_rows_sub[s] : n(Lf);
+    const double nring = gsf && gs.band ? (double)gs.ring_rows_sub[s] : 0.0;
+    const double nout = gsf && gs.band ? nring + (double)gs.far_rows_sub[s] : 0.0;
     if (gsf) {
-        put(Lf, gsmat + n(Lf) * (24.0 + minv(Lf) + 24.0 + 4.0 + 24.0 * (K - 1.0) / 2.0));  // forward
-        put(Lf, n(Lf) * (24.0 + 4.0 + 24.0 * (K - 1.0) / 2.0));                              // residual
+        put(Lf, 76.0 * nout);  // band mode: x = 0, r = b outside the colours (b read, x, r written, row index)
+        put(Lf, gsmat + nsw * (24.0 + minv(Lf) + 24.0 + 4.0 + 24.0 * (K - 1.0) / 2.0));  // forward
+        put(Lf, nsw * (24.0 + 4.0 + 24.0 * (K - 1.0) / 2.0));                              // residual
+        // band mode: the ring's residual over its band columns (blocks, b read, r written, x gathered)
+        put(Lf, gsvb * (double)(gs.band ? gs.ring_nnzb_sub[s] : 0) + nring * (24.0 + 24.0 + 4.0 + 24.0));
     } else {
         put(Lf, n(Lf) * (48.0 + minv(Lf) + (cheb ? 24.0 : 0.0)));  // k_jac0: b in, x out
     }
@@ -2859,7 +3001,8 @@ void MgpisDevice::vcycle_bytes(int s, double out[2]) const {
         pb += 4.0 * 8.0 * (double)F.tblk_sub[s];
         put(l, pb);
         if (gsf && l == Lf) {
-            put(l, gsmat + n(l) * (24.0 + minv(l) + 24.0 + 4.0 + 24.0 * (K - 1.0)));  // backward
+            put(l, gsmat + nsw * (24.0 + minv(l) + 24.0 + 4.0 + 24.0 * (K - 1.0)));  // backward
+            put(l, 52.0 * nout);  // band mode: b . x of the rows outside the colours (b, x read, row index)
             continue;
         }
         for (int k = 0; k < opt.nu; ++k) put(l, sweep(l));
@@ -2889,7 +3032,8 @@ int64_t MgpisDevice::iteration_launches() const {
     // place of jac0, nu - 1 + 1 + nu sweep launches
     const int64_t nd = (int64_t)lev.size() - 1 - clev;
     const int64_t base = 5 + (nd == 0 ? 2 : 1 + nd * (opt.nu + 1) + 1 + nd * (1 + opt.nu));
-    return gs_fine() && nd > 0 ? base - 1 - 2 * opt.nu + 2 * gs.ncol + 1 : base;
+    // (band mode: + the x = 0 / r = b launch, the ring's residual and the dot of the other rows)
+    return gs_fine() && nd > 0 ? base - 1 - 2 * opt.nu + 2 * gs.ncol + 1 + (gs.band ? 3 : 0) : base;
 }
 
 // k_fin over every member

@@ -167,6 +167,13 @@ struct GsFine {
     // 0..K-1, the residual, backward colours K-1..0 (stored blocks, per-row vectors, every distinct
     // x entry gathered once; profiles/gs_table.py sets the rocprof / PMC figures beside them)
     std::vector<double> launch_bytes;
+    // band mode (locally refined fine level): the colours cover only the band -- the
+    // nodes the fine level adds to the next coarser one and their neighbours; two more chunk groups
+    // per member follow the colours: the ring (non-band rows with a band neighbour: their band
+    // columns only, for the residual) and the far rows (no blocks).  first / count then hold ncol + 2
+    // groups; the sweeps run over the colours, k_gs_aux over the ring and far groups.
+    bool band = false;
+    std::vector<int64_t> band_rows_sub, ring_rows_sub, far_rows_sub, ring_nnzb_sub;
 };
 
 class MgpisDevice {

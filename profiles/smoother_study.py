@@ -12,6 +12,8 @@ could run at equal fine-level operator passes:
   mcgs_band  (--general: bench.py's general mesh, contact band refined once more) mcgs on the finest
          level restricted to the band -- the rows of the nodes level L adds to level L-1 and their
          K_L neighbours -- bj below (level L-1 already smooths the unrefined rows' identical stencils)
+  mcgs_band2 mcgs_band on the finest level and mcgs on level L-1, bj below; mcgs_two: mcgs on the two
+         finest levels, bj below
   hgs_fine   hybrid (tile-local) multicolour GS on the finest level, bj below: the colours are swept
          inside 3D tiles of nodes (--tile tx,ty,tz, default 16,16,8), couplings across tiles read the
          values from before the sweep (block Jacobi over tiles, GS inside: what one launch per sweep
@@ -132,7 +134,7 @@ class VCycle:
             elif smoother.startswith("mcgs") or smoother.startswith("hgs"):
                 c = colouring(K[l], node[l])
                 self.rows[l] = [np.nonzero(c == k)[0] for k in range(c.max() + 1)]
-                if smoother == "mcgs_band" and l == self.L:
+                if smoother in ("mcgs_band", "mcgs_band2") and l == self.L:
                     new = (node[l] >= NN[l - 1]).astype(np.float64)
                     A = sp.csr_matrix((np.ones(K[l].nnz), K[l].indices, K[l].indptr), shape=K[l].shape)
                     band = (new > 0) | ((A @ new) > 0)
@@ -170,6 +172,7 @@ class VCycle:
 
     def is_bj(self, l):
         return self.sm == "bj" or (self.sm in ("mcgs_fine", "hgs_fine", "hgs_l1_fine", "mcgs_band") and l < self.L) or \
+            (self.sm in ("mcgs_band2", "mcgs_two") and l < self.L - 1) or \
             (self.sm == "mcgs_coarse" and l == self.L)
 
     def smooth(self, l, x, b, forward: bool):
@@ -268,7 +271,7 @@ def main():
         res = np.linalg.norm(b - K[-1] @ x) / np.linalg.norm(b)
         ncol = max((len(v) for v in V.rows.values()), default=0)
         extra = f"  tiles {V.ntile} of {TILE}" if sm.startswith("hgs") else \
-            f"  band rows {V.band_rows} of {K[-1].shape[0]}" if sm == "mcgs_band" else ""
+            f"  band rows {V.band_rows} of {K[-1].shape[0]}" if sm.startswith("mcgs_band") else ""
         print(f"{sm:5s} PCG iterations {it:3d}  true relres {res:.2e}  colours {ncol}{extra}  ({time.time() - t:.1f} s)")
 
 
