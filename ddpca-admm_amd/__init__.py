@@ -861,7 +861,7 @@ class MCONTACT:
 
     def get(self, what: str, index: int = 0) -> np.ndarray:
         n = _check(lib().mcontact_gpu_get(self._h, what.encode(), index, None, 0))
-        dtype = (np.int64 if what in ("pcg_iters", "owned", "mass_iters")
+        dtype = (np.int64 if what in ("pcg_iters", "owned", "mass_iters", "coarse_solve", "gs_rows")
                  else np.int32 if what == "fricStat" else np.float64)
         out = np.zeros(n, dtype)
         if n:

@@ -2921,7 +2921,23 @@ int64_t mcontact_gpu_get(mcontact_t h, const char* what, int64_t index, void* ou
             if (out && cap >= 1) static_cast<int64_t*>(out)[0] = (int64_t)h->mass_iters;
             return;
         }
+        if (w == "gs_rows") {  // int64 [rows the colour sweeps cover, ring rows, far rows] (GsFine::band)
+            int64_t v[3] = {0, 0, 0};
+            if (h->mg && h->mg->gs_fine()) {
+                const GsFine& G = h->mg->gs;
+                for (int s = 0; s < h->mg->nsub; ++s) {
+                    v[0] += G.band ? G.band_rows_sub[s] : h->mg->lev.back().nloc[s];
+                    v[1] += G.band ? G.ring_rows_sub[s] : 0;
+                    v[2] += G.band ? G.far_rows_sub[s] : 0;
+                }
+            }
+            n = 3;
+            if (out)
+                for (int64_t i = 0; i < std::min<int64_t>(3, cap); ++i) static_cast<int64_t*>(out)[i] = v[i];
+            return;
+        }
         if (w == "gs_launch_bytes") {  // the colour sweeps' per-launch byte model (GsFine::launch_bytes), doubles
+            if (!h->mg) throw ApiError(DDPCA_ESTATE, "no owned subdomain");
             const auto& v = h->mg->gs.launch_bytes;
             n = (int64_t)v.size();
             if (out)

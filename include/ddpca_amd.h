@@ -446,7 +446,11 @@ int64_t mcontact_gpu_monitor(mcontact_t h, double* out, int64_t cap_rows);
 /* Copy state to host: what = "resuDisp" (index = subdomain, nodal 3N), "inteAuxi"/"inteLagr"
  * (index = 2*ts+side), "inpoGamm" (index = ts, projected gamma of the last iteration),
  * "fricStat" (index = ts, int32 per integration point: 0 open, 1 slip, 2 stick, MCONTACT.h:2647-2666),
- * "pcg_iters" (int64 per owned subdomain, last iteration). */
+ * "pcg_iters" (int64 per owned subdomain, last iteration), "mass_iters" (int64: surface-mass CG
+ * iterations of the last iterate call), "coarse_solve" (int64 x4: coarse rows, DOUBLE_M?, dense
+ * bytes, dense fallback?), "gs_rows" (int64 x3: the fine rows the multicolour sweeps cover, the
+ * band mode's ring and far rows -- 0, 0 without it), "gs_launch_bytes" (the sweeps' per-launch byte
+ * model, doubles). */
 int64_t mcontact_gpu_get(mcontact_t h, const char* what, int64_t index, void* out, int64_t cap);
 /* Timing of the last iterate() call, summed over its iterations: [total_ms (host wall),
  * solve_ms (host wall of the body balance), iface_ms (device, interface step + monitor),

@@ -290,6 +290,39 @@ def _oracle_problem_no_coarse(P, oracle):
     return subs, ifaces
 
 
+def test_band_sweeps_match_full_sweeps(ddpca, gpu, monkeypatch):
+    """Band mode of the multicolour fine level (GsFine::band, DESIGN §7d): on the general mesh the
+    colours cover only the nodes the band level adds and their neighbours (the rest is level L-1's),
+    and the ADMM trajectory with it matches the full-level sweeps' to the PCG tolerance -- the
+    preconditioner changes, the 1e-14 stop on the same fp64 operator does not: resuMoni rows 1e-7
+    (SURVEY §8 c4), displacements 1e-9.  The headline's uniform fine level has no band."""
+    monkeypatch.setenv("DDPCA_LATTICE", "0")
+    H, M = ddpca.HEADLINE_OPTIONS, ddpca.HEADLINE_MUSC
+    P = ddpca.headline_problem(gl=3, **ddpca.GENERAL_FEATURES)
+    P.set_coarse(M["muscSett"], [M["doleMcsc"]] * P.nsub)
+    P.ESTABLISH()
+    k = 8
+    runs = {}
+    for band in ("1", "0"):
+        monkeypatch.setenv("DDPCA_GS_BAND", band)
+        mc = ddpca.MCONTACT(P, **H)
+        assert mc.CONTACT_ANALYSIS(k, check=False) == k
+        runs[band] = (mc.get("gs_rows"), mc.monitor(), [mc.get("resuDisp", tv) for tv in range(P.nsub)])
+        del mc
+    (rb, mb, ub), (rf, mf, uf) = runs["1"], runs["0"]
+    print("gs rows band / ring / far", list(rb), "full", list(rf))
+    assert rb[1] > 0 and rb[2] > 0 and rb[0] < 0.6 * rf[0] and rf[1] == rf[2] == 0
+    ok, worst = _rows_close(mb, mf, k=k, rtol=1e-7)
+    assert ok, worst
+    for a, b in zip(ub, uf):
+        assert np.linalg.norm(a - b) <= 1e-9 * np.linalg.norm(b)
+    monkeypatch.delenv("DDPCA_GS_BAND")
+    Q = ddpca.headline_problem(gl=3).ESTABLISH()
+    mq = ddpca.MCONTACT(Q, **H)
+    rows = mq.get("gs_rows")
+    assert rows[1] == rows[2] == 0 and rows[0] > 0
+
+
 @pytest.mark.parametrize("opts", ["HEADLINE_OPTIONS"])
 def test_general_mesh_trajectory_matches_oracle(ddpca, oracle, gpu, monkeypatch, opts):
     """bench.py's general-mesh line at reduced size: the DEHW chain with its contact band refined
