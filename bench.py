@@ -248,6 +248,8 @@ def main():
             },
             "mgpis_dof_iter_per_s": dof_its / elapsed,
             "pcg_iters_per_solve": pcg_its / max(n * nsub, 1),
+            # this rank's subdomains in the last timed ADMM iteration (the state cpu_baseline prices)
+            "pcg_iters_last_iteration": [int(v) for v in mc.get("pcg_iters")],
             "setup_s": t_setup,
             "mass_cg_iters_per_admm_iter": int(mc.get("mass_iters")[0]) / max(n, 1),
             # device time per ADMM iteration of the interface step (gamma, projection, aux / lambda

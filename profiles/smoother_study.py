@@ -37,6 +37,8 @@ D = importlib.import_module("ddpca-admm_amd")
 
 
 TILE = (16, 16, 8)
+NEWONLY = False  # --new-only: the band is the new nodes alone (no neighbour ring)
+ORDER = None  # --order 0,7,...: the fine level's colours swept in this order (forward; backward reversed)
 
 
 GENERAL = False
@@ -131,13 +133,26 @@ class VCycle:
                 lam = spl.eigsh(spl.LinearOperator(K[l].shape, matvec=lambda x, l=l: bd.apply(K[l] @ x)), k=1,
                                 which="LM", return_eigenvectors=False, tol=1e-3)[0]
                 self.omega[l] = 1.7 / lam
-            elif smoother.startswith("mcgs") or smoother.startswith("hgs"):
+            elif smoother.startswith("mcgs") or smoother.startswith("hgs") or smoother.startswith("bmcgs"):
                 c = colouring(K[l], node[l])
-                self.rows[l] = [np.nonzero(c == k)[0] for k in range(c.max() + 1)]
+                if smoother.startswith("bmcgs") and l == self.L:
+                    # 2x2x2 node blocks coloured by the block lattice's parity, each block swept in
+                    # lexicographic order: 64 "colours" = block colour x position in the block
+                    xyz = COORD[node[l]]
+                    idx = []
+                    for d in range(3):
+                        u = np.unique(np.round(COORD[np.unique(node[l])][:, d], 12))
+                        idx.append(np.searchsorted(u, np.round(xyz[:, d], 12)))
+                    bx, by, bz = idx[0] // 2, idx[1] // 2, idx[2] // 2
+                    bc = (bx % 2) + 2 * (by % 2) + 4 * (bz % 2)
+                    lp = (idx[0] % 2) + 2 * (idx[1] % 2) + 4 * (idx[2] % 2)
+                    c = bc * 8 + lp
+                order = ORDER if ORDER and l == self.L and len(ORDER) == c.max() + 1 else list(range(c.max() + 1))
+                self.rows[l] = [np.nonzero(c == k)[0] for k in order]
                 if smoother in ("mcgs_band", "mcgs_band2") and l == self.L:
                     new = (node[l] >= NN[l - 1]).astype(np.float64)
                     A = sp.csr_matrix((np.ones(K[l].nnz), K[l].indices, K[l].indptr), shape=K[l].shape)
-                    band = (new > 0) | ((A @ new) > 0)
+                    band = (new > 0) | ((A @ new) > 0) if not NEWONLY else new > 0
                     self.band_rows = int(band.sum())
                     self.rows[l] = [r[band[r]] for r in self.rows[l]]
                 self.Krows[l] = [K[l][r] for r in self.rows[l]]
@@ -171,7 +186,7 @@ class VCycle:
                 self.tri[l] = (sp.tril(K[l], format="csr"), sp.triu(K[l], format="csr"))
 
     def is_bj(self, l):
-        return self.sm == "bj" or (self.sm in ("mcgs_fine", "hgs_fine", "hgs_l1_fine", "mcgs_band") and l < self.L) or \
+        return self.sm == "bj" or (self.sm in ("mcgs_fine", "hgs_fine", "hgs_l1_fine", "mcgs_band", "bmcgs_fine") and l < self.L) or \
             (self.sm in ("mcgs_band2", "mcgs_two") and l < self.L - 1) or \
             (self.sm == "mcgs_coarse" and l == self.L)
 
@@ -187,7 +202,7 @@ class VCycle:
                 Kin, Koff = self.split[l][k]
                 x[r] += self.bd[l].apply(b[r] - Kin @ x - Koff @ x0, r)
             return x
-        if self.sm.startswith("mcgs"):
+        if self.sm.startswith("mcgs") or self.sm.startswith("bmcgs"):
             order = range(len(self.rows[l])) if forward else reversed(range(len(self.rows[l])))
             x = x.copy()
             for k in order:
@@ -248,8 +263,11 @@ def round_h16(K, node):
 
 
 def main():
-    global TILE, GENERAL
+    global TILE, GENERAL, ORDER, NEWONLY
     GENERAL = "--general" in sys.argv
+    NEWONLY = "--new-only" in sys.argv
+    if "--order" in sys.argv:
+        ORDER = [int(v) for v in sys.argv[sys.argv.index("--order") + 1].split(",")]
     if "--tile" in sys.argv:
         TILE = tuple(int(v) for v in sys.argv[sys.argv.index("--tile") + 1].split(","))
     gl = int(sys.argv[1]) if len(sys.argv) > 1 else 4
