@@ -37,6 +37,7 @@ D = importlib.import_module("ddpca-admm_amd")
 
 
 TILE = (16, 16, 8)
+RHS = None
 NEWONLY = False  # --new-only: the band is the new nodes alone (no neighbour ring)
 ORDER = None  # --order 0,7,...: the fine level's colours swept in this order (forward; backward reversed)
 
@@ -61,6 +62,9 @@ def hierarchy(gl: int, tv: int):
         assert len(dofs) == K[l].shape[0]
         node.append(dofs // 3)
     b = np.asarray(P.array("consForc", tv), dtype=np.float64)
+    if RHS is not None:  # --rhs FILE.npy: a right-hand side saved by profiles/dump_rhs.py
+        b = np.load(RHS)
+        assert len(b) == K[L].shape[0]
     if not np.any(b):
         b = np.random.default_rng(0).standard_normal(K[L].shape[0])
     return K, Pr, node, b
@@ -182,11 +186,11 @@ class VCycle:
                         off = tid[Kc.row] != tid[Kc.col]
                         l1 = np.bincount(Kc.row[off], weights=np.abs(Kc.data[off]), minlength=K[l].shape[0])
                         self.bd[l] = BlockDiag(K[l] + sp.diags(l1), node[l])
-            elif smoother == "sgs":
+            elif smoother.startswith("sgs"):
                 self.tri[l] = (sp.tril(K[l], format="csr"), sp.triu(K[l], format="csr"))
 
     def is_bj(self, l):
-        return self.sm == "bj" or (self.sm in ("mcgs_fine", "hgs_fine", "hgs_l1_fine", "mcgs_band", "bmcgs_fine") and l < self.L) or \
+        return self.sm == "bj" or (self.sm in ("mcgs_fine", "hgs_fine", "hgs_l1_fine", "mcgs_band", "bmcgs_fine", "mcgs_ssor_fine") and l < self.L) or \
             (self.sm in ("mcgs_band2", "mcgs_two") and l < self.L - 1) or \
             (self.sm == "mcgs_coarse" and l == self.L)
 
@@ -218,12 +222,20 @@ class VCycle:
         if l == self.coarse:
             return self.lu.solve(b)
         nu = self.nu_fine if l == self.L else self.nu_second if l == self.L - 1 else self.nu_coarse
+        # SSOR smoothing ("ssor" in the name, the reference's MULT_VCYC, MGPIS.h:64-76, 101-114):
+        # every smoothing step is a forward AND a backward sweep, before and after the coarse
+        # correction, on the levels the named smoother sweeps
+        ssor = "ssor" in self.sm and not self.is_bj(l)
         x = np.zeros_like(b)
         for _ in range(nu):
             x = self.smooth(l, x, b, True)
+            if ssor:
+                x = self.smooth(l, x, b, False)
         r = b - self.K[l] @ x
         x = x + self.Pr[l - 1] @ self.apply(l - 1, self.Pr[l - 1].T @ r)
         for _ in range(nu):
+            if ssor:
+                x = self.smooth(l, x, b, True)
             x = self.smooth(l, x, b, False)
         return x
 
@@ -263,7 +275,9 @@ def round_h16(K, node):
 
 
 def main():
-    global TILE, GENERAL, ORDER, NEWONLY
+    global TILE, GENERAL, ORDER, NEWONLY, RHS
+    if "--rhs" in sys.argv:
+        RHS = sys.argv[sys.argv.index("--rhs") + 1]
     GENERAL = "--general" in sys.argv
     NEWONLY = "--new-only" in sys.argv
     if "--order" in sys.argv:
