@@ -140,6 +140,8 @@ def _declare(L: C.CDLL) -> None:
     L.ddpca_problem_destroy.argtypes = [_P]
     L.ddpca_problem_mgpis.argtypes = [_P, C.c_int64, C.c_int, C.POINTER(MgpisOptions), C.POINTER(_P)]
     L.ddpca_problem_empty.argtypes = [C.c_int64, C.c_int64, C.POINTER(_P)]
+    L.ddpca_problem_set_contact.argtypes = [_P, C.c_int64, C.c_int64, C.c_int64]
+    L.ddpca_problem_set_subdomain_tree.argtypes = [_P, C.c_int64, _P]
     L.ddpca_problem_set_subdomain.argtypes = [_P, C.c_int64, C.c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]
     L.ddpca_problem_set_subdomain_prol.argtypes = [_P, C.c_int64, C.c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
                                                    _P]

@@ -21,6 +21,7 @@
 #include <unistd.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <memory>
 #include <thread>
 #include <fstream>
@@ -110,7 +111,21 @@ int main(int argc, char** argv) {
     });
     std::vector<int32_t> owner(c.multGrid.size(), 0);
     mcontact_t h = nullptr;
-    ddpca_bind::check(mcontact_gpu_create(p, 0, 0, 1, owner.data(), nullptr, &h));
+    // DDPCA_REF_OPTIONS=multicolour: the headline's V-cycle (colour Gauss-Seidel on the fine level --
+    // band mode where the fine level refines a band -- two block-Jacobi sweeps below, block-exponent
+    // fp16 copies) instead of the default block Jacobi
+    mgpis_options_t opt;
+    mgpis_default_options(&opt);
+    const char* oe = std::getenv("DDPCA_REF_OPTIONS");
+    const bool mcol = oe && std::string(oe) == "multicolour";
+    if (mcol) {
+        opt.smoother = 3;
+        opt.nu = 2;
+        opt.precond_fp32 = 2;
+    }
+    ddpca_bind::check(mcontact_gpu_create(p, 0, 0, 1, owner.data(), &opt, &h));
+    int64_t gsr[3] = {0, 0, 0};
+    ddpca_bind::check((int)std::min<int64_t>(mcontact_gpu_get(h, "gs_rows", 0, gsr, 3), 0));
     const int64_t n_gpu = noref ? 0 : mcontact_gpu_iterate(h, 3000, 1);
     ddpca_bind::check((int)std::min<int64_t>(n_gpu, 0));
     // displacements: position order (hanging level last) -> node-id order
@@ -190,9 +205,9 @@ int main(int argc, char** argv) {
     std::fprintf(stderr,
                  "{\"native\": %s, \"K_rel\": %.3g, \"subdomains\": %zu, \"nodes\": %ld, \"hanging_nodes\": %ld, \"iters_gpu\": %ld, \"iters_ref\": %ld, "
                  "\"resuDisp_rel\": %.3g, \"moni_rows\": %ld, \"moni_rel\": %.3g, \"pressure_rel\": %.3g, \"interfaces\": %s, "
-                 "\"ranks2\": %s}\n",
+                 "\"ranks2\": %s, \"multicolour\": %s, \"gs_rows\": [%ld, %ld, %ld]}\n",
                  native ? "true" : "false", dK, c.multGrid.size(), nnodes, nhang, (long)n_gpu, (long)c.iterNumbReco, du,
                  (long)kmax, dmoni, dp_all,
-                 itf.c_str(), ranks2.c_str());
+                 itf.c_str(), ranks2.c_str(), mcol ? "true" : "false", (long)gsr[0], (long)gsr[1], (long)gsr[2]);
     return 0;
 }

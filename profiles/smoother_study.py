@@ -191,7 +191,7 @@ class VCycle:
 
     def is_bj(self, l):
         return self.sm == "bj" or (self.sm in ("mcgs_fine", "hgs_fine", "hgs_l1_fine", "mcgs_band", "bmcgs_fine", "mcgs_ssor_fine") and l < self.L) or \
-            (self.sm in ("mcgs_band2", "mcgs_two") and l < self.L - 1) or \
+            (self.sm in ("mcgs_band2", "mcgs_two", "mcgs_l1ssor") and l < self.L - 1) or \
             (self.sm == "mcgs_coarse" and l == self.L)
 
     def smooth(self, l, x, b, forward: bool):
@@ -226,6 +226,8 @@ class VCycle:
         # every smoothing step is a forward AND a backward sweep, before and after the coarse
         # correction, on the levels the named smoother sweeps
         ssor = "ssor" in self.sm and not self.is_bj(l)
+        if self.sm == "mcgs_l1ssor":  # colour GS on the fine level, colour SSOR on L-1, bj below
+            ssor = l == self.L - 1
         x = np.zeros_like(b)
         for _ in range(nu):
             x = self.smooth(l, x, b, True)

@@ -54,6 +54,26 @@ def test_device_entry_points_fail_loudly_without_gpu(ddpca):
         ddpca.MCONTACT(P)
 
 
+def test_round5_entry_points_refuse_bad_arguments(ddpca):
+    """The tree-input ESTABLISH (ddpca_problem_set_subdomain_tree / _set_contact) and the timing
+    transport (mcontact_gpu_comm_loopback) check their arguments before anything changes (no GPU)."""
+    L = ddpca.lib()
+    assert L.mcontact_gpu_comm_loopback(None, None) == -1
+    assert L.ddpca_problem_set_contact(None, 0, 0, 1) == -1
+    assert L.ddpca_problem_set_subdomain_tree(None, 0, None) == -1
+    h = ctypes.c_void_p()
+    assert L.ddpca_problem_empty(2, 1, ctypes.byref(h)) == 0
+    try:
+        assert L.ddpca_problem_set_contact(h, 1, 0, 1) == -1   # interface index
+        assert L.ddpca_problem_set_contact(h, 0, 0, 0) == -1   # one body twice
+        assert L.ddpca_problem_set_contact(h, 0, 0, 2) == -1   # body out of range
+        assert L.ddpca_problem_set_contact(h, 0, 1, 0) == 0
+        assert L.ddpca_problem_set_subdomain_tree(h, 0, None) < 0  # no tree
+        assert L.ddpca_problem_set_subdomain_tree(h, 2, None) == -1  # subdomain index
+    finally:
+        L.ddpca_problem_destroy(h)
+
+
 def test_last_error_is_thread_local_string(ddpca):
     with pytest.raises(ddpca.DdpcaError):
         ddpca.Problem("beam", 1)

@@ -419,8 +419,9 @@ def test_block_patch_pressure_known_answer(gpu, tmp_path, musc):
             assert abs(itf[k] - 1e7) <= 1e-5 * 1e7, (musc, itf)
 
 
-@pytest.mark.parametrize("native", [False, True], ids=["reference-operators", "native-operators"])
-def test_cylinder_known_answer(gpu, tmp_path, native):
+@pytest.mark.parametrize("native,mcol", [(False, False), (True, False), (True, True)],
+                         ids=["reference-operators", "native-operators", "native-multicolour"])
+def test_cylinder_known_answer(gpu, tmp_path, native, mcol):
     """native: every subdomain's MGPIS hierarchy, consForc and hanging rows come from the library's
     own pipeline on the reference's element trees (ddpca_multigrid_*: TRANSFER with the hanging
     level, PATCH, STIF_MATR + the contact systMass, CONSTRAINT(1)) instead of the
@@ -433,7 +434,10 @@ def test_cylinder_known_answer(gpu, tmp_path, native):
     contact band 2e-4): the reference builds and solves it, oracle/ref_bind.hpp hands the
     operators over with the hanging level, and the device ADMM loop reaches the reference's
     iteration count (+-1), resuDisp on every node (1e-6), the resuMoni norm columns of rows
-    k <= 50 (1e-7) and the contact pressures of its last resuCont files (1e-5 of the peak)."""
+    k <= 50 (1e-7) and the contact pressures of its last resuCont files (1e-5 of the peak).
+    native-multicolour: the same with the headline's V-cycle (colour Gauss-Seidel on the fine level,
+    in band mode where that level refines a band: GsFine::band) -- the preconditioner differs from
+    the reference's SGS, the answers may not."""
     import json
     import os
     import subprocess
@@ -441,8 +445,11 @@ def test_cylinder_known_answer(gpu, tmp_path, native):
     exe = Path(__file__).resolve().parents[1] / "oracle" / "_ref" / "ref_cylinder"
     if not exe.exists():
         pytest.skip("oracle/_ref/ref_cylinder is built only where the reference is (travels with the snapshot)")
+    env = dict(os.environ)
+    if mcol:
+        env["DDPCA_REF_OPTIONS"] = "multicolour"
     out = subprocess.run([str(exe), "1", "4", "2", "2e-4"] + (["native"] if native else []), capture_output=True,
-                         text=True, timeout=170, env=dict(os.environ), cwd=tmp_path)
+                         text=True, timeout=170, env=env, cwd=tmp_path)
     assert out.returncode == 0, out.stderr[-2000:]
     res = json.loads(out.stderr.strip().splitlines()[-1])
     print(res)
@@ -454,6 +461,7 @@ def test_cylinder_known_answer(gpu, tmp_path, native):
     assert res["pressure_rel"] <= 1e-5, res
     for itf in res["interfaces"]:
         assert itf["active"] > 0, itf
+    assert res["multicolour"] == mcol and (res["gs_rows"][0] > 0) == mcol, res
 
 
 @pytest.mark.parametrize("owners", ["0101", "0011"])
