@@ -452,6 +452,76 @@ __global__ __launch_bounds__(256) void k_mcg_axpy(EllArgs e, const PcgScal* sc, 
     }
 }
 
+// ---- Chebyshev iteration on D^-1 M (MassBatch::cheb_; Saad, Iterative Methods, Alg. 12.1): a fixed
+// number of steps from setup bounds of each system's spectrum, one launch per step, no reductions;
+// the CG below then restarts from its iterate (k_mcg_restart) and usually finds it converged.
+// x = 0, r = b, d = D^-1 b / theta_sys
+__global__ __launch_bounds__(256) void k_mcheb_init(const double* b, const double* dinv, const double* ith,
+                                                    const int32_t* csys, double* x, double* r, double* d, int64_t nrow) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= nrow) return;
+    const double bi = b[i];
+    x[i] = 0.0;
+    r[i] = bi;
+    d[i] = ith[csys[i >> 6]] * dinv[i] * bi;
+}
+
+// step k: x += d, r -= M d, dn = c1 d + c2 D^-1 r (coef[(k nsys + sys) 2 + {0, 1}]); systems whose
+// step count kmax is reached keep their x, r.  The paired form (MassBatch::paired_) reads the
+// shared matrix once for chunk c and its twin c + nch2, as k_mcg_spmv2.
+template <bool PAIR>
+__global__ __launch_bounds__(256) void k_mcheb_step(EllArgs e, const double* coef, const int32_t* kmax, int nsys, int k,
+                                                    const double* d, double* dn, double* x, double* r, int64_t R,
+                                                    int64_t nch_launch) {
+    const int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (c >= nch_launch) return;
+    const int sw = e.csys[c];
+    const int sv = PAIR ? e.csys[c + nch_launch] : sw;
+    const bool aw = k < kmax[sw], av = PAIR && k < kmax[sv];
+    if (!aw && !av) return;
+    const int lane = threadIdx.x & 63;
+    const int64_t row = c * 64 + lane;
+    const int ns = e.slots[c];
+    const int32_t* cp = e.col + e.off[c] * 64 + lane;
+    const double* vp = e.val + e.off[c] * 64 + lane;
+    double s0 = 0.0, s1 = 0.0;
+#pragma unroll 4
+    for (int q = 0; q < ns; ++q) {
+        const double v = vp[(int64_t)q * 64];
+        const int32_t j = cp[(int64_t)q * 64];
+        s0 += v * d[j];
+        if (PAIR) s1 += v * d[j + R];
+    }
+    auto upd = [&](int sys, int64_t i, double sum) {
+        const double di = d[i];
+        x[i] += di;
+        const double ri = r[i] - sum;
+        r[i] = ri;
+        const double* cc = coef + 2 * ((int64_t)k * nsys + sys);
+        dn[i] = cc[0] * di + cc[1] * e.dinv[i] * ri;
+    };
+    if (aw) upd(sw, row, s0);
+    if (av) upd(sv, row + R, s1);
+}
+
+// CG restart from the Chebyshev iterate: z = D^-1 r, p = q = 0; partials (r.z, r.r) per chunk and
+// b.b per chunk at bb (the stop rule stays relative to ||b||)
+__global__ __launch_bounds__(256) void k_mcg_restart(const double* b, const double* dinv, const double* r, double* z,
+                                                     double* p, double* q, double* partial, double* bbp, int64_t nrow) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= nrow) return;
+    const double ri = r[i], zi = dinv[i] * ri, bi = b[i];
+    z[i] = zi;
+    p[i] = 0.0;
+    q[i] = 0.0;
+    const double a = wsum(ri * zi), c = wsum(ri * ri), d = wsum(bi * bi);
+    if ((threadIdx.x & 63) == 0) {
+        partial[2 * (i >> 6)] = a;
+        partial[2 * (i >> 6) + 1] = c;
+        bbp[i >> 6] = d;
+    }
+}
+
 enum McgWhat { kMcgInit = 0, kMcgAlpha = 1, kMcgBeta = 2 };
 
 // per-system scalars: one workgroup per system, fixed order over its chunks
@@ -512,6 +582,47 @@ __global__ __launch_bounds__(256) void k_mcg_fin(int what, const double* partial
         sc->delta = b;
         mirror_store(mirror + sys, sc->iter, sc->done, sc->fail);
     }
+}
+
+// the CG's scalars after k_mcg_restart: delta = r.z, rr = r.r, bb = b.b (one workgroup per system,
+// a fixed order), tol2 scaled by b.b as k_mcg_fin's init does
+__global__ __launch_bounds__(256) void k_mcg_fin_restart(const double* partial, const double* bbp, const int64_t* cb,
+                                                         PcgScal* scv, PcgMirror* mirror) {
+    const int sys = blockIdx.x;
+    PcgScal* sc = scv + sys;
+    __shared__ double r0[4], r1[4], r2[4];
+    double a = 0.0, b = 0.0, c = 0.0;
+    for (int64_t k = cb[sys] + threadIdx.x; k < cb[sys + 1]; k += 256) {
+        a += partial[2 * k];
+        b += partial[2 * k + 1];
+        c += bbp[k];
+    }
+    a = wsum(a);
+    b = wsum(b);
+    c = wsum(c);
+    if ((threadIdx.x & 63) == 0) {
+        r0[threadIdx.x >> 6] = a;
+        r1[threadIdx.x >> 6] = b;
+        r2[threadIdx.x >> 6] = c;
+    }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    a = (r0[0] + r0[1]) + (r0[2] + r0[3]);
+    b = (r1[0] + r1[1]) + (r1[2] + r1[3]);
+    c = (r2[0] + r2[1]) + (r2[2] + r2[3]);
+    sc->delta = a;
+    sc->bb = c;
+    sc->rr = b;
+    sc->tol2 = sc->tol2 * c;
+    sc->beta = 0.0;
+    sc->iter = 0;
+    sc->fail = 0;
+    sc->done = (b <= sc->tol2 || sc->maxit <= 0 || !(c > 0.0)) ? 1 : 0;
+    if (!isfinite(a) || !isfinite(b)) {
+        sc->fail = 1;
+        sc->done = 1;
+    }
+    mirror_store(mirror + sys, 0, sc->done, sc->fail);
 }
 
 // All MONITOR pair norms of an iteration in two launches (instead of two per vector pair, 3.63 ->
@@ -757,8 +868,89 @@ __global__ void k_scal_merge(PcgScal* sc, const PcgScal* scs, const int32_t* hal
     if (i < n) sc[i] = scs[half[i] * n + i];
 }
 
+// Extreme eigenvalues of D^-1 M for an SPD CSR M (MassBatch's Chebyshev steps): Lanczos on the
+// symmetric D^-1/2 M D^-1/2 (m steps from a fixed start vector), Ritz extremes by bisection on
+// the tridiagonal (Sturm counts); *gersh = max_i sum_j |M_ij| / M_ii, an upper bound
+void mass_spectrum(const Csr& M, int m, double* lmin, double* lmax, double* gersh) {
+    const int64_t n = M.nrow;
+    std::vector<double> dis(n, 0.0);
+    double g = 0.0;
+    for (int64_t r = 0; r < n; ++r) {
+        double dg = 0.0, sa = 0.0;
+        for (int64_t k = M.ptr[r]; k < M.ptr[r + 1]; ++k) {
+            sa += std::abs(M.val[k]);
+            if (M.col[k] == r) dg = M.val[k];
+        }
+        dis[r] = dg > 0.0 ? 1.0 / std::sqrt(dg) : 0.0;
+        if (dg > 0.0) g = std::max(g, sa / dg);
+    }
+    *gersh = g;
+    m = (int)std::min<int64_t>(m, n);
+    std::vector<double> v(n), vp(n, 0.0), w(n), alpha, beta;
+    double nv = 0.0;
+    for (int64_t i = 0; i < n; ++i) v[i] = 1.0 + 0.5 * std::sin(0.7 * (double)i + 0.3), nv += v[i] * v[i];
+    nv = std::sqrt(nv);
+    for (double& x : v) x /= nv;
+    double bprev = 0.0;
+    for (int j = 0; j < m; ++j) {
+        for (int64_t r = 0; r < n; ++r) {
+            double acc = 0.0;
+            for (int64_t k = M.ptr[r]; k < M.ptr[r + 1]; ++k) acc += M.val[k] * dis[M.col[k]] * v[M.col[k]];
+            w[r] = dis[r] * acc - bprev * vp[r];
+        }
+        double a = 0.0;
+        for (int64_t r = 0; r < n; ++r) a += w[r] * v[r];
+        double b = 0.0;
+        for (int64_t r = 0; r < n; ++r) {
+            w[r] -= a * v[r];
+            b += w[r] * w[r];
+        }
+        b = std::sqrt(b);
+        alpha.push_back(a);
+        if (j + 1 == m || !(b > 1e-14)) break;
+        beta.push_back(b);
+        for (int64_t r = 0; r < n; ++r) {
+            vp[r] = v[r];
+            v[r] = w[r] / b;
+        }
+        bprev = b;
+    }
+    const int t = (int)alpha.size();
+    auto count_below = [&](double x) {  // eigenvalues of T below x (Sturm sequence)
+        int c = 0;
+        double q = alpha[0] - x;
+        if (q < 0) ++c;
+        for (int i = 1; i < t; ++i) {
+            const double qq = std::abs(q) < 1e-300 ? 1e-300 : q;
+            q = alpha[i] - x - beta[i - 1] * beta[i - 1] / qq;
+            if (q < 0) ++c;
+        }
+        return c;
+    };
+    double lo = 0.0, hi = 0.0;
+    for (int i = 0; i < t; ++i) {
+        const double rad = (i > 0 ? std::abs(beta[i - 1]) : 0.0) + (i + 1 < t ? std::abs(beta[i]) : 0.0);
+        lo = std::min(lo, alpha[i] - rad);
+        hi = std::max(hi, alpha[i] + rad);
+    }
+    auto kth = [&](int k) {  // the k-th smallest eigenvalue (0-based)
+        double a = lo, b = hi;
+        for (int it = 0; it < 200; ++it) {
+            const double mid = 0.5 * (a + b);
+            if (count_below(mid) > k) b = mid;
+            else a = mid;
+        }
+        return 0.5 * (a + b);
+    };
+    *lmin = kth(0);
+    *lmax = kth(t - 1);
+}
+
 // Batched surface-mass solver: one graph of `k` CG iterations over every system, replayed
-// until every system reports done through the host-mapped mirror.
+// until every system reports done through the host-mapped mirror.  Chebyshev mode (cheb_, the
+// default where every system's steps fit kChebMax): a fixed-length Chebyshev iteration first, one
+// launch per step, then the CG from its iterate -- usually converged at its first check.
+constexpr int64_t kChebMax = 120;
 class MassBatch {
 public:
     int nsys = 0;
@@ -772,6 +964,11 @@ public:
     int64_t k = 8;
     int64_t last_iters = 0;
     double alg_bytes = 0.0;  // accumulated by check(): init + iterations of every system
+    // Chebyshev mode: spectral bounds per system from build(), steps from the first solve's rtol
+    bool cheb_ = false;
+    int64_t cheb_k_ = 0;                       // steps of the captured Chebyshev graph (max over systems)
+    std::vector<double> lam_lo_, lam_hi_;      // D^-1 M spectrum bounds used, per system
+    std::vector<int32_t> cheb_ks_;             // steps per system
 
     // A[i] = system i (rows m_i), placed at rows roff[i] (multiples of 64) of nrow_total.
     void build(const std::vector<const Csr*>& A, const std::vector<int64_t>& roff, int64_t nrow_total) {
@@ -841,6 +1038,23 @@ public:
         }
         partial.alloc(3 * std::max<int64_t>(nch, 1));  // (a, b) pairs + the fused form's p.q
         sc.alloc(std::max(nsys, 1));
+        // Chebyshev bounds: [0.9 Ritz min, min(Gershgorin, 1.05 Ritz max)] of D^-1 M after 60 Lanczos
+        // steps (the CG that follows the fixed step count repairs an estimate that was off);
+        // DDPCA_MASS_CHEB=0 keeps the plain CG
+        const char* ce = std::getenv("DDPCA_MASS_CHEB");
+        cheb_ = !(ce && ce[0] == '0') && nsys > 0;
+        lam_lo_.assign(nsys, 0.0);
+        lam_hi_.assign(nsys, 0.0);
+        if (cheb_) {
+            std::vector<double> lo(nsys), hi(nsys), gh(nsys);
+#pragma omp parallel for schedule(dynamic, 1)
+            for (int s2 = 0; s2 < nsys; ++s2) mass_spectrum(*A[s2], 60, &lo[s2], &hi[s2], &gh[s2]);
+            for (int s2 = 0; s2 < nsys; ++s2) {
+                lam_lo_[s2] = 0.9 * lo[s2];
+                lam_hi_[s2] = std::min(gh[s2], 1.05 * hi[s2]);
+                if (!(lam_lo_[s2] > 0.0) || !(lam_hi_[s2] > lam_lo_[s2])) cheb_ = false;
+            }
+        }
         DDPCA_HIP(hipHostMalloc(reinterpret_cast<void**>(&sc_host), std::max(nsys, 1) * sizeof(PcgScal)));
         mirror.alloc(nsys);
     }
@@ -861,6 +1075,10 @@ public:
             drop_graphs();
             x_target_ = x_out;
         }
+        if (cheb_ && rtol != cheb_rtol_) {
+            drop_graphs();
+            cheb_plan(rtol);
+        }
         if (!graph_) capture(s);
         mirror.reset();  // the previous solve on `s` was paced to completion before this point
         for (int i = 0; i < nsys; ++i) {
@@ -869,11 +1087,20 @@ public:
             sc_host[i].maxit = maxit;
         }
         DDPCA_HIP(hipMemcpyAsync(sc.p, sc_host, nsys * sizeof(PcgScal), hipMemcpyHostToDevice, s));
-        // x0 = 0 (warm starts from the previous ADMM iteration's solution: 39.3 -> 37.1 mass-CG
-        // iterations at the headline, no measurable gain, profiles/r03v)
-        hipLaunchKernelGGL(k_mcg_init, dim3(nb256(nrow)), dim3(256), 0, s, b.p, dinv.p, x_out, r.p, z.p, p.p, q.p,
-                           partial.p, nrow);
-        hipLaunchKernelGGL(k_mcg_fin, dim3(nsys), dim3(256), 0, s, (int)kMcgInit, partial.p, cb.p, sc.p, mirror.dev);
+        // Chebyshev mode: the fixed-length Chebyshev graph, then the CG restarted from its iterate
+        // (the host launches CG replays only once the mirror says a system is not done, or the
+        // stream drained); else x0 = 0 (warm starts from the previous ADMM iteration's solution:
+        // 39.3 -> 37.1 mass-CG iterations at the headline, no measurable gain, profiles/r03v)
+        int64_t launched0 = 0;
+        cheb_used_ = cheb_ && cgraph_;
+        if (cheb_used_) {
+            DDPCA_HIP(hipGraphLaunch(cgraph_, s));
+            launched0 = k + 1;
+        } else {
+            hipLaunchKernelGGL(k_mcg_init, dim3(nb256(nrow)), dim3(256), 0, s, b.p, dinv.p, x_out, r.p, z.p, p.p, q.p,
+                               partial.p, nrow);
+            hipLaunchKernelGGL(k_mcg_fin, dim3(nsys), dim3(256), 0, s, (int)kMcgInit, partial.p, cb.p, sc.p, mirror.dev);
+        }
         if (split_) {
             // fork into the two halves' streams, pace both, join and merge the scalars back
             hipLaunchKernelGGL(k_scal_split, dim3(ceil_div(nsys, 64)), dim3(64), 0, s, sc.p, sc_half_.p, half_.p, nsys);
@@ -881,13 +1108,13 @@ public:
             DDPCA_HIP(hipStreamWaitEvent(s2_, ev_fork_, 0));
             hipStream_t st[2] = {s, s2_};
             const int64_t hz[2] = {horizon(0), horizon(1)};
-            pace_halves(st, graph_h_, mirror, half_host_, k, 0, graph1_h_, hz);
+            pace_halves(st, graph_h_, mirror, half_host_, k, launched0, graph1_h_, hz);
             DDPCA_HIP(hipEventRecord(ev_join_, s2_));
             DDPCA_HIP(hipStreamWaitEvent(s, ev_join_, 0));
             hipLaunchKernelGGL(k_scal_merge, dim3(ceil_div(nsys, 64)), dim3(64), 0, s, sc.p, sc_half_.p, half_.p, nsys);
             return;
         }
-        pace_until_done(s, graph_, mirror, k, 0, graph1_, horizon(-1));
+        pace_until_done(s, graph_, mirror, k, launched0, graph1_, horizon(-1));
     }
 
     // Two-stream split of the systems (as MgpisDevice::set_split): two halves of equal rows, each
@@ -944,11 +1171,19 @@ public:
                 throw ApiError(DDPCA_ENUMERIC, "surface mass CG breakdown in system " + std::to_string(i));
             }
             expect_[i] = mirror.host[i].iter;  // paces the next solve's tail
-            last_iters = std::max<int64_t>(last_iters, mirror.host[i].iter);
+            const int64_t ck = cheb_used_ ? (int64_t)cheb_ks_[i] : 0;
+            last_iters = std::max<int64_t>(last_iters, mirror.host[i].iter + ck);
             if (solved_) {
                 int64_t mit = mirror.host[i].iter;
                 if (pair_used_) mit = i < nsys / 2 ? std::max(mit, mirror.host[i + nsys / 2].iter) : 0;
                 alg_bytes += init_bytes_[i] + (double)mirror.host[i].iter * it_bytes_[i] + (double)mit * mat_bytes_[i];
+                // Chebyshev: init (b, D^-1 read; x, r, d written) + per step (d gathered once, read;
+                // x, r read + written; D^-1 read; d' written: 56 B per row) + the matrix once per
+                // pair + the restart (b, r, D^-1 read; z, p, q written)
+                if (cheb_used_)
+                    alg_bytes += init_bytes_[i] * (40.0 / 56.0) + (double)ck * (it_bytes_[i] * (56.0 / 112.0)) +
+                                 (pair_used_ ? (i < nsys / 2 ? (double)ck * mat_bytes_[i] : 0.0) : (double)ck * mat_bytes_[i]) +
+                                 init_bytes_[i] * (48.0 / 56.0);
             }
         }
         solved_ = false;
@@ -974,7 +1209,7 @@ private:
         return h;
     }
     void drop_graphs() {
-        for (hipGraphExec_t* g : {&graph_h_[0], &graph_h_[1], &graph1_h_[0], &graph1_h_[1], &graph1_}) {
+        for (hipGraphExec_t* g : {&graph_h_[0], &graph_h_[1], &graph1_h_[0], &graph1_h_[1], &graph1_, &cgraph_}) {
             if (*g) (void)hipGraphExecDestroy(*g);
             *g = nullptr;
         }
@@ -982,6 +1217,47 @@ private:
         graph_ = nullptr;
     }
     double* x_target_ = nullptr;
+    hipGraphExec_t cgraph_ = nullptr;  // Chebyshev: init, steps, CG restart
+    double cheb_rtol_ = -1.0;
+    bool cheb_used_ = false;
+    DevBuf<double> ccoef_, cith_;
+    DevBuf<int32_t> ckmax_;
+    // the step counts and coefficients for a relative residual rtol: per system kappa = hi / lo,
+    // K = ceil(ln(4 sqrt(kappa) / rtol) / ln sigma), sigma = (sqrt(kappa) + 1) / (sqrt(kappa) - 1)
+    // (the residual bound 2 sqrt(kappa) sigma^-K at half of rtol); none past kChebMax
+    void cheb_plan(double rtol) {
+        cheb_rtol_ = rtol;
+        cheb_ks_.assign(nsys, 0);
+        int64_t K = 0;
+        for (int s2 = 0; s2 < nsys; ++s2) {
+            const double kap = lam_hi_[s2] / lam_lo_[s2], sk = std::sqrt(kap);
+            const double sig = (sk + 1.0) / (sk - 1.0);
+            const int64_t ks = (int64_t)std::ceil(std::log(4.0 * sk / rtol) / std::log(sig));
+            cheb_ks_[s2] = (int32_t)std::max<int64_t>(1, ks);
+            K = std::max<int64_t>(K, cheb_ks_[s2]);
+        }
+        cheb_k_ = K;
+        if (K > kChebMax) {
+            cheb_ = false;
+            return;
+        }
+        std::vector<double> coef((size_t)2 * K * nsys, 0.0), ith(nsys);
+        for (int s2 = 0; s2 < nsys; ++s2) {
+            const double th = 0.5 * (lam_hi_[s2] + lam_lo_[s2]), de = 0.5 * (lam_hi_[s2] - lam_lo_[s2]);
+            const double s1 = th / de;
+            ith[s2] = 1.0 / th;
+            double rho = 1.0 / s1;
+            for (int64_t kk = 0; kk < K; ++kk) {
+                const double rn = 1.0 / (2.0 * s1 - rho);
+                coef[2 * (kk * nsys + s2)] = rn * rho;
+                coef[2 * (kk * nsys + s2) + 1] = 2.0 * rn / de;
+                rho = rn;
+            }
+        }
+        ccoef_.upload(coef);
+        cith_.upload(ith);
+        ckmax_.upload(cheb_ks_);
+    }
     bool split_ = false;
     hipStream_t s2_ = nullptr;
     hipEvent_t ev_fork_ = nullptr, ev_join_ = nullptr;
@@ -993,6 +1269,7 @@ private:
     bool solved_ = false;
     bool paired_ = false, pair_used_ = false;
     void capture(hipStream_t s) {
+        if (cheb_ && cheb_k_ > 0 && cheb_k_ <= kChebMax) capture_cheb(s);
         if (split_) {
             capture_one(s, sc_half_.p, &graph_h_[0], k);
             capture_one(s, sc_half_.p + nsys, &graph_h_[1], k);
@@ -1005,6 +1282,33 @@ private:
         }
         capture_one(s, sc.p, &graph_, k);
         if (k > 1) capture_one(s, sc.p, &graph1_, 1);
+    }
+    void capture_cheb(hipStream_t s) {
+        EllArgs e{slots.p, off.p, col.p, val.p, csys.p, dinv.p, nch};
+        const char* ep = std::getenv("DDPCA_MCG_PAIR");
+        const bool pair = paired_ && !(ep && std::atoi(ep) == 0);
+        hipGraph_t g;
+        DDPCA_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+        hipLaunchKernelGGL(k_mcheb_init, dim3(nb256(nrow)), dim3(256), 0, s, b.p, dinv.p, cith_.p, csys.p, x_target_, r.p,
+                           z.p, nrow);
+        double* d[2] = {z.p, p.p};
+        for (int64_t kk = 0; kk < cheb_k_; ++kk) {
+            const double* din = d[kk & 1];
+            double* dout = d[(kk + 1) & 1];
+            if (pair)
+                hipLaunchKernelGGL(k_mcheb_step<true>, dim3(ceil_div(nch / 2, 4)), dim3(256), 0, s, e, ccoef_.p, ckmax_.p,
+                                   nsys, (int)kk, din, dout, x_target_, r.p, nrow / 2, nch / 2);
+            else
+                hipLaunchKernelGGL(k_mcheb_step<false>, dim3(ceil_div(nch, 4)), dim3(256), 0, s, e, ccoef_.p, ckmax_.p,
+                                   nsys, (int)kk, din, dout, x_target_, r.p, (int64_t)0, nch);
+        }
+        hipLaunchKernelGGL(k_mcg_restart, dim3(nb256(nrow)), dim3(256), 0, s, b.p, dinv.p, r.p, z.p, p.p, q.p, partial.p,
+                           partial.p + 2 * nch, nrow);
+        hipLaunchKernelGGL(k_mcg_fin_restart, dim3(nsys), dim3(256), 0, s, partial.p, partial.p + 2 * nch, cb.p, sc.p,
+                           mirror.dev);
+        DDPCA_HIP(hipStreamEndCapture(s, &g));
+        DDPCA_HIP(hipGraphInstantiate(&cgraph_, g, nullptr, nullptr, 0));
+        DDPCA_HIP(hipGraphDestroy(g));
     }
     void capture_one(hipStream_t s, PcgScal* scp, hipGraphExec_t* out, int64_t iters) {
         EllArgs e{slots.p, off.p, col.p, val.p, csys.p, dinv.p, nch};

@@ -471,7 +471,11 @@ int mcontact_gpu_destroy(mcontact_t h);
 /* The batched surface-mass solver of the ADMM loop on its own (replaces the interface mass solves
  * of MCONTACT.h:2671-2704: SimplicialLDLT below 120000 rows, MCONTACT.h:838-847, Eigen CG above,
  * 2680-2682): nsys square CSR systems A[s], right-hand sides b and solutions x concatenated in
- * system order; Jacobi-PCG per system from x0 = 0 to ||r|| <= rtol ||b|| or maxit.  fuse_alpha:
+ * system order; Jacobi-PCG per system from x0 = 0 to ||r|| <= rtol ||b|| or maxit -- by default
+ * started by a fixed-length Chebyshev iteration on D^-1 A (bounds from 60 Lanczos steps and
+ * Gershgorin at setup; skipped for the batch when a bound is not positive or the steps exceed 120;
+ * DDPCA_MASS_CHEB=0 turns it off), the CG then restarting from its iterate, iters[] counting the
+ * CG's iterations after the restart.  fuse_alpha:
  * -1 the production rule (alpha inside the update kernel up to 1024 chunks per system), 0 / 1
  * force the separate / fused alpha launch.  iters[nsys] (may be NULL).  On a breakdown (p.q <= 0
  * or not finite) the system's x is its last good iterate and the call returns DDPCA_ENUMERIC. */

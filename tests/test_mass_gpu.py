@@ -21,12 +21,13 @@ def _mass_like(n, seed):
     return (d @ A @ d).tocsr()
 
 
-def test_mass_solve_forms_agree_with_direct_solve(ddpca, gpu):
+def test_mass_solve_forms_agree_with_direct_solve(ddpca, gpu, monkeypatch):
     """Systems of 37 rows (one chunk) to 70,000 rows (1,094 chunks: past the fused form's limit, so
     the default rule -- per batch: fused only when every system is within 1024 chunks -- takes the
     separate launch for this batch and the fused one for the batch without it).  Both forms against
     scipy's direct solve (1e-10) and against each other (1e-12): the same CG, alpha summed in
-    another order."""
+    another order.  (The CG alone: the Chebyshev start is off, DDPCA_MASS_CHEB=0.)"""
+    monkeypatch.setenv("DDPCA_MASS_CHEB", "0")
     sizes = [37, 4000, 18915, 70000]
     A = [_mass_like(n, 20251017 + i) for i, n in enumerate(sizes)]
     rng = np.random.default_rng(7)
@@ -52,11 +53,13 @@ def test_mass_solve_forms_agree_with_direct_solve(ddpca, gpu):
 
 
 @pytest.mark.parametrize("fa", [0, 1], ids=["separate-alpha", "fused-alpha"])
-def test_mass_solve_breakdown_keeps_last_iterate(ddpca, gpu, fa):
+def test_mass_solve_breakdown_keeps_last_iterate(ddpca, gpu, fa, monkeypatch):
     """An indefinite system ([[1, 2], [2, 1]], b on its negative eigenvector: p.q = -2 at the first
     step) next to a healthy one: DDPCA_ENUMERIC, the failing system's x stays its last good iterate
     (x0 = 0) in both forms -- every wave of the fused update sees the same p.q and leaves x, r, z
-    alone -- and the healthy system is still solved."""
+    alone -- and the healthy system is still solved.  (The indefinite system's spectrum estimate is
+    not positive, so the batch would skip the Chebyshev start anyway; it is off here.)"""
+    monkeypatch.setenv("DDPCA_MASS_CHEB", "0")
     good = _mass_like(500, 3)
     bad = sp.csr_matrix(np.array([[1.0, 2.0], [2.0, 1.0]]))
     rng = np.random.default_rng(11)
@@ -71,15 +74,57 @@ def test_mass_solve_breakdown_keeps_last_iterate(ddpca, gpu, fa):
     assert np.linalg.norm(e.x[:500] - xr) <= 1e-10 * np.linalg.norm(xr)
 
 
+def test_mass_solve_chebyshev_start(ddpca, gpu, monkeypatch):
+    """The default surface-mass solve: a fixed-length Chebyshev iteration on D^-1 M (bounds from 60
+    Lanczos steps and Gershgorin at setup, one launch per step, no reductions), then the CG
+    restarted from its iterate under the same stop rule (||r|| <= 1e-14 ||b||).  Against scipy's
+    direct solve 1e-10 and against the CG alone 1e-11; the CG after the Chebyshev steps takes at most
+    a handful of iterations.  An indefinite system in the batch turns the Chebyshev start off for the
+    batch (DDPCA_ENUMERIC from the CG as before)."""
+    sizes = [37, 4000, 18915]
+    A = [_mass_like(n, 20251017 + i) for i, n in enumerate(sizes)]
+    rng = np.random.default_rng(9)
+    b = rng.standard_normal(sum(sizes))
+    monkeypatch.setenv("DDPCA_MASS_CHEB", "1")
+    xc, itc = ddpca.mass_solve(A, b)
+    monkeypatch.setenv("DDPCA_MASS_CHEB", "0")
+    xg, itg = ddpca.mass_solve(A, b)
+    print("CG iterations after the Chebyshev steps", list(itc), "CG alone", list(itg))
+    o = 0
+    for k, n in enumerate(sizes):
+        xr = spla.spsolve(A[k].tocsc(), b[o:o + n])
+        assert np.linalg.norm(xc[o:o + n] - xr) <= 1e-10 * np.linalg.norm(xr), n
+        assert np.linalg.norm(xc[o:o + n] - xg[o:o + n]) <= 1e-11 * np.linalg.norm(xg[o:o + n]), n
+        assert 0 <= itc[k] <= 5 and itg[k] > 5, (itc, itg)
+        o += n
+    monkeypatch.setenv("DDPCA_MASS_CHEB", "1")
+    bad = sp.csr_matrix(np.array([[1.0, 2.0], [2.0, 1.0]]))
+    with pytest.raises(ddpca.DdpcaError) as ei:
+        ddpca.mass_solve([A[0], bad], np.concatenate([b[:37], [1.0, -1.0]]))
+    assert ei.value.code == -6
+
+
 def test_admm_trajectory_fused_vs_separate_alpha(ddpca, gpu, monkeypatch):
     """The ADMM loop with the surface-mass CG's alpha fused (the default at the headline's side
     sizes) against the separate k_mcg_fin launch (DDPCA_MCG_FUSE_ALPHA=0): p.q is summed in another
     order, so not bit-identical -- resuMoni rows within 1e-8 relative and displacements within 1e-9
-    after 10 ADMM iterations on the reduced headline chain."""
+    after 10 ADMM iterations on the reduced headline chain (the CG alone, DDPCA_MASS_CHEB=0)."""
+    monkeypatch.setenv("DDPCA_MASS_CHEB", "0")
+    _admm_pair(ddpca, monkeypatch, "DDPCA_MCG_FUSE_ALPHA")
+
+
+def test_admm_trajectory_chebyshev_vs_cg(ddpca, gpu, monkeypatch):
+    """The ADMM loop with the Chebyshev-started surface-mass solves (the default) against the CG
+    alone (DDPCA_MASS_CHEB=0): both stop at ||r|| <= 1e-14 ||b||, so the trajectories agree to the
+    solves' accuracy -- resuMoni rows 1e-8 relative, displacements 1e-9 after 10 ADMM iterations."""
+    _admm_pair(ddpca, monkeypatch, "DDPCA_MASS_CHEB")
+
+
+def _admm_pair(ddpca, monkeypatch, var):
     H, M = ddpca.HEADLINE_OPTIONS, ddpca.HEADLINE_MUSC
     out = {}
     for v in ("0", "1"):
-        monkeypatch.setenv("DDPCA_MCG_FUSE_ALPHA", v)
+        monkeypatch.setenv(var, v)
         P = ddpca.headline_problem(gl=3)
         P.set_coarse(M["muscSett"], [M["doleMcsc"]] * P.nsub)
         P.ESTABLISH()
@@ -91,6 +136,6 @@ def test_admm_trajectory_fused_vs_separate_alpha(ddpca, gpu, monkeypatch):
     scale = np.abs(a).max(axis=0, keepdims=True)
     rel = np.abs(a - b) / np.maximum(np.abs(a), 1e-12 * scale)
     du = max(np.linalg.norm(x - y) / np.linalg.norm(y) for x, y in zip(out["0"][1], out["1"][1]) if np.any(y))
-    print(f"fused vs separate alpha: worst resuMoni rel {rel.max():.2e}, displacements {du:.2e}")
+    print(f"{var} 0 vs 1: worst resuMoni rel {rel.max():.2e}, displacements {du:.2e}")
     assert rel.max() <= 1e-8
     assert du <= 1e-9
