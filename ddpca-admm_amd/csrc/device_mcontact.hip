@@ -1055,6 +1055,9 @@ public:
                 if (!(lam_lo_[s2] > 0.0) || !(lam_hi_[s2] > lam_lo_[s2])) cheb_ = false;
             }
         }
+        // the ADMM loop's tolerance planned here, at setup: solve() uploads nothing while other
+        // in-process ranks may be capturing graphs
+        if (cheb_) cheb_plan(1.0e-14);
         DDPCA_HIP(hipHostMalloc(reinterpret_cast<void**>(&sc_host), std::max(nsys, 1) * sizeof(PcgScal)));
         mirror.alloc(nsys);
     }
@@ -1288,7 +1291,7 @@ private:
         const char* ep = std::getenv("DDPCA_MCG_PAIR");
         const bool pair = paired_ && !(ep && std::atoi(ep) == 0);
         hipGraph_t g;
-        DDPCA_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+        DDPCA_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed));
         hipLaunchKernelGGL(k_mcheb_init, dim3(nb256(nrow)), dim3(256), 0, s, b.p, dinv.p, cith_.p, csys.p, x_target_, r.p,
                            z.p, nrow);
         double* d[2] = {z.p, p.p};
@@ -1313,7 +1316,7 @@ private:
     void capture_one(hipStream_t s, PcgScal* scp, hipGraphExec_t* out, int64_t iters) {
         EllArgs e{slots.p, off.p, col.p, val.p, csys.p, dinv.p, nch};
         hipGraph_t g;
-        DDPCA_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+        DDPCA_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed));
         const bool fa = fuse_alpha();
         // DDPCA_MCG_PAIR=0: the unpaired k_mcg_spmv on a paired batch (bit-identical, A/B and tests)
         const char* ep = std::getenv("DDPCA_MCG_PAIR");
