@@ -367,7 +367,8 @@ def test_torsion_known_answer(gpu, tmp_path):
     rk = res["ranks"]
     assert rk["nranks"] == 4 and rk["cross_interfaces"] == res["interfaces"], rk
     assert rk["iters"] == [rk["iters_1rank"]] * 4, rk
-    assert rk["moni_rel"] <= 1e-7 and rk["resuDisp_rel"] <= 1e-8 and rk["gamma_rel"] <= 1e-7, rk
+    assert rk["moni_rel"] <= 1e-7 and rk["moni_diff_rel"] <= 1e-6, rk
+    assert rk["resuDisp_rel"] <= 1e-8 and rk["gamma_rel"] <= 1e-7, rk
     assert abs(res["iters_gpu"] - res["iters_ref"]) <= 1, res
     assert res["resuDisp_rel"] <= 1e-6, res
     assert abs(res["umax_gpu"] - res["umax_ref"]) <= 1e-6 * res["umax_ref"], res
@@ -495,5 +496,9 @@ def test_cylinder_two_ranks_in_one_process(gpu, tmp_path, owners):
     r2 = res["ranks2"]
     assert r2["cross_interfaces"] == (1 if owners == "0011" else 3), r2
     assert r2["iters"] == [r2["iters_1rank"], r2["iters_1rank"]] and r2["iters_1rank"] > 1, r2
-    assert r2["moni_rel"] <= 1e-7 and r2["resuDisp_rel"] <= 1e-8 and r2["gamma_rel"] <= 1e-7, r2
+    # resuMoni: the norm columns at SURVEY c4's 1e-7, the successive-difference columns (late rows:
+    # differences of nearly equal iterates) at 1e-6 -- measured 5.9e-8 / 1.0e-7 on all columns
+    # before the split, the rank split's other summation order of the coarse operator showing there
+    assert r2["moni_rel"] <= 1e-7 and r2["moni_diff_rel"] <= 1e-6, r2
+    assert r2["resuDisp_rel"] <= 1e-8 and r2["gamma_rel"] <= 1e-7, r2
 
