@@ -1120,6 +1120,17 @@ public:
         pace_until_done(s, graph_, mirror, k, launched0, graph1_, horizon(-1));
     }
 
+    // capture the solve's graphs now (create time, one thread) for solves into x_out: the first
+    // solve of an in-process rank then captures nothing while the other rank threads run
+    void prepare(hipStream_t s, double* x_out) {
+        if (nsys == 0) return;
+        if (x_out != x_target_) {
+            drop_graphs();
+            x_target_ = x_out;
+        }
+        if (!graph_) capture(s);
+    }
+
     // Two-stream split of the systems (as MgpisDevice::set_split): two halves of equal rows, each
     // half's CG iterations a graph of its own on its own stream, on a copy of the scalars where
     // the other half's systems are done -- the latency-bound launches of the two halves overlap.
@@ -1291,7 +1302,7 @@ private:
         const char* ep = std::getenv("DDPCA_MCG_PAIR");
         const bool pair = paired_ && !(ep && std::atoi(ep) == 0);
         hipGraph_t g;
-        DDPCA_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed));
+        DDPCA_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
         hipLaunchKernelGGL(k_mcheb_init, dim3(nb256(nrow)), dim3(256), 0, s, b.p, dinv.p, cith_.p, csys.p, x_target_, r.p,
                            z.p, nrow);
         double* d[2] = {z.p, p.p};
@@ -1316,7 +1327,7 @@ private:
     void capture_one(hipStream_t s, PcgScal* scp, hipGraphExec_t* out, int64_t iters) {
         EllArgs e{slots.p, off.p, col.p, val.p, csys.p, dinv.p, nch};
         hipGraph_t g;
-        DDPCA_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed));
+        DDPCA_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
         const bool fa = fuse_alpha();
         // DDPCA_MCG_PAIR=0: the unpaired k_mcg_spmv on a paired batch (bit-identical, A/B and tests)
         const char* ep = std::getenv("DDPCA_MCG_PAIR");
@@ -2976,6 +2987,21 @@ bool iterate_once(ddpca_mcontact& H, bool check) {
 
 extern "C" {
 
+// Every graph the ADMM iteration replays, captured on the calling thread (create, or after the
+// in-process ranks' setup threads joined): a capture running on one rank thread was invalidated
+// by another rank thread's synchronous HIP calls in the in-process multi-rank runs.
+// Idempotent: what exists is kept.
+void prepare_graphs(ddpca_mcontact& H) {
+    if (H.mg) H.mg->prepare_graphs(1);
+    if (H.fused) H.mb_wv.prepare(H.main, H.mb_wv.x.p);
+    else if (!H.sides.empty()) {
+        H.mb_aux.prepare(H.main, H.state);
+        H.mb_lam.prepare(H.main, H.mb_lam.x.p);
+    }
+    if (H.cs.cmg) H.cs.cmg->prepare_graphs(1);
+    DDPCA_HIP(hipStreamSynchronize(H.main));
+}
+
 int mcontact_gpu_create(ddpca_problem_t p, int device, int rank, int nranks, const int32_t* owner,
                         const mgpis_options_t* opt, mcontact_t* out) {
     return guarded([&] {
@@ -2996,6 +3022,7 @@ int mcontact_gpu_create(ddpca_problem_t p, int device, int rank, int nranks, con
         build(*H, P);
         build_coarse(*H, P);
         if (nranks == 1) coarse_invert(*H);
+        prepare_graphs(*H);
         *out = H.release();
     });
 }
@@ -3021,6 +3048,7 @@ int mcontact_gpu_comm_init(mcontact_t h, const void* uid) {
         DDPCA_NCCL(ncclCommInitRank(&t->comm, h->nranks, id, h->rank));
         h->comm = std::move(t);
         coarse_invert(*h);
+        prepare_graphs(*h);
     });
 }
 
@@ -3056,6 +3084,10 @@ int mcontact_gpu_comm_local(mcontact_t* handles, int n) {
         for (auto& t : th) t.join();
         for (int r = 0; r < n; ++r)
             if (rc[r] < 0) throw ApiError(rc[r], "rank " + std::to_string(r) + ": " + msg[r]);
+        for (int r = 0; r < n; ++r) {  // the gathered DOUBLE_M solvers' graphs, one rank at a time
+            select_device(handles[r]->device);
+            prepare_graphs(*handles[r]);
+        }
     });
 }
 
@@ -3079,6 +3111,7 @@ int mcontact_gpu_comm_loopback(mcontact_t h, ddpca_problem_t p) {
                     C.dense[(size_t)r * n + cs.globCoup_1.col[k]] = cs.globCoup_1.val[k];
         }
         coarse_invert(*h);
+        prepare_graphs(*h);
     });
 }
 

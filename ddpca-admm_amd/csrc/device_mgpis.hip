@@ -3069,7 +3069,7 @@ hipGraphExec_t MgpisDevice::capture_iterations(int prec, int count, PcgScal* scp
     sc_cur_ = scp;
     hipGraph_t g;
     hipGraphExec_t ge = nullptr;
-    DDPCA_HIP(hipStreamBeginCapture(stream, hipStreamCaptureModeRelaxed));
+    DDPCA_HIP(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
     for (int k = 0; k < count; ++k) enqueue_iteration(prec, false);
     DDPCA_HIP(hipStreamEndCapture(stream, &g));
     sc_cur_ = nullptr;

@@ -302,6 +302,8 @@ public:
     // `stream` over the whole batch.
     void set_split(bool on);
     bool split() const { return split_; }
+    // capture the PCG graphs of preconditioner prec now (create time) instead of at the first solve
+    void prepare_graphs(int prec) { build_graph(prec); }
 
 private:
     hipGraphExec_t graph_[2] = {nullptr, nullptr};

@@ -159,7 +159,7 @@ extern "C" int ddpca_probe_grid_barrier(int device, int64_t n, int phases, int b
         hipGraphExec_t ge;
         xg.upload(h);
         yg.alloc(n);
-        DDPCA_HIP(hipStreamBeginCapture(st, hipStreamCaptureModeRelaxed));
+        DDPCA_HIP(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
         for (int p = 0; p < phases; ++p)
             hipLaunchKernelGGL(k_phase, dim3(blocks), dim3(256), 0, st, (p & 1) ? yg.p : xg.p, (p & 1) ? xg.p : yg.p, n);
         DDPCA_HIP(hipStreamEndCapture(st, &g));
