@@ -66,8 +66,8 @@ def parse():
     ap.add_argument("--warm-start", type=int, default=H["warm_start"],
                     help="1: each subdomain PCG starts from its previous solution (same 1e-14 stop rule)")
     ap.add_argument("--precond-fp32", type=int, default=H["precond_fp32"],
-                    help="1: V-cycle level operators stored in fp32; 2: and the fine level's V-cycle copy in block-exponent fp16 "
-                         "(arithmetic, Krylov operator and stop rule fp64)")
+                    help="1: V-cycle level operators stored in fp32; 2: and the finest levels' V-cycle copies in block-exponent fp16; "
+                         "3: in block-scaled int8 instead (arithmetic, Krylov operator and stop rule fp64)")
     ap.add_argument("--table-mode", type=int, default=H["table_mode"],
                     help="1: keep one copy of bit-identical operator rows (pays on regular meshes only; the "
                          "synthetic box mesh is far more regular than DEHW's curved one, so the headline keeps 0)")
@@ -239,7 +239,9 @@ def main():
                 "pcg_x0": "previous solution" if a.warm_start else "zero",
                 "vcycle_operator_storage": {0: "fp64", 1: "fp32",
                                             2: f"fp32, the {os.environ.get('DDPCA_H16_LEVELS', '3')} finest levels "
-                                               "block-exponent fp16"}[a.precond_fp32],
+                                               "block-exponent fp16",
+                                            3: f"fp32, the {os.environ.get('DDPCA_H16_LEVELS', '3')} finest levels "
+                                               "block-scaled int8"}[a.precond_fp32],
                 "operator_rows": "deduplicated table" if a.table_mode else "streamed",
                 "coarse_space": f"interface-eliminated (muscSett={a.musc}, doleMcsc={a.dole})" if a.musc else "none",
                 **({"hanging_dofs": int(sum(P.grid(tv).hangRows().shape[0] for tv in range(nsub) if owner[tv] == rank)),

@@ -166,6 +166,7 @@ def _declare(L: C.CDLL) -> None:
                                      C.POINTER(C.c_int)]
     L.mgpis_gpu_gmres.argtypes = [_P, _P, _P, C.c_int, C.c_double, C.c_int64, C.c_int64, _I64P, _DP]
     L.mgpis_gpu_spmv.argtypes = [_P, C.c_int, _P, _P]
+    L.mgpis_gpu_spmv_copy.argtypes = [_P, C.c_int, C.c_int, _P, _P]
     L.ddpca_write_resuDisp.argtypes = [C.c_char_p, _P, C.c_int64, C.c_int64, _P, _P]
     L.ddpca_write_resuCont.argtypes = [C.c_char_p, C.c_double, C.c_int64, _P, _P, _P]
     L.ddpca_write_resuMoni.argtypes = [C.c_char_p, _P, C.c_int64, C.c_int64]
@@ -754,6 +755,13 @@ class MGPIS:
         y = np.zeros_like(x)
         info = self.info()
         _check(lib().mgpis_gpu_spmv(self._h, info["nlev"] - 1, _ptr(x), _ptr(y)))
+        return y
+
+    def spmv_vcycle_copy(self, x: np.ndarray) -> np.ndarray:
+        """y = K x through the V-cycle's reduced-precision copy of the fine level (precond_fp32 >= 1)."""
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        y = np.zeros_like(x)
+        _check(lib().mgpis_gpu_spmv_copy(self._h, self.info()["nlev"] - 1, 1, _ptr(x), _ptr(y)))
         return y
 
 

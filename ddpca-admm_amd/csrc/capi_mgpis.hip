@@ -235,18 +235,22 @@ int mgpis_gpu_gmres(mgpis_t h, const double* b, double* x, int prec, double rtol
     });
 }
 
-int mgpis_gpu_spmv(mgpis_t h, int level, const double* x, double* y) {
+int mgpis_gpu_spmv(mgpis_t h, int level, const double* x, double* y) { return mgpis_gpu_spmv_copy(h, level, 0, x, y); }
+
+int mgpis_gpu_spmv_copy(mgpis_t h, int level, int vcycle_copy, const double* x, double* y) {
     return guarded([&] {
+        if (!h || !x || !y) throw ApiError(DDPCA_EINVAL, "null argument");
         MgpisDevice& D = *h->dev;
         select_device(D.device);
         if (level < 0 || level >= (int)D.lev.size()) throw ApiError(DDPCA_EINVAL, "level");
         if (level != (int)D.lev.size() - 1) throw ApiError(DDPCA_EINVAL, "condensed spmv is defined on the fine level");
+        if (vcycle_copy && D.vc_type(level) == kVal64) throw ApiError(DDPCA_EINVAL, "no reduced-precision V-cycle copy (precond_fp32 = 0)");
         DevBuf<double> tmp, full_x, full_y;
         tmp.upload(x, D.nfree[0]);
         full_x.alloc(3 * D.lev.back().nn);
         full_y.alloc(3 * D.lev.back().nn);
         D.scatter_free(0, tmp.p, full_x.p);
-        D.spmv(level, full_x.p, full_y.p);
+        D.spmv(level, full_x.p, full_y.p, vcycle_copy != 0);
         D.gather_free(0, full_y.p, tmp.p);
         DDPCA_HIP(hipMemcpyAsync(y, tmp.p, D.nfree[0] * sizeof(double), hipMemcpyDeviceToHost, D.stream));
         DDPCA_HIP(hipStreamSynchronize(D.stream));
@@ -295,7 +299,7 @@ int mgpis_gpu_bench_spmv(mgpis_t h, int variant, int reps, double* ms, double* b
         const double per_node[4] = {24.0, 96.0, 48.0, 24.0 * 5.0 + 72.0};
         const int mode = (variant >> 2) & 3;
         const bool f32 = (variant & 16) != 0;
-        if (bytes) *bytes = D.fine_matrix_bytes(0, !f32 ? kVal64 : D.lev.back().val16.p ? kValH16 : kVal32, false) + (24.0 + per_node[mode]) * (double)D.lev.back().nloc[0];
+        if (bytes) *bytes = D.fine_matrix_bytes(0, !f32 ? kVal64 : D.vc_type((int)D.lev.size() - 1), false) + (24.0 + per_node[mode]) * (double)D.lev.back().nloc[0];
     });
 }
 

@@ -43,7 +43,7 @@
 namespace ddpca {
 
 // Storage type of streamed operator values (arithmetic is fp64 throughout).
-enum ValType { kVal64 = 0, kVal32 = 1, kValH16 = 2 };  // H16: block-exponent fp16
+enum ValType { kVal64 = 0, kVal32 = 1, kValH16 = 2, kValQ8 = 3 };  // H16: block-exponent fp16, Q8: block-scaled int8
 
 // Per-subdomain scalar block of the PCG recurrence (device memory, read by every kernel).
 struct PcgScal {
@@ -84,6 +84,7 @@ struct LevelDev {
                            // V-cycle runs on fp64 operators
     DevBuf<float> val32;   // V-cycle operator rounded once to fp32 (opt.precond_fp32), levels >= 1
     DevBuf<uint16_t> val16;  // fine level's V-cycle copy in block-exponent fp16 (opt.precond_fp32 = 2)
+    DevBuf<int8_t> val8;     // ... in block-scaled int8 (opt.precond_fp32 = 3)
     // table mode: rows whose block values (in device slot order, masks applied) are bit-identical
     // share one table row; the kernel streams only column indices and a row type, the values
     // come from the cache-resident table (structured meshes: ~30x fewer distinct rows than rows)
@@ -154,6 +155,7 @@ struct GsFine {
     DevBuf<int32_t> col;                 // per slot lane (when the level has no 16-bit offsets)
     DevBuf<int16_t> col16;
     DevBuf<uint16_t> val16;
+    DevBuf<int8_t> val8;
     DevBuf<float> val32;
     DevBuf<double> val64;
     DevBuf<float> minvc;                 // the rows' fp32 3x3 inverses in chunk order, [chunk][ij][lane]
@@ -245,7 +247,7 @@ public:
     // storage type of the V-cycle's copy of level l (table-mode levels: the table)
     int vc_type(int l) const {
         if (!vc32() || lev[l].tbl) return kVal64;
-        return lev[l].val16.p ? kValH16 : kVal32;
+        return lev[l].val8.p ? kValQ8 : lev[l].val16.p ? kValH16 : kVal32;
     }
     // z = M^-1 r (fine level); dot: leave the partials of r.z (vc_partial)
     void vcycle(const double* r, double* z, bool dot);

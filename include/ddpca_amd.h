@@ -57,7 +57,9 @@ typedef struct {
                           2: as 1, and the fine level's V-cycle copy (smoothing sweeps and the
                           V-cycle residual) stored as block-exponent fp16 (2^e x nine fp16 per 3x3
                           block) -- 24 instead of 40 B per block on the two fine smoother passes
-                          of every PCG iteration. */
+                          of every PCG iteration.
+                          3: as 2 with block-scaled int8 instead of fp16 (2^s x nine int8 per
+                          block, 7-8 significant bits of the block maximum) -- 12 B per block. */
     int table_mode;    /* levels >= 1: 0 stream every block value; 1 (default) when the rows'
                           block values deduplicate well (structured meshes), keep one copy per
                           distinct row in a cache-resident table and stream only column indices
@@ -143,6 +145,11 @@ int mgpis_gpu_gmres(mgpis_t h, const double* b, double* x, int prec, double rtol
                     int64_t restart, int64_t* iters, double* relres);
 /* y = consStif[level] * x (condensed host vectors), for parity tests of the SpMV kernel. */
 int mgpis_gpu_spmv(mgpis_t h, int level, const double* x, double* y);
+/* The same through the V-cycle's stored copy of the fine level (vcycle_copy = 1: fp32,
+ * block-exponent fp16 or block-scaled int8 values per precond_fp32; DDPCA_EINVAL without one),
+ * or the fp64 operator (0) -- the decode of the reduced-precision records against their host
+ * rounding, for parity tests. */
+int mgpis_gpu_spmv_copy(mgpis_t h, int level, int vcycle_copy, const double* x, double* y);
 /* z = M^-1 r: one V-cycle from zero (MGPIS::MULT_VCYC, MGPIS.h:55-128) on condensed vectors. */
 int mgpis_gpu_vcycle(mgpis_t h, const double* r, double* z);
 /* Informational: [nlev, n_fine_free, nnzb_fine, chunks_fine, omega*1e6, lambda_max*1e6, device] */

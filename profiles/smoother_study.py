@@ -276,6 +276,21 @@ def round_h16(K, node):
     return sp.csr_matrix((v, (Kc.row, Kc.col)), shape=K.shape)
 
 
+def round_i8(K, node, bits=8):
+    """K with every 3x3 node block stored as 2^e x nine signed (bits)-bit integers (a block-scaled
+    integer copy: |q| <= 2^(bits-1) - 1, e the smallest exponent that fits the block's largest entry)"""
+    Kc = K.tocoo()
+    key = node[Kc.row].astype(np.int64) * (node.max() + 1) + node[Kc.col]
+    uk, inv = np.unique(key, return_inverse=True)
+    mx = np.zeros(len(uk))
+    np.maximum.at(mx, inv, np.abs(Kc.data))
+    qmax = 2 ** (bits - 1) - 1
+    e = np.ceil(np.log2(np.maximum(mx, 1e-300) / qmax))
+    sc = np.ldexp(1.0, e.astype(np.int64))[inv]
+    v = np.clip(np.rint(Kc.data / sc), -qmax, qmax) * sc
+    return sp.csr_matrix((v, (Kc.row, Kc.col)), shape=K.shape)
+
+
 def main():
     global TILE, GENERAL, ORDER, NEWONLY, RHS
     if "--rhs" in sys.argv:
@@ -295,6 +310,16 @@ def main():
         Kv = K[:-1] + [K16]
         print("fine level rounded to block-exponent fp16: |K16 - K| / |K| =",
               spl.norm(K16 - K[-1]) / spl.norm(K[-1]))
+    elif "--i8" in sys.argv or "--ibits" in sys.argv:
+        # the V-cycle's finest levels on a block-scaled integer copy (--ibits B, default 8; --ilevels N
+        # finest levels, default 1)
+        bits = int(sys.argv[sys.argv.index("--ibits") + 1]) if "--ibits" in sys.argv else 8
+        nl = int(sys.argv[sys.argv.index("--ilevels") + 1]) if "--ilevels" in sys.argv else 1
+        Kv = list(K)
+        for l in range(len(K) - nl, len(K)):
+            Kv[l] = round_i8(K[l], node[l], bits)
+            print(f"level {l} rounded to block-scaled int{bits}: |Kq - K| / |K| =",
+                  spl.norm(Kv[l] - K[l]) / spl.norm(K[l]))
     else:
         Kv = K
     print(f"gl {gl} subdomain {tv}: levels {len(K)}, fine rows {K[-1].shape[0]}")

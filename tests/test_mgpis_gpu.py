@@ -112,7 +112,7 @@ def test_vcycle_is_symmetric_positive(ddpca, gpu):
     n = len(P.grid(0).consForc)
     rng = np.random.default_rng(20251017)
     for smoother, nu, f32 in [(0, 1, 0), (1, 1, 0), (2, 2, 0), (2, 2, 1), (1, 1, 2), (2, 2, 2), (3, 1, 0), (3, 2, 1),
-                              (3, 2, 2)]:
+                              (3, 2, 2), (1, 1, 3), (3, 2, 3)]:
         M = ddpca.MGPIS.from_problem(P, 0, smoother=smoother, nu=nu, precond_fp32=f32)
         u, v = rng.standard_normal(n), rng.standard_normal(n)
         Mu, Mv = M.MULT_VCYC(u), M.MULT_VCYC(v)
@@ -136,6 +136,72 @@ def test_multicolour_gauss_seidel_on_the_headline_subdomains(ddpca, gpu, f32):
         assert rr <= 1e-14
         assert ig <= 0.85 * ij, (ig, ij)
         assert np.linalg.norm(xg - xj) <= 1e-10 * np.linalg.norm(xj)
+
+
+def test_int8_smoother_copy_keeps_the_solution(ddpca, gpu):
+    """precond_fp32 = 3: the fine levels' V-cycle copies in block-scaled int8 (2^s x nine int8 per
+    3x3 block) instead of block-exponent fp16.  The Krylov operator and the stop rule stay fp64:
+    the same ||r|| <= 1e-14 ||b||, the solution within the PCG's tolerance of the fp16 run's, and
+    at most two more iterations on the headline's subdomains (CPU study at gl = 5 on late
+    right-hand sides: 18-19 against 18, profiles/smoother_study.py --ibits 8).  The int8 blocks
+    decode to exactly the host rounding: y = K_q8 x through the V-cycle copy matches the
+    restated rounding applied to the fp64 operator."""
+    P = ddpca.headline_problem(gl=3).ESTABLISH()
+    for tv in (0, 1):
+        b = P.grid(tv).consForc
+        if not np.any(b):
+            b = np.random.default_rng(tv).standard_normal(len(b))
+        x2, i2, _ = ddpca.MGPIS.from_problem(P, tv, smoother=3, nu=2, omega=-1.7, precond_fp32=2).CG_SOLV(1, b)
+        x3, i3, rr = ddpca.MGPIS.from_problem(P, tv, smoother=3, nu=2, omega=-1.7, precond_fp32=3).CG_SOLV(1, b)
+        print(tv, "fp16 copy", i2, "int8 copy", i3)
+        assert rr <= 1e-14
+        assert i3 <= i2 + 2, (i3, i2)
+        assert np.linalg.norm(x3 - x2) <= 1e-10 * np.linalg.norm(x2)
+
+
+def _round_blocks(K, node, kind):
+    """K with every 3x3 node block rounded as the device stores its V-cycle copy: kind 2 block-exponent
+    fp16 (2^e x fp16, e = frexp exponent of the block maximum), kind 3 block-scaled int8 (2^(e-7) x
+    int8, clamped to +-127)"""
+    Kc = K.tocoo()
+    key = node[Kc.row].astype(np.int64) * (node.max() + 1) + node[Kc.col]
+    _, inv = np.unique(key, return_inverse=True)
+    mx = np.zeros(inv.max() + 1)
+    np.maximum.at(mx, inv, np.abs(Kc.data))
+    e = np.frexp(mx)[1][inv]
+    if kind == 2:
+        v = np.ldexp(np.ldexp(Kc.data, -e).astype(np.float16).astype(np.float64), e)
+    else:
+        v = np.ldexp(np.clip(np.rint(np.ldexp(Kc.data, 7 - e)), -127, 127), e - 7)
+    return sp.csr_matrix((v, (Kc.row, Kc.col)), shape=K.shape)
+
+
+@pytest.mark.parametrize("lowp", [2, 3])
+def test_reduced_precision_copy_decodes_the_host_rounding(ddpca, gpu, lowp):
+    """The V-cycle's fine-level copy (precond_fp32 = 2: block-exponent fp16, 3: block-scaled int8)
+    applied through the device kernels equals the restated rounding of the fp64 operator applied
+    in fp64 (only the summation order differs), and differs from the fp64 product by the
+    rounding's size -- the records are decoded exactly, not approximately."""
+    P = ddpca.headline_problem(gl=3).ESTABLISH()
+    tv = 1
+    G = P.grid(tv)
+    L = G.maxiLeve
+    nn = [int(v) for v in P.array("leveCount", tv)]
+    flag = np.asarray(P.array("consFlag", tv))
+    node = np.nonzero(flag[:3 * nn[L]])[0] // 3
+    K = G.consStif(L).tocsr()
+    x = np.random.default_rng(7).standard_normal(K.shape[0])
+    M = ddpca.MGPIS.from_problem(P, tv, smoother=3, nu=2, omega=-1.7, precond_fp32=lowp)
+    y = M.spmv_vcycle_copy(x)
+    yq = _round_blocks(K, node, lowp) @ x
+    y64 = K @ x
+    rel = np.linalg.norm(y - yq) / np.linalg.norm(yq)
+    off = np.linalg.norm(y - y64) / np.linalg.norm(y64)
+    print("lowp", lowp, "device vs host rounding", rel, "vs fp64", off)
+    assert rel <= 1e-13
+    assert off >= (1e-6 if lowp == 2 else 1e-4)
+    assert np.array_equal(M.spmv(x), M.spmv(x))  # the fp64 path untouched
+    assert np.linalg.norm(M.spmv(x) - y64) <= 1e-13 * np.linalg.norm(y64)
 
 
 def test_csr_dropin_matches_native(ddpca, gpu):
