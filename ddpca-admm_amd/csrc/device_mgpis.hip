@@ -107,16 +107,16 @@ typedef double dbl2_t __attribute__((ext_vector_type(2)));
 // 256-B dword run per pair: a slot is 1280 B, 20 B per block against 36 B for fp32.  A block
 // and its transpose share e and round alike, so the operator stays exactly symmetric.
 //
-// Block-scaled int8 storage (T = int8_t; precond_fp32 = 3): each 3x3 block is 2^s times nine
-// int8 values, s = e - 7 for the block's largest |entry| = f 2^e (f in [0.5, 1)), so the largest
-// entry keeps 7-8 significant bits and every entry is within 2^(s-1) of its value; the record is
-// ten bytes, (q0..q3) (q4..q7) as two 256-B dword runs and (q8, s) as one 128-B ushort run: a
-// slot is 640 B, 10 B per block against 20 for fp16.  Symmetric as the fp16 copy.  With the
-// Krylov operator and the stop rule in fp64 only the preconditioner moves: 18-19 PCG iterations
-// on the headline's late right-hand sides against 18 with the fp16 copy (profiles/smoother_study.py
-// --ibits 8).
+// Block-scaled int8 storage (T = uint8_t; precond_fp32 = 3): nine int8 values times a per-block
+// scale max|entry| / 127 kept to 16 mantissa bits (the fp32 scale's top 24 bits, the low byte of
+// its word holds q8), so the largest entry maps to 127 and every entry is within half a scale of
+// its value; the record is three 256-B dword runs per slot, (q0..q3) (q4..q7) (q8 | scale bits
+// 8..31): 12 B per block against 20 for fp16.  Symmetric as the fp16 copy (a block and its
+// transpose share the scale).  With the Krylov operator and the stop rule in fp64 only the
+// preconditioner moves: 18-19 PCG iterations per solve against 18 with the fp16 copy, the
+// headline +5.7 % (a power-of-two scale, 10 B per block, took 19-20 and +4.0 %).
 template <typename T>
-constexpr int slot_vals() { return sizeof(T) <= 2 ? 10 : 9; }
+constexpr int slot_vals() { return sizeof(T) == 1 ? 12 : sizeof(T) == 2 ? 10 : 9; }
 
 // storage type of the smoother inverse on a level whose operator values are stored as T: fp64
 // with fp64 operators, fp32 on the reduced-precision levels (precond_fp32 >= 1)
@@ -138,24 +138,29 @@ inline void to_h16_block(const double* v, uint16_t* rec) {
     rec[9] = (uint16_t)(int16_t)e;
 }
 
-// host: one block -> the ten-byte record (nine values, then s); false when s leaves int8's range
-inline bool to_q8_block(const double* v, int8_t* rec) {
+// host: one block -> the twelve-byte int8 record (nine values, then the scale's bits 8..31)
+inline bool to_q8_block(const double* v, uint8_t* rec) {
     double m = 0.0;
     for (int k = 0; k < 9; ++k) m = std::max(m, std::fabs(v[k]));
-    int e = 0;
-    if (m > 0.0) std::frexp(m, &e);
-    const int sh = e - 7;
-    if (sh < -128 || sh > 127) return false;
-    for (int k = 0; k < 9; ++k) rec[k] = (int8_t)std::max(-127.0, std::min(127.0, std::nearbyint(std::ldexp(v[k], -sh))));
-    rec[9] = (int8_t)sh;
+    const float s32 = (float)(m / 127.0);
+    if (m > 0.0 && !(s32 > 0.0f && std::isfinite(s32) && std::isnormal(s32))) return false;
+    const uint32_t bits = __builtin_bit_cast(uint32_t, s32) & 0xFFFFFF00u;
+    const double sc = (double)__builtin_bit_cast(float, bits);
+    for (int k = 0; k < 9; ++k)
+        rec[k] = (uint8_t)(int8_t)(sc > 0.0 ? std::max(-127.0, std::min(127.0, std::nearbyint(v[k] / sc))) : 0.0);
+    rec[9] = (uint8_t)(bits >> 8);
+    rec[10] = (uint8_t)(bits >> 16);
+    rec[11] = (uint8_t)(bits >> 24);
     return true;
 }
 
-// stored bytes of one 3x3 block's values in storage type vt (ValType)
-inline double vbytes(int vt) { return vt == kValQ8 ? 10.0 : vt == kValH16 ? 20.0 : vt == kVal32 ? 36.0 : 72.0; }
+// position of record byte k (0..11) of `lane` in a 768-B int8 slot
+inline int64_t q8_pos(int k, int64_t lane) { return 256 * (k / 4) + 4 * lane + k % 4; }
 
-// position of record byte k (0..9) of `lane` in a 640-B int8 slot
-inline int64_t q8_pos(int k, int64_t lane) { return k < 4 ? 4 * lane + k : k < 8 ? 256 + 4 * lane + (k - 4) : 512 + 2 * lane + (k - 8); }
+// stored bytes of one 3x3 block's values in storage type vt (ValType)
+inline double vbytes(int vt) {
+    return vt == kValQ8 ? 12.0 : vt == kValH16 ? 20.0 : vt == kVal32 ? 36.0 : 72.0;
+}
 
 template <typename T>
 __host__ __device__ inline int64_t slot_elem(int ij, int64_t lane) {
@@ -176,14 +181,11 @@ __device__ __forceinline__ void block_fma_any(const T* v, const double* xj, doub
     // column-indexed and stencil-coded slots)
     auto dot3 = [x0, x1, x2](double v0, double v1, double v2) { return __builtin_fma(v2, x2, __builtin_fma(v1, x1, v0 * x0)); };
     if constexpr (sizeof(T) == 1) {
-        // v = slot base + lane in bytes; the lane's dwords at 4 lane and 256 + 4 lane, (q8, s) at 512 + 2 lane
-        const int8_t* sb = reinterpret_cast<const int8_t*>(v) - lane;
-        const uint32_t* p = reinterpret_cast<const uint32_t*>(sb) + lane;
-        const uint16_t* h = reinterpret_cast<const uint16_t*>(sb + 512) + lane;
-        const uint32_t a = ldv(p), b = ldv(p + 64);
-        const uint32_t c = ldv(h);
+        // v = slot base + lane in bytes; the lane's dwords at 4 lane, 256 + 4 lane, 512 + 4 lane
+        const uint32_t* p = reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(v) - lane) + lane;
+        const uint32_t a = ldv(p), b = ldv(p + 64), c = ldv(p + 128);
         auto q = [](uint32_t w, int k) { return (double)((int32_t)(w << (24 - 8 * k)) >> 24); };  // signed byte k
-        const double sc = __builtin_amdgcn_ldexp(1.0, (int32_t)(c << 16) >> 24);
+        const double sc = (double)__builtin_bit_cast(float, c & 0xFFFFFF00u);
         s0 = __builtin_fma(sc, dot3(q(a, 0), q(a, 1), q(a, 2)), s0);
         s1 = __builtin_fma(sc, dot3(q(a, 3), q(b, 0), q(b, 1)), s1);
         s2 = __builtin_fma(sc, dot3(q(b, 2), q(b, 3), q(c, 0)), s2);
@@ -1742,9 +1744,9 @@ void build_gs(GsFine& G, const LevelDev& L, int nsub, const std::vector<int64_t>
     const bool c16 = L.col16.p != nullptr;
     std::vector<int32_t> gcol(c16 ? 0 : std::max<int64_t>(nslot * kChunk, 1), 0);
     std::vector<int16_t> gcol16(c16 ? std::max<int64_t>(nslot * kChunk, 1) : 0, 0);
-    const int nv = vt == kValH16 || vt == kValQ8 ? 10 : 9;
+    const int nv = vt == kValQ8 ? 12 : vt == kValH16 ? 10 : 9;
     std::vector<uint16_t> v16(vt == kValH16 ? std::max<int64_t>(nslot * nv * kChunk, 1) : 0, 0);
-    std::vector<int8_t> v8(vt == kValQ8 ? std::max<int64_t>(nslot * nv * kChunk, 1) : 0, 0);
+    std::vector<uint8_t> v8(vt == kValQ8 ? std::max<int64_t>(nslot * nv * kChunk, 1) : 0, 0);
     bool q8_ok = true;
     std::vector<float> v32(vt == kVal32 ? std::max<int64_t>(nslot * nv * kChunk, 1) : 0, 0.0f);
     std::vector<double> v64(vt == kVal64 ? std::max<int64_t>(nslot * nv * kChunk, 1) : 0, 0.0);
@@ -1780,9 +1782,9 @@ void build_gs(GsFine& G, const LevelDev& L, int nsub, const std::vector<int64_t>
                     to_h16_block(blk, rec);
                     for (int e = 0; e < 10; ++e) v16[t * 10 * kChunk + 128 * (e / 2) + 2 * lane + e % 2] = rec[e];
                 } else if (vt == kValQ8) {
-                    int8_t rec[10];
+                    uint8_t rec[12];
                     if (!to_q8_block(blk, rec)) q8_ok = false;
-                    for (int e = 0; e < 10; ++e) v8[t * 10 * kChunk + q8_pos(e, lane)] = rec[e];
+                    for (int e = 0; e < 12; ++e) v8[t * 12 * kChunk + q8_pos(e, lane)] = rec[e];
                 } else if (vt == kVal32) {
                     for (int ij = 0; ij < 9; ++ij) v32[t * 9 * kChunk + slot_elem<float>(ij, lane)] = (float)blk[ij];
                 } else {
@@ -1796,7 +1798,7 @@ void build_gs(GsFine& G, const LevelDev& L, int nsub, const std::vector<int64_t>
     // gathers (forward colour k: rows of earlier colours; residual: later ones; backward: all
     // other colours) once
     {
-        if (!q8_ok) throw ApiError(DDPCA_EINVAL, "block-scaled int8 copy: a block's exponent is out of range");
+        if (!q8_ok) throw ApiError(DDPCA_EINVAL, "block-scaled int8 copy: a block's scale is out of fp32's normal range");
         const double vb = vbytes(vt) + (c16 ? 2.0 : 4.0);
         const double rowf = 24.0 + (vt == kVal64 ? 72.0 : 36.0) + 24.0 + 4.0;
         std::vector<double> nl_k(K, 0.0), nu_k(K, 0.0), rows_k(K, 0.0), gx_f(K, 0.0), gx_b(K, 0.0);
@@ -2066,16 +2068,16 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
         static const int q8_levels = std::getenv("DDPCA_Q8_LEVELS") ? std::atoi(std::getenv("DDPCA_Q8_LEVELS")) : 64;
         const bool lowp = !L.tbl && vc32 && l >= 1 && l >= nlev - h16_levels && opt.precond_fp32 >= 2;
         if (lowp && opt.precond_fp32 == 3 && l >= nlev - q8_levels) {
-            std::vector<int8_t> v8((size_t)vc_nslot * 10 * kChunk, 0);
+            std::vector<uint8_t> v8((size_t)vc_nslot * 12 * kChunk, 0);
             std::atomic<bool> ok{true};
             for_vc_slots([&](int64_t q, int64_t dst, int64_t lane) {
                 double blk[9];
-                int8_t rec[10];
+                uint8_t rec[12];
                 for (int ij = 0; ij < 9; ++ij) blk[ij] = val[(q * 9 + ij) * kChunk + lane];
                 if (!to_q8_block(blk, rec)) ok = false;
-                for (int k = 0; k < 10; ++k) v8[dst * 10 * kChunk + q8_pos(k, lane)] = rec[k];
+                for (int k = 0; k < 12; ++k) v8[dst * 12 * kChunk + q8_pos(k, lane)] = rec[k];
             });
-            if (!ok) throw ApiError(DDPCA_EINVAL, "block-scaled int8 copy: a block's exponent is out of range");
+            if (!ok) throw ApiError(DDPCA_EINVAL, "block-scaled int8 copy: a block's scale is out of fp32's normal range");
             L.val8.upload(v8);
         } else if (lowp) {
             // block-exponent fp16 copy of the fine level for the smoother and the V-cycle
@@ -2567,11 +2569,11 @@ void launch_sell(int vt, const SellArgs& a, hipStream_t s) {
         if (!a.tab && a.nch <= split_max) {
             const dim3 gs((unsigned)a.nch);
             if (a.col16) {
-                if (vt == kValQ8) hipLaunchKernelGGL((k_sell_split<MODE, BJ, int8_t, I16>), gs, dim3(kBlock), 0, s, a);
+                if (vt == kValQ8) hipLaunchKernelGGL((k_sell_split<MODE, BJ, uint8_t, I16>), gs, dim3(kBlock), 0, s, a);
                 else if (vt == kValH16) hipLaunchKernelGGL((k_sell_split<MODE, BJ, uint16_t, I16>), gs, dim3(kBlock), 0, s, a);
                 else if (vt == kVal32) hipLaunchKernelGGL((k_sell_split<MODE, BJ, float, I16>), gs, dim3(kBlock), 0, s, a);
                 else hipLaunchKernelGGL((k_sell_split<MODE, BJ, double, I16>), gs, dim3(kBlock), 0, s, a);
-            } else if (vt == kValQ8) hipLaunchKernelGGL((k_sell_split<MODE, BJ, int8_t, int32_t>), gs, dim3(kBlock), 0, s, a);
+            } else if (vt == kValQ8) hipLaunchKernelGGL((k_sell_split<MODE, BJ, uint8_t, int32_t>), gs, dim3(kBlock), 0, s, a);
             else if (vt == kValH16) hipLaunchKernelGGL((k_sell_split<MODE, BJ, uint16_t, int32_t>), gs, dim3(kBlock), 0, s, a);
             else if (vt == kVal32) hipLaunchKernelGGL((k_sell_split<MODE, BJ, float, int32_t>), gs, dim3(kBlock), 0, s, a);
             else hipLaunchKernelGGL((k_sell_split<MODE, BJ, double, int32_t>), gs, dim3(kBlock), 0, s, a);
@@ -2580,11 +2582,11 @@ void launch_sell(int vt, const SellArgs& a, hipStream_t s) {
     }
     if (a.tab) hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, double, V, true>), dim3(grid), dim3(kBlock), 0, s, a, a.tab);
     else if (a.col16) {
-        if (vt == kValQ8) hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, int8_t, V, false, I16>), dim3(grid), dim3(kBlock), 0, s, a, a.tab);
+        if (vt == kValQ8) hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, uint8_t, V, false, I16>), dim3(grid), dim3(kBlock), 0, s, a, a.tab);
         else if (vt == kValH16) hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, uint16_t, V, false, I16>), dim3(grid), dim3(kBlock), 0, s, a, a.tab);
         else if (vt == kVal32) hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, float, V, false, I16>), dim3(grid), dim3(kBlock), 0, s, a, a.tab);
         else hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, double, V, false, I16>), dim3(grid), dim3(kBlock), 0, s, a, a.tab);
-    } else if (vt == kValQ8) hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, int8_t>), dim3(grid), dim3(kBlock), 0, s, a, a.tab);
+    } else if (vt == kValQ8) hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, uint8_t>), dim3(grid), dim3(kBlock), 0, s, a, a.tab);
     else if (vt == kValH16) hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, uint16_t>), dim3(grid), dim3(kBlock), 0, s, a, a.tab);
     else if (vt == kVal32) hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, float>), dim3(grid), dim3(kBlock), 0, s, a, a.tab);
     else hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, double>), dim3(grid), dim3(kBlock), 0, s, a, a.tab);
@@ -2594,10 +2596,10 @@ template <int MODE, bool BJ, bool DOT>
 void launch_loop(int loop, int vt, const SellArgs& a, int grid, hipStream_t s) {
     if (vt == kValQ8) {
         switch (loop) {
-            case 0: hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, int8_t, 0>), dim3(grid), dim3(kBlock), 0, s, a, a.tab); break;
-            case 1: hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, int8_t, 1>), dim3(grid), dim3(kBlock), 0, s, a, a.tab); break;
-            case 2: hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, int8_t, 2>), dim3(grid), dim3(kBlock), 0, s, a, a.tab); break;
-            default: hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, int8_t, 3>), dim3(grid), dim3(kBlock), 0, s, a, a.tab); break;
+            case 0: hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, uint8_t, 0>), dim3(grid), dim3(kBlock), 0, s, a, a.tab); break;
+            case 1: hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, uint8_t, 1>), dim3(grid), dim3(kBlock), 0, s, a, a.tab); break;
+            case 2: hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, uint8_t, 2>), dim3(grid), dim3(kBlock), 0, s, a, a.tab); break;
+            default: hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, uint8_t, 3>), dim3(grid), dim3(kBlock), 0, s, a, a.tab); break;
         }
         return;
     }
@@ -2700,7 +2702,7 @@ double MgpisDevice::bench_spmv(int variant, int reps) {
     const LevelDev& L = lev.back();
     const int loop = variant & 3, mode = (variant >> 2) & 3;
     const bool f32 = (variant & 16) != 0;
-    const int vt = !f32 ? kVal64 : L.val8.p ? kValQ8 : L.val16.p ? kValH16 : kVal32;  // the V-cycle's copy
+    const int vt = !f32 ? kVal64 : vc_type((int)lev.size() - 1);  // the V-cycle's copy
     const int tloop = (variant & 32) ? 4 + (loop & 1) : loop;
     if (variant >= 64 || ((variant & 32) && (!L.tbl || mode != 0 || f32))) throw ApiError(DDPCA_EINVAL, "unknown SpMV variant");
     if (mode == 3 && (lev.size() < 2 || opt.smoother < 1)) throw ApiError(DDPCA_EINVAL, "Chebyshev mode needs block smoothing");
@@ -2708,7 +2710,7 @@ double MgpisDevice::bench_spmv(int variant, int reps) {
     DDPCA_HIP(hipMemsetAsync(sc.p, 0, nsub * sizeof(PcgScal), stream));  // done = 0, beta = 0
     SellArgs a = level_args(L);
     if (f32) {
-        a.val = vt == kValQ8 ? (const void*)L.val8.p : vt == kValH16 ? (const void*)L.val16.p : (const void*)L.val32.p;
+        a.val = vc_level_args(*this, (int)lev.size() - 1).val;
         a.tab = nullptr;
     }
     a.x = xs.p;
@@ -2815,8 +2817,8 @@ void launch_gs(const MgpisDevice& D, int k, double* x, const double* b, double* 
     if (G.val8.p) {
         a.val = G.val8.p;
         a.minv = F.minv32.p;
-        if constexpr (PH >= 3) launch_gs_aux_t<PH, int8_t>(a, c16, D.stream);
-        else launch_gs_t<PH, DOT, int8_t>(a, c16, D.stream);
+        if constexpr (PH >= 3) launch_gs_aux_t<PH, uint8_t>(a, c16, D.stream);
+        else launch_gs_t<PH, DOT, uint8_t>(a, c16, D.stream);
     } else if (G.val16.p) {
         a.val = G.val16.p;
         a.minv = F.minv32.p;

@@ -84,7 +84,7 @@ struct LevelDev {
                            // V-cycle runs on fp64 operators
     DevBuf<float> val32;   // V-cycle operator rounded once to fp32 (opt.precond_fp32), levels >= 1
     DevBuf<uint16_t> val16;  // fine level's V-cycle copy in block-exponent fp16 (opt.precond_fp32 = 2)
-    DevBuf<int8_t> val8;     // ... in block-scaled int8 (opt.precond_fp32 = 3)
+    DevBuf<uint8_t> val8;    // ... in block-scaled int8 (opt.precond_fp32 = 3)
     // table mode: rows whose block values (in device slot order, masks applied) are bit-identical
     // share one table row; the kernel streams only column indices and a row type, the values
     // come from the cache-resident table (structured meshes: ~30x fewer distinct rows than rows)
@@ -155,7 +155,7 @@ struct GsFine {
     DevBuf<int32_t> col;                 // per slot lane (when the level has no 16-bit offsets)
     DevBuf<int16_t> col16;
     DevBuf<uint16_t> val16;
-    DevBuf<int8_t> val8;
+    DevBuf<uint8_t> val8;
     DevBuf<float> val32;
     DevBuf<double> val64;
     DevBuf<float> minvc;                 // the rows' fp32 3x3 inverses in chunk order, [chunk][ij][lane]

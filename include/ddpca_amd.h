@@ -58,8 +58,8 @@ typedef struct {
                           V-cycle residual) stored as block-exponent fp16 (2^e x nine fp16 per 3x3
                           block) -- 24 instead of 40 B per block on the two fine smoother passes
                           of every PCG iteration.
-                          3: as 2 with block-scaled int8 instead of fp16 (2^s x nine int8 per
-                          block, 7-8 significant bits of the block maximum) -- 12 B per block. */
+                          3: as 2 with block-scaled int8 instead of fp16 (nine int8 and a scale
+                          = the block maximum / 127 per 3x3 block) -- 14 B per block. */
     int table_mode;    /* levels >= 1: 0 stream every block value; 1 (default) when the rows'
                           block values deduplicate well (structured meshes), keep one copy per
                           distinct row in a cache-resident table and stream only column indices

@@ -9,7 +9,7 @@ all worms never sees the loaded wheels here: its right-hand sides stay zero and 
 at once, so the wheel ranks (odd ranks at N = 8) are the ones that time the solves -- in the real
 run a worm's PCG takes the same iteration count as a wheel's (cpu_baseline: 15 and 15).
 
-    python profiles/one_rank_probe.py OUT.json [--layouts 8:0,8:1,4:0,2:0] [--steps 10] [--warmup 2]
+    python profiles/one_rank_probe.py OUT.json [--layouts 8:0,8:1,4:0,2:0] [--steps 10] [--warmup 2] [--precond-fp32 P]
 
 (world:rank pairs; bench.py's N-rank run is as slow as its slowest rank plus its RCCL traffic.)
 """
@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--layouts", default="8:0,8:1")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--precond-fp32", type=int, default=None, help="override the option set's precond_fp32")
     a = ap.parse_args()
     import torch
     t0 = time.perf_counter()
@@ -44,6 +45,8 @@ def main():
         world, r = (int(x) for x in lay.split(":"))
         owner = part.block_owner(nsub, world)
         H = D.headline_options(max(list(owner).count(q) for q in range(world)))
+        if a.precond_fp32 is not None:
+            H["precond_fp32"] = a.precond_fp32
         mc = D.MCONTACT(P, device=0, rank=r, nranks=world, owner=owner, **H)
         mc.comm_loopback()
         mc.CONTACT_ANALYSIS(a.warmup, check=False)
