@@ -52,11 +52,13 @@ class MgpisOptions(C.Structure):
 # this exact set against the oracle): multicolour block Gauss-Seidel on the fine level (one
 # forward sweep before, one backward after the coarse correction), 3x3 block-Jacobi with two
 # sweeps (damping 1.7 / lambda_max) on the levels below, V-cycle levels stored fp32 with the three
-# finest as block-exponent fp16, streamed operator rows, automatic exact-solve level, 4 PCG
-# iterations per hipGraph replay, x0 = 0.  (18.0 instead of block-Jacobi V(1,1)'s 23.6 PCG
-# iterations per solve, +8-10 % ADMM it/s at 8 subdomains per GPU, +5 % at 4, equal at 2:
-# profiles/r03j; round 4: +10 % at 4, +4 % at 2, profiles/r04l/ab_small_batch.txt.)
-HEADLINE_OPTIONS = dict(smoother=3, nu=2, omega=-1.7, iters_per_graph=4, warm_start=0, precond_fp32=2,
+# finest as block-scaled int8 (nine int8 and a scale per 3x3 block), streamed operator rows,
+# automatic exact-solve level, 4 PCG iterations per hipGraph replay, x0 = 0.  (18.0 instead of
+# block-Jacobi V(1,1)'s 23.6 PCG iterations per solve, +8-10 % ADMM it/s at 8 subdomains per GPU,
+# +5 % at 4, equal at 2: profiles/r03j; round 4: +10 % at 4, +4 % at 2,
+# profiles/r04l/ab_small_batch.txt.  The int8 copies instead of block-exponent fp16: 18.6 instead
+# of 18.0 PCG iterations, +6 % ADMM it/s, the one-subdomain rank -7.5 %, profiles/r05r.)
+HEADLINE_OPTIONS = dict(smoother=3, nu=2, omega=-1.7, iters_per_graph=4, warm_start=0, precond_fp32=3,
                         table_mode=0, coarse_level=-1)
 # ... for a rank that owns one subdomain (the 8-GPU run of the same chain): a colour launch then
 # holds ~400 chunks, the 17 fine-level launches per V-cycle are latency-bound, so the block-Jacobi

@@ -112,8 +112,8 @@ int main(int argc, char** argv) {
     std::vector<int32_t> owner(c.multGrid.size(), 0);
     mcontact_t h = nullptr;
     // DDPCA_REF_OPTIONS=multicolour: the headline's V-cycle (colour Gauss-Seidel on the fine level --
-    // band mode where the fine level refines a band -- two block-Jacobi sweeps below, block-exponent
-    // fp16 copies) instead of the default block Jacobi
+    // band mode where the fine level refines a band -- two block-Jacobi sweeps below, block-scaled
+    // int8 copies) instead of the default block Jacobi
     mgpis_options_t opt;
     mgpis_default_options(&opt);
     const char* oe = std::getenv("DDPCA_REF_OPTIONS");
@@ -121,7 +121,7 @@ int main(int argc, char** argv) {
     if (mcol) {
         opt.smoother = 3;
         opt.nu = 2;
-        opt.precond_fp32 = 2;
+        opt.precond_fp32 = 3;
     }
     ddpca_bind::check(mcontact_gpu_create(p, 0, 0, 1, owner.data(), &opt, &h));
     int64_t gsr[3] = {0, 0, 0};

@@ -1,8 +1,8 @@
 """Parity at the bench's full subdomain size (BASELINE.json config 5 shape: one wheel subdomain
 of the synthetic DEHW chain, 1,216,800 free dof, 6 MG levels; measured: 24 device PCG
 iterations vs 16 SGS, solutions 5e-14 apart, true residual 1.9e-13) -- the size the headline number
-is measured on, with the bench's preconditioner storage (precond_fp32 = 2: fp32 levels,
-block-exponent fp16 on the three finest, 16-bit column offsets).
+is measured on, with the bench's preconditioner storage (HEADLINE_OPTIONS' precond_fp32 = 3: fp32
+levels, block-scaled int8 on the three finest, 16-bit column offsets).
 
 * MGPIS CG_SOLV(1) on the device vs the SGS-faithful oracle's CG_SOLV(1) (oracle.cpp, pinned to
   the reference by test_oracle.py) on the same operators and right-hand side: solutions to 1e-8
@@ -30,7 +30,7 @@ def test_fullsize_cg_matches_oracle(ddpca, oracle, wheel):
     L = G.maxiLeve
     b = G.consForc
     assert len(b) > 1_000_000 and L == 5
-    M = ddpca.MGPIS.from_problem(P, 1, precond_fp32=2, table_mode=0)
+    M = ddpca.MGPIS.from_problem(P, 1, precond_fp32=ddpca.HEADLINE_OPTIONS["precond_fp32"], table_mode=0)
     x, it, rr = M.CG_SOLV(1, b)
     K = G.consStif(L)
     true_rr = np.linalg.norm(b - K @ x) / np.linalg.norm(b)
@@ -48,7 +48,7 @@ def test_fullsize_spmv_and_bicgstab(ddpca, wheel):
     L = G.maxiLeve
     K = G.consStif(L)
     b = G.consForc
-    M = ddpca.MGPIS.from_problem(P, 1, precond_fp32=2, table_mode=0)
+    M = ddpca.MGPIS.from_problem(P, 1, precond_fp32=ddpca.HEADLINE_OPTIONS["precond_fp32"], table_mode=0)
     v = ((np.arange(len(b)) * 7919 + 13) % 2003) / 2003.0 - 0.5
     y = M.spmv(v)
     scale = (abs(K) @ np.abs(v)).max()

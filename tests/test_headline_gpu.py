@@ -2,7 +2,7 @@
 
 bench.py runs MCONTACT on the synthetic DEHW chain with ``HEADLINE_OPTIONS`` (ddpca-admm_amd/
 __init__.py: multicolour block Gauss-Seidel on the fine level, block-Jacobi with two sweeps
-below, damping 1.7/lambda_max, fp32 V-cycle levels with block-exponent fp16 on the three finest,
+below, damping 1.7/lambda_max, fp32 V-cycle levels with block-scaled int8 on the three finest,
 streamed rows (table_mode 0), automatic exact-solve level, 4 PCG iterations per hipGraph replay) and ``HEADLINE_MUSC`` (interface-eliminated coarse space,
 muscSett = 2, doleMcsc = 1).  These tests run that same set:
 
@@ -10,7 +10,7 @@ muscSett = 2, doleMcsc = 1).  These tests run that same set:
   batch, 4 frictional contacts and 6 glued interfaces, contact faces integrated over 4 x 4
   polygons and glued faces over 2 x 2, i.e. the same integration points per contact node as the
   bench) at 4 MG levels (21k dof per subdomain), so the automatic exact-solve level lands on level 1
-  exactly as at the bench's size, and the fine and next level run the fp16 smoother copies.  A fixed-k trajectory (20 ADMM iterations) against the CPU oracle
+  exactly as at the bench's size, and the fine and next level run the int8 smoother copies.  A fixed-k trajectory (20 ADMM iterations) against the CPU oracle
   (oracle.admm, MCONTACT.h:2493-2845, with exact subdomain solves: the SGS-faithful oracle CG to
   1e-14) on the same host operators: resuMoni rows within 1e-7 relative,
   displacements 1e-7, contact tractions 1e-7.
@@ -248,7 +248,7 @@ def test_schedule_variants_are_bit_identical(ddpca, gpu, monkeypatch, env, opts)
 def test_coarse_correction_kx_from_recursive_residual(ddpca, gpu, monkeypatch):
     """The coarse-space correction takes consStif[L] x as b - r from PCG's recursive residual
     (device_mcontact.hip coarse_correct) instead of the reference's explicit product
-    (MCONTACT.h:2585-2587).  On the headline option set (fp16 / fp32 V-cycle copies) the two
+    (MCONTACT.h:2585-2587).  On the headline option set (int8 / fp32 V-cycle copies) the two
     schedules must agree: resuMoni rows within 1e-8 relative and displacements within 1e-9 after
     10 ADMM iterations (DDPCA_CS_SPMV=1 forces the explicit fp64 SpMV)."""
     H, M = ddpca.HEADLINE_OPTIONS, ddpca.HEADLINE_MUSC
