@@ -32,6 +32,8 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--precond-fp32", type=int, default=None, help="override the option set's precond_fp32")
+    ap.add_argument("--options", choices=["auto", "headline", "small"], default="auto",
+                    help="the option set: bench.py's choice by subdomains per rank, or force one")
     a = ap.parse_args()
     import torch
     t0 = time.perf_counter()
@@ -44,7 +46,8 @@ def main():
     for lay in a.layouts.split(","):
         world, r = (int(x) for x in lay.split(":"))
         owner = part.block_owner(nsub, world)
-        H = D.headline_options(max(list(owner).count(q) for q in range(world)))
+        H = D.headline_options(max(list(owner).count(q) for q in range(world))) if a.options == "auto" else \
+            dict(D.HEADLINE_OPTIONS if a.options == "headline" else D.HEADLINE_OPTIONS_SMALL)
         if a.precond_fp32 is not None:
             H["precond_fp32"] = a.precond_fp32
         mc = D.MCONTACT(P, device=0, rank=r, nranks=world, owner=owner, **H)
