@@ -2067,6 +2067,9 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
         // precond_fp32 = 3: the same levels in block-scaled int8 (the finest DDPCA_Q8_LEVELS of them, default all)
         static const int q8_levels = std::getenv("DDPCA_Q8_LEVELS") ? std::atoi(std::getenv("DDPCA_Q8_LEVELS")) : 64;
         const bool lowp = !L.tbl && vc32 && l >= 1 && l >= nlev - h16_levels && opt.precond_fp32 >= 2;
+        // (a level with a block whose scale leaves fp32's normal range -- entries beyond ~1e38 or
+        // below ~1e-36 -- keeps the block-exponent fp16 copy, whose exponent has no such limit)
+        bool q8_done = false;
         if (lowp && opt.precond_fp32 == 3 && l >= nlev - q8_levels) {
             std::vector<uint8_t> v8((size_t)vc_nslot * 12 * kChunk, 0);
             std::atomic<bool> ok{true};
@@ -2077,9 +2080,14 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
                 if (!to_q8_block(blk, rec)) ok = false;
                 for (int k = 0; k < 12; ++k) v8[dst * 12 * kChunk + q8_pos(k, lane)] = rec[k];
             });
-            if (!ok) throw ApiError(DDPCA_EINVAL, "block-scaled int8 copy: a block's scale is out of fp32's normal range");
-            L.val8.upload(v8);
-        } else if (lowp) {
+            if (ok) {
+                L.val8.upload(v8);
+                q8_done = true;
+            } else if (std::getenv("DDPCA_VERBOSE")) {
+                std::fprintf(stderr, "[ddpca] level %d: int8 scale out of range, block-exponent fp16 copy instead\n", l);
+            }
+        }
+        if (!q8_done && lowp) {
             // block-exponent fp16 copy of the fine level for the smoother and the V-cycle
             // residual (symmetric: a block and its transpose round alike); coarser levels fp32
             std::vector<uint16_t> v16((size_t)vc_nslot * 10 * kChunk, 0);  // zero blocks: e = 0, values 0
@@ -2091,7 +2099,7 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
                 for (int k = 0; k < 10; ++k) v16[dst * 10 * kChunk + 128 * (k / 2) + 2 * lane + k % 2] = rec[k];
             });
             L.val16.upload(v16);
-        } else if (!L.tbl && vc32 && l >= 1) {
+        } else if (!q8_done && !L.tbl && vc32 && l >= 1) {
             std::vector<float> v32((size_t)vc_nslot * 9 * kChunk, 0.0f);
             for_vc_slots([&](int64_t q, int64_t dst, int64_t lane) {
                 for (int ij = 0; ij < 9; ++ij)

@@ -148,12 +148,14 @@ def test_rotated_prol_dropin_one_rotation(ddpca, oracle, gpu, case):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("smoother,nu,fp32", [(1, 1, 0), (0, 1, 0), (2, 2, 0), (1, 1, 1), (1, 1, 2), (2, 2, 2)])
+@pytest.mark.parametrize("smoother,nu,fp32", [(1, 1, 0), (0, 1, 0), (2, 2, 0), (1, 1, 1), (1, 1, 2), (2, 2, 2),
+                                               (1, 1, 3), (3, 2, 3)])
 def test_rotated_prol_dropin_many_rotations(ddpca, oracle, gpu, smoother, nu, fp32):
     """Per-node rotations: the reference's both-rotated rule (w * I) makes the hierarchy a
     different, still valid preconditioner; the solution must still be x' = Q^T x.  Every smoother
     (point / block Jacobi, Chebyshev: the first coarse sweep after a block restriction runs as
-    k_jac0) and every V-cycle operator storage (fp64, fp32, fine level block-exponent fp16)."""
+    k_jac0) and every V-cycle operator storage (fp64, fp32, the finest levels block-exponent fp16 or
+    block-scaled int8; the multicolour fine level on int8)."""
     g = golden("beam_s1")
     nn, fd, K, P, Q, b = _hierarchy(ddpca, "many")
     x_ref = Q.T @ g["x_mg"]
