@@ -58,7 +58,7 @@ def parse():
     # defaults: the fastest configuration of the round-1 sweep (profiles/r01_sweep.txt)
     ap.add_argument("--smoother", type=int, default=None, help="0 point Jacobi, 1 block Jacobi, 2 Chebyshev, "
                     "3 multicolour block Gauss-Seidel on the fine level (block Jacobi below, --nu sweeps); default: "
-                    "headline_options(subdomains per rank) -- 3 with nu 2 from 2 subdomains per rank, else 1 with nu 1")
+                    "headline_options(subdomains per rank) -- 3 with nu 2 above 4 subdomains per rank, else 1 with nu 2")
     ap.add_argument("--nu", type=int, default=None)
     ap.add_argument("--omega-scale", type=float, default=-H["omega"],
                     help="Jacobi damping = scale / lambda_max(M^-1 K) per level (profiles/r01_sweep_omega.txt)")

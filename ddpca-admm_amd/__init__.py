@@ -60,19 +60,20 @@ class MgpisOptions(C.Structure):
 # of 18.0 PCG iterations, +6 % ADMM it/s, the one-subdomain rank -7.5 %, profiles/r05r.)
 HEADLINE_OPTIONS = dict(smoother=3, nu=2, omega=-1.7, iters_per_graph=4, warm_start=0, precond_fp32=3,
                         table_mode=0, coarse_level=-1)
-# ... for a rank that owns one subdomain (the 8-GPU run of the same chain): a colour launch then
-# holds ~400 chunks, the 17 fine-level launches per V-cycle are latency-bound, so the block-Jacobi
-# V(1,1) set, pinned by the same tests.  (Round 3 measured the two equal at 2 subdomains per GPU,
-# profiles/r03j; with the round-4 library the multicolour set is ahead there, 59.4-59.6 vs
-# 57.0-57.2 ADMM it/s, and at 4, 33.2 vs 30.1: profiles/r04l/ab_small_batch.txt.  One subdomain
-# per GPU, the subdomain solve alone: block Jacobi 10.1 ms (23 PCG iterations) vs multicolour
-# 10.9 ms (18), profiles/r04l/one_sub_probe.json.)
-HEADLINE_OPTIONS_SMALL = dict(HEADLINE_OPTIONS, smoother=1, nu=1)
+# ... for a rank that owns at most 4 subdomains (the 2-, 4- and 8-GPU runs of the same chain): a
+# colour launch then holds <= 1,600 chunks and the 17 fine-level launches per V-cycle are
+# latency-bound, so block Jacobi with two sweeps per level, pinned by the same tests.  Round 5, on
+# the int8 copies (profiles/r05y, one rank of each layout under the loopback transport, ms per ADMM
+# iteration): 1 subdomain 9.50 (17 PCG iterations) against 9.93 with one sweep (24), 9.80 with three
+# (14) and 11.33 for the multicolour set (19); 2 subdomains 15.34 vs multicolour 16.47; 4 subdomains
+# 27.95 vs 28.72; at 8 the multicolour set leads, 18.98 vs 18.28 ADMM it/s.  (Before the int8
+# copies the one-sweep set was the small one: profiles/r03j, r04l.)
+HEADLINE_OPTIONS_SMALL = dict(HEADLINE_OPTIONS, smoother=1, nu=2)
 
 
 def headline_options(n_owned: int) -> dict:
     """The measured-best headline option set for a rank owning n_owned subdomains."""
-    return dict(HEADLINE_OPTIONS if n_owned >= 2 else HEADLINE_OPTIONS_SMALL)
+    return dict(HEADLINE_OPTIONS if n_owned > 4 else HEADLINE_OPTIONS_SMALL)
 # and the ADMM setting it runs: interface-eliminated coarse space (muscSett = 2) on level 1 of
 # every subdomain (DEHW.h:2222, 2239)
 HEADLINE_MUSC = dict(muscSett=2, doleMcsc=1)

@@ -83,8 +83,8 @@ def _oracle_problem(P, oracle, lazy=False):
 
 @pytest.mark.parametrize("opts", ["HEADLINE_OPTIONS", "HEADLINE_OPTIONS_SMALL"])
 def test_headline_options_trajectory_matches_oracle(ddpca, oracle, gpu, opts):
-    """Both headline option sets (bench.py takes HEADLINE_OPTIONS_SMALL on ranks owning one
-    subdomain, headline_options)."""
+    """Both headline option sets (bench.py takes HEADLINE_OPTIONS_SMALL -- two-sweep block Jacobi --
+    on ranks owning at most 4 subdomains, headline_options)."""
     H, M = getattr(ddpca, opts), ddpca.HEADLINE_MUSC
     P = ddpca.headline_problem(gl=3)
     P.set_coarse(M["muscSett"], [M["doleMcsc"]] * P.nsub)
