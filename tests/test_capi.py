@@ -55,10 +55,12 @@ def test_device_entry_points_fail_loudly_without_gpu(ddpca):
 
 
 def test_round5_entry_points_refuse_bad_arguments(ddpca):
-    """The tree-input ESTABLISH (ddpca_problem_set_subdomain_tree / _set_contact) and the timing
-    transport (mcontact_gpu_comm_loopback) check their arguments before anything changes (no GPU)."""
+    """The tree-input ESTABLISH (ddpca_problem_set_subdomain_tree / _set_contact), the timing
+    transport (mcontact_gpu_comm_loopback) and the V-cycle-copy SpMV (mgpis_gpu_spmv_copy) check
+    their arguments before anything changes (no GPU)."""
     L = ddpca.lib()
     assert L.mcontact_gpu_comm_loopback(None, None) == -1
+    assert L.mgpis_gpu_spmv_copy(None, 0, 1, None, None) == -1
     assert L.ddpca_problem_set_contact(None, 0, 0, 1) == -1
     assert L.ddpca_problem_set_subdomain_tree(None, 0, None) == -1
     h = ctypes.c_void_p()
