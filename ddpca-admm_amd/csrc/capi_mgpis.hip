@@ -34,7 +34,15 @@ std::unique_ptr<MgpisDevice> single(int device, const std::vector<int64_t>& nn, 
     ops.dof_free = fr.data();
     ops.S = S;
     ops.coords = coords;
-    return std::make_unique<MgpisDevice>(device, std::vector<SubdomainOps>{ops}, resolve(opt));
+    auto d = std::make_unique<MgpisDevice>(device, std::vector<SubdomainOps>{ops}, resolve(opt));
+    // The reference calls CG_SOLV on different MGPIS objects from an omp parallel for
+    // (MCONTACT.h:2511-2531): every graph a solve replays is captured here, on the creating
+    // thread, so a solve only replays (no capture on a solving thread), and the
+    // solve's condensed staging buffer is allocated here too (no hipMalloc / hipFree per solve).
+    d->prepare_graphs(0);
+    if (!d->no_coarse) d->prepare_graphs(1);
+    d->stage.alloc((size_t)std::max<int64_t>(d->nfree[0], 1));
+    return d;
 }
 
 }  // namespace
@@ -170,13 +178,14 @@ int mgpis_gpu_solve(mgpis_t h, const double* b, double* x, int prec, double rtol
         if (prec != 0 && prec != 1) throw ApiError(DDPCA_EINVAL, "prec must be 0 or 1");
         MgpisDevice& D = *h->dev;
         select_device(D.device);
-        DevBuf<double> tmp;
-        tmp.upload(b, D.nfree[0]);
-        D.scatter_free(0, tmp.p, D.bs.p);
+        if (prec == 1 && D.no_coarse) throw ApiError(DDPCA_ESTATE, "one-level handle without a coarse inverse: diagonal preconditioner only");
+        // stream-ordered only: the handle's own staging buffer and stream, graphs captured at create
+        DDPCA_HIP(hipMemcpyAsync(D.stage.p, b, D.nfree[0] * sizeof(double), hipMemcpyHostToDevice, D.stream));
+        D.scatter_free(0, D.stage.p, D.bs.p);
         D.pcg_solve(prec, rtol, {maxit});
         it = D.sc_host[0].iter;
-        D.gather_free(0, D.xs.p, tmp.p);
-        DDPCA_HIP(hipMemcpyAsync(x, tmp.p, D.nfree[0] * sizeof(double), hipMemcpyDeviceToHost, D.stream));
+        D.gather_free(0, D.xs.p, D.stage.p);
+        DDPCA_HIP(hipMemcpyAsync(x, D.stage.p, D.nfree[0] * sizeof(double), hipMemcpyDeviceToHost, D.stream));
         DDPCA_HIP(hipStreamSynchronize(D.stream));
         if (iters) *iters = it;
         if (relres) *relres = D.sc_host[0].bb > 0 ? std::sqrt(D.sc_host[0].rr / D.sc_host[0].bb) : 0.0;
@@ -259,15 +268,15 @@ int mgpis_gpu_spmv_copy(mgpis_t h, int level, int vcycle_copy, const double* x, 
 
 int mgpis_gpu_vcycle(mgpis_t h, const double* r, double* z) {
     return guarded([&] {
+        if (!h || !r || !z) throw ApiError(DDPCA_EINVAL, "null argument");
         MgpisDevice& D = *h->dev;
         select_device(D.device);
-        DevBuf<double> tmp;
-        tmp.upload(r, D.nfree[0]);
-        D.scatter_free(0, tmp.p, D.rs.p);
+        DDPCA_HIP(hipMemcpyAsync(D.stage.p, r, D.nfree[0] * sizeof(double), hipMemcpyHostToDevice, D.stream));
+        D.scatter_free(0, D.stage.p, D.rs.p);
         DDPCA_HIP(hipMemsetAsync(D.sc.p, 0, sizeof(PcgScal), D.stream));  // done = 0
         D.vcycle(D.rs.p, D.zs.p, false);
-        D.gather_free(0, D.zs.p, tmp.p);
-        DDPCA_HIP(hipMemcpyAsync(z, tmp.p, D.nfree[0] * sizeof(double), hipMemcpyDeviceToHost, D.stream));
+        D.gather_free(0, D.zs.p, D.stage.p);
+        DDPCA_HIP(hipMemcpyAsync(z, D.stage.p, D.nfree[0] * sizeof(double), hipMemcpyDeviceToHost, D.stream));
         DDPCA_HIP(hipStreamSynchronize(D.stream));
     });
 }

@@ -5,6 +5,7 @@
 #include <climits>
 #include <cstdlib>
 #include <mutex>
+#include <shared_mutex>
 #include <cstdint>
 #include <string>
 #include <vector>
@@ -25,6 +26,39 @@ constexpr int kWave = 64;      // CDNA wavefront
 constexpr int kChunk = 64;     // SELL chunk = one node row per lane of a wave
 constexpr int kBlock = 256;    // 4 waves per workgroup
 
+// Stream capture vs. synchronous HIP calls on other host threads.  ROCm 7.2 invalidated a
+// hipStreamCaptureModeThreadLocal capture on one thread while another thread of the process made
+// synchronous calls (its first solve's hipMalloc / hipMemcpy / hipFree: "hipStreamEndCapture:
+// operation failed due to a previous error during capture", profiles/r05p/gputest_first.log).  So
+// every capture of the library holds this lock exclusively (CaptureSection), and every device
+// allocation, free and synchronous copy (DevBuf) holds it shared for the length of that one call:
+// no synchronous call of the library overlaps a capture on another thread.  Neither side ever waits
+// on another thread while holding it (no deadlock with the in-process ranks' barriers).  A thread
+// inside its own capture skips the shared side (it makes no such call there).
+struct CaptureLock {
+    static std::shared_mutex& mutex() {
+        static std::shared_mutex m;
+        return m;
+    }
+    static bool& capturing() {
+        static thread_local bool c = false;
+        return c;
+    }
+};
+struct CaptureSection {
+    std::unique_lock<std::shared_mutex> g{CaptureLock::mutex()};
+    CaptureSection() { CaptureLock::capturing() = true; }
+    ~CaptureSection() { CaptureLock::capturing() = false; }
+    CaptureSection(const CaptureSection&) = delete;
+    CaptureSection& operator=(const CaptureSection&) = delete;
+};
+struct SyncCallGuard {
+    std::shared_lock<std::shared_mutex> g;
+    SyncCallGuard() {
+        if (!CaptureLock::capturing()) g = std::shared_lock<std::shared_mutex>(CaptureLock::mutex());
+    }
+};
+
 // Owning device allocation.
 template <typename T>
 struct DevBuf {
@@ -43,16 +77,25 @@ struct DevBuf {
     void alloc(size_t count) {
         release();
         n = count;
-        if (count) DDPCA_HIP(hipMalloc(&p, count * sizeof(T)));
+        if (count) {
+            SyncCallGuard g;
+            DDPCA_HIP(hipMalloc(&p, count * sizeof(T)));
+        }
     }
     void release() {
-        if (p) (void)hipFree(p);
+        if (p) {
+            SyncCallGuard g;
+            (void)hipFree(p);
+        }
         p = nullptr;
         n = 0;
     }
     void upload(const T* h, size_t count) {
         alloc(count);
-        if (count) DDPCA_HIP(hipMemcpy(p, h, count * sizeof(T), hipMemcpyHostToDevice));
+        if (count) {
+            SyncCallGuard g;
+            DDPCA_HIP(hipMemcpy(p, h, count * sizeof(T), hipMemcpyHostToDevice));
+        }
     }
     void upload(const std::vector<T>& v) { upload(v.data(), v.size()); }
     void zero(hipStream_t s = 0) {
@@ -60,7 +103,10 @@ struct DevBuf {
     }
     std::vector<T> download() const {
         std::vector<T> v(n);
-        if (n) DDPCA_HIP(hipMemcpy(v.data(), p, n * sizeof(T), hipMemcpyDeviceToHost));
+        if (n) {
+            SyncCallGuard g;
+            DDPCA_HIP(hipMemcpy(v.data(), p, n * sizeof(T), hipMemcpyDeviceToHost));
+        }
         return v;
     }
 };

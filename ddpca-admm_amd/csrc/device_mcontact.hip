@@ -209,7 +209,11 @@ __global__ __launch_bounds__(256) void k_gamma_ip(const double* B, IpSide s0, Ip
 #pragma unroll
     for (int j = 0; j < 9; ++j) b[j / 3][j % 3] = B[(int64_t)j * nip + q];
     const double pen[3] = {p0, p1, p2};
+    // gamma = (constant + side 0's half) + side 1's half, in that order whichever rank holds which
+    // side (a cross-rank interface adds the received half to its own: the same two sums, and a + b
+    // is b + a): the same bits on every rank layout
     double g[3] = {0.0, 0.0, 0.0};
+    for (int m = 0; m < C; ++m) g[m] = gcst[C * q + m];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
         if (!(s ? own1 : own0)) continue;
@@ -239,7 +243,13 @@ __global__ __launch_bounds__(256) void k_gamma_ip(const double* B, IpSide s0, Ip
                              pen[m] * (b[m][0] * u[0] + b[m][1] * u[1] + b[m][2] * u[2]));
         }
     }
-    for (int m = 0; m < C; ++m) gamma[C * q + m] = gcst[C * q + m] + g[m];
+    for (int m = 0; m < C; ++m) gamma[C * q + m] = g[m];
+}
+
+// y[dst[i]] += x[i]: the side-1 halves of rank-local interfaces onto their side-0 halves
+__global__ void k_add_idx(double* y, const double* x, const int32_t* dst, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) y[dst[i]] += x[i];
 }
 
 // the projected traction in global components, T[3 q + k] = sum_m basis[m][k] gamma[3 q + m]
@@ -697,6 +707,15 @@ __global__ __launch_bounds__(256) void k_csr_wave(const int64_t* ptr, const int3
     if (lane == 0) y[r] = add[r] + s;
 }
 
+// g[r] = the row's per-source slots in ascending source order (build_coarse)
+__global__ void k_slot_sum(const int64_t* sptr, const double* gs, double* g, int64_t n) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    double s = 0.0;
+    for (int64_t k = sptr[r]; k < sptr[r + 1]; ++k) s += gs[k];
+    g[r] = s;
+}
+
 // g[rows[i]] -= yd[src[i]]: the stiffness part of globTran_D_1 u, restricted on the device
 __global__ void k_cs_kpart(const int32_t* rows, const int64_t* src, const double* yd, double* g, int64_t n) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1079,6 +1098,8 @@ public:
             x_target_ = x_out;
         }
         if (cheb_ && rtol != cheb_rtol_) {
+            // a tolerance other than the setup plan's (1e-14, the ADMM loop's): re-plan and
+            // re-capture here -- the capture holds the library's capture lock (device_common.hpp)
             drop_graphs();
             cheb_plan(rtol);
         }
@@ -1251,10 +1272,9 @@ private:
             K = std::max<int64_t>(K, cheb_ks_[s2]);
         }
         cheb_k_ = K;
-        if (K > kChebMax) {
-            cheb_ = false;
-            return;
-        }
+        // past kChebMax steps this tolerance runs the plain CG (capture() skips the Chebyshev
+        // graph); cheb_ stays set, so a later solve at a looser tolerance plans it again
+        if (K > kChebMax) return;
         std::vector<double> coef((size_t)2 * K * nsys, 0.0), ith(nsys);
         for (int s2 = 0; s2 < nsys; ++s2) {
             const double th = 0.5 * (lam_hi_[s2] + lam_lo_[s2]), de = 0.5 * (lam_hi_[s2] - lam_lo_[s2]);
@@ -1302,6 +1322,7 @@ private:
         const char* ep = std::getenv("DDPCA_MCG_PAIR");
         const bool pair = paired_ && !(ep && std::atoi(ep) == 0);
         hipGraph_t g;
+        CaptureSection capture_section;  // device_common.hpp CaptureLock
         DDPCA_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
         hipLaunchKernelGGL(k_mcheb_init, dim3(nb256(nrow)), dim3(256), 0, s, b.p, dinv.p, cith_.p, csys.p, x_target_, r.p,
                            z.p, nrow);
@@ -1327,6 +1348,7 @@ private:
     void capture_one(hipStream_t s, PcgScal* scp, hipGraphExec_t* out, int64_t iters) {
         EllArgs e{slots.p, off.p, col.p, val.p, csys.p, dinv.p, nch};
         hipGraph_t g;
+        CaptureSection capture_section;  // device_common.hpp CaptureLock
         DDPCA_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
         const bool fa = fuse_alpha();
         // DDPCA_MCG_PAIR=0: the unpaired k_mcg_spmv on a paired batch (bit-identical, A/B and tests)
@@ -1379,6 +1401,11 @@ struct CoarseDev {
     double dense_bytes = 0.0;  // n^2 8 B: what the dense inverse would hold per rank
     bool mg_fallback = false;  // (kept for the "coarse_solve" getter: DOUBLE_M is always buildable now)
     DevBuf<double> g, f0, xc, xn, ainv;
+    // the right-hand side's per-source slots (build_coarse): rptr/rcol/rval and f0 are per slot,
+    // gs the slot values (all-reduced), sptr the slots of each coarse row
+    int64_t nslot = 0;
+    DevBuf<double> gs;
+    DevBuf<int64_t> sptr;
     DevBuf<int64_t> rptr;
     DevBuf<int32_t> rcol;
     DevBuf<double> rval;
@@ -1630,6 +1657,11 @@ struct ddpca_mcontact {
     DevBuf<int32_t> norm_bseg;
     DevBuf<double> norm_partial;
     SellOp op_gamma, op_aux, op_lam;     // gamma (my halves), aux RHS, lambda RHS
+    // rank-local interfaces' side-1 halves (SELL rows; the factored ones in k_gamma_ip), added onto
+    // the side-0 halves by k_add_idx: gamma = (constant + half 0) + half 1 on every rank layout
+    SellOp op_gamma1;
+    DevBuf<double> gam1;
+    DevBuf<int32_t> gam1_dst;
     // interfaces whose per-ip operators are applied in factored form (Interface::factored)
     struct FactItf {
         int64_t ts = 0, nip = 0, goff = 0;
@@ -1876,7 +1908,9 @@ void build(ddpca_mcontact& H, Problem& P) {
     }
     // ---- interface operators over W (MCONTACT.h:2632-2636, 2671-2704)
     {
-        Rows rg(H.G), ra(H.R), rl(H.R);
+        Rows rg(H.G), ra(H.R), rl(H.R), rg1;
+        std::vector<int32_t> g1dst;
+        std::map<int64_t, int64_t> g1off;  // rank-local SELL interface -> its first row in rg1
         std::vector<double> gc(H.G, 0.0);
         for (const auto& sd : H.sides) {
             const Interface& itf = mc.searCont[sd.ts];
@@ -1888,9 +1922,16 @@ void build(ddpca_mcontact& H, Problem& P) {
             // gamma half: +-1/2 (inpoLagr lambda + pemaInpo_r u); side 0 adds -1/2 pema g
             const Csr& Lg = itf.inpoLagr[s];
             const Csr& Rg = itf.pemaInpo_r[s];
+            // a rank-local interface's side 1 sums its half in rows of its own (op_gamma1)
+            const bool own_rows1 = !itf.factored && s == 1 && !I.cross;
+            if (own_rows1 && !g1off.count(sd.ts)) {
+                g1off[sd.ts] = (int64_t)rg1.size();
+                for (int64_t i = 0; i < sd.mip; ++i) g1dst.push_back((int32_t)(I.goff + i));
+                rg1.resize(rg1.size() + sd.mip);
+            }
             for (int64_t i = 0; i < sd.mip; ++i) {
                 if (!itf.factored) {  // factored interfaces: k_gamma_ip
-                    auto& row = rg[I.goff + i];
+                    auto& row = own_rows1 ? rg1[g1off[sd.ts] + i] : rg[I.goff + i];
                     for (int64_t k = Lg.ptr[i]; k < Lg.ptr[i + 1]; ++k) row.push_back({lam0 + Lg.col[k], half * Lg.val[k]});
                     for (int64_t k = Rg.ptr[i]; k < Rg.ptr[i + 1]; ++k) row.push_back({Su.wcol(Rg.col[k], H.oH), half * Rg.val[k]});
                 }
@@ -1915,6 +1956,11 @@ void build(ddpca_mcontact& H, Problem& P) {
             }
         }
         H.op_gamma.build(rg);
+        if (!rg1.empty()) {
+            H.op_gamma1.build(rg1);
+            H.gam1.alloc(H.op_gamma1.nrow);
+            H.gam1_dst.upload(g1dst);
+        }
         H.op_aux.build(ra);
         H.op_lam.build(rl);
         H.gcst.upload(gc);
@@ -2078,6 +2124,8 @@ void build(ddpca_mcontact& H, Problem& P) {
         // interface: gamma (stored rows + the constant), factored per-ip kernels, projection,
         // the aux / lambda right-hand sides, the fused update (or the lambda add)
         H.bytes_iface += H.op_gamma.nch ? H.op_gamma.bytes + 8.0 * (double)H.op_gamma.nrow : 0.0;
+        // side-1 halves of rank-local interfaces: their rows, then gamma read + written and the half read
+        H.bytes_iface += H.op_gamma1.nch ? H.op_gamma1.bytes + 28.0 * (double)H.gam1_dst.n : 0.0;
         for (auto& F : H.fitfs) H.bytes_iface += F.bytes_gamma + (H.fused ? F.bytes_inpo : 0.0);
         for (auto& I : H.itfs)
             if (I.mine) H.bytes_iface += (double)(I.mip / I.comp) * (16.0 * I.comp + 4.0) + (I.cross ? 24.0 * I.mip : 0.0);
@@ -2302,24 +2350,92 @@ void build_coarse(ddpca_mcontact& H, Problem& P) {
         for (int64_t r = cs.baseReco[tv]; r < cs.baseReco[tv + 1]; ++r) C.own_rows.push_back(r);
     }
     C.nown = (int64_t)C.own_rows.size();
-    // RHS rows over W: + globTran_1 (owned sides, lambda columns), - interface part of
-    // globTran_D_1 (owned subdomains, u columns)
-    std::vector<std::vector<std::pair<int32_t, double>>> rows(n);
-    auto add_rows = [&](const Csr& T, int64_t c0, double sgn) {
-        for (int64_t r = 0; r < T.nrow; ++r)
-            for (int64_t k = T.ptr[r]; k < T.ptr[r + 1]; ++k) rows[r].push_back({(int32_t)(c0 + T.col[k]), sgn * T.val[k]});
-    };
-    for (const auto& sd : H.sides) {
-        const int64_t lam0 = H.oS + H.R + sd.roff, aux0 = H.oS + sd.roff;
-        if (cs.latin) {  // + globTran lambda - globTran_pena aux + globTran_D u   (MCONTACT.h:2540-2548)
-            add_rows(cs.globTran_L[sd.ts][sd.s], lam0, 1.0);
-            add_rows(cs.globTran_pena_L[sd.ts][sd.s], aux0, -1.0);
-            const auto& Su = H.subs[sd.sub];
-            const Csr& D = cs.globTran_D_L[sd.ts][sd.s];
-            for (int64_t r = 0; r < D.nrow; ++r)
-                for (int64_t k = D.ptr[r]; k < D.ptr[r + 1]; ++k) rows[r].push_back({(int32_t)Su.wcol(D.col[k], H.oH), D.val[k]});
+    // ---- the right-hand side in per-source slots.  Row r of the coarse right-hand side sums
+    // contributions of several subdomains (its own u and lambda, its interface mates' through
+    // globTran_1 / globTran_S; LATIN's contact rows both bodies of the interface), and every source
+    // subdomain lives on exactly one rank.  Summing the row over this rank's W columns and then
+    // all-reducing across ranks would round differently for every rank layout; instead every row
+    // has one slot per structurally possible source (the same layout on every rank: itself and its
+    // interface mates, for LATIN's contact rows both bodies), each slot is summed in a fixed,
+    // layout-independent order by its source's owner (the other ranks contribute exact zeros to
+    // it), the slots are all-reduced, and k_slot_sum adds a row's slots in ascending source order.
+    // The coarse right-hand side -- and so the whole trajectory -- is then the same bits on any
+    // number of ranks (tests/test_mcontact_gpu.py: resuMoni rows of the multi-rank runs).
+    const int64_t nsg = (int64_t)cs.baseReco.size() - 1, nbase = cs.baseReco.back();
+    std::vector<std::vector<int64_t>> srcs(n);
+    {
+        std::vector<std::vector<int64_t>> nbr(nsg);
+        std::vector<int64_t> bodies;
+        for (int64_t tv = 0; tv < nsg; ++tv) nbr[tv].push_back(tv);
+        for (const auto& itf : mc.searCont) {
+            nbr[itf.body[0]].push_back(itf.body[1]);
+            nbr[itf.body[1]].push_back(itf.body[0]);
+            bodies.push_back(itf.body[0]);
+            bodies.push_back(itf.body[1]);
+        }
+        auto uniq = [](std::vector<int64_t>& v) {
+            std::sort(v.begin(), v.end());
+            v.erase(std::unique(v.begin(), v.end()), v.end());
+        };
+        for (auto& v : nbr) uniq(v);
+        uniq(bodies);
+        for (int64_t tv = 0; tv < nsg; ++tv)
+            for (int64_t r = cs.baseReco[tv]; r < cs.baseReco[tv + 1]; ++r) srcs[r] = nbr[tv];
+        // LATIN's coarse contact unknowns: rows of interface ts take its two bodies when the
+        // unknowns are known per interface (coarNode), else every body of an interface
+        int64_t known = 0;
+        for (int64_t ts = 0; ts < (int64_t)cs.coarNode.size(); ++ts)
+            known += mc.searCont[ts].comp() * (int64_t)cs.coarNode[ts].size();
+        if (cs.coarNode.size() == mc.searCont.size() && nbase + known == n) {
+            int64_t r = nbase;
+            for (int64_t ts = 0; ts < (int64_t)cs.coarNode.size(); ++ts) {
+                std::vector<int64_t> b{mc.searCont[ts].body[0], mc.searCont[ts].body[1]};
+                uniq(b);
+                for (int64_t q = 0; q < mc.searCont[ts].comp() * (int64_t)cs.coarNode[ts].size(); ++q) srcs[r++] = b;
+            }
         } else {
-            add_rows(cs.globTran_1[sd.ts][sd.s], lam0, 1.0);
+            for (int64_t r = nbase; r < n; ++r) srcs[r] = bodies;
+        }
+    }
+    std::vector<int64_t> sptr(n + 1, 0);
+    for (int64_t r = 0; r < n; ++r) sptr[r + 1] = sptr[r] + (int64_t)srcs[r].size();
+    C.nslot = sptr[n];
+    auto slot_of = [&](int64_t r, int64_t tv) {
+        const auto& v = srcs[r];
+        const auto it = std::lower_bound(v.begin(), v.end(), tv);
+        if (it == v.end() || *it != tv)
+            throw ApiError(DDPCA_EINVAL, "coarse right-hand side: row " + std::to_string(r) + " has an entry of subdomain " +
+                                             std::to_string(tv) + ", which is not on the row's interface graph");
+        return sptr[r] + (int64_t)(it - v.begin());
+    };
+    // RHS entries over W: + globTran_1 (owned sides, lambda columns), - interface part of
+    // globTran_D_1 (owned subdomains, u columns); LATIN + globTran lambda - globTran_pena aux +
+    // globTran_D u.  Sort key inside a slot: (segment, global side, column in the source's own
+    // numbering) -- none of it depends on where the source's columns sit in this rank's W
+    struct Ent {
+        int64_t seg, side, lcol;
+        int32_t wc;
+        double v;
+        bool operator<(const Ent& o) const {
+            return seg != o.seg ? seg < o.seg : side != o.side ? side < o.side : lcol < o.lcol;
+        }
+    };
+    std::vector<std::vector<Ent>> ents(C.nslot);
+    auto put = [&](int64_t r, int64_t tv, Ent e) { ents[slot_of(r, tv)].push_back(e); };
+    for (const auto& sd : H.sides) {
+        const int64_t lam0 = H.oS + H.R + sd.roff, aux0 = H.oS + sd.roff, sg = 2 * sd.ts + sd.s;
+        const auto& Su = H.subs[sd.sub];
+        auto add_rows = [&](const Csr& T, int64_t seg, int64_t c0, double sgn, bool ucol) {
+            for (int64_t r = 0; r < T.nrow; ++r)
+                for (int64_t k = T.ptr[r]; k < T.ptr[r + 1]; ++k)
+                    put(r, sd.tv, Ent{seg, sg, T.col[k], (int32_t)(ucol ? Su.wcol(T.col[k], H.oH) : c0 + T.col[k]), sgn * T.val[k]});
+        };
+        if (cs.latin) {  // (MCONTACT.h:2540-2548)
+            add_rows(cs.globTran_D_L[sd.ts][sd.s], 1, 0, 1.0, true);
+            add_rows(cs.globTran_pena_L[sd.ts][sd.s], 2, aux0, -1.0, false);
+            add_rows(cs.globTran_L[sd.ts][sd.s], 3, lam0, 1.0, false);
+        } else {
+            add_rows(cs.globTran_1[sd.ts][sd.s], 3, lam0, 1.0, false);
         }
     }
     for (size_t i = 0; i < H.subs.size() && !cs.latin; ++i) {
@@ -2328,34 +2444,42 @@ void build_coarse(ddpca_mcontact& H, Problem& P) {
         const Csr& T = cs.assembled ? cs.globTran_D_full[H.subs[i].tv] : cs.globTran_S[H.subs[i].tv];
         const auto& Su = H.subs[i];
         for (int64_t r = 0; r < T.nrow; ++r)
-            for (int64_t k = T.ptr[r]; k < T.ptr[r + 1]; ++k) rows[r].push_back({(int32_t)Su.wcol(T.col[k], H.oH), -T.val[k]});
+            for (int64_t k = T.ptr[r]; k < T.ptr[r + 1]; ++k)
+                put(r, Su.tv, Ent{0, 0, T.col[k], (int32_t)Su.wcol(T.col[k], H.oH), -T.val[k]});
     }
     {
-        std::vector<int64_t> ptr(n + 1, 0);
+        std::vector<int64_t> ptr(C.nslot + 1, 0);
         std::vector<int32_t> col;
         std::vector<double> val;
-        for (int64_t r = 0; r < n; ++r) {
-            auto& row = rows[r];
-            std::sort(row.begin(), row.end());
-            for (const auto& e : row) {
-                col.push_back(e.first);
-                val.push_back(e.second);
+        for (int64_t q = 0; q < C.nslot; ++q) {
+            auto& e = ents[q];
+            std::stable_sort(e.begin(), e.end());
+            for (const auto& x : e) {
+                col.push_back(x.wc);
+                val.push_back(x.v);
             }
-            ptr[r + 1] = (int64_t)col.size();
-            std::vector<std::pair<int32_t, double>>().swap(row);
+            ptr[q + 1] = (int64_t)col.size();
+            std::vector<Ent>().swap(e);
         }
         C.rptr.upload(ptr);
         C.rcol.upload(col.empty() ? std::vector<int32_t>{0} : col);
         C.rval.upload(val.empty() ? std::vector<double>{0.0} : val);
-        // right-hand side CSR over W: entries, each distinct W entry once, f0 read and g written
+        C.sptr.upload(sptr);
+        // right-hand side CSR over W: entries, each distinct W entry once, f0 read and the slot
+        // written; the slot sum reads the slots and row pointers and writes g
         std::vector<int32_t> uc(col);
         std::sort(uc.begin(), uc.end());
         const double uniq = (double)(std::unique(uc.begin(), uc.end()) - uc.begin());
-        C.bytes_iter = 12.0 * (double)col.size() + 8.0 * uniq + 16.0 * (double)n;
+        C.bytes_iter = 12.0 * (double)col.size() + 8.0 * uniq + 16.0 * (double)C.nslot +
+                       8.0 * (double)C.nslot + 16.0 * (double)n;
     }
-    std::vector<double> f0(n, 0.0);
-    for (int64_t r : C.own_rows) f0[r] = cs.globForc_1[r];
+    // globForc_1 enters the slot of the row's own subdomain (the rank that owns the row)
+    std::vector<double> f0(std::max<int64_t>(C.nslot, 1), 0.0);
+    for (size_t i = 0; i < H.subs.size(); ++i)
+        for (int64_t r = cs.baseReco[H.subs[i].tv]; r < cs.baseReco[H.subs[i].tv + 1]; ++r)
+            f0[slot_of(r, H.subs[i].tv)] = cs.globForc_1[r];
     C.f0.upload(f0);
+    C.gs.alloc(std::max<int64_t>(C.nslot, 1));
     C.g.alloc(std::max<int64_t>(n, 1));
     C.xc.alloc(std::max<int64_t>(C.nown, 1));
     // the reference solves globCoup_1 directly below DIRE_MAXI = 120000 rows and with its DOUBLE_M_1
@@ -2459,7 +2583,7 @@ void build_coarse(ddpca_mcontact& H, Problem& P) {
         for (int64_t dof = 0; dof < 3 * g.leveCount[d]; ++dof) {
             const int32_t fi = g.freeIndex[dof];
             if (fi < 0) continue;
-            grp.first.push_back((int32_t)(cs.baseReco[tv] + fi));
+            grp.first.push_back((int32_t)slot_of(cs.baseReco[tv] + fi, tv));  // the row's own slot
             grp.second.push_back(3 * (D.lev[d].noff[i] + perm[dof / 3]) + dof % 3);
         }
         xnoff[i] = nxn;
@@ -2702,18 +2826,20 @@ void coarse_correct(ddpca_mcontact& H) {
                                3 * D.lev[L].nn);
         for (int l = L; l > C.dmin; --l) D.restrict_level(l, l == L ? D.lev[L].r.p : D.lev[l].b.p, D.lev[l - 1].b.p);
     }
-    hipLaunchKernelGGL(k_csr_wave, dim3(ceil_div(n, 4)), dim3(256), 0, st, C.rptr.p, C.rcol.p, C.rval.p, n, H.W.p,
-                       C.g.p, C.f0.p);
+    hipLaunchKernelGGL(k_csr_wave, dim3(std::max(1, ceil_div(C.nslot, 4))), dim3(256), 0, st, C.rptr.p, C.rcol.p,
+                       C.rval.p, C.nslot, H.W.p, C.gs.p, C.f0.p);
     if (H.mg && !C.assembled) {
         MgpisDevice& D = *H.mg;
         const int L = (int)D.lev.size() - 1;
         for (auto& G : C.kg) {
             const double* yd = G.level == L ? D.lev[L].r.p : D.lev[G.level].b.p;
-            hipLaunchKernelGGL(k_cs_kpart, dim3(nb256(G.rows.n)), dim3(256), 0, st, G.rows.p, G.src.p, yd, C.g.p,
+            hipLaunchKernelGGL(k_cs_kpart, dim3(nb256(G.rows.n)), dim3(256), 0, st, G.rows.p, G.src.p, yd, C.gs.p,
                                (int64_t)G.rows.n);
         }
     }
-    if (H.comm) H.comm->allreduce_sum(C.g.p, n, st);
+    // every slot has one source subdomain, so one rank: the others add exact zeros
+    if (H.comm) H.comm->allreduce_sum(C.gs.p, C.nslot, st);
+    hipLaunchKernelGGL(k_slot_sum, dim3(nb256(n)), dim3(256), 0, st, C.sptr.p, C.gs.p, C.g.p, n);
     if (!C.nown) return;
     if (C.mg) {  // mgpi_1.CG_SOLV(1, globForc, globSolu) (MCONTACT.h:2594), on the coarse solver's stream
         MgpisDevice& M = *C.cmg;
@@ -2837,6 +2963,11 @@ bool iterate_once(ddpca_mcontact& H, bool check) {
     const double t_solve = ms_since(t0);
     // ---- interface balance: this rank's gamma halves, one launch for every owned side
     H.op_gamma.apply(st, H.W.p, H.gamma, H.gcst.p);
+    if (H.op_gamma1.nch) {
+        H.op_gamma1.apply(st, H.W.p, H.gam1.p, nullptr);
+        hipLaunchKernelGGL(k_add_idx, dim3(nb256((int64_t)H.gam1_dst.n)), dim3(256), 0, st, H.gamma, H.gam1.p, H.gam1_dst.p,
+                           (int64_t)H.gam1_dst.n);
+    }
     for (auto& F : H.fitfs) {
         const IpSide s0{F.M[0].p, F.lam[0].p, F.u[0].p}, s1{F.M[1].p, F.lam[1].p, F.u[1].p};
         if (F.nip)
@@ -3096,8 +3227,13 @@ int mcontact_gpu_comm_loopback(mcontact_t h, ddpca_problem_t p) {
         if (!h || !p) throw ApiError(DDPCA_EINVAL, "handle / problem");
         select_device(h->device);
         if (h->comm) throw ApiError(DDPCA_ESTATE, "handle already has a communicator");
-        h->comm = std::make_unique<LoopbackTransport>();
         CoarseDev& C = h->cs;
+        // a rank-local DOUBLE_M operator would be "gathered" through the identity all-reduce: this
+        // rank's rows only, a singular coarse hierarchy
+        if (C.on && !C.inverted && C.mg_gather)
+            throw ApiError(DDPCA_ESTATE, "loopback: the problem must be the handle's, established in full "
+                                         "(a rank-local DOUBLE_M coarse operator cannot be gathered)");
+        h->comm = std::make_unique<LoopbackTransport>();
         if (C.on && !C.inverted && !C.mg) {
             // the other ranks' rows of the dense coarse operator come from the problem itself (the
             // setup all-reduce that would sum them is the identity here)

@@ -168,12 +168,23 @@ __host__ __device__ inline int64_t slot_elem(int ij, int64_t lane) {
     return ij == 8 ? 512 + lane : 128 * (ij / 2) + 2 * lane + ij % 2;
 }
 
+// x_j gathered for a block product: three fp64 values at stride 3 (three 8-B loads), or -- the
+// multicolour sweeps' fp32 iterate copy (GsFine::x4, precond_fp32 = 4) -- one 16-B load of the
+// node's (x0, x1, x2, 0) in fp32, widened to fp64
+struct X3 {
+    double a, b, c;
+};
+__device__ __forceinline__ X3 ldx(const double* x, int64_t j) { return X3{x[3 * j], x[3 * j + 1], x[3 * j + 2]}; }
+__device__ __forceinline__ X3 ldx(const float4* x, int64_t j) {
+    const float4 v = x[j];
+    return X3{(double)v.x, (double)v.y, (double)v.z};
+}
+
 // 3x3 block times x_j, accumulated in fp64; v = slot base + lane.  The matrix is streamed once
 // per launch (NT: non-temporal loads, leaving the caches to the x gathers).
 template <bool NT, typename T>
-__device__ __forceinline__ void block_fma_any(const T* v, const double* xj, double& s0, double& s1, double& s2,
-                                              int lane) {
-    const double x0 = xj[0], x1 = xj[1], x2 = xj[2];
+__device__ __forceinline__ void block_fma_any(const T* v, X3 xj, double& s0, double& s1, double& s2, int lane) {
+    const double x0 = xj.a, x1 = xj.b, x2 = xj.c;
     auto ldv = [](const auto* p) { if constexpr (NT) return __builtin_nontemporal_load(p); else return *p; };
     // row . x as fma(v2, x2, fma(v1, x1, v0 x0)), added to the accumulator: the contraction is
     // spelled out so every kernel instantiating this rounds alike (left to fp-contract, the
@@ -213,12 +224,12 @@ __device__ __forceinline__ void block_fma_any(const T* v, const double* xj, doub
 }
 
 template <typename T>
-__device__ __forceinline__ void block_fma(const T* v, const double* xj, double& s0, double& s1, double& s2) {
+__device__ __forceinline__ void block_fma(const T* v, X3 xj, double& s0, double& s1, double& s2) {
     block_fma_any<true>(v, xj, s0, s1, s2, threadIdx.x & 63);
 }
 
 template <typename T>
-__device__ __forceinline__ void block_fma_plain(const T* v, const double* xj, double& s0, double& s1, double& s2) {
+__device__ __forceinline__ void block_fma_plain(const T* v, X3 xj, double& s0, double& s1, double& s2) {
     block_fma_any<false>(v, xj, s0, s1, s2, threadIdx.x & 63);
 }
 
@@ -237,18 +248,18 @@ __device__ __forceinline__ int64_t col_of(CT c, int64_t row) {
     else return (int64_t)c;
 }
 
-template <int V, typename T, typename CT = int32_t>
-__device__ __forceinline__ void sell_rows(const CT* colp, const T* valp, const double* x, int ns, int64_t row,
+template <int V, typename T, typename CT = int32_t, typename XT = double>
+__device__ __forceinline__ void sell_rows(const CT* colp, const T* valp, const XT* x, int ns, int64_t row,
                                           double& s0, double& s1, double& s2) {
     constexpr int64_t SV = slot_vals<T>() * kChunk;
     if constexpr (V == 0) {
 #pragma unroll 3
         for (int k = 0; k < ns; ++k)
-            block_fma_plain(valp + (int64_t)k * SV, x + 3 * col_of(colp[(int64_t)k * kChunk], row), s0, s1, s2);
+            block_fma_plain(valp + (int64_t)k * SV, ldx(x, col_of(colp[(int64_t)k * kChunk], row)), s0, s1, s2);
     } else if constexpr (V == 1) {
 #pragma unroll 3
         for (int k = 0; k < ns; ++k)
-            block_fma(valp + (int64_t)k * SV, x + 3 * col_of(__builtin_nontemporal_load(colp + (int64_t)k * kChunk), row),
+            block_fma(valp + (int64_t)k * SV, ldx(x, col_of(__builtin_nontemporal_load(colp + (int64_t)k * kChunk), row)),
                       s0, s1, s2);
     } else if constexpr (V == 3) {
         // diagnostic bound only (wrong product): as 1 but x gathered at the row's own node, i.e.
@@ -256,7 +267,7 @@ __device__ __forceinline__ void sell_rows(const CT* colp, const T* valp, const d
 #pragma unroll 3
         for (int k = 0; k < ns; ++k) {
             const int64_t j = col_of(__builtin_nontemporal_load(colp + (int64_t)k * kChunk), row);
-            block_fma(valp + (int64_t)k * SV, x + 3 * (row + (j & 0)), s0, s1, s2);
+            block_fma(valp + (int64_t)k * SV, ldx(x, row + (j & 0)), s0, s1, s2);
         }
     } else {
         int k = 0;
@@ -274,11 +285,11 @@ __device__ __forceinline__ void sell_rows(const CT* colp, const T* valp, const d
                 c2 = __builtin_nontemporal_load(colp + (int64_t)(k + 5) * kChunk);
             }
             const T* v = valp + (int64_t)k * SV;
-            block_fma(v, x + 3 * j0, s0, s1, s2);
-            block_fma(v + SV, x + 3 * j1, s0, s1, s2);
-            block_fma(v + 2 * SV, x + 3 * j2, s0, s1, s2);
+            block_fma(v, ldx(x, j0), s0, s1, s2);
+            block_fma(v + SV, ldx(x, j1), s0, s1, s2);
+            block_fma(v + 2 * SV, ldx(x, j2), s0, s1, s2);
         }
-        for (; k < ns; ++k) block_fma(valp + (int64_t)k * SV, x + 3 * col_of(colp[(int64_t)k * kChunk], row), s0, s1, s2);
+        for (; k < ns; ++k) block_fma(valp + (int64_t)k * SV, ldx(x, col_of(colp[(int64_t)k * kChunk], row)), s0, s1, s2);
     }
 }
 
@@ -468,7 +479,7 @@ __global__ __launch_bounds__(kBlock) void k_sell_split(SellArgs a) {
         else colp = a.col + base * kChunk + rin;
 #pragma unroll 2
         for (int k = g; k < ns; k += 4)
-            block_fma_any<true>(valp + (int64_t)k * SV, a.x + 3 * col_of(colp[(int64_t)k * kChunk], row), s0, s1, s2, rin);
+            block_fma_any<true>(valp + (int64_t)k * SV, ldx(a.x, col_of(colp[(int64_t)k * kChunk], row)), s0, s1, s2, rin);
     }
     s0 += __shfl_xor(s0, 16, 64);
     s1 += __shfl_xor(s1, 16, 64);
@@ -520,11 +531,14 @@ struct GsArgs {
     const PcgScal* sc;
     double* partial;
     const float* minvc;  // chunk-ordered fp32 inverses (GsFine::minvc), or null (fp64 copy): minv by row
+    float4* x4;          // the fp32 iterate copy the sweeps gather (GsFine::x4), or null
 };
 
 // the colour sweep's per-row tail: PH 1 stores r = -s; PH 0 / 2 store x = M (b - s) and return
-// its share of b.x (DOT); ln = the row's position in its colour chunk
-template <int PH, bool DOT, typename T>
+// its share of b.x (DOT); ln = the row's position in its colour chunk.  X4 (GsFine::x4): the new
+// x goes to the fp32 iterate copy the sweeps gather; only the backward sweep (PH 2), whose x is
+// the V-cycle's output, also writes it in fp64
+template <int PH, bool DOT, typename T, bool X4 = false>
 __device__ __forceinline__ double gs_epilogue(const GsArgs& a, int64_t c, int ln, int64_t row, bool real, double s0,
                                               double s1, double s2) {
     const int64_t o = 3 * row;
@@ -549,9 +563,12 @@ __device__ __forceinline__ double gs_epilogue(const GsArgs& a, int64_t c, int ln
             apply_m<true>(static_cast<const SmoothInv<T>*>(a.minv), row, b0 - s0, b1 - s1, b2 - s2, m0, m1, m2);
         }
         if (real) {
-            a.x[o] = m0;
-            a.x[o + 1] = m1;
-            a.x[o + 2] = m2;
+            if (X4) a.x4[row] = make_float4((float)m0, (float)m1, (float)m2, 0.0f);
+            if (!X4 || PH == 2) {
+                a.x[o] = m0;
+                a.x[o + 1] = m1;
+                a.x[o + 2] = m2;
+            }
             if (DOT) dotv = __builtin_fma(b2, m2, __builtin_fma(b1, m1, b0 * m0));
         }
     }
@@ -560,7 +577,7 @@ __device__ __forceinline__ double gs_epilogue(const GsArgs& a, int64_t c, int ln
 
 // One wave per workgroup: a colour's chunks spread over more CUs than four-wave groups (+1 % at 8
 // subdomains per GPU, profiles/r03j)
-template <int PH, bool DOT, typename T, typename CT>
+template <int PH, bool DOT, typename T, typename CT, bool X4 = false>
 __global__ __launch_bounds__(kWave) void k_gs(GsArgs a) {
     const int lane = threadIdx.x;
     const int64_t li = blockIdx.x;
@@ -579,13 +596,15 @@ __global__ __launch_bounds__(kWave) void k_gs(GsArgs a) {
     else colp = a.col;
     if (PH != 1) {
         const int64_t o = a.offl[c];
-        sell_rows<1, T, CT>(colp + o * kChunk + lane, val + o * SV + lane, a.x, a.nsl[c], row, s0, s1, s2);
+        if constexpr (X4) sell_rows<1, T, CT>(colp + o * kChunk + lane, val + o * SV + lane, (const float4*)a.x4, a.nsl[c], row, s0, s1, s2);
+        else sell_rows<1, T, CT>(colp + o * kChunk + lane, val + o * SV + lane, (const double*)a.x, a.nsl[c], row, s0, s1, s2);
     }
     if (PH != 0) {
         const int64_t o = a.offu[c];
-        sell_rows<1, T, CT>(colp + o * kChunk + lane, val + o * SV + lane, a.x, a.nsu[c], row, s0, s1, s2);
+        if constexpr (X4) sell_rows<1, T, CT>(colp + o * kChunk + lane, val + o * SV + lane, (const float4*)a.x4, a.nsu[c], row, s0, s1, s2);
+        else sell_rows<1, T, CT>(colp + o * kChunk + lane, val + o * SV + lane, (const double*)a.x, a.nsu[c], row, s0, s1, s2);
     }
-    const double dotv = gs_epilogue<PH, DOT, T>(a, c, lane, row, real, s0, s1, s2);
+    const double dotv = gs_epilogue<PH, DOT, T, X4>(a, c, lane, row, real, s0, s1, s2);
     if (DOT) chunk_partial(dotv, a.partial, c);
 }
 
@@ -625,7 +644,7 @@ __global__ __launch_bounds__(kWave) void k_gs_aux(GsArgs a) {
     else colp = a.col;
     constexpr int64_t SV = slot_vals<T>() * kChunk;
     const int64_t q = a.offl[c];
-    sell_rows<1, T, CT>(colp + q * kChunk + lane, static_cast<const T*>(a.val) + q * SV + lane, a.x, a.nsl[c], row, s0, s1, s2);
+    sell_rows<1, T, CT>(colp + q * kChunk + lane, static_cast<const T*>(a.val) + q * SV + lane, (const double*)a.x, a.nsl[c], row, s0, s1, s2);
     if (real) {
         a.r[o] = a.b[o] - s0;
         a.r[o + 1] = a.b[o + 1] - s1;
@@ -805,6 +824,35 @@ __global__ __launch_bounds__(kBlock) void k_prolong_lat(const double* ec, const 
     if (m & 1) xf[3 * i] += wt * e0;
     if (m & 2) xf[3 * i + 1] += wt * e1;
     if (m & 4) xf[3 * i + 2] += wt * e2;
+}
+
+// The same into the multicolour sweeps' fp32 iterate copy (GsFine::x4): x4_f = fp32(x4_f + mask_f
+// 2^-k sum e_c), the sum and the add in fp64 -- what the backward sweep then gathers
+__global__ __launch_bounds__(kBlock) void k_prolong_lat_x4(const double* ec, const uint32_t* ppk, const int32_t* pstr,
+                                                           const uint8_t* fmask, float4* x4, int64_t nf,
+                                                           const int32_t* csub, const PcgScal* sc) {
+    NODE_PROLOGUE(nf, csub, sc)
+    const uint32_t w = ppk[i];
+    const int64_t p0 = w & 0x1fffffffu;
+    const uint32_t code = w >> 29;
+    const int64_t s0 = pstr[3 * sub], s1 = pstr[3 * sub + 1], s2 = pstr[3 * sub + 2];
+    double e0 = 0.0, e1 = 0.0, e2 = 0.0;
+#pragma unroll
+    for (uint32_t q = 0; q < 8; ++q) {
+        const bool in = (q & ~code) == 0;
+        const int64_t c = in ? p0 + ((q & 1) ? s0 : 0) + ((q & 2) ? s1 : 0) + ((q & 4) ? s2 : 0) : p0;
+        const double w = in ? 1.0 : 0.0;
+        e0 += w * ec[3 * c];
+        e1 += w * ec[3 * c + 1];
+        e2 += w * ec[3 * c + 2];
+    }
+    const double wt = 1.0 / (double)(1 << __popc(code));
+    const uint8_t m = fmask[i];
+    float4 v = x4[i];
+    if (m & 1) v.x = (float)((double)v.x + wt * e0);
+    if (m & 2) v.y = (float)((double)v.y + wt * e1);
+    if (m & 4) v.z = (float)((double)v.z + wt * e2);
+    x4[i] = v;
 }
 
 // Block transfer entries (rotated nodes): x_f += mask_f (B e_c) per fine node that owns one
@@ -1747,7 +1795,7 @@ void build_gs(GsFine& G, const LevelDev& L, int nsub, const std::vector<int64_t>
     const int nv = vt == kValQ8 ? 12 : vt == kValH16 ? 10 : 9;
     std::vector<uint16_t> v16(vt == kValH16 ? std::max<int64_t>(nslot * nv * kChunk, 1) : 0, 0);
     std::vector<uint8_t> v8(vt == kValQ8 ? std::max<int64_t>(nslot * nv * kChunk, 1) : 0, 0);
-    bool q8_ok = true;
+    std::atomic<bool> q8_ok{true};  // written from the omp loop below
     std::vector<float> v32(vt == kVal32 ? std::max<int64_t>(nslot * nv * kChunk, 1) : 0, 0.0f);
     std::vector<double> v64(vt == kVal64 ? std::max<int64_t>(nslot * nv * kChunk, 1) : 0, 0.0);
 #pragma omp parallel for schedule(dynamic, 64)
@@ -1783,7 +1831,7 @@ void build_gs(GsFine& G, const LevelDev& L, int nsub, const std::vector<int64_t>
                     for (int e = 0; e < 10; ++e) v16[t * 10 * kChunk + 128 * (e / 2) + 2 * lane + e % 2] = rec[e];
                 } else if (vt == kValQ8) {
                     uint8_t rec[12];
-                    if (!to_q8_block(blk, rec)) q8_ok = false;
+                    if (!to_q8_block(blk, rec)) q8_ok.store(false, std::memory_order_relaxed);
                     for (int e = 0; e < 12; ++e) v8[t * 12 * kChunk + q8_pos(e, lane)] = rec[e];
                 } else if (vt == kVal32) {
                     for (int ij = 0; ij < 9; ++ij) v32[t * 9 * kChunk + slot_elem<float>(ij, lane)] = (float)blk[ij];
@@ -1830,6 +1878,10 @@ void build_gs(GsFine& G, const LevelDev& L, int nsub, const std::vector<int64_t>
         }
         G.launch_bytes.push_back(res + 24.0 * gx_r);
         for (int k = K - 1; k >= 0; --k) G.launch_bytes.push_back(vb * (nl_k[k] + nu_k[k]) + rowf * rows_k[k] + 24.0 * gx_b[k]);
+        G.gx_f = gx_f;
+        G.gx_b = gx_b;
+        G.rows_k = rows_k;
+        G.gx_r = gx_r;
     }
     G.ncol = K;
     G.nchunk = nch;
@@ -2070,7 +2122,7 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
         // (a level with a block whose scale leaves fp32's normal range -- entries beyond ~1e38 or
         // below ~1e-36 -- keeps the block-exponent fp16 copy, whose exponent has no such limit)
         bool q8_done = false;
-        if (lowp && opt.precond_fp32 == 3 && l >= nlev - q8_levels) {
+        if (lowp && opt.precond_fp32 >= 3 && l >= nlev - q8_levels) {
             std::vector<uint8_t> v8((size_t)vc_nslot * 12 * kChunk, 0);
             std::atomic<bool> ok{true};
             for_vc_slots([&](int64_t q, int64_t dst, int64_t lane) {
@@ -2445,6 +2497,18 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
     for (auto& L : lev) maxch = std::max<int64_t>(maxch, L.nch);
     partial.alloc(2 * maxch);
     if (gs_fine()) gs.partial.alloc(gs.nchunk);
+    if (gs_fine() && opt.precond_fp32 == 4 && !gs.band && lev.back().lat && lev.back().nrot == 0) {
+        gs.x4.alloc(4 * lev.back().nn);
+        gs.x4.zero(stream);
+        // the per-launch byte model on the 16-B iterate: gathers 16 instead of 24 B per distinct
+        // node, the forward sweep writes 16 B per row, the backward sweep 16 + 24
+        const int K = gs.ncol;
+        for (int k = 0; k < K; ++k) {
+            gs.launch_bytes[k] -= 8.0 * gs.gx_f[k] + 8.0 * gs.rows_k[k];
+            gs.launch_bytes[2 * K - k] += -8.0 * gs.gx_b[k] + 16.0 * gs.rows_k[k];
+        }
+        gs.launch_bytes[K] -= 8.0 * gs.gx_r;
+    }
     sc.alloc(nsub);
     DDPCA_HIP(hipHostMalloc(reinterpret_cast<void**>(&sc_host), nsub * sizeof(PcgScal)));
     std::memset(sc_host, 0, nsub * sizeof(PcgScal));
@@ -2775,6 +2839,11 @@ namespace {
 // one k_gs launch: phase ph over colour k's chunks (k < 0: every chunk)
 template <int PH, bool DOT, typename T>
 void launch_gs_t(const GsArgs& a, bool c16, hipStream_t st) {  // c16: 16-bit column offsets, else int32 columns
+    if (a.x4) {
+        if (c16) hipLaunchKernelGGL((k_gs<PH, DOT, T, int16_t, true>), dim3((unsigned)a.n), dim3(kWave), 0, st, a);
+        else hipLaunchKernelGGL((k_gs<PH, DOT, T, int32_t, true>), dim3((unsigned)a.n), dim3(kWave), 0, st, a);
+        return;
+    }
     if (c16) hipLaunchKernelGGL((k_gs<PH, DOT, T, int16_t>), dim3((unsigned)a.n), dim3(kWave), 0, st, a);
     else hipLaunchKernelGGL((k_gs<PH, DOT, T, int32_t>), dim3((unsigned)a.n), dim3(kWave), 0, st, a);
 }
@@ -2821,6 +2890,7 @@ void launch_gs(const MgpisDevice& D, int k, double* x, const double* b, double* 
     // the rows' fp32 inverses in chunk order (coalesced: read by row at stride 2 nodes they pulled
     // whole lines for half the data, +1.1 %, profiles/r03o); the fp64 copy reads minv by row
     a.minvc = G.minvc.p;
+    a.x4 = reinterpret_cast<float4*>(G.x4.p);
     const bool c16 = G.col16.p != nullptr;
     if (G.val8.p) {
         a.val = G.val8.p;
@@ -2975,7 +3045,10 @@ void MgpisDevice::vcycle(const double* rin, double* zout, bool dot) {
     // ---- ascend
     for (int l = cl + 1; l <= Lf; ++l) {
         const LevelDev& F = lev[l];
-        if (F.lat) hipLaunchKernelGGL(k_prolong_lat, dim3(ceil_div(F.nn, kBlock)), dim3(kBlock), 0, stream, cur[l - 1], F.ppk.p,
+        if (gsf && l == Lf && gs.x4.p)  // (x4 mode: lattice fine transfer, no block entries, GsFine::x4)
+            hipLaunchKernelGGL(k_prolong_lat_x4, dim3(ceil_div(F.nn, kBlock)), dim3(kBlock), 0, stream, cur[l - 1], F.ppk.p,
+                               F.pstr.p, F.mask.p, reinterpret_cast<float4*>(gs.x4.p), F.nn, F.csub.p, scp);
+        else if (F.lat) hipLaunchKernelGGL(k_prolong_lat, dim3(ceil_div(F.nn, kBlock)), dim3(kBlock), 0, stream, cur[l - 1], F.ppk.p,
                                       F.pstr.p, F.mask.p, cur[l], F.nn, F.csub.p, scp);
         else if (F.uw) hipLaunchKernelGGL(k_prolong<true>, dim3(ceil_div(F.nn, kBlock)), dim3(kBlock), 0, stream, cur[l - 1], F.ppar.p, F.pw.p,
                            F.mask.p, cur[l], F.nn, F.csub.p, scp);
@@ -3056,10 +3129,13 @@ void MgpisDevice::vcycle_bytes(int s, double out[2]) const {
     const double nsw = gsf && gs.band ? (double)gs.band_rows_sub[s] : n(Lf);
     const double nring = gsf && gs.band ? (double)gs.ring_rows_sub[s] : 0.0;
     const double nout = gsf && gs.band ? nring + (double)gs.far_rows_sub[s] : 0.0;
+    // x4 mode (GsFine::x4): the iterate the sweeps gather and the forward sweep / prolongation
+    // write is the 16-B fp32 copy; the backward sweep writes it and the fp64 output
+    const double xb = gsf && gs.x4.p ? 16.0 : 24.0;
     if (gsf) {
         put(Lf, 76.0 * nout);  // band mode: x = 0, r = b outside the colours (b read, x, r written, row index)
-        put(Lf, gsmat + nsw * (24.0 + minv(Lf) + 24.0 + 4.0 + 24.0 * (K - 1.0) / 2.0));  // forward
-        put(Lf, nsw * (24.0 + 4.0 + 24.0 * (K - 1.0) / 2.0));                              // residual
+        put(Lf, gsmat + nsw * (24.0 + minv(Lf) + xb + 4.0 + xb * (K - 1.0) / 2.0));  // forward
+        put(Lf, nsw * (24.0 + 4.0 + xb * (K - 1.0) / 2.0));                          // residual
         // band mode: the ring's residual over its band columns (blocks, b read, r written, x gathered)
         put(Lf, gsvb * (double)(gs.band ? gs.ring_nnzb_sub[s] : 0) + nring * (24.0 + 24.0 + 4.0 + 24.0));
     } else {
@@ -3085,13 +3161,13 @@ void MgpisDevice::vcycle_bytes(int s, double out[2]) const {
     for (int l = cl + 1; l <= Lf; ++l) {
         const LevelDev& F = lev[l];
         // x_f += mask P e_c: e_c read once, mask, x_f read + written, the parent encoding
-        double pb = 24.0 * n(l - 1) + n(l) * (1.0 + 48.0);
+        double pb = 24.0 * n(l - 1) + n(l) * (1.0 + (gsf && l == Lf ? 2.0 * xb : 48.0));
         if (F.lat) pb += 4.0 * n(l);
         else pb += (F.uw ? 4.0 : 12.0) * (double)F.tent_sub[s];
         pb += 4.0 * 8.0 * (double)F.tblk_sub[s];
         put(l, pb);
         if (gsf && l == Lf) {
-            put(l, gsmat + nsw * (24.0 + minv(l) + 24.0 + 4.0 + 24.0 * (K - 1.0)));  // backward
+            put(l, gsmat + nsw * (24.0 + minv(l) + 24.0 + (xb < 24.0 ? xb : 0.0) + 4.0 + xb * (K - 1.0)));  // backward
             put(l, 52.0 * nout);  // band mode: b . x of the rows outside the colours (b, x read, row index)
             continue;
         }
@@ -3159,6 +3235,7 @@ hipGraphExec_t MgpisDevice::capture_iterations(int prec, int count, PcgScal* scp
     sc_cur_ = scp;
     hipGraph_t g;
     hipGraphExec_t ge = nullptr;
+    CaptureSection capture_section;  // device_common.hpp CaptureLock
     DDPCA_HIP(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
     for (int k = 0; k < count; ++k) enqueue_iteration(prec, false);
     DDPCA_HIP(hipStreamEndCapture(stream, &g));

@@ -161,6 +161,12 @@ struct GsFine {
     DevBuf<float> minvc;                 // the rows' fp32 3x3 inverses in chunk order, [chunk][ij][lane]
                                          // (coalesced; the natural array at stride 2 nodes wastes half of every line)
     DevBuf<int64_t> cb;                  // per member: first colour chunk (nsub + 1), the dot partials
+    // precond_fp32 = 4: the sweeps' iterate as an fp32 copy, 16 B per node (x0, x1, x2, 0), which every
+    // sweep gathers with one 16-B load per neighbour block instead of three 8-B fp64 loads; the
+    // forward sweep and the prolongation write only it, the backward sweep also the fp64 output z.
+    // The block products, the epilogues and z stay fp64: the preconditioner moves by the fp32
+    // rounding of the neighbours' values (lattice fine transfers without block entries, no band)
+    DevBuf<float> x4;
     DevBuf<double> partial;              // per colour chunk: the backward sweep's dot partials (their own
                                          // buffer: a split batch's other half writes the Krylov partials meanwhile)
     std::vector<int64_t> nnzb_sub;       // per member: stored off-diagonal blocks (byte model)
@@ -169,6 +175,8 @@ struct GsFine {
     // 0..K-1, the residual, backward colours K-1..0 (stored blocks, per-row vectors, every distinct
     // x entry gathered once; profiles/gs_table.py sets the rocprof / PMC figures beside them)
     std::vector<double> launch_bytes;
+    std::vector<double> gx_f, gx_b, rows_k;  // per colour: distinct x gathered (forward, backward), rows
+    double gx_r = 0.0;                       // distinct x the residual gathers
     // band mode (locally refined fine level): the colours cover only the band -- the
     // nodes the fine level adds to the next coarser one and their neighbours; two more chunk groups
     // per member follow the colours: the ring (non-band rows with a band neighbour: their band
@@ -232,6 +240,7 @@ public:
     // PCG work vectors (fine level, 3 nn_L) + per-subdomain scalars
     DevBuf<double> pcg_mem, partial;         // pcg_mem holds the six vectors below
     DevSpan<double> xs, rs, zs, ps, qs, bs;
+    DevBuf<double> stage;  // condensed b / x of the C-ABI solve (allocated at create, capi_mgpis.hip)
     DevBuf<PcgScal> sc;
     PcgScal* sc_host = nullptr;      // pinned, filled by pcg_finish()
     MirrorBuf mirror;                // per-subdomain stop state, host-mapped

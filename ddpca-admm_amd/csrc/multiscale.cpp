@@ -39,9 +39,12 @@ struct Trip {
     double v;
 };
 
-// CSR from triplets, duplicates summed, columns sorted (Eigen setFromTriplets)
+// CSR from triplets, duplicates summed in insertion order, columns sorted (Eigen setFromTriplets).
+// The sort is stable: an entry's sum then depends only on the order its own contributions were
+// appended, not on what else the array holds -- a rank-local build (ESTABLISH(owner, rank)) gives
+// the full build's rows bit for bit, and the multi-rank runs stay the single-rank run's arithmetic
 Csr from_triplets(int64_t nrow, int64_t ncol, std::vector<Trip>& t) {
-    std::sort(t.begin(), t.end(), [](const Trip& a, const Trip& b) { return a.r != b.r ? a.r < b.r : a.c < b.c; });
+    std::stable_sort(t.begin(), t.end(), [](const Trip& a, const Trip& b) { return a.r != b.r ? a.r < b.r : a.c < b.c; });
     Csr m;
     m.nrow = nrow;
     m.ncol = ncol;

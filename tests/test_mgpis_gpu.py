@@ -265,6 +265,93 @@ print(json.dumps(res))
 '''
 
 
+_CONCURRENT_CG = r'''
+import importlib, json, sys, threading
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+D = importlib.import_module("ddpca-admm_amd")
+# the reference's pattern: MGPIS objects filled one after another, then CG_SOLV(1) on each from an
+# omp parallel for (MCONTACT.h:2511-2531); handles alternate between the default V-cycle and the
+# headline's (multicolour Gauss-Seidel fine level, int8 / fp32 copies)
+opts = [{}, dict(D.HEADLINE_OPTIONS), {}, dict(D.HEADLINE_OPTIONS)]
+probs = [D.Problem("beam", 16, 4, 2, 2, 1, 1, 1).ESTABLISH() for _ in range(4)]
+n = len(probs[0].grid(0).consForc)
+rng = np.random.default_rng(20251017)
+rhs = [probs[0].grid(0).consForc] + [rng.standard_normal(n) * 1e3 for _ in range(2)]
+res = {"n": n, "errors": [], "phases": {}}
+def serial_ref(i):
+    M = D.MGPIS.from_problem(probs[i], 0, **opts[i])
+    return [M.CG_SOLV(1, b) for b in rhs]
+ref = [serial_ref(i) for i in range(4)]
+def compare(name, out):
+    ok = []
+    for i in range(4):
+        if out[i] is None:
+            ok.append(False)
+            continue
+        ok.append(all(np.array_equal(x, xr) and it == itr for (x, it, _), (xr, itr, _) in zip(out[i], ref[i])))
+    res["phases"][name] = ok
+# phase 1: handles created serially on this thread, four threads solving at once, three RHS each
+Ms = [D.MGPIS.from_problem(probs[i], 0, **opts[i]) for i in range(4)]
+out, err = [None] * 4, [None] * 4
+bar = threading.Barrier(4)
+def solve(i):
+    try:
+        bar.wait()
+        out[i] = [Ms[i].CG_SOLV(1, b) for b in rhs]
+    except Exception as e:
+        err[i] = repr(e)
+ts = [threading.Thread(target=solve, args=(i,)) for i in range(4)]
+for t in ts: t.start()
+for t in ts: t.join()
+compare("serial_create_concurrent_solve", out)
+res["errors"] += [e for e in err if e]
+# phase 2: threads 0-2 create their handles (graph capture at create) while thread 3 solves on a
+# handle created before -- the r05p hazard (a capture overlapping another thread's synchronous calls)
+out, err = [None] * 4, [None] * 4
+def create_and_solve(i):
+    try:
+        bar.wait()
+        M = Ms[i] if i == 3 else D.MGPIS.from_problem(probs[i], 0, **opts[i])
+        out[i] = [M.CG_SOLV(1, b) for b in rhs]
+    except Exception as e:
+        err[i] = repr(e)
+ts = [threading.Thread(target=create_and_solve, args=(i,)) for i in range(4)]
+for t in ts: t.start()
+for t in ts: t.join()
+compare("concurrent_create_and_solve", out)
+res["errors"] += [e for e in err if e]
+res["iters"] = [[it for _, it, _ in r] for r in ref]
+print(json.dumps(res))
+'''
+
+
+def test_concurrent_cg_solv_bit_identical(ddpca, gpu):
+    """The reference calls MGPIS::CG_SOLV(1) on different MGPIS objects from concurrent OpenMP
+    threads (MCONTACT.h:2511-2531, MGPIS.h:163-225); include/ddpca_amd.h promises the same for
+    handles.  In a fresh process: four host threads each solve three right-hand sides on their own
+    handle at once (two handles with the default V-cycle, two with the headline's), then three
+    threads create handles -- every PCG graph is captured at create, under the library's capture
+    lock -- while the fourth solves.  Every solution and iteration count must equal the serial
+    solve's on the same handle options, bit for bit, and no call may fail (the r05p failure was a
+    lazily captured graph on a solving thread: hipStreamEndCapture ... previous error during
+    capture)."""
+    import json
+    import os
+    import subprocess
+    import sys
+    from pathlib import Path
+    root = str(Path(__file__).resolve().parents[1])
+    p = subprocess.run([sys.executable, "-c", _CONCURRENT_CG, root], capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ))
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert p.returncode == 0 and lines, (p.stdout[-2000:], p.stderr[-3000:])
+    res = json.loads(lines[-1])
+    print(f"concurrent CG_SOLV, n = {res['n']}: {res}")
+    assert not res["errors"], res
+    assert all(all(v) for v in res["phases"].values()), res
+
+
 def test_concurrent_dense_factorisations_bit_identical(ddpca, gpu, tmp_path):
     """Four host threads of one fresh process factorise the same dense SPD matrix at once -- each its
     own MGPIS handle whose exact level is the whole fine level (potrf + potri by rocSOLVER on its own

@@ -27,18 +27,36 @@ def _problem(ddpca, musc, owner=None, rank=0):
     return P.ESTABLISH(owner, rank) if owner is not None else P.ESTABLISH()
 
 
-@pytest.mark.parametrize("musc", [0, 2, 1])
+CASES = [(0, False), (2, False), (1, False), (2, True), (1, True)]
+
+
+@pytest.mark.parametrize("musc,double_m", CASES, ids=[f"musc{m}{'-double_m' if d else ''}" for m, d in CASES])
 @pytest.mark.parametrize("owner", [[0, 1, 0, 1], [0, 0, 1, 1]])
-def test_two_ranks_in_one_process_match_single_rank(ddpca, gpu, owner, musc):
+def test_two_ranks_in_one_process_match_single_rank(ddpca, gpu, owner, musc, double_m, monkeypatch):
     """owner [0,1,0,1] puts every worm/wheel contact across the ranks (gamma halves exchanged),
     [0,0,1,1] the glued chain links; musc 2 / 1: interface-eliminated / LATIN coarse space built
-    rank-locally."""
+    rank-locally.  double_m: the coarse problem forced onto DOUBLE_M_1 / DOUBLE_M's MGPIS
+    (DDPCA_COARSE_MG_MIN = 1; MCONTACT.h:1857-1866, 1229-1237) -- the rank-local build then gathers
+    the whole coarse operator at setup (two all-reduces of (row, col, value) triplets, duplicates
+    summed) and every rank builds the same hierarchy.
+
+    The V-cycle's exact-solve level is pinned (its automatic choice depends on the members per
+    rank), so the ranks do the single-rank run's arithmetic: per-subdomain kernels, the MONITOR
+    norms and the coarse right-hand side in per-source slots (build_coarse), the coarse operator's
+    entries each from one side.  Required: resuMoni rows, displacements and gamma within 1e-12 of the
+    single-rank run (measured: identical bits), far inside SURVEY c4's 1e-7."""
+    if double_m:
+        monkeypatch.setenv("DDPCA_COARSE_MG_MIN", "1")
     maxit = 300
-    ref = ddpca.MCONTACT(_problem(ddpca, musc))
+    opts = dict(coarse_level=1)
+    ref = ddpca.MCONTACT(_problem(ddpca, musc), **opts)
     n_ref = ref.CONTACT_ANALYSIS(maxit)
     rows_ref = ref.monitor()
+    if double_m:
+        cs = ref.get("coarse_solve", 0)
+        assert cs[1] == 1, cs  # the multigrid coarse solve
     probs = [_problem(ddpca, musc, owner, r) for r in range(2)]
-    ranks = [ddpca.MCONTACT(probs[r], rank=r, nranks=2, owner=owner) for r in range(2)]
+    ranks = [ddpca.MCONTACT(probs[r], rank=r, nranks=2, owner=owner, **opts) for r in range(2)]
     ddpca.MCONTACT.comm_local(ranks)
     out, err = [None, None], [None, None]
 
@@ -56,19 +74,22 @@ def test_two_ranks_in_one_process_match_single_rank(ddpca, gpu, owner, musc):
     assert not any(t.is_alive() for t in th), "a rank hung"
     assert err == [None, None], err
     assert out[0] == out[1] == n_ref, (out, n_ref)
+    worst = {"moni": 0.0, "u": 0.0, "gamma": 0.0}
     for r in range(2):
         rows = ranks[r].monitor()
         assert rows.shape == rows_ref.shape
         scale = np.abs(rows_ref).max(axis=0, keepdims=True)
-        bad = np.abs(rows - rows_ref) > 1e-8 * np.abs(rows_ref) + 1e-12 * scale
-        assert not bad.any(), (r, np.argwhere(bad)[:5])
+        rel = np.abs(rows - rows_ref) / (np.abs(rows_ref) + 1e-12 * scale + 1e-300)
+        worst["moni"] = max(worst["moni"], float(rel.max()))
         for tv in range(4):
             if owner[tv] != r:
                 continue
             u, ur = ranks[r].get("resuDisp", tv), ref.get("resuDisp", tv)
-            assert np.linalg.norm(u - ur) <= 1e-8 * np.linalg.norm(ur)
+            worst["u"] = max(worst["u"], float(np.linalg.norm(u - ur) / np.linalg.norm(ur)))
         for ts in range(probs[r].nint):
             body = [int(b) for b in probs[r].array("iface_body", ts)]
             if r in (owner[body[0]], owner[body[1]]):
                 g, gr = ranks[r].get("inpoGamm", ts), ref.get("inpoGamm", ts)
-                assert np.abs(g - gr).max() <= 1e-7 * np.abs(gr).max()
+                worst["gamma"] = max(worst["gamma"], float(np.abs(g - gr).max() / np.abs(gr).max()))
+    print(f"owner {owner} musc {musc} double_m {double_m}: {n_ref} iterations, worst relative differences {worst}")
+    assert worst["moni"] <= 1e-12 and worst["u"] <= 1e-12 and worst["gamma"] <= 1e-12, worst
