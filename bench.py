@@ -57,7 +57,7 @@ def parse():
     ap.add_argument("--ip-glued", type=int, default=W["ip_glued"], help="the same for the glued faces")
     # defaults: the fastest configuration of the round-1 sweep (profiles/r01_sweep.txt)
     ap.add_argument("--smoother", type=int, default=None, help="0 point Jacobi, 1 block Jacobi, 2 Chebyshev, "
-                    "3 multicolour block Gauss-Seidel on the fine level (block Jacobi below, --nu sweeps); default: "
+                    "3 multicolour block Gauss-Seidel on the fine level (block Jacobi below, --nu sweeps), 4 the same as colour SSOR; default: "
                     "headline_options(subdomains per rank) -- 3 with nu 2 above 4 subdomains per rank, else 1 with nu 2")
     ap.add_argument("--nu", type=int, default=None)
     ap.add_argument("--omega-scale", type=float, default=-H["omega"],
@@ -67,7 +67,8 @@ def parse():
                     help="1: each subdomain PCG starts from its previous solution (same 1e-14 stop rule)")
     ap.add_argument("--precond-fp32", type=int, default=H["precond_fp32"],
                     help="1: V-cycle level operators stored in fp32; 2: and the finest levels' V-cycle copies in block-exponent fp16; "
-                         "3: in block-scaled int8 instead (arithmetic, Krylov operator and stop rule fp64)")
+                         "3: in block-scaled int8 instead; 4: as 3, the fine colour sweeps gathering an fp32 copy of "
+                         "the iterate (arithmetic, Krylov operator and stop rule fp64)")
     ap.add_argument("--table-mode", type=int, default=H["table_mode"],
                     help="1: keep one copy of bit-identical operator rows (pays on regular meshes only; the "
                          "synthetic box mesh is far more regular than DEHW's curved one, so the headline keeps 0)")
@@ -80,6 +81,9 @@ def parse():
                     help="general: DEHW's general-mesh features on the same chain (the contact band refined once "
                          "more -> hanging level, rotated support nodes, explicit transfer lists) with the same "
                          "coarse space (MULTISCALE_1 on the general tree)")
+    ap.add_argument("--uneven", action="store_true",
+                    help="group g (1 + g mod 3) times --nx cells long: subdomains of three sizes, packed onto the "
+                         "ranks by LPT (partition.owner_for) as DEHW's uneven subdomains (not the headline)")
     ap.add_argument("--no-general", action="store_true",
                     help="skip the general-mesh line the N = 1 headline run adds (a child process, before the headline)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -121,10 +125,12 @@ def main():
     general = a.mesh == "general"
     feat = dict(D.GENERAL_FEATURES) if general else {}
     P = D.headline_problem(groups=a.groups, nx=a.nx, ny=a.ny, nz=a.nz, gl=a.gl, fric=a.fric,
-                           ip_contact=a.ip_contact, ip_glued=a.ip_glued, **feat)
+                           ip_contact=a.ip_contact, ip_glued=a.ip_glued, uneven=int(a.uneven), **feat)
     nip = sum(len(P.array("ip_w", ts)) for ts in range(P.nint))
     nsub = P.nsub
-    owner = part.block_owner(nsub, world)
+    # contiguous blocks for equal subdomains (worm/wheel pairs stay together), LPT by node count
+    # when the sizes differ (--uneven; DEHW's 52 subdomains)
+    owner = part.owner_for([len(P.array("coords", tv)) // 3 for tv in range(nsub)], world)
     # the option set of the rank with the most subdomains (all ranks run the same set)
     Hs = D.headline_options(max(list(owner).count(r) for r in range(world)))
     if a.smoother is None:
@@ -221,7 +227,7 @@ def main():
             "dtype": "f64",
             "data": "synthetic",
             "config": {
-                "workload": (f"dehw-synthetic{' general-mesh' if general else ''}: {nsub} subdomains x "
+                "workload": (f"dehw-synthetic{' general-mesh' if general else ''}{' uneven' if a.uneven else ''}: {nsub} subdomains x "
                              f"{total_dofs // nsub} DOF = {total_dofs} DOF, "
                              f"{a.groups} frictional contacts (mu={a.fric}) + {2 * (a.groups - 1)} glued interfaces, "
                              f"{nip} integration points ({nip / total_dofs:.2f} per DOF), "
@@ -234,14 +240,19 @@ def main():
                 "integration_points": nip,
                 "ip_per_dof": nip / total_dofs,
                 "mg_levels": a.gl + 1 + (1 if general else 0),
-                "smoother": {0: "jacobi", 1: "block-jacobi", 2: "chebyshev"}[a.smoother] + f"({a.nu})" if a.smoother != 3
-                else f"fine: multicolour block Gauss-Seidel (1 forward, 1 backward); below: block-jacobi({a.nu})",
+                "smoother": {0: "jacobi", 1: "block-jacobi", 2: "chebyshev"}[a.smoother] + f"({a.nu})" if a.smoother < 3
+                else f"fine: multicolour block Gauss-Seidel (1 forward, 1 backward); below: block-jacobi({a.nu})"
+                if a.smoother == 3 else
+                f"fine: multicolour block SSOR (forward + backward before and after); below: block-jacobi({a.nu})",
                 "pcg_x0": "previous solution" if a.warm_start else "zero",
                 "vcycle_operator_storage": {0: "fp64", 1: "fp32",
                                             2: f"fp32, the {os.environ.get('DDPCA_H16_LEVELS', '3')} finest levels "
                                                "block-exponent fp16",
                                             3: f"fp32, the {os.environ.get('DDPCA_H16_LEVELS', '3')} finest levels "
-                                               "block-scaled int8"}[a.precond_fp32],
+                                               "block-scaled int8",
+                                            4: f"fp32, the {os.environ.get('DDPCA_H16_LEVELS', '3')} finest levels "
+                                               "block-scaled int8; the fine colour sweeps gather an fp32 copy "
+                                               "of the iterate"}[a.precond_fp32],
                 "operator_rows": "deduplicated table" if a.table_mode else "streamed",
                 "coarse_space": f"interface-eliminated (muscSett={a.musc}, doleMcsc={a.dole})" if a.musc else "none",
                 **({"hanging_dofs": int(sum(P.grid(tv).hangRows().shape[0] for tv in range(nsub) if owner[tv] == rank)),

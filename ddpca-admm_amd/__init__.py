@@ -97,7 +97,7 @@ def headline_problem(gl: int | None = None, **override) -> "Problem":
     if gl is not None:
         w["gl"] = gl
     return Problem("dehw", w["groups"], w["nx"], w["ny"], w["nz"], w["gl"], w["fric"], w["ip_contact"],
-                   w["ip_glued"], w["band"], w["rot"])
+                   w["ip_glued"], w["band"], w["rot"], w.get("uneven", 0))
 
 _P = C.c_void_p
 _I64P = C.POINTER(C.c_int64)

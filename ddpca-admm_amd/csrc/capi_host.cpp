@@ -248,19 +248,27 @@ void make_dehw(Problem& P, const double* q, int nq) {
     //         an angle varying with y and supported along its local z (a curved roller bed) --
     //         prolongation blocks off w I, R^T K R, CONSTRAINT with nodeRota (MULTIGRID.h:1102-1255)
     const bool band = nq > 8 && q[8] != 0.0, rot = nq > 9 && q[9] != 0.0;
+    //   uneven (q[10], default off): group g is (1 + g mod 3) times n[0] cells long in x -- subdomains
+    //         of three sizes, as DEHW's 52 uneven subdomains (DEHW.h:2238-2258) that LPT packs onto ranks
+    const bool uneven = nq > 10 && q[10] != 0.0;
     if (G < 1) throw std::invalid_argument("dehw: ngroups >= 1");
     if (kc < 0 || kc > 4 || kg < 0 || kg > 4) throw std::invalid_argument("dehw: integration refinement in [0, 4]");
     const double h = 0.01;  // cubic coarse elements
-    const double Lx = n[0] * h, Ly = n[1] * h, H = n[2] * h, p = 1.0e7;
+    const double Ly = n[1] * h, H = n[2] * h, p = 1.0e7;
+    std::vector<int64_t> nxg(G), xo(G + 1, 0);  // per group: cells along x, first cell
+    for (int64_t g = 0; g < G; ++g) {
+        nxg[g] = uneven ? n[0] * (1 + g % 3) : n[0];
+        xo[g + 1] = xo[g] + nxg[g];
+    }
     P.mc.multGrid.resize(2 * G);
 #pragma omp parallel for schedule(dynamic, 1)
     for (int64_t s = 0; s < 2 * G; ++s) {
         const int64_t g = s / 2, wheel = s % 2;
-        const double lo[3] = {g * Lx, 0.0, wheel * H}, hi[3] = {(g + 1) * Lx, Ly, (wheel + 1) * H};
-        const int64_t off[3] = {g * n[0], 0, wheel * n[2]};
+        const double lo[3] = {xo[g] * h, 0.0, wheel * H}, hi[3] = {xo[g + 1] * h, Ly, (wheel + 1) * H};
+        const int64_t off[3] = {xo[g], 0, wheel * n[2]}, ng[3] = {nxg[g], n[1], n[2]};
         MULTIGRID& m = P.mc.multGrid[s];
         if (wheel) m.mateElas = 110.0e9;
-        build_box(m, lo, hi, n, gl, off);
+        build_box(m, lo, hi, ng, gl, off);
         if (wheel) {  // (on the lattice, before any local refinement)
             const double t[3] = {0.5 * fric * p, 0.0, -p};
             face_traction(m, 2, 2 * n[2] * (int64_t(1) << gl), t);
@@ -311,7 +319,7 @@ void make_dehw(Problem& P, const double* q, int nq) {
             P.mc.searCont[ts].body[0] = 2 * g + w;
             P.mc.searCont[ts].body[1] = 2 * (g + 1) + w;
             P.mc.searCont[ts].fric = -1.0;
-            plane[ts] = {0, (g + 1) * n[0] * scale};
+            plane[ts] = {0, xo[g + 1] * scale};
         }
     std::vector<std::exception_ptr> err(nint);
 #pragma omp parallel for schedule(dynamic, 1)
@@ -323,7 +331,7 @@ void make_dehw(Problem& P, const double* q, int nq) {
             // refined contact faces are half as wide: one subdivision level less keeps the
             // integration points per unit area
             const int ke = ts < G ? std::max(k - 1, 0) : k;
-            const double v = (double)plane[ts][1] / (double)scale * (plane[ts][0] == 2 ? H / n[2] : Lx / n[0]);
+            const double v = (double)plane[ts][1] / (double)scale * h;
             conforming_interface_xyz(P.mc.multGrid[itf.body[0]], P.mc.multGrid[itf.body[1]], (int)plane[ts][0], v, itf.ip,
                                      1 << ke);
         } else {

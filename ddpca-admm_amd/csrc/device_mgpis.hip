@@ -532,6 +532,8 @@ struct GsArgs {
     double* partial;
     const float* minvc;  // chunk-ordered fp32 inverses (GsFine::minvc), or null (fp64 copy): minv by row
     float4* x4;          // the fp32 iterate copy the sweeps gather (GsFine::x4), or null
+    float4* r4;          // X4 residual (PH 1) in fp32 for the restriction (GsFine::r4), or null: r in fp64
+    double* w;           // SSOR (k_gs_ssor): the partial sums a sweep hands to the next one, 3 per row
 };
 
 // the colour sweep's per-row tail: PH 1 stores r = -s; PH 0 / 2 store x = M (b - s) and return
@@ -545,9 +547,13 @@ __device__ __forceinline__ double gs_epilogue(const GsArgs& a, int64_t c, int ln
     double dotv = 0.0;
     if (PH == 1) {
         if (real) {
-            a.r[o] = -s0;
-            a.r[o + 1] = -s1;
-            a.r[o + 2] = -s2;
+            if (X4 && a.r4) {
+                a.r4[row] = make_float4((float)-s0, (float)-s1, (float)-s2, 0.0f);
+            } else {
+                a.r[o] = -s0;
+                a.r[o + 1] = -s1;
+                a.r[o + 2] = -s2;
+            }
         }
     } else {
         const double b0 = a.b[o], b1 = a.b[o + 1], b2 = a.b[o + 2];
@@ -606,6 +612,97 @@ __global__ __launch_bounds__(kWave) void k_gs(GsArgs a) {
     }
     const double dotv = gs_epilogue<PH, DOT, T, X4>(a, c, lane, row, real, s0, s1, s2);
     if (DOT) chunk_partial(dotv, a.partial, c);
+}
+
+// Multicolour block SSOR on the fine level (opt.smoother = 4, the reference's MULT_VCYC smoothing
+// order, MGPIS.h:64-76, 101-114: a forward AND a backward sweep before and after the coarse
+// correction), with the reference's reuse of the previous sweep's partial sums (its p0 / p1) so
+// that each sweep reads only the blocks it must: per row the sums L x, U x of the colour split
+// (L = earlier colours), w = 3 doubles per row handed from one phase to the next.
+//   PH 6  forward from zero:      x = M (b - L x),          w = L x                 (L)
+//   PH 7  backward:               x = M (b - w - U x)                               (U)
+//   PH 8  residual:               r = w - L x   (= b - M^-1 x - L x - U x)          (L)
+//   PH 9  forward from P e:       x = M (b - L x - U x),    w = b - L x             (L + U)
+//   PH 10 backward:               x = M (w - U x), DOT: b . x                       (U)
+// Three operator passes per V-cycle against the Gauss-Seidel pair's two.
+template <int PH, bool DOT, typename T, typename CT, bool X4 = false>
+__global__ __launch_bounds__(kWave) void k_gs_ssor(GsArgs a) {
+    const int lane = threadIdx.x;
+    const int64_t li = blockIdx.x;
+    if (li >= a.n) return;
+    const int64_t c = a.list ? (int64_t)a.list[li] : li;
+    const int sub = a.csub[c];
+    if (stopped(a.sc, sub)) return;
+    const int32_t rr = a.rowidx[c * kChunk + lane];
+    const bool real = rr >= 0;
+    const int64_t row = real ? rr : ~rr;
+    constexpr int64_t SV = slot_vals<T>() * kChunk;
+    const T* val = static_cast<const T*>(a.val);
+    const CT* colp;
+    if constexpr (sizeof(CT) == 2) colp = a.col16;
+    else colp = a.col;
+    double l0 = 0.0, l1 = 0.0, l2 = 0.0, u0 = 0.0, u1 = 0.0, u2 = 0.0;
+    if constexpr (PH == 6 || PH == 8 || PH == 9) {
+        const int64_t o = a.offl[c];
+        if constexpr (X4) sell_rows<1, T, CT>(colp + o * kChunk + lane, val + o * SV + lane, (const float4*)a.x4, a.nsl[c], row, l0, l1, l2);
+        else sell_rows<1, T, CT>(colp + o * kChunk + lane, val + o * SV + lane, (const double*)a.x, a.nsl[c], row, l0, l1, l2);
+    }
+    if constexpr (PH == 7 || PH == 9 || PH == 10) {
+        const int64_t o = a.offu[c];
+        if constexpr (X4) sell_rows<1, T, CT>(colp + o * kChunk + lane, val + o * SV + lane, (const float4*)a.x4, a.nsu[c], row, u0, u1, u2);
+        else sell_rows<1, T, CT>(colp + o * kChunk + lane, val + o * SV + lane, (const double*)a.x, a.nsu[c], row, u0, u1, u2);
+    }
+    const int64_t o = 3 * row;
+    if constexpr (PH == 8) {
+        if (!real) return;
+        const double r0 = a.w[o] - l0, r1 = a.w[o + 1] - l1, r2 = a.w[o + 2] - l2;
+        if (X4 && a.r4) {
+            a.r4[row] = make_float4((float)r0, (float)r1, (float)r2, 0.0f);
+        } else {
+            a.r[o] = r0;
+            a.r[o + 1] = r1;
+            a.r[o + 2] = r2;
+        }
+        return;
+    } else {
+        const double b0 = a.b[o], b1 = a.b[o + 1], b2 = a.b[o + 2];
+        double c0, c1, c2;
+        if constexpr (PH == 6) {
+            c0 = b0 - l0, c1 = b1 - l1, c2 = b2 - l2;
+        } else if constexpr (PH == 7) {
+            c0 = (b0 - a.w[o]) - u0, c1 = (b1 - a.w[o + 1]) - u1, c2 = (b2 - a.w[o + 2]) - u2;
+        } else if constexpr (PH == 9) {
+            c0 = (b0 - l0) - u0, c1 = (b1 - l1) - u1, c2 = (b2 - l2) - u2;
+        } else {
+            c0 = a.w[o] - u0, c1 = a.w[o + 1] - u1, c2 = a.w[o + 2] - u2;
+        }
+        const float* m = a.minvc + c * 9 * kChunk + lane;
+        const double m0 = __builtin_fma((double)m[2 * kChunk], c2, __builtin_fma((double)m[kChunk], c1, (double)m[0] * c0));
+        const double m1 = __builtin_fma((double)m[5 * kChunk], c2, __builtin_fma((double)m[4 * kChunk], c1, (double)m[3 * kChunk] * c0));
+        const double m2 = __builtin_fma((double)m[8 * kChunk], c2, __builtin_fma((double)m[7 * kChunk], c1, (double)m[6 * kChunk] * c0));
+        double dotv = 0.0;
+        if (real) {
+            if constexpr (PH == 6) {
+                a.w[o] = l0;
+                a.w[o + 1] = l1;
+                a.w[o + 2] = l2;
+            } else if constexpr (PH == 9) {
+                a.w[o] = b0 - l0;
+                a.w[o + 1] = b1 - l1;
+                a.w[o + 2] = b2 - l2;
+            }
+            // x4 mode: every sweep writes the fp32 copy the later colours gather; the last backward
+            // sweep (PH 10) also the fp64 output z
+            if (X4) a.x4[row] = make_float4((float)m0, (float)m1, (float)m2, 0.0f);
+            if (!X4 || PH == 10) {
+                a.x[o] = m0;
+                a.x[o + 1] = m1;
+                a.x[o + 2] = m2;
+            }
+            if (DOT) dotv = __builtin_fma(b2, m2, __builtin_fma(b1, m1, b0 * m0));
+        }
+        if (DOT) chunk_partial(dotv, a.partial, c);
+    }
 }
 
 // Band mode's rows outside the colours (GsFine::band; one wave per chunk of the ring / far groups):
@@ -737,8 +834,8 @@ __global__ __launch_bounds__(kBlock) void k_restrict(const double* rf, const int
 // Lattice restriction (LevelDev::lat): children f0 + d0 t0 + d1 t1 + d2 t2 for the bits of the
 // coarse node's 27-bit mask, weight 2^-(|d0|+|d1|+|d2|); every index is computed, the 27 gathers
 // are independent (no index / weight stream)
-template <bool INIT, bool BJ, bool SETD, typename MT = double>
-__global__ __launch_bounds__(kBlock) void k_restrict_lat(const double* rf, const uint32_t* rmsk, const int32_t* rf0,
+template <bool INIT, bool BJ, bool SETD, typename MT = double, typename RT = double>
+__global__ __launch_bounds__(kBlock) void k_restrict_lat(const RT* rf, const uint32_t* rmsk, const int32_t* rf0,
                                                          const int32_t* rstr, const uint8_t* cmask, double* bc,
                                                          double* xc, double* dc, const MT* minv, const double* coef,
                                                          int64_t nc, const int32_t* csub, const PcgScal* sc) {
@@ -757,9 +854,10 @@ __global__ __launch_bounds__(kBlock) void k_restrict_lat(const double* rf, const
         const double w = 1.0 / (double)(1 << ((d0 != 0) + (d1 != 0) + (d2 != 0)));
         const int64_t f = f0 + d0 * t0 + d1 * t1 + d2 * t2;
         if ((msk >> q) & 1u) {
-            s0 += w * rf[3 * f];
-            s1 += w * rf[3 * f + 1];
-            s2 += w * rf[3 * f + 2];
+            const X3 v = ldx(rf, f);  // RT = float4: the fine residual's fp32 copy (GsFine::r4), one 16-B load
+            s0 += w * v.a;
+            s1 += w * v.b;
+            s2 += w * v.c;
         }
     }
     restrict_store<INIT, BJ, SETD>(cmask, bc, xc, dc, minv, coef, j, sub, s0, s1, s2);
@@ -1946,9 +2044,9 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
     DDPCA_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
     if (opt.nu < 1) opt.nu = 1;
     if (opt.iters_per_graph < 1) opt.iters_per_graph = 1;
-    if (opt.smoother < 0 || opt.smoother > 3) throw ApiError(DDPCA_EINVAL, "smoother must be 0..3");
+    if (opt.smoother < 0 || opt.smoother > 4) throw ApiError(DDPCA_EINVAL, "smoother must be 0..4");
     // the multicolour sweeps' symmetric pairing needs K = K^T: nonsymmetric handles smooth with block Jacobi
-    if (opt.smoother == 3 && general) opt.smoother = 1;
+    if (opt.smoother >= 3 && general) opt.smoother = 1;
     const bool bj = opt.smoother >= 1;
     // device numbering: perm[l][s][reference local node] = device local node.  Levels >= 1 with
     // coordinates: lexicographic, or -- table mode, when the level's distinct rows compress --
@@ -2174,7 +2272,7 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
             }
             L.minv32.upload(m32);
         }
-        if (l == nlev - 1 && nlev > 1 && opt.smoother == 3) {
+        if (l == nlev - 1 && nlev > 1 && opt.smoother >= 3) {
             // the V-cycle copy's storage type of this level (vc_type once the level is up)
             const int vt = (!vc32 || L.tbl) ? kVal64 : L.val8.p ? kValQ8 : L.val16.p ? kValH16 : kVal32;
             // band mode (locally refined fine level): sweep only the nodes this level
@@ -2183,7 +2281,7 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
             // is at most 60 % of the rows; DDPCA_GS_BAND=0 sweeps every row
             std::vector<uint8_t> bandv;
             const char* be = std::getenv("DDPCA_GS_BAND");
-            if (!(be && be[0] == '0')) {
+            if (!(be && be[0] == '0') && opt.smoother == 3) {  // (colour SSOR sweeps every row)
                 bandv.assign(L.nn, 0);
                 int64_t nreal = 0, nband = 0;
                 for (int s = 0; s < nsub; ++s) {
@@ -2497,9 +2595,20 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
     for (auto& L : lev) maxch = std::max<int64_t>(maxch, L.nch);
     partial.alloc(2 * maxch);
     if (gs_fine()) gs.partial.alloc(gs.nchunk);
+    if (gs_fine() && opt.smoother == 4) {
+        if (gs.band) throw ApiError(DDPCA_EINVAL, "colour SSOR (smoother 4) on a band-mode fine level");
+        gs.w.alloc(3 * lev.back().nn);
+        gs.w.zero(stream);
+    }
     if (gs_fine() && opt.precond_fp32 == 4 && !gs.band && lev.back().lat && lev.back().nrot == 0) {
         gs.x4.alloc(4 * lev.back().nn);
         gs.x4.zero(stream);
+        // the residual the restriction reads, in fp32 too (DDPCA_GS_R32=0: fp64, A/B)
+        const char* er = std::getenv("DDPCA_GS_R32");
+        if (!(er && er[0] == '0')) {
+            gs.r4.alloc(4 * lev.back().nn);
+            gs.r4.zero(stream);
+        }
         // the per-launch byte model on the 16-B iterate: gathers 16 instead of 24 B per distinct
         // node, the forward sweep writes 16 B per row, the backward sweep 16 + 24
         const int K = gs.ncol;
@@ -2508,6 +2617,8 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
             gs.launch_bytes[2 * K - k] += -8.0 * gs.gx_b[k] + 16.0 * gs.rows_k[k];
         }
         gs.launch_bytes[K] -= 8.0 * gs.gx_r;
+        if (gs.r4.p)
+            for (int k = 0; k < K; ++k) gs.launch_bytes[K] -= 8.0 * gs.rows_k[k];  // r written in 16 B
     }
     sc.alloc(nsub);
     DDPCA_HIP(hipHostMalloc(reinterpret_cast<void**>(&sc_host), nsub * sizeof(PcgScal)));
@@ -2721,7 +2832,14 @@ namespace {
 template <bool INIT, bool BJ, bool SETD, typename MT>
 void launch_restrict(const LevelDev& F, int grid, hipStream_t st, const double* rf, const uint8_t* cmask, double* bc,
                      double* xc, double* dc, const MT* minv, const double* coef, int64_t nc, const int32_t* csub,
-                     const PcgScal* sc) {
+                     const PcgScal* sc, const float4* rf4 = nullptr) {
+    // rf4: the fine residual in the colour sweeps' fp32 copy (lattice transfers only, GsFine::r4)
+    if (rf4) {
+        if (!F.lat) throw ApiError(DDPCA_ESTATE, "fp32 residual copy without lattice transfers");
+        hipLaunchKernelGGL((k_restrict_lat<INIT, BJ, SETD, MT, float4>), dim3(grid), dim3(kBlock), 0, st, rf4, F.rmsk.p,
+                           F.rf0.p, F.rstr.p, cmask, bc, xc, dc, minv, coef, nc, csub, sc);
+        return;
+    }
     // stored weights: deriving them from a gathered parent count (as k_prolong<true> does)
     // measured 58 -> 102 us on the fine level (profiles/r01_transfer_weights.txt)
     if (F.lat) {
@@ -2848,6 +2966,17 @@ void launch_gs_t(const GsArgs& a, bool c16, hipStream_t st) {  // c16: 16-bit co
     else hipLaunchKernelGGL((k_gs<PH, DOT, T, int32_t>), dim3((unsigned)a.n), dim3(kWave), 0, st, a);
 }
 
+template <int PH, bool DOT, typename T>
+void launch_gs_ssor_t(const GsArgs& a, bool c16, hipStream_t st) {
+    if (a.x4) {
+        if (c16) hipLaunchKernelGGL((k_gs_ssor<PH, DOT, T, int16_t, true>), dim3((unsigned)a.n), dim3(kWave), 0, st, a);
+        else hipLaunchKernelGGL((k_gs_ssor<PH, DOT, T, int32_t, true>), dim3((unsigned)a.n), dim3(kWave), 0, st, a);
+        return;
+    }
+    if (c16) hipLaunchKernelGGL((k_gs_ssor<PH, DOT, T, int16_t>), dim3((unsigned)a.n), dim3(kWave), 0, st, a);
+    else hipLaunchKernelGGL((k_gs_ssor<PH, DOT, T, int32_t>), dim3((unsigned)a.n), dim3(kWave), 0, st, a);
+}
+
 template <int PH, typename T>
 void launch_gs_aux_t(const GsArgs& a, bool c16, hipStream_t st) {
     if (c16) hipLaunchKernelGGL((k_gs_aux<PH, T, int16_t>), dim3((unsigned)a.n), dim3(kWave), 0, st, a);
@@ -2891,7 +3020,17 @@ void launch_gs(const MgpisDevice& D, int k, double* x, const double* b, double* 
     // whole lines for half the data, +1.1 %, profiles/r03o); the fp64 copy reads minv by row
     a.minvc = G.minvc.p;
     a.x4 = reinterpret_cast<float4*>(G.x4.p);
+    a.r4 = reinterpret_cast<float4*>(G.r4.p);
+    a.w = G.w.p;
     const bool c16 = G.col16.p != nullptr;
+    if constexpr (PH >= 6) {  // SSOR phases: the reduced-precision copies' chunk-ordered inverses
+        if (!G.minvc.p) throw ApiError(DDPCA_ESTATE, "colour SSOR needs a reduced-precision V-cycle copy (precond_fp32 >= 1)");
+        a.minv = F.minv32.p;
+        if (G.val8.p) a.val = G.val8.p, launch_gs_ssor_t<PH, DOT, uint8_t>(a, c16, D.stream);
+        else if (G.val16.p) a.val = G.val16.p, launch_gs_ssor_t<PH, DOT, uint16_t>(a, c16, D.stream);
+        else a.val = G.val32.p, launch_gs_ssor_t<PH, DOT, float>(a, c16, D.stream);
+        return;
+    }
     if (G.val8.p) {
         a.val = G.val8.p;
         a.minv = F.minv32.p;
@@ -2970,7 +3109,13 @@ void MgpisDevice::vcycle(const double* rin, double* zout, bool dot) {
     const bool gsf = gs_fine();
     if (gsf) cur[Lf] = zout;  // the Gauss-Seidel sweeps run in place
     // ---- descend
-    if (gsf) {
+    const bool ssor = gsf && opt.smoother == 4;
+    if (ssor) {
+        // colour SSOR: forward sweep from zero, backward sweep, residual r = w - L x
+        for (int k = 0; k < gs.ncol; ++k) launch_gs<6, false>(*this, k, zout, rin, nullptr, scp, nullptr);
+        for (int k = gs.ncol - 1; k >= 0; --k) launch_gs<7, false>(*this, k, zout, rin, nullptr, scp, nullptr);
+        launch_gs<8, false>(*this, -1, zout, rin, lev[Lf].r.p, scp, nullptr);
+    } else if (gsf) {
         // forward sweep from zero, colour by colour, then r = -U x in one launch; band mode: the
         // rows outside the colours start at x = 0, r = b, the ring's r = b - K x after the sweep
         if (gs.band) launch_gs<5, false>(*this, -3, zout, rin, lev[Lf].r.p, scp, nullptr);
@@ -3020,22 +3165,24 @@ void MgpisDevice::vcycle(const double* rin, double* zout, bool dot) {
                 else hipLaunchKernelGGL((k_jac0<false, false>), dim3(grid), dim3(kBlock), 0, stream, C.b.p, C.minv.p, cf, cur[c], nullptr, C.nn, C.csub.p, scp);
             }
         } else {
+            // x4 mode: the colour sweeps' residual is the fp32 copy (GsFine::r4)
+            const float4* rf4 = gsf && l == Lf && gs.r4.p ? reinterpret_cast<const float4*>(gs.r4.p) : nullptr;
             if (c == cl)
-                launch_restrict<false, false, false, double>(F, grid, stream, F.r.p, C.mask.p, C.b.p, nullptr, nullptr, nullptr, nullptr, C.nn, C.csub.p, scp);
+                launch_restrict<false, false, false, double>(F, grid, stream, F.r.p, C.mask.p, C.b.p, nullptr, nullptr, nullptr, nullptr, C.nn, C.csub.p, scp, rf4);
             else if (vc_type(c) != kVal64) {
                 const float* m = C.minv32.p;
                 if (cheb)
-                    launch_restrict<true, true, true, float>(F, grid, stream, F.r.p, C.mask.p, C.b.p, cur[c], C.d.p, m, cf, C.nn, C.csub.p, scp);
+                    launch_restrict<true, true, true, float>(F, grid, stream, F.r.p, C.mask.p, C.b.p, cur[c], C.d.p, m, cf, C.nn, C.csub.p, scp, rf4);
                 else if (bj)
-                    launch_restrict<true, true, false, float>(F, grid, stream, F.r.p, C.mask.p, C.b.p, cur[c], nullptr, m, cf, C.nn, C.csub.p, scp);
+                    launch_restrict<true, true, false, float>(F, grid, stream, F.r.p, C.mask.p, C.b.p, cur[c], nullptr, m, cf, C.nn, C.csub.p, scp, rf4);
                 else
-                    launch_restrict<true, false, false, float>(F, grid, stream, F.r.p, C.mask.p, C.b.p, cur[c], nullptr, m, cf, C.nn, C.csub.p, scp);
+                    launch_restrict<true, false, false, float>(F, grid, stream, F.r.p, C.mask.p, C.b.p, cur[c], nullptr, m, cf, C.nn, C.csub.p, scp, rf4);
             } else if (cheb)
-                launch_restrict<true, true, true, double>(F, grid, stream, F.r.p, C.mask.p, C.b.p, cur[c], C.d.p, C.minv.p, cf, C.nn, C.csub.p, scp);
+                launch_restrict<true, true, true, double>(F, grid, stream, F.r.p, C.mask.p, C.b.p, cur[c], C.d.p, C.minv.p, cf, C.nn, C.csub.p, scp, rf4);
             else if (bj)
-                launch_restrict<true, true, false, double>(F, grid, stream, F.r.p, C.mask.p, C.b.p, cur[c], nullptr, C.minv.p, cf, C.nn, C.csub.p, scp);
+                launch_restrict<true, true, false, double>(F, grid, stream, F.r.p, C.mask.p, C.b.p, cur[c], nullptr, C.minv.p, cf, C.nn, C.csub.p, scp, rf4);
             else
-                launch_restrict<true, false, false, double>(F, grid, stream, F.r.p, C.mask.p, C.b.p, cur[c], nullptr, C.minv.p, cf, C.nn, C.csub.p, scp);
+                launch_restrict<true, false, false, double>(F, grid, stream, F.r.p, C.mask.p, C.b.p, cur[c], nullptr, C.minv.p, cf, C.nn, C.csub.p, scp, rf4);
         }
     }
     if (ainv32.p) hipLaunchKernelGGL(k_coarse<float>, dim3(ceil_div(3 * lev[cl].nn, 4)), dim3(kBlock), 0, stream, ainv32.p, aoff.p, c_noff.p,
@@ -3055,6 +3202,15 @@ void MgpisDevice::vcycle(const double* rin, double* zout, bool dot) {
         else hipLaunchKernelGGL(k_prolong<false>, dim3(ceil_div(F.nn, kBlock)), dim3(kBlock), 0, stream, cur[l - 1], F.ppar.p, F.pw.p,
                            F.mask.p, cur[l], F.nn, F.csub.p, scp);
         rot_prolong(l, cur[l - 1], cur[l], scp);
+        if (ssor && l == Lf) {
+            // colour SSOR after the coarse correction: forward, then backward with the dot partials
+            for (int k = 0; k < gs.ncol; ++k) launch_gs<9, false>(*this, k, zout, rin, nullptr, scp, nullptr);
+            for (int k = gs.ncol - 1; k >= 0; --k) {
+                if (dot) launch_gs<10, true>(*this, k, zout, rin, nullptr, scp, gs.partial.p);
+                else launch_gs<10, false>(*this, k, zout, rin, nullptr, scp, nullptr);
+            }
+            continue;
+        }
         if (gsf && l == Lf) {
             // backward sweep; the dot product's partials per colour chunk (vc_cb)
             for (int k = gs.ncol - 1; k >= 0; --k) {
@@ -3132,10 +3288,19 @@ void MgpisDevice::vcycle_bytes(int s, double out[2]) const {
     // x4 mode (GsFine::x4): the iterate the sweeps gather and the forward sweep / prolongation
     // write is the 16-B fp32 copy; the backward sweep writes it and the fp64 output
     const double xb = gsf && gs.x4.p ? 16.0 : 24.0;
-    if (gsf) {
+    const double rb = gsf && gs.r4.p ? 16.0 : 24.0;  // the residual written by the sweeps, read by the restriction
+    const bool ssor = gsf && opt.smoother == 4;
+    if (ssor) {
+        // colour SSOR: forward from zero (L; b, M^-1, x, w written), backward (U; b, w, M^-1 read, x
+        // written), residual (L; w read, r written); x entries gathered as the Gauss-Seidel pair's
+        const double lpass = gsmat * 0.5, upass = gsmat * 0.5, row = 4.0;
+        put(Lf, lpass + nsw * (24.0 + minv(Lf) + xb + 24.0 + row + xb * (K - 1.0) / 2.0));
+        put(Lf, upass + nsw * (48.0 + minv(Lf) + xb + row + xb * (K - 1.0) / 2.0));
+        put(Lf, lpass + nsw * (24.0 + rb + row + xb * (K - 1.0) / 2.0));
+    } else if (gsf) {
         put(Lf, 76.0 * nout);  // band mode: x = 0, r = b outside the colours (b read, x, r written, row index)
         put(Lf, gsmat + nsw * (24.0 + minv(Lf) + xb + 4.0 + xb * (K - 1.0) / 2.0));  // forward
-        put(Lf, nsw * (24.0 + 4.0 + xb * (K - 1.0) / 2.0));                          // residual
+        put(Lf, nsw * (rb + 4.0 + xb * (K - 1.0) / 2.0));                            // residual
         // band mode: the ring's residual over its band columns (blocks, b read, r written, x gathered)
         put(Lf, gsvb * (double)(gs.band ? gs.ring_nnzb_sub[s] : 0) + nring * (24.0 + 24.0 + 4.0 + 24.0));
     } else {
@@ -3151,7 +3316,7 @@ void MgpisDevice::vcycle_bytes(int s, double out[2]) const {
         const bool init = c != cl;
         // coarse node: mask + b_c written (+ x_c = w M b_c: M^-1 read, x_c written; Chebyshev d_c)
         double cn = 1.0 + 24.0 + (init ? minv(c) + 24.0 + (cheb ? 24.0 : 0.0) : 0.0);
-        double tr = 24.0 * n(l);  // r_f read once
+        double tr = (gsf && l == Lf ? rb : 24.0) * n(l);  // r_f read once
         if (F.lat) cn += 8.0;     // 27-bit child mask + fine copy
         else tr += 12.0 * (double)F.tent_sub[s];  // child index + weight per stencil entry
         tr += 4.0 * 8.0 * (double)F.tblk_sub[s] + (F.tblk_sub[s] ? 24.0 * n(c) : 0.0);  // block entries (B^T r_f)
@@ -3166,6 +3331,13 @@ void MgpisDevice::vcycle_bytes(int s, double out[2]) const {
         else pb += (F.uw ? 4.0 : 12.0) * (double)F.tent_sub[s];
         pb += 4.0 * 8.0 * (double)F.tblk_sub[s];
         put(l, pb);
+        if (ssor && l == Lf) {
+            // forward from the prolongated x (L + U; b, M^-1 read, x, w written), backward (U; b, w,
+            // M^-1 read, z written)
+            put(l, gsmat + nsw * (24.0 + minv(l) + xb + 24.0 + 4.0 + xb * (K - 1.0)));
+            put(l, gsmat * 0.5 + nsw * (48.0 + minv(l) + 24.0 + 4.0 + xb * (K - 1.0) / 2.0));
+            continue;
+        }
         if (gsf && l == Lf) {
             put(l, gsmat + nsw * (24.0 + minv(l) + 24.0 + (xb < 24.0 ? xb : 0.0) + 4.0 + xb * (K - 1.0)));  // backward
             put(l, 52.0 * nout);  // band mode: b . x of the rows outside the colours (b, x read, row index)
@@ -3199,6 +3371,7 @@ int64_t MgpisDevice::iteration_launches() const {
     const int64_t nd = (int64_t)lev.size() - 1 - clev;
     const int64_t base = 5 + (nd == 0 ? 2 : 1 + nd * (opt.nu + 1) + 1 + nd * (1 + opt.nu));
     // (band mode: + the x = 0 / r = b launch, the ring's residual and the dot of the other rows)
+    if (gs_fine() && nd > 0 && opt.smoother == 4) return base - 1 - 2 * opt.nu + 4 * gs.ncol + 1;  // colour SSOR
     return gs_fine() && nd > 0 ? base - 1 - 2 * opt.nu + 2 * gs.ncol + 1 + (gs.band ? 3 : 0) : base;
 }
 

@@ -167,6 +167,8 @@ struct GsFine {
     // The block products, the epilogues and z stay fp64: the preconditioner moves by the fp32
     // rounding of the neighbours' values (lattice fine transfers without block entries, no band)
     DevBuf<float> x4;
+    DevBuf<double> w;  // colour SSOR (opt.smoother = 4, k_gs_ssor): the partial sums handed between sweeps
+    DevBuf<float> r4;  // ... and the residual after the forward sweep (PH 1), which the fine restriction reads
     DevBuf<double> partial;              // per colour chunk: the backward sweep's dot partials (their own
                                          // buffer: a split batch's other half writes the Krylov partials meanwhile)
     std::vector<int64_t> nnzb_sub;       // per member: stored off-diagonal blocks (byte model)

@@ -30,3 +30,12 @@ def block_owner(nsub: int, nranks: int) -> list[int]:
     if nranks < 1:
         raise ValueError("nranks must be >= 1")
     return [min(nranks - 1, tv * nranks // nsub) for tv in range(nsub)]
+
+
+def owner_for(sizes: Sequence[int], nranks: int) -> list[int]:
+    """The bench's and the tests' layout rule: contiguous blocks (block_owner, which keeps DEHW's
+    worm/wheel contact pairs on one rank) when every subdomain has the same size, LPT packing by
+    size (lpt_owner) when they differ -- DEHW's 52 subdomains of different sizes (DEHW.h:2238-2258)."""
+    if len(set(int(s) for s in sizes)) <= 1:
+        return block_owner(len(sizes), nranks)
+    return lpt_owner(sizes, nranks)

@@ -91,6 +91,22 @@ def test_partition_helpers():
     own = part.lpt_owner([5, 4, 3, 3, 2, 1], 3)
     loads = [sum(d for d, o in zip([5, 4, 3, 3, 2, 1], own) if o == r) for r in range(3)]
     assert max(loads) - min(loads) <= 1
+    # the layout rule of bench.py: blocks for equal sizes, LPT otherwise
+    assert part.owner_for([7] * 8, 4) == part.block_owner(8, 4)
+    assert part.owner_for([5, 4, 3, 3, 2, 1], 3) == own
+
+
+def test_uneven_dehw_chain_sizes(ddpca):
+    """The dehw generator's `uneven` chain (q[10]): group g is 1 + g mod 3 blocks long, so the
+    subdomains come in three sizes (DEHW's uneven subdomains, DEHW.h:2238-2258), with the glued
+    x planes at the groups' cumulative lengths: every interface still conforming (integration
+    points on both sides)."""
+    P = ddpca.Problem("dehw", 6, 2, 2, 1, 1, 0.3, 0, 0, 0, 0, 1)
+    sizes = [len(P.array("coords", tv)) // 3 for tv in range(P.nsub)]
+    assert len(set(sizes)) == 3 and sizes[0] < sizes[2] < sizes[4] and sizes[0] == sizes[6], sizes
+    for ts in range(P.nint):
+        assert len(P.array("ip_w", ts)) > 0
+    P.ESTABLISH()
 
 
 REF_BIND = Path(__file__).resolve().parents[1] / "oracle" / "_ref" / "ref_bind"

@@ -113,12 +113,23 @@ def test_vcycle_is_symmetric_positive(ddpca, gpu):
     n = len(P.grid(0).consForc)
     rng = np.random.default_rng(20251017)
     for smoother, nu, f32 in [(0, 1, 0), (1, 1, 0), (2, 2, 0), (2, 2, 1), (1, 1, 2), (2, 2, 2), (3, 1, 0), (3, 2, 1),
-                              (3, 2, 2), (1, 1, 3), (3, 2, 3)]:
+                              (3, 2, 2), (1, 1, 3), (3, 2, 3), (4, 2, 3), (4, 2, 1)]:
         M = ddpca.MGPIS.from_problem(P, 0, smoother=smoother, nu=nu, precond_fp32=f32)
         u, v = rng.standard_normal(n), rng.standard_normal(n)
         Mu, Mv = M.MULT_VCYC(u), M.MULT_VCYC(v)
         assert abs(u @ Mv - v @ Mu) <= 1e-10 * abs(u @ Mv)
         assert v @ Mv > 0
+    # precond_fp32 = 4: the colour sweeps gather an fp32 copy of the iterate (GsFine::x4; lattice
+    # fine transfers, so on a headline subdomain), so the V-cycle is symmetric only to that rounding
+    # (a few 1e-8 relative); still positive
+    H = ddpca.headline_problem(gl=3).ESTABLISH()
+    n = len(H.grid(1).consForc)
+    M = ddpca.MGPIS.from_problem(H, 1, smoother=3, nu=2, precond_fp32=4)
+    u, v = rng.standard_normal(n), rng.standard_normal(n)
+    Mu, Mv = M.MULT_VCYC(u), M.MULT_VCYC(v)
+    print("fp32 iterate copy: symmetry", abs(u @ Mv - v @ Mu) / abs(u @ Mv))
+    assert abs(u @ Mv - v @ Mu) <= 1e-6 * abs(u @ Mv)
+    assert v @ Mv > 0
 
 
 @pytest.mark.parametrize("f32", [0, 2])
@@ -137,6 +148,56 @@ def test_multicolour_gauss_seidel_on_the_headline_subdomains(ddpca, gpu, f32):
         assert rr <= 1e-14
         assert ig <= 0.85 * ij, (ig, ij)
         assert np.linalg.norm(xg - xj) <= 1e-10 * np.linalg.norm(xj)
+
+
+def test_fp32_iterate_copy_keeps_the_solution(ddpca, gpu):
+    """precond_fp32 = 4: as 3 (int8 V-cycle copies), and the fine colour sweeps gather the iterate
+    from an fp32 stride-4 copy (one 16-B load per neighbour block instead of three 8-B fp64 loads;
+    the forward sweep and the prolongation write only that copy, the backward sweep also the fp64
+    output z).  The products, the epilogues and z stay fp64, so the preconditioner moves only by the
+    fp32 rounding of the neighbours' values: PCG (the Krylov operator and vectors, the dot products and
+    the stop rule in fp64) must reach the same ||r|| <= 1e-14 ||b|| within one more iteration, and the
+    solution within the PCG's tolerance of the int8 run's."""
+    P = ddpca.headline_problem(gl=3).ESTABLISH()
+    for tv in (0, 1):
+        b = P.grid(tv).consForc
+        if not np.any(b):
+            b = np.random.default_rng(tv).standard_normal(len(b))
+        opt = dict(smoother=3, nu=2, omega=-1.7, table_mode=0)
+        M3 = ddpca.MGPIS.from_problem(P, tv, precond_fp32=3, **opt)
+        M4 = ddpca.MGPIS.from_problem(P, tv, precond_fp32=4, **opt)
+        x3, i3, _ = M3.CG_SOLV(1, b)
+        x4, i4, rr = M4.CG_SOLV(1, b)
+        # the fp32 copy is on (the V-cycles differ by the rounding of the gathered iterate only)
+        r = np.random.default_rng(7).standard_normal(len(b))
+        z3, z4 = M3.MULT_VCYC(r), M4.MULT_VCYC(r)
+        dz = np.linalg.norm(z4 - z3) / np.linalg.norm(z3)
+        print(tv, "int8", i3, "int8 + fp32 iterate", i4, "V-cycle difference", dz)
+        assert 0.0 < dz <= 1e-5
+        assert rr <= 1e-14
+        assert i4 <= i3 + 1, (i4, i3)
+        assert np.linalg.norm(x4 - x3) <= 1e-10 * np.linalg.norm(x3)
+
+
+@pytest.mark.parametrize("lowp", [3, 4])
+def test_colour_ssor_keeps_the_solution(ddpca, gpu, lowp):
+    """smoother = 4: multicolour block SSOR on the fine level -- a forward and a backward sweep before
+    AND after the coarse correction, the reference's MULT_VCYC smoothing order (MGPIS.h:64-76,
+    101-114), with its reuse of the previous sweep's partial sums (three operator passes per V-cycle
+    instead of the Gauss-Seidel pair's two).  Same stop rule and solution as smoother 3, in no more
+    PCG iterations (CPU study, profiles/r06_study: 18 -> 17 at gl 4 on the int8 copies)."""
+    P = ddpca.headline_problem(gl=3).ESTABLISH()
+    for tv in (0, 1):
+        b = P.grid(tv).consForc
+        if not np.any(b):
+            b = np.random.default_rng(tv).standard_normal(len(b))
+        opt = dict(nu=2, omega=-1.7, table_mode=0, precond_fp32=lowp)  # 4: on the fp32 iterate copy too
+        x3, i3, _ = ddpca.MGPIS.from_problem(P, tv, smoother=3, **opt).CG_SOLV(1, b)
+        x4, i4, rr = ddpca.MGPIS.from_problem(P, tv, smoother=4, **opt).CG_SOLV(1, b)
+        print(tv, "precond_fp32", lowp, "colour GS", i3, "colour SSOR", i4)
+        assert rr <= 1e-14
+        assert i4 <= i3, (i4, i3)
+        assert np.linalg.norm(x4 - x3) <= 1e-10 * np.linalg.norm(x3)
 
 
 def test_int8_smoother_copy_keeps_the_solution(ddpca, gpu):

@@ -93,3 +93,73 @@ def test_two_ranks_in_one_process_match_single_rank(ddpca, gpu, owner, musc, dou
                 worst["gamma"] = max(worst["gamma"], float(np.abs(g - gr).max() / np.abs(gr).max()))
     print(f"owner {owner} musc {musc} double_m {double_m}: {n_ref} iterations, worst relative differences {worst}")
     assert worst["moni"] <= 1e-12 and worst["u"] <= 1e-12 and worst["gamma"] <= 1e-12, worst
+
+
+@pytest.mark.parametrize("musc", [0, 2])
+def test_lpt_packed_uneven_subdomains_match_single_rank(ddpca, gpu, musc):
+    """DEHW's subdomains differ in size (52 of them, DEHW.h:2238-2258) and SURVEY §8 e1 packs them
+    onto the GPUs by LPT.  Twelve subdomains of three sizes (the dehw generator's `uneven` chain:
+    group g is 1 + g mod 3 blocks long) packed by partition.owner_for (LPT by node count: uneven
+    batches, every rank holding subdomains of different sizes, interfaces crossing ranks in every
+    direction) on four in-process ranks, against the single-rank run of the same options: the same
+    iteration count on every rank, resuMoni rows, displacements and gamma equal to 1e-12 (the rank
+    layout does not enter the arithmetic)."""
+    from importlib import import_module
+    part = import_module("ddpca-admm_amd.partition")
+    args = ("dehw", 6, 2, 2, 1, 2, 0.3, 0, 0, 0, 0, 1)
+
+    def problem(owner=None, rank=0):
+        P = ddpca.Problem(*args)
+        if musc:
+            P.set_coarse(musc, [1] * P.nsub)
+        return P.ESTABLISH(owner, rank) if owner is not None else P.ESTABLISH()
+
+    P0 = problem()
+    sizes = [len(P0.array("coords", tv)) // 3 for tv in range(P0.nsub)]
+    assert len(set(sizes)) == 3, sizes
+    nr = 4
+    owner = part.owner_for(sizes, nr)
+    assert owner == part.lpt_owner(sizes, nr)
+    loads = [sum(s for s, o in zip(sizes, owner) if o == r) for r in range(nr)]
+    print("sizes", sizes, "owner", owner, "loads", loads)
+    maxit = 300
+    opts = dict(coarse_level=1)
+    ref = ddpca.MCONTACT(P0, **opts)
+    n_ref = ref.CONTACT_ANALYSIS(maxit)
+    rows_ref = ref.monitor()
+    probs = [problem(owner, r) for r in range(nr)]
+    ranks = [ddpca.MCONTACT(probs[r], rank=r, nranks=nr, owner=owner, **opts) for r in range(nr)]
+    ddpca.MCONTACT.comm_local(ranks)
+    out, err = [None] * nr, [None] * nr
+
+    def run(r):
+        try:
+            out[r] = ranks[r].CONTACT_ANALYSIS(maxit)
+        except Exception as e:  # noqa: BLE001 -- reported below
+            err[r] = e
+
+    th = [threading.Thread(target=run, args=(r,)) for r in range(nr)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=240)
+    assert not any(t.is_alive() for t in th), "a rank hung"
+    assert err == [None] * nr, err
+    assert out == [n_ref] * nr, (out, n_ref)
+    worst = {"moni": 0.0, "u": 0.0, "gamma": 0.0}
+    for r in range(nr):
+        rows = ranks[r].monitor()
+        assert rows.shape == rows_ref.shape
+        scale = np.abs(rows_ref).max(axis=0, keepdims=True)
+        worst["moni"] = max(worst["moni"], float((np.abs(rows - rows_ref) / (np.abs(rows_ref) + 1e-12 * scale + 1e-300)).max()))
+        for tv in range(P0.nsub):
+            if owner[tv] == r:
+                u, ur = ranks[r].get("resuDisp", tv), ref.get("resuDisp", tv)
+                worst["u"] = max(worst["u"], float(np.linalg.norm(u - ur) / np.linalg.norm(ur)))
+        for ts in range(P0.nint):
+            body = [int(b) for b in P0.array("iface_body", ts)]
+            if owner[body[0]] == r:
+                g, gr = ranks[r].get("inpoGamm", ts), ref.get("inpoGamm", ts)
+                worst["gamma"] = max(worst["gamma"], float(np.abs(g - gr).max() / np.abs(gr).max()))
+    print(f"musc {musc}: {n_ref} iterations, worst relative differences {worst}")
+    assert worst["moni"] <= 1e-12 and worst["u"] <= 1e-12 and worst["gamma"] <= 1e-12, worst
