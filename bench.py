@@ -329,6 +329,9 @@ def run_general_child(a) -> dict:
            "--no-stream-ceiling", "--steps", str(a.steps), "--warmup", str(a.warmup), "--groups", str(a.groups),
            "--nx", str(a.nx), "--ny", str(a.ny), "--nz", str(a.nz), "--gl", str(a.gl), "--fric", str(a.fric),
            "--ip-contact", str(a.ip_contact), "--ip-glued", str(a.ip_glued),
+           # the fp32 iterate copy (precond_fp32 = 4) needs lattice fine transfers without band mode;
+           # the general line has neither, so it runs the int8 set it would fall back to
+           "--precond-fp32", str(min(a.precond_fp32, 3)),
            "--traffic-json", str(ROOT / "profiles" / "traffic_general.json")]
     env = dict(os.environ, DDPCA_LATTICE="0")
     t0 = time.perf_counter()
@@ -380,6 +383,24 @@ def cpu_baseline(P, mc, budget_s=20.0):
         print(f"[cpu_baseline] reference CG_SOLV leg failed: {e}", file=sys.stderr, flush=True)
         res = cpu_admm.price_iteration(P, mc, budget_s)
         res["reference_measured"] = {"error": str(e)[-300:]}
+    res["host"] = host_cpu()
+    # the reference's WHOLE ADMM iteration on this workload -- its unmodified CONTACT_ANALYSIS
+    # (every subdomain's CG_SOLV(1) in its omp parallel for, the coarse correction, the interface
+    # step, MONITOR, its text output) on the bench's operators at the device run's late state,
+    # measured on a GPU box's host by profiles/ref_admm_time.py (minutes of CPU work: not rerun
+    # here), replayed when it was measured on this workload
+    full = ROOT / "profiles" / "ref_admm_full.json"
+    if full.exists():
+        j = json.loads(full.read_text())
+        if j.get("dof") == P_dofs(P) and j.get("integration_points") == P_nip(P):
+            its = j["iteration_s"]
+            res["reference_full_iteration"] = {
+                "value": j["value"], "unit": "ADMM it/s", "kind": "reference", "cores": j["threads"],
+                "iteration_s": its, "cpu": j.get("cpu"), "host_cores": j.get("host_cores"),
+                "source": f"replayed: {full.relative_to(ROOT)} (profiles/ref_admm_time.py, oracle/ref_admm_time.cpp: "
+                          "the reference's own MCONTACT::CONTACT_ANALYSIS, text output included)",
+                "sample": f"{len(its)} reference ADMM iterations from the device run's state after "
+                          f"{j.get('device_iterations')} iterations: {[round(x, 1) for x in its]} s"}
     cal = ROOT / "profiles" / "r03_cpu_calibration_host.json"
     if not cal.exists():
         cal = ROOT / "profiles" / "r02_cpu_calibration.json"
@@ -390,6 +411,32 @@ def cpu_baseline(P, mc, budget_s=20.0):
                               "port_s": c["port"]["median_s"], "source": str(cal.relative_to(ROOT))}
         res["reference_equivalent"] = res["value"] / c["ref_over_port"]
     return res
+
+
+def P_dofs(P) -> int:
+    return int(sum(int(P.array("freeCount", tv)[-1]) for tv in range(P.nsub)))
+
+
+def P_nip(P) -> int:
+    return int(sum(len(P.array("ip_w", ts)) for ts in range(P.nint)))
+
+
+def host_cpu() -> dict:
+    """The CPU the baseline ran on: model, the machine's physical cores (per socket x sockets) and
+    the threads this process may use (the lease's OMP_NUM_THREADS on the GPU box)"""
+    import re
+    info = {"threads_used": int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)), "logical_cpus": os.cpu_count()}
+    try:
+        txt = open("/proc/cpuinfo").read()
+        m = re.search(r"model name\s*:\s*(.+)", txt)
+        cores = {int(c) for c in re.findall(r"cpu cores\s*:\s*(\d+)", txt)}
+        sockets = {int(p) for p in re.findall(r"physical id\s*:\s*(\d+)", txt)}
+        info.update({"model": m.group(1).strip() if m else None,
+                     "physical_cores": (max(cores) * max(len(sockets), 1)) if cores else None,
+                     "sockets": len(sockets) or None})
+    except OSError:
+        pass
+    return info
 
 
 if __name__ == "__main__":

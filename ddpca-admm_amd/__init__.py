@@ -57,8 +57,12 @@ class MgpisOptions(C.Structure):
 # block-Jacobi V(1,1)'s 23.6 PCG iterations per solve, +8-10 % ADMM it/s at 8 subdomains per GPU,
 # +5 % at 4, equal at 2: profiles/r03j; round 4: +10 % at 4, +4 % at 2,
 # profiles/r04l/ab_small_batch.txt.  The int8 copies instead of block-exponent fp16: 18.6 instead
-# of 18.0 PCG iterations, +6 % ADMM it/s, the one-subdomain rank -7.5 %, profiles/r05r.)
-HEADLINE_OPTIONS = dict(smoother=3, nu=2, omega=-1.7, iters_per_graph=4, warm_start=0, precond_fp32=3,
+# of 18.0 PCG iterations, +6 % ADMM it/s, the one-subdomain rank -7.5 %, profiles/r05r.  Round 6:
+# precond_fp32 = 4 -- the same int8 copies, and the fine colour sweeps gather an fp32 stride-4 copy of
+# the iterate and restrict an fp32 copy of their residual: the same 18.6 PCG iterations, 18.93 ->
+# 19.74 ADMM it/s alternating in one call, profiles/r06d.  Colour SSOR on the fine level (smoother 4,
+# the reference's smoothing order) took 17.6 iterations at 59 instead of 50.6 ms, profiles/r06e.)
+HEADLINE_OPTIONS = dict(smoother=3, nu=2, omega=-1.7, iters_per_graph=4, warm_start=0, precond_fp32=4,
                         table_mode=0, coarse_level=-1)
 # ... for a rank that owns at most 4 subdomains (the 2-, 4- and 8-GPU runs of the same chain): a
 # colour launch then holds <= 1,600 chunks and the 17 fine-level launches per V-cycle are

@@ -1949,7 +1949,9 @@ void build_gs(GsFine& G, const LevelDev& L, int nsub, const std::vector<int64_t>
         const double rowf = 24.0 + (vt == kVal64 ? 72.0 : 36.0) + 24.0 + 4.0;
         std::vector<double> nl_k(K, 0.0), nu_k(K, 0.0), rows_k(K, 0.0), gx_f(K, 0.0), gx_b(K, 0.0);
         double gx_r = 0.0;
-        std::vector<int32_t> seen_f(L.nn, -1), seen_b(L.nn, -1), seen_r(L.nn, 0);
+        std::vector<int32_t> seen_f(L.nn, -1), seen_b(L.nn, -1), seen_r(L.nn, 0), seen_u(L.nn, -1), seen_l(L.nn, 0);
+        std::vector<double> gx_u(K, 0.0);
+        double gx_l = 0.0;
         for (int k = 0; k < K; ++k)
             for (int s = 0; s < nsub; ++s)
                 for (int64_t g : rows[(size_t)s * KG + k]) {
@@ -1961,9 +1963,11 @@ void build_gs(GsFine& G, const LevelDev& L, int nsub, const std::vector<int64_t>
                         if (colour[j] < k) {
                             nl_k[k] += 1.0;
                             if (seen_f[j] != k) seen_f[j] = k, gx_f[k] += 1.0;
+                            if (!seen_l[j]) seen_l[j] = 1, gx_l += 1.0;
                         } else {
                             nu_k[k] += 1.0;
                             if (!seen_r[j]) seen_r[j] = 1, gx_r += 1.0;
+                            if (seen_u[j] != k) seen_u[j] = k, gx_u[k] += 1.0;
                         }
                         if (seen_b[j] != k) seen_b[j] = k, gx_b[k] += 1.0;
                     }
@@ -1980,6 +1984,11 @@ void build_gs(GsFine& G, const LevelDev& L, int nsub, const std::vector<int64_t>
         G.gx_b = gx_b;
         G.rows_k = rows_k;
         G.gx_r = gx_r;
+        G.gx_u = gx_u;
+        G.gx_l = gx_l;
+        G.nl_k = nl_k;
+        G.nu_k = nu_k;
+        G.vb = vb;
     }
     G.ncol = K;
     G.nchunk = nch;
@@ -2595,11 +2604,6 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
     for (auto& L : lev) maxch = std::max<int64_t>(maxch, L.nch);
     partial.alloc(2 * maxch);
     if (gs_fine()) gs.partial.alloc(gs.nchunk);
-    if (gs_fine() && opt.smoother == 4) {
-        if (gs.band) throw ApiError(DDPCA_EINVAL, "colour SSOR (smoother 4) on a band-mode fine level");
-        gs.w.alloc(3 * lev.back().nn);
-        gs.w.zero(stream);
-    }
     if (gs_fine() && opt.precond_fp32 == 4 && !gs.band && lev.back().lat && lev.back().nrot == 0) {
         gs.x4.alloc(4 * lev.back().nn);
         gs.x4.zero(stream);
@@ -2610,15 +2614,37 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
             gs.r4.zero(stream);
         }
         // the per-launch byte model on the 16-B iterate: gathers 16 instead of 24 B per distinct
-        // node, the forward sweep writes 16 B per row, the backward sweep 16 + 24
-        const int K = gs.ncol;
+        // node, the forward sweep writes 16 B per row, the backward sweep 16 + 24 (colour SSOR
+        // builds its own model below)
+        const int K = opt.smoother == 3 ? gs.ncol : 0;
         for (int k = 0; k < K; ++k) {
             gs.launch_bytes[k] -= 8.0 * gs.gx_f[k] + 8.0 * gs.rows_k[k];
             gs.launch_bytes[2 * K - k] += -8.0 * gs.gx_b[k] + 16.0 * gs.rows_k[k];
         }
-        gs.launch_bytes[K] -= 8.0 * gs.gx_r;
+        if (K) gs.launch_bytes[K] -= 8.0 * gs.gx_r;
         if (gs.r4.p)
             for (int k = 0; k < K; ++k) gs.launch_bytes[K] -= 8.0 * gs.rows_k[k];  // r written in 16 B
+    }
+    if (gs_fine() && opt.smoother == 4) {
+        if (gs.band) throw ApiError(DDPCA_EINVAL, "colour SSOR (smoother 4) on a band-mode fine level");
+        gs.w.alloc(3 * lev.back().nn);
+        gs.w.zero(stream);
+        // the per-launch byte model in k_gs_ssor's launch order: forward colours 0..K-1 (L), backward
+        // K-1..0 (U), the residual (L, every chunk), forward 0..K-1 (L + U), backward K-1..0 (U); per
+        // row b, the fp32 inverse, w and x as each phase moves them, x gathered once per distinct node
+        const int K = gs.ncol;
+        const double xb = gs.x4.p ? 16.0 : 24.0, rb = gs.r4.p ? 16.0 : 24.0, m = 36.0, ix = 4.0;
+        std::vector<double> lb;
+        for (int k = 0; k < K; ++k) lb.push_back(gs.vb * gs.nl_k[k] + gs.rows_k[k] * (24 + m + xb + 24 + ix) + xb * gs.gx_f[k]);
+        for (int k = K - 1; k >= 0; --k) lb.push_back(gs.vb * gs.nu_k[k] + gs.rows_k[k] * (48 + m + xb + ix) + xb * gs.gx_u[k]);
+        double res = xb * gs.gx_l;
+        for (int k = 0; k < K; ++k) res += gs.vb * gs.nl_k[k] + gs.rows_k[k] * (24 + rb + ix);
+        lb.push_back(res);
+        for (int k = 0; k < K; ++k)
+            lb.push_back(gs.vb * (gs.nl_k[k] + gs.nu_k[k]) + gs.rows_k[k] * (24 + m + xb + 24 + ix) + xb * gs.gx_b[k]);
+        for (int k = K - 1; k >= 0; --k)
+            lb.push_back(gs.vb * gs.nu_k[k] + gs.rows_k[k] * (48 + m + 24 + (gs.x4.p ? xb : 0.0) + ix) + xb * gs.gx_u[k]);
+        gs.launch_bytes = lb;
     }
     sc.alloc(nsub);
     DDPCA_HIP(hipHostMalloc(reinterpret_cast<void**>(&sc_host), nsub * sizeof(PcgScal)));

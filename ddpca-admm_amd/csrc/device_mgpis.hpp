@@ -179,6 +179,8 @@ struct GsFine {
     std::vector<double> launch_bytes;
     std::vector<double> gx_f, gx_b, rows_k;  // per colour: distinct x gathered (forward, backward), rows
     double gx_r = 0.0;                       // distinct x the residual gathers
+    std::vector<double> gx_u, nl_k, nu_k;    // per colour: distinct U-side x gathered, L / U blocks
+    double gx_l = 0.0, vb = 0.0;             // distinct L-side x over all colours; bytes per stored block
     // band mode (locally refined fine level): the colours cover only the band -- the
     // nodes the fine level adds to the next coarser one and their neighbours; two more chunk groups
     // per member follow the colours: the ring (non-band rows with a band neighbour: their band

@@ -9,7 +9,11 @@
  * is owned by the handle.  Return 0 on success, a negative DDPCA_E* code on error; a positive
  * return from a solve is the iteration count when the iteration cap was reached.
  * Handles are independent: calls on different handles may run concurrently from different
- * host threads (the reference calls CG_SOLV concurrently per subdomain, MCONTACT.h:2511).
+ * host threads (the reference calls CG_SOLV concurrently per subdomain, MCONTACT.h:2511), creates
+ * included: every graph a handle replays is captured at its create, on the creating thread, under a
+ * process-wide capture lock that the library's synchronous allocations and copies also take, so a
+ * solve only replays (tests/test_mgpis_gpu.py::test_concurrent_cg_solv_bit_identical).  Calls on
+ * ONE handle are not to overlap.
  */
 #ifndef DDPCA_AMD_H
 #define DDPCA_AMD_H

@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--precond-fp32", type=int, default=None, help="override the option set's precond_fp32")
     ap.add_argument("--nu", type=int, default=None, help="override the option set's sweeps per level")
+    ap.add_argument("--smoother", type=int, default=None, help="override the option set's smoother")
     ap.add_argument("--options", choices=["auto", "headline", "small"], default="auto",
                     help="the option set: bench.py's choice by subdomains per rank, or force one")
     a = ap.parse_args()
@@ -53,6 +54,8 @@ def main():
             H["precond_fp32"] = a.precond_fp32
         if a.nu is not None:
             H["nu"] = a.nu
+        if a.smoother is not None:
+            H["smoother"] = a.smoother
         mc = D.MCONTACT(P, device=0, rank=r, nranks=world, owner=owner, **H)
         mc.comm_loopback()
         mc.CONTACT_ANALYSIS(a.warmup, check=False)

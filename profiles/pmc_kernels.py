@@ -35,6 +35,11 @@ N_F, N_C, NNZB = 3_278_600, 426_888, 86_119_688
 ALGO = {  # (kernel prefix, grid) -> algorithmic bytes per launch at the bench configuration
     ("k_sell<1,", 3278848): 22 * NNZB + 72 * N_F,
     ("k_sell<2,", 3278848): 22 * NNZB + 108 * N_F,
+    # precond_fp32 = 4 (round 6): the fine prolongation into the colour sweeps' fp32 iterate copy
+    # (4-B code, mask, 16 B read + written per fine node), the restriction from their fp32 residual
+    # (16 B per fine node): checked before the fp64 forms below (prefix match)
+    ("k_prolong_lat_x4", 3278848): 37 * N_F + 24 * N_C,
+    ("k_restrict_lat<true, true, false, float, HIP_vector_type", 427008): 16 * N_F + 93 * N_C,
     ("k_prolong_lat", 3278848): 53 * N_F + 24 * N_C,
     ("k_prolong<true>", 3278848): 53 * N_F + 24 * N_C,
     ("k_restrict_lat", 427008): 24 * N_F + 93 * N_C,

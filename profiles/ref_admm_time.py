@@ -204,6 +204,9 @@ def main():
     res.update(dev)
     res.update({"dof": ndof, "subdomains": nsub, "integration_points": nip, "dump_bytes": sz,
                 "cpu": _cpu(), "value": 1.0 / (sum(its) / len(its)), "unit": "ADMM it/s"})
+    sys.path.insert(0, str(ROOT))
+    import bench  # noqa: E402 -- the same host description as the bench line's
+    res["host_cores"] = bench.host_cpu()
     Path(a.out).write_text(json.dumps(res))
     _log(f"reference ADMM iterations: {[round(x, 2) for x in its]} s ({res['threads']} threads) -> {res['value']:.4f} it/s")
 
