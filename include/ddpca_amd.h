@@ -46,7 +46,12 @@ int ddpca_gpu_available(void);
 typedef struct ddpca_mgpis* mgpis_t;
 
 typedef struct {
-    int smoother;      /* 0 = damped point Jacobi, 1 = 3x3 node-block Jacobi, 2 = Chebyshev(deg) on block Jacobi */
+    int smoother;      /* 0 = damped point Jacobi, 1 = 3x3 node-block Jacobi, 2 = Chebyshev(deg) on block Jacobi,
+                          3 = multicolour block Gauss-Seidel on the fine level (forward before, backward after
+                          the coarse correction; band mode on a refined band) + nu block-Jacobi sweeps below,
+                          4 = as 3 with colour SSOR on the fine level (forward + backward before and after,
+                          the reference's MULT_VCYC order, MGPIS.h:64-76, 101-114; measured slower, A/B only).
+                          4 needs precond_fp32 >= 1 */
     int nu;            /* sweeps (Jacobi) or polynomial degree (Chebyshev) pre and post */
     double omega;      /* Jacobi damping; > 0: this value; 0: 4 / (3 lambda_max(M^-1 K)) estimated at
                           create per level and subdomain; < 0: -omega / lambda_max(M^-1 K)
@@ -63,7 +68,11 @@ typedef struct {
                           block) -- 24 instead of 40 B per block on the two fine smoother passes
                           of every PCG iteration.
                           3: as 2 with block-scaled int8 instead of fp16 (nine int8 and a scale
-                          = the block maximum / 127 per 3x3 block) -- 14 B per block. */
+                          = the block maximum / 127 per 3x3 block) -- 14 B per block.
+                          4: as 3, and with smoother 3 / 4 on lattice transfers the colour sweeps
+                          gather an fp32 stride-4 copy of the fine V-cycle iterate (one 16-B load
+                          per neighbour) and the fine restriction reads an fp32 copy of the
+                          residual; products, dot products and the V-cycle output stay fp64. */
     int table_mode;    /* levels >= 1: 0 stream every block value; 1 (default) when the rows'
                           block values deduplicate well (structured meshes), keep one copy per
                           distinct row in a cache-resident table and stream only column indices

@@ -2,7 +2,6 @@
 # r06h: evidence on the round's headline set (precond_fp32 = 4): PMC of the V-cycle's fine-level
 # transfers (pmc_kernels.py), the colour sweeps' per-launch table (gs_probe / gs_table.py), the
 # whole-step cross-check -- a one-stream kernel trace and PMC passes over every kernel of one ADMM
-# iteration (step_check.py) -- and one rank of the 2-, 4- and 8-rank layouts (one_rank_probe.py)
 set -eo pipefail
 export TMPDIR=/tmp
 OUT=gpurun_out/r06h
@@ -21,7 +20,5 @@ DDPCA_STREAMS=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace
 DDPCA_STREAMS=1 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch -o run --output-format csv -- $B > $OUT/pmc_fetch.json 2> $OUT/pmc_fetch.err
 DDPCA_STREAMS=1 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write -o run --output-format csv -- $B > $OUT/pmc_write.json 2> $OUT/pmc_write.err
 python3 profiles/step_check.py $(find $OUT/trace1 -name "*.db" | head -1) $OUT/trace1.json --fetch $(find $OUT/pmc_fetch -name "*counter_collection.csv" | head -1) --write $(find $OUT/pmc_write -name "*counter_collection.csv" | head -1) --pmc-bench $OUT/pmc_fetch.json --out $OUT/step_check.json > $OUT/step_check.log 2>&1 || true
-timeout -k 10 400 python3 -u profiles/one_rank_probe.py $OUT/one_rank.json --layouts 8:1,4:0,2:0 > $OUT/one_rank.log 2>&1
-timeout -k 10 300 python3 -u profiles/one_rank_probe.py $OUT/one_rank_headline.json --layouts 4:0,2:0 --options headline > $OUT/one_rank_headline.log 2>&1
 find $OUT -name "*.csv" -size +20M -delete || true
 find $OUT -name "*.db" -size +50M -delete || true

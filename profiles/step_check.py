@@ -18,7 +18,7 @@ in one of bench.py's phases by name, grid and position:
                             the fine level
   coarse_levels_and_scalars every other launch of the PCG (coarser levels, k_coarse, k_fin)
   coarse_space              launches between k_outp and the interface's first launch
-  mass_cg                   k_mcg_*, k_scal_*
+  mass_cg                   k_mcg_*, k_mcheb_* (the Chebyshev start), k_scal_*
   interface_rhs_monitor     the rest (copies, k_cpl, k_outp, gamma, projection, traction, norms)
 """
 from __future__ import annotations
@@ -76,7 +76,7 @@ def classify(it):
             continue
         elif stage == "cs" and n.startswith(IFACE_START):
             stage = "iface"
-        if n.startswith(("k_mcg", "k_scal")):
+        if n.startswith(("k_mcg", "k_mcheb", "k_scal")):
             out.append("mass_cg")
         elif stage == "pcg" and n.startswith(PCG):
             fine = (n.startswith(("k_sell", "k_jac0", "k_prolong", "k_axpy", "k_pcg_init")) and r[1] >= 0.5 * fine_grid) or \

@@ -202,7 +202,7 @@ def test_headline_fullsize_step_matches_oracle(ddpca, oracle, gpu):
         coarse["accuProl"].append(P.csr("accuProl", tv))
         print(f"  coarse operators of subdomain {tv}: globTran_D_1 {coarse['globTran_D_1'][-1].nnz} entries "
               f"({time.time() - t0:.0f} s)", flush=True)
-    res = oracle.admm(subs, ifaces, maxit=1, check=False, coarse=coarse, init=init, body_only=True, workers=4)
+    res = oracle.admm(subs, ifaces, maxit=1, check=False, coarse=coarse, init=init, body_only=True, workers=8)
     eu = [np.linalg.norm(ud[tv] - res["u"][tv]) / np.linalg.norm(res["u"][tv]) for tv in range(P.nsub)]
     assert all(np.linalg.norm(res["u"][tv]) > 0 for tv in range(P.nsub))
     print(f"full size, ADMM iteration 4 from the device's iterate 3 ({time.time() - t0:.0f} s): device PCG its {its}; "
