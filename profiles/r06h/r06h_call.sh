@@ -2,6 +2,7 @@
 # r06h: evidence on the round's headline set (precond_fp32 = 4): PMC of the V-cycle's fine-level
 # transfers (pmc_kernels.py), the colour sweeps' per-launch table (gs_probe / gs_table.py), the
 # whole-step cross-check -- a one-stream kernel trace and PMC passes over every kernel of one ADMM
+# iteration (step_check.py); one rank per layout is r06i
 set -eo pipefail
 export TMPDIR=/tmp
 OUT=gpurun_out/r06h
