@@ -159,10 +159,15 @@ struct MirrorBuf {
 // solves' expected count), single iterations are queued two ahead of the slowest solve instead.
 int64_t pace_until_done(hipStream_t stream, hipGraphExec_t graph, const MirrorBuf& m, int64_t k, int64_t launched,
                         hipGraphExec_t graph1 = nullptr, int64_t horizon = INT64_MAX);
-// the same for a batch split into two halves (half[s] = 0 or 1), each half's graph on its stream
-// (g1 / horizon: per half, or null)
-int64_t pace_halves(hipStream_t st[2], hipGraphExec_t g[2], const MirrorBuf& m, const std::vector<int>& half, int64_t k,
-                    int64_t launched0, hipGraphExec_t* g1 = nullptr, const int64_t* horizon = nullptr);
+// the same for a batch split into np parts (part[s] in 0 .. np-1, np <= kMaxParts), each part's
+// graph on its stream (g1 / horizon: per part, or null); pace_halves: np = 2
+constexpr int kMaxParts = 4;
+int64_t pace_parts(int np, hipStream_t* st, hipGraphExec_t* g, const MirrorBuf& m, const std::vector<int>& part, int64_t k,
+                   int64_t launched0, hipGraphExec_t* g1 = nullptr, const int64_t* horizon = nullptr);
+inline int64_t pace_halves(hipStream_t st[2], hipGraphExec_t g[2], const MirrorBuf& m, const std::vector<int>& half, int64_t k,
+                           int64_t launched0, hipGraphExec_t* g1 = nullptr, const int64_t* horizon = nullptr) {
+    return pace_parts(2, st, g, m, half, k, launched0, g1, horizon);
+}
 
 // rocSOLVER / rocBLAS from several host threads of one process (the in-process ranks of the
 // multi-rank tests) gave non-deterministic potrf failures on the very same matrix (TORSION on 4

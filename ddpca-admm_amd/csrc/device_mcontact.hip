@@ -1738,8 +1738,9 @@ void build(ddpca_mcontact& H, Problem& P) {
         H.mg = std::make_unique<MgpisDevice>(H.device, ops, H.opt);
         H.main = H.mg->stream;
         // the body balance's batch on two streams (MgpisDevice::set_split); DDPCA_STREAMS=1 keeps
-        // the single-stream graph for A/B runs
-        H.mg->set_split(two_streams());
+        // the single-stream graph, DDPCA_PCG_STREAMS=3 / 4 splits it three / four ways (A/B runs)
+        const char* ps = std::getenv("DDPCA_PCG_STREAMS");
+        H.mg->set_split(two_streams(), ps ? std::max(2, std::min(kMaxParts, std::atoi(ps))) : 2);
     } else {
         DDPCA_HIP(hipStreamCreateWithFlags(&H.main, hipStreamNonBlocking));
     }

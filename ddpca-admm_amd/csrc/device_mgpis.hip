@@ -2673,17 +2673,20 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
 MgpisDevice::~MgpisDevice() {
     (void)hipSetDevice(device);
     if (stream) (void)hipStreamSynchronize(stream);
-    if (stream2_) (void)hipStreamSynchronize(stream2_);
+    for (hipStream_t xs : xstream_)
+        if (xs) (void)hipStreamSynchronize(xs);
     for (auto* ga : {graph_, graph1_})
         for (int p = 0; p < 2; ++p)
             if (ga[p]) (void)hipGraphExecDestroy(ga[p]);
     for (auto* gh : {graph_h_, graph1_h_})
         for (int p = 0; p < 2; ++p)
-            for (int h = 0; h < 2; ++h)
+            for (int h = 0; h < kMaxParts; ++h)
                 if (gh[p][h]) (void)hipGraphExecDestroy(gh[p][h]);
     if (ev_fork_) (void)hipEventDestroy(ev_fork_);
-    if (ev_join_) (void)hipEventDestroy(ev_join_);
-    if (stream2_) (void)hipStreamDestroy(stream2_);
+    for (hipEvent_t e : ev_join_)
+        if (e) (void)hipEventDestroy(e);
+    for (hipStream_t xs : xstream_)
+        if (xs) (void)hipStreamDestroy(xs);
     if (sc_host) (void)hipHostFree(sc_host);
     if (ev_k0) (void)hipEventDestroy(ev_k0);
     if (ev_k1) (void)hipEventDestroy(ev_k1);
@@ -3446,8 +3449,7 @@ hipGraphExec_t MgpisDevice::capture_iterations(int prec, int count, PcgScal* scp
 
 void MgpisDevice::build_graph(int prec) {
     if (split_) {
-        build_half_graph(prec, 0);
-        build_half_graph(prec, 1);
+        for (int h = 0; h < nparts_; ++h) build_half_graph(prec, h);
         return;
     }
     if (graph_[prec]) return;
@@ -3476,11 +3478,11 @@ int64_t MgpisDevice::horizon(int prec, int half) const {
     return h;
 }
 
-// scs[h][s] = sc[s], with done forced on the members of the other half
-__global__ void k_split_sc(const PcgScal* sc, PcgScal* scs, const int32_t* half, int nsub) {
+// scs[h][s] = sc[s], with done forced on the members of the other parts
+__global__ void k_split_sc(const PcgScal* sc, PcgScal* scs, const int32_t* half, int nsub, int np) {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= nsub) return;
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < np; ++h) {
         PcgScal v = sc[s];
         if (half[s] != h) v.done = 1;
         scs[h * nsub + s] = v;
@@ -3493,24 +3495,33 @@ __global__ void k_merge_sc(PcgScal* sc, const PcgScal* scs, const int32_t* half,
     if (s < nsub) sc[s] = scs[half[s] * nsub + s];
 }
 
-void MgpisDevice::set_split(bool on) {
+void MgpisDevice::set_split(bool on, int parts) {
     select_device(device);
+    if (on && (parts < 2 || parts > kMaxParts)) throw ApiError(DDPCA_EINVAL, "set_split: 2 .. 4 parts");
+    parts = std::min<int>(parts, (int)nsub);
     on = on && nsub >= 2 && !no_coarse;
-    if (on == split_) return;
+    if (on == split_ && (!on || parts == nparts_)) return;
+    if (split_ && on) throw ApiError(DDPCA_ESTATE, "set_split: the part count is fixed once split");
     DDPCA_HIP(hipStreamSynchronize(stream));
-    if (on && !stream2_) {
-        DDPCA_HIP(hipStreamCreateWithFlags(&stream2_, hipStreamNonBlocking));
+    if (on && !xstream_[0]) {
+        nparts_ = parts;
+        for (int h = 0; h + 1 < parts; ++h) {
+            DDPCA_HIP(hipStreamCreateWithFlags(&xstream_[h], hipStreamNonBlocking));
+            DDPCA_HIP(hipEventCreateWithFlags(&ev_join_[h], hipEventDisableTiming));
+        }
         DDPCA_HIP(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
-        DDPCA_HIP(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
-        sc_half_.alloc(2 * nsub);
-        // deal the members into two halves of equal fine-level work (largest first)
+        sc_half_.alloc((size_t)parts * nsub);
+        // deal the members into parts of equal fine-level work (largest first, to the lightest
+        // part; the lower part index on ties)
         std::vector<int> ord(nsub);
         for (int s = 0; s < nsub; ++s) ord[s] = s;
         std::stable_sort(ord.begin(), ord.end(), [&](int x, int y) { return lev.back().nnzb_sub[x] > lev.back().nnzb_sub[y]; });
         half_host_.assign(nsub, 0);
-        double w[2] = {0.0, 0.0};
+        double w[kMaxParts] = {0.0, 0.0, 0.0, 0.0};
         for (int s : ord) {
-            const int h = w[1] < w[0] ? 1 : 0;
+            int h = 0;
+            for (int q = 1; q < parts; ++q)
+                if (w[q] < w[h]) h = q;
             half_host_[s] = h;
             w[h] += (double)lev.back().nnzb_sub[s];
         }
@@ -3519,26 +3530,28 @@ void MgpisDevice::set_split(bool on) {
     split_ = on;
 }
 
-// Host pacing of the two halves' replays (pace_until_done per half, one loop): a half gets its
-// next replay when its slowest member has entered the last one enqueued for it.
-int64_t pace_halves(hipStream_t st[2], hipGraphExec_t g[2], const MirrorBuf& m, const std::vector<int>& half, int64_t k,
-                    int64_t launched0, hipGraphExec_t* g1, const int64_t* horizon) {
+// Host pacing of the parts' replays (pace_until_done per part, one loop): a part gets its next
+// replay when its slowest member has entered the last one enqueued for it.
+int64_t pace_parts(int np, hipStream_t* st, hipGraphExec_t* g, const MirrorBuf& m, const std::vector<int>& part, int64_t k,
+                   int64_t launched0, hipGraphExec_t* g1, const int64_t* horizon) {
     constexpr int64_t kRunway = 2;
-    int64_t launched[2] = {launched0, launched0}, replays = 0;
+    if (np < 1 || np > kMaxParts) throw ApiError(DDPCA_EINVAL, "pace_parts: part count");
+    int64_t launched[kMaxParts], replays = 0;
+    for (int h = 0; h < np; ++h) launched[h] = launched0;
     for (int64_t spin = 0;; ++spin) {
         bool all = true;
-        int64_t slowest[2] = {INT64_MAX, INT64_MAX};
-        bool busy[2] = {false, false};
+        int64_t slowest[kMaxParts];
+        bool busy[kMaxParts], tail[kMaxParts];
+        for (int h = 0; h < np; ++h) slowest[h] = INT64_MAX, busy[h] = false;
         for (int s = 0; s < m.n; ++s) {
             if (__atomic_load_n(&m.host[s].done, __ATOMIC_ACQUIRE)) continue;
             all = false;
-            busy[half[s]] = true;
-            slowest[half[s]] = std::min<int64_t>(slowest[half[s]], __atomic_load_n(&m.host[s].iter, __ATOMIC_RELAXED));
+            busy[part[s]] = true;
+            slowest[part[s]] = std::min<int64_t>(slowest[part[s]], __atomic_load_n(&m.host[s].iter, __ATOMIC_RELAXED));
         }
         if (all) return replays;
         bool launched_now = false;
-        bool tail[2];
-        for (int h = 0; h < 2; ++h) {
+        for (int h = 0; h < np; ++h) {
             tail[h] = g1 && horizon && g1[h] && launched[h] + k > horizon[h];
             if (busy[h] && (tail[h] ? launched[h] - slowest[h] <= kRunway : launched[h] - slowest[h] <= k)) {
                 DDPCA_HIP(hipGraphLaunch(tail[h] ? g1[h] : g[h], st[h]));
@@ -3549,14 +3562,14 @@ int64_t pace_halves(hipStream_t st[2], hipGraphExec_t g[2], const MirrorBuf& m, 
         }
         if (launched_now) continue;
         if ((spin & 255) == 255) {
-            for (int h = 0; h < 2; ++h) {
+            for (int h = 0; h < np; ++h) {
                 if (!busy[h]) continue;
                 const hipError_t q = hipStreamQuery(st[h]);
                 if (q == hipSuccess) {
-                    // this half's stream drained: its mirror entries are final for what it ran
+                    // this part's stream drained: its mirror entries are final for what it ran
                     bool done_now = true;
                     for (int s = 0; s < m.n; ++s)
-                        if (half[s] == h) done_now &= __atomic_load_n(&m.host[s].done, __ATOMIC_ACQUIRE) != 0;
+                        if (part[s] == h) done_now &= __atomic_load_n(&m.host[s].done, __ATOMIC_ACQUIRE) != 0;
                     if (!done_now) {
                         DDPCA_HIP(hipGraphLaunch(tail[h] ? g1[h] : g[h], st[h]));
                         launched[h] += tail[h] ? 1 : k;
@@ -3614,17 +3627,17 @@ void MgpisDevice::pcg_begin(int prec, double rtol, const std::vector<int64_t>& m
     }
     if (split_) {
         // fork: each half continues on its own stream from its own copy of the scalars
-        hipLaunchKernelGGL(k_split_sc, dim3(ceil_div(nsub, 64)), dim3(64), 0, stream, sc.p, sc_half_.p, half_.p, nsub);
+        hipLaunchKernelGGL(k_split_sc, dim3(ceil_div(nsub, 64)), dim3(64), 0, stream, sc.p, sc_half_.p, half_.p, nsub,
+                           nparts_);
         DDPCA_HIP(hipEventRecord(ev_fork_, stream));
-        DDPCA_HIP(hipStreamWaitEvent(stream2_, ev_fork_, 0));
+        for (int h = 1; h < nparts_; ++h) DDPCA_HIP(hipStreamWaitEvent(part_stream(h), ev_fork_, 0));
     }
 }
 
 void MgpisDevice::pcg_step(int prec) {
     if (split_) {
-        DDPCA_HIP(hipGraphLaunch(graph_h_[prec][0], stream));
-        DDPCA_HIP(hipGraphLaunch(graph_h_[prec][1], stream2_));
-        graphs_launched += 2;
+        for (int h = 0; h < nparts_; ++h) DDPCA_HIP(hipGraphLaunch(graph_h_[prec][h], part_stream(h)));
+        graphs_launched += nparts_;
         return;
     }
     DDPCA_HIP(hipGraphLaunch(graph_[prec], stream));
@@ -3635,14 +3648,15 @@ void MgpisDevice::pcg_wait(int prec, int64_t pre_enqueued) {
     const int64_t k = opt.iters_per_graph;
     const int64_t launched = (sample_pending_ ? 1 : 0) + pre_enqueued * k;
     if (split_) {
-        hipStream_t st[2] = {stream, stream2_};
-        hipGraphExec_t g[2] = {graph_h_[prec][0], graph_h_[prec][1]};
-        hipGraphExec_t g1[2] = {graph1_h_[prec][0], graph1_h_[prec][1]};
-        const int64_t hz[2] = {horizon(prec, 0), horizon(prec, 1)};
-        graphs_launched += pace_halves(st, g, mirror, half_host_, k, launched, g1, hz);
-        // join: `stream` continues after the second half's replays; the scalars merge back
-        DDPCA_HIP(hipEventRecord(ev_join_, stream2_));
-        DDPCA_HIP(hipStreamWaitEvent(stream, ev_join_, 0));
+        hipStream_t st[kMaxParts];
+        int64_t hz[kMaxParts];
+        for (int h = 0; h < nparts_; ++h) st[h] = part_stream(h), hz[h] = horizon(prec, h);
+        graphs_launched += pace_parts(nparts_, st, graph_h_[prec], mirror, half_host_, k, launched, graph1_h_[prec], hz);
+        // join: `stream` continues after the other parts' replays; the scalars merge back
+        for (int h = 1; h < nparts_; ++h) {
+            DDPCA_HIP(hipEventRecord(ev_join_[h - 1], part_stream(h)));
+            DDPCA_HIP(hipStreamWaitEvent(stream, ev_join_[h - 1], 0));
+        }
         hipLaunchKernelGGL(k_merge_sc, dim3(ceil_div(nsub, 64)), dim3(64), 0, stream, sc.p, sc_half_.p, half_.p, nsub);
         return;
     }

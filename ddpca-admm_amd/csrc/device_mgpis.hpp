@@ -315,29 +315,32 @@ public:
     // done members), so the two graphs touch disjoint chunks; pcg_wait joins the streams and
     // merges the copies back into `sc`.  Setup and the eagerly timed first iteration stay on
     // `stream` over the whole batch.
-    void set_split(bool on);
+    // parts > 2 (DDPCA_PCG_STREAMS=n): the same with n parts on n streams (A/B)
+    void set_split(bool on, int parts = 2);
     bool split() const { return split_; }
     // capture the PCG graphs of preconditioner prec now (create time) instead of at the first solve
     void prepare_graphs(int prec) { build_graph(prec); }
 
 private:
     hipGraphExec_t graph_[2] = {nullptr, nullptr};
-    hipGraphExec_t graph_h_[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};  // [prec][half]
+    hipGraphExec_t graph_h_[2][kMaxParts] = {};  // [prec][part]
     // one-iteration graphs for the tail of a solve: once the queued iterations reach the members'
     // expected count (their previous solve's, expect_[prec]), the host queues single iterations
     // two ahead of the slowest member instead of whole replays, so at most two iterations of
     // launches run after the last member converged (a replay of iters_per_graph left up to
     // ~1.5 k over, every launch of it dispatching its full grid to exit at once)
     hipGraphExec_t graph1_[2] = {nullptr, nullptr};
-    hipGraphExec_t graph1_h_[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
+    hipGraphExec_t graph1_h_[2][kMaxParts] = {};
     std::vector<int64_t> expect_[2];
     int last_prec_ = -1;
     int64_t horizon(int prec, int half) const;  // max expected iterations (half -1: all members), INT64_MAX unknown
     bool split_ = false;
-    hipStream_t stream2_ = nullptr;
-    hipEvent_t ev_fork_ = nullptr, ev_join_ = nullptr;
-    DevBuf<PcgScal> sc_half_;   // 2 x nsub: the scalars each half's graph runs on
-    DevBuf<int32_t> half_;      // per member: its half
+    int nparts_ = 1;                          // parts of the split batch (2: the halves)
+    hipStream_t xstream_[kMaxParts - 1] = {};  // part h >= 1 replays on xstream_[h - 1], part 0 on `stream`
+    hipStream_t part_stream(int h) const { return h == 0 ? stream : xstream_[h - 1]; }
+    hipEvent_t ev_fork_ = nullptr, ev_join_[kMaxParts - 1] = {};
+    DevBuf<PcgScal> sc_half_;   // nparts_ x nsub: the scalars each part's graph runs on
+    DevBuf<int32_t> half_;      // per member: its part
     std::vector<int> half_host_;
     PcgScal* sc_cur_ = nullptr; // the scalars enqueue_iteration / vcycle bind (sc, or a half's copy)
     void build_half_graph(int prec, int h);

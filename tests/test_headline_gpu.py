@@ -213,8 +213,10 @@ def test_headline_fullsize_step_matches_oracle(ddpca, oracle, gpu):
 @pytest.mark.parametrize("env,opts", [(("DDPCA_STREAMS", "1"), "HEADLINE_OPTIONS"),
                                       (("DDPCA_STREAMS", "1"), "HEADLINE_OPTIONS_SMALL"),
                                       (("DDPCA_TAIL_PACING", "0"), "HEADLINE_OPTIONS"),
-                                      (("DDPCA_MCG_PAIR", "0"), "HEADLINE_OPTIONS")],
-                         ids=["one-stream", "one-stream-small", "whole-replay-pacing", "unpaired-mass-spmv"])
+                                      (("DDPCA_MCG_PAIR", "0"), "HEADLINE_OPTIONS"),
+                                      (("DDPCA_PCG_STREAMS", "4"), "HEADLINE_OPTIONS")],
+                         ids=["one-stream", "one-stream-small", "whole-replay-pacing", "unpaired-mass-spmv",
+                              "four-part-split"])
 def test_schedule_variants_are_bit_identical(ddpca, gpu, monkeypatch, env, opts):
     """Schedule-only variants of the headline path must not change a bit: the two-stream split of
     the body-balance batch and of the mass CG (MgpisDevice / MassBatch ::set_split, default on)
