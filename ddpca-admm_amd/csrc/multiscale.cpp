@@ -310,35 +310,109 @@ Csr fold_cols(const Csr& H, const std::vector<int64_t>& f2d, const Csr& A) {
 }
 
 // Rc A = realProl[d]^T ... realProl[L-1]^T A for A with rows = free dofs of level L
-// (MCONTACT.h:1883-1885, 2017-2019, 2116-2118, 2269-2271): scatter form, touching only A's
-// nonempty rows (surface operators); prolOper's block entries as 3x3 blocks
+// (MCONTACT.h:1883-1885, 2017-2019, 2116-2118, 2269-2271), touching only A's nonempty rows (surface
+// operators); prolOper's block entries as 3x3 blocks.  Gather form: every coarse row lists its
+// (fine row, weight) children in the order the scatter form appended them (fine row ascending,
+// stencil entry, block row) and sums w * A[r, :] into a dense accumulator in that order -- per entry
+// the same additions in the same order as from_triplets over the scattered triplets, so the same
+// bits, without the triplet array (≈ 3.4 triplets per stored entry of A: 8 GB and a stable sort
+// for a 1.2M-dof subdomain's consStif, the full globTran_D_1 of the tests), rows in parallel.
 Csr restrict_chain(const MULTIGRID& g, int64_t d, const std::vector<int64_t>& f2d, Csr A) {
     const std::vector<Stencil>& P = !g.prolOper.empty() ? g.prolOper : g.scalProl;
     for (int64_t l = g.maxiLeve - 1; l >= d; --l) {
         const Stencil& S = P[l];
         const std::vector<int64_t> bo = block_of(S);
-        std::vector<Trip> t;
-        for (int64_t r = 0; r < A.nrow; ++r) {
-            if (A.ptr[r] == A.ptr[r + 1]) continue;
-            const int64_t dof = f2d[r];  // free row r of level l+1 -> nodal dof
-            const int64_t n = dof / 3, a = dof % 3;
-            for (int64_t s = S.ptr[n]; s < S.ptr[n + 1]; ++s) {
-                const int64_t cn = S.col[s];
-                if (bo[s] >= 0) {
-                    for (int b = 0; b < 3; ++b) {
-                        const int32_t c = g.freeIndex[3 * cn + b];
-                        const double w = S.bval[9 * bo[s] + 3 * a + b];
-                        if (c < 0 || w == 0.0) continue;
-                        for (int64_t k = A.ptr[r]; k < A.ptr[r + 1]; ++k) t.push_back({c, A.col[k], w * A.val[k]});
+        const int64_t nc = g.freeCount[l];
+        // the children of every coarse row, in the scatter form's order
+        auto visit = [&](auto&& emit) {
+            for (int64_t r = 0; r < A.nrow; ++r) {
+                if (A.ptr[r] == A.ptr[r + 1]) continue;
+                const int64_t dof = f2d[r];  // free row r of level l+1 -> nodal dof
+                const int64_t n = dof / 3, a = dof % 3;
+                for (int64_t s = S.ptr[n]; s < S.ptr[n + 1]; ++s) {
+                    const int64_t cn = S.col[s];
+                    if (bo[s] >= 0) {
+                        for (int b = 0; b < 3; ++b) {
+                            const int32_t c = g.freeIndex[3 * cn + b];
+                            const double w = S.bval[9 * bo[s] + 3 * a + b];
+                            if (c < 0 || w == 0.0) continue;
+                            emit(c, r, w);
+                        }
+                    } else {
+                        const int32_t c = g.freeIndex[3 * cn + a];
+                        if (c < 0) continue;  // realProl keeps free coarse columns only
+                        emit(c, r, S.w[s]);
                     }
-                } else {
-                    const int32_t c = g.freeIndex[3 * cn + a];
-                    if (c < 0) continue;  // realProl keeps free coarse columns only
-                    for (int64_t k = A.ptr[r]; k < A.ptr[r + 1]; ++k) t.push_back({c, A.col[k], S.w[s] * A.val[k]});
+                }
+            }
+        };
+        std::vector<int64_t> start(nc + 1, 0);
+        visit([&](int64_t c, int64_t, double) {
+            if (c >= nc) throw std::logic_error("MULTISCALE: restriction row out of range");
+            ++start[c + 1];
+        });
+        for (int64_t c = 0; c < nc; ++c) start[c + 1] += start[c];
+        std::vector<int64_t> cr(start[nc]);
+        std::vector<double> cw(start[nc]);
+        {
+            std::vector<int64_t> pos(start.begin(), start.end() - 1);
+            visit([&](int64_t c, int64_t r, double w) {
+                cr[pos[c]] = r;
+                cw[pos[c]++] = w;
+            });
+        }
+        std::vector<std::vector<int32_t>> rcol(nc);
+        std::vector<std::vector<double>> rval(nc);
+        // (called inside the subdomain-parallel loops too, where this region runs on one thread:
+        // the accumulator is per thread and kept across calls, its marks cleared row by row)
+#pragma omp parallel
+        {
+            thread_local std::vector<double> acc;
+            thread_local std::vector<uint8_t> mark;
+            if ((int64_t)acc.size() < A.ncol) {
+                acc.resize(A.ncol, 0.0);
+                mark.resize(A.ncol, 0);
+            }
+            std::vector<int32_t> touched;
+#pragma omp for schedule(dynamic, 64)
+            for (int64_t c = 0; c < nc; ++c) {
+                touched.clear();
+                for (int64_t q = start[c]; q < start[c + 1]; ++q) {
+                    const int64_t r = cr[q];
+                    const double w = cw[q];
+                    for (int64_t k = A.ptr[r]; k < A.ptr[r + 1]; ++k) {
+                        const int32_t j = A.col[k];
+                        const double t = w * A.val[k];  // rounded on its own, as the triplet's value
+                        if (!mark[j]) {
+                            mark[j] = 1;
+                            acc[j] = 0.0;
+                            touched.push_back(j);
+                        }
+                        acc[j] += t;
+                    }
+                }
+                std::sort(touched.begin(), touched.end());
+                rcol[c].assign(touched.begin(), touched.end());
+                rval[c].resize(touched.size());
+                for (size_t i = 0; i < touched.size(); ++i) {
+                    rval[c][i] = acc[touched[i]];
+                    mark[touched[i]] = 0;
                 }
             }
         }
-        A = from_triplets(g.freeCount[l], A.ncol, t);
+        Csr R;
+        R.nrow = nc;
+        R.ncol = A.ncol;
+        R.ptr.assign(nc + 1, 0);
+        for (int64_t c = 0; c < nc; ++c) R.ptr[c + 1] = R.ptr[c] + (int64_t)rcol[c].size();
+        R.col.resize(R.ptr[nc]);
+        R.val.resize(R.ptr[nc]);
+#pragma omp parallel for schedule(static)
+        for (int64_t c = 0; c < nc; ++c) {
+            std::copy(rcol[c].begin(), rcol[c].end(), R.col.begin() + R.ptr[c]);
+            std::copy(rval[c].begin(), rval[c].end(), R.val.begin() + R.ptr[c]);
+        }
+        A = std::move(R);
     }
     return A;
 }

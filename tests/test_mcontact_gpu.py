@@ -441,9 +441,35 @@ def test_block_patch_pressure_known_answer(gpu, tmp_path, musc):
             assert abs(itf[k] - 1e7) <= 1e-5 * 1e7, (musc, itf)
 
 
-@pytest.mark.parametrize("native,mcol", [(False, False), (True, False), (True, True)],
+@pytest.fixture(scope="module")
+def cylinder_runs(gpu, tmp_path_factory):
+    """The reference's CYLINDER solved once (oracle/ref_cylinder.cpp) and the device run on it three
+    times: on the reference's operators, on the library's own, and on the library's own with the
+    headline V-cycle -- one JSON line per variant -- plus, on the reference's operators, the two-rank
+    comparisons of both owner layouts (the reference's mesh, contact search, ESTABLISH and
+    CONTACT_ANALYSIS are the expensive part; the five tests share them)."""
+    import json
+    import os
+    import subprocess
+    from pathlib import Path
+    exe = Path(__file__).resolve().parents[1] / "oracle" / "_ref" / "ref_cylinder"
+    if not exe.exists():
+        pytest.skip("oracle/_ref/ref_cylinder is built only where the reference is (travels with the snapshot)")
+    env = {k: v for k, v in os.environ.items() if k != "DDPCA_REF_OPTIONS"}
+    out = subprocess.run([str(exe), "1", "4", "2", "2e-4", "ref,native,native-mc", "0101,0011"], capture_output=True,
+                         text=True, timeout=400, env=env, cwd=tmp_path_factory.mktemp("cylinder"))
+    assert out.returncode == 0, out.stderr[-2000:]
+    runs = {}
+    for line in out.stderr.strip().splitlines():
+        if line.startswith("{"):
+            r = json.loads(line)
+            runs[r["variant"]] = r
+    return runs
+
+
+@pytest.mark.parametrize("variant", ["ref", "native", "native-mc"],
                          ids=["reference-operators", "native-operators", "native-multicolour"])
-def test_cylinder_known_answer(gpu, tmp_path, native, mcol):
+def test_cylinder_known_answer(cylinder_runs, variant):
     """native: every subdomain's MGPIS hierarchy, consForc and hanging rows come from the library's
     own pipeline on the reference's element trees (ddpca_multigrid_*: TRANSFER with the hanging
     level, PATCH, STIF_MATR + the contact systMass, CONSTRAINT(1)) instead of the
@@ -459,21 +485,10 @@ def test_cylinder_known_answer(gpu, tmp_path, native, mcol):
     k <= 50 (1e-7) and the contact pressures of its last resuCont files (1e-5 of the peak).
     native-multicolour: the same with the headline's V-cycle (colour Gauss-Seidel on the fine level,
     in band mode where that level refines a band: GsFine::band) -- the preconditioner differs from
-    the reference's SGS, the answers may not."""
-    import json
-    import os
-    import subprocess
-    from pathlib import Path
-    exe = Path(__file__).resolve().parents[1] / "oracle" / "_ref" / "ref_cylinder"
-    if not exe.exists():
-        pytest.skip("oracle/_ref/ref_cylinder is built only where the reference is (travels with the snapshot)")
-    env = dict(os.environ)
-    if mcol:
-        env["DDPCA_REF_OPTIONS"] = "multicolour"
-    out = subprocess.run([str(exe), "1", "4", "2", "2e-4"] + (["native"] if native else []), capture_output=True,
-                         text=True, timeout=170, env=env, cwd=tmp_path)
-    assert out.returncode == 0, out.stderr[-2000:]
-    res = json.loads(out.stderr.strip().splitlines()[-1])
+    the reference's SGS, the answers may not.  The three variants share one reference run
+    (cylinder_runs)."""
+    native, mcol = variant.startswith("native"), variant.endswith("-mc")
+    res = cylinder_runs[variant]
     print(res)
     assert res["hanging_nodes"] > 0, res
     assert res["native"] == native and res["K_rel"] <= 1e-13, res
@@ -487,7 +502,7 @@ def test_cylinder_known_answer(gpu, tmp_path, native, mcol):
 
 
 @pytest.mark.parametrize("owners", ["0101", "0011"])
-def test_cylinder_two_ranks_in_one_process(gpu, tmp_path, owners):
+def test_cylinder_two_ranks_in_one_process(cylinder_runs, owners):
     """The locally refined path across ranks (MCONTACT.h:2511-2537, 2539-2576): the reference's
     CYLINDER_1 (hanging level, curved contacts, LATIN coarse space) on two device ranks of one
     process connected by the in-process transport (mcontact_gpu_comm_local).  0101: cylinders
@@ -500,21 +515,11 @@ def test_cylinder_two_ranks_in_one_process(gpu, tmp_path, owners):
     level pinned: its automatic choice depends on the subdomains per rank, which moved the rows by
     1.1e-7 in r03c): the same iteration count on both ranks, resuMoni rows within SURVEY §8 c4's
     1e-7 (relative, floor 1e-12 of the column), displacements 1e-8, contact tractions 1e-7 of the
-    largest.  The reference builds the problem but skips its own CONTACT_ANALYSIS ("noref": the
+    largest.  The comparison runs on the reference's operators inside cylinder_runs' process (the
     single-rank answers against the reference are test_cylinder_known_answer's)."""
-    import json
-    import os
-    import subprocess
-    from pathlib import Path
-    exe = Path(__file__).resolve().parents[1] / "oracle" / "_ref" / "ref_cylinder"
-    if not exe.exists():
-        pytest.skip("oracle/_ref/ref_cylinder is built only where the reference is (travels with the snapshot)")
-    out = subprocess.run([str(exe), "1", "4", "2", "2e-4", "ref", owners, "noref"], capture_output=True, text=True,
-                         timeout=240, env=dict(os.environ), cwd=tmp_path)
-    assert out.returncode == 0, out.stderr[-2000:]
-    res = json.loads(out.stderr.strip().splitlines()[-1])
-    print(res["ranks2"])
-    r2 = res["ranks2"]
+    res = cylinder_runs["ref"]
+    print(res["ranks2"][owners])
+    r2 = res["ranks2"][owners]
     assert r2["cross_interfaces"] == (1 if owners == "0011" else 3), r2
     assert r2["iters"] == [r2["iters_1rank"], r2["iters_1rank"]] and r2["iters_1rank"] > 1, r2
     # resuMoni: every column at SURVEY c4's 1e-7 (round 5 needed 1e-6 on the successive-difference
