@@ -251,8 +251,8 @@ def main():
                                             3: f"fp32, the {os.environ.get('DDPCA_H16_LEVELS', '3')} finest levels "
                                                "block-scaled int8",
                                             4: f"fp32, the {os.environ.get('DDPCA_H16_LEVELS', '3')} finest levels "
-                                               "block-scaled int8; the fine colour sweeps gather an fp32 copy "
-                                               "of the iterate"}[a.precond_fp32],
+                                               "block-scaled int8; the sweeps (fine colour sweeps, block-Jacobi "
+                                               "levels) gather fp32 copies of the iterate"}[a.precond_fp32],
                 "operator_rows": "deduplicated table" if a.table_mode else "streamed",
                 "coarse_space": f"interface-eliminated (muscSett={a.musc}, doleMcsc={a.dole})" if a.musc else "none",
                 **({"hanging_dofs": int(sum(P.grid(tv).hangRows().shape[0] for tv in range(nsub) if owner[tv] == rank)),

@@ -60,8 +60,10 @@ class MgpisOptions(C.Structure):
 # of 18.0 PCG iterations, +6 % ADMM it/s, the one-subdomain rank -7.5 %, profiles/r05r.  Round 6:
 # precond_fp32 = 4 -- the same int8 copies, and the fine colour sweeps gather an fp32 stride-4 copy of
 # the iterate and restrict an fp32 copy of their residual: the same 18.6 PCG iterations, 18.93 ->
-# 19.74 ADMM it/s alternating in one call, profiles/r06d.  Colour SSOR on the fine level (smoother 4,
-# the reference's smoothing order) took 17.6 iterations at 59 instead of 50.6 ms, profiles/r06e.)
+# 19.74 ADMM it/s alternating in one call, profiles/r06d; the block-Jacobi levels below on fp32
+# iterate copies too: 19.73 -> 20.05 ADMM it/s, the N = 8 rank 9.52 -> 9.00 ms, profiles/r06n.
+# Colour SSOR on the fine level (smoother 4, the reference's smoothing order) took 17.6 iterations
+# at 59 instead of 50.6 ms, profiles/r06e.)
 HEADLINE_OPTIONS = dict(smoother=3, nu=2, omega=-1.7, iters_per_graph=4, warm_start=0, precond_fp32=4,
                         table_mode=0, coarse_level=-1)
 # ... for a rank that owns at most 4 subdomains (the 2-, 4- and 8-GPU runs of the same chain): a

@@ -53,6 +53,11 @@ struct SellArgs {
     const double* tab;     // table mode: tstride doubles per table row, slot-major 3x3 blocks
     int64_t tstride;
     const int32_t* ctype;  // table mode: chunk -> its rows' common table row, -1 = mixed
+    // fp32 iterate copies of a block-Jacobi level (LevelDev::x4a / x4b, precond_fp32 = 4): the
+    // sweep / residual gathers x (and the sweep its own row's x) from x4; the sweep writes its new
+    // iterate to xo4 and / or, when xo is set (the level's last sweep), to xo in fp64
+    const float4* x4;
+    float4* xo4;
 };
 
 __device__ __forceinline__ double wave_sum(double v) {
@@ -372,7 +377,7 @@ constexpr int default_variant(int mode) { return (mode == 0 || mode == 1) ? 2 : 
 // One wavefront per 64-node chunk, one lane per node row, three accumulators per lane; T is the
 // storage type of streamed operator values (all arithmetic fp64); TBL: values from the table.
 template <int MODE, bool BJ, bool DOT, typename T = double, int V = default_variant(MODE), bool TBL = false,
-          typename CT = int32_t>
+          typename CT = int32_t, bool X4 = false>
 __global__ __launch_bounds__(kBlock) void k_sell(SellArgs a, const double* __restrict__ tab) {
     const int lane = threadIdx.x & 63;
     const int64_t c = (int64_t)blockIdx.x * (kBlock / kWave) + (threadIdx.x >> 6);
@@ -392,7 +397,10 @@ __global__ __launch_bounds__(kBlock) void k_sell(SellArgs a, const double* __res
                                                 s0, s1, s2);
         else
             sell_rows_tbl(a.col + base * kChunk + lane, tab + (int64_t)a.rtype[row] * a.tstride, a.x, ns, s0, s1, s2);
-    } else if constexpr (sizeof(CT) == 2)
+    } else if constexpr (X4 && sizeof(CT) == 2)
+        sell_rows<V, T, CT>(a.col16 + base * kChunk + lane, static_cast<const T*>(a.val) + base * slot_vals<T>() * kChunk + lane,
+                            a.x4, ns, row, s0, s1, s2);
+    else if constexpr (sizeof(CT) == 2)
         sell_rows<V, T, CT>(a.col16 + base * kChunk + lane, static_cast<const T*>(a.val) + base * slot_vals<T>() * kChunk + lane,
                             a.x, ns, row, s0, s1, s2);
     else
@@ -416,11 +424,20 @@ __global__ __launch_bounds__(kBlock) void k_sell(SellArgs a, const double* __res
         double m0, m1, m2;
         apply_m<BJ>(static_cast<const SmoothInv<T>*>(a.minv), row, b0 - s0, b1 - s1, b2 - s2, m0, m1, m2);
         // (explicit contraction throughout the epilogues: every instantiation rounds alike)
-        const double n0 = __builtin_fma(om, m0, a.x[o]), n1 = __builtin_fma(om, m1, a.x[o + 1]),
-                     n2 = __builtin_fma(om, m2, a.x[o + 2]);
-        a.xo[o] = n0;
-        a.xo[o + 1] = n1;
-        a.xo[o + 2] = n2;
+        double x0, x1, x2;
+        if constexpr (X4) {
+            const float4 xv = a.x4[row];
+            x0 = xv.x, x1 = xv.y, x2 = xv.z;
+        } else {
+            x0 = a.x[o], x1 = a.x[o + 1], x2 = a.x[o + 2];
+        }
+        const double n0 = __builtin_fma(om, m0, x0), n1 = __builtin_fma(om, m1, x1), n2 = __builtin_fma(om, m2, x2);
+        if (!X4 || a.xo) {
+            a.xo[o] = n0;
+            a.xo[o + 1] = n1;
+            a.xo[o + 2] = n2;
+        }
+        if (X4 && a.xo4) a.xo4[row] = make_float4((float)n0, (float)n1, (float)n2, 0.0f);
         if (DOT) dotv = __builtin_fma(b2, n2, __builtin_fma(b1, n1, b0 * n0));
     } else if (MODE == kPcg) {
         // q = K z + beta q_old, p = z + beta p_old  (K p = K z + beta K p_old)
@@ -460,7 +477,7 @@ __global__ __launch_bounds__(kBlock) void k_sell(SellArgs a, const double* __res
 // quarters summed by lane shuffles -- four times the waves and a quarter of the dependent
 // column -> x chain per lane.  Same operator bytes; y = Kx, residual and Jacobi-sweep epilogues
 // (the V-cycle's small-level launches carry no dot product).
-template <int MODE, bool BJ, typename T, typename CT>
+template <int MODE, bool BJ, typename T, typename CT, bool X4 = false>
 __global__ __launch_bounds__(kBlock) void k_sell_split(SellArgs a) {
     const int64_t c = blockIdx.x;
     const int sub = a.csub[c];
@@ -478,8 +495,11 @@ __global__ __launch_bounds__(kBlock) void k_sell_split(SellArgs a) {
         if constexpr (sizeof(CT) == 2) colp = a.col16 + base * kChunk + rin;
         else colp = a.col + base * kChunk + rin;
 #pragma unroll 2
-        for (int k = g; k < ns; k += 4)
-            block_fma_any<true>(valp + (int64_t)k * SV, ldx(a.x, col_of(colp[(int64_t)k * kChunk], row)), s0, s1, s2, rin);
+        for (int k = g; k < ns; k += 4) {
+            const int64_t j = col_of(colp[(int64_t)k * kChunk], row);
+            if constexpr (X4) block_fma_any<true>(valp + (int64_t)k * SV, ldx(a.x4, j), s0, s1, s2, rin);
+            else block_fma_any<true>(valp + (int64_t)k * SV, ldx(a.x, j), s0, s1, s2, rin);
+        }
     }
     s0 += __shfl_xor(s0, 16, 64);
     s1 += __shfl_xor(s1, 16, 64);
@@ -501,9 +521,20 @@ __global__ __launch_bounds__(kBlock) void k_sell_split(SellArgs a) {
         const double om = a.coef[2 * sub + 1];
         double m0, m1, m2;
         apply_m<BJ>(static_cast<const SmoothInv<T>*>(a.minv), row, a.b[o] - s0, a.b[o + 1] - s1, a.b[o + 2] - s2, m0, m1, m2);
-        a.xo[o] = a.x[o] + om * m0;
-        a.xo[o + 1] = a.x[o + 1] + om * m1;
-        a.xo[o + 2] = a.x[o + 2] + om * m2;
+        if constexpr (X4) {
+            const float4 xv = a.x4[row];
+            const double n0 = (double)xv.x + om * m0, n1 = (double)xv.y + om * m1, n2 = (double)xv.z + om * m2;
+            if (a.xo) {
+                a.xo[o] = n0;
+                a.xo[o + 1] = n1;
+                a.xo[o + 2] = n2;
+            }
+            if (a.xo4) a.xo4[row] = make_float4((float)n0, (float)n1, (float)n2, 0.0f);
+        } else {
+            a.xo[o] = a.x[o] + om * m0;
+            a.xo[o + 1] = a.x[o + 1] + om * m1;
+            a.xo[o + 2] = a.x[o + 2] + om * m2;
+        }
     }
 }
 
@@ -758,16 +789,22 @@ __global__ __launch_bounds__(kWave) void k_gs_aux(GsArgs a) {
     if (stopped((sc), sub)) return;
 
 // x = omega M b  (first smoothing sweep from a zero guess); CHEB: also d = x
+// (x4: the level's fp32 iterate copy takes x instead, LevelDev::x4a)
 template <bool BJ, bool SETD, typename MT = double>
 __global__ __launch_bounds__(kBlock) void k_jac0(const double* b, const MT* minv, const double* coef, double* x,
-                                                 double* d, int64_t nn, const int32_t* csub, const PcgScal* sc) {
+                                                 double* d, int64_t nn, const int32_t* csub, const PcgScal* sc,
+                                                 float4* x4 = nullptr) {
     NODE_PROLOGUE(nn, csub, sc)
     const double om = coef[2 * sub + 1];
     double m0, m1, m2;
     apply_m<BJ>(minv, i, b[3 * i], b[3 * i + 1], b[3 * i + 2], m0, m1, m2);
-    x[3 * i] = om * m0;
-    x[3 * i + 1] = om * m1;
-    x[3 * i + 2] = om * m2;
+    if (x4) {
+        x4[i] = make_float4((float)(om * m0), (float)(om * m1), (float)(om * m2), 0.0f);
+    } else {
+        x[3 * i] = om * m0;
+        x[3 * i + 1] = om * m1;
+        x[3 * i + 2] = om * m2;
+    }
     if (SETD) {
         d[3 * i] = om * m0;
         d[3 * i + 1] = om * m1;
@@ -785,7 +822,7 @@ __constant__ double kInvCount[9] = {0.0, 1.0, 0.5, 1.0 / 3.0, 0.25, 0.2, 1.0 / 6
 template <bool INIT, bool BJ, bool SETD, typename MT>
 __device__ __forceinline__ void restrict_store(const uint8_t* cmask, double* bc, double* xc, double* dc, const MT* minv,
                                                const double* coef, int64_t j, int sub, double s0, double s1,
-                                               double s2) {
+                                               double s2, float4* xc4) {
     const uint8_t m = cmask[j];
     s0 = (m & 1) ? s0 : 0.0;
     s1 = (m & 2) ? s1 : 0.0;
@@ -797,9 +834,13 @@ __device__ __forceinline__ void restrict_store(const uint8_t* cmask, double* bc,
         const double om = coef[2 * sub + 1];
         double m0, m1, m2;
         apply_m<BJ>(minv, j, s0, s1, s2, m0, m1, m2);
-        xc[3 * j] = om * m0;
-        xc[3 * j + 1] = om * m1;
-        xc[3 * j + 2] = om * m2;
+        if (xc4) {  // the coarse level's fp32 iterate copy (LevelDev::x4a) instead of x_c
+            xc4[j] = make_float4((float)(om * m0), (float)(om * m1), (float)(om * m2), 0.0f);
+        } else {
+            xc[3 * j] = om * m0;
+            xc[3 * j + 1] = om * m1;
+            xc[3 * j + 2] = om * m2;
+        }
         if (SETD) {
             dc[3 * j] = om * m0;
             dc[3 * j + 1] = om * m1;
@@ -813,7 +854,7 @@ __global__ __launch_bounds__(kBlock) void k_restrict(const double* rf, const int
                                                      const int32_t* rcol, const double* rwt, const uint8_t* cmask,
                                                      double* bc, double* xc, double* dc, const MT* minv,
                                                      const double* coef, int64_t nc, const int32_t* csub,
-                                                     const PcgScal* sc) {
+                                                     const PcgScal* sc, float4* xc4) {
     NODE_PROLOGUE(nc, csub, sc)
     const int64_t j = i, c = j >> 6;
     const int ns = rslots[c];
@@ -828,7 +869,7 @@ __global__ __launch_bounds__(kBlock) void k_restrict(const double* rf, const int
         s1 += w * rf[3 * f + 1];
         s2 += w * rf[3 * f + 2];
     }
-    restrict_store<INIT, BJ, SETD>(cmask, bc, xc, dc, minv, coef, j, sub, s0, s1, s2);
+    restrict_store<INIT, BJ, SETD>(cmask, bc, xc, dc, minv, coef, j, sub, s0, s1, s2, xc4);
 }
 
 // Lattice restriction (LevelDev::lat): children f0 + d0 t0 + d1 t1 + d2 t2 for the bits of the
@@ -838,7 +879,8 @@ template <bool INIT, bool BJ, bool SETD, typename MT = double, typename RT = dou
 __global__ __launch_bounds__(kBlock) void k_restrict_lat(const RT* rf, const uint32_t* rmsk, const int32_t* rf0,
                                                          const int32_t* rstr, const uint8_t* cmask, double* bc,
                                                          double* xc, double* dc, const MT* minv, const double* coef,
-                                                         int64_t nc, const int32_t* csub, const PcgScal* sc) {
+                                                         int64_t nc, const int32_t* csub, const PcgScal* sc,
+                                                         float4* xc4) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= nc) return;
     const int sub = csub[i >> 6];
@@ -860,7 +902,7 @@ __global__ __launch_bounds__(kBlock) void k_restrict_lat(const RT* rf, const uin
             s2 += w * v.c;
         }
     }
-    restrict_store<INIT, BJ, SETD>(cmask, bc, xc, dc, minv, coef, j, sub, s0, s1, s2);
+    restrict_store<INIT, BJ, SETD>(cmask, bc, xc, dc, minv, coef, j, sub, s0, s1, s2, xc4);
 }
 
 // x_f += mask_f (P e_c)
@@ -891,6 +933,38 @@ __global__ __launch_bounds__(kBlock) void k_prolong(const double* ec, const int3
     if (m & 1) xf[3 * i] += e0;
     if (m & 2) xf[3 * i + 1] += e1;
     if (m & 4) xf[3 * i + 2] += e2;
+}
+
+// the same into a block-Jacobi level's fp32 iterate copy (LevelDev::x4a): the sum and the add in fp64
+template <bool UW = false>
+__global__ __launch_bounds__(kBlock) void k_prolong_x4(const double* ec, const int32_t* ppar, const double* pw,
+                                                       const uint8_t* fmask, float4* x4, int64_t nf, const int32_t* csub,
+                                                       const PcgScal* sc) {
+    NODE_PROLOGUE(nf, csub, sc)
+    double e0 = 0.0, e1 = 0.0, e2 = 0.0;
+    int np = 0;
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+        const int32_t c = ppar[p * nf + i];
+        if (c < 0) break;
+        const double w = UW ? 1.0 : pw[p * nf + i];
+        e0 += w * ec[3 * (int64_t)c];
+        e1 += w * ec[3 * (int64_t)c + 1];
+        e2 += w * ec[3 * (int64_t)c + 2];
+        ++np;
+    }
+    if (UW) {
+        const double w = kInvCount[np];
+        e0 *= w;
+        e1 *= w;
+        e2 *= w;
+    }
+    const uint8_t m = fmask[i];
+    float4 v = x4[i];
+    if (m & 1) v.x = (float)((double)v.x + e0);
+    if (m & 2) v.y = (float)((double)v.y + e1);
+    if (m & 4) v.z = (float)((double)v.z + e2);
+    x4[i] = v;
 }
 
 // Lattice prolongation (LevelDev::lat): parents p0 + the subset sums of the coarse strides the
@@ -2625,6 +2699,25 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
         if (gs.r4.p)
             for (int k = 0; k < K; ++k) gs.launch_bytes[K] -= 8.0 * gs.rows_k[k];  // r written in 16 B
     }
+    // fp32 iterate copies of the block-Jacobi levels (precond_fp32 = 4, block-Jacobi smoothing;
+    // DDPCA_BJ_X4=0 keeps them fp64, A/B): every level the V-cycle smooths by block Jacobi whose
+    // copy has 16-bit columns and streamed values, with no rotation block entries into it -- its
+    // sweeps and residual gather one 16-B load per neighbour, only the level's last sweep writes
+    // fp64.  Alternating in one call (profiles/r06n): the N = 8 rank 9.52 / 9.55 -> 9.00 / 9.00 ms
+    // per ADMM iteration, the headline 19.73 / 19.74 -> 20.05 / 20.06 ADMM it/s, PCG iterations equal
+    {
+        const char* eb = std::getenv("DDPCA_BJ_X4");
+        const bool on = !(eb && eb[0] == '0');
+        if (on && opt.precond_fp32 == 4 && (opt.smoother == 1 || opt.smoother >= 3))
+            for (int l = clev + 1; l < (int)lev.size(); ++l) {
+                LevelDev& L = lev[l];
+                if ((gs_fine() && l == (int)lev.size() - 1) || !L.col16.p || L.tbl || L.nrot) continue;
+                L.x4a.alloc(4 * L.nn);
+                L.x4b.alloc(4 * L.nn);
+                L.x4a.zero(stream);
+                L.x4b.zero(stream);
+            }
+    }
     if (gs_fine() && opt.smoother == 4) {
         if (gs.band) throw ApiError(DDPCA_EINVAL, "colour SSOR (smoother 4) on a band-mode fine level");
         gs.w.alloc(3 * lev.back().nn);
@@ -2776,6 +2869,26 @@ void launch_sell(int vt, const SellArgs& a, hipStream_t s) {
     // (read per launch: launches are captured into graphs once per handle, and tests switch it)
     const char* esp = std::getenv("DDPCA_SPLIT_CHUNKS");
     const int64_t split_max = esp ? std::atoll(esp) : 2048;
+    if constexpr (MODE == kResid || MODE == kJac) {
+        if (a.x4) {
+            // a block-Jacobi level's fp32 iterate copy (LevelDev::x4a): the constructor enables it
+            // on levels with 16-bit columns and streamed values only
+            if (a.tab || !a.col16) throw ApiError(DDPCA_ESTATE, "fp32 iterate copy needs 16-bit columns and streamed values");
+            if (!DOT && a.nch <= split_max) {
+                const dim3 gs((unsigned)a.nch);
+                if (vt == kValQ8) hipLaunchKernelGGL((k_sell_split<MODE, BJ, uint8_t, I16, true>), gs, dim3(kBlock), 0, s, a);
+                else if (vt == kValH16) hipLaunchKernelGGL((k_sell_split<MODE, BJ, uint16_t, I16, true>), gs, dim3(kBlock), 0, s, a);
+                else if (vt == kVal32) hipLaunchKernelGGL((k_sell_split<MODE, BJ, float, I16, true>), gs, dim3(kBlock), 0, s, a);
+                else hipLaunchKernelGGL((k_sell_split<MODE, BJ, double, I16, true>), gs, dim3(kBlock), 0, s, a);
+                return;
+            }
+            if (vt == kValQ8) hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, uint8_t, V, false, I16, true>), dim3(grid), dim3(kBlock), 0, s, a, a.tab);
+            else if (vt == kValH16) hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, uint16_t, V, false, I16, true>), dim3(grid), dim3(kBlock), 0, s, a, a.tab);
+            else if (vt == kVal32) hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, float, V, false, I16, true>), dim3(grid), dim3(kBlock), 0, s, a, a.tab);
+            else hipLaunchKernelGGL((k_sell<MODE, BJ, DOT, double, V, false, I16, true>), dim3(grid), dim3(kBlock), 0, s, a, a.tab);
+            return;
+        }
+    }
     // (V-cycle modes only: y = Kx keeps the slot order the table mode reproduces bit for bit)
     if constexpr (!DOT && (MODE == kResid || MODE == kJac)) {
         if (!a.tab && a.nch <= split_max) {
@@ -2861,23 +2974,24 @@ namespace {
 template <bool INIT, bool BJ, bool SETD, typename MT>
 void launch_restrict(const LevelDev& F, int grid, hipStream_t st, const double* rf, const uint8_t* cmask, double* bc,
                      double* xc, double* dc, const MT* minv, const double* coef, int64_t nc, const int32_t* csub,
-                     const PcgScal* sc, const float4* rf4 = nullptr) {
-    // rf4: the fine residual in the colour sweeps' fp32 copy (lattice transfers only, GsFine::r4)
+                     const PcgScal* sc, const float4* rf4 = nullptr, float4* xc4 = nullptr) {
+    // rf4: the fine residual in the colour sweeps' fp32 copy (lattice transfers only, GsFine::r4);
+    // xc4: the fused first coarse sweep writes the coarse level's fp32 iterate copy (LevelDev::x4a)
     if (rf4) {
         if (!F.lat) throw ApiError(DDPCA_ESTATE, "fp32 residual copy without lattice transfers");
         hipLaunchKernelGGL((k_restrict_lat<INIT, BJ, SETD, MT, float4>), dim3(grid), dim3(kBlock), 0, st, rf4, F.rmsk.p,
-                           F.rf0.p, F.rstr.p, cmask, bc, xc, dc, minv, coef, nc, csub, sc);
+                           F.rf0.p, F.rstr.p, cmask, bc, xc, dc, minv, coef, nc, csub, sc, xc4);
         return;
     }
     // stored weights: deriving them from a gathered parent count (as k_prolong<true> does)
     // measured 58 -> 102 us on the fine level (profiles/r01_transfer_weights.txt)
     if (F.lat) {
         hipLaunchKernelGGL((k_restrict_lat<INIT, BJ, SETD, MT>), dim3(grid), dim3(kBlock), 0, st, rf, F.rmsk.p, F.rf0.p,
-                           F.rstr.p, cmask, bc, xc, dc, minv, coef, nc, csub, sc);
+                           F.rstr.p, cmask, bc, xc, dc, minv, coef, nc, csub, sc, xc4);
         return;
     }
     hipLaunchKernelGGL((k_restrict<INIT, BJ, SETD, MT>), dim3(grid), dim3(kBlock), 0, st, rf, F.rslots.p, F.roff.p,
-                       F.rcol.p, F.rwt.p, cmask, bc, xc, dc, minv, coef, nc, csub, sc);
+                       F.rcol.p, F.rwt.p, cmask, bc, xc, dc, minv, coef, nc, csub, sc, xc4);
 }
 }  // namespace
 
@@ -3107,10 +3221,20 @@ void MgpisDevice::vcycle(const double* rin, double* zout, bool dot) {
     for (int l = 0; l < nlev; ++l) { cur[l] = lev[l].x.p; oth[l] = lev[l].t.p; }
     cur[Lf] = lev[Lf].t.p;
     oth[Lf] = zout;
+    // block-Jacobi levels with fp32 iterate copies (LevelDev::x4a / x4b, precond_fp32 = 4): their
+    // first sweep, the sweeps and the prolongation into them write the copy, the sweeps and the
+    // residual gather it, and only the level's last sweep writes its fp64 iterate
+    std::vector<float4*> cur4(nlev, nullptr), oth4(nlev, nullptr);
+    for (int l = 0; l < nlev; ++l)
+        if (lev[l].x4a.p) {
+            cur4[l] = reinterpret_cast<float4*>(lev[l].x4a.p);
+            oth4[l] = reinterpret_cast<float4*>(lev[l].x4b.p);
+        }
     auto bvec = [&](int l) -> const double* { return l == Lf ? rin : lev[l].b.p; };
     auto coef = [&](int l, int sweep) { return lev[l].coef.p + 2 * (int64_t)sweep * nsub; };
-    // smoothing sweeps on level l from the current iterate (first: jac0/restrict already did sweep 0)
-    auto smooth = [&](int l, int first, int count, bool last_dot) {
+    // smoothing sweeps on level l from the current iterate (first: jac0/restrict already did sweep 0);
+    // out64: the last of them is the level's output (fp64 also on an fp32-copy level)
+    auto smooth = [&](int l, int first, int count, bool last_dot, bool out64) {
         const int f32 = vc_type(l);
         for (int s = first; s < first + count; ++s) {
             SellArgs a = vc_level_args(*this, l);
@@ -3120,6 +3244,12 @@ void MgpisDevice::vcycle(const double* rin, double* zout, bool dot) {
             a.b = bvec(l);
             a.xo = oth[l];
             a.coef = coef(l, s);
+            if (cur4[l]) {
+                const bool fin = out64 && s == first + count - 1;
+                a.x4 = cur4[l];
+                a.xo4 = fin ? nullptr : oth4[l];
+                a.xo = fin ? oth[l] : nullptr;
+            }
             const bool d = last_dot && s == first + count - 1;
             if (cheb) {
                 a.p = lev[l].d.p;
@@ -3133,6 +3263,7 @@ void MgpisDevice::vcycle(const double* rin, double* zout, bool dot) {
                 else launch_sell<kJac, false, false>(f32, a, stream);
             }
             std::swap(cur[l], oth[l]);
+            std::swap(cur4[l], oth4[l]);
         }
     };
     const bool gsf = gs_fine();
@@ -3156,19 +3287,20 @@ void MgpisDevice::vcycle(const double* rin, double* zout, bool dot) {
         const int grid = ceil_div(F.nn, kBlock);
         if (vc_type(Lf) != kVal64) {
             const float* m = F.minv32.p;
-            if (cheb) hipLaunchKernelGGL((k_jac0<true, true, float>), dim3(grid), dim3(kBlock), 0, stream, rin, m, coef(Lf, 0), cur[Lf], F.d.p, F.nn, F.csub.p, scp);
-            else if (bj) hipLaunchKernelGGL((k_jac0<true, false, float>), dim3(grid), dim3(kBlock), 0, stream, rin, m, coef(Lf, 0), cur[Lf], nullptr, F.nn, F.csub.p, scp);
-            else hipLaunchKernelGGL((k_jac0<false, false, float>), dim3(grid), dim3(kBlock), 0, stream, rin, m, coef(Lf, 0), cur[Lf], nullptr, F.nn, F.csub.p, scp);
-        } else if (cheb) hipLaunchKernelGGL((k_jac0<true, true>), dim3(grid), dim3(kBlock), 0, stream, rin, F.minv.p, coef(Lf, 0), cur[Lf], F.d.p, F.nn, F.csub.p, scp);
-        else if (bj) hipLaunchKernelGGL((k_jac0<true, false>), dim3(grid), dim3(kBlock), 0, stream, rin, F.minv.p, coef(Lf, 0), cur[Lf], nullptr, F.nn, F.csub.p, scp);
-        else hipLaunchKernelGGL((k_jac0<false, false>), dim3(grid), dim3(kBlock), 0, stream, rin, F.minv.p, coef(Lf, 0), cur[Lf], nullptr, F.nn, F.csub.p, scp);
+            if (cheb) hipLaunchKernelGGL((k_jac0<true, true, float>), dim3(grid), dim3(kBlock), 0, stream, rin, m, coef(Lf, 0), cur[Lf], F.d.p, F.nn, F.csub.p, scp, cur4[Lf]);
+            else if (bj) hipLaunchKernelGGL((k_jac0<true, false, float>), dim3(grid), dim3(kBlock), 0, stream, rin, m, coef(Lf, 0), cur[Lf], nullptr, F.nn, F.csub.p, scp, cur4[Lf]);
+            else hipLaunchKernelGGL((k_jac0<false, false, float>), dim3(grid), dim3(kBlock), 0, stream, rin, m, coef(Lf, 0), cur[Lf], nullptr, F.nn, F.csub.p, scp, cur4[Lf]);
+        } else if (cheb) hipLaunchKernelGGL((k_jac0<true, true>), dim3(grid), dim3(kBlock), 0, stream, rin, F.minv.p, coef(Lf, 0), cur[Lf], F.d.p, F.nn, F.csub.p, scp, cur4[Lf]);
+        else if (bj) hipLaunchKernelGGL((k_jac0<true, false>), dim3(grid), dim3(kBlock), 0, stream, rin, F.minv.p, coef(Lf, 0), cur[Lf], nullptr, F.nn, F.csub.p, scp, cur4[Lf]);
+        else hipLaunchKernelGGL((k_jac0<false, false>), dim3(grid), dim3(kBlock), 0, stream, rin, F.minv.p, coef(Lf, 0), cur[Lf], nullptr, F.nn, F.csub.p, scp, cur4[Lf]);
     }
     for (int l = Lf; l >= cl + 1; --l) {
         if (!(gsf && l == Lf)) {
-            smooth(l, 1, nu - 1, false);
+            smooth(l, 1, nu - 1, false, false);
             SellArgs a = vc_level_args(*this, l);
             a.sc = scp;
             a.x = cur[l];
+            a.x4 = cur4[l];
             a.b = bvec(l);
             a.y = lev[l].r.p;
             launch_sell<kResid, false, false>(vc_type(l), a, stream);
@@ -3186,12 +3318,12 @@ void MgpisDevice::vcycle(const double* rin, double* zout, bool dot) {
             if (c != cl) {
                 const bool f32c = vc_type(c) != kVal64;
                 const float* m32 = C.minv32.p;
-                if (cheb && f32c) hipLaunchKernelGGL((k_jac0<true, true, float>), dim3(grid), dim3(kBlock), 0, stream, C.b.p, m32, cf, cur[c], C.d.p, C.nn, C.csub.p, scp);
-                else if (bj && f32c) hipLaunchKernelGGL((k_jac0<true, false, float>), dim3(grid), dim3(kBlock), 0, stream, C.b.p, m32, cf, cur[c], nullptr, C.nn, C.csub.p, scp);
-                else if (f32c) hipLaunchKernelGGL((k_jac0<false, false, float>), dim3(grid), dim3(kBlock), 0, stream, C.b.p, m32, cf, cur[c], nullptr, C.nn, C.csub.p, scp);
-                else if (cheb) hipLaunchKernelGGL((k_jac0<true, true>), dim3(grid), dim3(kBlock), 0, stream, C.b.p, C.minv.p, cf, cur[c], C.d.p, C.nn, C.csub.p, scp);
-                else if (bj) hipLaunchKernelGGL((k_jac0<true, false>), dim3(grid), dim3(kBlock), 0, stream, C.b.p, C.minv.p, cf, cur[c], nullptr, C.nn, C.csub.p, scp);
-                else hipLaunchKernelGGL((k_jac0<false, false>), dim3(grid), dim3(kBlock), 0, stream, C.b.p, C.minv.p, cf, cur[c], nullptr, C.nn, C.csub.p, scp);
+                if (cheb && f32c) hipLaunchKernelGGL((k_jac0<true, true, float>), dim3(grid), dim3(kBlock), 0, stream, C.b.p, m32, cf, cur[c], C.d.p, C.nn, C.csub.p, scp, cur4[c]);
+                else if (bj && f32c) hipLaunchKernelGGL((k_jac0<true, false, float>), dim3(grid), dim3(kBlock), 0, stream, C.b.p, m32, cf, cur[c], nullptr, C.nn, C.csub.p, scp, cur4[c]);
+                else if (f32c) hipLaunchKernelGGL((k_jac0<false, false, float>), dim3(grid), dim3(kBlock), 0, stream, C.b.p, m32, cf, cur[c], nullptr, C.nn, C.csub.p, scp, cur4[c]);
+                else if (cheb) hipLaunchKernelGGL((k_jac0<true, true>), dim3(grid), dim3(kBlock), 0, stream, C.b.p, C.minv.p, cf, cur[c], C.d.p, C.nn, C.csub.p, scp, cur4[c]);
+                else if (bj) hipLaunchKernelGGL((k_jac0<true, false>), dim3(grid), dim3(kBlock), 0, stream, C.b.p, C.minv.p, cf, cur[c], nullptr, C.nn, C.csub.p, scp, cur4[c]);
+                else hipLaunchKernelGGL((k_jac0<false, false>), dim3(grid), dim3(kBlock), 0, stream, C.b.p, C.minv.p, cf, cur[c], nullptr, C.nn, C.csub.p, scp, cur4[c]);
             }
         } else {
             // x4 mode: the colour sweeps' residual is the fp32 copy (GsFine::r4)
@@ -3201,17 +3333,17 @@ void MgpisDevice::vcycle(const double* rin, double* zout, bool dot) {
             else if (vc_type(c) != kVal64) {
                 const float* m = C.minv32.p;
                 if (cheb)
-                    launch_restrict<true, true, true, float>(F, grid, stream, F.r.p, C.mask.p, C.b.p, cur[c], C.d.p, m, cf, C.nn, C.csub.p, scp, rf4);
+                    launch_restrict<true, true, true, float>(F, grid, stream, F.r.p, C.mask.p, C.b.p, cur[c], C.d.p, m, cf, C.nn, C.csub.p, scp, rf4, cur4[c]);
                 else if (bj)
-                    launch_restrict<true, true, false, float>(F, grid, stream, F.r.p, C.mask.p, C.b.p, cur[c], nullptr, m, cf, C.nn, C.csub.p, scp, rf4);
+                    launch_restrict<true, true, false, float>(F, grid, stream, F.r.p, C.mask.p, C.b.p, cur[c], nullptr, m, cf, C.nn, C.csub.p, scp, rf4, cur4[c]);
                 else
-                    launch_restrict<true, false, false, float>(F, grid, stream, F.r.p, C.mask.p, C.b.p, cur[c], nullptr, m, cf, C.nn, C.csub.p, scp, rf4);
+                    launch_restrict<true, false, false, float>(F, grid, stream, F.r.p, C.mask.p, C.b.p, cur[c], nullptr, m, cf, C.nn, C.csub.p, scp, rf4, cur4[c]);
             } else if (cheb)
-                launch_restrict<true, true, true, double>(F, grid, stream, F.r.p, C.mask.p, C.b.p, cur[c], C.d.p, C.minv.p, cf, C.nn, C.csub.p, scp, rf4);
+                launch_restrict<true, true, true, double>(F, grid, stream, F.r.p, C.mask.p, C.b.p, cur[c], C.d.p, C.minv.p, cf, C.nn, C.csub.p, scp, rf4, cur4[c]);
             else if (bj)
-                launch_restrict<true, true, false, double>(F, grid, stream, F.r.p, C.mask.p, C.b.p, cur[c], nullptr, C.minv.p, cf, C.nn, C.csub.p, scp, rf4);
+                launch_restrict<true, true, false, double>(F, grid, stream, F.r.p, C.mask.p, C.b.p, cur[c], nullptr, C.minv.p, cf, C.nn, C.csub.p, scp, rf4, cur4[c]);
             else
-                launch_restrict<true, false, false, double>(F, grid, stream, F.r.p, C.mask.p, C.b.p, cur[c], nullptr, C.minv.p, cf, C.nn, C.csub.p, scp, rf4);
+                launch_restrict<true, false, false, double>(F, grid, stream, F.r.p, C.mask.p, C.b.p, cur[c], nullptr, C.minv.p, cf, C.nn, C.csub.p, scp, rf4, cur4[c]);
         }
     }
     if (ainv32.p) hipLaunchKernelGGL(k_coarse<float>, dim3(ceil_div(3 * lev[cl].nn, 4)), dim3(kBlock), 0, stream, ainv32.p, aoff.p, c_noff.p,
@@ -3224,6 +3356,13 @@ void MgpisDevice::vcycle(const double* rin, double* zout, bool dot) {
         if (gsf && l == Lf && gs.x4.p)  // (x4 mode: lattice fine transfer, no block entries, GsFine::x4)
             hipLaunchKernelGGL(k_prolong_lat_x4, dim3(ceil_div(F.nn, kBlock)), dim3(kBlock), 0, stream, cur[l - 1], F.ppk.p,
                                F.pstr.p, F.mask.p, reinterpret_cast<float4*>(gs.x4.p), F.nn, F.csub.p, scp);
+        else if (cur4[l] && F.lat)  // a block-Jacobi level's fp32 copy (no block entries into it)
+            hipLaunchKernelGGL(k_prolong_lat_x4, dim3(ceil_div(F.nn, kBlock)), dim3(kBlock), 0, stream, cur[l - 1], F.ppk.p,
+                               F.pstr.p, F.mask.p, cur4[l], F.nn, F.csub.p, scp);
+        else if (cur4[l] && F.uw) hipLaunchKernelGGL(k_prolong_x4<true>, dim3(ceil_div(F.nn, kBlock)), dim3(kBlock), 0, stream, cur[l - 1],
+                                                F.ppar.p, F.pw.p, F.mask.p, cur4[l], F.nn, F.csub.p, scp);
+        else if (cur4[l]) hipLaunchKernelGGL(k_prolong_x4<false>, dim3(ceil_div(F.nn, kBlock)), dim3(kBlock), 0, stream, cur[l - 1],
+                                        F.ppar.p, F.pw.p, F.mask.p, cur4[l], F.nn, F.csub.p, scp);
         else if (F.lat) hipLaunchKernelGGL(k_prolong_lat, dim3(ceil_div(F.nn, kBlock)), dim3(kBlock), 0, stream, cur[l - 1], F.ppk.p,
                                       F.pstr.p, F.mask.p, cur[l], F.nn, F.csub.p, scp);
         else if (F.uw) hipLaunchKernelGGL(k_prolong<true>, dim3(ceil_div(F.nn, kBlock)), dim3(kBlock), 0, stream, cur[l - 1], F.ppar.p, F.pw.p,
@@ -3251,7 +3390,7 @@ void MgpisDevice::vcycle(const double* rin, double* zout, bool dot) {
             continue;
         }
         // post-smoothing restarts the smoother (Chebyshev recurrence) from the prolongated iterate
-        smooth(l, 0, nu, dot && l == Lf);
+        smooth(l, 0, nu, dot && l == Lf, true);
     }
     if (cur[Lf] != zout) throw ApiError(DDPCA_ESTATE, "V-cycle buffer parity");
 }
@@ -3294,8 +3433,14 @@ void MgpisDevice::vcycle_bytes(int s, double out[2]) const {
     };
     auto minv = [&](int l) { return (bj ? 9.0 : 3.0) * (vc_type(l) != kVal64 ? 4.0 : 8.0); };
     auto put = [&](int l, double b) { out[l == Lf ? 0 : 1] += b; };
-    // x' = x + w M (b - K x): operator, x gathered, b, M^-1, x' (Chebyshev: d read + written)
-    auto sweep = [&](int l) { return mat(l) + n(l) * (24.0 * 3 + minv(l) + (cheb ? 48.0 : 0.0)); };
+    // x' = x + w M (b - K x): operator, x gathered, b, M^-1, x' (Chebyshev: d read + written); on a
+    // level with fp32 iterate copies x is gathered in 16 B and x' written in 16 B, in fp64 by the
+    // level's last sweep (fin)
+    auto x4 = [&](int l) { return lev[l].x4a.p != nullptr; };
+    auto sweep = [&](int l, bool fin = true) {
+        if (x4(l)) return mat(l) + n(l) * (16.0 + 24.0 + (fin ? 24.0 : 16.0) + minv(l));
+        return mat(l) + n(l) * (24.0 * 3 + minv(l) + (cheb ? 48.0 : 0.0));
+    };
     const double n0 = 3.0 * (double)lev[cl].nloc[s];
     const double coarse = (ainv32.p ? 4.0 : 8.0) * n0 * n0 + 16.0 * n0;  // dense inverse + b in, x out
     if (Lf == cl) {
@@ -3333,18 +3478,18 @@ void MgpisDevice::vcycle_bytes(int s, double out[2]) const {
         // band mode: the ring's residual over its band columns (blocks, b read, r written, x gathered)
         put(Lf, gsvb * (double)(gs.band ? gs.ring_nnzb_sub[s] : 0) + nring * (24.0 + 24.0 + 4.0 + 24.0));
     } else {
-        put(Lf, n(Lf) * (48.0 + minv(Lf) + (cheb ? 24.0 : 0.0)));  // k_jac0: b in, x out
+        put(Lf, n(Lf) * ((x4(Lf) ? 40.0 : 48.0) + minv(Lf) + (cheb ? 24.0 : 0.0)));  // k_jac0: b in, x out
     }
     for (int l = Lf; l >= cl + 1; --l) {
         if (!(gsf && l == Lf)) {
-            for (int k = 1; k < opt.nu; ++k) put(l, sweep(l));
-            put(l, mat(l) + 72.0 * n(l));  // residual: x gathered, b, r
+            for (int k = 1; k < opt.nu; ++k) put(l, sweep(l, false));
+            put(l, mat(l) + (x4(l) ? 64.0 : 72.0) * n(l));  // residual: x gathered, b, r
         }
         const LevelDev& F = lev[l];
         const int c = l - 1;
         const bool init = c != cl;
         // coarse node: mask + b_c written (+ x_c = w M b_c: M^-1 read, x_c written; Chebyshev d_c)
-        double cn = 1.0 + 24.0 + (init ? minv(c) + 24.0 + (cheb ? 24.0 : 0.0) : 0.0);
+        double cn = 1.0 + 24.0 + (init ? minv(c) + (x4(c) ? 16.0 : 24.0) + (cheb ? 24.0 : 0.0) : 0.0);
         double tr = (gsf && l == Lf ? rb : 24.0) * n(l);  // r_f read once
         if (F.lat) cn += 8.0;     // 27-bit child mask + fine copy
         else tr += 12.0 * (double)F.tent_sub[s];  // child index + weight per stencil entry
@@ -3355,7 +3500,7 @@ void MgpisDevice::vcycle_bytes(int s, double out[2]) const {
     for (int l = cl + 1; l <= Lf; ++l) {
         const LevelDev& F = lev[l];
         // x_f += mask P e_c: e_c read once, mask, x_f read + written, the parent encoding
-        double pb = 24.0 * n(l - 1) + n(l) * (1.0 + (gsf && l == Lf ? 2.0 * xb : 48.0));
+        double pb = 24.0 * n(l - 1) + n(l) * (1.0 + (gsf && l == Lf ? 2.0 * xb : x4(l) ? 32.0 : 48.0));
         if (F.lat) pb += 4.0 * n(l);
         else pb += (F.uw ? 4.0 : 12.0) * (double)F.tent_sub[s];
         pb += 4.0 * 8.0 * (double)F.tblk_sub[s];
@@ -3372,7 +3517,7 @@ void MgpisDevice::vcycle_bytes(int s, double out[2]) const {
             put(l, 52.0 * nout);  // band mode: b . x of the rows outside the colours (b, x read, row index)
             continue;
         }
-        for (int k = 0; k < opt.nu; ++k) put(l, sweep(l));
+        for (int k = 0; k < opt.nu; ++k) put(l, sweep(l, k == opt.nu - 1));
     }
 }
 

@@ -133,6 +133,9 @@ struct LevelDev {
     DevBuf<double> rot_blk, rotc_blk;
     // vectors (3 nn)
     DevBuf<double> x, t, b, r, d;
+    // fp32 iterate copies (x0, x1, x2, 0 per node) of a block-Jacobi level, or empty
+    // (precond_fp32 = 4, MgpisDevice constructor): the V-cycle's x / t pair in 16 B per node
+    DevBuf<float> x4a, x4b;
 };
 
 // Multicolour node-block Gauss-Seidel on the fine level (opt.smoother = 3): the fine nodes of

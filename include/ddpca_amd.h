@@ -69,10 +69,12 @@ typedef struct {
                           of every PCG iteration.
                           3: as 2 with block-scaled int8 instead of fp16 (nine int8 and a scale
                           = the block maximum / 127 per 3x3 block) -- 14 B per block.
-                          4: as 3, and with smoother 3 / 4 on lattice transfers the colour sweeps
-                          gather an fp32 stride-4 copy of the fine V-cycle iterate (one 16-B load
-                          per neighbour) and the fine restriction reads an fp32 copy of the
-                          residual; products, dot products and the V-cycle output stay fp64. */
+                          4: as 3, and the V-cycle sweeps gather fp32 stride-4 copies of their
+                          iterates (one 16-B load per neighbour): the colour sweeps of smoother
+                          3 / 4 on lattice transfers (the fine restriction then reads an fp32 copy
+                          of the residual) and every block-Jacobi level with 16-bit columns (only
+                          its last sweep writes fp64); products, dot products and the V-cycle
+                          output stay fp64. */
     int table_mode;    /* levels >= 1: 0 stream every block value; 1 (default) when the rows'
                           block values deduplicate well (structured meshes), keep one copy per
                           distinct row in a cache-resident table and stream only column indices

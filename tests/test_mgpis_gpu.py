@@ -179,6 +179,43 @@ def test_fp32_iterate_copy_keeps_the_solution(ddpca, gpu):
         assert np.linalg.norm(x4 - x3) <= 1e-10 * np.linalg.norm(x3)
 
 
+@pytest.mark.parametrize("smoother", [1, 3])
+def test_block_jacobi_fp32_iterate_copy_keeps_the_solution(ddpca, gpu, monkeypatch, smoother):
+    """precond_fp32 = 4 (DDPCA_BJ_X4=0 turns this part off): every block-Jacobi level of the V-cycle (all of them
+    under smoother 1 -- the fine one included --, the levels below the colour sweeps under smoother
+    3) keeps its iterate in fp32 copies (LevelDev::x4a / x4b): the first sweep (k_jac0 / the fused
+    restriction), the sweeps and the prolongation write the copy, the sweeps and the residual
+    gather it, and only the level's last sweep writes fp64.  The products and epilogues stay fp64:
+    the V-cycle moves by the fp32 rounding of the iterates only, stays symmetric to that rounding,
+    and PCG reaches the same ||r|| <= 1e-14 ||b|| within one more iteration."""
+    P = ddpca.headline_problem(gl=3).ESTABLISH()
+    # (the exact solve pinned at level 1: a lone gl-3 subdomain otherwise takes it right below the
+    # fine level, and under smoother 3 no block-Jacobi level would be left)
+    opt = dict(smoother=smoother, nu=2, omega=-1.7, table_mode=0, precond_fp32=4, coarse_level=1)
+    for tv in (0, 1):
+        b = P.grid(tv).consForc
+        if not np.any(b):
+            b = np.random.default_rng(tv).standard_normal(len(b))
+        monkeypatch.setenv("DDPCA_BJ_X4", "0")
+        M = ddpca.MGPIS.from_problem(P, tv, **opt)
+        monkeypatch.delenv("DDPCA_BJ_X4")
+        Mx = ddpca.MGPIS.from_problem(P, tv, **opt)
+        x, i, _ = M.CG_SOLV(1, b)
+        xx, ix, rr = Mx.CG_SOLV(1, b)
+        rng = np.random.default_rng(11)
+        u, v = rng.standard_normal(len(b)), rng.standard_normal(len(b))
+        zu, zux = M.MULT_VCYC(u), Mx.MULT_VCYC(u)
+        zvx = Mx.MULT_VCYC(v)
+        dz = np.linalg.norm(zux - zu) / np.linalg.norm(zu)
+        asym = abs(u @ zvx - v @ zux) / (np.linalg.norm(u) * np.linalg.norm(zvx))
+        print(tv, "smoother", smoother, "PCG", i, "->", ix, "V-cycle difference", dz, "asymmetry", asym)
+        assert 0.0 < dz <= 1e-5
+        assert asym <= 1e-6
+        assert rr <= 1e-14
+        assert ix <= i + 1, (ix, i)
+        assert np.linalg.norm(xx - x) <= 1e-10 * np.linalg.norm(x)
+
+
 @pytest.mark.parametrize("lowp", [3, 4])
 def test_colour_ssor_keeps_the_solution(ddpca, gpu, lowp):
     """smoother = 4: multicolour block SSOR on the fine level -- a forward and a backward sweep before
