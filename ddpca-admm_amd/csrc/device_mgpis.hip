@@ -1052,6 +1052,32 @@ __global__ __launch_bounds__(kBlock) void k_prolong_rot(const double* ec, const 
     if (m & 4) xf[3 * i + 2] += e2;
 }
 
+// the same into a block-Jacobi level's fp32 iterate copy (LevelDev::x4a), after k_prolong_x4
+__global__ __launch_bounds__(kBlock) void k_prolong_rot_x4(const double* ec, const int32_t* row, const int64_t* ptr,
+                                                           const int32_t* par, const double* blk, const uint8_t* fmask,
+                                                           float4* x4, int64_t nr, const int32_t* csub,
+                                                           const PcgScal* sc) {
+    const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (t >= nr) return;
+    const int64_t i = row[t];
+    if (stopped(sc, csub[i >> 6])) return;
+    double e0 = 0.0, e1 = 0.0, e2 = 0.0;
+    for (int64_t k = ptr[t]; k < ptr[t + 1]; ++k) {
+        const double* B = blk + 9 * k;
+        const int64_t c = par[k];
+        const double c0 = ec[3 * c], c1 = ec[3 * c + 1], c2 = ec[3 * c + 2];
+        e0 += B[0] * c0 + B[1] * c1 + B[2] * c2;
+        e1 += B[3] * c0 + B[4] * c1 + B[5] * c2;
+        e2 += B[6] * c0 + B[7] * c1 + B[8] * c2;
+    }
+    const uint8_t m = fmask[i];
+    float4 v = x4[i];
+    if (m & 1) v.x = (float)((double)v.x + e0);
+    if (m & 2) v.y = (float)((double)v.y + e1);
+    if (m & 4) v.z = (float)((double)v.z + e2);
+    x4[i] = v;
+}
+
 // ... and b_c += mask_c (B^T r_f) per coarse node that receives one (after k_restrict).
 __global__ __launch_bounds__(kBlock) void k_restrict_rot(const double* rf, const int32_t* row, const int64_t* ptr,
                                                          const int32_t* kid, const double* blk, const uint8_t* cmask,
@@ -2701,7 +2727,7 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
     }
     // fp32 iterate copies of the block-Jacobi levels (precond_fp32 = 4, block-Jacobi smoothing;
     // DDPCA_BJ_X4=0 keeps them fp64, A/B): every level the V-cycle smooths by block Jacobi whose
-    // copy has 16-bit columns and streamed values, with no rotation block entries into it -- its
+    // copy has 16-bit columns and streamed values (rotation block entries into it included) -- its
     // sweeps and residual gather one 16-B load per neighbour, only the level's last sweep writes
     // fp64.  Alternating in one call (profiles/r06n): the N = 8 rank 9.52 / 9.55 -> 9.00 / 9.00 ms
     // per ADMM iteration, the headline 19.73 / 19.74 -> 20.05 / 20.06 ADMM it/s, PCG iterations equal
@@ -2711,7 +2737,7 @@ MgpisDevice::MgpisDevice(int dev, const std::vector<SubdomainOps>& subs, const m
         if (on && opt.precond_fp32 == 4 && (opt.smoother == 1 || opt.smoother >= 3))
             for (int l = clev + 1; l < (int)lev.size(); ++l) {
                 LevelDev& L = lev[l];
-                if ((gs_fine() && l == (int)lev.size() - 1) || !L.col16.p || L.tbl || L.nrot) continue;
+                if ((gs_fine() && l == (int)lev.size() - 1) || !L.col16.p || L.tbl) continue;
                 L.x4a.alloc(4 * L.nn);
                 L.x4b.alloc(4 * L.nn);
                 L.x4a.zero(stream);
@@ -3011,11 +3037,15 @@ void MgpisDevice::rot_restrict(int l, const double* rf, double* bc, const PcgSca
                        F.rotc_ptr.p, F.rotc_kid.p, F.rotc_blk.p, lev[l - 1].mask.p, bc, F.nrotc, lev[l - 1].csub.p, scp);
 }
 
-void MgpisDevice::rot_prolong(int l, const double* ec, double* xf, const PcgScal* scp) {
+void MgpisDevice::rot_prolong(int l, const double* ec, double* xf, const PcgScal* scp, float4* xf4) {
     const LevelDev& F = lev[l];
     if (!F.nrot) return;
-    hipLaunchKernelGGL(k_prolong_rot, dim3(ceil_div(F.nrot, kBlock)), dim3(kBlock), 0, stream, ec, F.rot_row.p,
-                       F.rot_ptr.p, F.rot_par.p, F.rot_blk.p, F.mask.p, xf, F.nrot, F.csub.p, scp);
+    if (xf4)  // the level's fp32 iterate copy (LevelDev::x4a)
+        hipLaunchKernelGGL(k_prolong_rot_x4, dim3(ceil_div(F.nrot, kBlock)), dim3(kBlock), 0, stream, ec, F.rot_row.p,
+                           F.rot_ptr.p, F.rot_par.p, F.rot_blk.p, F.mask.p, xf4, F.nrot, F.csub.p, scp);
+    else
+        hipLaunchKernelGGL(k_prolong_rot, dim3(ceil_div(F.nrot, kBlock)), dim3(kBlock), 0, stream, ec, F.rot_row.p,
+                           F.rot_ptr.p, F.rot_par.p, F.rot_blk.p, F.mask.p, xf, F.nrot, F.csub.p, scp);
 }
 
 void MgpisDevice::spmv(int level, const double* x, double* y, bool vc_op) {
@@ -3369,7 +3399,7 @@ void MgpisDevice::vcycle(const double* rin, double* zout, bool dot) {
                            F.mask.p, cur[l], F.nn, F.csub.p, scp);
         else hipLaunchKernelGGL(k_prolong<false>, dim3(ceil_div(F.nn, kBlock)), dim3(kBlock), 0, stream, cur[l - 1], F.ppar.p, F.pw.p,
                            F.mask.p, cur[l], F.nn, F.csub.p, scp);
-        rot_prolong(l, cur[l - 1], cur[l], scp);
+        rot_prolong(l, cur[l - 1], cur[l], scp, cur4[l]);
         if (ssor && l == Lf) {
             // colour SSOR after the coarse correction: forward, then backward with the dot partials
             for (int k = 0; k < gs.ncol; ++k) launch_gs<9, false>(*this, k, zout, rin, nullptr, scp, nullptr);

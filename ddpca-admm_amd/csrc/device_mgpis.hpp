@@ -271,7 +271,7 @@ public:
     void restrict_level(int l, const double* rf, double* bc);
     // block (rotated-node) parts of the transfer from level l-1 to l: b_c += B^T r_f, x_f += B e_c
     void rot_restrict(int l, const double* rf, double* bc, const PcgScal* scp);
-    void rot_prolong(int l, const double* ec, double* xf, const PcgScal* scp);
+    void rot_prolong(int l, const double* ec, double* xf, const PcgScal* scp, float4* xf4 = nullptr);
     // PCG over every subdomain of the batch; b in bs, result in xs (x0 = xs when warm).
     // begin() enqueues the setup, step() one graph replay (iters_per_graph iterations),
     // wait() paces replays on the host-mapped stop flags until every subdomain is done.

@@ -179,16 +179,22 @@ def test_fp32_iterate_copy_keeps_the_solution(ddpca, gpu):
         assert np.linalg.norm(x4 - x3) <= 1e-10 * np.linalg.norm(x3)
 
 
-@pytest.mark.parametrize("smoother", [1, 3])
-def test_block_jacobi_fp32_iterate_copy_keeps_the_solution(ddpca, gpu, monkeypatch, smoother):
+@pytest.mark.parametrize("smoother,mesh", [(1, "headline"), (3, "headline"), (1, "general")])
+def test_block_jacobi_fp32_iterate_copy_keeps_the_solution(ddpca, gpu, monkeypatch, smoother, mesh):
     """precond_fp32 = 4 (DDPCA_BJ_X4=0 turns this part off): every block-Jacobi level of the V-cycle (all of them
     under smoother 1 -- the fine one included --, the levels below the colour sweeps under smoother
     3) keeps its iterate in fp32 copies (LevelDev::x4a / x4b): the first sweep (k_jac0 / the fused
     restriction), the sweeps and the prolongation write the copy, the sweeps and the residual
     gather it, and only the level's last sweep writes fp64.  The products and epilogues stay fp64:
     the V-cycle moves by the fp32 rounding of the iterates only, stays symmetric to that rounding,
-    and PCG reaches the same ||r|| <= 1e-14 ||b|| within one more iteration."""
-    P = ddpca.headline_problem(gl=3).ESTABLISH()
+    and PCG reaches the same ||r|| <= 1e-14 ||b|| within one more iteration.  general: the general
+    mesh's rotated support nodes (rotation block entries in the prolongation, k_prolong_rot_x4) and
+    explicit transfer lists (k_prolong_x4)."""
+    if mesh == "general":
+        monkeypatch.setenv("DDPCA_LATTICE", "0")
+        P = ddpca.headline_problem(gl=3, **ddpca.GENERAL_FEATURES).ESTABLISH()
+    else:
+        P = ddpca.headline_problem(gl=3).ESTABLISH()
     # (the exact solve pinned at level 1: a lone gl-3 subdomain otherwise takes it right below the
     # fine level, and under smoother 3 no block-Jacobi level would be left)
     opt = dict(smoother=smoother, nu=2, omega=-1.7, table_mode=0, precond_fp32=4, coarse_level=1)
