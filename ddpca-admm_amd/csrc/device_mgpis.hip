@@ -253,7 +253,14 @@ __device__ __forceinline__ int64_t col_of(CT c, int64_t row) {
     else return (int64_t)c;
 }
 
-template <int V, typename T, typename CT = int32_t, typename XT = double>
+// slot-loop unroll of the sweeps gathering an fp32 iterate copy (colour sweeps, block-Jacobi
+// levels; A/B builds: -DDDPCA_GS_UNROLL=n)
+#ifndef DDPCA_GS_UNROLL
+#define DDPCA_GS_UNROLL 3
+#endif
+constexpr int kGsUnroll = DDPCA_GS_UNROLL;
+
+template <int V, typename T, typename CT = int32_t, typename XT = double, int U = 3>
 __device__ __forceinline__ void sell_rows(const CT* colp, const T* valp, const XT* x, int ns, int64_t row,
                                           double& s0, double& s1, double& s2) {
     constexpr int64_t SV = slot_vals<T>() * kChunk;
@@ -262,7 +269,7 @@ __device__ __forceinline__ void sell_rows(const CT* colp, const T* valp, const X
         for (int k = 0; k < ns; ++k)
             block_fma_plain(valp + (int64_t)k * SV, ldx(x, col_of(colp[(int64_t)k * kChunk], row)), s0, s1, s2);
     } else if constexpr (V == 1) {
-#pragma unroll 3
+#pragma unroll U
         for (int k = 0; k < ns; ++k)
             block_fma(valp + (int64_t)k * SV, ldx(x, col_of(__builtin_nontemporal_load(colp + (int64_t)k * kChunk), row)),
                       s0, s1, s2);
@@ -398,8 +405,9 @@ __global__ __launch_bounds__(kBlock) void k_sell(SellArgs a, const double* __res
         else
             sell_rows_tbl(a.col + base * kChunk + lane, tab + (int64_t)a.rtype[row] * a.tstride, a.x, ns, s0, s1, s2);
     } else if constexpr (X4 && sizeof(CT) == 2)
-        sell_rows<V, T, CT>(a.col16 + base * kChunk + lane, static_cast<const T*>(a.val) + base * slot_vals<T>() * kChunk + lane,
-                            a.x4, ns, row, s0, s1, s2);
+        sell_rows<V, T, CT, float4, kGsUnroll>(a.col16 + base * kChunk + lane,
+                                               static_cast<const T*>(a.val) + base * slot_vals<T>() * kChunk + lane, a.x4, ns,
+                                               row, s0, s1, s2);
     else if constexpr (sizeof(CT) == 2)
         sell_rows<V, T, CT>(a.col16 + base * kChunk + lane, static_cast<const T*>(a.val) + base * slot_vals<T>() * kChunk + lane,
                             a.x, ns, row, s0, s1, s2);
@@ -633,12 +641,12 @@ __global__ __launch_bounds__(kWave) void k_gs(GsArgs a) {
     else colp = a.col;
     if (PH != 1) {
         const int64_t o = a.offl[c];
-        if constexpr (X4) sell_rows<1, T, CT>(colp + o * kChunk + lane, val + o * SV + lane, (const float4*)a.x4, a.nsl[c], row, s0, s1, s2);
+        if constexpr (X4) sell_rows<1, T, CT, float4, kGsUnroll>(colp + o * kChunk + lane, val + o * SV + lane, (const float4*)a.x4, a.nsl[c], row, s0, s1, s2);
         else sell_rows<1, T, CT>(colp + o * kChunk + lane, val + o * SV + lane, (const double*)a.x, a.nsl[c], row, s0, s1, s2);
     }
     if (PH != 0) {
         const int64_t o = a.offu[c];
-        if constexpr (X4) sell_rows<1, T, CT>(colp + o * kChunk + lane, val + o * SV + lane, (const float4*)a.x4, a.nsu[c], row, s0, s1, s2);
+        if constexpr (X4) sell_rows<1, T, CT, float4, kGsUnroll>(colp + o * kChunk + lane, val + o * SV + lane, (const float4*)a.x4, a.nsu[c], row, s0, s1, s2);
         else sell_rows<1, T, CT>(colp + o * kChunk + lane, val + o * SV + lane, (const double*)a.x, a.nsu[c], row, s0, s1, s2);
     }
     const double dotv = gs_epilogue<PH, DOT, T, X4>(a, c, lane, row, real, s0, s1, s2);
